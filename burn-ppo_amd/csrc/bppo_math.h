@@ -1,0 +1,190 @@
+// bppo_math.h — bit-exact restatement of the platform libm transcendentals the
+// reference's Rust code calls (f32::ln -> logf, f32::sin/cos -> sinf/cosf).
+//
+// The reference runs on glibc 2.35 (x86-64, FMA ifunc variants): logf is
+// sysdeps/ieee754/flt-32/e_logf.c and sinf/cosf are s_sinf.c / s_cosf.c with
+// sincosf.h (ARM optimized-routines algorithms, double-precision evaluation,
+// compiled with -mfma so a*b+c contracts to fma).  Call sites:
+//   utils.rs:25         gumbel = -ln(-ln(u))
+//   cartpole.rs:51-52   theta.cos(), theta.sin()
+// The constant tables below are the data that glibc's libm.so.6 carries
+// (__logf_data, __sincosf_table, __inv_pio4).  tests/test_libm_restatement.py
+// checks every Gumbel input and every float |x| < 1 against the real glibc on
+// the host, and the GPU tests check device == host on the same inputs, so the
+// device kernels reproduce the reference bit for bit.
+//
+// Shared verbatim between host C++ and HIP device code; every operation is an
+// explicit IEEE double op or fma (build with -ffp-contract=off).
+#pragma once
+#include <stdint.h>
+#include <string.h>
+#include <math.h>
+
+#if defined(__HIPCC__)
+#define BPPO_HD __host__ __device__ __forceinline__
+#else
+#define BPPO_HD static inline
+#endif
+
+namespace bppo_math {
+
+BPPO_HD uint32_t asuint(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+BPPO_HD float asfloat(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+
+// ------------------------------------------------------------------ logf ----
+BPPO_HD float logf_glibc(float x) {
+    // __logf_data (LOGF_TABLE_BITS = 4): {invc, logc}
+    const double T_invc[16] = {
+        0x1.661ec79f8f3bep+0, 0x1.571ed4aaf883dp+0, 0x1.49539f0f010bp+0,  0x1.3c995b0b80385p+0,
+        0x1.30d190c8864a5p+0, 0x1.25e227b0b8eap+0,  0x1.1bb4a4a1a343fp+0, 0x1.12358f08ae5bap+0,
+        0x1.0953f419900a7p+0, 0x1.0p+0,             0x1.e608cfd9a47acp-1, 0x1.ca4b31f026aap-1,
+        0x1.b2036576afce6p-1, 0x1.9c2d163a1aa2dp-1, 0x1.886e6037841edp-1, 0x1.767dcf5534862p-1};
+    const double T_logc[16] = {
+        -0x1.57bf7808caadep-2, -0x1.2bef0a7c06ddbp-2, -0x1.01eae7f513a67p-2, -0x1.b31d8a68224e9p-3,
+        -0x1.6574f0ac07758p-3, -0x1.1aa2bc79c81p-3,   -0x1.a4e76ce8c0e5ep-4, -0x1.1973c5a611cccp-4,
+        -0x1.252f438e10c1ep-5, 0x0.0p+0,              0x1.aa5aa5df25984p-5,  0x1.c5e53aa362eb4p-4,
+        0x1.526e57720db08p-3,  0x1.bc2860d22477p-3,   0x1.1058bc8a07ee1p-2,  0x1.4043057b6ee09p-2};
+    const double Ln2 = 0x1.62e42fefa39efp-1;
+    const double A0 = -0x1.00ea348b88334p-2, A1 = 0x1.5575b0be00b6ap-2,
+                 A2 = -0x1.ffffef20a4123p-2;
+    uint32_t ix = asuint(x);
+    if (ix == 0x3f800000u) return 0.0f;
+    if (ix - 0x00800000u >= 0x7f800000u - 0x00800000u) {
+        if (ix * 2 == 0) return -INFINITY;
+        if (ix == 0x7f800000u) return x;
+        if ((ix & 0x80000000u) || ix * 2 >= 0xff000000u) return (x - x) / (x - x);
+        ix = asuint(x * 0x1p23f);
+        ix -= 23u << 23;
+    }
+    uint32_t tmp = ix - 0x3f330000u;
+    int i = (int)((tmp >> (23 - 4)) % 16);
+    int k = (int32_t)tmp >> 23;
+    uint32_t iz = ix - (tmp & (0x1ffu << 23));
+    double invc = T_invc[i], logc = T_logc[i];
+    double z = (double)asfloat(iz);
+    double r = fma(z, invc, -1.0);
+    double y0 = fma((double)k, Ln2, logc);
+    double r2 = r * r;
+    double y = fma(A1, r, A2);
+    y = fma(A0, r2, y);
+    y = fma(y, r2, y0 + r);
+    return (float)y;
+}
+
+// ---------------------------------------------------------- sinf / cosf ----
+struct sincos_t {
+    double sign[4], hpi_inv, hpi, c0, c1, s1, c2, s2, c3, s3, c4;
+};
+
+BPPO_HD sincos_t sincos_table(int which) {
+    // __sincosf_table[0] / [1] (table 1 negates the cosine coefficients)
+    const double g = which ? -1.0 : 1.0;
+    sincos_t t = {{1.0, -1.0, -1.0, 1.0}, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0,
+                  g * 0x1.0p+0, g * -0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3,
+                  g * 0x1.55553e1068f19p-5, 0x1.1107605230bc4p-7, g * -0x1.6c087e89a359dp-10,
+                  -0x1.994eb3774cf24p-13, g * 0x1.99343027bf8c3p-16};
+    return t;
+}
+
+BPPO_HD uint32_t abstop12(float x) { return (asuint(x) >> 20) & 0x7ff; }
+
+BPPO_HD float sinf_poly(double x, double x2, const sincos_t &p, int n) {
+    if ((n & 1) == 0) {
+        double x3 = x * x2;
+        double s1 = fma(x2, p.s3, p.s2);
+        double x7 = x3 * x2;
+        double s = fma(x3, p.s1, x);
+        return (float)fma(x7, s1, s);
+    } else {
+        double x4 = x2 * x2;
+        double c2 = fma(x2, p.c4, p.c3);
+        double c1 = fma(x2, p.c1, p.c0);
+        double x6 = x4 * x2;
+        double c = fma(x4, p.c2, c1);
+        return (float)fma(x6, c2, c);
+    }
+}
+
+BPPO_HD double reduce_fast(double x, const sincos_t &p, int *np) {
+    double r = x * p.hpi_inv;
+    int32_t n = ((int32_t)r + 0x800000) >> 24;
+    *np = n;
+    return fma(-(double)n, p.hpi, x);
+}
+
+BPPO_HD double reduce_large(uint32_t xi, int *np) {
+    // __inv_pio4: bits of 4/pi, each entry the previous shifted by 8 bits
+    const uint32_t inv_pio4[24] = {
+        0xa2u,       0xa2f9u,     0xa2f983u,   0xa2f9836eu, 0xf9836e4eu, 0x836e4e44u,
+        0x6e4e4415u, 0x4e441529u, 0x441529fcu, 0x1529fc27u, 0x29fc2757u, 0xfc2757d1u,
+        0x2757d1f5u, 0x57d1f534u, 0xd1f534ddu, 0xf534ddc0u, 0x34ddc0dbu, 0xddc0db62u,
+        0xc0db6295u, 0xdb629599u, 0x6295993cu, 0x95993c43u, 0x993c4390u, 0x3c439041u};
+    const double pi63 = 0x1.921fb54442d18p-62;
+    const uint32_t *arr = &inv_pio4[(xi >> 26) & 15];
+    int shift = (xi >> 23) & 7;
+    uint64_t n, res0, res1, res2;
+    xi = (xi & 0xffffff) | 0x800000;
+    xi <<= shift;
+    res0 = xi * arr[0];
+    res1 = (uint64_t)xi * arr[4];
+    res2 = (uint64_t)xi * arr[8];
+    res0 = (res2 >> 32) | (res0 << 32);
+    res0 += res1;
+    n = (res0 + (1ULL << 61)) >> 62;
+    res0 -= n << 62;
+    double x = (double)(int64_t)res0;
+    *np = (int)n;
+    return x * pi63;
+}
+
+BPPO_HD float sinf_glibc(float y) {
+    double x = y;
+    int n;
+    if (abstop12(y) < 0x3f4u) {            // abstop12(pio4)
+        double s = x * x;
+        if (abstop12(y) < 0x398u) return y;  // abstop12(0x1p-12f)
+        return sinf_poly(x, s, sincos_table(0), 0);
+    } else if (abstop12(y) < 0x42fu) {     // abstop12(120.0f)
+        sincos_t p = sincos_table(0);
+        x = reduce_fast(x, p, &n);
+        double s = p.sign[n & 3];
+        if (n & 2) p = sincos_table(1);
+        return sinf_poly(x * s, x * x, p, n);
+    } else if (abstop12(y) < 0x7f8u) {
+        uint32_t xi = asuint(y);
+        int sign = xi >> 31;
+        x = reduce_large(xi, &n);
+        sincos_t p = sincos_table(0);
+        double s = p.sign[(n + sign) & 3];
+        if ((n + sign) & 2) p = sincos_table(1);
+        return sinf_poly(x * s, x * x, p, n);
+    }
+    return (y - y) / (y - y);
+}
+
+BPPO_HD float cosf_glibc(float y) {
+    double x = y;
+    int n;
+    if (abstop12(y) < 0x3f4u) {
+        double x2 = x * x;
+        if (abstop12(y) < 0x398u) return 1.0f;
+        return sinf_poly(x, x2, sincos_table(0), 1);
+    } else if (abstop12(y) < 0x42fu) {
+        sincos_t p = sincos_table(0);
+        x = reduce_fast(x, p, &n);
+        double s = p.sign[n & 3];
+        if (n & 2) p = sincos_table(1);
+        return sinf_poly(x * s, x * x, p, n ^ 1);
+    } else if (abstop12(y) < 0x7f8u) {
+        uint32_t xi = asuint(y);
+        int sign = xi >> 31;
+        x = reduce_large(xi, &n);
+        sincos_t p = sincos_table(0);
+        double s = p.sign[(n + sign) & 3];
+        if ((n + sign) & 2) p = sincos_table(1);
+        return sinf_poly(x * s, x * x, p, n ^ 1);
+    }
+    return (y - y) / (y - y);
+}
+
+}  // namespace bppo_math

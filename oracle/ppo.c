@@ -1,0 +1,380 @@
+/*
+ * ppo.c — GAE (ppo.rs:1069-1264), explained variance (ppo.rs:1268-1294) and a
+ * trainer that restates one update of run_training (main.rs:684-988):
+ * collect_rollouts (ppo.rs:213-500) -> bootstrap + GAE (main.rs:877-947) ->
+ * ppo_update (ppo.rs:1661-2112).  TEST INFRASTRUCTURE ONLY.
+ */
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include "oracle.h"
+
+/* ppo.rs:1094-1123 — fmaf exactly where the reference calls mul_add. */
+void or_compute_gae(const float *r, const float *d, const float *v, const float *last_v, int T,
+                    int N, float gamma, float lambda, float *adv, float *ret) {
+    float *last = calloc((size_t)N, sizeof(float));
+    for (int t = T - 1; t >= 0; t--)
+        for (int e = 0; e < N; e++) {
+            size_t i = (size_t)t * N + e;
+            float nv = t == T - 1 ? last_v[e] : v[i + N];
+            float delta = fmaf(gamma * nv, 1.0f - d[i], r[i]) - v[i];
+            last[e] = fmaf(gamma * lambda * (1.0f - d[i]), last[e], delta);
+            adv[i] = last[e];
+        }
+    if (ret) for (size_t i = 0; i < (size_t)T * N; i++) ret[i] = adv[i] + v[i];
+    free(last);
+}
+
+/* ppo.rs:1174-1263 — two reverse passes with per-player carries. */
+void or_compute_gae_mp(const float *all_r, const int32_t *pl, const float *d, const float *v,
+                       const float *last_v_pp, int T, int N, int P, float gamma, float lambda,
+                       float *adv, float *ret) {
+    size_t TN = (size_t)T * N;
+    float *ar = malloc(sizeof(float) * TN);
+    float *carry = calloc((size_t)N * P, sizeof(float));
+    for (int t = T - 1; t >= 0; t--)
+        for (int e = 0; e < N; e++) {
+            size_t i = (size_t)t * N + e;
+            int a = pl[i];
+            float *c = carry + (size_t)e * P;
+            if (d[i] > 0.5f) for (int p = 0; p < P; p++) c[p] = 0.0f;
+            ar[i] = all_r[i * P + a] + c[a];
+            c[a] = 0.0f;
+            for (int p = 0; p < P; p++) if (p != a) c[p] += all_r[i * P + p];
+        }
+    float *gc = calloc((size_t)N * P, sizeof(float));
+    float *nv = malloc(sizeof(float) * (size_t)N * P);
+    memcpy(nv, last_v_pp, sizeof(float) * (size_t)N * P);
+    for (int t = T - 1; t >= 0; t--)
+        for (int e = 0; e < N; e++) {
+            size_t i = (size_t)t * N + e;
+            int a = pl[i];
+            float *g = gc + (size_t)e * P, *n = nv + (size_t)e * P;
+            if (d[i] > 0.5f) {
+                for (int p = 0; p < P; p++) g[p] = 0.0f;
+                for (int p = 0; p < P; p++) if (p != a) n[p] = 0.0f;
+            }
+            float delta = fmaf(gamma * n[a], 1.0f - d[i], ar[i]) - v[i];
+            float A = fmaf(gamma * lambda * (1.0f - d[i]), g[a], delta);
+            adv[i] = A;
+            g[a] = A;
+            n[a] = v[i];
+        }
+    if (ret) for (size_t i = 0; i < TN; i++) ret[i] = adv[i] + v[i];
+    free(ar); free(carry); free(gc); free(nv);
+}
+
+/* ppo.rs:1268-1294 — f32 sequential sums, population variance. */
+float or_explained_variance(const float *values, const float *returns, size_t n_) {
+    float n = (float)n_;
+    if (n < 2.0f) return 0.0f;
+    float s = 0.0f;
+    for (size_t i = 0; i < n_; i++) s += returns[i];
+    float mr = s / n, vr = 0.0f;
+    for (size_t i = 0; i < n_; i++) { float q = returns[i] - mr; vr += q * q; }
+    vr /= n;
+    if (vr < 1e-8f) return 0.0f;
+    float sr = 0.0f;
+    for (size_t i = 0; i < n_; i++) sr += returns[i] - values[i];
+    float mres = sr / n, vres = 0.0f;
+    for (size_t i = 0; i < n_; i++) { float q = (returns[i] - values[i]) - mres; vres += q * q; }
+    vres /= n;
+    return 1.0f - vres / vr;
+}
+
+/* ================================================================ trainer == */
+struct or_trainer {
+    or_train_cfg c;
+    or_net_desc net;
+    float *params;
+    or_adam adam;
+    or_vecenv *env;
+    or_obs_norm on;
+    or_ret_norm rn;
+    or_rng rng;
+    int T, N, D, A, P, G;
+    float *obs, *priv, *rewards, *dones, *values, *logp, *all_r, *masks, *adv, *ret, *raw, *lvpp;
+    int32_t *actions, *players;
+    int has_masks;
+    or_episode *eps;
+    int n_eps, eps_cap;
+    double phase_s[3];
+};
+
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+
+or_trainer *or_trainer_new(const or_train_cfg *c, const float *init_params) {
+    or_trainer *t = calloc(1, sizeof *t);
+    t->c = *c;
+    t->env = or_vecenv_new(c->env_kind, c->num_envs, c->seed);
+    or_vecenv_set_shaping(t->env, (float)c->reward_shaping);
+    t->T = c->num_steps; t->N = c->num_envs;
+    t->D = or_vecenv_obs_dim(t->env); t->A = or_vecenv_act_dim(t->env);
+    t->P = or_vecenv_players(t->env); t->G = c->ctde ? or_vecenv_priv_dim(t->env) : 0;
+    t->net.ctde = c->ctde; t->net.obs_dim = t->D; t->net.priv_dim = t->G; t->net.act_dim = t->A;
+    t->net.relu = c->relu; t->net.n_actor = c->num_hidden; t->net.actor_width = c->hidden;
+    t->net.n_critic = c->ctde ? c->critic_num_hidden : 0;
+    t->net.critic_width = c->ctde ? c->critic_hidden : 0;
+    t->net.n_params = or_net_num_params(&t->net);
+    t->params = malloc(sizeof(float) * t->net.n_params);
+    memcpy(t->params, init_params, sizeof(float) * t->net.n_params);
+    or_adam_init(&t->adam, &t->net);
+    or_obs_norm_init(&t->on, t->D, 10.0f);
+    or_ret_norm_init(&t->rn, t->N, t->P, c->gamma, c->return_clip);
+    or_rng_seed_u64(&t->rng, c->seed);   /* main.rs:189 */
+    size_t TN = (size_t)t->T * t->N;
+    t->obs = malloc(sizeof(float) * TN * t->D);
+    t->raw = malloc(sizeof(float) * TN * t->D);
+    t->priv = t->G ? malloc(sizeof(float) * TN * t->G) : NULL;
+    t->rewards = malloc(sizeof(float) * TN);
+    t->dones = malloc(sizeof(float) * TN);
+    t->values = malloc(sizeof(float) * TN);
+    t->logp = malloc(sizeof(float) * TN);
+    t->all_r = malloc(sizeof(float) * TN * t->P);
+    t->masks = c->env_kind != OR_ENV_CARTPOLE ? malloc(sizeof(float) * TN * t->A) : NULL;
+    t->adv = malloc(sizeof(float) * TN);
+    t->ret = malloc(sizeof(float) * TN);
+    t->actions = malloc(sizeof(int32_t) * TN);
+    t->players = malloc(sizeof(int32_t) * TN);
+    t->lvpp = calloc((size_t)t->N * t->P, sizeof(float));
+    t->eps_cap = t->N * 4 + 1024;
+    t->eps = malloc(sizeof(or_episode) * t->eps_cap);
+    return t;
+}
+
+void or_trainer_free(or_trainer *t) {
+    if (!t) return;
+    or_vecenv_free(t->env); or_adam_free(&t->adam); or_obs_norm_free(&t->on); or_ret_norm_free(&t->rn);
+    free(t->params); free(t->obs); free(t->raw); free(t->priv); free(t->rewards); free(t->dones);
+    free(t->values); free(t->logp); free(t->all_r); free(t->masks); free(t->adv); free(t->ret);
+    free(t->actions); free(t->players); free(t->lvpp); free(t->eps); free(t);
+}
+
+size_t or_trainer_num_params(const or_trainer *t) { return t->net.n_params; }
+void or_trainer_get_params(const or_trainer *t, float *o) { memcpy(o, t->params, sizeof(float) * t->net.n_params); }
+void or_trainer_set_params(or_trainer *t, const float *i) { memcpy(t->params, i, sizeof(float) * t->net.n_params); }
+uint64_t or_trainer_rng_pos(const or_trainer *t) { return t->rng.word_pos; }
+double or_trainer_last_phase_seconds(const or_trainer *t, int ph) { return t->phase_s[ph]; }
+
+static void forward_rows(or_trainer *t, const float *obs, const float *priv, size_t B,
+                         float *logits, float *values) {
+    or_net_forward(&t->net, t->params, obs, priv, B, logits, values);
+}
+
+/* ppo.rs:213-500 collect_rollouts (self-play / single-player path). */
+int or_trainer_collect(or_trainer *t) {
+    double t0 = now_s();
+    const int N = t->N, D = t->D, A = t->A, P = t->P, G = t->G;
+    float *obs = malloc(sizeof(float) * N * D);
+    float *logits = malloc(sizeof(float) * N * A);
+    float *vals = malloc(sizeof(float) * N);
+    float *rw = malloc(sizeof(float) * N * P);
+    uint8_t *dn = malloc(N);
+    uint8_t *mk = malloc((size_t)N * A);
+    int32_t *cp = malloc(sizeof(int32_t) * N);
+    int32_t *act = malloc(sizeof(int32_t) * N);
+    t->n_eps = 0;
+    memset(t->lvpp, 0, sizeof(float) * (size_t)N * P);
+    for (int s = 0; s < t->T; s++) {
+        size_t base = (size_t)s * N;
+        or_vecenv_get_players(t->env, cp);                       /* :275 */
+        or_vecenv_get_obs(t->env, obs);                          /* :278 */
+        if (G) or_vecenv_get_priv(t->env, t->priv + base * G);   /* :282 */
+        memcpy(t->raw + base * D, obs, sizeof(float) * N * D);   /* :287-289 */
+        if (t->c.normalize_obs) or_obs_norm_normalize_batch(&t->on, obs, N); /* :292-294 lagged */
+        int hm = or_vecenv_get_masks(t->env, mk);                /* :297 */
+        t->has_masks = hm;
+        if (hm)
+            for (size_t q = 0; q < (size_t)N * A; q++) t->masks[base * A + q] = mk[q] ? 1.0f : 0.0f;
+        forward_rows(t, obs, G ? t->priv + base * G : NULL, N, logits, vals);  /* :322-333 */
+        if (hm) {                                                /* :337 apply_action_mask */
+            for (int e = 0; e < N; e++) {
+                int any = 0;
+                for (int a = 0; a < A; a++) any |= mk[(size_t)e * A + a];
+                if (!any) { fprintf(stderr, "Empty action mask: env %d\n", e); abort(); }
+                for (int a = 0; a < A; a++)
+                    logits[(size_t)e * A + a] += mk[(size_t)e * A + a] ? 0.0f : -INFINITY;
+            }
+        }
+        or_sample_categorical(&t->rng, logits, N, A, act);       /* :338 */
+        for (int e = 0; e < N; e++) {                            /* :339 */
+            float lp = or_log_prob(logits + (size_t)e * A, A, act[e]);
+            if (!isfinite(lp)) { fprintf(stderr, "NaN/Inf in log probs\n"); abort(); }
+            t->logp[base + e] = lp;
+        }
+        int ne = or_vecenv_step(t->env, act, NULL, rw, dn, t->eps + t->n_eps,
+                                t->eps_cap - t->n_eps);         /* :374-378 */
+        t->n_eps += ne < t->eps_cap - t->n_eps ? ne : t->eps_cap - t->n_eps;
+        for (int e = 0; e < N; e++) {                            /* :382-408 */
+            int p = cp[e];
+            float r = rw[(size_t)e * P + p];
+            if (t->c.normalize_returns) {
+                or_ret_norm_update_return(&t->rn, e, p, r);
+                or_ret_norm_update_variance(&t->rn, e, p);
+                r = or_ret_norm_normalize(&t->rn, r);
+                if (dn[e]) or_ret_norm_reset_player(&t->rn, e, p);
+            }
+            t->rewards[base + e] = r;
+            for (int q = 0; q < P; q++)                          /* :412-428 */
+                t->all_r[(base + e) * P + q] = q == p ? r : rw[(size_t)e * P + q];
+        }
+        memcpy(t->obs + base * D, obs, sizeof(float) * N * D);  /* :431-440 */
+        for (int e = 0; e < N; e++) {
+            t->actions[base + e] = act[e];
+            t->dones[base + e] = dn[e] ? 1.0f : 0.0f;
+            t->values[base + e] = vals[e];
+            t->players[base + e] = cp[e];
+            t->lvpp[(size_t)e * P + cp[e]] = vals[e];           /* :443-445 */
+        }
+    }
+    if (t->c.normalize_obs) or_obs_norm_update_batch(&t->on, t->raw, (size_t)t->T * N); /* :495-497 */
+    free(obs); free(logits); free(vals); free(rw); free(dn); free(mk); free(cp); free(act);
+    t->phase_s[0] = now_s() - t0;
+    return t->n_eps;
+}
+
+/* main.rs:877-947 bootstrap (UPDATED normalizer stats) then GAE dispatch. */
+void or_trainer_gae(or_trainer *t) {
+    double t0 = now_s();
+    const int N = t->N, D = t->D, A = t->A, P = t->P, G = t->G;
+    float *obs = malloc(sizeof(float) * N * D);
+    float *priv = G ? malloc(sizeof(float) * N * G) : NULL;
+    float *logits = malloc(sizeof(float) * N * A);
+    float *lv = malloc(sizeof(float) * N);
+    or_vecenv_get_obs(t->env, obs);
+    if (t->c.normalize_obs) or_obs_norm_normalize_batch(&t->on, obs, N);
+    if (G) or_vecenv_get_priv(t->env, priv);
+    forward_rows(t, obs, priv, N, logits, lv);
+    if (P > 1) {
+        int32_t *cp = malloc(sizeof(int32_t) * N);
+        or_vecenv_get_players(t->env, cp);
+        for (int e = 0; e < N; e++) t->lvpp[(size_t)e * P + cp[e]] = lv[e];
+        or_compute_gae_mp(t->all_r, t->players, t->dones, t->values, t->lvpp, t->T, N, P,
+                          (float)t->c.gamma, (float)t->c.gae_lambda, t->adv, t->ret);
+        free(cp);
+    } else {
+        or_compute_gae(t->rewards, t->dones, t->values, lv, t->T, N, (float)t->c.gamma,
+                       (float)t->c.gae_lambda, t->adv, t->ret);
+    }
+    free(obs); free(priv); free(logits); free(lv);
+    t->phase_s[1] = now_s() - t0;
+}
+
+/* ppo.rs:1661-2112 ppo_update (no pool, no PopArt). */
+void or_trainer_update(or_trainer *t, or_update_metrics *m) {
+    double t0 = now_s();
+    const size_t B = (size_t)t->T * t->N;
+    const int D = t->D, A = t->A, G = t->G;
+    const or_ppo_cfg *c = &t->c.ppo;
+    uint32_t *idx = malloc(sizeof(uint32_t) * B);
+    size_t np = t->net.n_params;
+    float *grads = malloc(sizeof(float) * np);
+    size_t mbmax = B / c->num_minibatches + 1;
+    float *mo = malloc(sizeof(float) * mbmax * D), *mp = G ? malloc(sizeof(float) * mbmax * G) : NULL;
+    float *mm = t->has_masks ? malloc(sizeof(float) * mbmax * A) : NULL;
+    int32_t *ma = malloc(sizeof(int32_t) * mbmax);
+    float *mlp = malloc(sizeof(float) * mbmax), *madv = malloc(sizeof(float) * mbmax);
+    float *mret = malloc(sizeof(float) * mbmax), *mov = malloc(sizeof(float) * mbmax);
+    float *madvn = malloc(sizeof(float) * mbmax);
+    float tp = 0, tv = 0, th = 0, tk = 0, tc = 0, tl = 0, tvm = 0, trm = 0, tam = 0, tas = 0;
+    float tamin = INFINITY, tamax = -INFINITY, tvem = 0, tves = 0, tvemax = -INFINITY;
+    float tav = 0, tevp = 0;
+    int nup = 0, epochs_run = 0, stop = 0;
+    for (int ep = 0; ep < c->num_epochs && !stop; ep++) {
+        epochs_run++;
+        for (size_t i = 0; i < B; i++) idx[i] = (uint32_t)i;  /* :1815 */
+        or_shuffle_u32(&t->rng, idx, B);                         /* :1816 */
+        size_t base = B / c->num_minibatches, rem = B % c->num_minibatches, start = 0;
+        for (int mbi = 0; mbi < c->num_minibatches; mbi++) {
+            size_t sz = base + ((size_t)mbi < rem ? 1 : 0);
+            if (sz == 0) continue;
+            for (size_t q = 0; q < sz; q++) {                    /* :1833-1857 gather */
+                size_t r = idx[start + q];
+                memcpy(mo + q * D, t->obs + r * D, sizeof(float) * D);
+                if (G) memcpy(mp + q * G, t->priv + r * G, sizeof(float) * G);
+                if (mm) memcpy(mm + q * A, t->masks + r * A, sizeof(float) * A);
+                ma[q] = t->actions[r]; mlp[q] = t->logp[r]; madv[q] = t->adv[r];
+                mret[q] = t->ret[r]; mov[q] = t->values[r];
+            }
+            float am, as, amn, amx;
+            or_normalize_advantages(madv, sz, madvn, &am, &as, &amn, &amx);
+            or_mb_stats st;
+            or_minibatch_loss_grad(&t->net, t->params, sz, mo, mp, ma, mlp, madvn, mret, mov, mm, c,
+                                   t->c.ent_coef, grads, &st);
+            or_adam_step(&t->net, &t->adam, t->params, grads, t->c.lr, (float)c->max_grad_norm,
+                         c->adam_epsilon);
+            tp += st.policy_loss; tv += st.value_loss; th += st.entropy; tk += st.approx_kl;
+            tc += st.clip_fraction; tl += st.loss; tvm += st.value_mean; trm += st.returns_mean;
+            tam += am; tas += as;
+            tamin = fminf(tamin, amn); tamax = fmaxf(tamax, amx);
+            tvem += st.value_error_mean; tves += st.value_error_std;
+            tvemax = fmaxf(tvemax, st.value_error_max);
+            tav += st.avg_valid_actions; tevp += st.entropy_valid_pct;
+            nup++;
+            if (c->target_kl >= 0 && st.approx_kl > (float)c->target_kl) { stop = 1; break; } /* :2019-2023 */
+            start += sz;
+        }
+    }
+    if (m) {
+        float n = (float)nup;
+        memset(m, 0, sizeof *m);
+        m->policy_loss = tp / n; m->value_loss = tv / n; m->entropy = th / n;
+        m->entropy_scaled = m->entropy / logf((float)A);
+        m->approx_kl = tk / n; m->clip_fraction = tc / n;
+        m->explained_variance = or_explained_variance(t->values, t->ret, B);
+        m->total_loss = tl / n; m->value_mean = tvm / n; m->returns_mean = trm / n;
+        m->adv_mean_raw = tam / n; m->adv_std_raw = tas / n; m->adv_min_raw = tamin; m->adv_max_raw = tamax;
+        m->value_error_mean = tvem / n; m->value_error_std = tves / n; m->value_error_max = tvemax;
+        m->avg_valid_actions = t->has_masks ? tav / n : 0.0f;
+        m->entropy_valid_pct = t->has_masks ? tevp / n : 0.0f;
+        m->num_updates = nup; m->epochs_run = epochs_run;
+    }
+    free(idx); free(grads); free(mo); free(mp); free(mm); free(ma); free(mlp); free(madv);
+    free(mret); free(mov); free(madvn);
+    t->phase_s[2] = now_s() - t0;
+}
+
+size_t or_trainer_buffer(const or_trainer *t, const char *name, void *out, size_t bytes) {
+    size_t TN = (size_t)t->T * t->N;
+    const void *src = NULL; size_t n = 0;
+    if (!strcmp(name, "obs")) { src = t->obs; n = TN * t->D * 4; }
+    else if (!strcmp(name, "raw_obs")) { src = t->raw; n = TN * t->D * 4; }
+    else if (!strcmp(name, "priv")) { src = t->priv; n = t->G ? TN * t->G * 4 : 0; }
+    else if (!strcmp(name, "actions")) { src = t->actions; n = TN * 4; }
+    else if (!strcmp(name, "rewards")) { src = t->rewards; n = TN * 4; }
+    else if (!strcmp(name, "dones")) { src = t->dones; n = TN * 4; }
+    else if (!strcmp(name, "values")) { src = t->values; n = TN * 4; }
+    else if (!strcmp(name, "log_probs")) { src = t->logp; n = TN * 4; }
+    else if (!strcmp(name, "advantages")) { src = t->adv; n = TN * 4; }
+    else if (!strcmp(name, "returns")) { src = t->ret; n = TN * 4; }
+    else if (!strcmp(name, "players")) { src = t->players; n = TN * 4; }
+    else if (!strcmp(name, "all_rewards")) { src = t->all_r; n = TN * t->P * 4; }
+    else if (!strcmp(name, "masks")) { src = t->masks; n = t->masks ? TN * t->A * 4 : 0; }
+    else if (!strcmp(name, "last_v_pp")) { src = t->lvpp; n = (size_t)t->N * t->P * 4; }
+    if (!src) return 0;
+    if (out && bytes >= n) memcpy(out, src, n);
+    return n;
+}
+
+void or_trainer_obs_norm_state(const or_trainer *t, double *mean, double *var, double *count) {
+    if (mean) memcpy(mean, t->on.mean, sizeof(double) * t->D);
+    if (var) memcpy(var, t->on.var, sizeof(double) * t->D);
+    if (count) *count = t->on.count;
+}
+
+void or_trainer_ret_norm_state(const or_trainer *t, double *mvc, double *returns) {
+    if (mvc) { mvc[0] = t->rn.mean; mvc[1] = t->rn.var; mvc[2] = t->rn.count; }
+    if (returns) memcpy(returns, t->rn.returns, sizeof(double) * (size_t)t->N * t->P);
+}
+
+int or_trainer_episodes(const or_trainer *t, or_episode *out, int cap) {
+    int n = t->n_eps < cap ? t->n_eps : cap;
+    if (out) memcpy(out, t->eps, sizeof(or_episode) * n);
+    return t->n_eps;
+}

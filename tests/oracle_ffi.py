@@ -1,0 +1,330 @@
+"""ctypes bindings for the CPU oracle (oracle/build/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: the oracle is the parity checker and the timed CPU
+baseline.  The product path (burn-ppo_amd/bppo -> libbppo.so) never imports
+this module.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+LIB_PATH = os.path.join(ORACLE_DIR, "build", "liboracle.so")
+
+ENV_CARTPOLE, ENV_CONNECT_FOUR, ENV_LIARS_DICE = 0, 1, 2
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+
+
+class Rng(C.Structure):
+    _fields_ = [("key", C.c_uint32 * 8), ("stream", C.c_uint64), ("word_pos", C.c_uint64),
+                ("cached_block", C.c_uint64), ("block", C.c_uint32 * 16), ("rounds", C.c_int)]
+
+
+class CartPole(C.Structure):
+    _fields_ = [("x", C.c_float), ("x_dot", C.c_float), ("theta", C.c_float),
+                ("theta_dot", C.c_float), ("steps", C.c_int32), ("rng", Rng)]
+
+
+class ConnectFour(C.Structure):
+    _fields_ = [("board", (C.c_int8 * 7) * 6), ("current", C.c_int8), ("game_over", C.c_int8),
+                ("winner", C.c_int8)]
+
+
+class LiarsDice(C.Structure):
+    _fields_ = [("dice", (C.c_uint8 * 2) * 4), ("num_dice", C.c_uint8 * 4), ("current", C.c_uint8),
+                ("has_bid", C.c_int8), ("bid_qty", C.c_uint8), ("bid_face", C.c_uint8),
+                ("last_bidder", C.c_int8), ("bid_count", C.c_int32),
+                ("hist_player", C.c_uint8 * 16), ("hist_qty", C.c_uint8 * 16),
+                ("hist_face", C.c_uint8 * 16), ("hist_len", C.c_int32),
+                ("elim_order", C.c_int8 * 4), ("num_elim", C.c_int32), ("game_over", C.c_int8),
+                ("global_step", C.c_uint64), ("rng", Rng)]
+
+
+class Episode(C.Structure):
+    _fields_ = [("total_rewards", C.c_float * 4), ("length", C.c_int32), ("env_index", C.c_int32)]
+
+
+class NetDesc(C.Structure):
+    _fields_ = [("ctde", C.c_int), ("obs_dim", C.c_int), ("priv_dim", C.c_int), ("act_dim", C.c_int),
+                ("relu", C.c_int), ("n_actor", C.c_int), ("actor_width", C.c_int),
+                ("n_critic", C.c_int), ("critic_width", C.c_int), ("n_params", C.c_size_t)]
+
+
+class PpoCfg(C.Structure):
+    _fields_ = [("num_epochs", C.c_int), ("num_minibatches", C.c_int), ("clip_epsilon", C.c_float),
+                ("clip_epsilon_d", C.c_double), ("value_coef", C.c_double),
+                ("max_grad_norm", C.c_double), ("adam_epsilon", C.c_float),
+                ("target_kl", C.c_double), ("clip_value", C.c_int)]
+
+
+class TrainCfg(C.Structure):
+    _fields_ = [("env_kind", C.c_int), ("num_envs", C.c_int), ("num_steps", C.c_int),
+                ("hidden", C.c_int), ("num_hidden", C.c_int), ("relu", C.c_int), ("ctde", C.c_int),
+                ("critic_hidden", C.c_int), ("critic_num_hidden", C.c_int),
+                ("normalize_obs", C.c_int), ("normalize_returns", C.c_int),
+                ("return_clip", C.c_float), ("gamma", C.c_double), ("gae_lambda", C.c_double),
+                ("lr", C.c_double), ("ent_coef", C.c_double), ("reward_shaping", C.c_double),
+                ("ppo", PpoCfg), ("seed", C.c_uint64), ("threads", C.c_int)]
+
+
+class UpdateMetrics(C.Structure):
+    _fields_ = [(n, C.c_float) for n in (
+        "policy_loss", "value_loss", "entropy", "entropy_scaled", "approx_kl", "clip_fraction",
+        "explained_variance", "total_loss", "value_mean", "returns_mean", "adv_mean_raw",
+        "adv_std_raw", "adv_min_raw", "adv_max_raw", "value_error_mean", "value_error_std",
+        "value_error_max", "avg_valid_actions", "entropy_valid_pct")] + [
+        ("num_updates", C.c_int32), ("epochs_run", C.c_int32)]
+
+
+class MbStats(C.Structure):
+    _fields_ = [(n, C.c_float) for n in (
+        "loss", "policy_loss", "value_loss", "entropy", "approx_kl", "clip_fraction", "value_mean",
+        "returns_mean", "value_error_mean", "value_error_std", "value_error_max",
+        "avg_valid_actions", "entropy_valid_pct")]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = C.CDLL(LIB_PATH)
+        fp = np.ctypeslib.ndpointer
+        f32 = fp(np.float32, flags="C_CONTIGUOUS")
+        f64 = fp(np.float64, flags="C_CONTIGUOUS")
+        i32 = fp(np.int32, flags="C_CONTIGUOUS")
+        u32 = fp(np.uint32, flags="C_CONTIGUOUS")
+        u8 = fp(np.uint8, flags="C_CONTIGUOUS")
+        sig = {
+            "or_chacha_block": (None, [u32, C.c_uint64, C.c_uint64, C.c_int, u32]),
+            "or_rng_seed_u64": (None, [C.POINTER(Rng), C.c_uint64]),
+            "or_rng_next_u32": (C.c_uint32, [C.POINTER(Rng)]),
+            "or_rng_next_u64": (C.c_uint64, [C.POINTER(Rng)]),
+            "or_rng_fill_bytes": (None, [C.POINTER(Rng), u8, C.c_size_t]),
+            "or_gen_range_f32": (C.c_float, [C.POINTER(Rng), C.c_float, C.c_float]),
+            "or_gen_range_u32": (C.c_uint32, [C.POINTER(Rng), C.c_uint32, C.c_uint32]),
+            "or_gen_range_u8_incl": (C.c_uint8, [C.POINTER(Rng), C.c_uint8, C.c_uint8]),
+            "or_shuffle_u32": (None, [C.POINTER(Rng), u32, C.c_size_t]),
+            "or_rng_words": (None, [C.c_uint64, C.c_uint64, u32, C.c_size_t]),
+            "or_rng_words_key": (None, [u32, C.c_int, C.c_uint64, u32, C.c_size_t]),
+            "or_rng_seed_key": (None, [C.c_uint64, u32]),
+            "or_cartpole_new": (None, [C.POINTER(CartPole), C.c_uint64]),
+            "or_cartpole_reset": (None, [C.POINTER(CartPole), f32]),
+            "or_cartpole_step": (None, [C.POINTER(CartPole), C.c_int32, f32, C.POINTER(C.c_float),
+                                        C.POINTER(C.c_int)]),
+            "or_c4_new": (None, [C.POINTER(ConnectFour)]),
+            "or_c4_reset": (None, [C.POINTER(ConnectFour), f32]),
+            "or_c4_step": (None, [C.POINTER(ConnectFour), C.c_int32, f32, f32, C.POINTER(C.c_int)]),
+            "or_c4_mask": (None, [C.POINTER(ConnectFour), u8]),
+            "or_c4_get_obs": (None, [C.POINTER(ConnectFour), f32]),
+            "or_ld_new": (None, [C.POINTER(LiarsDice), C.c_uint64]),
+            "or_ld_reset": (None, [C.POINTER(LiarsDice), f32]),
+            "or_ld_step": (None, [C.POINTER(LiarsDice), C.c_int32, C.c_float, f32, f32,
+                                  C.POINTER(C.c_int)]),
+            "or_ld_mask": (None, [C.POINTER(LiarsDice), u8]),
+            "or_ld_priv": (None, [C.POINTER(LiarsDice), f32]),
+            "or_ld_get_obs": (None, [C.POINTER(LiarsDice), f32]),
+            "or_vecenv_new": (C.c_void_p, [C.c_int, C.c_int, C.c_uint64]),
+            "or_vecenv_free": (None, [C.c_void_p]),
+            "or_vecenv_get_obs": (None, [C.c_void_p, f32]),
+            "or_vecenv_get_players": (None, [C.c_void_p, i32]),
+            "or_vecenv_get_masks": (C.c_int, [C.c_void_p, u8]),
+            "or_vecenv_get_priv": (None, [C.c_void_p, f32]),
+            "or_vecenv_set_shaping": (None, [C.c_void_p, C.c_float]),
+            "or_vecenv_step": (C.c_int, [C.c_void_p, i32, f32, f32, u8, C.POINTER(Episode), C.c_int]),
+            "or_vecenv_env_ptr": (C.c_void_p, [C.c_void_p, C.c_int]),
+            "or_net_num_params": (C.c_size_t, [C.POINTER(NetDesc)]),
+            "or_net_forward": (None, [C.POINTER(NetDesc), f32, f32, C.c_void_p, C.c_size_t, f32, f32]),
+            "or_sample_categorical": (None, [C.POINTER(Rng), f32, C.c_size_t, C.c_int, i32]),
+            "or_log_prob": (C.c_float, [f32, C.c_int, C.c_int32]),
+            "or_entropy": (C.c_float, [f32, C.c_int]),
+            "or_compute_gae": (None, [f32, f32, f32, f32, C.c_int, C.c_int, C.c_float, C.c_float,
+                                      f32, f32]),
+            "or_compute_gae_mp": (None, [f32, i32, f32, f32, f32, C.c_int, C.c_int, C.c_int,
+                                         C.c_float, C.c_float, f32, f32]),
+            "or_explained_variance": (C.c_float, [f32, f32, C.c_size_t]),
+            "or_normalize_advantages": (None, [f32, C.c_size_t, f32, C.POINTER(C.c_float),
+                                               C.POINTER(C.c_float), C.POINTER(C.c_float),
+                                               C.POINTER(C.c_float)]),
+            "or_minibatch_loss_grad": (None, [C.POINTER(NetDesc), f32, C.c_size_t, f32, C.c_void_p,
+                                              i32, f32, f32, f32, f32, C.c_void_p, C.POINTER(PpoCfg),
+                                              C.c_double, f32, C.POINTER(MbStats)]),
+            "or_trainer_new": (C.c_void_p, [C.POINTER(TrainCfg), f32]),
+            "or_trainer_free": (None, [C.c_void_p]),
+            "or_trainer_num_params": (C.c_size_t, [C.c_void_p]),
+            "or_trainer_get_params": (None, [C.c_void_p, f32]),
+            "or_trainer_set_params": (None, [C.c_void_p, f32]),
+            "or_trainer_rng_pos": (C.c_uint64, [C.c_void_p]),
+            "or_trainer_collect": (C.c_int, [C.c_void_p]),
+            "or_trainer_gae": (None, [C.c_void_p]),
+            "or_trainer_update": (None, [C.c_void_p, C.POINTER(UpdateMetrics)]),
+            "or_trainer_buffer": (C.c_size_t, [C.c_void_p, C.c_char_p, C.c_void_p, C.c_size_t]),
+            "or_trainer_obs_norm_state": (None, [C.c_void_p, f64, f64, C.POINTER(C.c_double)]),
+            "or_trainer_ret_norm_state": (None, [C.c_void_p, f64, C.c_void_p]),
+            "or_trainer_episodes": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
+            "or_trainer_last_phase_seconds": (C.c_double, [C.c_void_p, C.c_int]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+# ------------------------------------------------------------- helpers ---
+def chacha_block(key_words, counter, stream=0, rounds=20):
+    out = np.zeros(16, np.uint32)
+    lib().or_chacha_block(np.asarray(key_words, np.uint32), counter, stream, rounds, out)
+    return out
+
+
+def stdrng_words(seed, n, skip=0):
+    out = np.zeros(n, np.uint32)
+    lib().or_rng_words(seed, skip, out, n)
+    return out
+
+
+def seed_key(seed):
+    k = np.zeros(8, np.uint32)
+    lib().or_rng_seed_key(seed, k)
+    return k
+
+
+def new_rng(seed):
+    r = Rng()
+    lib().or_rng_seed_u64(C.byref(r), seed)
+    return r
+
+
+def mlp_desc(obs_dim, act_dim, hidden, num_hidden, relu=True):
+    d = NetDesc(ctde=0, obs_dim=obs_dim, priv_dim=0, act_dim=act_dim, relu=int(relu),
+                n_actor=num_hidden, actor_width=hidden, n_critic=0, critic_width=0)
+    d.n_params = lib().or_net_num_params(C.byref(d))
+    return d
+
+
+def ctde_desc(obs_dim, priv_dim, act_dim, hidden, num_hidden, critic_hidden, critic_num_hidden,
+              relu=True):
+    d = NetDesc(ctde=1, obs_dim=obs_dim, priv_dim=priv_dim, act_dim=act_dim, relu=int(relu),
+                n_actor=num_hidden, actor_width=hidden, n_critic=critic_num_hidden,
+                critic_width=critic_hidden)
+    d.n_params = lib().or_net_num_params(C.byref(d))
+    return d
+
+
+def net_forward(desc, params, obs, priv=None):
+    B = obs.shape[0]
+    logits = np.zeros((B, desc.act_dim), np.float32)
+    values = np.zeros(B, np.float32)
+    pp = None if priv is None else np.ascontiguousarray(priv, np.float32)
+    lib().or_net_forward(C.byref(desc), np.ascontiguousarray(params, np.float32),
+                         np.ascontiguousarray(obs, np.float32),
+                         None if pp is None else pp.ctypes.data, B, logits, values)
+    return logits, values
+
+
+def compute_gae(rewards, dones, values, last_values, gamma, lam):
+    T, N = rewards.shape
+    adv = np.zeros((T, N), np.float32)
+    ret = np.zeros((T, N), np.float32)
+    lib().or_compute_gae(np.ascontiguousarray(rewards, np.float32), np.ascontiguousarray(dones, np.float32),
+                         np.ascontiguousarray(values, np.float32),
+                         np.ascontiguousarray(last_values, np.float32), T, N, gamma, lam, adv, ret)
+    return adv, ret
+
+
+def compute_gae_mp(all_rewards, players, dones, values, last_v_pp, gamma, lam):
+    T, N, P = all_rewards.shape
+    adv = np.zeros((T, N), np.float32)
+    ret = np.zeros((T, N), np.float32)
+    lib().or_compute_gae_mp(np.ascontiguousarray(all_rewards, np.float32),
+                            np.ascontiguousarray(players, np.int32),
+                            np.ascontiguousarray(dones, np.float32),
+                            np.ascontiguousarray(values, np.float32),
+                            np.ascontiguousarray(last_v_pp, np.float32), T, N, P, gamma, lam, adv, ret)
+    return adv, ret
+
+
+def ppo_cfg(num_epochs=4, num_minibatches=4, clip=0.2, value_coef=0.5, max_grad_norm=0.5,
+            adam_eps=1e-5, target_kl=None, clip_value=False):
+    return PpoCfg(num_epochs=num_epochs, num_minibatches=num_minibatches, clip_epsilon=clip,
+                  clip_epsilon_d=clip, value_coef=value_coef, max_grad_norm=max_grad_norm,
+                  adam_epsilon=adam_eps, target_kl=-1.0 if target_kl is None else target_kl,
+                  clip_value=int(clip_value))
+
+
+def train_cfg(env_kind=ENV_CARTPOLE, num_envs=8, num_steps=128, hidden=64, num_hidden=2, relu=True,
+              ctde=False, critic_hidden=0, critic_num_hidden=0, normalize_obs=True,
+              normalize_returns=True, return_clip=10.0, gamma=0.99, gae_lambda=0.95, lr=1e-3,
+              ent_coef=0.01, reward_shaping=0.0, seed=42, threads=0, **ppo):
+    return TrainCfg(env_kind=env_kind, num_envs=num_envs, num_steps=num_steps, hidden=hidden,
+                    num_hidden=num_hidden, relu=int(relu), ctde=int(ctde), critic_hidden=critic_hidden,
+                    critic_num_hidden=critic_num_hidden, normalize_obs=int(normalize_obs),
+                    normalize_returns=int(normalize_returns), return_clip=return_clip, gamma=gamma,
+                    gae_lambda=gae_lambda, lr=lr, ent_coef=ent_coef, reward_shaping=reward_shaping,
+                    ppo=ppo_cfg(**ppo), seed=seed, threads=threads)
+
+
+class Trainer:
+    """One oracle training run (main.rs:684-988 restated)."""
+
+    def __init__(self, cfg, params):
+        self.cfg = cfg
+        self.h = lib().or_trainer_new(C.byref(cfg), np.ascontiguousarray(params, np.float32))
+        self.n_params = lib().or_trainer_num_params(self.h)
+
+    def close(self):
+        if self.h:
+            lib().or_trainer_free(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def collect(self):
+        return lib().or_trainer_collect(self.h)
+
+    def gae(self):
+        lib().or_trainer_gae(self.h)
+
+    def update(self):
+        m = UpdateMetrics()
+        lib().or_trainer_update(self.h, C.byref(m))
+        return {k: getattr(m, k) for k, _ in UpdateMetrics._fields_}
+
+    def params(self):
+        out = np.zeros(self.n_params, np.float32)
+        lib().or_trainer_get_params(self.h, out)
+        return out
+
+    def rng_pos(self):
+        return lib().or_trainer_rng_pos(self.h)
+
+    def buffer(self, name, dtype=np.float32):
+        n = lib().or_trainer_buffer(self.h, name.encode(), None, 0)
+        out = np.zeros(n // 4, dtype)
+        lib().or_trainer_buffer(self.h, name.encode(), out.ctypes.data, n)
+        return out
+
+    def obs_norm_state(self, dim):
+        mean = np.zeros(dim, np.float64)
+        var = np.zeros(dim, np.float64)
+        cnt = C.c_double()
+        lib().or_trainer_obs_norm_state(self.h, mean, var, C.byref(cnt))
+        return mean, var, cnt.value
+
+    def ret_norm_state(self):
+        mvc = np.zeros(3, np.float64)
+        lib().or_trainer_ret_norm_state(self.h, mvc, None)
+        return mvc
+
+    def phase_seconds(self, ph):
+        return lib().or_trainer_last_phase_seconds(self.h, ph)

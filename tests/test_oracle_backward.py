@@ -1,0 +1,118 @@
+"""The oracle's hand-written PPO loss backward (oracle/net.c, restating
+ppo.rs:1385-1502 + Burn autodiff) checked against torch CPU autograd of the
+same loss expression in float64."""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+import oracle_ffi as O
+
+
+def layer_shapes(desc):
+    shapes = []
+    i = desc.obs_dim
+    for _ in range(desc.n_actor):
+        shapes.append((i, desc.actor_width)); i = desc.actor_width
+    shapes.append((i, desc.act_dim))
+    if desc.ctde:
+        c = desc.priv_dim + desc.obs_dim
+        for _ in range(desc.n_critic):
+            shapes.append((c, desc.critic_width)); c = desc.critic_width
+        shapes.append((c, 1))
+    else:
+        shapes.append((i, 1))
+    return shapes
+
+
+def torch_loss(desc, params, obs, priv, actions, old_logp, adv_n, returns, old_values, masks,
+               clip=0.2, vcoef=0.5, ent=0.01, clip_value=False):
+    p = torch.tensor(params, dtype=torch.float64, requires_grad=True)
+    off = 0
+    Ws = []
+    for (i, o) in layer_shapes(desc):
+        W = p[off:off + i * o].view(i, o); off += i * o
+        b = p[off:off + o]; off += o
+        Ws.append((W, b))
+    act = torch.relu if desc.relu else torch.tanh
+    x = torch.tensor(obs, dtype=torch.float64)
+    h = x
+    for W, b in Ws[:desc.n_actor]:
+        h = act(h @ W + b)
+    logits = h @ Ws[desc.n_actor][0] + Ws[desc.n_actor][1]
+    if desc.ctde:
+        hc = torch.cat([torch.tensor(priv, dtype=torch.float64), x], 1)
+        for W, b in Ws[desc.n_actor + 1:-1]:
+            hc = act(hc @ W + b)
+        v = (hc @ Ws[-1][0] + Ws[-1][1])[:, 0]
+    else:
+        v = (h @ Ws[-1][0] + Ws[-1][1])[:, 0]
+    if masks is not None:
+        logits = logits + (torch.tensor(masks, dtype=torch.float64) - 1.0) * 1e9
+    ls = torch.log_softmax(logits, 1)
+    newlp = ls.gather(1, torch.tensor(actions, dtype=torch.long)[:, None])[:, 0]
+    H = -(ls.exp() * ls).sum(1)
+    ratio = torch.exp(newlp - torch.tensor(old_logp, dtype=torch.float64))
+    na = -torch.tensor(adv_n, dtype=torch.float64)
+    pl = torch.maximum(na * ratio, na * ratio.clamp(1 - clip, 1 + clip)).mean()
+    R = torch.tensor(returns, dtype=torch.float64)
+    if clip_value:
+        vo = torch.tensor(old_values, dtype=torch.float64)
+        vc = vo + (v - vo).clamp(-clip, clip)
+        vl = torch.maximum((v - R) ** 2, (vc - R) ** 2).mean() * 0.5
+    else:
+        vl = ((v - R) ** 2).mean() * 0.5
+    loss = pl + vl * vcoef - H.mean() * ent
+    loss.backward()
+    return loss.item(), p.grad.numpy()
+
+
+def run_case(desc, mb, masks=False, seed=0, clip_value=False):
+    rng = np.random.default_rng(seed)
+    params = (rng.normal(size=desc.n_params) * 0.3).astype(np.float32)
+    obs = rng.normal(size=(mb, desc.obs_dim)).astype(np.float32)
+    priv = rng.normal(size=(mb, desc.priv_dim)).astype(np.float32) if desc.ctde else None
+    A = desc.act_dim
+    mk = None
+    if masks:
+        mk = (rng.random((mb, A)) < 0.6).astype(np.float32)
+        mk[np.arange(mb), rng.integers(0, A, mb)] = 1.0
+    actions = np.array([rng.choice(np.flatnonzero(mk[i])) if masks else rng.integers(0, A)
+                        for i in range(mb)], np.int32)
+    old_logp = (rng.normal(size=mb) * 0.3 - 1.0).astype(np.float32)
+    adv = rng.normal(size=mb).astype(np.float32)
+    ret = rng.normal(size=mb).astype(np.float32)
+    ov = rng.normal(size=mb).astype(np.float32)
+    cfg = O.ppo_cfg(clip_value=clip_value)
+    grads = np.zeros(desc.n_params, np.float32)
+    st = O.MbStats()
+    O.lib().or_minibatch_loss_grad(C.byref(desc), params, mb, obs,
+                                   None if priv is None else priv.ctypes.data, actions, old_logp,
+                                   adv, ret, ov, None if mk is None else mk.ctypes.data,
+                                   C.byref(cfg), 0.01, grads, C.byref(st))
+    loss_t, g_t = torch_loss(desc, params, obs, priv, actions, old_logp, adv, ret, ov, mk,
+                             clip_value=clip_value)
+    assert abs(st.loss - loss_t) <= 1e-5 * max(1.0, abs(loss_t))
+    scale = np.abs(g_t).max()
+    np.testing.assert_allclose(grads, g_t, rtol=0, atol=2e-5 * scale)
+
+
+def test_mlp_cartpole_shape():
+    run_case(O.mlp_desc(5, 2, 64, 2), mb=257)
+
+
+def test_mlp_masked_connect_four_shape():
+    run_case(O.mlp_desc(86, 7, 32, 2), mb=129, masks=True, seed=1)
+
+
+def test_ctde_liars_dice_shape():
+    run_case(O.ctde_desc(270, 120, 49, 32, 2, 48, 3), mb=65, masks=True, seed=2)
+
+
+def test_clip_value_branch():
+    run_case(O.mlp_desc(5, 2, 16, 1), mb=200, seed=3, clip_value=True)
+
+
+def test_tanh_activation():
+    run_case(O.mlp_desc(5, 2, 16, 2, relu=False), mb=100, seed=4)
