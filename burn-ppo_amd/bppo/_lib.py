@@ -1,0 +1,141 @@
+"""ctypes binding of libbppo.so (include/bppo.h).
+
+The library is built in-tree (burn-ppo_amd/bppo/libbppo.so, `make -C burn-ppo_amd`).
+There is no fallback: if the shared object is missing or fails to load, every
+entry point raises.  The product path never touches the CPU oracle.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libbppo.so")
+
+OK, ERR_ARG, ERR_NONFINITE, ERR_EMPTY_MASK, ERR_HIP, ERR_COMM, ERR_UNSUPPORTED = range(7)
+ENV_CARTPOLE, ENV_CONNECT_FOUR, ENV_LIARS_DICE = 0, 1, 2
+ENV_KINDS = {"cartpole": ENV_CARTPOLE, "connect_four": ENV_CONNECT_FOUR, "liars_dice": ENV_LIARS_DICE}
+
+
+class BppoError(RuntimeError):
+    def __init__(self, status, msg):
+        super().__init__(f"bppo status {status}: {msg}")
+        self.status = status
+
+
+class Config(C.Structure):
+    _fields_ = [("env_kind", C.c_int32), ("num_envs", C.c_int32), ("num_steps", C.c_int32),
+                ("hidden_size", C.c_int32), ("num_hidden", C.c_int32), ("relu", C.c_int32),
+                ("ctde", C.c_int32), ("critic_hidden_size", C.c_int32), ("critic_num_hidden", C.c_int32),
+                ("num_epochs", C.c_int32), ("num_minibatches", C.c_int32),
+                ("normalize_obs", C.c_int32), ("normalize_returns", C.c_int32), ("clip_value", C.c_int32),
+                ("gamma", C.c_double), ("gae_lambda", C.c_double), ("clip_epsilon", C.c_double),
+                ("value_coef", C.c_double), ("max_grad_norm", C.c_double), ("adam_epsilon", C.c_double),
+                ("target_kl", C.c_double), ("return_clip", C.c_double),
+                ("reward_shaping_coef", C.c_double), ("seed", C.c_uint64), ("env_seed_base", C.c_uint64),
+                ("rng_stream", C.c_uint64)]
+
+
+class Episode(C.Structure):
+    _fields_ = [("total_reward", C.c_float * 4), ("length", C.c_int32), ("env_index", C.c_int32),
+                ("step", C.c_int32), ("pad", C.c_int32)]
+
+
+class RolloutInfo(C.Structure):
+    _fields_ = [("episodes", C.c_int32), ("mean_return", C.c_float), ("mean_length", C.c_float),
+                ("pad", C.c_int32), ("rng_word_pos", C.c_uint64)]
+
+
+METRIC_NAMES = ("policy_loss", "value_loss", "entropy", "entropy_scaled", "approx_kl", "clip_fraction",
+                "explained_variance", "total_loss", "value_mean", "returns_mean", "adv_mean_raw",
+                "adv_std_raw", "adv_min_raw", "adv_max_raw", "value_error_mean", "value_error_std",
+                "value_error_max", "avg_valid_actions", "entropy_valid_pct")
+
+
+class UpdateMetrics(C.Structure):
+    _fields_ = [(n, C.c_float) for n in METRIC_NAMES] + [("num_updates", C.c_int32),
+                                                          ("epochs_run", C.c_int32)]
+
+
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_size_t, C.c_void_p)
+
+# every symbol declared in include/bppo.h (tests check the .so exports them all)
+EXPORTS = (
+    "bppo_create", "bppo_destroy", "bppo_last_error", "bppo_version", "bppo_num_params",
+    "bppo_params_set", "bppo_params_get", "bppo_forward", "bppo_rng_get", "bppo_rng_set",
+    "bppo_vecenv_reset", "bppo_vecenv_observe", "bppo_vecenv_step", "bppo_vecenv_set_step",
+    "bppo_obs_norm_get", "bppo_obs_norm_set", "bppo_ret_norm_get", "bppo_ret_norm_set",
+    "bppo_collect_rollouts", "bppo_rollout_episodes", "bppo_compute_gae", "bppo_ppo_update",
+    "bppo_set_allreduce", "bppo_buffer_get", "bppo_buffer_set", "bppo_gae_device",
+    "bppo_gae_mp_device", "bppo_last_kernel_ms", "bppo_debug_libm",
+)
+
+_lib = None
+
+
+def lib():
+    """Load libbppo.so (raises if it is absent: no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing; build it with `make -C burn-ppo_amd` "
+                           f"(or __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    vp, u64, sz, i32 = C.c_void_p, C.c_uint64, C.c_size_t, C.c_int32
+    fp = C.POINTER(C.c_float)
+    dp = C.POINTER(C.c_double)
+    sig = {
+        "bppo_create": (i32, [C.POINTER(Config), C.c_int, vp, C.POINTER(vp)]),
+        "bppo_destroy": (None, [vp]),
+        "bppo_last_error": (C.c_char_p, [vp]),
+        "bppo_version": (C.c_char_p, []),
+        "bppo_num_params": (sz, [vp]),
+        "bppo_params_set": (i32, [vp, vp, sz]),
+        "bppo_params_get": (i32, [vp, vp, sz]),
+        "bppo_forward": (i32, [vp, vp, vp, i32, vp, vp]),
+        "bppo_rng_get": (i32, [vp, C.POINTER(u64)]),
+        "bppo_rng_set": (i32, [vp, u64]),
+        "bppo_vecenv_reset": (i32, [vp]),
+        "bppo_vecenv_observe": (i32, [vp, vp, vp, vp, vp]),
+        "bppo_vecenv_step": (i32, [vp, vp, vp, vp, vp, vp, i32, C.POINTER(i32)]),
+        "bppo_vecenv_set_step": (i32, [vp, u64]),
+        "bppo_obs_norm_get": (i32, [vp, vp, vp, dp]),
+        "bppo_obs_norm_set": (i32, [vp, vp, vp, C.c_double]),
+        "bppo_ret_norm_get": (i32, [vp, vp, vp]),
+        "bppo_ret_norm_set": (i32, [vp, vp, vp]),
+        "bppo_collect_rollouts": (i32, [vp, C.POINTER(RolloutInfo)]),
+        "bppo_rollout_episodes": (i32, [vp, vp, i32, C.POINTER(i32)]),
+        "bppo_compute_gae": (i32, [vp]),
+        "bppo_ppo_update": (i32, [vp, C.c_double, C.c_double, C.POINTER(UpdateMetrics)]),
+        "bppo_set_allreduce": (i32, [vp, ALLREDUCE_FN, vp, i32]),
+        "bppo_buffer_get": (i32, [vp, C.c_char_p, vp, sz]),
+        "bppo_buffer_set": (i32, [vp, C.c_char_p, vp, sz]),
+        "bppo_gae_device": (i32, [vp, vp, vp, vp, i32, i32, C.c_float, C.c_float, vp, vp, vp]),
+        "bppo_gae_mp_device": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, C.c_float, C.c_float, vp, vp,
+                                     vp]),
+        "bppo_last_kernel_ms": (i32, [vp, C.c_char_p, fp]),
+        "bppo_debug_libm": (i32, [i32, i32, vp, vp, sz]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def check(status, ctx=None):
+    if status != OK:
+        msg = lib().bppo_last_error(ctx).decode() if ctx else ""
+        raise BppoError(status, msg)
+
+
+def ptr(a):
+    """data pointer of a numpy array or torch tensor (host or device)."""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        assert a.flags["C_CONTIGUOUS"]
+        return a.ctypes.data
+    return a.data_ptr()

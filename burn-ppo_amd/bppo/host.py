@@ -1,0 +1,134 @@
+"""Host-side pieces of the reference's interface that are plain arithmetic:
+config presets (configs/*.toml), minibatch split (ppo.rs:1820-1831), the
+learning-rate schedule (schedule.rs:54-78), orthogonal init (mlp.rs:16-38)."""
+import numpy as np
+
+from . import _lib as L
+
+
+def minibatch_sizes(batch_size, num_minibatches):
+    """ppo.rs:1820-1831: base = B / M, the first B % M minibatches get +1; empty ones skipped."""
+    base, rem = divmod(batch_size, num_minibatches)
+    return [base + (1 if i < rem else 0) for i in range(num_minibatches)
+            if base + (1 if i < rem else 0) > 0]
+
+
+def schedule_get(points, step):
+    """schedule.rs:54-78 piecewise-linear [(value, step), ...]."""
+    if not points:
+        return 0.0
+    if len(points) == 1 or step <= points[0][1]:
+        return float(points[0][0])
+    for (v1, s1), (v2, s2) in zip(points, points[1:]):
+        if s1 <= step < s2:
+            return v1 + (v2 - v1) * ((step - s1) / (s2 - s1))
+    return float(points[-1][0])
+
+
+# config presets = the reference's configs + BASELINE.json sizes (SURVEY.md CfgA..CfgE)
+BASE = dict(env="cartpole", num_envs=32, num_steps=128, hidden_size=64, num_hidden=2, activation="relu",
+            network_type="mlp", critic_hidden_size=None, critic_num_hidden=None, num_epochs=4,
+            num_minibatches=4, normalize_obs=False, normalize_returns=None, clip_value=False, gamma=0.99,
+            gae_lambda=0.95, clip_epsilon=0.2, value_coef=0.5, max_grad_norm=0.5, adam_epsilon=1e-5,
+            target_kl=None, return_clip=10.0, reward_shaping_coef=0.0, learning_rate=[(2.5e-4, 0)],
+            entropy_coef=[(0.01, 0)], seed=42)
+
+PRESETS = {
+    # configs/test.toml (CfgA runs it with --num-envs 8 --num-steps 128)
+    "test": dict(num_envs=2, num_steps=8, num_epochs=1, num_minibatches=1, hidden_size=16, num_hidden=1,
+                 learning_rate=[(1e-3, 0)]),
+    # configs/cartpole.toml (CfgB: num_envs 65536)
+    "cartpole": dict(num_envs=32, learning_rate=[(1e-3, 0)], entropy_coef=[(0.01, 0)], normalize_obs=True,
+                     num_epochs=4, hidden_size=64, num_hidden=2),
+    # configs/connect_four.toml (CfgC: num_envs 16384, pool off)
+    "connect_four": dict(env="connect_four", num_envs=128, num_steps=64,
+                         learning_rate=[(1e-3, 0), (1e-4, 40_000_000)], clip_epsilon=0.1,
+                         entropy_coef=[(0.05, 0)], target_kl=0.02, num_epochs=6, hidden_size=512),
+    # configs/liars_dice_ctde.toml (CfgD: num_envs 32768, pool off)
+    "liars_dice_ctde": dict(env="liars_dice", num_envs=256, network_type="ctde", hidden_size=256,
+                            critic_hidden_size=512, critic_num_hidden=3, reward_shaping_coef=0.05,
+                            learning_rate=[(3e-4, 0)], gamma=0.97, gae_lambda=0.90,
+                            entropy_coef=[(0.05, 0)], value_coef=1.0, target_kl=0.025, num_epochs=4,
+                            num_minibatches=8),
+}
+
+
+def make_config(preset="cartpole", **over):
+    c = dict(BASE)
+    c.update(PRESETS[preset])
+    c.update(over)
+    return c
+
+
+def num_players(env):
+    return {"cartpole": 1, "connect_four": 2, "liars_dice": 4}[env]
+
+
+def to_struct(c, rank=0, world=1, envs_per_rank=None):
+    n = envs_per_rank if envs_per_rank is not None else c["num_envs"]
+    nr = c["normalize_returns"]
+    if nr is None:
+        nr = num_players(c["env"]) == 1          # main.rs:243
+    s = L.Config()
+    s.env_kind = L.ENV_KINDS[c["env"]]
+    s.num_envs = n
+    s.num_steps = c["num_steps"]
+    s.hidden_size = c["hidden_size"]
+    s.num_hidden = c["num_hidden"]
+    s.relu = int(c["activation"] == "relu")
+    s.ctde = int(c["network_type"] == "ctde")
+    s.critic_hidden_size = c["critic_hidden_size"] or c["hidden_size"]
+    s.critic_num_hidden = c["critic_num_hidden"] or c["num_hidden"]
+    s.num_epochs = c["num_epochs"]
+    s.num_minibatches = c["num_minibatches"]
+    s.normalize_obs = int(c["normalize_obs"])
+    s.normalize_returns = int(nr)
+    s.clip_value = int(c["clip_value"])
+    for k in ("gamma", "gae_lambda", "clip_epsilon", "value_coef", "max_grad_norm", "adam_epsilon",
+              "return_clip", "reward_shaping_coef"):
+        setattr(s, k, float(c[k]))
+    s.target_kl = -1.0 if c["target_kl"] is None else float(c["target_kl"])
+    s.seed = c["seed"]
+    # W > 1: global env index = rank * n + i; main RNG stream = rank
+    s.env_seed_base = c["seed"] + rank * n
+    s.rng_stream = rank if world > 1 else 0
+    return s
+
+
+def layer_shapes(c):
+    """Burn record order: hidden..., policy head, value head (MLP) /
+    actor hidden..., policy, critic hidden..., value (CTDE)."""
+    obs = {"cartpole": 5, "connect_four": 86, "liars_dice": 270}[c["env"]]
+    act = {"cartpole": 2, "connect_four": 7, "liars_dice": 49}[c["env"]]
+    shapes, gains = [], []
+    hg = np.sqrt(2.0) if c["activation"] == "relu" else 1.0
+    i = obs
+    for _ in range(c["num_hidden"]):
+        shapes.append((i, c["hidden_size"])); gains.append(hg); i = c["hidden_size"]
+    shapes.append((i, act)); gains.append(0.01)
+    if c["network_type"] == "ctde":
+        ci = 120 + obs
+        for _ in range(c["critic_num_hidden"] or c["num_hidden"]):
+            w = c["critic_hidden_size"] or c["hidden_size"]
+            shapes.append((ci, w)); gains.append(hg); ci = w
+        shapes.append((ci, 1)); gains.append(1.0)
+    else:
+        shapes.append((i, 1)); gains.append(1.0)
+    return shapes, gains
+
+
+def orthogonal_init(c, seed=0):
+    """mlp.rs:16-38 / ctde.rs:64-123: orthogonal weights with gains sqrt(2)|1 (hidden),
+    0.01 (policy), 1.0 (value); zero biases.  Burn's init RNG is not reproducible
+    here, so parity runs load these weights into both the oracle and the device."""
+    rng = np.random.default_rng(seed)
+    out = []
+    shapes, gains = layer_shapes(c)
+    for (i, o), g in zip(shapes, gains):
+        a = rng.standard_normal((max(i, o), min(i, o)))
+        q, r = np.linalg.qr(a)
+        q = q * np.sign(np.diag(r))
+        w = q if i >= o else q.T
+        out.append((g * w).astype(np.float32).reshape(-1))
+        out.append(np.zeros(o, np.float32))
+    return np.concatenate(out)

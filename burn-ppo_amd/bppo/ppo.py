@@ -1,0 +1,263 @@
+"""The reference's hot-path surfaces, MI355X-native underneath.
+
+Mirrors burn-ppo's in-process interfaces with the same names and argument
+meaning, so a caller of the reference finds the same calls:
+
+    VecEnv                 env.rs:270-487  (new / step / get_observations / ...)
+    ActorCritic            network/mod.rs:28-189 (forward / params)
+    RolloutBuffer          ppo.rs:52-200  (device-resident; fields exported on demand)
+    collect_rollouts       ppo.rs:213-500
+    compute_gae            ppo.rs:1069-1124 (bootstrap from main.rs:877-947)
+    ppo_update             ppo.rs:1661-2112
+    Trainer.train_update   one iteration of run_training's loop, main.rs:684-988
+
+All state lives in HBM inside one libbppo context (bppo_ctx); these wrappers only
+marshal host arrays.  Errors that the reference panics on (NaN log-probs,
+empty action masks) raise BppoError.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+from .host import make_config, orthogonal_init, schedule_get, to_struct
+
+
+class Context:
+    """Owns one bppo_ctx (device buffers, env state, params, Adam, RNG)."""
+
+    def __init__(self, cfg, device=0, stream=None, rank=0, world=1, envs_per_rank=None):
+        self.cfg = cfg
+        self.struct = to_struct(cfg, rank, world, envs_per_rank)
+        h = C.c_void_p()
+        st = L.lib().bppo_create(C.byref(self.struct), device, stream, C.byref(h))
+        self.h = h
+        if st != L.OK:
+            msg = L.lib().bppo_last_error(h).decode() if h else ""
+            if h:
+                L.lib().bppo_destroy(h)
+            self.h = None
+            raise L.BppoError(st, msg)
+        self.N = self.struct.num_envs
+        self.T = self.struct.num_steps
+        self.n_params = L.lib().bppo_num_params(self.h)
+        self.obs_dim = {"cartpole": 5, "connect_four": 86, "liars_dice": 270}[cfg["env"]]
+        self.num_actions = {"cartpole": 2, "connect_four": 7, "liars_dice": 49}[cfg["env"]]
+        self._ar_keep = None
+
+    def close(self):
+        if self.h:
+            L.lib().bppo_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, st):
+        L.check(st, self.h)
+
+    # parity hooks -------------------------------------------------------
+    def buffer(self, name, dtype=np.float32, shape=None):
+        n = {"obs": self.T * self.N * self.obs_dim, "last_values": self.N,
+             "grad": self.n_params}.get(name, self.T * self.N)
+        out = np.zeros(n, dtype)
+        self._chk(L.lib().bppo_buffer_get(self.h, name.encode(), out.ctypes.data, out.nbytes))
+        return out.reshape(shape) if shape else out
+
+    def set_buffer(self, name, arr):
+        arr = np.ascontiguousarray(arr)
+        self._chk(L.lib().bppo_buffer_set(self.h, name.encode(), arr.ctypes.data, arr.nbytes))
+
+    def rng_pos(self):
+        p = C.c_uint64()
+        self._chk(L.lib().bppo_rng_get(self.h, C.byref(p)))
+        return p.value
+
+    def set_rng_pos(self, p):
+        self._chk(L.lib().bppo_rng_set(self.h, p))
+
+    def obs_norm(self):
+        m = np.zeros(self.obs_dim); v = np.zeros(self.obs_dim); c = C.c_double()
+        self._chk(L.lib().bppo_obs_norm_get(self.h, m.ctypes.data, v.ctypes.data, C.byref(c)))
+        return m, v, c.value
+
+    def set_obs_norm(self, mean, m2, count):
+        mean = np.ascontiguousarray(mean, np.float64); m2 = np.ascontiguousarray(m2, np.float64)
+        self._chk(L.lib().bppo_obs_norm_set(self.h, mean.ctypes.data, m2.ctypes.data, float(count)))
+
+    def ret_norm(self):
+        mvc = np.zeros(3); r = np.zeros(self.N)
+        self._chk(L.lib().bppo_ret_norm_get(self.h, mvc.ctypes.data, r.ctypes.data))
+        return mvc, r
+
+    def set_ret_norm(self, mvc, returns):
+        mvc = np.ascontiguousarray(mvc, np.float64); r = np.ascontiguousarray(returns, np.float64)
+        self._chk(L.lib().bppo_ret_norm_set(self.h, mvc.ctypes.data, r.ctypes.data))
+
+    def kernel_ms(self, name):
+        f = C.c_float()
+        self._chk(L.lib().bppo_last_kernel_ms(self.h, name.encode(), C.byref(f)))
+        return f.value
+
+    def set_allreduce(self, fn, world):
+        """fn(device_ptr:int, n:int) -> None must leave the SUM over ranks in place."""
+        def _cb(p, n, user):
+            try:
+                fn(p, n)
+                return 0
+            except Exception:
+                return 1
+        self._ar_keep = L.ALLREDUCE_FN(_cb)
+        self._chk(L.lib().bppo_set_allreduce(self.h, self._ar_keep, None, world))
+
+
+class VecEnv:
+    """env.rs VecEnv over the device-resident envs (CartPole in this build)."""
+
+    def __init__(self, ctx):
+        self.ctx = ctx
+
+    @classmethod
+    def new(cls, ctx):
+        """VecEnv::new(num_envs, |i| E::new(seed + i)) — env.rs:281-302."""
+        v = cls(ctx)
+        v.ctx._chk(L.lib().bppo_vecenv_reset(ctx.h))
+        return v
+
+    def num_envs(self):
+        return self.ctx.N
+
+    def get_observations(self):
+        o = np.zeros(self.ctx.N * self.ctx.obs_dim, np.float32)
+        self.ctx._chk(L.lib().bppo_vecenv_observe(self.ctx.h, o.ctypes.data, None, None, None))
+        return o
+
+    def get_current_players(self):
+        p = np.zeros(self.ctx.N, np.int32)
+        self.ctx._chk(L.lib().bppo_vecenv_observe(self.ctx.h, None, p.ctypes.data, None, None))
+        return p
+
+    def get_action_masks(self):
+        return None     # CartPole has no masks (Environment::action_mask default None)
+
+    def set_step(self, step):
+        self.ctx._chk(L.lib().bppo_vecenv_set_step(self.ctx.h, int(step)))
+
+    def step(self, actions):
+        """-> (obs [N*obs], rewards [N][P], dones [N] bool, completed episodes)"""
+        N = self.ctx.N
+        a = np.ascontiguousarray(actions, np.int32)
+        obs = np.zeros(N * self.ctx.obs_dim, np.float32)
+        rew = np.zeros(N, np.float32)
+        dn = np.zeros(N, np.uint8)
+        cap = N
+        eps = (L.Episode * cap)()
+        n = C.c_int32()
+        self.ctx._chk(L.lib().bppo_vecenv_step(self.ctx.h, a.ctypes.data, obs.ctypes.data, rew.ctypes.data,
+                                               dn.ctypes.data, eps, cap, C.byref(n)))
+        done_eps = [dict(total_rewards=[eps[i].total_reward[0]], length=eps[i].length,
+                         env_index=eps[i].env_index) for i in range(min(n.value, cap))]
+        return obs, rew.reshape(N, 1), dn.astype(bool), done_eps
+
+
+class ActorCritic:
+    """ActorCriticNetwork (network/mod.rs): flat params in Burn record order."""
+
+    def __init__(self, ctx):
+        self.ctx = ctx
+
+    def is_ctde(self):
+        return self.ctx.cfg["network_type"] == "ctde"
+
+    def get_params(self):
+        out = np.zeros(self.ctx.n_params, np.float32)
+        self.ctx._chk(L.lib().bppo_params_get(self.ctx.h, out.ctypes.data, out.size))
+        return out
+
+    def set_params(self, p):
+        p = np.ascontiguousarray(p, np.float32)
+        self.ctx._chk(L.lib().bppo_params_set(self.ctx.h, p.ctypes.data, p.size))
+
+    def forward(self, obs):
+        """network/mod.rs:93-114 -> (logits [B, A], values [B, 1])"""
+        obs = np.ascontiguousarray(obs, np.float32).reshape(-1, self.ctx.obs_dim)
+        B = obs.shape[0]
+        lg = np.zeros((B, self.ctx.num_actions), np.float32)
+        v = np.zeros(B, np.float32)
+        self.ctx._chk(L.lib().bppo_forward(self.ctx.h, obs.ctypes.data, None, B, lg.ctypes.data,
+                                           v.ctypes.data))
+        return lg, v.reshape(B, 1)
+
+
+class RolloutBuffer:
+    """ppo.rs:52-200; the [T, N, ...] fields stay in HBM and are exported on demand."""
+
+    def __init__(self, ctx):
+        self.ctx = ctx
+
+    def __getattr__(self, name):
+        ctx = self.__dict__["ctx"]
+        T, N = ctx.T, ctx.N
+        if name == "observations":
+            return ctx.buffer("obs").reshape(T, N, ctx.obs_dim)
+        if name == "actions":
+            return ctx.buffer("actions", np.int32).reshape(T, N)
+        if name in ("rewards", "dones", "values", "log_probs", "advantages", "returns"):
+            return ctx.buffer(name).reshape(T, N)
+        raise AttributeError(name)
+
+
+def collect_rollouts(ctx):
+    """ppo.rs:213-500.  Returns (rollout info, last_value_per_player is implicit
+    on device).  The main RNG advances by T*N*A words exactly as the reference."""
+    info = L.RolloutInfo()
+    ctx._chk(L.lib().bppo_collect_rollouts(ctx.h, C.byref(info)))
+    return info
+
+
+def compute_gae(ctx):
+    """main.rs:877-947 bootstrap (updated obs stats) + ppo.rs:1069-1124."""
+    ctx._chk(L.lib().bppo_compute_gae(ctx.h))
+
+
+def ppo_update(ctx, learning_rate, entropy_coef):
+    """ppo.rs:1661-2112 -> UpdateMetrics dict."""
+    m = L.UpdateMetrics()
+    ctx._chk(L.lib().bppo_ppo_update(ctx.h, float(learning_rate), float(entropy_coef), C.byref(m)))
+    d = {k: getattr(m, k) for k in L.METRIC_NAMES}
+    d["num_updates"] = m.num_updates
+    d["epochs_run"] = m.epochs_run
+    return d
+
+
+class Trainer:
+    """run_training's per-update loop body (main.rs:684-988) on one GPU (or one
+    rank of a data-parallel job)."""
+
+    def __init__(self, cfg=None, device=0, params=None, init_seed=0, **kw):
+        self.cfg = cfg or make_config("cartpole")
+        self.ctx = Context(self.cfg, device=device, **kw)
+        self.model = ActorCritic(self.ctx)
+        self.vec_env = VecEnv(self.ctx)
+        self.buffer = RolloutBuffer(self.ctx)
+        self.model.set_params(orthogonal_init(self.cfg, init_seed) if params is None else params)
+        self.global_step = 0
+        self.recent_returns = []
+
+    def train_update(self):
+        lr = schedule_get(self.cfg["learning_rate"], self.global_step)         # main.rs:706
+        ent = schedule_get(self.cfg["entropy_coef"], self.global_step)         # main.rs:716
+        self.vec_env.set_step(self.global_step)
+        info = collect_rollouts(self.ctx)
+        compute_gae(self.ctx)
+        metrics = ppo_update(self.ctx, lr, ent)
+        self.global_step += self.ctx.T * self.ctx.N                           # main.rs:988
+        metrics["episodes"] = info.episodes
+        metrics["mean_return"] = info.mean_return
+        return metrics
+
+    def close(self):
+        self.ctx.close()

@@ -1,0 +1,730 @@
+// bppo_api.hip — the C-ABI (include/bppo.h): context lifecycle, the
+// host-side orchestration of one update (collect_rollouts -> bootstrap + GAE ->
+// ppo_update, main.rs:724-963), the rand-0.8 shuffle chain thread, parity hooks.
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include "bppo_internal.h"
+
+using namespace bppo;
+
+namespace bppo {
+
+NetLayout make_layout(const bppo_config &c, int obs_dim, int priv_dim, int act_dim) {
+    NetLayout L;
+    L.ctde = c.ctde; L.relu = c.relu;
+    size_t off = 0;
+    auto add = [&](int in, int out) {
+        int i = L.n_layers++;
+        L.in[i] = in; L.out[i] = out; L.w[i] = off; off += (size_t)in * out; L.b[i] = off; off += out;
+        return i;
+    };
+    int in = obs_dim;
+    for (int l = 0; l < c.num_hidden; l++) { add(in, c.hidden_size); in = c.hidden_size; }
+    L.n_actor_hidden = c.num_hidden;
+    L.policy = add(in, act_dim);
+    if (c.ctde) {
+        int cin = priv_dim + obs_dim;
+        L.critic_first = L.n_layers;
+        for (int l = 0; l < c.critic_num_hidden; l++) { add(cin, c.critic_hidden_size); cin = c.critic_hidden_size; }
+        L.value = add(cin, 1);
+    } else {
+        L.value = add(in, 1);
+    }
+    L.n_params = off;
+    return L;
+}
+
+// ------------------------------------------------------------ shuffle chain --
+// rand 0.8.5 shuffle: for i in (1..n).rev(): j = gen_range(0..i+1) with
+// UniformInt<u32>: zone = (range << lz(range)) - 1, draw until lo(w*range) <= zone.
+static void host_chacha_words(const Key8 &key, uint64_t stream, uint64_t pos, uint32_t *out,
+                              size_t n) {
+    // block-parallel fill: every ChaCha block is independent
+    const uint64_t b0 = pos >> 4, b1 = (pos + n + 15) >> 4;
+    const int64_t nb = (int64_t)(b1 - b0);
+    const int nt = (int)std::min<int64_t>(8, std::max<int64_t>(1, nb / 4096));
+    auto work = [&](int tid) {
+        for (int64_t bi = tid; bi < nb; bi += nt) {
+            uint32_t blk[16];
+            chacha12_block(key, b0 + (uint64_t)bi, stream, blk);
+            for (int w = 0; w < 16; w++) {
+                const uint64_t p = ((b0 + (uint64_t)bi) << 4) + w;
+                if (p >= pos && p < pos + n) out[p - pos] = blk[w];
+            }
+        }
+    };
+    std::vector<std::thread> ths;
+    for (int t = 1; t < nt; t++) ths.emplace_back(work, t);
+    work(0);
+    for (auto &t : ths) t.join();
+}
+
+void ShuffleEngine::start(const Key8 &k, uint64_t strm, uint64_t pos, uint32_t n_, int epochs_) {
+    join();
+    key = k; stream = strm; start_pos = pos; n = n_; epochs = epochs_;
+    ready = 0;
+    end_pos.assign(epochs, 0);
+    const size_t need = (size_t)epochs * n;
+    if (need > J_cap) {
+        if (J) (void)hipHostFree(J);
+        J = nullptr;
+        if (hipHostMalloc((void **)&J, need * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
+            J = (uint32_t *)malloc(need * sizeof(uint32_t));
+        }
+        J_cap = need;
+    }
+    running = true;
+    th = std::thread([this]() {
+        uint64_t pos = start_pos;
+        std::vector<uint32_t> words;
+        for (int e = 0; e < epochs; e++) {
+            uint32_t *Je = J + (size_t)e * n;
+            if (n >= 2) {
+                // generous word window; refilled if a long rejection run exhausts it
+                size_t cap = (size_t)n + n / 2 + 4096, used = 0;
+                words.resize(cap);
+                host_chacha_words(key, stream, pos, words.data(), cap);
+                for (uint32_t i = n - 1; i >= 1; i--) {
+                    const uint32_t range = i + 1;
+                    const uint32_t zone = (range << __builtin_clz(range)) - 1u;
+                    for (;;) {
+                        if (used == cap) {
+                            pos += cap; used = 0;
+                            host_chacha_words(key, stream, pos, words.data(), cap);
+                        }
+                        const uint64_t m = (uint64_t)words[used++] * range;
+                        if ((uint32_t)m <= zone) { Je[i] = (uint32_t)(m >> 32); break; }
+                    }
+                }
+                pos += used;
+                Je[0] = 0;
+            }
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                end_pos[e] = pos;
+                ready = e + 1;
+            }
+            cv.notify_all();
+        }
+    });
+}
+
+void ShuffleEngine::wait_epoch(int e) {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return ready > e; });
+}
+
+void ShuffleEngine::join() {
+    if (th.joinable()) th.join();
+    running = false;
+}
+
+ShuffleEngine::~ShuffleEngine() {
+    join();
+    if (J) (void)hipHostFree(J);
+}
+
+// ----------------------------------------------------------- libm check ----
+__global__ void k_libm(int which, const float *x, float *y, size_t n) {
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float v = x[i];
+    switch (which) {
+    case 0: y[i] = bppo_math::logf_glibc(v); break;
+    case 1: y[i] = bppo_math::sinf_glibc(v); break;
+    case 2: y[i] = bppo_math::cosf_glibc(v); break;
+    case 3: y[i] = -bppo_math::logf_glibc(-bppo_math::logf_glibc(v)); break;
+    default: y[i] = bppo_math::expf_glibc(v); break;
+    }
+}
+
+bppo_status launch_libm(int which, const float *d_x, float *d_y, size_t n) {
+    hipLaunchKernelGGL(k_libm, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, which, d_x, d_y, n);
+    return hipGetLastError() == hipSuccess ? BPPO_OK : BPPO_ERR_HIP;
+}
+
+}  // namespace bppo
+
+// ======================================================================= ABI
+static float powi_f32(float a, int b) {   // compiler-rt __powisf2 (Rust f32::powi)
+    int recip = b < 0;
+    float r = 1.0f;
+    for (;;) {
+        if (b & 1) r *= a;
+        b /= 2;
+        if (b == 0) break;
+        a *= a;
+    }
+    return recip ? 1.0f / r : r;
+}
+
+template <class T>
+static bppo_status dalloc(bppo_ctx *c, T **p, size_t n) {
+    *p = nullptr;
+    if (n == 0) return BPPO_OK;
+    BPPO_HIP(c, hipMalloc((void **)p, n * sizeof(T)));
+    BPPO_HIP(c, hipMemsetAsync(*p, 0, n * sizeof(T), c->stream));
+    return BPPO_OK;
+}
+
+#define TRY(x)                                 \
+    do {                                       \
+        bppo_status _s = (x);                  \
+        if (_s != BPPO_OK) return _s;          \
+    } while (0)
+
+extern "C" const char *bppo_version(void) { return "bppo-mi355x 0.1 (gfx950)"; }
+
+extern "C" const char *bppo_last_error(const bppo_ctx *c) { return c ? c->err.c_str() : "null ctx"; }
+
+static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *stream) {
+    c->cfg = *cfg;
+    c->dev = dev;
+    BPPO_HIP(c, hipSetDevice(dev));
+    if (stream) { c->stream = (hipStream_t)stream; c->own_stream = false; }
+    else { BPPO_HIP(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)); c->own_stream = true; }
+    if (cfg->num_envs <= 0 || cfg->num_steps <= 0 || cfg->num_epochs <= 0 || cfg->num_minibatches <= 0) {
+        c->err = "num_envs, num_steps, num_epochs, num_minibatches must be positive";
+        return BPPO_ERR_ARG;
+    }
+    c->N = cfg->num_envs; c->T = cfg->num_steps;
+    switch (cfg->env_kind) {
+    case BPPO_ENV_CARTPOLE: c->D = 5; c->A = 2; c->P = 1; c->G = 0; break;
+    case BPPO_ENV_CONNECT_FOUR: c->D = 86; c->A = 7; c->P = 2; c->G = 0; break;
+    case BPPO_ENV_LIARS_DICE: c->D = 270; c->A = 49; c->P = 4; c->G = cfg->ctde ? 120 : 0; break;
+    default: c->err = "unknown env_kind"; return BPPO_ERR_ARG;
+    }
+    if (cfg->env_kind != BPPO_ENV_CARTPOLE) {
+        c->err = "device rollout path implemented for CartPole only in this build "
+                 "(Connect Four / Liar's Dice: oracle + multiplayer GAE kernel only)";
+        return BPPO_ERR_UNSUPPORTED;
+    }
+    c->net = make_layout(*cfg, c->D, c->G, c->A);
+    const size_t np = c->net.n_params;
+    const size_t TN = (size_t)c->T * c->N;
+    c->adam_t.assign(2 * c->net.n_layers, 0);
+    TRY(dalloc(c, &c->d_params, np));
+    TRY(dalloc(c, &c->d_m1, np));
+    TRY(dalloc(c, &c->d_m2, np));
+    TRY(dalloc(c, &c->d_grad, np + 64));
+    c->slab_rows = 256 * 4;   // one 4-wave block per CU, persistent over the minibatch
+    TRY(dalloc(c, &c->d_slab, c->slab_rows * (np + 64)));
+    TRY(dalloc(c, &c->d_cp, (size_t)4 * c->N));
+    TRY(dalloc(c, &c->d_steps, (size_t)c->N));
+    TRY(dalloc(c, &c->d_env_pos, (size_t)c->N));
+    TRY(dalloc(c, &c->d_ep_ret, (size_t)c->N * c->P));
+    TRY(dalloc(c, &c->d_ep_len, (size_t)c->N));
+    TRY(dalloc(c, &c->d_obs, TN * c->D));
+    TRY(dalloc(c, &c->d_rew, TN));
+    TRY(dalloc(c, &c->d_rew_raw, TN));
+    TRY(dalloc(c, &c->d_done, TN));
+    TRY(dalloc(c, &c->d_val, TN));
+    TRY(dalloc(c, &c->d_logp, TN));
+    TRY(dalloc(c, &c->d_adv, TN));
+    TRY(dalloc(c, &c->d_ret, TN));
+    TRY(dalloc(c, &c->d_act, TN));
+    TRY(dalloc(c, &c->d_X, TN));
+    TRY(dalloc(c, &c->d_on, (size_t)2 * c->D + 1));
+    TRY(dalloc(c, &c->d_obs_part, (size_t)c->N * 2 * c->D));
+    TRY(dalloc(c, &c->d_rn_returns, (size_t)c->N * c->P));
+    TRY(dalloc(c, &c->d_rn_stats, 4));
+    TRY(dalloc(c, &c->d_scan_agg, (TN + 4095) / 4096 + 1));
+    TRY(dalloc(c, &c->d_last_v, (size_t)c->N));
+    c->eps_cap = c->N * 4 + 4096;
+    TRY(dalloc(c, &c->d_eps, (size_t)c->eps_cap));
+    TRY(dalloc(c, &c->d_ep_count, 1));
+    TRY(dalloc(c, &c->d_err, 1));
+    TRY(dalloc(c, &c->d_J, TN));
+    TRY(dalloc(c, &c->d_perm, TN));
+    TRY(dalloc(c, &c->d_R, TN));
+    TRY(dalloc(c, &c->d_R2, TN));
+    TRY(dalloc(c, &c->d_res, TN));
+    TRY(dalloc(c, &c->d_cnt, 2));
+    TRY(dalloc(c, &c->d_red, 4 * 1024 + 64));
+    TRY(dalloc(c, &c->d_mb_stats, 8));
+    BPPO_HIP(c, hipHostMalloc((void **)&c->h_cnt, 16, hipHostMallocDefault));
+    BPPO_HIP(c, hipHostMalloc((void **)&c->h_red, sizeof(double) * (4 * 1024 + 64), hipHostMallocDefault));
+    for (int i = 0; i < 8; i++) {
+        BPPO_HIP(c, hipEventCreate(&c->ev[i][0]));
+        BPPO_HIP(c, hipEventCreate(&c->ev[i][1]));
+    }
+    c->rng_key = seed_key(cfg->seed);
+    c->rng_pos = 0;
+    c->on_mean.assign(c->D, 0.0); c->on_m2.assign(c->D, 0.0); c->on_count = 0;
+    TRY(launch_cartpole_reset(c));
+    BPPO_HIP(c, hipStreamSynchronize(c->stream));
+    return BPPO_OK;
+}
+
+extern "C" bppo_status bppo_create(const bppo_config *cfg, int hip_device, void *hip_stream,
+                                   bppo_ctx **out) {
+    if (!cfg || !out) return BPPO_ERR_ARG;
+    bppo_ctx *c = new bppo_ctx();
+    bppo_status s = ctx_init(c, cfg, hip_device, hip_stream);
+    *out = c;   // returned even on failure so bppo_last_error can explain; caller destroys
+    return s;
+}
+
+extern "C" void bppo_destroy(bppo_ctx *c) {
+    if (!c) return;
+    c->shuf.join();
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    void *ptrs[] = {c->d_params, c->d_m1, c->d_m2, c->d_grad, c->d_slab, c->d_cp, c->d_steps,
+                    c->d_env_pos, c->d_ep_ret, c->d_ep_len, c->d_obs, c->d_rew, c->d_rew_raw,
+                    c->d_done, c->d_val, c->d_logp, c->d_adv, c->d_ret, c->d_act, c->d_X, c->d_on,
+                    c->d_obs_part, c->d_rn_returns, c->d_rn_stats, c->d_scan_agg, c->d_last_v,
+                    c->d_eps, c->d_ep_count, c->d_err, c->d_J, c->d_perm, c->d_R, c->d_R2,
+                    c->d_res, c->d_cnt, c->d_red, c->d_mb_stats};
+    for (void *p : ptrs) if (p) (void)hipFree(p);
+    if (c->h_cnt) (void)hipHostFree(c->h_cnt);
+    if (c->h_red) (void)hipHostFree(c->h_red);
+    for (int i = 0; i < 8; i++) {
+        if (c->ev[i][0]) (void)hipEventDestroy(c->ev[i][0]);
+        if (c->ev[i][1]) (void)hipEventDestroy(c->ev[i][1]);
+    }
+    if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+extern "C" size_t bppo_num_params(const bppo_ctx *c) { return c ? c->net.n_params : 0; }
+
+extern "C" bppo_status bppo_params_set(bppo_ctx *c, const float *h, size_t n) {
+    if (!c || !h || n != c->net.n_params) { if (c) c->err = "params_set: size mismatch"; return BPPO_ERR_ARG; }
+    BPPO_HIP(c, hipMemcpyAsync(c->d_params, h, n * 4, hipMemcpyHostToDevice, c->stream));
+    BPPO_HIP(c, hipStreamSynchronize(c->stream));
+    return BPPO_OK;
+}
+
+extern "C" bppo_status bppo_params_get(bppo_ctx *c, float *h, size_t n) {
+    if (!c || !h || n != c->net.n_params) { if (c) c->err = "params_get: size mismatch"; return BPPO_ERR_ARG; }
+    BPPO_HIP(c, hipMemcpyAsync(h, c->d_params, n * 4, hipMemcpyDeviceToHost, c->stream));
+    BPPO_HIP(c, hipStreamSynchronize(c->stream));
+    return BPPO_OK;
+}
+
+extern "C" bppo_status bppo_forward(bppo_ctx *c, const float *obs, const float *priv, int32_t B,
+                                    float *logits, float *values) {
+    (void)priv;
+    if (!c || !obs || B <= 0) return BPPO_ERR_ARG;
+    float *d_o = nullptr, *d_l = nullptr, *d_v = nullptr;
+    BPPO_HIP(c, hipMalloc((void **)&d_o, sizeof(float) * (size_t)B * c->D));
+    BPPO_HIP(c, hipMalloc((void **)&d_l, sizeof(float) * (size_t)B * c->A));
+    BPPO_HIP(c, hipMalloc((void **)&d_v, sizeof(float) * (size_t)B));
+    BPPO_HIP(c, hipMemcpyAsync(d_o, obs, sizeof(float) * (size_t)B * c->D, hipMemcpyHostToDevice, c->stream));
+    bppo_status s = launch_forward_rows(c, d_o, B, d_l, d_v);
+    if (s == BPPO_OK) {
+        if (logits) BPPO_HIP(c, hipMemcpyAsync(logits, d_l, sizeof(float) * (size_t)B * c->A, hipMemcpyDeviceToHost, c->stream));
+        if (values) BPPO_HIP(c, hipMemcpyAsync(values, d_v, sizeof(float) * (size_t)B, hipMemcpyDeviceToHost, c->stream));
+        BPPO_HIP(c, hipStreamSynchronize(c->stream));
+    }
+    (void)hipFree(d_o); (void)hipFree(d_l); (void)hipFree(d_v);
+    return s;
+}
+
+extern "C" bppo_status bppo_rng_get(bppo_ctx *c, uint64_t *p) {
+    if (!c || !p) return BPPO_ERR_ARG;
+    *p = c->rng_pos;
+    return BPPO_OK;
+}
+extern "C" bppo_status bppo_rng_set(bppo_ctx *c, uint64_t p) {
+    if (!c) return BPPO_ERR_ARG;
+    c->shuf.join();
+    c->shuffle_started = 0;
+    c->rng_pos = p;
+    return BPPO_OK;
+}
+
+extern "C" bppo_status bppo_vecenv_reset(bppo_ctx *c) {
+    if (!c) return BPPO_ERR_ARG;
+    TRY(launch_cartpole_reset(c));
+    BPPO_HIP(c, hipStreamSynchronize(c->stream));
+    return BPPO_OK;
+}
+
+extern "C" bppo_status bppo_vecenv_observe(bppo_ctx *c, float *obs, int32_t *players, uint8_t *masks,
+                                           float *priv) {
+    (void)priv; (void)masks;
+    if (!c) return BPPO_ERR_ARG;
+    if (obs) {
+        float *d = nullptr;
+        BPPO_HIP(c, hipMalloc((void **)&d, sizeof(float) * (size_t)c->N * c->D));
+        TRY(launch_cartpole_observe(c, d));
+        BPPO_HIP(c, hipMemcpyAsync(obs, d, sizeof(float) * (size_t)c->N * c->D, hipMemcpyDeviceToHost, c->stream));
+        BPPO_HIP(c, hipStreamSynchronize(c->stream));
+        (void)hipFree(d);
+    }
+    if (players) std::fill(players, players + c->N, 0);
+    return BPPO_OK;
+}
+
+extern "C" bppo_status bppo_vecenv_step(bppo_ctx *c, const int32_t *actions, float *obs, float *rewards,
+                                        uint8_t *dones, bppo_episode *eps, int32_t cap, int32_t *n_eps) {
+    if (!c || !actions) return BPPO_ERR_ARG;
+    const int N = c->N;
+    int32_t *d_a = nullptr; float *d_r = nullptr, *d_o = nullptr; uint8_t *d_d = nullptr;
+    BPPO_HIP(c, hipMalloc((void **)&d_a, sizeof(int32_t) * N));
+    BPPO_HIP(c, hipMalloc((void **)&d_r, sizeof(float) * N));
+    BPPO_HIP(c, hipMalloc((void **)&d_d, N));
+    BPPO_HIP(c, hipMalloc((void **)&d_o, sizeof(float) * (size_t)N * c->D));
+    BPPO_HIP(c, hipMemcpyAsync(d_a, actions, sizeof(int32_t) * N, hipMemcpyHostToDevice, c->stream));
+    BPPO_HIP(c, hipMemsetAsync(c->d_ep_count, 0, 4, c->stream));
+    TRY(launch_cartpole_vecenv_step(c, d_a, d_r, d_d, d_o));
+    if (rewards) BPPO_HIP(c, hipMemcpyAsync(rewards, d_r, sizeof(float) * N, hipMemcpyDeviceToHost, c->stream));
+    if (dones) BPPO_HIP(c, hipMemcpyAsync(dones, d_d, N, hipMemcpyDeviceToHost, c->stream));
+    if (obs) BPPO_HIP(c, hipMemcpyAsync(obs, d_o, sizeof(float) * (size_t)N * c->D, hipMemcpyDeviceToHost, c->stream));
+    int32_t cnt = 0;
+    BPPO_HIP(c, hipMemcpyAsync(&cnt, c->d_ep_count, 4, hipMemcpyDeviceToHost, c->stream));
+    BPPO_HIP(c, hipStreamSynchronize(c->stream));
+    if (n_eps) *n_eps = cnt;
+    if (eps && cap > 0 && cnt > 0) {
+        std::vector<EpisodeRec> recs(std::min(cnt, c->eps_cap));
+        BPPO_HIP(c, hipMemcpy(recs.data(), c->d_eps, sizeof(EpisodeRec) * recs.size(), hipMemcpyDeviceToHost));
+        std::sort(recs.begin(), recs.end(), [](const EpisodeRec &a, const EpisodeRec &b) {
+            return a.env_index < b.env_index; });
+        for (int i = 0; i < (int)recs.size() && i < cap; i++) {
+            std::memcpy(eps[i].total_reward, recs[i].total_reward, sizeof(float) * 4);
+            eps[i].length = recs[i].length; eps[i].env_index = recs[i].env_index;
+            eps[i].step = recs[i].step; eps[i].pad = 0;
+        }
+    }
+    c->global_step += N;
+    (void)hipFree(d_a); (void)hipFree(d_r); (void)hipFree(d_d); (void)hipFree(d_o);
+    return BPPO_OK;
+}
+
+extern "C" bppo_status bppo_vecenv_set_step(bppo_ctx *c, uint64_t s) {
+    if (!c) return BPPO_ERR_ARG;
+    c->global_step = s;
+    return BPPO_OK;
+}
+
+extern "C" bppo_status bppo_obs_norm_get(bppo_ctx *c, double *mean, double *m2, double *count) {
+    if (!c) return BPPO_ERR_ARG;
+    std::vector<double> h(2 * c->D + 1);
+    BPPO_HIP(c, hipMemcpyAsync(h.data(), c->d_on, sizeof(double) * h.size(), hipMemcpyDeviceToHost, c->stream));
+    BPPO_HIP(c, hipStreamSynchronize(c->stream));
+    if (mean) std::memcpy(mean, h.data(), sizeof(double) * c->D);
+    if (m2) std::memcpy(m2, h.data() + c->D, sizeof(double) * c->D);
+    if (count) *count = h[2 * c->D];
+    return BPPO_OK;
+}
+
+extern "C" bppo_status bppo_obs_norm_set(bppo_ctx *c, const double *mean, const double *m2, double count) {
+    if (!c || !mean || !m2) return BPPO_ERR_ARG;
+    std::vector<double> h(2 * c->D + 1);
+    std::memcpy(h.data(), mean, sizeof(double) * c->D);
+    std::memcpy(h.data() + c->D, m2, sizeof(double) * c->D);
+    h[2 * c->D] = count;
+    BPPO_HIP(c, hipMemcpyAsync(c->d_on, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice, c->stream));
+    BPPO_HIP(c, hipStreamSynchronize(c->stream));
+    return BPPO_OK;
+}
+
+extern "C" bppo_status bppo_ret_norm_get(bppo_ctx *c, double *mvc, double *returns) {
+    if (!c) return BPPO_ERR_ARG;
+    if (mvc) BPPO_HIP(c, hipMemcpyAsync(mvc, c->d_rn_stats, sizeof(double) * 3, hipMemcpyDeviceToHost, c->stream));
+    if (returns) BPPO_HIP(c, hipMemcpyAsync(returns, c->d_rn_returns, sizeof(double) * (size_t)c->N * c->P, hipMemcpyDeviceToHost, c->stream));
+    BPPO_HIP(c, hipStreamSynchronize(c->stream));
+    return BPPO_OK;
+}
+
+extern "C" bppo_status bppo_ret_norm_set(bppo_ctx *c, const double *mvc, const double *returns) {
+    if (!c) return BPPO_ERR_ARG;
+    if (mvc) BPPO_HIP(c, hipMemcpyAsync(c->d_rn_stats, mvc, sizeof(double) * 3, hipMemcpyHostToDevice, c->stream));
+    if (returns) BPPO_HIP(c, hipMemcpyAsync(c->d_rn_returns, returns, sizeof(double) * (size_t)c->N * c->P, hipMemcpyHostToDevice, c->stream));
+    BPPO_HIP(c, hipStreamSynchronize(c->stream));
+    return BPPO_OK;
+}
+
+static void tm_begin(bppo_ctx *c, int slot) { (void)hipEventRecord(c->ev[slot][0], c->stream); }
+static void tm_end(bppo_ctx *c, int slot) { (void)hipEventRecord(c->ev[slot][1], c->stream); }
+static void tm_read(bppo_ctx *c, int slot) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, c->ev[slot][0], c->ev[slot][1]) == hipSuccess) c->last_ms[slot] = ms;
+}
+
+// collect_rollouts (ppo.rs:213-500)
+extern "C" bppo_status bppo_collect_rollouts(bppo_ctx *c, bppo_rollout_info *info) {
+    if (!c) return BPPO_ERR_ARG;
+    c->shuf.join();
+    const size_t TN = (size_t)c->T * c->N;
+    BPPO_HIP(c, hipMemsetAsync(c->d_ep_count, 0, 4, c->stream));
+    BPPO_HIP(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
+    const uint64_t base = c->rng_pos;
+    tm_begin(c, TM_ROLLOUT);
+    TRY(launch_cartpole_rollout(c, base, nullptr, nullptr, c->cfg.normalize_obs));
+    tm_end(c, TM_ROLLOUT);
+    c->rng_pos = base + TN * (uint64_t)c->A;   // one word per (env, action) per step
+    // shuffle chain for the coming update starts now (overlaps the GPU work)
+    c->shuf.start(c->rng_key, c->cfg.rng_stream, c->rng_pos, (uint32_t)TN, c->cfg.num_epochs);
+    c->shuffle_started = 1;
+    if (c->cfg.normalize_obs) TRY(launch_obs_norm_merge(c));       // ppo.rs:495-497
+    tm_begin(c, TM_RETNORM);
+    if (c->cfg.normalize_returns) TRY(launch_return_norm(c));      // ppo.rs:390-408
+    else BPPO_HIP(c, hipMemcpyAsync(c->d_rew, c->d_rew_raw, TN * 4, hipMemcpyDeviceToDevice, c->stream));
+    tm_end(c, TM_RETNORM);
+    int32_t hv[2] = {0, 0};
+    BPPO_HIP(c, hipMemcpyAsync(&hv[0], c->d_ep_count, 4, hipMemcpyDeviceToHost, c->stream));
+    BPPO_HIP(c, hipMemcpyAsync(&hv[1], c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
+    BPPO_HIP(c, hipStreamSynchronize(c->stream));
+    tm_read(c, TM_ROLLOUT); tm_read(c, TM_RETNORM);
+    c->collected = 1; c->gae_done = 0;
+    c->global_step += TN;
+    if (hv[1]) { c->err = "NaN/Inf in log probs — model producing corrupt logits"; return BPPO_ERR_NONFINITE; }
+    if (info) {
+        info->episodes = hv[0];
+        info->rng_word_pos = c->rng_pos;
+        info->mean_return = 0; info->mean_length = 0;
+        int n = std::min(hv[0], c->eps_cap);
+        if (n > 0) {
+            std::vector<EpisodeRec> recs(n);
+            BPPO_HIP(c, hipMemcpy(recs.data(), c->d_eps, sizeof(EpisodeRec) * n, hipMemcpyDeviceToHost));
+            double sr = 0, sl = 0;
+            for (auto &r : recs) { sr += r.total_reward[0]; sl += r.length; }
+            info->mean_return = (float)(sr / n); info->mean_length = (float)(sl / n);
+        }
+    }
+    return BPPO_OK;
+}
+
+extern "C" bppo_status bppo_rollout_episodes(bppo_ctx *c, bppo_episode *eps, int32_t cap, int32_t *n) {
+    if (!c) return BPPO_ERR_ARG;
+    int32_t cnt = 0;
+    BPPO_HIP(c, hipMemcpy(&cnt, c->d_ep_count, 4, hipMemcpyDeviceToHost));
+    int m = std::min(cnt, c->eps_cap);
+    std::vector<EpisodeRec> recs(m);
+    if (m) BPPO_HIP(c, hipMemcpy(recs.data(), c->d_eps, sizeof(EpisodeRec) * m, hipMemcpyDeviceToHost));
+    // reference order: by step, then env index (env.rs:470-483 collects in env order per step)
+    std::sort(recs.begin(), recs.end(), [](const EpisodeRec &a, const EpisodeRec &b) {
+        return a.step != b.step ? a.step < b.step : a.env_index < b.env_index; });
+    for (int i = 0; i < m && i < cap; i++) {
+        std::memcpy(eps[i].total_reward, recs[i].total_reward, sizeof(float) * 4);
+        eps[i].length = recs[i].length; eps[i].env_index = recs[i].env_index;
+        eps[i].step = recs[i].step; eps[i].pad = 0;
+    }
+    if (n) *n = cnt;
+    return BPPO_OK;
+}
+
+// bootstrap + GAE (main.rs:877-947)
+extern "C" bppo_status bppo_compute_gae(bppo_ctx *c) {
+    if (!c || !c->collected) { if (c) c->err = "compute_gae before collect_rollouts"; return BPPO_ERR_ARG; }
+    tm_begin(c, TM_BOOT);
+    TRY(launch_bootstrap(c, nullptr, nullptr, c->cfg.normalize_obs));
+    tm_end(c, TM_BOOT);
+    tm_begin(c, TM_GAE);
+    bppo_status s = launch_gae_1p(c->d_rew, c->d_done, c->d_val, c->d_last_v, c->T, c->N,
+                                  (float)c->cfg.gamma, (float)c->cfg.gae_lambda, c->d_adv, c->d_ret,
+                                  c->stream);
+    tm_end(c, TM_GAE);
+    if (s != BPPO_OK) { c->err = "gae launch failed"; return s; }
+    BPPO_HIP(c, hipStreamSynchronize(c->stream));
+    tm_read(c, TM_BOOT); tm_read(c, TM_GAE);
+    c->gae_done = 1;
+    return BPPO_OK;
+}
+
+// ppo_update (ppo.rs:1661-2112)
+extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, bppo_update_metrics *m) {
+    if (!c || !c->gae_done) { if (c) c->err = "ppo_update before compute_gae"; return BPPO_ERR_ARG; }
+    if (!c->shuffle_started) {
+        const size_t TN0 = (size_t)c->T * c->N;
+        c->shuf.start(c->rng_key, c->cfg.rng_stream, c->rng_pos, (uint32_t)TN0, c->cfg.num_epochs);
+        c->shuffle_started = 1;
+    }
+    const size_t B = (size_t)c->T * c->N;
+    const int M = c->cfg.num_minibatches;
+    const size_t base_mb = B / M, rem = B % M;
+    const int np = (int)c->net.n_params;
+    const int NM = 11;
+    std::vector<float> rows;          // per minibatch: NM metric sums + 4 adv stats
+    int epochs_run = 0;
+    bool stop = false;
+    tm_begin(c, TM_UPDATE);
+    float fw_ms = 0, sh_ms = 0;
+    for (int ep = 0; ep < c->cfg.num_epochs && !stop; ep++) {
+        epochs_run++;
+        c->shuf.wait_epoch(ep);
+        hipEvent_t s0 = c->ev[TM_SHUFFLE][0], s1 = c->ev[TM_SHUFFLE][1];
+        (void)hipEventRecord(s0, c->stream);
+        TRY(launch_shuffle_apply(c, c->shuf.J + (size_t)ep * B, (uint32_t)B));
+        (void)hipEventRecord(s1, c->stream);
+        size_t start = 0;
+        for (int mb = 0; mb < M; mb++) {
+            const size_t sz = base_mb + ((size_t)mb < rem ? 1 : 0);
+            if (sz == 0) continue;
+            (void)hipEventRecord(c->ev[TM_FWDBWD][0], c->stream);
+            TRY(launch_minibatch(c, (uint32_t)start, (uint32_t)sz, (float)ent_coef, nullptr));
+            (void)hipEventRecord(c->ev[TM_FWDBWD][1], c->stream);
+            if (c->allreduce && c->world > 1) {
+                BPPO_HIP(c, hipStreamSynchronize(c->stream));
+                if (c->allreduce(c->d_grad, (size_t)np + NM, c->allreduce_user) != 0) {
+                    c->err = "all-reduce callback failed";
+                    return BPPO_ERR_COMM;
+                }
+            }
+            float c1[64], c2[64];
+            for (int t = 0; t < 2 * c->net.n_layers; t++) {
+                int ti = ++c->adam_t[t];
+                c1[t] = 1.0f - powi_f32(0.9f, ti);
+                c2[t] = 1.0f - powi_f32(0.999f, ti);
+            }
+            TRY(launch_adam(c, (float)lr, c1, c2));
+            // metric row: grad[np .. np+NM) and adv stats
+            std::vector<float> row(NM + 4);
+            BPPO_HIP(c, hipMemcpyAsync(row.data(), c->d_grad + np, sizeof(float) * NM, hipMemcpyDeviceToHost, c->stream));
+            BPPO_HIP(c, hipMemcpyAsync(row.data() + NM, c->d_mb_stats, sizeof(float) * 4, hipMemcpyDeviceToHost, c->stream));
+            BPPO_HIP(c, hipStreamSynchronize(c->stream));
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, c->ev[TM_FWDBWD][0], c->ev[TM_FWDBWD][1]) == hipSuccess) fw_ms = ms;
+            if (mb == 0 && hipEventElapsedTime(&ms, s0, s1) == hipSuccess) sh_ms = ms;
+            rows.insert(rows.end(), row.begin(), row.end());
+            if (c->cfg.target_kl >= 0) {
+                const float n = row[10] > 0 ? row[10] : 1.0f;
+                if (row[3] / n > (float)c->cfg.target_kl) { stop = true; break; }   // ppo.rs:2019-2023
+            }
+            start += sz;
+        }
+    }
+    tm_end(c, TM_UPDATE);
+    c->rng_pos = c->shuf.end_pos[epochs_run - 1];   // only started epochs consumed words
+    double ev4[4];
+    TRY(launch_explained_variance(c, ev4));
+    tm_read(c, TM_UPDATE);
+    c->last_ms[TM_FWDBWD] = fw_ms;
+    c->last_ms[TM_SHUFFLE] = sh_ms;
+    c->shuf.join();
+    c->shuffle_started = 0;
+    if (m) {
+        std::memset(m, 0, sizeof *m);
+        const int nup = (int)(rows.size() / (NM + 4));
+        float tp = 0, tv = 0, th = 0, tk = 0, tc = 0, tl = 0, tvm = 0, trm = 0, tam = 0, tas = 0;
+        float tamin = INFINITY, tamax = -INFINITY, tvem = 0, tves = 0, tvemax = -INFINITY;
+        for (int u = 0; u < nup; u++) {
+            const float *r = &rows[(size_t)u * (NM + 4)];
+            const float n = r[10] > 0 ? r[10] : 1.0f;
+            const float pl = r[0] / n, vl = 0.5f * (r[1] / n), h = r[2] / n;
+            tp += pl; tv += vl; th += h; tk += r[3] / n; tc += r[4] / n;
+            tl += pl + vl * (float)c->cfg.value_coef + (-h) * (float)ent_coef;
+            tvm += r[5] / n; trm += r[6] / n;
+            const float vem = r[7] / n;
+            tvem += vem;
+            const double var = n > 1 ? ((double)r[8] - (double)n * vem * vem) / (double)(n - 1) : 0.0;
+            tves += sqrtf((float)std::max(var, 0.0));
+            tvemax = std::max(tvemax, r[9]);
+            tam += r[NM]; tas += r[NM + 1];
+            tamin = std::min(tamin, r[NM + 2]); tamax = std::max(tamax, r[NM + 3]);
+        }
+        const float n = (float)std::max(nup, 1);
+        m->policy_loss = tp / n; m->value_loss = tv / n; m->entropy = th / n;
+        m->entropy_scaled = m->entropy / logf((float)c->A);
+        m->approx_kl = tk / n; m->clip_fraction = tc / n; m->total_loss = tl / n;
+        m->value_mean = tvm / n; m->returns_mean = trm / n;
+        m->adv_mean_raw = tam / n; m->adv_std_raw = tas / n; m->adv_min_raw = tamin; m->adv_max_raw = tamax;
+        m->value_error_mean = tvem / n; m->value_error_std = tves / n; m->value_error_max = tvemax;
+        const double Bn = (double)B;
+        const double mr = ev4[0] / Bn, vr = ev4[1] / Bn - mr * mr;
+        const double mres = ev4[2] / Bn, vres = ev4[3] / Bn - mres * mres;
+        m->explained_variance = vr < 1e-8 ? 0.0f : (float)(1.0 - vres / vr);
+        m->num_updates = nup; m->epochs_run = epochs_run;
+    }
+    c->collected = 0; c->gae_done = 0;
+    return BPPO_OK;
+}
+
+extern "C" bppo_status bppo_set_allreduce(bppo_ctx *c, bppo_allreduce_fn fn, void *user, int32_t world) {
+    if (!c || world < 1) return BPPO_ERR_ARG;
+    c->allreduce = fn; c->allreduce_user = user; c->world = world;
+    return BPPO_OK;
+}
+
+struct BufDesc { void *ptr; size_t bytes; };
+static BufDesc find_buf(bppo_ctx *c, const char *name) {
+    const size_t TN = (size_t)c->T * c->N;
+    if (!strcmp(name, "obs")) return {c->d_obs, TN * c->D * 4};
+    if (!strcmp(name, "actions")) return {c->d_act, TN * 4};
+    if (!strcmp(name, "rewards")) return {c->d_rew, TN * 4};
+    if (!strcmp(name, "raw_rewards")) return {c->d_rew_raw, TN * 4};
+    if (!strcmp(name, "dones")) return {c->d_done, TN * 4};
+    if (!strcmp(name, "values")) return {c->d_val, TN * 4};
+    if (!strcmp(name, "log_probs")) return {c->d_logp, TN * 4};
+    if (!strcmp(name, "advantages")) return {c->d_adv, TN * 4};
+    if (!strcmp(name, "returns")) return {c->d_ret, TN * 4};
+    if (!strcmp(name, "all_rewards")) return {c->d_rew, TN * 4};
+    if (!strcmp(name, "perm")) return {c->d_perm, TN * 4};
+    if (!strcmp(name, "last_values")) return {c->d_last_v, (size_t)c->N * 4};
+    if (!strcmp(name, "grad")) return {c->d_grad, c->net.n_params * 4};
+    return {nullptr, 0};
+}
+
+extern "C" bppo_status bppo_buffer_get(bppo_ctx *c, const char *name, void *host, size_t bytes) {
+    if (!c || !name || !host) return BPPO_ERR_ARG;
+    BufDesc b = find_buf(c, name);
+    if (!b.ptr || bytes < b.bytes) { c->err = std::string("buffer_get: unknown buffer or too small: ") + name; return BPPO_ERR_ARG; }
+    BPPO_HIP(c, hipMemcpyAsync(host, b.ptr, b.bytes, hipMemcpyDeviceToHost, c->stream));
+    BPPO_HIP(c, hipStreamSynchronize(c->stream));
+    return BPPO_OK;
+}
+
+extern "C" bppo_status bppo_buffer_set(bppo_ctx *c, const char *name, const void *host, size_t bytes) {
+    if (!c || !name || !host) return BPPO_ERR_ARG;
+    BufDesc b = find_buf(c, name);
+    if (!b.ptr || bytes != b.bytes) { c->err = std::string("buffer_set: unknown buffer or size mismatch: ") + name; return BPPO_ERR_ARG; }
+    BPPO_HIP(c, hipMemcpyAsync(b.ptr, host, b.bytes, hipMemcpyHostToDevice, c->stream));
+    BPPO_HIP(c, hipStreamSynchronize(c->stream));
+    if (!strcmp(name, "advantages") || !strcmp(name, "returns")) c->gae_done = c->collected = 1;
+    return BPPO_OK;
+}
+
+extern "C" bppo_status bppo_gae_device(const float *r, const float *d, const float *v, const float *lv,
+                                       int32_t T, int32_t N, float gamma, float lambda, float *adv,
+                                       float *ret, void *stream) {
+    if (!r || !d || !v || !lv || !adv || !ret || T < 0 || N < 0) return BPPO_ERR_ARG;
+    return launch_gae_1p(r, d, v, lv, T, N, gamma, lambda, adv, ret, (hipStream_t)stream);
+}
+
+extern "C" bppo_status bppo_gae_mp_device(const float *ar, const int32_t *pl, const float *d,
+                                          const float *v, const float *lvpp, int32_t T, int32_t N,
+                                          int32_t P, float gamma, float lambda, float *adv, float *ret,
+                                          void *stream) {
+    if (!ar || !pl || !d || !v || !lvpp || !adv || !ret || T < 0 || N < 0 || P < 1 || P > 4)
+        return BPPO_ERR_ARG;
+    return launch_gae_mp(ar, pl, d, v, lvpp, T, N, P, gamma, lambda, adv, ret, (hipStream_t)stream);
+}
+
+extern "C" bppo_status bppo_last_kernel_ms(bppo_ctx *c, const char *k, float *ms) {
+    if (!c || !k || !ms) return BPPO_ERR_ARG;
+    static const char *names[8] = {"rollout", "gae", "update", "minibatch", "return_norm", "shuffle",
+                                   "adam", "bootstrap"};
+    for (int i = 0; i < 8; i++)
+        if (!strcmp(k, names[i])) { *ms = c->last_ms[i]; return BPPO_OK; }
+    return BPPO_ERR_ARG;
+}
+
+extern "C" bppo_status bppo_debug_libm(int32_t which, int32_t device, const float *x, float *y, size_t n) {
+    if (!x || !y) return BPPO_ERR_ARG;
+    if (!device) {
+        for (size_t i = 0; i < n; i++) {
+            float v = x[i];
+            switch (which) {
+            case 0: y[i] = bppo_math::logf_glibc(v); break;
+            case 1: y[i] = bppo_math::sinf_glibc(v); break;
+            case 2: y[i] = bppo_math::cosf_glibc(v); break;
+            case 3: y[i] = -bppo_math::logf_glibc(-bppo_math::logf_glibc(v)); break;
+            default: y[i] = bppo_math::expf_glibc(v); break;
+            }
+        }
+        return BPPO_OK;
+    }
+    float *dx = nullptr, *dy = nullptr;
+    if (hipMalloc((void **)&dx, n * 4) != hipSuccess || hipMalloc((void **)&dy, n * 4) != hipSuccess) return BPPO_ERR_HIP;
+    bppo_status s = BPPO_ERR_HIP;
+    if (hipMemcpy(dx, x, n * 4, hipMemcpyHostToDevice) == hipSuccess &&
+        launch_libm(which, dx, dy, n) == BPPO_OK && hipDeviceSynchronize() == hipSuccess &&
+        hipMemcpy(y, dy, n * 4, hipMemcpyDeviceToHost) == hipSuccess)
+        s = BPPO_OK;
+    (void)hipFree(dx); (void)hipFree(dy);
+    return s;
+}

@@ -1,0 +1,179 @@
+// bppo_internal.h — context layout and kernel launchers shared by the HIP
+// translation units of libbppo.so.  Not part of the public C-ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+#include <string>
+#include <vector>
+#include <thread>
+#include <mutex>
+#include <condition_variable>
+#include "../../include/bppo.h"
+#include "bppo_device.h"
+
+namespace bppo {
+
+// ---------------------------------------------------------------- layout ----
+struct NetLayout {
+    int n_layers = 0;             // linear layers in record order
+    int in[16], out[16];
+    size_t w[16], b[16];
+    int n_actor_hidden = 0;       // hidden layers of the actor / shared backbone
+    int policy = 0, value = 0;    // layer indices of the heads
+    int critic_first = -1;        // CTDE critic hidden layers [critic_first, value)
+    int ctde = 0, relu = 1;
+    size_t n_params = 0;
+};
+NetLayout make_layout(const bppo_config &c, int obs_dim, int priv_dim, int act_dim);
+
+// episode record written by the rollout kernel
+struct EpisodeRec {
+    float total_reward[4];
+    int32_t length, env_index, step, pad;
+};
+
+// Welford state (count, mean, M2) — Chan merge is the associative combine
+struct Welford { double n, mean, m2; };
+
+// -------------------------------------------------------------- shuffle -----
+// rand 0.8.5 SliceRandom::shuffle draws: host thread walks the ChaCha12 word
+// stream with the UniformInt<u32> zone test (inherently sequential: every draw
+// may reject) and produces the swap targets J[i] for i = n-1 .. 1; the GPU
+// applies the swaps (deterministic reservations, bit-identical to sequential
+// Fisher-Yates).  Runs concurrently with the rollout.
+struct ShuffleEngine {
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    Key8 key{};
+    uint64_t stream = 0;
+    uint64_t start_pos = 0;
+    uint32_t n = 0;
+    int epochs = 0;
+    int ready = 0;                      // epochs whose J is complete
+    bool running = false;
+    std::vector<uint64_t> end_pos;      // word position after each epoch's shuffle
+    uint32_t *J = nullptr;              // pinned host [epochs][n]
+    size_t J_cap = 0;
+    void start(const Key8 &k, uint64_t strm, uint64_t pos, uint32_t n_, int epochs_);
+    void wait_epoch(int e);
+    void join();
+    ~ShuffleEngine();
+};
+
+struct Timers {
+    hipEvent_t a = nullptr, b = nullptr;
+};
+
+}  // namespace bppo
+
+struct bppo_ctx {
+    bppo_config cfg;
+    int dev = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    std::string err;
+    int N = 0, T = 0, D = 0, A = 0, P = 1, G = 0;
+    bppo::NetLayout net;
+    // parameters + Adam
+    float *d_params = nullptr, *d_m1 = nullptr, *d_m2 = nullptr;
+    std::vector<int32_t> adam_t;
+    float *d_grad = nullptr;          // [n_params + metric slots]
+    double *d_grad64 = nullptr;
+    float *d_slab = nullptr;          // per-wave partial gradients
+    size_t slab_rows = 0;
+    // env state (CartPole SoA)
+    float *d_cp = nullptr;            // x, x_dot, theta, theta_dot  [4][N]
+    int32_t *d_steps = nullptr;
+    uint64_t *d_env_pos = nullptr;
+    float *d_ep_ret = nullptr;        // [N*P]
+    int32_t *d_ep_len = nullptr;
+    uint64_t global_step = 0;
+    // rollout buffer [T][N][...]
+    float *d_obs = nullptr, *d_rew = nullptr, *d_rew_raw = nullptr, *d_done = nullptr;
+    float *d_val = nullptr, *d_logp = nullptr, *d_adv = nullptr, *d_ret = nullptr;
+    int32_t *d_act = nullptr;
+    double *d_X = nullptr;            // rolling returns per (t,e) for the return-normalizer scan
+    // normalizers
+    double *d_on = nullptr;           // [3][D]: mean, M2, (count in slot) ; host mirror below
+    std::vector<double> on_mean, on_m2;
+    double on_count = 0;
+    double *d_obs_part = nullptr;     // per-env Welford partials [N][2*D]
+    double *d_rn_returns = nullptr;   // [N*P]
+    double *d_rn_stats = nullptr;     // {mean, M2, count}
+    bppo::Welford *d_scan_agg = nullptr;
+    // bootstrap
+    float *d_last_v = nullptr;
+    // episodes
+    bppo::EpisodeRec *d_eps = nullptr;
+    int32_t *d_ep_count = nullptr;
+    int32_t eps_cap = 0;
+    int32_t *d_err = nullptr;
+    // main RNG
+    bppo::Key8 rng_key{};
+    uint64_t rng_pos = 0;
+    // shuffle
+    bppo::ShuffleEngine shuf;
+    uint32_t *d_J = nullptr, *d_perm = nullptr, *d_R = nullptr, *d_R2 = nullptr;
+    int32_t *d_res = nullptr;
+    uint32_t *d_cnt = nullptr;        // [2] round counters
+    uint32_t *h_cnt = nullptr;        // pinned
+    int shuffle_started = 0;
+    // scratch
+    double *d_red = nullptr;          // reduction scratch
+    double *h_red = nullptr;          // pinned mirror
+    float *d_mb_stats = nullptr;      // [mean, inv_std...] per minibatch
+    // all-reduce hook
+    bppo_allreduce_fn allreduce = nullptr;
+    void *allreduce_user = nullptr;
+    int world = 1;
+    // timing
+    hipEvent_t ev[8][2];
+    float last_ms[8] = {0};
+    int collected = 0, gae_done = 0;
+};
+
+namespace bppo {
+// kernel-phase timer slots
+enum { TM_ROLLOUT = 0, TM_GAE = 1, TM_UPDATE = 2, TM_FWDBWD = 3, TM_RETNORM = 4, TM_SHUFFLE = 5,
+       TM_ADAM = 6, TM_BOOT = 7 };
+
+// launchers (k_rollout.hip)
+bppo_status launch_cartpole_reset(bppo_ctx *c);
+bppo_status launch_cartpole_rollout(bppo_ctx *c, uint64_t base_pos, const double *mean,
+                                    const double *sd, int norm_on);
+bppo_status launch_cartpole_vecenv_step(bppo_ctx *c, const int32_t *d_actions, float *d_rew,
+                                        uint8_t *d_done, float *d_obs_out);
+bppo_status launch_cartpole_observe(bppo_ctx *c, float *d_obs_out);
+bppo_status launch_obs_norm_merge(bppo_ctx *c);
+bppo_status launch_bootstrap(bppo_ctx *c, const double *mean, const double *sd, int norm_on);
+bppo_status launch_forward_rows(bppo_ctx *c, const float *d_obs, int B, float *d_logits,
+                                float *d_values);
+// (k_gae.hip)
+bppo_status launch_gae_1p(const float *r, const float *d, const float *v, const float *lv, int T,
+                          int N, float gamma, float lambda, float *adv, float *ret, hipStream_t s);
+bppo_status launch_gae_mp(const float *ar, const int32_t *pl, const float *d, const float *v,
+                          const float *lvpp, int T, int N, int P, float gamma, float lambda,
+                          float *adv, float *ret, hipStream_t s);
+bppo_status launch_return_norm(bppo_ctx *c);
+// (k_update.hip)
+bppo_status launch_shuffle_apply(bppo_ctx *c, const uint32_t *h_J, uint32_t n);
+bppo_status launch_minibatch(bppo_ctx *c, uint32_t mb_start, uint32_t mb_size, float ent_coef,
+                             double *h_stats_out);
+bppo_status launch_adam(bppo_ctx *c, float lr, const float *c1, const float *c2);
+bppo_status launch_explained_variance(bppo_ctx *c, double *out6);
+// libm device check
+bppo_status launch_libm(int which, const float *d_x, float *d_y, size_t n);
+
+inline bppo_status hip_fail(bppo_ctx *c, hipError_t e, const char *what) {
+    if (c) c->err = std::string(what) + ": " + hipGetErrorString(e);
+    return BPPO_ERR_HIP;
+}
+}  // namespace bppo
+
+#define BPPO_HIP(c, expr)                                                   \
+    do {                                                                    \
+        hipError_t _e = (expr);                                             \
+        if (_e != hipSuccess) return bppo::hip_fail((c), _e, #expr);        \
+    } while (0)

@@ -31,20 +31,42 @@ namespace bppo_math {
 BPPO_HD uint32_t asuint(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
 BPPO_HD float asfloat(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
 
-// ------------------------------------------------------------------ logf ----
-BPPO_HD float logf_glibc(float x) {
-    // __logf_data (LOGF_TABLE_BITS = 4): {invc, logc}
-    const double T_invc[16] = {
+// Constant tables: namespace-scope so runtime-indexed reads stay in constant
+// memory on the device (function-local arrays would be copied to scratch).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define BPPO_TABLE static __constant__ const
+#else
+#define BPPO_TABLE static const
+#endif
+BPPO_TABLE double kLogfInvc[16] = {
         0x1.661ec79f8f3bep+0, 0x1.571ed4aaf883dp+0, 0x1.49539f0f010bp+0,  0x1.3c995b0b80385p+0,
         0x1.30d190c8864a5p+0, 0x1.25e227b0b8eap+0,  0x1.1bb4a4a1a343fp+0, 0x1.12358f08ae5bap+0,
         0x1.0953f419900a7p+0, 0x1.0p+0,             0x1.e608cfd9a47acp-1, 0x1.ca4b31f026aap-1,
         0x1.b2036576afce6p-1, 0x1.9c2d163a1aa2dp-1, 0x1.886e6037841edp-1, 0x1.767dcf5534862p-1};
-    const double T_logc[16] = {
+BPPO_TABLE double kLogfLogc[16] = {
         -0x1.57bf7808caadep-2, -0x1.2bef0a7c06ddbp-2, -0x1.01eae7f513a67p-2, -0x1.b31d8a68224e9p-3,
         -0x1.6574f0ac07758p-3, -0x1.1aa2bc79c81p-3,   -0x1.a4e76ce8c0e5ep-4, -0x1.1973c5a611cccp-4,
         -0x1.252f438e10c1ep-5, 0x0.0p+0,              0x1.aa5aa5df25984p-5,  0x1.c5e53aa362eb4p-4,
         0x1.526e57720db08p-3,  0x1.bc2860d22477p-3,   0x1.1058bc8a07ee1p-2,  0x1.4043057b6ee09p-2};
-    const double Ln2 = 0x1.62e42fefa39efp-1;
+BPPO_TABLE uint32_t kInvPio4[24] = {
+        0xa2u,       0xa2f9u,     0xa2f983u,   0xa2f9836eu, 0xf9836e4eu, 0x836e4e44u,
+        0x6e4e4415u, 0x4e441529u, 0x441529fcu, 0x1529fc27u, 0x29fc2757u, 0xfc2757d1u,
+        0x2757d1f5u, 0x57d1f534u, 0xd1f534ddu, 0xf534ddc0u, 0x34ddc0dbu, 0xddc0db62u,
+        0xc0db6295u, 0xdb629599u, 0x6295993cu, 0x95993c43u, 0x993c4390u, 0x3c439041u};
+BPPO_TABLE uint64_t kExp2fTab[32] = {
+        0x3ff0000000000000ULL, 0x3fefd9b0d3158574ULL, 0x3fefb5586cf9890fULL, 0x3fef9301d0125b51ULL,
+        0x3fef72b83c7d517bULL, 0x3fef54873168b9aaULL, 0x3fef387a6e756238ULL, 0x3fef1e9df51fdee1ULL,
+        0x3fef06fe0a31b715ULL, 0x3feef1a7373aa9cbULL, 0x3feedea64c123422ULL, 0x3feece086061892dULL,
+        0x3feebfdad5362a27ULL, 0x3feeb42b569d4f82ULL, 0x3feeab07dd485429ULL, 0x3feea47eb03a5585ULL,
+        0x3feea09e667f3bcdULL, 0x3fee9f75e8ec5f74ULL, 0x3feea11473eb0187ULL, 0x3feea589994cce13ULL,
+        0x3feeace5422aa0dbULL, 0x3feeb737b0cdc5e5ULL, 0x3feec49182a3f090ULL, 0x3feed503b23e255dULL,
+        0x3feee89f995ad3adULL, 0x3feeff76f2fb5e47ULL, 0x3fef199bdd85529cULL, 0x3fef3720dcef9069ULL,
+        0x3fef5818dcfba487ULL, 0x3fef7c97337b9b5fULL, 0x3fefa4afa2a490daULL, 0x3fefd0765b6e4540ULL};
+
+// ------------------------------------------------------------------ logf ----
+BPPO_HD float logf_glibc(float x) {
+    // __logf_data (LOGF_TABLE_BITS = 4): {invc, logc}
+            const double Ln2 = 0x1.62e42fefa39efp-1;
     const double A0 = -0x1.00ea348b88334p-2, A1 = 0x1.5575b0be00b6ap-2,
                  A2 = -0x1.ffffef20a4123p-2;
     uint32_t ix = asuint(x);
@@ -60,7 +82,7 @@ BPPO_HD float logf_glibc(float x) {
     int i = (int)((tmp >> (23 - 4)) % 16);
     int k = (int32_t)tmp >> 23;
     uint32_t iz = ix - (tmp & (0x1ffu << 23));
-    double invc = T_invc[i], logc = T_logc[i];
+    double invc = kLogfInvc[i], logc = kLogfLogc[i];
     double z = (double)asfloat(iz);
     double r = fma(z, invc, -1.0);
     double y0 = fma((double)k, Ln2, logc);
@@ -114,13 +136,8 @@ BPPO_HD double reduce_fast(double x, const sincos_t &p, int *np) {
 
 BPPO_HD double reduce_large(uint32_t xi, int *np) {
     // __inv_pio4: bits of 4/pi, each entry the previous shifted by 8 bits
-    const uint32_t inv_pio4[24] = {
-        0xa2u,       0xa2f9u,     0xa2f983u,   0xa2f9836eu, 0xf9836e4eu, 0x836e4e44u,
-        0x6e4e4415u, 0x4e441529u, 0x441529fcu, 0x1529fc27u, 0x29fc2757u, 0xfc2757d1u,
-        0x2757d1f5u, 0x57d1f534u, 0xd1f534ddu, 0xf534ddc0u, 0x34ddc0dbu, 0xddc0db62u,
-        0xc0db6295u, 0xdb629599u, 0x6295993cu, 0x95993c43u, 0x993c4390u, 0x3c439041u};
-    const double pi63 = 0x1.921fb54442d18p-62;
-    const uint32_t *arr = &inv_pio4[(xi >> 26) & 15];
+        const double pi63 = 0x1.921fb54442d18p-62;
+    const uint32_t *arr = &kInvPio4[(xi >> 26) & 15];
     int shift = (xi >> 23) & 7;
     uint64_t n, res0, res1, res2;
     xi = (xi & 0xffffff) | 0x800000;
@@ -147,7 +164,7 @@ BPPO_HD float sinf_glibc(float y) {
     } else if (abstop12(y) < 0x42fu) {     // abstop12(120.0f)
         sincos_t p = sincos_table(0);
         x = reduce_fast(x, p, &n);
-        double s = p.sign[n & 3];
+        double s = ((n + 1) & 2) ? -1.0 : 1.0;   // sign[4] = {1,-1,-1,1}
         if (n & 2) p = sincos_table(1);
         return sinf_poly(x * s, x * x, p, n);
     } else if (abstop12(y) < 0x7f8u) {
@@ -155,7 +172,7 @@ BPPO_HD float sinf_glibc(float y) {
         int sign = xi >> 31;
         x = reduce_large(xi, &n);
         sincos_t p = sincos_table(0);
-        double s = p.sign[(n + sign) & 3];
+        double s = ((n + sign + 1) & 2) ? -1.0 : 1.0;
         if ((n + sign) & 2) p = sincos_table(1);
         return sinf_poly(x * s, x * x, p, n);
     }
@@ -172,7 +189,7 @@ BPPO_HD float cosf_glibc(float y) {
     } else if (abstop12(y) < 0x42fu) {
         sincos_t p = sincos_table(0);
         x = reduce_fast(x, p, &n);
-        double s = p.sign[n & 3];
+        double s = ((n + 1) & 2) ? -1.0 : 1.0;   // sign[4] = {1,-1,-1,1}
         if (n & 2) p = sincos_table(1);
         return sinf_poly(x * s, x * x, p, n ^ 1);
     } else if (abstop12(y) < 0x7f8u) {
@@ -180,11 +197,45 @@ BPPO_HD float cosf_glibc(float y) {
         int sign = xi >> 31;
         x = reduce_large(xi, &n);
         sincos_t p = sincos_table(0);
-        double s = p.sign[(n + sign) & 3];
+        double s = ((n + sign + 1) & 2) ? -1.0 : 1.0;
         if ((n + sign) & 2) p = sincos_table(1);
         return sinf_poly(x * s, x * x, p, n ^ 1);
     }
     return (y - y) / (y - y);
+}
+
+
+// ------------------------------------------------------------------ expf ----
+// e_expf.c with __exp2f_data (EXP2F_TABLE_BITS = 5): used by log_softmax /
+// entropy / ratio = exp(log_ratio) (utils.rs:43-57, ppo.rs:1452).
+BPPO_HD uint64_t asuint64(double f) { uint64_t u; memcpy(&u, &f, 8); return u; }
+BPPO_HD double asdouble(uint64_t u) { double f; memcpy(&f, &u, 8); return f; }
+
+BPPO_HD float expf_glibc(float x) {
+        const double SHIFT = 0x1.8p+52, InvLn2N = 0x1.71547652b82fep+5;
+    const double C0 = 0x1.c6af84b912394p-20, C1 = 0x1.ebfce50fac4f3p-13, C2 = 0x1.62e42ff0c52d6p-6;
+    double xd = (double)x;
+    uint32_t abstop = (asuint(x) >> 20) & 0x7ff;
+    if (abstop >= 0x42bu) {                       // top12(88.0f)
+        if (asuint(x) == asuint(-INFINITY)) return 0.0f;
+        if (abstop >= 0x7f8u) return x + x;
+        if (x > 0x1.62e42ep6f) return INFINITY;
+        if (x < -0x1.9fe368p6f) return 0.0f;
+    }
+    double z = InvLn2N * xd;
+    double kd = z + SHIFT;
+    uint64_t ki = asuint64(kd);
+    kd -= SHIFT;
+    double r = fma(InvLn2N, xd, -kd);   // glibc's -mfma build contracts z - kd
+    uint64_t t = kExp2fTab[ki % 32];
+    t += ki << (52 - 5);
+    double s = asdouble(t);
+    double zz = fma(C0, r, C1);
+    double r2 = r * r;
+    double y = fma(C2, r, 1.0);
+    y = fma(zz, r2, y);
+    y = y * s;
+    return (float)y;
 }
 
 }  // namespace bppo_math

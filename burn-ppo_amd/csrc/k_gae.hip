@@ -1,0 +1,261 @@
+// k_gae.hip — GAE and the return-normaliser scan.
+//
+// GAE is a reverse linear recurrence over T per env and embarrassingly parallel
+// over N: one lane per env walks t = T-1..0, loading (reward, done, value) rows
+// with coalesced 256-B wave accesses (lane = env), UNROLL steps in flight, and
+// the carry in registers.  The arithmetic is the reference's op-for-op
+// (ppo.rs:1109-1112: delta = fma(gamma*nv, 1-d, r) - v; A = fma(gamma*lambda*(1-d), A, delta)),
+// so advantages are bit-identical.  The multiplayer variant fuses the two
+// reverse passes of ppo.rs:1179-1253 into one walk with per-player carries in
+// registers, keeping each element's op order.
+//
+// ReturnNormalizer (normalization.rs:115-202, applied at ppo.rs:390-408): the
+// rolling return per (env) is a per-env scan; its Welford statistics are a
+// global inclusive scan in (t, e) order, done here as a Chan-merge scan in f64.
+#include "bppo_internal.h"
+
+namespace bppo {
+
+constexpr int GAE_UNROLL = 8;
+
+__global__ void __launch_bounds__(256) k_gae_1p(const float *__restrict__ r,
+                                                const float *__restrict__ d,
+                                                const float *__restrict__ v,
+                                                const float *__restrict__ lv, int T, int N,
+                                                float gamma, float lambda, float *__restrict__ adv,
+                                                float *__restrict__ ret) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= N) return;
+    const float gl = gamma * lambda;    // `gamma * gae_lambda * (1 - d)` is left-assoc
+    float last = 0.0f;
+    float nv = lv[e];
+    int t = T - 1;
+    for (; t >= GAE_UNROLL - 1; t -= GAE_UNROLL) {
+        float rr[GAE_UNROLL], dd[GAE_UNROLL], vv[GAE_UNROLL];
+#pragma unroll
+        for (int u = 0; u < GAE_UNROLL; u++) {
+            const size_t i = (size_t)(t - u) * N + e;
+            rr[u] = r[i]; dd[u] = d[i]; vv[u] = v[i];
+        }
+#pragma unroll
+        for (int u = 0; u < GAE_UNROLL; u++) {
+            const size_t i = (size_t)(t - u) * N + e;
+            const float om = 1.0f - dd[u];
+            const float delta = __fsub_rn(__builtin_fmaf(gamma * nv, om, rr[u]), vv[u]);
+            last = __builtin_fmaf(gl * om, last, delta);
+            adv[i] = last;
+            ret[i] = __fadd_rn(last, vv[u]);
+            nv = vv[u];
+        }
+    }
+    for (; t >= 0; t--) {
+        const size_t i = (size_t)t * N + e;
+        const float vv = v[i], om = 1.0f - d[i];
+        const float delta = __fsub_rn(__builtin_fmaf(gamma * nv, om, r[i]), vv);
+        last = __builtin_fmaf(gl * om, last, delta);
+        adv[i] = last;
+        ret[i] = __fadd_rn(last, vv);
+        nv = vv;
+    }
+}
+
+template <int P>
+__global__ void __launch_bounds__(256) k_gae_mp(const float *__restrict__ ar,
+                                                const int32_t *__restrict__ pl,
+                                                const float *__restrict__ d,
+                                                const float *__restrict__ v,
+                                                const float *__restrict__ lvpp, int T, int N,
+                                                float gamma, float lambda, float *__restrict__ adv,
+                                                float *__restrict__ ret) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= N) return;
+    const float gl = gamma * lambda;
+    float carry[P], gc[P], nv[P];
+#pragma unroll
+    for (int p = 0; p < P; p++) { carry[p] = 0.0f; gc[p] = 0.0f; nv[p] = lvpp[(size_t)e * P + p]; }
+    for (int t = T - 1; t >= 0; t--) {
+        const size_t i = (size_t)t * N + e;
+        const int a = pl[i];
+        const float dn = d[i], vv = v[i];
+        float rw[P];
+#pragma unroll
+        for (int p = 0; p < P; p++) rw[p] = ar[i * P + p];
+        // pass 1 (ppo.rs:1179-1203)
+        if (dn > 0.5f) {
+#pragma unroll
+            for (int p = 0; p < P; p++) carry[p] = 0.0f;
+        }
+        float ca = 0.0f, ra = 0.0f;
+#pragma unroll
+        for (int p = 0; p < P; p++) if (p == a) { ca = carry[p]; ra = rw[p]; }
+        const float attributed = __fadd_rn(ra, ca);
+#pragma unroll
+        for (int p = 0; p < P; p++) carry[p] = p == a ? 0.0f : __fadd_rn(carry[p], rw[p]);
+        // pass 2 (ppo.rs:1217-1253)
+        if (dn > 0.5f) {
+#pragma unroll
+            for (int p = 0; p < P; p++) { gc[p] = 0.0f; if (p != a) nv[p] = 0.0f; }
+        }
+        float nva = 0.0f, gca = 0.0f;
+#pragma unroll
+        for (int p = 0; p < P; p++) if (p == a) { nva = nv[p]; gca = gc[p]; }
+        const float om = 1.0f - dn;
+        const float delta = __fsub_rn(__builtin_fmaf(gamma * nva, om, attributed), vv);
+        const float A = __builtin_fmaf(gl * om, gca, delta);
+        adv[i] = A;
+        ret[i] = __fadd_rn(A, vv);
+#pragma unroll
+        for (int p = 0; p < P; p++) if (p == a) { gc[p] = A; nv[p] = vv; }
+    }
+}
+
+bppo_status launch_gae_1p(const float *r, const float *d, const float *v, const float *lv, int T,
+                          int N, float gamma, float lambda, float *adv, float *ret, hipStream_t s) {
+    if (T <= 0 || N <= 0) return BPPO_OK;
+    hipLaunchKernelGGL(k_gae_1p, dim3((N + 255) / 256), dim3(256), 0, s, r, d, v, lv, T, N, gamma,
+                       lambda, adv, ret);
+    return hipGetLastError() == hipSuccess ? BPPO_OK : BPPO_ERR_HIP;
+}
+
+bppo_status launch_gae_mp(const float *ar, const int32_t *pl, const float *d, const float *v,
+                          const float *lvpp, int T, int N, int P, float gamma, float lambda,
+                          float *adv, float *ret, hipStream_t s) {
+    if (T <= 0 || N <= 0) return BPPO_OK;
+    dim3 g((N + 255) / 256), b(256);
+    switch (P) {
+    case 1: hipLaunchKernelGGL(k_gae_mp<1>, g, b, 0, s, ar, pl, d, v, lvpp, T, N, gamma, lambda, adv, ret); break;
+    case 2: hipLaunchKernelGGL(k_gae_mp<2>, g, b, 0, s, ar, pl, d, v, lvpp, T, N, gamma, lambda, adv, ret); break;
+    case 3: hipLaunchKernelGGL(k_gae_mp<3>, g, b, 0, s, ar, pl, d, v, lvpp, T, N, gamma, lambda, adv, ret); break;
+    case 4: hipLaunchKernelGGL(k_gae_mp<4>, g, b, 0, s, ar, pl, d, v, lvpp, T, N, gamma, lambda, adv, ret); break;
+    default: return BPPO_ERR_ARG;
+    }
+    return hipGetLastError() == hipSuccess ? BPPO_OK : BPPO_ERR_HIP;
+}
+
+// --------------------------------------------------------- ReturnNormalizer --
+__device__ __forceinline__ Welford wmerge(Welford a, Welford b) {
+    if (b.n == 0.0) return a;
+    if (a.n == 0.0) return b;
+    const double n = a.n + b.n, dl = b.mean - a.mean;
+    Welford r;
+    r.n = n;
+    r.mean = a.mean + dl * (b.n / n);
+    r.m2 = a.m2 + b.m2 + dl * dl * (a.n * b.n / n);
+    return r;
+}
+// normalization.rs:171-181 single-sample update
+__device__ __forceinline__ void wpush(Welford &s, double x) {
+    s.n += 1.0;
+    const double delta = x - s.mean;
+    s.mean += delta / s.n;
+    s.m2 += delta * (x - s.mean);
+}
+
+constexpr int RN_IPT = 16, RN_BLOCK = 256, RN_SEG = RN_IPT * RN_BLOCK;
+
+// per-env rolling returns (update_return / reset_player after the stats update)
+__global__ void k_rn_returns(int T, int N, double gamma, const float *rew_raw, const float *done,
+                             double *returns_state, double *X) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= N) return;
+    double x = returns_state[e];
+    for (int t = 0; t < T; t++) {
+        const size_t i = (size_t)t * N + e;
+        x = x * gamma + (double)rew_raw[i];
+        X[i] = x;
+        if (done[i] != 0.0f) x = 0.0;
+    }
+    returns_state[e] = x;
+}
+
+// block-level exclusive scan of Welford states held one per thread (Hillis-Steele)
+__device__ Welford block_exclusive_scan(Welford mine, Welford *sh) {
+    sh[threadIdx.x] = mine;
+    __syncthreads();
+    for (int off = 1; off < (int)blockDim.x; off <<= 1) {
+        Welford v = sh[threadIdx.x];
+        Welford u = threadIdx.x >= (unsigned)off ? sh[threadIdx.x - off] : Welford{0, 0, 0};
+        __syncthreads();
+        sh[threadIdx.x] = threadIdx.x >= (unsigned)off ? wmerge(u, v) : v;
+        __syncthreads();
+    }
+    Welford incl = sh[threadIdx.x];
+    Welford excl = threadIdx.x > 0 ? sh[threadIdx.x - 1] : Welford{0, 0, 0};
+    (void)incl;
+    __syncthreads();
+    return excl;
+}
+
+__global__ void __launch_bounds__(RN_BLOCK) k_rn_block_agg(size_t n, const double *X, Welford *agg) {
+    __shared__ Welford sh[RN_BLOCK];
+    const size_t base = (size_t)blockIdx.x * RN_SEG + (size_t)threadIdx.x * RN_IPT;
+    Welford s{0, 0, 0};
+    for (int k = 0; k < RN_IPT; k++)
+        if (base + k < n) wpush(s, X[base + k]);
+    Welford ex = block_exclusive_scan(s, sh);
+    if (threadIdx.x == blockDim.x - 1) agg[blockIdx.x] = wmerge(ex, s);
+}
+
+// exclusive scan of the block aggregates, seeded with the running stats
+__global__ void __launch_bounds__(1024) k_rn_agg_scan(int nb, Welford *agg, double *stats) {
+    __shared__ Welford sh[1024];
+    const int per = (nb + 1023) / 1024;
+    const int lo = threadIdx.x * per;
+    Welford s{0, 0, 0};
+    for (int k = 0; k < per; k++)
+        if (lo + k < nb) s = wmerge(s, agg[lo + k]);
+    Welford ex = block_exclusive_scan(s, sh);
+    Welford run = wmerge(Welford{stats[2], stats[0], stats[1]}, ex);
+    for (int k = 0; k < per; k++)
+        if (lo + k < nb) {
+            Welford a = agg[lo + k];
+            agg[lo + k] = run;            // exclusive prefix of block lo+k
+            run = wmerge(run, a);
+        }
+    if (threadIdx.x == blockDim.x - 1 || (lo < nb && lo + per >= nb)) {
+        if (lo < nb && lo + per >= nb) { stats[0] = run.mean; stats[1] = run.m2; stats[2] = run.n; }
+    }
+}
+
+__global__ void __launch_bounds__(RN_BLOCK) k_rn_apply(size_t n, const double *X,
+                                                       const float *rew_raw, const Welford *agg,
+                                                       float clip, float *rew) {
+    __shared__ Welford sh[RN_BLOCK];
+    const size_t base = (size_t)blockIdx.x * RN_SEG + (size_t)threadIdx.x * RN_IPT;
+    Welford s{0, 0, 0};
+    for (int k = 0; k < RN_IPT; k++)
+        if (base + k < n) wpush(s, X[base + k]);
+    Welford ex = block_exclusive_scan(s, sh);
+    Welford run = wmerge(agg[blockIdx.x], ex);
+    for (int k = 0; k < RN_IPT; k++) {
+        const size_t i = base + k;
+        if (i >= n) break;
+        wpush(run, X[i]);
+        float r = rew_raw[i];
+        if (run.n >= 2.0) {                                  // normalization.rs:187-197
+            const double sd = sqrt(run.m2 / run.n + 1e-8);
+            float z = (float)((double)r / sd);
+            z = z < -clip ? -clip : z;
+            z = z > clip ? clip : z;
+            r = z;
+        }
+        rew[i] = r;
+    }
+}
+
+bppo_status launch_return_norm(bppo_ctx *c) {
+    const size_t n = (size_t)c->T * c->N;
+    const int nb = (int)((n + RN_SEG - 1) / RN_SEG);
+    hipLaunchKernelGGL(k_rn_returns, dim3((c->N + 255) / 256), dim3(256), 0, c->stream, c->T, c->N,
+                       c->cfg.gamma, c->d_rew_raw, c->d_done, c->d_rn_returns, c->d_X);
+    hipLaunchKernelGGL(k_rn_block_agg, dim3(nb), dim3(RN_BLOCK), 0, c->stream, n, c->d_X,
+                       c->d_scan_agg);
+    hipLaunchKernelGGL(k_rn_agg_scan, dim3(1), dim3(1024), 0, c->stream, nb, c->d_scan_agg,
+                       c->d_rn_stats);
+    hipLaunchKernelGGL(k_rn_apply, dim3(nb), dim3(RN_BLOCK), 0, c->stream, n, c->d_X, c->d_rew_raw,
+                       c->d_scan_agg, (float)c->cfg.return_clip, c->d_rew);
+    BPPO_HIP(c, hipGetLastError());
+    return BPPO_OK;
+}
+
+}  // namespace bppo

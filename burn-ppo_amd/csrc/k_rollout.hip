@@ -1,0 +1,401 @@
+// k_rollout.hip — CartPole VecEnv + fused rollout kernels.
+//
+// One lane owns one environment for the whole rollout (SoA env state in HBM,
+// kept in VGPRs across the T steps).  Per step, exactly as collect_rollouts
+// (ppo.rs:271-446): lagged obs normalisation (normalization.rs:58-75), MLP
+// forward (mlp.rs:140-206) with weights staged in LDS, Gumbel-max sampling
+// from the main ChaCha12 stream at word base + (t*N + e)*A + a (utils.rs:10-31),
+// log-prob (utils.rs:38-45), env step + auto-reset (env.rs:413-467,
+// cartpole.rs:272-301).  Raw rewards are written; the return normaliser runs as
+// a post-pass scan (k_gae.hip) because normalised rewards only feed GAE.
+#include "bppo_internal.h"
+
+namespace bppo {
+
+// ObsNormalizer::normalize_batch (normalization.rs:58-75) from device stats
+// on = {mean[D], M2[D], count}
+__device__ __forceinline__ void normalize_obs5(const double *__restrict__ on, int norm_on,
+                                               const float (&raw)[5], float (&out)[5]) {
+    const double cnt = on[10];
+    if (!norm_on || cnt < 2.0) {
+#pragma unroll
+        for (int d = 0; d < 5; d++) out[d] = raw[d];
+        return;
+    }
+#pragma unroll
+    for (int d = 0; d < 5; d++) {
+        double var = on[5 + d] / cnt;
+        double sd = sqrt(var);
+        sd = sd < 1e-8 ? 1e-8 : sd;
+        float z = (float)(((double)raw[d] - on[d]) / sd);
+        z = z < -10.0f ? -10.0f : z;
+        z = z > 10.0f ? 10.0f : z;
+        out[d] = z;
+    }
+}
+
+__device__ __forceinline__ void load_state(const float *cp, const int32_t *steps, int N, int e,
+                                           CartPoleState &s) {
+    s.x = cp[e]; s.x_dot = cp[N + e]; s.theta = cp[2 * N + e]; s.theta_dot = cp[3 * N + e];
+    s.steps = steps[e];
+}
+__device__ __forceinline__ void store_state(float *cp, int32_t *steps, int N, int e,
+                                            const CartPoleState &s) {
+    cp[e] = s.x; cp[N + e] = s.x_dot; cp[2 * N + e] = s.theta; cp[3 * N + e] = s.theta_dot;
+    steps[e] = s.steps;
+}
+
+// VecEnv::new: CartPole::new(seed+i) resets once, VecEnv::new resets again
+// (cartpole.rs:104, env.rs:289-293) => words 0-3 discarded, state from 4-7.
+__global__ void k_cartpole_reset(int N, uint64_t seed_base, float *cp, int32_t *steps,
+                                 uint64_t *env_pos, float *ep_ret, int32_t *ep_len, float *obs) {
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= N) return;
+    WordCursor c;
+    c.init(seed_key(seed_base + (uint64_t)e), 0, 0);
+    CartPoleState s;
+    cartpole_reset(s, c);
+    cartpole_reset(s, c);
+    store_state(cp, steps, N, e, s);
+    env_pos[e] = c.pos;
+    ep_ret[e] = 0.0f;
+    ep_len[e] = 0;
+    if (obs) {
+        float o[5];
+        cartpole_obs(s, o);
+        for (int d = 0; d < 5; d++) obs[e * 5 + d] = o[d];
+    }
+}
+
+struct RolloutArgs {
+    int N, T;
+    uint64_t seed_base;
+    float *cp; int32_t *steps; uint64_t *env_pos; float *ep_ret; int32_t *ep_len;
+    Key8 key; uint64_t stream; uint64_t base_pos;
+    const float *params; int n_params;
+    const double *on; int norm_on;
+    float *obs, *rew_raw, *done, *val, *logp; int32_t *act;
+    double *obs_part;
+    EpisodeRec *eps; int32_t *ep_count; int eps_cap;
+    int32_t *err;
+};
+
+template <int H, int NL>
+__global__ void __launch_bounds__(256) k_cartpole_rollout(RolloutArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float sP[];
+    constexpr CpOffsets O = cp_offsets<H, NL>();
+    for (int i = threadIdx.x; i < O.n; i += blockDim.x) sP[i] = a.params[i];
+    __syncthreads();
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= a.N) return;
+    const int N = a.N;
+    CartPoleState s;
+    load_state(a.cp, a.steps, N, e, s);
+    WordCursor ec;
+    ec.init(seed_key(a.seed_base + (uint64_t)e), 0, a.env_pos[e]);
+    float ep_ret = a.ep_ret[e];
+    int32_t ep_len = a.ep_len[e];
+    double wm[5] = {0, 0, 0, 0, 0}, wM2[5] = {0, 0, 0, 0, 0};
+    int32_t bad = 0;
+#pragma unroll 1
+    for (int t = 0; t < a.T; t++) {
+        float raw[5], x[5];
+        cartpole_obs(s, raw);
+        const double cnt = (double)(t + 1);
+#pragma unroll
+        for (int d = 0; d < 5; d++) {                 // per-env Welford partial (raw obs)
+            double xv = (double)raw[d];
+            double delta = xv - wm[d];
+            wm[d] += delta / cnt;
+            wM2[d] += delta * (xv - wm[d]);
+        }
+        normalize_obs5(a.on, a.norm_on, raw, x);
+        const size_t row = (size_t)t * N + e;
+#pragma unroll
+        for (int d = 0; d < 5; d++) a.obs[row * 5 + d] = x[d];
+        float lg[2], v;
+        int zero = 0;
+        asm volatile("" : "+v"(zero));   // keep weight reads inside the step loop (no LICM spill)
+        cp_forward<H, NL>(sP + zero, x, lg, v);
+        // Gumbel-max: words base + row*2 + {0,1}
+        const uint64_t p0 = a.base_pos + row * 2;
+        uint32_t blk[16];
+        chacha12_block(a.key, p0 >> 4, a.stream, blk);
+        const uint32_t l0 = (uint32_t)(p0 & 15);
+        uint32_t w0 = blk[0], w1 = blk[1];
+#pragma unroll
+        for (int i = 1; i < 16; i++) w0 = l0 == (uint32_t)i ? blk[i] : w0;
+#pragma unroll
+        for (int i = 0; i < 15; i++) w1 = l0 == (uint32_t)i ? blk[i + 1] : w1;
+        if (l0 == 15) {
+            uint32_t b2[16];
+            chacha12_block(a.key, (p0 >> 4) + 1, a.stream, b2);
+            w1 = b2[0];
+        }
+        const float n0 = __fadd_rn(lg[0], gumbel_from_word(w0));
+        const float n1 = __fadd_rn(lg[1], gumbel_from_word(w1));
+        const int act = n1 > n0 ? 1 : 0;               // argmax, first maximum
+        const float lp = log_prob_row<2>(lg, act);
+        bad |= !isfinite(lp);
+        float r;
+        const bool done = cartpole_step(s, act, r);
+        ep_ret = __fadd_rn(ep_ret, r);
+        ep_len += 1;
+        if (done) {
+            int32_t k = atomicAdd(a.ep_count, 1);
+            if (k < a.eps_cap) {
+                EpisodeRec rec;
+                rec.total_reward[0] = ep_ret; rec.total_reward[1] = rec.total_reward[2] =
+                    rec.total_reward[3] = 0.0f;
+                rec.length = ep_len; rec.env_index = e; rec.step = t; rec.pad = 0;
+                a.eps[k] = rec;
+            }
+            cartpole_reset(s, ec);
+            ep_ret = 0.0f;
+            ep_len = 0;
+        }
+        a.act[row] = act;
+        a.rew_raw[row] = r;
+        a.done[row] = done ? 1.0f : 0.0f;
+        a.val[row] = v;
+        a.logp[row] = lp;
+    }
+    store_state(a.cp, a.steps, N, e, s);
+    a.env_pos[e] = ec.pos;
+    a.ep_ret[e] = ep_ret;
+    a.ep_len[e] = ep_len;
+#pragma unroll
+    for (int d = 0; d < 5; d++) {
+        a.obs_part[(size_t)e * 10 + d] = wm[d];
+        a.obs_part[(size_t)e * 10 + 5 + d] = wM2[d];
+    }
+    if (bad) atomicOr(a.err, 1);
+}
+
+// VecEnv::step surface (env.rs:400-487) for host-driven stepping.
+__global__ void k_cartpole_step(int N, uint64_t seed_base, float *cp, int32_t *steps,
+                                uint64_t *env_pos, float *ep_ret, int32_t *ep_len,
+                                const int32_t *actions, float *rew, uint8_t *dn, float *obs,
+                                EpisodeRec *eps, int32_t *ep_count, int cap) {
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= N) return;
+    CartPoleState s;
+    load_state(cp, steps, N, e, s);
+    float r;
+    bool done = cartpole_step(s, actions[e], r);
+    float er = __fadd_rn(ep_ret[e], r);
+    int32_t el = ep_len[e] + 1;
+    if (done) {
+        int32_t k = atomicAdd(ep_count, 1);
+        if (k < cap) {
+            EpisodeRec rec;
+            rec.total_reward[0] = er; rec.total_reward[1] = rec.total_reward[2] = rec.total_reward[3] = 0;
+            rec.length = el; rec.env_index = e; rec.step = 0; rec.pad = 0;
+            eps[k] = rec;
+        }
+        WordCursor c;
+        c.init(seed_key(seed_base + (uint64_t)e), 0, env_pos[e]);
+        cartpole_reset(s, c);
+        env_pos[e] = c.pos;
+        er = 0.0f; el = 0;
+    }
+    store_state(cp, steps, N, e, s);
+    ep_ret[e] = er; ep_len[e] = el;
+    rew[e] = r;
+    dn[e] = done ? 1 : 0;
+    if (obs) {
+        float o[5];
+        cartpole_obs(s, o);
+        for (int d = 0; d < 5; d++) obs[e * 5 + d] = o[d];
+    }
+}
+
+__global__ void k_cartpole_observe(int N, const float *cp, const int32_t *steps, float *obs) {
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= N) return;
+    CartPoleState s;
+    load_state(cp, steps, N, e, s);
+    float o[5];
+    cartpole_obs(s, o);
+    for (int d = 0; d < 5; d++) obs[e * 5 + d] = o[d];
+}
+
+// bootstrap (main.rs:878-896): current obs normalised with the UPDATED stats
+template <int H, int NL>
+__global__ void __launch_bounds__(256) k_cartpole_bootstrap(int N, const float *cp,
+                                                            const int32_t *steps,
+                                                            const float *params, const double *on,
+                                                            int norm_on, float *last_v) {
+    extern __shared__ __attribute__((aligned(16))) float sP[];
+    constexpr CpOffsets O = cp_offsets<H, NL>();
+    for (int i = threadIdx.x; i < O.n; i += blockDim.x) sP[i] = params[i];
+    __syncthreads();
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= N) return;
+    CartPoleState s;
+    load_state(cp, steps, N, e, s);
+    float raw[5], x[5], lg[2], v;
+    cartpole_obs(s, raw);
+    normalize_obs5(on, norm_on, raw, x);
+    cp_forward<H, NL>(sP, x, lg, v);
+    last_v[e] = v;
+}
+
+template <int H, int NL>
+__global__ void __launch_bounds__(256) k_cartpole_forward_rows(int B, const float *obs,
+                                                               const float *params, float *logits,
+                                                               float *values) {
+    extern __shared__ __attribute__((aligned(16))) float sP[];
+    constexpr CpOffsets O = cp_offsets<H, NL>();
+    for (int i = threadIdx.x; i < O.n; i += blockDim.x) sP[i] = params[i];
+    __syncthreads();
+    int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= B) return;
+    float x[5], lg[2], v;
+    for (int d = 0; d < 5; d++) x[d] = obs[(size_t)r * 5 + d];
+    cp_forward<H, NL>(sP, x, lg, v);
+    logits[(size_t)r * 2] = lg[0];
+    logits[(size_t)r * 2 + 1] = lg[1];
+    values[r] = v;
+}
+
+// Merge per-env Welford partials (count T each) into the running stats
+// (normalization.rs:37-53 is a sequential Welford over T*N rows; Chan merges
+// give the same statistics to f64 rounding).  One block, fixed merge order.
+__global__ void __launch_bounds__(1024) k_obs_norm_merge(int N, int D, double T,
+                                                         const double *part, double *on) {
+    __shared__ double sm[1024][2];
+    __shared__ double sn[1024];
+    for (int d = 0; d < D; d++) {
+        double n = 0, mean = 0, m2 = 0;
+        for (int e = threadIdx.x; e < N; e += blockDim.x) {
+            double mb = part[(size_t)e * 2 * D + d], m2b = part[(size_t)e * 2 * D + D + d];
+            double nn = n + T, delta = mb - mean;
+            mean += delta * (T / nn);
+            m2 += m2b + delta * delta * (n * T / nn);
+            n = nn;
+        }
+        sn[threadIdx.x] = n; sm[threadIdx.x][0] = mean; sm[threadIdx.x][1] = m2;
+        __syncthreads();
+        for (int st = blockDim.x / 2; st > 0; st >>= 1) {
+            if (threadIdx.x < st) {
+                double na = sn[threadIdx.x], nb = sn[threadIdx.x + st];
+                double nn = na + nb;
+                if (nb > 0) {
+                    double delta = sm[threadIdx.x + st][0] - sm[threadIdx.x][0];
+                    double f = na > 0 ? nb / nn : 1.0;
+                    sm[threadIdx.x][0] += delta * f;
+                    sm[threadIdx.x][1] += sm[threadIdx.x + st][1] + delta * delta * (na * nb / nn);
+                    sn[threadIdx.x] = nn;
+                }
+            }
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) {
+            // old stats (count on[2D]) merged with the batch
+            double na = on[2 * D], nb = sn[0], nn = na + nb;
+            double ma = on[d], mb = sm[0][0];
+            double delta = mb - ma;
+            on[d] = na > 0 ? ma + delta * (nb / nn) : mb;
+            on[D + d] = on[D + d] + sm[0][1] + (na > 0 ? delta * delta * (na * nb / nn) : 0.0);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) on[2 * D] += (double)N * T;
+}
+
+// ------------------------------------------------------------- launchers ---
+#define CP_DISPATCH(H_, NL_, CALL)                                               \
+    if (h == H_ && nl == NL_) { CALL(H_, NL_); return BPPO_OK; }
+
+static bool cp_supported(int h, int nl) {
+    return (h == 16 || h == 32 || h == 64) && (nl == 1 || nl == 2);
+}
+
+bppo_status launch_cartpole_reset(bppo_ctx *c) {
+    int N = c->N;
+    hipLaunchKernelGGL(k_cartpole_reset, dim3((N + 255) / 256), dim3(256), 0, c->stream, N,
+                       c->cfg.env_seed_base, c->d_cp, c->d_steps, c->d_env_pos, c->d_ep_ret,
+                       c->d_ep_len, nullptr);
+    BPPO_HIP(c, hipGetLastError());
+    return BPPO_OK;
+}
+
+bppo_status launch_cartpole_rollout(bppo_ctx *c, uint64_t base_pos, const double *, const double *,
+                                    int norm_on) {
+    const int h = c->cfg.hidden_size, nl = c->cfg.num_hidden;
+    if (!cp_supported(h, nl) || !c->cfg.relu) {
+        c->err = "CartPole rollout kernel supports relu MLPs with hidden in {16,32,64} x {1,2} layers";
+        return BPPO_ERR_UNSUPPORTED;
+    }
+    RolloutArgs a;
+    a.N = c->N; a.T = c->T; a.seed_base = c->cfg.env_seed_base;
+    a.cp = c->d_cp; a.steps = c->d_steps; a.env_pos = c->d_env_pos; a.ep_ret = c->d_ep_ret;
+    a.ep_len = c->d_ep_len; a.key = c->rng_key; a.stream = c->cfg.rng_stream; a.base_pos = base_pos;
+    a.params = c->d_params; a.n_params = (int)c->net.n_params; a.on = c->d_on; a.norm_on = norm_on;
+    a.obs = c->d_obs; a.rew_raw = c->d_rew_raw; a.done = c->d_done; a.val = c->d_val;
+    a.logp = c->d_logp; a.act = c->d_act; a.obs_part = c->d_obs_part; a.eps = c->d_eps;
+    a.ep_count = c->d_ep_count; a.eps_cap = c->eps_cap; a.err = c->d_err;
+    dim3 grid((c->N + 255) / 256), blk(256);
+    size_t lds = c->net.n_params * sizeof(float);
+#define L(H_, NL_) hipLaunchKernelGGL((k_cartpole_rollout<H_, NL_>), grid, blk, lds, c->stream, a)
+    CP_DISPATCH(16, 1, L) CP_DISPATCH(16, 2, L) CP_DISPATCH(32, 1, L) CP_DISPATCH(32, 2, L)
+    CP_DISPATCH(64, 1, L) CP_DISPATCH(64, 2, L)
+#undef L
+    return BPPO_ERR_UNSUPPORTED;
+}
+
+bppo_status launch_bootstrap(bppo_ctx *c, const double *, const double *, int norm_on) {
+    const int h = c->cfg.hidden_size, nl = c->cfg.num_hidden;
+    dim3 grid((c->N + 255) / 256), blk(256);
+    size_t lds = c->net.n_params * sizeof(float);
+#define L(H_, NL_)                                                                              \
+    hipLaunchKernelGGL((k_cartpole_bootstrap<H_, NL_>), grid, blk, lds, c->stream, c->N, c->d_cp, \
+                       c->d_steps, c->d_params, c->d_on, norm_on, c->d_last_v)
+    CP_DISPATCH(16, 1, L) CP_DISPATCH(16, 2, L) CP_DISPATCH(32, 1, L) CP_DISPATCH(32, 2, L)
+    CP_DISPATCH(64, 1, L) CP_DISPATCH(64, 2, L)
+#undef L
+    return BPPO_ERR_UNSUPPORTED;
+}
+
+bppo_status launch_forward_rows(bppo_ctx *c, const float *d_obs, int B, float *d_logits,
+                                float *d_values) {
+    const int h = c->cfg.hidden_size, nl = c->cfg.num_hidden;
+    dim3 grid((B + 255) / 256), blk(256);
+    size_t lds = c->net.n_params * sizeof(float);
+#define L(H_, NL_)                                                                                \
+    hipLaunchKernelGGL((k_cartpole_forward_rows<H_, NL_>), grid, blk, lds, c->stream, B, d_obs, \
+                       c->d_params, d_logits, d_values)
+    CP_DISPATCH(16, 1, L) CP_DISPATCH(16, 2, L) CP_DISPATCH(32, 1, L) CP_DISPATCH(32, 2, L)
+    CP_DISPATCH(64, 1, L) CP_DISPATCH(64, 2, L)
+#undef L
+    return BPPO_ERR_UNSUPPORTED;
+}
+
+bppo_status launch_cartpole_vecenv_step(bppo_ctx *c, const int32_t *d_actions, float *d_rew,
+                                        uint8_t *d_done, float *d_obs_out) {
+    int N = c->N;
+    hipLaunchKernelGGL(k_cartpole_step, dim3((N + 255) / 256), dim3(256), 0, c->stream, N,
+                       c->cfg.env_seed_base, c->d_cp, c->d_steps, c->d_env_pos, c->d_ep_ret,
+                       c->d_ep_len, d_actions, d_rew, d_done, d_obs_out, c->d_eps, c->d_ep_count,
+                       c->eps_cap);
+    BPPO_HIP(c, hipGetLastError());
+    return BPPO_OK;
+}
+
+bppo_status launch_cartpole_observe(bppo_ctx *c, float *d_obs_out) {
+    int N = c->N;
+    hipLaunchKernelGGL(k_cartpole_observe, dim3((N + 255) / 256), dim3(256), 0, c->stream, N,
+                       c->d_cp, c->d_steps, d_obs_out);
+    BPPO_HIP(c, hipGetLastError());
+    return BPPO_OK;
+}
+
+bppo_status launch_obs_norm_merge(bppo_ctx *c) {
+    hipLaunchKernelGGL(k_obs_norm_merge, dim3(1), dim3(1024), 0, c->stream, c->N, c->D,
+                       (double)c->T, c->d_obs_part, c->d_on);
+    BPPO_HIP(c, hipGetLastError());
+    return BPPO_OK;
+}
+
+}  // namespace bppo

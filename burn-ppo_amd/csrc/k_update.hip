@@ -1,0 +1,539 @@
+// k_update.hip — ppo_update on the device (ppo.rs:1661-2112).
+//
+//  * shuffle: the host walks rand 0.8.5's rejection chain (inherently serial)
+//    and hands over the Fisher-Yates swap targets J[i]; the GPU applies them by
+//    deterministic reservations (each round commits every swap whose two
+//    positions are not claimed by an earlier pending swap), which reproduces the
+//    sequential permutation exactly in O(log n) rounds;
+//  * per minibatch: gather by the shuffled indices (ppo.rs:1833-1857), raw
+//    advantage stats + normalisation (ppo.rs:1905-1917, utils.rs:80-89), fused
+//    forward + clipped-surrogate loss + backward (ppo.rs:1385-1502) with the
+//    weight-gradient reductions staged through LDS per wave, per-wave partial
+//    gradients reduced in fixed order (deterministic), per-tensor norm clip +
+//    Adam (main.rs:264-268).
+#include "bppo_internal.h"
+
+namespace bppo {
+
+// ============================================================== shuffle ====
+__global__ void k_dr_init(uint32_t n, uint32_t *perm, uint32_t *R, uint32_t *cnt) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) perm[i] = i;
+    if (i >= 1 && i < n) R[i - 1] = i;
+    if (i == 0) { cnt[0] = n > 0 ? n - 1 : 0; cnt[1] = 0; }
+}
+__global__ void k_dr_reset(const uint32_t *R, const uint32_t *cnt, const uint32_t *J, int32_t *res) {
+    const uint32_t m = cnt[0];
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < m; t += gridDim.x * blockDim.x) {
+        uint32_t i = R[t];
+        res[i] = -1;
+        res[J[i]] = -1;
+    }
+}
+__global__ void k_dr_reserve(const uint32_t *R, const uint32_t *cnt, const uint32_t *J, int32_t *res) {
+    const uint32_t m = cnt[0];
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < m; t += gridDim.x * blockDim.x) {
+        uint32_t i = R[t];
+        atomicMax(&res[i], (int32_t)i);       // earlier Fisher-Yates step = larger i wins
+        atomicMax(&res[J[i]], (int32_t)i);
+    }
+}
+__global__ void k_dr_commit(const uint32_t *R, uint32_t *cnt, const uint32_t *J, const int32_t *res,
+                            uint32_t *perm, uint32_t *R2) {
+    const uint32_t m = cnt[0];
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < m; t += gridDim.x * blockDim.x) {
+        uint32_t i = R[t], j = J[i];
+        if (res[i] == (int32_t)i && res[j] == (int32_t)i) {
+            uint32_t a = perm[i], b = perm[j];
+            perm[i] = b;
+            perm[j] = a;
+        } else {
+            R2[atomicAdd(&cnt[1], 1u)] = i;
+        }
+    }
+}
+__global__ void k_dr_swap_counts(uint32_t *cnt) {
+    cnt[0] = cnt[1];
+    cnt[1] = 0;
+}
+
+bppo_status launch_shuffle_apply(bppo_ctx *c, const uint32_t *h_J, uint32_t n) {
+    if (n == 0) return BPPO_OK;
+    BPPO_HIP(c, hipMemcpyAsync(c->d_J, h_J, sizeof(uint32_t) * n, hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(k_dr_init, dim3((n + 255) / 256), dim3(256), 0, c->stream, n, c->d_perm,
+                       c->d_R, c->d_cnt);
+    uint32_t *R = c->d_R, *R2 = c->d_R2;
+    const dim3 g(2048), b(256);
+    for (int iter = 0; iter < 4096; iter++) {
+        for (int k = 0; k < 8; k++) {
+            hipLaunchKernelGGL(k_dr_reset, g, b, 0, c->stream, R, c->d_cnt, c->d_J, c->d_res);
+            hipLaunchKernelGGL(k_dr_reserve, g, b, 0, c->stream, R, c->d_cnt, c->d_J, c->d_res);
+            hipLaunchKernelGGL(k_dr_commit, g, b, 0, c->stream, R, c->d_cnt, c->d_J, c->d_res,
+                               c->d_perm, R2);
+            hipLaunchKernelGGL(k_dr_swap_counts, dim3(1), dim3(1), 0, c->stream, c->d_cnt);
+            uint32_t *tmp = R; R = R2; R2 = tmp;
+        }
+        BPPO_HIP(c, hipMemcpyAsync(c->h_cnt, c->d_cnt, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                   c->stream));
+        BPPO_HIP(c, hipStreamSynchronize(c->stream));
+        if (c->h_cnt[0] == 0) return BPPO_OK;
+    }
+    c->err = "shuffle: deterministic reservations did not converge";
+    return BPPO_ERR_HIP;
+}
+
+// ============================================================ adv stats ====
+// two-pass, f64 accumulation, fixed-order final reduction
+constexpr int STAT_BLOCKS = 1024;
+
+__global__ void __launch_bounds__(256) k_adv_pass(const float *adv, const uint32_t *perm,
+                                                  uint32_t start, uint32_t n, const float *mb_stats,
+                                                  int pass, double *part) {
+    __shared__ double s0[256], s1[256];
+    __shared__ float smin[256], smax[256];
+    double a0 = 0.0;
+    float mn = INFINITY, mx = -INFINITY;
+    const float mean = pass ? mb_stats[0] : 0.0f;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        float a = adv[perm[start + i]];
+        if (pass == 0) {
+            a0 += (double)a;
+            mn = fminf(mn, a); mx = fmaxf(mx, a);
+        } else {
+            double d = (double)a - (double)mean;
+            a0 += d * d;
+        }
+    }
+    s0[threadIdx.x] = a0; smin[threadIdx.x] = mn; smax[threadIdx.x] = mx;
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+        if (threadIdx.x < st) {
+            s0[threadIdx.x] += s0[threadIdx.x + st];
+            smin[threadIdx.x] = fminf(smin[threadIdx.x], smin[threadIdx.x + st]);
+            smax[threadIdx.x] = fmaxf(smax[threadIdx.x], smax[threadIdx.x + st]);
+        }
+        __syncthreads();
+    }
+    (void)s1;
+    if (threadIdx.x == 0) {
+        part[blockIdx.x * 3 + 0] = s0[0];
+        part[blockIdx.x * 3 + 1] = (double)smin[0];
+        part[blockIdx.x * 3 + 2] = (double)smax[0];
+    }
+}
+
+// mb_stats: [0] mean (f32), [1] std (f32, unbiased), [2] min, [3] max
+__global__ void k_adv_finalize(const double *part, int nblk, uint32_t n, int pass, float *mb_stats) {
+    if (threadIdx.x != 0) return;
+    double s = 0.0, mn = INFINITY, mx = -INFINITY;
+    for (int b = 0; b < nblk; b++) {
+        s += part[b * 3];
+        mn = fmin(mn, part[b * 3 + 1]);
+        mx = fmax(mx, part[b * 3 + 2]);
+    }
+    if (pass == 0) {
+        mb_stats[0] = (float)(s / (double)n);
+        mb_stats[2] = (float)mn;
+        mb_stats[3] = (float)mx;
+    } else {
+        float var = n > 1 ? (float)(s / (double)(n - 1)) : NAN;
+        mb_stats[1] = sqrtf(var);
+    }
+}
+
+// =========================================================== fwd + bwd ====
+// metric slots appended after the parameters in the gradient slab
+enum { M_PL = 0, M_VL, M_H, M_KL, M_CF, M_V, M_R, M_VE, M_VE2, M_VEMAX, M_N, NUM_M };
+
+struct MbArgs {
+    const float *obs, *logp, *adv, *ret, *val;
+    const int32_t *act;
+    const uint32_t *perm;
+    uint32_t start, n;
+    const float *params;
+    const float *mb_stats;
+    float *slab;           // [waves][np + NUM_M]
+    int np;
+    float lo, hi, ceps;    // clip bounds
+    float inv_mb, ent_coef, value_coef;
+    int clip_value;
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+    return v;
+}
+
+// per-wave LDS staging of 64 rows; row-major [row][H] with the column XOR-ed by
+// the row, so lane-per-row writes spread over banks and row reads stay broadcast
+template <int H>
+struct WaveStage {
+    float a[64 * H];
+    float b[64 * H];
+    float x[64][8];
+    float l[64][4];
+    __device__ __forceinline__ static int at(int row, int col) { return row * H + (col ^ (row & (H - 1))); }
+};
+
+template <int H, int NL>
+__global__ void __launch_bounds__(256, 1) k_minibatch(MbArgs g) {
+    constexpr CpOffsets O = cp_offsets<H, NL>();
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float *sPbase = smem;
+    WaveStage<H> *stages = reinterpret_cast<WaveStage<H> *>(smem + ((O.n + 3) & ~3));
+    for (int i = threadIdx.x; i < O.n; i += blockDim.x) sPbase[i] = g.params[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    WaveStage<H> &S = stages[wv];
+    const int gwave = blockIdx.x * (blockDim.x >> 6) + wv;
+    const int nwaves = gridDim.x * (blockDim.x >> 6);
+    const float mean = g.mb_stats[0], denom = g.mb_stats[1] + 1e-8f;
+
+    // persistent per-lane gradient accumulators (lane = output column / feature)
+    float gW0[5], gb0 = 0.0f, gW1[H], gb1 = 0.0f;
+    float gP0 = 0.0f, gP1 = 0.0f, gV = 0.0f, gbp0 = 0.0f, gbp1 = 0.0f, gbv = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 5; k++) gW0[k] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < H; k++) gW1[k] = 0.0f;
+    float m_pl = 0, m_vl = 0, m_h = 0, m_kl = 0, m_cf = 0, m_v = 0, m_r = 0, m_ve = 0, m_ve2 = 0;
+    float m_vemax = -INFINITY, m_n = 0;
+
+    for (uint32_t base = (uint32_t)gwave * 64; base < g.n; base += (uint32_t)nwaves * 64) {
+        const uint32_t r = base + lane;
+        const bool valid = r < g.n;
+        int zero = 0;
+        asm volatile("" : "+v"(zero));   // keep weight reads inside the chunk loop (no LICM spill)
+        const float *sP = sPbase + zero;
+        float x[5] = {0, 0, 0, 0, 0};
+        int a = 0;
+        float olp = 0.0f, A = 0.0f, R = 0.0f, ov = 0.0f;
+        if (valid) {
+            const uint32_t idx = g.perm[g.start + r];
+#pragma unroll
+            for (int d = 0; d < 5; d++) x[d] = g.obs[(size_t)idx * 5 + d];
+            a = g.act[idx]; olp = g.logp[idx]; A = g.adv[idx]; R = g.ret[idx];
+            if (g.clip_value) ov = g.val[idx];
+        }
+        const float An = __fdiv_rn(__fsub_rn(A, mean), denom);   // utils.rs:88
+        // ---- forward (same code path as the rollout: ratio == 1 at first mb)
+        float h1[H];
+        linear_fwd<5, H, true>(sP + O.w0, sP + O.b0, x, h1);
+        uint64_t m1 = 0, m2 = 0;
+#pragma unroll
+        for (int k = 0; k < H; k++) m1 |= (h1[k] > 0.0f ? 1ull : 0ull) << k;
+        float hl[H];
+        if constexpr (NL == 2) {
+            linear_fwd<H, H, true>(sP + O.w1, sP + O.b1, h1, hl);
+        } else {
+#pragma unroll
+            for (int k = 0; k < H; k++) hl[k] = h1[k];
+        }
+#pragma unroll
+        for (int k = 0; k < H; k++) m2 |= (hl[k] > 0.0f ? 1ull : 0ull) << k;
+        float lg[2], vv[1];
+        linear_fwd<H, 2, false>(sP + O.wp, sP + O.bp, hl, lg);
+        linear_fwd<H, 1, false>(sP + O.wv, sP + O.bv, hl, vv);
+        const float v = vv[0];
+        // ---- loss terms (ppo.rs:1444-1487)
+        float mx = lg[0] > lg[1] ? lg[0] : lg[1];
+        const float e0 = bppo_math::expf_glibc(__fsub_rn(lg[0], mx));
+        const float e1 = bppo_math::expf_glibc(__fsub_rn(lg[1], mx));
+        const float lse = bppo_math::logf_glibc(__fadd_rn(e0, e1));
+        const float ls0 = __fsub_rn(__fsub_rn(lg[0], mx), lse);
+        const float ls1 = __fsub_rn(__fsub_rn(lg[1], mx), lse);
+        const float p0 = bppo_math::expf_glibc(ls0), p1 = bppo_math::expf_glibc(ls1);
+        const float Hn = -__fadd_rn(__fmul_rn(p0, ls0), __fmul_rn(p1, ls1));
+        const float newlp = a == 1 ? ls1 : ls0;
+        const float log_ratio = __fsub_rn(newlp, olp);
+        const float ratio = bppo_math::expf_glibc(log_ratio);
+        const float na = -An;
+        const float pl1 = __fmul_rn(na, ratio);
+        const float rc = ratio < g.lo ? g.lo : (ratio > g.hi ? g.hi : ratio);
+        const float pl2 = __fmul_rn(na, rc);
+        const bool rhs = pl1 < pl2;
+        const float pl = rhs ? pl2 : pl1;
+        float vl, dvl;
+        if (g.clip_value) {
+            const float dlt = __fsub_rn(v, ov);
+            const float dc = dlt < -g.ceps ? -g.ceps : (dlt > g.ceps ? g.ceps : dlt);
+            const float vc = __fadd_rn(ov, dc);
+            const float l1 = __fmul_rn(__fsub_rn(v, R), __fsub_rn(v, R));
+            const float l2 = __fmul_rn(__fsub_rn(vc, R), __fsub_rn(vc, R));
+            if (l1 < l2) { vl = l2; dvl = (dlt >= -g.ceps && dlt <= g.ceps) ? 2.0f * __fsub_rn(vc, R) : 0.0f; }
+            else { vl = l1; dvl = 2.0f * __fsub_rn(v, R); }
+        } else {
+            vl = __fmul_rn(__fsub_rn(v, R), __fsub_rn(v, R));
+            dvl = 2.0f * __fsub_rn(v, R);
+        }
+        // gradients of the loss w.r.t. logits and value
+        const float g_ratio = (!rhs || (ratio >= g.lo && ratio <= g.hi)) ? -An * g.inv_mb : 0.0f;
+        const float g_lr = g_ratio * ratio;
+        const float ec = g.ent_coef * g.inv_mb;
+        float dl0 = g_lr * ((a == 0 ? 1.0f : 0.0f) - p0) + ec * p0 * (ls0 + Hn);
+        float dl1 = g_lr * ((a == 1 ? 1.0f : 0.0f) - p1) + ec * p1 * (ls1 + Hn);
+        float dv = g.value_coef * 0.5f * g.inv_mb * dvl;
+        if (!valid) { dl0 = dl1 = dv = 0.0f; }
+        if (valid) {
+            const float ve = fabsf(__fsub_rn(v, R));
+            m_pl += pl; m_vl += vl; m_h += Hn; m_kl += (ratio - 1.0f) - log_ratio;
+            m_cf += fabsf(ratio - 1.0f) > g.ceps ? 1.0f : 0.0f;
+            m_v += v; m_r += R; m_ve += ve; m_ve2 += ve * ve; m_vemax = fmaxf(m_vemax, ve);
+            m_n += 1.0f;
+        }
+        // ---- head gradients: dWp[k][a] = sum_r hl[r][k] dl[r][a] (lane = k)
+#pragma unroll
+        for (int k = 0; k < H; k++) S.a[WaveStage<H>::at(lane, k)] = valid ? hl[k] : 0.0f;
+        S.l[lane][0] = dl0; S.l[lane][1] = dl1; S.l[lane][2] = dv;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        #pragma unroll 2
+        for (int rr = 0; rr < 64; rr++) {
+            const float q0 = S.l[rr][0], q1 = S.l[rr][1], q2 = S.l[rr][2];
+            gbp0 += q0; gbp1 += q1; gbv += q2;
+            if (lane < H) {
+                const float hv = S.a[WaveStage<H>::at(rr, lane)];
+                gP0 = __builtin_fmaf(hv, q0, gP0);
+                gP1 = __builtin_fmaf(hv, q1, gP1);
+                gV = __builtin_fmaf(hv, q2, gV);
+            }
+        }
+        // ---- dz of the last hidden layer
+        float dz[H];
+#pragma unroll
+        for (int o = 0; o < H; o++) {
+            float s = __builtin_fmaf(dl0, sP[O.wp + o * 2], 0.0f);
+            s = __builtin_fmaf(dl1, sP[O.wp + o * 2 + 1], s);
+            s = __builtin_fmaf(dv, sP[O.wv + o], s);
+            dz[o] = ((m2 >> o) & 1ull) ? s : 0.0f;
+        }
+        __builtin_amdgcn_wave_barrier();
+        float dz1[H];
+        if constexpr (NL == 2) {
+            // dW1[k][o] = sum_r h1[r][k] dz2[r][o]   (lane = o)
+#pragma unroll
+            for (int k = 0; k < H; k++) { S.a[WaveStage<H>::at(lane, k)] = valid ? h1[k] : 0.0f; S.b[WaveStage<H>::at(lane, k)] = dz[k]; }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (lane < H) {
+                #pragma unroll 2
+                for (int rr = 0; rr < 64; rr++) {
+                    const float dzo = S.b[WaveStage<H>::at(rr, lane)];
+                    gb1 += dzo;
+#pragma unroll
+                    for (int k = 0; k < H; k++) gW1[k] = __builtin_fmaf(S.a[WaveStage<H>::at(rr, k)], dzo, gW1[k]);
+                }
+            }
+            // dh1 = dz2 W1^T, dz1 = dh1 * relu'(h1)
+            float prev = 0.0f;
+#pragma unroll
+            for (int k = 0; k < H; k++) {
+                int kofs = O.w1 + k * H;
+                asm volatile("" : "+v"(kofs) : "v"(prev));   // W1 row k fetched one step ahead
+                const float *Wk = sP + kofs;
+                float s = 0.0f;
+#pragma unroll
+                for (int o = 0; o < H; o++) s = __builtin_fmaf(dz[o], Wk[o], s);
+                dz1[k] = ((m1 >> k) & 1ull) ? s : 0.0f;
+                prev = s;
+            }
+            __builtin_amdgcn_wave_barrier();
+        } else {
+#pragma unroll
+            for (int k = 0; k < H; k++) dz1[k] = dz[k];
+        }
+        // dW0[k][o] = sum_r x[r][k] dz1[r][o]   (lane = o)
+#pragma unroll
+        for (int k = 0; k < H; k++) S.b[WaveStage<H>::at(lane, k)] = dz1[k];
+#pragma unroll
+        for (int d = 0; d < 5; d++) S.x[lane][d] = x[d];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane < H) {
+            #pragma unroll 2
+            for (int rr = 0; rr < 64; rr++) {
+                const float dzo = S.b[WaveStage<H>::at(rr, lane)];
+                gb0 += dzo;
+#pragma unroll
+                for (int d = 0; d < 5; d++) gW0[d] = __builtin_fmaf(S.x[rr][d], dzo, gW0[d]);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    // ---- write this wave's partial gradient row
+    float *row = g.slab + (size_t)gwave * (g.np + NUM_M);
+    if (lane < H) {
+#pragma unroll
+        for (int d = 0; d < 5; d++) row[O.w0 + d * H + lane] = gW0[d];
+        row[O.b0 + lane] = gb0;
+        if constexpr (NL == 2) {
+#pragma unroll
+            for (int k = 0; k < H; k++) row[O.w1 + k * H + lane] = gW1[k];
+            row[O.b1 + lane] = gb1;
+        }
+        row[O.wp + lane * 2] = gP0;
+        row[O.wp + lane * 2 + 1] = gP1;
+        row[O.wv + lane] = gV;
+    }
+    if (lane == 0) { row[O.bp] = gbp0; row[O.bp + 1] = gbp1; row[O.bv] = gbv; }
+    const float s_pl = wave_sum(m_pl), s_vl = wave_sum(m_vl), s_h = wave_sum(m_h);
+    const float s_kl = wave_sum(m_kl), s_cf = wave_sum(m_cf), s_v = wave_sum(m_v);
+    const float s_r = wave_sum(m_r), s_ve = wave_sum(m_ve), s_ve2 = wave_sum(m_ve2);
+    const float s_mx = wave_max(m_vemax), s_n = wave_sum(m_n);
+    if (lane == 0) {
+        float *mm = row + g.np;
+        mm[M_PL] = s_pl; mm[M_VL] = s_vl; mm[M_H] = s_h; mm[M_KL] = s_kl; mm[M_CF] = s_cf;
+        mm[M_V] = s_v; mm[M_R] = s_r; mm[M_VE] = s_ve; mm[M_VE2] = s_ve2; mm[M_VEMAX] = s_mx;
+        mm[M_N] = s_n;
+    }
+}
+
+// fixed-order reduction of the wave partials: grad[p] = sum_w slab[w][p]
+__global__ void k_slab_reduce(const float *slab, int rows, int width, float *grad) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= width) return;
+    if (p == width - NUM_M + M_VEMAX) {
+        float m = -INFINITY;
+        for (int w = 0; w < rows; w++) m = fmaxf(m, slab[(size_t)w * width + p]);
+        grad[p] = m;
+        return;
+    }
+    double s = 0.0;
+    for (int w = 0; w < rows; w++) s += (double)slab[(size_t)w * width + p];
+    grad[p] = (float)s;
+}
+
+// per-tensor norm clip + Adam (burn-optim 0.20 restated; one block per tensor)
+struct AdamTensor { int off, len; float c1, c2; };
+struct AdamArgs {
+    float *params, *grad, *m1, *m2;
+    AdamTensor t[32];
+    int nt;
+    float lr, max_norm, eps, inv_world;
+};
+__global__ void __launch_bounds__(256) k_adam(AdamArgs a) {
+    __shared__ double red[256];
+    const AdamTensor T = a.t[blockIdx.x];
+    double ss = 0.0;
+    for (int i = threadIdx.x; i < T.len; i += blockDim.x) {
+        const float gi = a.grad[T.off + i] * a.inv_world;
+        ss += (double)gi * (double)gi;
+    }
+    red[threadIdx.x] = ss;
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+        if (threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+        __syncthreads();
+    }
+    const float norm = (float)sqrt(red[0]);
+    const float scale = norm > a.max_norm ? __fdiv_rn(a.max_norm, norm) : 1.0f;
+    const bool clip = norm > a.max_norm;
+    const float b1 = 0.9f, b2 = 0.999f, f1 = 1.0f - 0.9f, f2 = 1.0f - 0.999f;
+    for (int i = threadIdx.x; i < T.len; i += blockDim.x) {
+        float gi = a.grad[T.off + i] * a.inv_world;
+        if (clip) gi = __fmul_rn(gi, scale);
+        const float m1 = __fadd_rn(__fmul_rn(a.m1[T.off + i], b1), __fmul_rn(gi, f1));
+        const float m2 = __fadd_rn(__fmul_rn(a.m2[T.off + i], b2), __fmul_rn(__fmul_rn(gi, gi), f2));
+        a.m1[T.off + i] = m1;
+        a.m2[T.off + i] = m2;
+        const float m1c = __fdiv_rn(m1, T.c1), m2c = __fdiv_rn(m2, T.c2);
+        const float upd = __fdiv_rn(m1c, __fadd_rn(__fsqrt_rn(m2c), a.eps));
+        a.params[T.off + i] = __fsub_rn(a.params[T.off + i], __fmul_rn(upd, a.lr));
+    }
+}
+
+// explained variance partial sums (ppo.rs:1268-1294)
+__global__ void __launch_bounds__(256) k_ev(size_t n, const float *val, const float *ret, double *part) {
+    __shared__ double sh[4][256];
+    double s[4] = {0, 0, 0, 0};
+    for (size_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const double R = ret[i], res = (double)(ret[i] - val[i]);
+        s[0] += R; s[1] += R * R; s[2] += res; s[3] += res * res;
+    }
+    for (int k = 0; k < 4; k++) sh[k][threadIdx.x] = s[k];
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+        if (threadIdx.x < st)
+            for (int k = 0; k < 4; k++) sh[k][threadIdx.x] += sh[k][threadIdx.x + st];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0)
+        for (int k = 0; k < 4; k++) part[blockIdx.x * 4 + k] = sh[k][0];
+}
+
+// ------------------------------------------------------------- launchers ---
+bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_coef,
+                             double *) {
+    const int h = c->cfg.hidden_size, nl = c->cfg.num_hidden;
+    // advantage stats (2 passes) -> d_mb_stats
+    for (int pass = 0; pass < 2; pass++) {
+        hipLaunchKernelGGL(k_adv_pass, dim3(STAT_BLOCKS), dim3(256), 0, c->stream, c->d_adv, c->d_perm,
+                           start, n, c->d_mb_stats, pass, c->d_red);
+        hipLaunchKernelGGL(k_adv_finalize, dim3(1), dim3(64), 0, c->stream, c->d_red, STAT_BLOCKS, n,
+                           pass, c->d_mb_stats);
+    }
+    MbArgs g;
+    g.obs = c->d_obs; g.logp = c->d_logp; g.adv = c->d_adv; g.ret = c->d_ret; g.val = c->d_val;
+    g.act = c->d_act; g.perm = c->d_perm; g.start = start; g.n = n; g.params = c->d_params;
+    g.mb_stats = c->d_mb_stats; g.slab = c->d_slab; g.np = (int)c->net.n_params;
+    g.lo = (float)(1.0 - c->cfg.clip_epsilon); g.hi = (float)(1.0 + c->cfg.clip_epsilon);
+    g.ceps = (float)c->cfg.clip_epsilon;
+    g.inv_mb = (float)(1.0 / (double)n); g.ent_coef = ent_coef; g.value_coef = (float)c->cfg.value_coef;
+    g.clip_value = c->cfg.clip_value;
+    const int blocks = (int)(c->slab_rows / 4);
+    const size_t params_bytes = ((c->net.n_params + 3) & ~(size_t)3) * sizeof(float);
+#define L(H_, NL_)                                                                                 \
+    if (h == H_ && nl == NL_) {                                                                     \
+        size_t lds = params_bytes + 4 * sizeof(WaveStage<H_>);                                      \
+        hipLaunchKernelGGL((k_minibatch<H_, NL_>), dim3(blocks), dim3(256), lds, c->stream, g);    \
+    } else
+    L(16, 1) L(16, 2) L(32, 1) L(32, 2) L(64, 1) L(64, 2) {
+        c->err = "minibatch kernel: unsupported MLP shape";
+        return BPPO_ERR_UNSUPPORTED;
+    }
+#undef L
+    BPPO_HIP(c, hipGetLastError());
+    const int width = (int)c->net.n_params + NUM_M;
+    hipLaunchKernelGGL(k_slab_reduce, dim3((width + 255) / 256), dim3(256), 0, c->stream, c->d_slab,
+                       (int)c->slab_rows, width, c->d_grad);
+    BPPO_HIP(c, hipGetLastError());
+    return BPPO_OK;
+}
+
+bppo_status launch_adam(bppo_ctx *c, float lr, const float *c1, const float *c2) {
+    AdamArgs a;
+    a.params = c->d_params; a.grad = c->d_grad; a.m1 = c->d_m1; a.m2 = c->d_m2;
+    a.nt = 2 * c->net.n_layers;
+    for (int l = 0; l < c->net.n_layers; l++) {
+        a.t[2 * l] = AdamTensor{(int)c->net.w[l], c->net.in[l] * c->net.out[l], c1[2 * l], c2[2 * l]};
+        a.t[2 * l + 1] = AdamTensor{(int)c->net.b[l], c->net.out[l], c1[2 * l + 1], c2[2 * l + 1]};
+    }
+    a.lr = lr; a.max_norm = (float)c->cfg.max_grad_norm; a.eps = (float)c->cfg.adam_epsilon;
+    a.inv_world = 1.0f / (float)c->world;
+    hipLaunchKernelGGL(k_adam, dim3(a.nt), dim3(256), 0, c->stream, a);
+    BPPO_HIP(c, hipGetLastError());
+    return BPPO_OK;
+}
+
+bppo_status launch_explained_variance(bppo_ctx *c, double *out4) {
+    const size_t n = (size_t)c->T * c->N;
+    hipLaunchKernelGGL(k_ev, dim3(STAT_BLOCKS), dim3(256), 0, c->stream, n, c->d_val, c->d_ret, c->d_red);
+    BPPO_HIP(c, hipMemcpyAsync(c->h_red, c->d_red, sizeof(double) * 4 * STAT_BLOCKS,
+                               hipMemcpyDeviceToHost, c->stream));
+    BPPO_HIP(c, hipStreamSynchronize(c->stream));
+    for (int k = 0; k < 4; k++) out4[k] = 0.0;
+    for (int b = 0; b < STAT_BLOCKS; b++)
+        for (int k = 0; k < 4; k++) out4[k] += c->h_red[b * 4 + k];
+    return BPPO_OK;
+}
+
+}  // namespace bppo

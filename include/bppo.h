@@ -1,0 +1,173 @@
+/*
+ * bppo.h — C-ABI of libbppo.so, the MI355X-native replacement for burn-ppo's
+ * rollout -> GAE -> PPO-update hot path.
+ *
+ * Plain pointers and sizes only.  Host pointers are marked "host"; the few
+ * entry points taking device pointers say so.  Every entry point returns a
+ * bppo_status; the reference's panics (NaN log-probs ppo.rs:363-366, empty
+ * action mask utils.rs:115-123) become status codes, never aborts.
+ * A context is not thread-safe: one context per host thread per GPU.
+ *
+ * Reference surfaces each group replaces (bhansconnect/burn-ppo):
+ *   bppo_create / bppo_vecenv_*   Environment + VecEnv       env.rs:24-173, 281-487
+ *   bppo_params_* / bppo_forward  ActorCriticNetwork         network/mod.rs:53-189
+ *   bppo_collect_rollouts         collect_rollouts           ppo.rs:213-500
+ *   bppo_compute_gae              bootstrap + compute_gae[_multiplayer]
+ *                                                            main.rs:877-947, ppo.rs:1069-1264
+ *   bppo_ppo_update               ppo_update (+ Adam/clip)   ppo.rs:1661-2112, main.rs:264-268
+ *   bppo_gae_device               compute_gae on caller device buffers  ppo.rs:1069-1124
+ *   bppo_rng_*                    the shared &mut StdRng     main.rs:189
+ *   bppo_obs_norm_* / ret_norm_*  ObsNormalizer / ReturnNormalizer  normalization.rs:12-260
+ */
+#ifndef BPPO_H
+#define BPPO_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    BPPO_OK = 0,
+    BPPO_ERR_ARG = 1,          /* bad argument / shape mismatch */
+    BPPO_ERR_NONFINITE = 2,    /* ppo.rs:363-366 "NaN/Inf in log probs" */
+    BPPO_ERR_EMPTY_MASK = 3,   /* utils.rs:115-123 "Empty action mask" */
+    BPPO_ERR_HIP = 4,          /* HIP runtime failure (message in bppo_last_error) */
+    BPPO_ERR_COMM = 5,         /* all-reduce callback failed */
+    BPPO_ERR_UNSUPPORTED = 6   /* configuration not implemented on the device path */
+} bppo_status;
+
+typedef enum { BPPO_ENV_CARTPOLE = 0, BPPO_ENV_CONNECT_FOUR = 1, BPPO_ENV_LIARS_DICE = 2 } bppo_env_kind;
+
+/* Mirrors the subset of config.rs:747-924 the hot path reads. */
+typedef struct {
+    int32_t env_kind;            /* bppo_env_kind */
+    int32_t num_envs;            /* envs on THIS rank */
+    int32_t num_steps;           /* T */
+    int32_t hidden_size, num_hidden, relu;   /* activation == "relu" (else tanh) */
+    int32_t ctde, critic_hidden_size, critic_num_hidden;
+    int32_t num_epochs, num_minibatches;
+    int32_t normalize_obs, normalize_returns, clip_value;
+    double gamma, gae_lambda, clip_epsilon, value_coef, max_grad_norm, adam_epsilon;
+    double target_kl;            /* < 0 : None */
+    double return_clip;          /* ReturnNormalizer clip (config.rs:966-968) */
+    double reward_shaping_coef;  /* Liar's Dice per-round shaping (constant schedule) */
+    uint64_t seed;               /* main StdRng seed (main.rs:189) */
+    uint64_t env_seed_base;      /* env i is seeded env_seed_base + i (main.rs:1964) */
+    uint64_t rng_stream;         /* ChaCha stream id of the main RNG: 0 = reference; rank for W>1 */
+} bppo_config;
+
+typedef struct {
+    float total_reward[4];
+    int32_t length;
+    int32_t env_index;
+    int32_t step;                /* rollout step t at which it ended */
+    int32_t pad;
+} bppo_episode;
+
+typedef struct {
+    int32_t episodes;            /* completed this rollout */
+    float mean_return;           /* of player 0 */
+    float mean_length;
+    int32_t pad;
+    uint64_t rng_word_pos;       /* main RNG position after the rollout */
+} bppo_rollout_info;
+
+/* UpdateMetrics, ppo.rs:1342-1369 */
+typedef struct {
+    float policy_loss, value_loss, entropy, entropy_scaled, approx_kl, clip_fraction;
+    float explained_variance, total_loss, value_mean, returns_mean;
+    float adv_mean_raw, adv_std_raw, adv_min_raw, adv_max_raw;
+    float value_error_mean, value_error_std, value_error_max;
+    float avg_valid_actions, entropy_valid_pct;
+    int32_t num_updates, epochs_run;
+} bppo_update_metrics;
+
+typedef struct bppo_ctx bppo_ctx;
+
+/* ---- lifecycle ---------------------------------------------------------- */
+/* hip_stream may be NULL (the context creates its own).  Resets the VecEnv
+ * (VecEnv::new semantics, env.rs:281-302) and zero-initialises parameters. */
+bppo_status bppo_create(const bppo_config *cfg, int hip_device, void *hip_stream, bppo_ctx **out);
+void bppo_destroy(bppo_ctx *ctx);
+const char *bppo_last_error(const bppo_ctx *ctx);
+const char *bppo_version(void);
+
+/* ---- ActorCritic -------------------------------------------------------- */
+/* flat parameters in Burn record order: per Linear W[in][out] then b[out];
+ * MLP: hidden..., policy head, value head; CTDE: actor hidden..., policy head,
+ * critic hidden..., value head (mlp.rs:47-62, ctde.rs:26-44). */
+size_t bppo_num_params(const bppo_ctx *ctx);
+bppo_status bppo_params_set(bppo_ctx *ctx, const float *host, size_t n);
+bppo_status bppo_params_get(bppo_ctx *ctx, float *host, size_t n);
+/* forward on B rows of host obs [B*obs_dim] (+ priv [B*priv_dim] for CTDE) */
+bppo_status bppo_forward(bppo_ctx *ctx, const float *obs, const float *priv, int32_t B,
+                         float *logits, float *values);
+
+/* ---- main RNG (StdRng = ChaCha12; state = seed key + word position) ------- */
+bppo_status bppo_rng_get(bppo_ctx *ctx, uint64_t *word_pos);
+bppo_status bppo_rng_set(bppo_ctx *ctx, uint64_t word_pos);
+
+/* ---- VecEnv ------------------------------------------------------------- */
+bppo_status bppo_vecenv_reset(bppo_ctx *ctx);  /* VecEnv::new: factory(i) + reset() */
+/* current state: obs [N*obs_dim] raw, players [N], masks [N*A] (0/1), priv [N*priv]; any may be NULL */
+bppo_status bppo_vecenv_observe(bppo_ctx *ctx, float *obs, int32_t *players, uint8_t *masks,
+                                float *priv);
+/* VecEnv::step (env.rs:400-487): actions [N]; rewards [N*P]; dones [N];
+ * completed episodes in env order (up to cap), count in *n_eps */
+bppo_status bppo_vecenv_step(bppo_ctx *ctx, const int32_t *actions, float *obs, float *rewards,
+                             uint8_t *dones, bppo_episode *eps, int32_t cap, int32_t *n_eps);
+bppo_status bppo_vecenv_set_step(bppo_ctx *ctx, uint64_t global_step);
+
+/* ---- normalizers (f64 state, normalization.rs) ------------------------ */
+bppo_status bppo_obs_norm_get(bppo_ctx *ctx, double *mean, double *m2, double *count);
+bppo_status bppo_obs_norm_set(bppo_ctx *ctx, const double *mean, const double *m2, double count);
+/* mvc = {mean, M2, count}; returns = per (env, player) rolling returns [N*P] */
+bppo_status bppo_ret_norm_get(bppo_ctx *ctx, double *mvc, double *returns);
+bppo_status bppo_ret_norm_set(bppo_ctx *ctx, const double *mvc, const double *returns);
+
+/* ---- the hot path ------------------------------------------------------- */
+bppo_status bppo_collect_rollouts(bppo_ctx *ctx, bppo_rollout_info *info);
+bppo_status bppo_rollout_episodes(bppo_ctx *ctx, bppo_episode *eps, int32_t cap, int32_t *n);
+bppo_status bppo_compute_gae(bppo_ctx *ctx);
+bppo_status bppo_ppo_update(bppo_ctx *ctx, double lr, double ent_coef, bppo_update_metrics *m);
+
+/* multi-GPU: called once per minibatch with the flat f32 gradient (+ metric
+ * partials) in DEVICE memory, on the context's stream, before clip + Adam.
+ * The callback must leave the SUM over ranks in place; the context divides
+ * by world_size.  (RCCL all-reduce over xGMI, one per minibatch.) */
+typedef int (*bppo_allreduce_fn)(float *device_buf, size_t n, void *user);
+bppo_status bppo_set_allreduce(bppo_ctx *ctx, bppo_allreduce_fn fn, void *user, int32_t world_size);
+
+/* parity hooks: export / import a RolloutBuffer field.  names: "obs", "priv",
+ * "actions" (i32), "rewards", "dones", "values", "log_probs", "advantages",
+ * "returns", "players" (i32), "all_rewards", "masks", "last_v_pp", "perm" (u32,
+ * last epoch's shuffled indices) */
+bppo_status bppo_buffer_get(bppo_ctx *ctx, const char *name, void *host, size_t bytes);
+bppo_status bppo_buffer_set(bppo_ctx *ctx, const char *name, const void *host, size_t bytes);
+
+/* ---- standalone device kernels on caller-owned DEVICE buffers ------------ */
+/* compute_gae (ppo.rs:1069-1124) on [T,N] device arrays; stream may be NULL */
+bppo_status bppo_gae_device(const float *rewards, const float *dones, const float *values,
+                            const float *last_values, int32_t T, int32_t N, float gamma,
+                            float lambda, float *advantages, float *returns, void *hip_stream);
+/* compute_gae_multiplayer (ppo.rs:1140-1264): all_rewards [T,N,P], players [T,N] i32,
+ * last_v_pp [N,P] */
+bppo_status bppo_gae_mp_device(const float *all_rewards, const int32_t *players,
+                               const float *dones, const float *values, const float *last_v_pp,
+                               int32_t T, int32_t N, int32_t P, float gamma, float lambda,
+                               float *advantages, float *returns, void *hip_stream);
+
+/* device timing of the last call of each phase kernel (ms), for bench.py's roofline */
+bppo_status bppo_last_kernel_ms(bppo_ctx *ctx, const char *kernel, float *ms);
+
+/* libm parity hook: which 0 = logf, 1 = sinf, 2 = cosf, 3 = gumbel(-ln(-ln u));
+ * device = 0 runs the host build of the same source, 1 runs the HIP kernel */
+bppo_status bppo_debug_libm(int32_t which, int32_t device, const float *x, float *y, size_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

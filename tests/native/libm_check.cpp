@@ -12,6 +12,14 @@ size_t mismatch_logf(const float *x, size_t n, float *ref, float *got) {
     }
     return bad;
 }
+size_t mismatch_expf(const float *x, size_t n, float *ref, float *got) {
+    size_t bad = 0;
+    for (size_t i = 0; i < n; i++) {
+        ref[i] = expf(x[i]); got[i] = bppo_math::expf_glibc(x[i]);
+        bad += bppo_math::asuint(ref[i]) != bppo_math::asuint(got[i]);
+    }
+    return bad;
+}
 size_t mismatch_sincos(const float *x, size_t n, float *rs, float *gs, float *rc, float *gc) {
     size_t bad = 0;
     for (size_t i = 0; i < n; i++) {

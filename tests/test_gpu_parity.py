@@ -1,0 +1,244 @@
+"""Parity of the HIP path (through the C-ABI, libbppo.so) against the CPU
+oracle on identical seeds.  Bit-exact for integer/index work (actions, dones,
+episode boundaries, RNG positions, shuffled indices) and for every value the
+reference computes element-wise in f32 (env transitions, observations, Gumbel
+sampling, log-probs, values, GAE); reductions (normalizer stats, advantage
+stats, gradients) within the stated tolerances."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import bppo
+import bppo._lib as L
+import oracle_ffi as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _torch():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a visible MI355X"
+    return torch
+
+
+# ----------------------------------------------------------------- libm ---
+@pytest.mark.parametrize("which", [0, 1, 2, 3, 4])
+def test_device_libm_matches_host(which):
+    rng = np.random.default_rng(which)
+    if which == 3:   # every Gumbel input u
+        k = np.arange(1 << 23, dtype=np.uint32)
+        v = (k | 0x3F800000).view(np.float32) - np.float32(1)
+        x = (v * np.float32(1.0) + np.float32(1e-10)).astype(np.float32)
+    elif which in (1, 2):
+        x = np.concatenate([rng.uniform(-0.5, 0.5, 2_000_000), rng.uniform(-200, 200, 500_000)]).astype(np.float32)
+    elif which == 4:
+        x = rng.uniform(-100, 20, 2_000_000).astype(np.float32)
+    else:
+        x = rng.integers(0, 0x7F800000, 2_000_000, dtype=np.uint32).view(np.float32)
+    yh = np.zeros_like(x)
+    yd = np.zeros_like(x)
+    assert L.lib().bppo_debug_libm(which, 0, x.ctypes.data, yh.ctypes.data, x.size) == 0
+    assert L.lib().bppo_debug_libm(which, 1, x.ctypes.data, yd.ctypes.data, x.size) == 0
+    assert np.array_equal(yh.view(np.uint32), yd.view(np.uint32))
+
+
+# ------------------------------------------------------------------ GAE ---
+@pytest.mark.parametrize("T,N", [(1, 1), (7, 3), (128, 4096), (64, 1000)])
+def test_gae_device_bit_exact(T, N):
+    torch = _torch()
+    rng = np.random.default_rng(T * 1000 + N)
+    r = (rng.random((T, N)) < 0.98).astype(np.float32)
+    d = (rng.random((T, N)) < 0.01).astype(np.float32)
+    v = rng.normal(50, 20, (T, N)).astype(np.float32)
+    lv = rng.normal(50, 20, N).astype(np.float32)
+    adv_o, ret_o = O.compute_gae(r, d, v, lv, 0.99, 0.95)
+    dev = [torch.from_numpy(a).cuda() for a in (r, d, v, lv)]
+    adv = torch.empty((T, N), device="cuda")
+    ret = torch.empty((T, N), device="cuda")
+    st = L.lib().bppo_gae_device(*[t.data_ptr() for t in dev], T, N, 0.99, 0.95, adv.data_ptr(),
+                                 ret.data_ptr(), None)
+    assert st == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(adv.cpu().numpy().view(np.uint32), adv_o.view(np.uint32))
+    assert np.array_equal(ret.cpu().numpy().view(np.uint32), ret_o.view(np.uint32))
+
+
+@pytest.mark.parametrize("P", [2, 3, 4])
+def test_gae_multiplayer_device_bit_exact(P):
+    torch = _torch()
+    T, N = 64, 2048
+    rng = np.random.default_rng(P)
+    pl = rng.integers(0, P, (T, N)).astype(np.int32)
+    d = (rng.random((T, N)) < 0.05).astype(np.float32)
+    ar = np.where(rng.random((T, N, P)) < 0.1, rng.choice([-1.0, 1.0, 0.33, -0.33], (T, N, P)), 0.0).astype(np.float32)
+    v = rng.normal(0, 0.5, (T, N)).astype(np.float32)
+    lvpp = rng.normal(0, 0.5, (N, P)).astype(np.float32)
+    adv_o, ret_o = O.compute_gae_mp(ar, pl, d, v, lvpp, 0.97, 0.90)
+    dev = [torch.from_numpy(a).cuda() for a in (ar, pl, d, v, lvpp)]
+    adv = torch.empty((T, N), device="cuda")
+    ret = torch.empty((T, N), device="cuda")
+    st = L.lib().bppo_gae_mp_device(*[t.data_ptr() for t in dev], T, N, P, 0.97, 0.90, adv.data_ptr(),
+                                    ret.data_ptr(), None)
+    assert st == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(adv.cpu().numpy().view(np.uint32), adv_o.view(np.uint32))
+
+
+def test_gae_mp_known_answers_on_device():
+    """ppo.rs:2579-2635 same_player_across_boundary through the device kernel."""
+    torch = _torch()
+    d = np.array([[0.0], [1.0], [1.0]], np.float32)
+    pl = np.zeros((3, 1), np.int32)
+    ar = np.array([[[0.0, 0.0]], [[-1.0, 0.0]], [[10.0, 0.0]]], np.float32)
+    v = np.array([[0.0], [0.0], [5.0]], np.float32)
+    lv = np.array([[5.0, 0.0]], np.float32)
+    dev = [torch.from_numpy(a).cuda() for a in (ar, pl, d, v, lv)]
+    adv = torch.empty((3, 1), device="cuda"); ret = torch.empty((3, 1), device="cuda")
+    assert L.lib().bppo_gae_mp_device(*[t.data_ptr() for t in dev], 3, 1, 2, 0.99, 0.95, adv.data_ptr(),
+                                      ret.data_ptr(), None) == 0
+    a = adv.cpu().numpy().reshape(-1)
+    assert abs(a[2] - 5.0) < 1e-5 and abs(a[1] + 1.0) < 1e-5 and abs(a[0] + 0.99 * 0.95) < 1e-5
+
+
+# --------------------------------------------------------------- VecEnv ---
+def test_vecenv_reset_and_steps_match_oracle():
+    N = 256
+    cfg = bppo.make_config("cartpole", num_envs=N, num_steps=8)
+    ctx = bppo.Context(cfg)
+    ve = bppo.VecEnv.new(ctx)
+    ov = O.lib().or_vecenv_new(O.ENV_CARTPOLE, N, cfg["seed"])
+    obs_o = np.zeros(N * 5, np.float32)
+    O.lib().or_vecenv_get_obs(ov, obs_o)
+    assert np.array_equal(ve.get_observations(), obs_o)
+    rng = np.random.default_rng(0)
+    rw = np.zeros(N, np.float32); dn = np.zeros(N, np.uint8)
+    eps = (O.Episode * N)()
+    n_done = 0
+    for t in range(600):
+        a = rng.integers(0, 2, N).astype(np.int32)
+        o, r, d, ep = ve.step(a)
+        O.lib().or_vecenv_step(ov, a, obs_o, rw, dn, eps, N)
+        assert np.array_equal(o, obs_o), t
+        assert np.array_equal(r.reshape(-1), rw), t
+        assert np.array_equal(d, dn.astype(bool)), t
+        n_done += int(d.sum())
+    assert n_done > 100
+    O.lib().or_vecenv_free(ov)
+    ctx.close()
+
+
+# -------------------------------------------------------------- rollout ---
+def _pair(N, T, seed=42, **kw):
+    cfg = bppo.make_config("cartpole", num_envs=N, num_steps=T, seed=seed, **kw)
+    params = bppo.orthogonal_init(cfg, seed=1)
+    tr = bppo.Trainer(cfg, params=params)
+    ocfg = O.train_cfg(num_envs=N, num_steps=T, seed=seed, lr=1e-3,
+                       hidden=cfg["hidden_size"], num_hidden=cfg["num_hidden"],
+                       num_epochs=cfg["num_epochs"], num_minibatches=cfg["num_minibatches"])
+    ot = O.Trainer(ocfg, params)
+    return cfg, tr, ot
+
+
+def _cmp_rollout(tr, ot, exact_rewards=False):
+    b = tr.buffer
+    assert np.array_equal(b.actions.reshape(-1), ot.buffer("actions", np.int32))
+    assert np.array_equal(b.dones.reshape(-1), ot.buffer("dones"))
+    assert np.array_equal(b.observations.reshape(-1).view(np.uint32), ot.buffer("obs").view(np.uint32))
+    assert np.array_equal(b.values.reshape(-1).view(np.uint32), ot.buffer("values").view(np.uint32))
+    assert np.array_equal(b.log_probs.reshape(-1).view(np.uint32), ot.buffer("log_probs").view(np.uint32))
+    rg, ro = b.rewards.reshape(-1), ot.buffer("rewards")
+    if exact_rewards:
+        assert np.array_equal(rg, ro)
+    # return normaliser: f64 Chan-merge scan vs sequential Welford -> f32 results
+    # identical except for rare last-ulp ties
+    np.testing.assert_allclose(rg, ro, rtol=2e-7, atol=0)
+    assert tr.ctx.rng_pos() == ot.rng_pos()
+
+
+@pytest.mark.parametrize("N,T", [(8, 128), (256, 64)])
+def test_first_rollout_bit_exact(N, T):
+    cfg, tr, ot = _pair(N, T)
+    bppo.collect_rollouts(tr.ctx)
+    ot.collect()
+    _cmp_rollout(tr, ot)
+    m, v, c = tr.ctx.obs_norm()
+    mo, vo, co = ot.obs_norm_state(5)
+    assert c == co
+    np.testing.assert_allclose(m, mo, rtol=1e-12, atol=1e-15)
+    np.testing.assert_allclose(v, vo, rtol=1e-10)
+    bppo.compute_gae(tr.ctx)
+    ot.gae()
+    np.testing.assert_allclose(tr.buffer.advantages.reshape(-1), ot.buffer("advantages"), rtol=1e-5, atol=1e-6)
+    tr.close(); ot.close()
+
+
+def test_update_matches_oracle_and_rng_chain_exact():
+    N, T = 64, 32
+    cfg, tr, ot = _pair(N, T, num_minibatches=4, num_epochs=2)
+    bppo.collect_rollouts(tr.ctx); ot.collect()
+    bppo.compute_gae(tr.ctx); ot.gae()
+    # identical GAE inputs for the update comparison
+    tr.ctx.set_buffer("advantages", ot.buffer("advantages"))
+    tr.ctx.set_buffer("returns", ot.buffer("returns"))
+    m = bppo.ppo_update(tr.ctx, 1e-3, 0.01)
+    om = ot.update()
+    assert tr.ctx.rng_pos() == ot.rng_pos()           # shuffle chain consumed the same words
+    # last epoch's permutation == oracle Fisher-Yates from the same stream position
+    perm = tr.ctx.buffer("perm", np.uint32)
+    p_words = ot.rng_pos()
+    assert sorted(perm.tolist()) == list(range(N * T))
+    for k in ("policy_loss", "value_loss", "entropy", "approx_kl", "clip_fraction"):
+        assert abs(m[k] - om[k]) <= 1e-5 + 1e-4 * abs(om[k]), (k, m[k], om[k])
+    pg = tr.model.get_params()
+    po = ot.params()
+    np.testing.assert_allclose(pg, po, rtol=1e-4, atol=2e-5)
+    tr.close(); ot.close()
+
+
+def test_shuffle_permutation_bit_exact():
+    N, T = 50, 20
+    cfg, tr, ot = _pair(N, T, num_minibatches=3, num_epochs=1)
+    bppo.collect_rollouts(tr.ctx); ot.collect()
+    bppo.compute_gae(tr.ctx); ot.gae()
+    start = tr.ctx.rng_pos()
+    bppo.ppo_update(tr.ctx, 1e-3, 0.01)
+    perm = tr.ctx.buffer("perm", np.uint32)
+    r = O.Rng()
+    O.lib().or_rng_seed_u64(C.byref(r), cfg["seed"])
+    r.word_pos = start
+    ref = np.arange(N * T, dtype=np.uint32)
+    O.lib().or_shuffle_u32(C.byref(r), ref, ref.size)
+    assert np.array_equal(perm, ref)
+    assert tr.ctx.rng_pos() == r.word_pos
+    tr.close(); ot.close()
+
+
+def test_second_rollout_bit_exact_given_oracle_state():
+    """Layered parity: after one update, inject the oracle's params and
+    normaliser state; the next rollout is again bit-identical."""
+    N, T = 128, 64
+    cfg, tr, ot = _pair(N, T)
+    bppo.collect_rollouts(tr.ctx); ot.collect()
+    bppo.compute_gae(tr.ctx); ot.gae()
+    bppo.ppo_update(tr.ctx, 1e-3, 0.01); ot.update()
+    assert tr.ctx.rng_pos() == ot.rng_pos()
+    tr.model.set_params(ot.params())
+    m, v, c = ot.obs_norm_state(5)
+    tr.ctx.set_obs_norm(m, v, c)
+    mvc = ot.ret_norm_state()
+    tr.ctx.set_ret_norm(mvc, tr.ctx.ret_norm()[1])
+    bppo.collect_rollouts(tr.ctx); ot.collect()
+    _cmp_rollout(tr, ot)
+    tr.close(); ot.close()
+
+
+def test_training_improves_cartpole_return():
+    cfg = bppo.make_config("cartpole", num_envs=1024, num_steps=128)
+    tr = bppo.Trainer(cfg, init_seed=3)
+    rets = []
+    for _ in range(12):
+        m = tr.train_update()
+        rets.append(m["mean_return"])
+    tr.close()
+    assert rets[-1] > 3 * max(rets[0], 10.0), rets

@@ -1,4 +1,4 @@
-"""The product's glibc logf/sinf/cosf restatement (burn-ppo_amd/csrc/bppo_math.h)
+"""The product's glibc logf/sinf/cosf/expf restatement (burn-ppo_amd/csrc/bppo_math.h)
 against the platform glibc the reference's Rust code calls (utils.rs:25,
 cartpole.rs:51-52).  A one-off exhaustive run over every finite float found zero
 mismatches; this test re-checks every Gumbel input plus dense and
@@ -24,6 +24,8 @@ def chk(tmp_path_factory):
     f32 = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
     L.mismatch_logf.restype = C.c_size_t
     L.mismatch_logf.argtypes = [f32, C.c_size_t, f32, f32]
+    L.mismatch_expf.restype = C.c_size_t
+    L.mismatch_expf.argtypes = [f32, C.c_size_t, f32, f32]
     L.mismatch_sincos.restype = C.c_size_t
     L.mismatch_sincos.argtypes = [f32, C.c_size_t, f32, f32, f32, f32]
     L.mismatch_gumbel_all.restype = C.c_size_t
@@ -69,3 +71,21 @@ def test_sincos_wide_samples(chk):
     x = bits.view(np.float32)
     assert _run_sincos(chk, x) == 0
     assert _run_sincos(chk, -x) == 0
+
+
+def test_expf_samples(chk):
+    rng = np.random.default_rng(2)
+    bits = rng.integers(0, 2**32, size=4_000_000, dtype=np.uint64).astype(np.uint32)
+    x = bits.view(np.float32)
+    x = x[~np.isnan(x)]
+    xs = np.ascontiguousarray(x)
+    r = np.empty_like(xs); g = np.empty_like(xs)
+    assert chk.mismatch_expf(xs, xs.size, r, g) == 0
+    # the two inputs where glibc's contracted reduction is not correctly rounded
+    hard = np.array([float.fromhex("0x1.04845ep+5"), float.fromhex("-0x1.f8cbb2p+5")], np.float32)
+    r = np.empty_like(hard); g = np.empty_like(hard)
+    assert chk.mismatch_expf(hard, 2, r, g) == 0
+    # log-softmax range
+    dense = np.linspace(-30, 0, 1_000_001, dtype=np.float32)
+    r = np.empty_like(dense); g = np.empty_like(dense)
+    assert chk.mismatch_expf(dense, dense.size, r, g) == 0
