@@ -129,7 +129,7 @@ struct bppo_ctx {
     void *allreduce_user = nullptr;
     int world = 1;
     // timing
-    hipEvent_t ev[8][2];
+    hipEvent_t ev[8][2] = {};
     float last_ms[8] = {0};
     int collected = 0, gae_done = 0;
 };
