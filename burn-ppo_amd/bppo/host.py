@@ -4,6 +4,7 @@ learning-rate schedule (schedule.rs:54-78), orthogonal init (mlp.rs:16-38)."""
 import numpy as np
 
 from . import _lib as L
+from .dist import shard
 
 
 def minibatch_sizes(batch_size, num_minibatches):
@@ -90,8 +91,7 @@ def to_struct(c, rank=0, world=1, envs_per_rank=None):
     s.target_kl = -1.0 if c["target_kl"] is None else float(c["target_kl"])
     s.seed = c["seed"]
     # W > 1: global env index = rank * n + i; main RNG stream = rank
-    s.env_seed_base = c["seed"] + rank * n
-    s.rng_stream = rank if world > 1 else 0
+    s.env_seed_base, s.rng_stream = shard(c, rank, world, n)
     return s
 
 

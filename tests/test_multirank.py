@@ -1,0 +1,107 @@
+"""N>1 data-parallel path: world_size-2 ranks.
+
+CPU (gloo): the all-reduce callback libbppo calls once per minibatch leaves the
+SUM over ranks in place, and the per-rank sharding (env seeds, RNG streams).
+GPU (gloo, host-staged, both ranks on cuda:0): two ranks fed IDENTICAL shards
+must apply the same step as one rank alone — x+x then x0.5 is exact in f32 — so
+their parameters equal the single-rank run bit for bit, and the two ranks stay
+in sync.  This pins the callback placement, the 1/world scaling before clip +
+Adam, and the metric-partial reduction."""
+import ctypes as C
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+import bppo
+from bppo.dist import make_allreduce, shard
+from bppo.host import to_struct
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _init(rank, world, port):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    return dist
+
+
+def _cpu_worker(rank, world, port, q):
+    dist = _init(rank, world, port)
+    try:
+        fn = make_allreduce(dist, mode="host")
+        n = 4739 + 11
+        buf = (np.arange(n, dtype=np.float32) * (rank + 1)).astype(np.float32)
+        fn(buf.ctypes.data, n)
+        cfg = bppo.make_config("cartpole", num_envs=64)
+        s = to_struct(cfg, rank, world, 64)
+        q.put((rank, buf.copy(), s.env_seed_base, s.rng_stream))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_allreduce_callback_and_sharding_gloo():
+    world, port = 2, _port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_cpu_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    n = res[0][1].size
+    want = np.arange(n, dtype=np.float32) * 3
+    for rank, buf, seed_base, stream in res:
+        assert np.array_equal(buf, want)
+        assert seed_base == 42 + rank * 64
+        assert stream == rank
+    assert shard(bppo.make_config("cartpole"), 0, 1, 64) == (42, 0)
+
+
+def _gpu_worker(rank, world, port, q, updates):
+    dist = _init(rank, world, port)
+    try:
+        cfg = bppo.make_config("cartpole", num_envs=256, num_steps=32)
+        # identical shards on purpose: rank=0 seeding for both processes
+        tr = bppo.Trainer(cfg, device=0, init_seed=3)
+        tr.ctx.set_allreduce(make_allreduce(dist, mode="host_staged"), world)
+        ms = [tr.train_update() for _ in range(updates)]
+        q.put((rank, tr.model.get_params(), ms[-1]["policy_loss"]))
+        tr.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_ranks_identical_shards_match_single_rank():
+    updates = 3
+    cfg = bppo.make_config("cartpole", num_envs=256, num_steps=32)
+    solo = bppo.Trainer(cfg, device=0, init_seed=3)
+    ms = [solo.train_update() for _ in range(updates)]
+    p_solo = solo.model.get_params()
+    solo.close()
+    world, port = 2, _port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gpu_worker, args=(r, world, port, q, updates)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert np.array_equal(res[0][1], res[1][1]), "ranks diverged"
+    assert np.array_equal(res[0][1], p_solo)
+    assert abs(res[0][2] - ms[-1]["policy_loss"]) <= 1e-6 + 1e-5 * abs(ms[-1]["policy_loss"])
