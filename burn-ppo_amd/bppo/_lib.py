@@ -67,7 +67,8 @@ EXPORTS = (
     "bppo_obs_norm_get", "bppo_obs_norm_set", "bppo_ret_norm_get", "bppo_ret_norm_set",
     "bppo_collect_rollouts", "bppo_rollout_episodes", "bppo_compute_gae", "bppo_ppo_update",
     "bppo_set_allreduce", "bppo_buffer_get", "bppo_buffer_set", "bppo_gae_device",
-    "bppo_gae_mp_device", "bppo_last_kernel_ms", "bppo_debug_libm",
+    "bppo_gae_mp_device", "bppo_last_kernel_ms", "bppo_debug_libm", "bppo_debug_shuffle_chain",
+    "bppo_debug_fisher_yates",
 )
 
 _lib = None
@@ -116,6 +117,8 @@ def lib():
                                      vp]),
         "bppo_last_kernel_ms": (i32, [vp, C.c_char_p, fp]),
         "bppo_debug_libm": (i32, [i32, i32, vp, vp, sz]),
+        "bppo_debug_shuffle_chain": (i32, [u64, u64, u64, C.c_uint32, vp, C.POINTER(u64)]),
+        "bppo_debug_fisher_yates": (i32, [i32, vp, C.c_uint32, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

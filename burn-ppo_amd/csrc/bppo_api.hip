@@ -36,96 +36,6 @@ NetLayout make_layout(const bppo_config &c, int obs_dim, int priv_dim, int act_d
     return L;
 }
 
-// ------------------------------------------------------------ shuffle chain --
-// rand 0.8.5 shuffle: for i in (1..n).rev(): j = gen_range(0..i+1) with
-// UniformInt<u32>: zone = (range << lz(range)) - 1, draw until lo(w*range) <= zone.
-static void host_chacha_words(const Key8 &key, uint64_t stream, uint64_t pos, uint32_t *out,
-                              size_t n) {
-    // block-parallel fill: every ChaCha block is independent
-    const uint64_t b0 = pos >> 4, b1 = (pos + n + 15) >> 4;
-    const int64_t nb = (int64_t)(b1 - b0);
-    const int nt = (int)std::min<int64_t>(8, std::max<int64_t>(1, nb / 4096));
-    auto work = [&](int tid) {
-        for (int64_t bi = tid; bi < nb; bi += nt) {
-            uint32_t blk[16];
-            chacha12_block(key, b0 + (uint64_t)bi, stream, blk);
-            for (int w = 0; w < 16; w++) {
-                const uint64_t p = ((b0 + (uint64_t)bi) << 4) + w;
-                if (p >= pos && p < pos + n) out[p - pos] = blk[w];
-            }
-        }
-    };
-    std::vector<std::thread> ths;
-    for (int t = 1; t < nt; t++) ths.emplace_back(work, t);
-    work(0);
-    for (auto &t : ths) t.join();
-}
-
-void ShuffleEngine::start(const Key8 &k, uint64_t strm, uint64_t pos, uint32_t n_, int epochs_) {
-    join();
-    key = k; stream = strm; start_pos = pos; n = n_; epochs = epochs_;
-    ready = 0;
-    end_pos.assign(epochs, 0);
-    const size_t need = (size_t)epochs * n;
-    if (need > J_cap) {
-        if (J) (void)hipHostFree(J);
-        J = nullptr;
-        if (hipHostMalloc((void **)&J, need * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
-            J = (uint32_t *)malloc(need * sizeof(uint32_t));
-        }
-        J_cap = need;
-    }
-    running = true;
-    th = std::thread([this]() {
-        uint64_t pos = start_pos;
-        std::vector<uint32_t> words;
-        for (int e = 0; e < epochs; e++) {
-            uint32_t *Je = J + (size_t)e * n;
-            if (n >= 2) {
-                // generous word window; refilled if a long rejection run exhausts it
-                size_t cap = (size_t)n + n / 2 + 4096, used = 0;
-                words.resize(cap);
-                host_chacha_words(key, stream, pos, words.data(), cap);
-                for (uint32_t i = n - 1; i >= 1; i--) {
-                    const uint32_t range = i + 1;
-                    const uint32_t zone = (range << __builtin_clz(range)) - 1u;
-                    for (;;) {
-                        if (used == cap) {
-                            pos += cap; used = 0;
-                            host_chacha_words(key, stream, pos, words.data(), cap);
-                        }
-                        const uint64_t m = (uint64_t)words[used++] * range;
-                        if ((uint32_t)m <= zone) { Je[i] = (uint32_t)(m >> 32); break; }
-                    }
-                }
-                pos += used;
-                Je[0] = 0;
-            }
-            {
-                std::lock_guard<std::mutex> lk(mu);
-                end_pos[e] = pos;
-                ready = e + 1;
-            }
-            cv.notify_all();
-        }
-    });
-}
-
-void ShuffleEngine::wait_epoch(int e) {
-    std::unique_lock<std::mutex> lk(mu);
-    cv.wait(lk, [&] { return ready > e; });
-}
-
-void ShuffleEngine::join() {
-    if (th.joinable()) th.join();
-    running = false;
-}
-
-ShuffleEngine::~ShuffleEngine() {
-    join();
-    if (J) (void)hipHostFree(J);
-}
-
 // ----------------------------------------------------------- libm check ----
 __global__ void k_libm(int which, const float *x, float *y, size_t n) {
     size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -236,15 +146,11 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     TRY(dalloc(c, &c->d_eps, (size_t)c->eps_cap));
     TRY(dalloc(c, &c->d_ep_count, 1));
     TRY(dalloc(c, &c->d_err, 1));
-    TRY(dalloc(c, &c->d_J, TN));
     TRY(dalloc(c, &c->d_perm, TN));
-    TRY(dalloc(c, &c->d_R, TN));
-    TRY(dalloc(c, &c->d_R2, TN));
-    TRY(dalloc(c, &c->d_res, TN));
-    TRY(dalloc(c, &c->d_cnt, 2));
+    TRY(dalloc(c, &c->d_fy, 4 * TN));
+    TRY(dalloc(c, &c->d_scan, TN / 8192 + 2));
     TRY(dalloc(c, &c->d_red, 4 * 1024 + 64));
     TRY(dalloc(c, &c->d_mb_stats, 8));
-    BPPO_HIP(c, hipHostMalloc((void **)&c->h_cnt, 16, hipHostMallocDefault));
     BPPO_HIP(c, hipHostMalloc((void **)&c->h_red, sizeof(double) * (4 * 1024 + 64), hipHostMallocDefault));
     for (int i = 0; i < 8; i++) {
         BPPO_HIP(c, hipEventCreate(&c->ev[i][0]));
@@ -252,6 +158,7 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     }
     c->rng_key = seed_key(cfg->seed);
     c->rng_pos = 0;
+    TRY(c->shuf.init(dev, c->rng_key, cfg->rng_stream, (uint32_t)TN, cfg->num_epochs, c->err));
     c->on_mean.assign(c->D, 0.0); c->on_m2.assign(c->D, 0.0); c->on_count = 0;
     TRY(launch_cartpole_reset(c));
     BPPO_HIP(c, hipStreamSynchronize(c->stream));
@@ -269,16 +176,15 @@ extern "C" bppo_status bppo_create(const bppo_config *cfg, int hip_device, void 
 
 extern "C" void bppo_destroy(bppo_ctx *c) {
     if (!c) return;
-    c->shuf.join();
+    c->shuf.shutdown();
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void *ptrs[] = {c->d_params, c->d_m1, c->d_m2, c->d_grad, c->d_slab, c->d_cp, c->d_steps,
                     c->d_env_pos, c->d_ep_ret, c->d_ep_len, c->d_obs, c->d_rew, c->d_rew_raw,
                     c->d_done, c->d_val, c->d_logp, c->d_adv, c->d_ret, c->d_act, c->d_X, c->d_on,
                     c->d_obs_part, c->d_rn_returns, c->d_rn_stats, c->d_scan_agg, c->d_last_v,
-                    c->d_eps, c->d_ep_count, c->d_err, c->d_J, c->d_perm, c->d_R, c->d_R2,
-                    c->d_res, c->d_cnt, c->d_red, c->d_mb_stats};
+                    c->d_eps, c->d_ep_count, c->d_err, c->d_perm, c->d_fy, c->d_scan,
+                    c->d_red, c->d_mb_stats};
     for (void *p : ptrs) if (p) (void)hipFree(p);
-    if (c->h_cnt) (void)hipHostFree(c->h_cnt);
     if (c->h_red) (void)hipHostFree(c->h_red);
     for (int i = 0; i < 8; i++) {
         if (c->ev[i][0]) (void)hipEventDestroy(c->ev[i][0]);
@@ -330,8 +236,7 @@ extern "C" bppo_status bppo_rng_get(bppo_ctx *c, uint64_t *p) {
 }
 extern "C" bppo_status bppo_rng_set(bppo_ctx *c, uint64_t p) {
     if (!c) return BPPO_ERR_ARG;
-    c->shuf.join();
-    c->shuffle_started = 0;
+    c->shuf_slot = -1;
     c->rng_pos = p;
     return BPPO_OK;
 }
@@ -448,7 +353,6 @@ static void tm_read(bppo_ctx *c, int slot) {
 // collect_rollouts (ppo.rs:213-500)
 extern "C" bppo_status bppo_collect_rollouts(bppo_ctx *c, bppo_rollout_info *info) {
     if (!c) return BPPO_ERR_ARG;
-    c->shuf.join();
     const size_t TN = (size_t)c->T * c->N;
     BPPO_HIP(c, hipMemsetAsync(c->d_ep_count, 0, 4, c->stream));
     BPPO_HIP(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
@@ -457,9 +361,8 @@ extern "C" bppo_status bppo_collect_rollouts(bppo_ctx *c, bppo_rollout_info *inf
     TRY(launch_cartpole_rollout(c, base, nullptr, nullptr, c->cfg.normalize_obs));
     tm_end(c, TM_ROLLOUT);
     c->rng_pos = base + TN * (uint64_t)c->A;   // one word per (env, action) per step
-    // shuffle chain for the coming update starts now (overlaps the GPU work)
-    c->shuf.start(c->rng_key, c->cfg.rng_stream, c->rng_pos, (uint32_t)TN, c->cfg.num_epochs);
-    c->shuffle_started = 1;
+    // this update's shuffles start here; the engine usually began them already
+    c->shuf_slot = c->shuf.ensure(c->rng_pos);
     if (c->cfg.normalize_obs) TRY(launch_obs_norm_merge(c));       // ppo.rs:495-497
     tm_begin(c, TM_RETNORM);
     if (c->cfg.normalize_returns) TRY(launch_return_norm(c));      // ppo.rs:390-408
@@ -529,11 +432,8 @@ extern "C" bppo_status bppo_compute_gae(bppo_ctx *c) {
 // ppo_update (ppo.rs:1661-2112)
 extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, bppo_update_metrics *m) {
     if (!c || !c->gae_done) { if (c) c->err = "ppo_update before compute_gae"; return BPPO_ERR_ARG; }
-    if (!c->shuffle_started) {
-        const size_t TN0 = (size_t)c->T * c->N;
-        c->shuf.start(c->rng_key, c->cfg.rng_stream, c->rng_pos, (uint32_t)TN0, c->cfg.num_epochs);
-        c->shuffle_started = 1;
-    }
+    if (c->shuf_slot < 0) c->shuf_slot = c->shuf.ensure(c->rng_pos);
+    const int slot = c->shuf_slot;
     const size_t B = (size_t)c->T * c->N;
     const int M = c->cfg.num_minibatches;
     const size_t base_mb = B / M, rem = B % M;
@@ -546,10 +446,11 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
     float fw_ms = 0, sh_ms = 0;
     for (int ep = 0; ep < c->cfg.num_epochs && !stop; ep++) {
         epochs_run++;
-        c->shuf.wait_epoch(ep);
+        c->shuf.wait_epoch(slot, ep);
+        BPPO_HIP(c, hipStreamWaitEvent(c->stream, c->shuf.ev[slot][ep], 0));
         hipEvent_t s0 = c->ev[TM_SHUFFLE][0], s1 = c->ev[TM_SHUFFLE][1];
         (void)hipEventRecord(s0, c->stream);
-        TRY(launch_shuffle_apply(c, c->shuf.J + (size_t)ep * B, (uint32_t)B));
+        TRY(launch_fisher_yates(c, c->shuf.d_J[slot] + (size_t)ep * B, (uint32_t)B));
         (void)hipEventRecord(s1, c->stream);
         size_t start = 0;
         for (int mb = 0; mb < M; mb++) {
@@ -589,14 +490,15 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
         }
     }
     tm_end(c, TM_UPDATE);
-    c->rng_pos = c->shuf.end_pos[epochs_run - 1];   // only started epochs consumed words
+    c->rng_pos = c->shuf.end_pos[slot][epochs_run - 1];   // only started epochs consumed words
+    c->shuf_slot = -1;
+    // the next update's shuffles begin after its rollout's T*N*A Gumbel words
+    c->shuf.ensure(c->rng_pos + (uint64_t)c->T * c->N * (uint64_t)c->A);
     double ev4[4];
     TRY(launch_explained_variance(c, ev4));
     tm_read(c, TM_UPDATE);
     c->last_ms[TM_FWDBWD] = fw_ms;
     c->last_ms[TM_SHUFFLE] = sh_ms;
-    c->shuf.join();
-    c->shuffle_started = 0;
     if (m) {
         std::memset(m, 0, sizeof *m);
         const int nup = (int)(rows.size() / (NM + 4));
@@ -726,5 +628,31 @@ extern "C" bppo_status bppo_debug_libm(int32_t which, int32_t device, const floa
         hipMemcpy(y, dy, n * 4, hipMemcpyDeviceToHost) == hipSuccess)
         s = BPPO_OK;
     (void)hipFree(dx); (void)hipFree(dy);
+    return s;
+}
+
+// shuffle parity hooks: the host draw chain alone, and the device Fisher-Yates
+// on caller-given swap targets
+extern "C" bppo_status bppo_debug_shuffle_chain(uint64_t seed, uint64_t stream, uint64_t word_pos, uint32_t n,
+                                                uint32_t *J, uint64_t *end_pos) {
+    if (!J && n) return BPPO_ERR_ARG;
+    const Key8 key = seed_key(seed);
+    const uint64_t e = shuffle_walk_host(key, stream, word_pos, n, J);
+    if (end_pos) *end_pos = e;
+    return BPPO_OK;
+}
+
+extern "C" bppo_status bppo_debug_fisher_yates(int32_t device, const uint32_t *J, uint32_t n, uint32_t *perm) {
+    if (!J || !perm) return BPPO_ERR_ARG;
+    if (hipSetDevice(device) != hipSuccess) return BPPO_ERR_HIP;
+    uint32_t *dJ = nullptr, *dP = nullptr, *dS = nullptr, *dC = nullptr;
+    bppo_status s = BPPO_ERR_HIP;
+    if (hipMalloc((void **)&dJ, 4ull * n + 4) == hipSuccess && hipMalloc((void **)&dP, 4ull * n + 4) == hipSuccess &&
+        hipMalloc((void **)&dS, 16ull * n + 16) == hipSuccess && hipMalloc((void **)&dC, 4ull * (n / 8192 + 2)) == hipSuccess &&
+        hipMemcpy(dJ, J, 4ull * n, hipMemcpyHostToDevice) == hipSuccess &&
+        fisher_yates_device(dJ, n, dS, dC, dP, nullptr) == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
+        hipMemcpy(perm, dP, 4ull * n, hipMemcpyDeviceToHost) == hipSuccess)
+        s = BPPO_OK;
+    (void)hipFree(dJ); (void)hipFree(dP); (void)hipFree(dS); (void)hipFree(dC);
     return s;
 }

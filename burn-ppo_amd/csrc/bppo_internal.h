@@ -9,6 +9,7 @@
 #include <thread>
 #include <mutex>
 #include <condition_variable>
+#include <atomic>
 #include "../../include/bppo.h"
 #include "bppo_device.h"
 
@@ -37,30 +38,66 @@ struct EpisodeRec {
 struct Welford { double n, mean, m2; };
 
 // -------------------------------------------------------------- shuffle -----
-// rand 0.8.5 SliceRandom::shuffle draws: host thread walks the ChaCha12 word
-// stream with the UniformInt<u32> zone test (inherently sequential: every draw
-// may reject) and produces the swap targets J[i] for i = n-1 .. 1; the GPU
-// applies the swaps (deterministic reservations, bit-identical to sequential
-// Fisher-Yates).  Runs concurrently with the rollout.
+// rand 0.8.5 SliceRandom::shuffle (ppo.rs:1816) on the main StdRng.  The draw
+// chain (every draw may reject, so each draw's word position depends on all
+// earlier ones) is walked on a host thread (shuffle_host.cpp) from ChaCha12
+// words made by producer threads; each epoch's swap targets J[i] go to HBM on a
+// copy stream and the GPU turns them into the permutation (k_shuffle.hip).
+// The thread runs ahead: the next update's shuffles start at a position known
+// in advance (the rollout consumes exactly T*N*A words), so the chain overlaps
+// the rollout, the GAE and the previous epochs' minibatches.
+constexpr int SHUF_MAX_EPOCHS = 32;
+
+struct WordRing {              // ChaCha12 words in fixed chunks, filled ahead of the walker
+    static constexpr size_t C = (size_t)1 << 18;  // words per chunk
+    static constexpr int R = 40;                  // chunks in the ring
+    uint32_t *buf = nullptr;                      // [R][C]
+    int64_t chunk_id[R];
+    Key8 key{};
+    uint64_t stream = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    int64_t next = 0, floor = 0;                  // next chunk to produce; consumer done below floor
+    uint64_t gen = 0;
+    int inflight = 0;
+    bool quit = false;
+    std::vector<std::thread> producers;
+    void start(const Key8 &k, uint64_t strm, int nthreads);
+    void reset(int64_t first_chunk);              // drop everything, restart at first_chunk
+    const uint32_t *get(int64_t chunk);           // blocks until produced
+    void release_below(int64_t chunk);
+    void stop();
+};
+
 struct ShuffleEngine {
+    int dev = 0;
+    uint32_t n = 0;
+    int epochs = 0;
+    WordRing words;
     std::thread th;
     std::mutex mu;
     std::condition_variable cv;
-    Key8 key{};
-    uint64_t stream = 0;
-    uint64_t start_pos = 0;
-    uint32_t n = 0;
-    int epochs = 0;
-    int ready = 0;                      // epochs whose J is complete
-    bool running = false;
-    std::vector<uint64_t> end_pos;      // word position after each epoch's shuffle
-    uint32_t *J = nullptr;              // pinned host [epochs][n]
-    size_t J_cap = 0;
-    void start(const Key8 &k, uint64_t strm, uint64_t pos, uint32_t n_, int epochs_);
-    void wait_epoch(int e);
-    void join();
-    ~ShuffleEngine();
+    bool quit = false;
+    // job: the shuffles of one update, starting at word position job_start
+    bool job_pending = false, job_running = false, job_valid = false;
+    uint64_t job_start = 0;
+    int job_slot = 1;
+    bool cancel = false;
+    int ready[2] = {0, 0};                    // epochs of the slot's job already on the device
+    uint64_t end_pos[2][SHUF_MAX_EPOCHS];
+    uint32_t *J_host[2] = {nullptr, nullptr}; // pinned [epochs][n]
+    uint32_t *d_J[2] = {nullptr, nullptr};    // device [epochs][n]
+    hipEvent_t ev[2][SHUF_MAX_EPOCHS] = {};
+    bool ev_used[2][SHUF_MAX_EPOCHS] = {};
+    hipStream_t copy = nullptr;
+    double walk_ms[2][SHUF_MAX_EPOCHS] = {};
+    bppo_status init(int device, const Key8 &key, uint64_t stream, uint32_t n_, int epochs_, std::string &err);
+    int ensure(uint64_t start);               // job for this start (reused if already running/done) -> slot
+    void wait_epoch(int slot, int e);
+    void shutdown();
+    void run();
 };
+uint64_t shuffle_walk_host(const Key8 &key, uint64_t stream, uint64_t pos, uint32_t n, uint32_t *J);
 
 struct Timers {
     hipEvent_t a = nullptr, b = nullptr;
@@ -115,11 +152,10 @@ struct bppo_ctx {
     uint64_t rng_pos = 0;
     // shuffle
     bppo::ShuffleEngine shuf;
-    uint32_t *d_J = nullptr, *d_perm = nullptr, *d_R = nullptr, *d_R2 = nullptr;
-    int32_t *d_res = nullptr;
-    uint32_t *d_cnt = nullptr;        // [2] round counters
-    uint32_t *h_cnt = nullptr;        // pinned
-    int shuffle_started = 0;
+    uint32_t *d_perm = nullptr;       // shuffled indices of the current epoch
+    uint32_t *d_fy = nullptr;         // Fisher-Yates scratch [4][TN]: count/offset, bucket, succ, fw
+    uint32_t *d_scan = nullptr;       // scan block sums
+    int shuf_slot = -1;               // engine slot holding this update's J
     // scratch
     double *d_red = nullptr;          // reduction scratch
     double *h_red = nullptr;          // pinned mirror
@@ -158,7 +194,9 @@ bppo_status launch_gae_mp(const float *ar, const int32_t *pl, const float *d, co
                           float *adv, float *ret, hipStream_t s);
 bppo_status launch_return_norm(bppo_ctx *c);
 // (k_update.hip)
-bppo_status launch_shuffle_apply(bppo_ctx *c, const uint32_t *h_J, uint32_t n);
+bppo_status launch_fisher_yates(bppo_ctx *c, const uint32_t *d_J, uint32_t n);
+hipError_t fisher_yates_device(const uint32_t *d_J, uint32_t n, uint32_t *scratch, uint32_t *scan, uint32_t *perm,
+                               hipStream_t st);
 bppo_status launch_minibatch(bppo_ctx *c, uint32_t mb_start, uint32_t mb_size, float ent_coef,
                              double *h_stats_out);
 bppo_status launch_adam(bppo_ctx *c, float lr, const float *c1, const float *c2);

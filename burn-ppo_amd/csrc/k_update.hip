@@ -1,10 +1,6 @@
 // k_update.hip — ppo_update on the device (ppo.rs:1661-2112).
 //
-//  * shuffle: the host walks rand 0.8.5's rejection chain (inherently serial)
-//    and hands over the Fisher-Yates swap targets J[i]; the GPU applies them by
-//    deterministic reservations (each round commits every swap whose two
-//    positions are not claimed by an earlier pending swap), which reproduces the
-//    sequential permutation exactly in O(log n) rounds;
+//  * shuffle: shuffle_engine.hip (host draw chain) + k_shuffle.hip (permutation);
 //  * per minibatch: gather by the shuffled indices (ppo.rs:1833-1857), raw
 //    advantage stats + normalisation (ppo.rs:1905-1917, utils.rs:80-89), fused
 //    forward + clipped-surrogate loss + backward (ppo.rs:1385-1502) with the
@@ -14,73 +10,6 @@
 #include "bppo_internal.h"
 
 namespace bppo {
-
-// ============================================================== shuffle ====
-__global__ void k_dr_init(uint32_t n, uint32_t *perm, uint32_t *R, uint32_t *cnt) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) perm[i] = i;
-    if (i >= 1 && i < n) R[i - 1] = i;
-    if (i == 0) { cnt[0] = n > 0 ? n - 1 : 0; cnt[1] = 0; }
-}
-__global__ void k_dr_reset(const uint32_t *R, const uint32_t *cnt, const uint32_t *J, int32_t *res) {
-    const uint32_t m = cnt[0];
-    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < m; t += gridDim.x * blockDim.x) {
-        uint32_t i = R[t];
-        res[i] = -1;
-        res[J[i]] = -1;
-    }
-}
-__global__ void k_dr_reserve(const uint32_t *R, const uint32_t *cnt, const uint32_t *J, int32_t *res) {
-    const uint32_t m = cnt[0];
-    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < m; t += gridDim.x * blockDim.x) {
-        uint32_t i = R[t];
-        atomicMax(&res[i], (int32_t)i);       // earlier Fisher-Yates step = larger i wins
-        atomicMax(&res[J[i]], (int32_t)i);
-    }
-}
-__global__ void k_dr_commit(const uint32_t *R, uint32_t *cnt, const uint32_t *J, const int32_t *res,
-                            uint32_t *perm, uint32_t *R2) {
-    const uint32_t m = cnt[0];
-    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < m; t += gridDim.x * blockDim.x) {
-        uint32_t i = R[t], j = J[i];
-        if (res[i] == (int32_t)i && res[j] == (int32_t)i) {
-            uint32_t a = perm[i], b = perm[j];
-            perm[i] = b;
-            perm[j] = a;
-        } else {
-            R2[atomicAdd(&cnt[1], 1u)] = i;
-        }
-    }
-}
-__global__ void k_dr_swap_counts(uint32_t *cnt) {
-    cnt[0] = cnt[1];
-    cnt[1] = 0;
-}
-
-bppo_status launch_shuffle_apply(bppo_ctx *c, const uint32_t *h_J, uint32_t n) {
-    if (n == 0) return BPPO_OK;
-    BPPO_HIP(c, hipMemcpyAsync(c->d_J, h_J, sizeof(uint32_t) * n, hipMemcpyHostToDevice, c->stream));
-    hipLaunchKernelGGL(k_dr_init, dim3((n + 255) / 256), dim3(256), 0, c->stream, n, c->d_perm,
-                       c->d_R, c->d_cnt);
-    uint32_t *R = c->d_R, *R2 = c->d_R2;
-    const dim3 g(2048), b(256);
-    for (int iter = 0; iter < 4096; iter++) {
-        for (int k = 0; k < 8; k++) {
-            hipLaunchKernelGGL(k_dr_reset, g, b, 0, c->stream, R, c->d_cnt, c->d_J, c->d_res);
-            hipLaunchKernelGGL(k_dr_reserve, g, b, 0, c->stream, R, c->d_cnt, c->d_J, c->d_res);
-            hipLaunchKernelGGL(k_dr_commit, g, b, 0, c->stream, R, c->d_cnt, c->d_J, c->d_res,
-                               c->d_perm, R2);
-            hipLaunchKernelGGL(k_dr_swap_counts, dim3(1), dim3(1), 0, c->stream, c->d_cnt);
-            uint32_t *tmp = R; R = R2; R2 = tmp;
-        }
-        BPPO_HIP(c, hipMemcpyAsync(c->h_cnt, c->d_cnt, sizeof(uint32_t), hipMemcpyDeviceToHost,
-                                   c->stream));
-        BPPO_HIP(c, hipStreamSynchronize(c->stream));
-        if (c->h_cnt[0] == 0) return BPPO_OK;
-    }
-    c->err = "shuffle: deterministic reservations did not converge";
-    return BPPO_ERR_HIP;
-}
 
 // ============================================================ adv stats ====
 // two-pass, f64 accumulation, fixed-order final reduction

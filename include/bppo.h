@@ -167,6 +167,14 @@ bppo_status bppo_last_kernel_ms(bppo_ctx *ctx, const char *kernel, float *ms);
  * device = 0 runs the host build of the same source, 1 runs the HIP kernel */
 bppo_status bppo_debug_libm(int32_t which, int32_t device, const float *x, float *y, size_t n);
 
+/* shuffle parity hooks (ppo.rs:1816, rand 0.8.5 SliceRandom::shuffle on StdRng):
+ * the host draw chain alone — J[i] = gen_range(0..i+1) for i = n-1..1 from word
+ * position word_pos of StdRng(seed) stream `stream`, *end_pos = position after —
+ * and the device Fisher-Yates permutation of 0..n-1 for given swap targets J */
+bppo_status bppo_debug_shuffle_chain(uint64_t seed, uint64_t stream, uint64_t word_pos, uint32_t n,
+                                     uint32_t *J, uint64_t *end_pos);
+bppo_status bppo_debug_fisher_yates(int32_t device, const uint32_t *J, uint32_t n, uint32_t *perm);
+
 #ifdef __cplusplus
 }
 #endif

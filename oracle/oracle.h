@@ -54,6 +54,8 @@ float or_gen_range_f32(or_rng *r, float low, float high);
 uint32_t or_gen_range_u32(or_rng *r, uint32_t low, uint32_t high);     /* [low, high) */
 uint8_t or_gen_range_u8_incl(or_rng *r, uint8_t low, uint8_t high);    /* [low, high] */
 void or_shuffle_u32(or_rng *r, uint32_t *v, size_t n);
+void or_shuffle_targets(or_rng *r, uint32_t *J, size_t n);
+void or_apply_swaps(const uint32_t *J, uint32_t *v, size_t n);
 /* helpers for ctypes: run n draws and return them */
 void or_rng_words(uint64_t seed, uint64_t skip, uint32_t *out, size_t n);
 void or_rng_words_key(const uint32_t key[8], int rounds, uint64_t skip, uint32_t *out, size_t n);

@@ -138,6 +138,21 @@ void or_shuffle_u32(or_rng *r, uint32_t *v, size_t n) {
     }
 }
 
+/* the swap targets of or_shuffle_u32 (J[i] = gen_range(0..i+1), i = n-1..1; J[0] = 0)
+ * and the sequential swap pass that turns them into the permutation */
+void or_shuffle_targets(or_rng *r, uint32_t *J, size_t n) {
+    if (n == 0) return;
+    J[0] = 0;
+    for (size_t i = n - 1; i >= 1; i--) J[i] = or_gen_range_u32(r, 0, (uint32_t)(i + 1));
+}
+
+void or_apply_swaps(const uint32_t *J, uint32_t *v, size_t n) {
+    for (size_t i = n; i-- > 1;) {
+        uint32_t j = J[i], t = v[i];
+        v[i] = v[j]; v[j] = t;
+    }
+}
+
 void or_rng_words(uint64_t seed, uint64_t skip, uint32_t *out, size_t n) {
     or_rng r;
     or_rng_seed_u64(&r, seed);

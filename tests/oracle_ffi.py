@@ -113,6 +113,8 @@ def lib():
             "or_gen_range_u32": (C.c_uint32, [C.POINTER(Rng), C.c_uint32, C.c_uint32]),
             "or_gen_range_u8_incl": (C.c_uint8, [C.POINTER(Rng), C.c_uint8, C.c_uint8]),
             "or_shuffle_u32": (None, [C.POINTER(Rng), u32, C.c_size_t]),
+            "or_shuffle_targets": (None, [C.POINTER(Rng), u32, C.c_size_t]),
+            "or_apply_swaps": (None, [u32, u32, C.c_size_t]),
             "or_rng_words": (None, [C.c_uint64, C.c_uint64, u32, C.c_size_t]),
             "or_rng_words_key": (None, [u32, C.c_int, C.c_uint64, u32, C.c_size_t]),
             "or_rng_seed_key": (None, [C.c_uint64, u32]),

@@ -1,0 +1,66 @@
+"""ppo_update's per-epoch shuffle (ppo.rs:1816, rand 0.8.5 SliceRandom::shuffle
+on StdRng): the product's host draw chain (shuffle_host.cpp, AVX-512 or scalar
+walker, ChaCha12 words made by its own SIMD generator) against the oracle's
+gen_range(0..i+1) loop, and the device Fisher-Yates (k_shuffle.hip) against the
+sequential swap pass.  Bit-exact: swap targets, word positions, permutations."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import bppo._lib as L
+import oracle_ffi as O
+
+
+def _oracle_targets(seed, stream, pos, n):
+    r = O.Rng()
+    O.lib().or_rng_seed_u64(C.byref(r), seed)
+    r.stream = stream
+    r.word_pos = pos
+    J = np.zeros(n, np.uint32)
+    O.lib().or_shuffle_targets(C.byref(r), J, n)
+    return J, r.word_pos
+
+
+@pytest.mark.parametrize("seed,stream,pos,n", [
+    (42, 0, 0, 1), (42, 0, 0, 2), (42, 0, 7, 3), (7, 0, 123, 1000),
+    (42, 0, 262_141, 70_001),            # crosses the 2^18-word chunk boundary mid-walk
+    (42, 3, 5, 1 << 17),                 # rank stream 3, n a power of two (first draw never rejects)
+    (9, 0, 1_000_003, (1 << 16) + 1),    # n just above a power of two (rejection ~1/2)
+])
+def test_host_chain_matches_oracle(seed, stream, pos, n):
+    J = np.zeros(n, np.uint32)
+    end = C.c_uint64()
+    assert L.lib().bppo_debug_shuffle_chain(seed, stream, pos, n, J.ctypes.data, C.byref(end)) == 0
+    Jo, endo = _oracle_targets(seed, stream, pos, n)
+    assert np.array_equal(J, Jo)
+    assert end.value == endo
+
+
+def test_host_chain_full_cfgb_epoch():
+    """one CfgB epoch (B = 2^23 draws, ~11.6 M words): targets and end position"""
+    n = 1 << 23
+    J = np.zeros(n, np.uint32)
+    end = C.c_uint64()
+    assert L.lib().bppo_debug_shuffle_chain(42, 0, 16_777_216, n, J.ctypes.data, C.byref(end)) == 0
+    Jo, endo = _oracle_targets(42, 0, 16_777_216, n)
+    assert end.value == endo
+    assert np.array_equal(J, Jo)
+    assert np.all(J <= np.arange(n, dtype=np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 2, 3, 17, 1000, 8193, 100_003, 1 << 23])
+def test_device_fisher_yates_matches_sequential(n):
+    rng = np.random.default_rng(n)
+    i = np.arange(n, dtype=np.uint64)
+    J = np.minimum((rng.random(n) * (i + 1)).astype(np.uint64), i).astype(np.uint32)
+    J[0] = 0
+    if n > 10:
+        J[n // 2] = n // 2            # self-swaps
+        J[n - 1] = 0                  # a long bucket at 0
+    perm = np.zeros(n, np.uint32)
+    assert L.lib().bppo_debug_fisher_yates(0, J.ctypes.data, n, perm.ctypes.data) == 0
+    ref = np.arange(n, dtype=np.uint32)
+    O.lib().or_apply_swaps(J, ref, n)
+    assert np.array_equal(perm, ref)
