@@ -68,7 +68,7 @@ EXPORTS = (
     "bppo_collect_rollouts", "bppo_rollout_episodes", "bppo_compute_gae", "bppo_ppo_update",
     "bppo_set_allreduce", "bppo_buffer_get", "bppo_buffer_set", "bppo_gae_device",
     "bppo_gae_mp_device", "bppo_last_kernel_ms", "bppo_debug_libm", "bppo_debug_shuffle_chain",
-    "bppo_debug_fisher_yates",
+    "bppo_debug_fisher_yates", "bppo_debug_gemm",
 )
 
 _lib = None
@@ -119,6 +119,7 @@ def lib():
         "bppo_debug_libm": (i32, [i32, i32, vp, vp, sz]),
         "bppo_debug_shuffle_chain": (i32, [u64, u64, u64, C.c_uint32, vp, C.POINTER(u64)]),
         "bppo_debug_fisher_yates": (i32, [i32, vp, C.c_uint32, vp]),
+        "bppo_debug_gemm": (i32, [i32, i32, i32, i32, vp, vp, vp, i32, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

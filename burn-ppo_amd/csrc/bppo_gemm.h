@@ -1,0 +1,27 @@
+// bppo_gemm.h — launchers of the f32 MFMA GEMM engine (k_gemm.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace bppo {
+
+constexpr int GEMM_MAX_SPLITS = 256;
+
+// Y = act(X W + b): X [M][K] (ldx), W [K][N] (ldw), bias [N]; columns [0, n0)
+// go to out0 (ld0), [n0, N) to out1 (ld1) when out1 != nullptr.  Bit-exact
+// with matrixmultiply's KC=256 k-ordered fma chains (see k_gemm.hip).
+hipError_t gemm_fwd(hipStream_t st, int M, int N, int K, const float *X, int ldx, const float *W,
+                    int ldw, const float *bias, int relu, float *out0, int ld0, int n0, float *out1,
+                    int ld1);
+// out = (dZ W^T) masked by H > 0 (H may be null): dZ [M][K] (ldz), W [N][K] (ldw)
+hipError_t gemm_dx(hipStream_t st, int M, int N, int K, const float *dZ, int ldz, const float *W,
+                   int ldw, const float *H, int ldh, float *out, int ldo);
+// dW = X^T dZ over `rows` rows: X [rows][Kin] (ldx), dZ [rows][N] (ldz).
+// Columns [0, n0) -> dW0 [Kin][ldw0], [n0, N) -> dW1 [Kin][ldw1] (when dW1);
+// bias gradient (column sums of dZ) -> db0 / db1 likewise (either may be null).
+// part: [splits][Kin][N] scratch, colsum: [splits][N] scratch.
+hipError_t gemm_wgrad(hipStream_t st, int Kin, int N, int rows, const float *X, int ldx, const float *dZ,
+                      int ldz, float *part, float *colsum, float *dW0, int ldw0, int n0, float *dW1, int ldw1,
+                      float *db0, float *db1, int splits);
+int gemm_wg_splits(int Kin, int N, int rows);
+
+}  // namespace bppo

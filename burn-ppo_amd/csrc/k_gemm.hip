@@ -1,0 +1,348 @@
+// k_gemm.hip — f32 MFMA GEMM engine for the wide actor-critic MLPs
+// (Connect Four 86->512->512->{7,1}, Liar's Dice CTDE actor 270->256->256->49 and
+// critic 390->512->512->512->1; mlp.rs:140-206, ctde.rs:132-183).
+//
+// v_mfma_f32_32x32x2_f32 computes, per output element, a k-ordered fmaf chain
+// (one rounding per product, MI355X guide §3 "FP32-input MFMA"), so a forward
+// GEMM that walks k in order, restarting the chain at every KC=256 block and
+// summing the block results into C, reproduces matrixmultiply 0.3's sgemm
+// (oracle/net.c or_linear) bit for bit: the rollout forward, the bootstrap and
+// the update forward all go through gemm_fwd, so the first-minibatch PPO ratio
+// is exactly 1 (ppo.rs:1452) and the sampled actions match the reference.
+//
+// Three operand forms, one kernel template:
+//   FWD  Y = act(X W + b)           X [M][K] row-major, W [K][N] (Burn Linear)
+//   DX   dX = (dZ W^T) * [H > 0]    dZ [M][K=out], W [N=in][K=out]
+//   WG   dW = X^T dZ (+ db = 1^T dZ) split over row chunks, partial slabs
+//        reduced in a fixed order (deterministic, no float atomics).
+// Block = 4 waves; wave tile = TM x TN accumulators of 32x32; LDS holds one
+// BK=32 stage of A (k-major, padded row) and B (k-major) double-buffered, the
+// next stage prefetched into registers while the MFMAs of the current run.
+#include "bppo_internal.h"
+#include "bppo_gemm.h"
+
+namespace bppo {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int GBK = 32;      // k per LDS stage
+constexpr int KC = 256;      // matrixmultiply sgemm k-block
+
+template <int BM, int BN, int WM, int WN>
+struct GemmShape {
+    static constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+    static constexpr int APAD = BM + 1;             // k-major A rows, +1: conflict-free transposing writes
+    static constexpr int BPAD = BN + 1;
+    static constexpr int A_ELEMS = GBK * BM / 256;  // per thread per stage
+    static constexpr int B_ELEMS = GBK * BN / 256;
+    static_assert(WM * WN == 4, "4 waves");
+    static_assert(TM >= 1 && TN >= 1, "wave tile >= 32x32");
+};
+
+// operand element (row r of the tile's M/N side, k) -> global address
+//   KCONTIG: element at base[r * ld + k]  (row-major, k contiguous)
+//   else:    element at base[k * ld + r]  (k-major, r contiguous)
+template <int R, bool KCONTIG>
+struct TileLoader {
+    static constexpr int E = GBK * R / 256;
+    float v[E];
+    // ones_row >= 0: tile row index r == ones_row (global) reads 1.0 (bias-gradient row)
+    __device__ __forceinline__ void load(const float *__restrict__ base, int ld, int r0, int rmax, int k0,
+                                         int kmax, int tid) {
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            int r, k;
+            if constexpr (KCONTIG) { k = tid & 31; r = (tid >> 5) + e * 8; }
+            else { r = tid % R; k = tid / R + e * (256 / R); }
+            const int gr = r0 + r, gk = k0 + k;
+            v[e] = (gr < rmax && gk < kmax) ? base[(size_t)(KCONTIG ? gr : gk) * ld + (KCONTIG ? gk : gr)] : 0.0f;
+        }
+    }
+    __device__ __forceinline__ void store(float *__restrict__ s, int tid) const {
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            int r, k;
+            if constexpr (KCONTIG) { k = tid & 31; r = (tid >> 5) + e * 8; }
+            else { r = tid % R; k = tid / R + e * (256 / R); }
+            s[k * (R + 1) + r] = v[e];
+        }
+    }
+};
+
+struct GemmArgs {
+    const float *A; int lda;
+    const float *B; int ldb;
+    int M, N, K;                 // C is M x N, reduction K
+    // FWD epilogue
+    const float *bias; int act;  // act: 1 relu, 0 none
+    float *out0; int ld0; int n0;   // cols [0, n0) -> out0[row*ld0 + col]
+    float *out1; int ld1;           // cols [n0, N) -> out1[row*ld1 + col - n0]
+    // DX epilogue: relu mask from H [M][ldh] (nullptr: no mask)
+    const float *H; int ldh;
+    // WG: partial slab [split][M][N] and column sums [split][N]; rows of the
+    // reduction per split
+    float *part; float *colsum; int k_per_split;
+};
+
+enum { GEMM_FWD = 0, GEMM_DX = 1, GEMM_WG = 2 };
+
+template <int MODE, int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(256, 2) k_gemm(GemmArgs g) {
+    using S = GemmShape<BM, BN, WM, WN>;
+    constexpr bool A_KC = MODE != GEMM_WG;        // FWD/DX: A row-major [M][K]; WG: A = X^T, X [K][M]
+    constexpr bool B_KC = MODE == GEMM_DX;        // FWD: W [K][N]; DX: W [N][K]; WG: dZ [K][N]
+    __shared__ float sA[2][GBK * S::APAD];
+    __shared__ float sB[2][GBK * S::BPAD];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+    int kbeg = 0, kend = g.K;
+    if constexpr (MODE == GEMM_WG) {
+        kbeg = blockIdx.z * g.k_per_split;
+        kend = min(g.K, kbeg + g.k_per_split);
+    }
+    TileLoader<BM, A_KC> la;
+    TileLoader<BN, B_KC> lb;
+    f32x16 acc[S::TM][S::TN], tot[S::TM][S::TN];
+#pragma unroll
+    for (int i = 0; i < S::TM; i++)
+#pragma unroll
+        for (int j = 0; j < S::TN; j++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) { acc[i][j][r] = 0.0f; tot[i][j][r] = 0.0f; }
+    // bias-gradient column sums (WG, first row tile only): 256/BN threads per column
+    float csum = 0.0f;
+    const bool do_colsum = MODE == GEMM_WG && g.colsum != nullptr && blockIdx.y == 0;
+
+    la.load(g.A, g.lda, m0, g.M, kbeg, kend, tid);
+    lb.load(g.B, g.ldb, n0, g.N, kbeg, kend, tid);
+    la.store(sA[0], tid);
+    lb.store(sB[0], tid);
+    __syncthreads();
+    int buf = 0;
+    for (int k0 = kbeg; k0 < kend; k0 += GBK) {
+        const bool more = k0 + GBK < kend;
+        if (more) {
+            la.load(g.A, g.lda, m0, g.M, k0 + GBK, kend, tid);
+            lb.load(g.B, g.ldb, n0, g.N, k0 + GBK, kend, tid);
+        }
+        if (do_colsum) {
+            const int c = tid % BN, part = tid / BN, np = 256 / BN;
+#pragma unroll 4
+            for (int k = part; k < GBK; k += np) csum += sB[buf][k * S::BPAD + c];
+        }
+        const float *a = sA[buf], *b = sB[buf];
+        const int h = lane >> 5, r = lane & 31;
+#pragma unroll
+        for (int kk = 0; kk < GBK; kk += 2) {
+            float af[S::TM], bf[S::TN];
+#pragma unroll
+            for (int i = 0; i < S::TM; i++) af[i] = a[(kk + h) * S::APAD + (wm * S::TM + i) * 32 + r];
+#pragma unroll
+            for (int j = 0; j < S::TN; j++) bf[j] = b[(kk + h) * S::BPAD + (wn * S::TN + j) * 32 + r];
+#pragma unroll
+            for (int i = 0; i < S::TM; i++)
+#pragma unroll
+                for (int j = 0; j < S::TN; j++)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+        }
+        if constexpr (MODE == GEMM_FWD) {
+            // matrixmultiply KC block boundary: the chain restarts from 0 and the
+            // finished block is summed into C (first block stored as is)
+            if (((k0 + GBK) % KC) == 0 && more) {
+#pragma unroll
+                for (int i = 0; i < S::TM; i++)
+#pragma unroll
+                    for (int j = 0; j < S::TN; j++)
+#pragma unroll
+                        for (int q = 0; q < 16; q++) {
+                            tot[i][j][q] = (k0 + GBK == KC) ? acc[i][j][q] : __fadd_rn(tot[i][j][q], acc[i][j][q]);
+                            acc[i][j][q] = 0.0f;
+                        }
+            }
+        }
+        if (more) {
+            __syncthreads();          // everyone done reading buf^1 (two stages ago)
+            la.store(sA[buf ^ 1], tid);
+            lb.store(sB[buf ^ 1], tid);
+            __syncthreads();
+            buf ^= 1;
+        }
+    }
+    if constexpr (MODE == GEMM_FWD) {
+        if (g.K > KC) {
+#pragma unroll
+            for (int i = 0; i < S::TM; i++)
+#pragma unroll
+                for (int j = 0; j < S::TN; j++)
+#pragma unroll
+                    for (int q = 0; q < 16; q++) acc[i][j][q] = __fadd_rn(tot[i][j][q], acc[i][j][q]);
+        }
+    }
+    // ---- epilogue: C/D map col = lane&31, row = (q&3) + 8*(q>>2) + 4*(lane>>5)
+    const int col_l = lane & 31, rq = 4 * (lane >> 5);
+#pragma unroll
+    for (int i = 0; i < S::TM; i++)
+#pragma unroll
+        for (int j = 0; j < S::TN; j++) {
+            const int col = n0 + (wn * S::TN + j) * 32 + col_l;
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const int row = m0 + (wm * S::TM + i) * 32 + (q & 3) + 8 * (q >> 2) + rq;
+                if (row >= g.M || col >= g.N) continue;
+                float v = acc[i][j][q];
+                if constexpr (MODE == GEMM_FWD) {
+                    v = __fadd_rn(v, g.bias[col]);
+                    if (g.act == 1) v = v > 0.0f ? v : 0.0f;
+                    if (col < g.n0) g.out0[(size_t)row * g.ld0 + col] = v;
+                    else g.out1[(size_t)row * g.ld1 + (col - g.n0)] = v;
+                } else if constexpr (MODE == GEMM_DX) {
+                    if (g.H && !(g.H[(size_t)row * g.ldh + col] > 0.0f)) v = 0.0f;
+                    g.out0[(size_t)row * g.ld0 + col] = v;
+                } else {
+                    g.part[((size_t)blockIdx.z * g.M + row) * g.N + col] = v;
+                }
+            }
+        }
+    if (do_colsum) {
+        __shared__ float red[256];
+        red[tid] = csum;
+        __syncthreads();
+        if (tid < BN) {
+            float s = 0.0f;
+            for (int p = 0; p < 256 / BN; p++) s += red[tid + p * BN];
+            const int col = n0 + tid;
+            if (col < g.N) g.colsum[(size_t)blockIdx.z * g.N + col] = s;
+        }
+    }
+}
+
+// fixed-order sum of the split partials: dst[r][c] = sum_s part[s][r][c] (f64),
+// written to out0 for c < n0 and out1 (ld1) otherwise; scale applied at the end
+__global__ void k_split_reduce(const float *__restrict__ part, int splits, int M, int N, int n0,
+                               float *out0, int ld0, float *out1, int ld1) {
+    const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= (size_t)M * N) return;
+    double s = 0.0;
+    for (int k = 0; k < splits; k++) s += (double)part[(size_t)k * M * N + i];
+    const int r = (int)(i / N), c = (int)(i % N);
+    if (c < n0) out0[(size_t)r * ld0 + c] = (float)s;
+    else out1[(size_t)r * ld1 + (c - n0)] = (float)s;
+}
+
+// -------------------------------------------------------------- launchers --
+template <int MODE, int BM, int BN, int WM, int WN>
+static hipError_t launch(const GemmArgs &g, int splits, hipStream_t st) {
+    dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, splits);
+    hipLaunchKernelGGL((k_gemm<MODE, BM, BN, WM, WN>), grid, dim3(256), 0, st, g);
+    return hipGetLastError();
+}
+
+template <int MODE>
+static hipError_t launch_by_width(const GemmArgs &g, int splits, hipStream_t st) {
+    if (g.N <= 32) return launch<MODE, 128, 32, 4, 1>(g, splits, st);
+    if (g.N <= 64) return launch<MODE, 128, 64, 4, 1>(g, splits, st);
+    return launch<MODE, 128, 128, 2, 2>(g, splits, st);
+}
+
+hipError_t gemm_fwd(hipStream_t st, int M, int N, int K, const float *X, int ldx, const float *W,
+                    int ldw, const float *bias, int relu, float *out0, int ld0, int n0, float *out1,
+                    int ld1) {
+    if (M <= 0 || N <= 0) return hipSuccess;
+    GemmArgs g{};
+    g.A = X; g.lda = ldx; g.B = W; g.ldb = ldw; g.M = M; g.N = N; g.K = K;
+    g.bias = bias; g.act = relu ? 1 : 0;
+    g.out0 = out0; g.ld0 = ld0; g.n0 = out1 ? n0 : N; g.out1 = out1; g.ld1 = ld1;
+    return launch_by_width<GEMM_FWD>(g, 1, st);
+}
+
+hipError_t gemm_dx(hipStream_t st, int M, int N, int K, const float *dZ, int ldz, const float *W,
+                   int ldw, const float *H, int ldh, float *out, int ldo) {
+    if (M <= 0 || N <= 0) return hipSuccess;
+    GemmArgs g{};
+    g.A = dZ; g.lda = ldz; g.B = W; g.ldb = ldw; g.M = M; g.N = N; g.K = K;
+    g.H = H; g.ldh = ldh; g.out0 = out; g.ld0 = ldo; g.n0 = N;
+    return launch_by_width<GEMM_DX>(g, 1, st);
+}
+
+int gemm_wg_splits(int Kin, int N, int rows) {
+    const int tiles = ((Kin + 127) / 128) * ((N + (N <= 32 ? 31 : N <= 64 ? 63 : 127)) / (N <= 32 ? 32 : N <= 64 ? 64 : 128));
+    int s = (2048 + tiles - 1) / tiles;                  // ~2048 blocks
+    const int max_by_rows = (rows + 1023) / 1024;        // >= 1024 rows per split
+    if (s > max_by_rows) s = max_by_rows;
+    if (s > GEMM_MAX_SPLITS) s = GEMM_MAX_SPLITS;
+    if (s < 1) s = 1;
+    return s;
+}
+
+hipError_t gemm_wgrad(hipStream_t st, int Kin, int N, int rows, const float *X, int ldx, const float *dZ,
+                      int ldz, float *part, float *colsum, float *dW0, int ldw0, int n0, float *dW1, int ldw1,
+                      float *db0, float *db1, int splits) {
+    if (Kin <= 0 || N <= 0) return hipSuccess;
+    GemmArgs g{};
+    g.A = X; g.lda = ldx; g.B = dZ; g.ldb = ldz; g.M = Kin; g.N = N; g.K = rows;
+    g.part = part; g.colsum = (db0 || db1) ? colsum : nullptr;
+    g.k_per_split = ((rows + splits - 1) / splits + GBK - 1) / GBK * GBK;
+    const int sp = (rows + g.k_per_split - 1) / g.k_per_split;
+    hipError_t e = launch_by_width<GEMM_WG>(g, sp, st);
+    if (e != hipSuccess) return e;
+    const size_t MN = (size_t)Kin * N;
+    const int nn0 = dW1 ? n0 : N;
+    hipLaunchKernelGGL(k_split_reduce, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, st, part, sp, Kin, N,
+                       nn0, dW0, ldw0, dW1, ldw1);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (db0 || db1) {
+        // bias gradient: colsum [sp][N] -> db0 (cols < n0) / db1
+        hipLaunchKernelGGL(k_split_reduce, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, colsum, sp, 1, N,
+                           db1 ? n0 : N, db0, 0, db1, 0);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+}  // namespace bppo
+
+// ------------------------------------------------------------ parity hook ---
+// bppo_debug_gemm: host buffers in/out; mode 0 FWD (bias, relu), 1 DX (H mask
+// optional), 2 WG (out = [Kin][N] weight grad, out2 = [N] bias grad).
+extern "C" bppo_status bppo_debug_gemm(int32_t mode, int32_t M, int32_t N, int32_t K, const float *A,
+                                       const float *B, const float *bias_or_H, int32_t relu, float *out,
+                                       float *out2) {
+    using namespace bppo;
+    if (!A || !B || !out || M <= 0 || N <= 0 || K <= 0 || mode < 0 || mode > 2) return BPPO_ERR_ARG;
+    float *dA = nullptr, *dB = nullptr, *dX = nullptr, *dO = nullptr, *dO2 = nullptr, *dP = nullptr, *dC = nullptr;
+    size_t nA = mode == 2 ? (size_t)K * M : (size_t)M * K;   // WG: X [rows=K][Kin=M]
+    size_t nB = mode == 1 ? (size_t)N * K : (size_t)K * N;
+    size_t nX = mode == 0 ? (size_t)N : (mode == 1 ? (size_t)M * N : 0);
+    bppo_status s = BPPO_ERR_HIP;
+    const int splits = mode == 2 ? gemm_wg_splits(M, N, K) : 1;
+    do {
+        if (hipMalloc((void **)&dA, nA * 4) != hipSuccess || hipMalloc((void **)&dB, nB * 4) != hipSuccess) break;
+        if (hipMalloc((void **)&dO, (size_t)M * N * 4) != hipSuccess) break;
+        if (hipMemcpy(dA, A, nA * 4, hipMemcpyHostToDevice) != hipSuccess) break;
+        if (hipMemcpy(dB, B, nB * 4, hipMemcpyHostToDevice) != hipSuccess) break;
+        if (nX && bias_or_H) {
+            if (hipMalloc((void **)&dX, nX * 4) != hipSuccess) break;
+            if (hipMemcpy(dX, bias_or_H, nX * 4, hipMemcpyHostToDevice) != hipSuccess) break;
+        }
+        hipError_t e;
+        if (mode == 0) {
+            if (!dX) break;
+            e = gemm_fwd(nullptr, M, N, K, dA, K, dB, N, dX, relu, dO, N, N, nullptr, 0);
+        } else if (mode == 1) {
+            e = gemm_dx(nullptr, M, N, K, dA, K, dB, K, dX, N, dO, N);
+        } else {
+            if (hipMalloc((void **)&dO2, (size_t)N * 4) != hipSuccess) break;
+            if (hipMalloc((void **)&dP, (size_t)splits * M * N * 4) != hipSuccess) break;
+            if (hipMalloc((void **)&dC, (size_t)splits * N * 4) != hipSuccess) break;
+            e = gemm_wgrad(nullptr, M, N, K, dA, M, dB, N, dP, dC, dO, N, N, nullptr, 0, dO2, nullptr, splits);
+        }
+        if (e != hipSuccess || hipDeviceSynchronize() != hipSuccess) break;
+        if (hipMemcpy(out, dO, (size_t)M * N * 4, hipMemcpyDeviceToHost) != hipSuccess) break;
+        if (mode == 2 && out2 && hipMemcpy(out2, dO2, (size_t)N * 4, hipMemcpyDeviceToHost) != hipSuccess) break;
+        s = BPPO_OK;
+    } while (0);
+    (void)hipFree(dA); (void)hipFree(dB); (void)hipFree(dX); (void)hipFree(dO); (void)hipFree(dO2);
+    (void)hipFree(dP); (void)hipFree(dC);
+    return s;
+}

@@ -175,6 +175,13 @@ bppo_status bppo_debug_shuffle_chain(uint64_t seed, uint64_t stream, uint64_t wo
                                      uint32_t *J, uint64_t *end_pos);
 bppo_status bppo_debug_fisher_yates(int32_t device, const uint32_t *J, uint32_t n, uint32_t *perm);
 
+/* GEMM engine parity hook (host buffers).  mode 0: out[M][N] = act(A[M][K] B[K][N] + bias[N])
+ * with matrixmultiply's KC=256 fma-chain order (Burn Linear forward, mlp.rs:140-206);
+ * mode 1: out[M][N] = (A[M][K] B[N][K]^T) * [H[M][N] > 0] (H = bias_or_H, may be NULL);
+ * mode 2: out[M][N] = A[K][M]^T B[K][N] (weight gradient), out2[N] = column sums of B */
+bppo_status bppo_debug_gemm(int32_t mode, int32_t M, int32_t N, int32_t K, const float *A, const float *B,
+                            const float *bias_or_H, int32_t relu, float *out, float *out2);
+
 #ifdef __cplusplus
 }
 #endif

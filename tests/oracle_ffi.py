@@ -144,6 +144,7 @@ def lib():
             "or_vecenv_step": (C.c_int, [C.c_void_p, i32, f32, f32, u8, C.POINTER(Episode), C.c_int]),
             "or_vecenv_env_ptr": (C.c_void_p, [C.c_void_p, C.c_int]),
             "or_net_num_params": (C.c_size_t, [C.POINTER(NetDesc)]),
+            "or_linear": (None, [f32, f32, f32, C.c_size_t, C.c_int, C.c_int, C.c_int, f32]),
             "or_net_forward": (None, [C.POINTER(NetDesc), f32, f32, C.c_void_p, C.c_size_t, f32, f32]),
             "or_sample_categorical": (None, [C.POINTER(Rng), f32, C.c_size_t, C.c_int, i32]),
             "or_log_prob": (C.c_float, [f32, C.c_int, C.c_int32]),
@@ -232,6 +233,16 @@ def net_forward(desc, params, obs, priv=None):
                          np.ascontiguousarray(obs, np.float32),
                          None if pp is None else pp.ctypes.data, B, logits, values)
     return logits, values
+
+
+def linear(x, W, b, relu):
+    """or_linear: y = act(x W + b) in matrixmultiply's KC=256 fma-chain order (relu: 1, 0 tanh, -1 none)"""
+    B, K = x.shape
+    N = W.shape[1]
+    y = np.zeros((B, N), np.float32)
+    lib().or_linear(np.ascontiguousarray(x, np.float32), np.ascontiguousarray(W, np.float32),
+                    np.ascontiguousarray(b, np.float32), B, K, N, relu, y)
+    return y
 
 
 def compute_gae(rewards, dones, values, last_values, gamma, lam):
