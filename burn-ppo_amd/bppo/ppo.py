@@ -43,6 +43,10 @@ class Context:
         self.n_params = L.lib().bppo_num_params(self.h)
         self.obs_dim = {"cartpole": 5, "connect_four": 86, "liars_dice": 270}[cfg["env"]]
         self.num_actions = {"cartpole": 2, "connect_four": 7, "liars_dice": 49}[cfg["env"]]
+        self.num_players = {"cartpole": 1, "connect_four": 2, "liars_dice": 4}[cfg["env"]]
+        # liars_dice.rs:459; the device keeps privileged rows only for CTDE nets
+        self.priv_dim = 120 if cfg["env"] == "liars_dice" and cfg["network_type"] == "ctde" else 0
+        self.has_masks = cfg["env"] != "cartpole"
         self._ar_keep = None
 
     def close(self):
@@ -61,8 +65,10 @@ class Context:
 
     # parity hooks -------------------------------------------------------
     def buffer(self, name, dtype=np.float32, shape=None):
-        n = {"obs": self.T * self.N * self.obs_dim, "last_values": self.N,
-             "grad": self.n_params}.get(name, self.T * self.N)
+        TN = self.T * self.N
+        n = {"obs": TN * self.obs_dim, "last_values": self.N, "grad": self.n_params,
+             "priv": TN * self.priv_dim, "masks": TN * self.num_actions,
+             "all_rewards": TN * self.num_players, "last_v_pp": self.N * self.num_players}.get(name, TN)
         out = np.zeros(n, dtype)
         self._chk(L.lib().bppo_buffer_get(self.h, name.encode(), out.ctypes.data, out.nbytes))
         return out.reshape(shape) if shape else out
@@ -115,7 +121,7 @@ class Context:
 
 
 class VecEnv:
-    """env.rs VecEnv over the device-resident envs (CartPole in this build)."""
+    """env.rs VecEnv over the device-resident envs (CartPole, Connect Four, Liar's Dice)."""
 
     def __init__(self, ctx):
         self.ctx = ctx
@@ -141,7 +147,20 @@ class VecEnv:
         return p
 
     def get_action_masks(self):
-        return None     # CartPole has no masks (Environment::action_mask default None)
+        """env.rs:350-362: [N*A] bool, None when the env has no masks (CartPole)."""
+        if not self.ctx.has_masks:
+            return None
+        m = np.zeros(self.ctx.N * self.ctx.num_actions, np.uint8)
+        self.ctx._chk(L.lib().bppo_vecenv_observe(self.ctx.h, None, None, m.ctypes.data, None))
+        return m.astype(bool)
+
+    def get_privileged_obs(self):
+        """env.rs:365-376: [N*120] for Liar's Dice, None otherwise."""
+        if not self.ctx.priv_dim:
+            return None
+        g = np.zeros(self.ctx.N * self.ctx.priv_dim, np.float32)
+        self.ctx._chk(L.lib().bppo_vecenv_observe(self.ctx.h, None, None, None, g.ctypes.data))
+        return g
 
     def set_step(self, step):
         self.ctx._chk(L.lib().bppo_vecenv_set_step(self.ctx.h, int(step)))
@@ -151,16 +170,17 @@ class VecEnv:
         N = self.ctx.N
         a = np.ascontiguousarray(actions, np.int32)
         obs = np.zeros(N * self.ctx.obs_dim, np.float32)
-        rew = np.zeros(N, np.float32)
+        P = self.ctx.num_players
+        rew = np.zeros(N * P, np.float32)
         dn = np.zeros(N, np.uint8)
         cap = N
         eps = (L.Episode * cap)()
         n = C.c_int32()
         self.ctx._chk(L.lib().bppo_vecenv_step(self.ctx.h, a.ctypes.data, obs.ctypes.data, rew.ctypes.data,
                                                dn.ctypes.data, eps, cap, C.byref(n)))
-        done_eps = [dict(total_rewards=[eps[i].total_reward[0]], length=eps[i].length,
+        done_eps = [dict(total_rewards=list(eps[i].total_reward[:P]), length=eps[i].length,
                          env_index=eps[i].env_index) for i in range(min(n.value, cap))]
-        return obs, rew.reshape(N, 1), dn.astype(bool), done_eps
+        return obs, rew.reshape(N, P), dn.astype(bool), done_eps
 
 
 class ActorCritic:
@@ -181,14 +201,18 @@ class ActorCritic:
         p = np.ascontiguousarray(p, np.float32)
         self.ctx._chk(L.lib().bppo_params_set(self.ctx.h, p.ctypes.data, p.size))
 
-    def forward(self, obs):
-        """network/mod.rs:93-114 -> (logits [B, A], values [B, 1])"""
+    def forward(self, obs, priv=None):
+        """network/mod.rs:93-114 (MLP) / forward_actor + forward_critic (CTDE, ctde.rs:132-183)
+        -> (logits [B, A], values [B, 1]); priv [B, 120] is required for CTDE."""
         obs = np.ascontiguousarray(obs, np.float32).reshape(-1, self.ctx.obs_dim)
         B = obs.shape[0]
+        pr = None
+        if priv is not None:
+            pr = np.ascontiguousarray(priv, np.float32).reshape(B, -1)
         lg = np.zeros((B, self.ctx.num_actions), np.float32)
         v = np.zeros(B, np.float32)
-        self.ctx._chk(L.lib().bppo_forward(self.ctx.h, obs.ctypes.data, None, B, lg.ctypes.data,
-                                           v.ctypes.data))
+        self.ctx._chk(L.lib().bppo_forward(self.ctx.h, obs.ctypes.data, None if pr is None else pr.ctypes.data,
+                                           B, lg.ctypes.data, v.ctypes.data))
         return lg, v.reshape(B, 1)
 
 
@@ -207,6 +231,14 @@ class RolloutBuffer:
             return ctx.buffer("actions", np.int32).reshape(T, N)
         if name in ("rewards", "dones", "values", "log_probs", "advantages", "returns"):
             return ctx.buffer(name).reshape(T, N)
+        if name == "privileged_obs" and ctx.priv_dim:
+            return ctx.buffer("priv").reshape(T, N, ctx.priv_dim)
+        if name == "action_masks" and ctx.has_masks:
+            return ctx.buffer("masks").reshape(T, N, ctx.num_actions)
+        if name == "acting_players":
+            return ctx.buffer("players", np.int32).reshape(T, N)
+        if name == "all_rewards":
+            return ctx.buffer("all_rewards").reshape(T, N, ctx.num_players)
         raise AttributeError(name)
 
 

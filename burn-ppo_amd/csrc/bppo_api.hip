@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstring>
 #include "bppo_internal.h"
+#include "bppo_wide.h"
 
 using namespace bppo;
 
@@ -106,11 +107,8 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     case BPPO_ENV_LIARS_DICE: c->D = 270; c->A = 49; c->P = 4; c->G = cfg->ctde ? 120 : 0; break;
     default: c->err = "unknown env_kind"; return BPPO_ERR_ARG;
     }
-    if (cfg->env_kind != BPPO_ENV_CARTPOLE) {
-        c->err = "device rollout path implemented for CartPole only in this build "
-                 "(Connect Four / Liar's Dice: oracle + multiplayer GAE kernel only)";
-        return BPPO_ERR_UNSUPPORTED;
-    }
+    c->wide = cfg->env_kind != BPPO_ENV_CARTPOLE;
+    if (c->wide && !cfg->ctde) c->G = 0;
     c->net = make_layout(*cfg, c->D, c->G, c->A);
     const size_t np = c->net.n_params;
     const size_t TN = (size_t)c->T * c->N;
@@ -120,13 +118,13 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     TRY(dalloc(c, &c->d_m2, np));
     TRY(dalloc(c, &c->d_grad, np + 64));
     c->slab_rows = 256 * 4;   // one 4-wave block per CU, persistent over the minibatch
-    TRY(dalloc(c, &c->d_slab, c->slab_rows * (np + 64)));
+    if (!c->wide) TRY(dalloc(c, &c->d_slab, c->slab_rows * (np + 64)));
     TRY(dalloc(c, &c->d_cp, (size_t)4 * c->N));
     TRY(dalloc(c, &c->d_steps, (size_t)c->N));
     TRY(dalloc(c, &c->d_env_pos, (size_t)c->N));
     TRY(dalloc(c, &c->d_ep_ret, (size_t)c->N * c->P));
     TRY(dalloc(c, &c->d_ep_len, (size_t)c->N));
-    TRY(dalloc(c, &c->d_obs, TN * c->D));
+    if (!c->wide) TRY(dalloc(c, &c->d_obs, TN * c->D));
     TRY(dalloc(c, &c->d_rew, TN));
     TRY(dalloc(c, &c->d_rew_raw, TN));
     TRY(dalloc(c, &c->d_done, TN));
@@ -135,9 +133,9 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     TRY(dalloc(c, &c->d_adv, TN));
     TRY(dalloc(c, &c->d_ret, TN));
     TRY(dalloc(c, &c->d_act, TN));
-    TRY(dalloc(c, &c->d_X, TN));
+    if (!c->wide) TRY(dalloc(c, &c->d_X, TN));
     TRY(dalloc(c, &c->d_on, (size_t)2 * c->D + 1));
-    TRY(dalloc(c, &c->d_obs_part, (size_t)c->N * 2 * c->D));
+    if (!c->wide) TRY(dalloc(c, &c->d_obs_part, (size_t)c->N * 2 * c->D));
     TRY(dalloc(c, &c->d_rn_returns, (size_t)c->N * c->P));
     TRY(dalloc(c, &c->d_rn_stats, 4));
     TRY(dalloc(c, &c->d_scan_agg, (TN + 4095) / 4096 + 1));
@@ -160,7 +158,13 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     c->rng_pos = 0;
     TRY(c->shuf.init(dev, c->rng_key, cfg->rng_stream, (uint32_t)TN, cfg->num_epochs, c->err));
     c->on_mean.assign(c->D, 0.0); c->on_m2.assign(c->D, 0.0); c->on_count = 0;
-    TRY(launch_cartpole_reset(c));
+    if (c->wide) {
+        TRY(wide_init(c));
+        TRY(wide_reset(c));
+        TRY(wide_pack(c));
+    } else {
+        TRY(launch_cartpole_reset(c));
+    }
     BPPO_HIP(c, hipStreamSynchronize(c->stream));
     return BPPO_OK;
 }
@@ -178,6 +182,7 @@ extern "C" void bppo_destroy(bppo_ctx *c) {
     if (!c) return;
     c->shuf.shutdown();
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    wide_free(c);
     void *ptrs[] = {c->d_params, c->d_m1, c->d_m2, c->d_grad, c->d_slab, c->d_cp, c->d_steps,
                     c->d_env_pos, c->d_ep_ret, c->d_ep_len, c->d_obs, c->d_rew, c->d_rew_raw,
                     c->d_done, c->d_val, c->d_logp, c->d_adv, c->d_ret, c->d_act, c->d_X, c->d_on,
@@ -199,6 +204,7 @@ extern "C" size_t bppo_num_params(const bppo_ctx *c) { return c ? c->net.n_param
 extern "C" bppo_status bppo_params_set(bppo_ctx *c, const float *h, size_t n) {
     if (!c || !h || n != c->net.n_params) { if (c) c->err = "params_set: size mismatch"; return BPPO_ERR_ARG; }
     BPPO_HIP(c, hipMemcpyAsync(c->d_params, h, n * 4, hipMemcpyHostToDevice, c->stream));
+    if (c->wide) TRY(wide_pack(c));
     BPPO_HIP(c, hipStreamSynchronize(c->stream));
     return BPPO_OK;
 }
@@ -212,8 +218,8 @@ extern "C" bppo_status bppo_params_get(bppo_ctx *c, float *h, size_t n) {
 
 extern "C" bppo_status bppo_forward(bppo_ctx *c, const float *obs, const float *priv, int32_t B,
                                     float *logits, float *values) {
-    (void)priv;
     if (!c || !obs || B <= 0) return BPPO_ERR_ARG;
+    if (c->wide) return wide_forward_host(c, obs, priv, B, logits, values);
     float *d_o = nullptr, *d_l = nullptr, *d_v = nullptr;
     BPPO_HIP(c, hipMalloc((void **)&d_o, sizeof(float) * (size_t)B * c->D));
     BPPO_HIP(c, hipMalloc((void **)&d_l, sizeof(float) * (size_t)B * c->A));
@@ -243,7 +249,7 @@ extern "C" bppo_status bppo_rng_set(bppo_ctx *c, uint64_t p) {
 
 extern "C" bppo_status bppo_vecenv_reset(bppo_ctx *c) {
     if (!c) return BPPO_ERR_ARG;
-    TRY(launch_cartpole_reset(c));
+    TRY(c->wide ? wide_reset(c) : launch_cartpole_reset(c));
     BPPO_HIP(c, hipStreamSynchronize(c->stream));
     return BPPO_OK;
 }
@@ -252,6 +258,7 @@ extern "C" bppo_status bppo_vecenv_observe(bppo_ctx *c, float *obs, int32_t *pla
                                            float *priv) {
     (void)priv; (void)masks;
     if (!c) return BPPO_ERR_ARG;
+    if (c->wide) return wide_observe_host(c, obs, players, masks, priv);
     if (obs) {
         float *d = nullptr;
         BPPO_HIP(c, hipMalloc((void **)&d, sizeof(float) * (size_t)c->N * c->D));
@@ -268,6 +275,25 @@ extern "C" bppo_status bppo_vecenv_step(bppo_ctx *c, const int32_t *actions, flo
                                         uint8_t *dones, bppo_episode *eps, int32_t cap, int32_t *n_eps) {
     if (!c || !actions) return BPPO_ERR_ARG;
     const int N = c->N;
+    if (c->wide) {
+        BPPO_HIP(c, hipMemsetAsync(c->d_ep_count, 0, 4, c->stream));
+        int32_t cnt = 0;
+        TRY(wide_step_host(c, actions, obs, rewards, dones, &cnt));
+        if (n_eps) *n_eps = cnt;
+        if (eps && cap > 0 && cnt > 0) {
+            std::vector<EpisodeRec> recs(std::min(cnt, c->eps_cap));
+            BPPO_HIP(c, hipMemcpy(recs.data(), c->d_eps, sizeof(EpisodeRec) * recs.size(), hipMemcpyDeviceToHost));
+            std::sort(recs.begin(), recs.end(), [](const EpisodeRec &a, const EpisodeRec &b) {
+                return a.env_index < b.env_index; });
+            for (int i = 0; i < (int)recs.size() && i < cap; i++) {
+                std::memcpy(eps[i].total_reward, recs[i].total_reward, sizeof(float) * 4);
+                eps[i].length = recs[i].length; eps[i].env_index = recs[i].env_index;
+                eps[i].step = recs[i].step; eps[i].pad = 0;
+            }
+        }
+        c->global_step += N;
+        return BPPO_OK;
+    }
     int32_t *d_a = nullptr; float *d_r = nullptr, *d_o = nullptr; uint8_t *d_d = nullptr;
     BPPO_HIP(c, hipMalloc((void **)&d_a, sizeof(int32_t) * N));
     BPPO_HIP(c, hipMalloc((void **)&d_r, sizeof(float) * N));
@@ -358,7 +384,8 @@ extern "C" bppo_status bppo_collect_rollouts(bppo_ctx *c, bppo_rollout_info *inf
     BPPO_HIP(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
     const uint64_t base = c->rng_pos;
     tm_begin(c, TM_ROLLOUT);
-    TRY(launch_cartpole_rollout(c, base, nullptr, nullptr, c->cfg.normalize_obs));
+    if (c->wide) TRY(wide_collect(c, base));
+    else TRY(launch_cartpole_rollout(c, base, nullptr, nullptr, c->cfg.normalize_obs));
     tm_end(c, TM_ROLLOUT);
     c->rng_pos = base + TN * (uint64_t)c->A;   // one word per (env, action) per step
     // this update's shuffles start here; the engine usually began them already
@@ -366,7 +393,7 @@ extern "C" bppo_status bppo_collect_rollouts(bppo_ctx *c, bppo_rollout_info *inf
     if (c->cfg.normalize_obs) TRY(launch_obs_norm_merge(c));       // ppo.rs:495-497
     tm_begin(c, TM_RETNORM);
     if (c->cfg.normalize_returns) TRY(launch_return_norm(c));      // ppo.rs:390-408
-    else BPPO_HIP(c, hipMemcpyAsync(c->d_rew, c->d_rew_raw, TN * 4, hipMemcpyDeviceToDevice, c->stream));
+    else if (!c->wide) BPPO_HIP(c, hipMemcpyAsync(c->d_rew, c->d_rew_raw, TN * 4, hipMemcpyDeviceToDevice, c->stream));
     tm_end(c, TM_RETNORM);
     int32_t hv[2] = {0, 0};
     BPPO_HIP(c, hipMemcpyAsync(&hv[0], c->d_ep_count, 4, hipMemcpyDeviceToHost, c->stream));
@@ -375,6 +402,7 @@ extern "C" bppo_status bppo_collect_rollouts(bppo_ctx *c, bppo_rollout_info *inf
     tm_read(c, TM_ROLLOUT); tm_read(c, TM_RETNORM);
     c->collected = 1; c->gae_done = 0;
     c->global_step += TN;
+    if (hv[1] & 2) { c->err = "Empty action mask: an env has no valid action"; return BPPO_ERR_EMPTY_MASK; }
     if (hv[1]) { c->err = "NaN/Inf in log probs — model producing corrupt logits"; return BPPO_ERR_NONFINITE; }
     if (info) {
         info->episodes = hv[0];
@@ -414,6 +442,15 @@ extern "C" bppo_status bppo_rollout_episodes(bppo_ctx *c, bppo_episode *eps, int
 // bootstrap + GAE (main.rs:877-947)
 extern "C" bppo_status bppo_compute_gae(bppo_ctx *c) {
     if (!c || !c->collected) { if (c) c->err = "compute_gae before collect_rollouts"; return BPPO_ERR_ARG; }
+    if (c->wide) {
+        tm_begin(c, TM_GAE);
+        TRY(wide_bootstrap_gae(c));
+        tm_end(c, TM_GAE);
+        BPPO_HIP(c, hipStreamSynchronize(c->stream));
+        tm_read(c, TM_GAE);
+        c->gae_done = 1;
+        return BPPO_OK;
+    }
     tm_begin(c, TM_BOOT);
     TRY(launch_bootstrap(c, nullptr, nullptr, c->cfg.normalize_obs));
     tm_end(c, TM_BOOT);
@@ -438,7 +475,7 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
     const int M = c->cfg.num_minibatches;
     const size_t base_mb = B / M, rem = B % M;
     const int np = (int)c->net.n_params;
-    const int NM = 11;
+    const int NM = WM_COUNT;
     std::vector<float> rows;          // per minibatch: NM metric sums + 4 adv stats
     int epochs_run = 0;
     bool stop = false;
@@ -457,7 +494,12 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
             const size_t sz = base_mb + ((size_t)mb < rem ? 1 : 0);
             if (sz == 0) continue;
             (void)hipEventRecord(c->ev[TM_FWDBWD][0], c->stream);
-            TRY(launch_minibatch(c, (uint32_t)start, (uint32_t)sz, (float)ent_coef, nullptr));
+            if (c->wide) {
+                TRY(launch_adv_stats(c, (uint32_t)start, (uint32_t)sz));
+                TRY(wide_minibatch(c, (uint32_t)start, (uint32_t)sz, (float)ent_coef));
+            } else {
+                TRY(launch_minibatch(c, (uint32_t)start, (uint32_t)sz, (float)ent_coef, nullptr));
+            }
             (void)hipEventRecord(c->ev[TM_FWDBWD][1], c->stream);
             if (c->allreduce && c->world > 1) {
                 BPPO_HIP(c, hipStreamSynchronize(c->stream));
@@ -473,6 +515,7 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
                 c2[t] = 1.0f - powi_f32(0.999f, ti);
             }
             TRY(launch_adam(c, (float)lr, c1, c2));
+            if (c->wide) TRY(wide_pack(c));
             // metric row: grad[np .. np+NM) and adv stats
             std::vector<float> row(NM + 4);
             BPPO_HIP(c, hipMemcpyAsync(row.data(), c->d_grad + np, sizeof(float) * NM, hipMemcpyDeviceToHost, c->stream));
@@ -504,6 +547,7 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
         const int nup = (int)(rows.size() / (NM + 4));
         float tp = 0, tv = 0, th = 0, tk = 0, tc = 0, tl = 0, tvm = 0, trm = 0, tam = 0, tas = 0;
         float tamin = INFINITY, tamax = -INFINITY, tvem = 0, tves = 0, tvemax = -INFINITY;
+        float tav = 0, tevp = 0;
         for (int u = 0; u < nup; u++) {
             const float *r = &rows[(size_t)u * (NM + 4)];
             const float n = r[10] > 0 ? r[10] : 1.0f;
@@ -516,6 +560,8 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
             const double var = n > 1 ? ((double)r[8] - (double)n * vem * vem) / (double)(n - 1) : 0.0;
             tves += sqrtf((float)std::max(var, 0.0));
             tvemax = std::max(tvemax, r[9]);
+            tav += r[WM_VALID] / n;
+            tevp += r[WM_NCHOICE] > 0 ? r[WM_HV] / r[WM_NCHOICE] : 0.0f;
             tam += r[NM]; tas += r[NM + 1];
             tamin = std::min(tamin, r[NM + 2]); tamax = std::max(tamax, r[NM + 3]);
         }
@@ -530,6 +576,7 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
         const double mr = ev4[0] / Bn, vr = ev4[1] / Bn - mr * mr;
         const double mres = ev4[2] / Bn, vres = ev4[3] / Bn - mres * mres;
         m->explained_variance = vr < 1e-8 ? 0.0f : (float)(1.0 - vres / vr);
+        if (c->wide) { m->avg_valid_actions = tav / n; m->entropy_valid_pct = tevp / n; }
         m->num_updates = nup; m->epochs_run = epochs_run;
     }
     c->collected = 0; c->gae_done = 0;
@@ -563,6 +610,11 @@ static BufDesc find_buf(bppo_ctx *c, const char *name) {
 
 extern "C" bppo_status bppo_buffer_get(bppo_ctx *c, const char *name, void *host, size_t bytes) {
     if (!c || !name || !host) return BPPO_ERR_ARG;
+    if (c->wide) {
+        bool handled = false;
+        bppo_status s = wide_buffer_get(c, name, host, bytes, &handled);
+        if (handled) return s;
+    }
     BufDesc b = find_buf(c, name);
     if (!b.ptr || bytes < b.bytes) { c->err = std::string("buffer_get: unknown buffer or too small: ") + name; return BPPO_ERR_ARG; }
     BPPO_HIP(c, hipMemcpyAsync(host, b.ptr, b.bytes, hipMemcpyDeviceToHost, c->stream));

@@ -164,6 +164,31 @@ struct bppo_ctx {
     bppo_allreduce_fn allreduce = nullptr;
     void *allreduce_user = nullptr;
     int world = 1;
+    // ---- multi-player ("wide") path: Connect Four / Liar's Dice (wide_api.hip)
+    int wide = 0;                     // env_kind != CartPole
+    int L = 0;                        // rollout row length G + D: [priv | obs]
+    int rows_max = 0;                 // max(N, largest minibatch): rows of the activation buffers
+    void *d_wstate = nullptr;         // per-env state structs [N]
+    float *d_xc = nullptr;            // rollout rows [T][N][L]
+    uint8_t *d_mask = nullptr;        // action masks [T][N][A] (0/1)
+    int32_t *d_players = nullptr;     // acting player [T][N]
+    float *d_allr = nullptr;          // all_rewards [T][N][P]
+    float *d_lvpp = nullptr;          // last_value_per_player [N][P]
+    float *d_hbuf = nullptr;          // hidden activations, layer l at hoff[l], [rows][out[l]]
+    size_t hoff[16] = {};
+    float *d_logits = nullptr, *d_values = nullptr;  // forward outputs [rows][A], [rows]
+    float *d_xcg = nullptr;           // gathered minibatch rows [mb][L]
+    float *d_dout = nullptr;          // dL/d[logits | value] [mb][A+1]
+    float *d_dz[2] = {nullptr, nullptr};            // backward ping-pong [mb][Wmax]
+    float *d_heads = nullptr, *d_heads_b = nullptr; // packed shared-trunk heads [W][A+1], [A+1]
+    float *d_part = nullptr, *d_colsum = nullptr;   // split-K weight-grad scratch
+    double *d_mpart = nullptr;        // loss-metric partials
+    float *d_bxc = nullptr;           // bootstrap / VecEnv scratch rows [N][L]
+    uint8_t *d_bmask = nullptr;
+    int32_t *d_bplayers = nullptr;
+    int32_t *d_act_in = nullptr;      // VecEnv::step actions [N]
+    float *d_scr_r = nullptr;         // VecEnv::step rewards [N][P]
+    uint8_t *d_scr_d = nullptr;       // VecEnv::step dones [N]
     // timing
     hipEvent_t ev[8][2] = {};
     float last_ms[8] = {0};
@@ -197,10 +222,26 @@ bppo_status launch_return_norm(bppo_ctx *c);
 bppo_status launch_fisher_yates(bppo_ctx *c, const uint32_t *d_J, uint32_t n);
 hipError_t fisher_yates_device(const uint32_t *d_J, uint32_t n, uint32_t *scratch, uint32_t *scan, uint32_t *perm,
                                hipStream_t st);
+bppo_status launch_adv_stats(bppo_ctx *c, uint32_t start, uint32_t n);
 bppo_status launch_minibatch(bppo_ctx *c, uint32_t mb_start, uint32_t mb_size, float ent_coef,
                              double *h_stats_out);
 bppo_status launch_adam(bppo_ctx *c, float lr, const float *c1, const float *c2);
 bppo_status launch_explained_variance(bppo_ctx *c, double *out6);
+// (wide_api.hip) multi-player path
+bppo_status wide_init(bppo_ctx *c);
+void wide_free(bppo_ctx *c);
+bppo_status wide_reset(bppo_ctx *c);
+bppo_status wide_pack(bppo_ctx *c);
+bppo_status wide_forward(bppo_ctx *c, int rows, const float *xc, int ldxc, float *logits, float *values);
+bppo_status wide_collect(bppo_ctx *c, uint64_t base);
+bppo_status wide_bootstrap_gae(bppo_ctx *c);
+bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_coef);
+bppo_status wide_observe_host(bppo_ctx *c, float *obs, int32_t *players, uint8_t *masks, float *priv);
+bppo_status wide_step_host(bppo_ctx *c, const int32_t *actions, float *obs, float *rewards, uint8_t *dones,
+                           int32_t *n_eps);
+bppo_status wide_forward_host(bppo_ctx *c, const float *obs, const float *priv, int B, float *logits,
+                              float *values);
+bppo_status wide_buffer_get(bppo_ctx *c, const char *name, void *host, size_t bytes, bool *handled);
 // libm device check
 bppo_status launch_libm(int which, const float *d_x, float *d_y, size_t n);
 

@@ -400,16 +400,23 @@ __global__ void __launch_bounds__(256) k_ev(size_t n, const float *val, const fl
 }
 
 // ------------------------------------------------------------- launchers ---
-bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_coef,
-                             double *) {
-    const int h = c->cfg.hidden_size, nl = c->cfg.num_hidden;
-    // advantage stats (2 passes) -> d_mb_stats
+// raw advantage stats of the minibatch (ppo.rs:1905-1913, utils.rs:80-89) -> d_mb_stats
+bppo_status launch_adv_stats(bppo_ctx *c, uint32_t start, uint32_t n) {
     for (int pass = 0; pass < 2; pass++) {
         hipLaunchKernelGGL(k_adv_pass, dim3(STAT_BLOCKS), dim3(256), 0, c->stream, c->d_adv, c->d_perm,
                            start, n, c->d_mb_stats, pass, c->d_red);
         hipLaunchKernelGGL(k_adv_finalize, dim3(1), dim3(64), 0, c->stream, c->d_red, STAT_BLOCKS, n,
                            pass, c->d_mb_stats);
     }
+    BPPO_HIP(c, hipGetLastError());
+    return BPPO_OK;
+}
+
+bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_coef,
+                             double *) {
+    const int h = c->cfg.hidden_size, nl = c->cfg.num_hidden;
+    bppo_status st = launch_adv_stats(c, start, n);
+    if (st != BPPO_OK) return st;
     MbArgs g;
     g.obs = c->d_obs; g.logp = c->d_logp; g.adv = c->d_adv; g.ret = c->d_ret; g.val = c->d_val;
     g.act = c->d_act; g.perm = c->d_perm; g.start = start; g.n = n; g.params = c->d_params;

@@ -1,0 +1,171 @@
+"""Parity of the multi-player path (Connect Four, Liar's Dice MLP and CTDE)
+through libbppo.so against the CPU oracle on identical seeds.
+
+Bit-exact: env transitions (observations, privileged obs, action masks, acting
+players, rewards, dones, episode records), masked Gumbel-max actions, log-probs,
+values (the MFMA GEMM forward reproduces matrixmultiply's fma chains), the main
+RNG position, multiplayer GAE.  The update (gradients reduced in a different
+order) is within rtol 1e-4 / atol 2e-5 on the parameters after Adam."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import bppo
+import bppo._lib as L
+import oracle_ffi as O
+
+pytestmark = pytest.mark.gpu
+
+ENV = {"connect_four": (O.ENV_CONNECT_FOUR, 86, 7, 2, 0), "liars_dice": (O.ENV_LIARS_DICE, 270, 49, 4, 120)}
+
+
+# --------------------------------------------------------------- VecEnv ---
+@pytest.mark.parametrize("env", ["connect_four", "liars_dice"])
+def test_vecenv_matches_oracle(env):
+    kind, D, A, P, G = ENV[env]
+    N = 300
+    preset = "connect_four" if env == "connect_four" else "liars_dice_ctde"
+    cfg = bppo.make_config(preset, num_envs=N, num_steps=4, reward_shaping_coef=0.05 if G else 0.0)
+    ctx = bppo.Context(cfg)
+    ve = bppo.VecEnv.new(ctx)
+    ov = O.lib().or_vecenv_new(kind, N, cfg["seed"])
+    O.lib().or_vecenv_set_shaping(ov, cfg["reward_shaping_coef"])
+    obs_o = np.zeros(N * D, np.float32)
+    m_o = np.zeros(N * A, np.uint8)
+    pl_o = np.zeros(N, np.int32)
+    g_o = np.zeros(max(N * G, 1), np.float32)
+    rw = np.zeros(N * P, np.float32); dn = np.zeros(N, np.uint8)
+    eps = (O.Episode * N)()
+    rng = np.random.default_rng(1)
+    n_done = 0
+    for t in range(400):
+        O.lib().or_vecenv_get_obs(ov, obs_o)
+        O.lib().or_vecenv_get_masks(ov, m_o)
+        O.lib().or_vecenv_get_players(ov, pl_o)
+        assert np.array_equal(ve.get_observations(), obs_o), t
+        assert np.array_equal(ve.get_action_masks(), m_o.astype(bool)), t
+        assert np.array_equal(ve.get_current_players(), pl_o), t
+        if G:
+            O.lib().or_vecenv_get_priv(ov, g_o)
+            assert np.array_equal(ve.get_privileged_obs(), g_o), t
+        # a random VALID action per env (an invalid one now and then: the env's own rule)
+        m = m_o.reshape(N, A).astype(bool)
+        a = np.array([rng.choice(np.flatnonzero(row)) for row in m], np.int32)
+        bad = rng.random(N) < 0.002
+        a[bad] = rng.integers(0, A, bad.sum())
+        o, r, d, ep = ve.step(a)
+        ne = O.lib().or_vecenv_step(ov, a, obs_o, rw, dn, eps, N)
+        assert np.array_equal(o, obs_o), t
+        assert np.array_equal(r.reshape(-1), rw), t
+        assert np.array_equal(d, dn.astype(bool)), t
+        assert len(ep) == ne
+        for i, e in enumerate(ep):
+            assert e["env_index"] == eps[i].env_index and e["length"] == eps[i].length
+            assert np.array_equal(np.float32(e["total_rewards"]), np.float32(eps[i].total_rewards[:P]))
+        n_done += int(d.sum())
+    assert n_done > 50
+    O.lib().or_vecenv_free(ov)
+    ctx.close()
+
+
+# -------------------------------------------------------------- rollout ---
+def _pair(env, N, T, seed=42, ctde=None, **kw):
+    kind, D, A, P, G = ENV[env]
+    if env == "connect_four":
+        cfg = bppo.make_config("connect_four", num_envs=N, num_steps=T, seed=seed, **kw)
+    else:
+        cfg = bppo.make_config("liars_dice_ctde", num_envs=N, num_steps=T, seed=seed, **kw)
+        if ctde is False:
+            cfg.update(network_type="mlp", hidden_size=128)
+    params = bppo.orthogonal_init(cfg, seed=5)
+    tr = bppo.Trainer(cfg, params=params)
+    is_ctde = cfg["network_type"] == "ctde"
+    ocfg = O.train_cfg(env_kind=kind, num_envs=N, num_steps=T, seed=seed, hidden=cfg["hidden_size"],
+                       num_hidden=cfg["num_hidden"], ctde=is_ctde,
+                       critic_hidden=cfg["critic_hidden_size"] or 0,
+                       critic_num_hidden=cfg["critic_num_hidden"] or 0, normalize_obs=False,
+                       normalize_returns=False, gamma=cfg["gamma"], gae_lambda=cfg["gae_lambda"],
+                       lr=bppo.schedule_get(cfg["learning_rate"], 0),
+                       ent_coef=bppo.schedule_get(cfg["entropy_coef"], 0),
+                       reward_shaping=cfg["reward_shaping_coef"], num_epochs=cfg["num_epochs"],
+                       num_minibatches=cfg["num_minibatches"], clip=cfg["clip_epsilon"],
+                       value_coef=cfg["value_coef"], target_kl=cfg["target_kl"])
+    ot = O.Trainer(ocfg, params)
+    return cfg, tr, ot
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def _cmp_rollout(env, tr, ot):
+    kind, D, A, P, G = ENV[env]
+    b = tr.buffer
+    assert np.array_equal(b.acting_players.reshape(-1), ot.buffer("players", np.int32))
+    assert np.array_equal(_bits(b.observations.reshape(-1)), _bits(ot.buffer("obs")))
+    assert np.array_equal(b.action_masks.reshape(-1), ot.buffer("masks"))
+    if G and tr.model.is_ctde():
+        assert np.array_equal(_bits(b.privileged_obs.reshape(-1)), _bits(ot.buffer("priv")))
+    assert np.array_equal(b.actions.reshape(-1), ot.buffer("actions", np.int32))
+    assert np.array_equal(_bits(b.values.reshape(-1)), _bits(ot.buffer("values")))
+    assert np.array_equal(_bits(b.log_probs.reshape(-1)), _bits(ot.buffer("log_probs")))
+    assert np.array_equal(b.dones.reshape(-1), ot.buffer("dones"))
+    assert np.array_equal(_bits(b.rewards.reshape(-1)), _bits(ot.buffer("rewards")))
+    assert np.array_equal(_bits(b.all_rewards.reshape(-1)), _bits(ot.buffer("all_rewards")))
+    assert tr.ctx.rng_pos() == ot.rng_pos()
+
+
+CASES = [("connect_four", 64, 16, None), ("liars_dice", 48, 16, None), ("liars_dice", 40, 12, False)]
+
+
+@pytest.mark.parametrize("env,N,T,ctde", CASES)
+def test_rollout_and_gae_bit_exact(env, N, T, ctde):
+    cfg, tr, ot = _pair(env, N, T, ctde=ctde)
+    info = bppo.collect_rollouts(tr.ctx)
+    n_eps = ot.collect()
+    _cmp_rollout(env, tr, ot)
+    assert info.episodes == n_eps
+    bppo.compute_gae(tr.ctx)
+    ot.gae()
+    assert np.array_equal(_bits(tr.ctx.buffer("last_v_pp")), _bits(ot.buffer("last_v_pp")))
+    assert np.array_equal(_bits(tr.buffer.advantages.reshape(-1)), _bits(ot.buffer("advantages")))
+    assert np.array_equal(_bits(tr.buffer.returns.reshape(-1)), _bits(ot.buffer("returns")))
+    tr.close(); ot.close()
+
+
+@pytest.mark.parametrize("env,N,T,ctde", CASES)
+def test_update_then_second_rollout(env, N, T, ctde):
+    cfg, tr, ot = _pair(env, N, T, ctde=ctde)
+    bppo.collect_rollouts(tr.ctx); ot.collect()
+    bppo.compute_gae(tr.ctx); ot.gae()
+    lr = bppo.schedule_get(cfg["learning_rate"], 0)
+    ent = bppo.schedule_get(cfg["entropy_coef"], 0)
+    m = bppo.ppo_update(tr.ctx, lr, ent)
+    om = ot.update()
+    assert m["epochs_run"] == om["epochs_run"] and m["num_updates"] == om["num_updates"]
+    assert tr.ctx.rng_pos() == ot.rng_pos()
+    for k in ("policy_loss", "value_loss", "entropy", "approx_kl", "clip_fraction", "avg_valid_actions",
+              "entropy_valid_pct", "explained_variance"):
+        assert abs(m[k] - om[k]) <= 2e-5 + 1e-4 * abs(om[k]), (k, m[k], om[k])
+    np.testing.assert_allclose(tr.model.get_params(), ot.params(), rtol=1e-4, atol=2e-5)
+    # the next rollout from the oracle's parameters is bit-identical again
+    tr.model.set_params(ot.params())
+    bppo.collect_rollouts(tr.ctx); ot.collect()
+    _cmp_rollout(env, tr, ot)
+    tr.close(); ot.close()
+
+
+def test_forward_matches_oracle_ctde():
+    cfg = bppo.make_config("liars_dice_ctde", num_envs=16, num_steps=2)
+    params = bppo.orthogonal_init(cfg, seed=9)
+    tr = bppo.Trainer(cfg, params=params)
+    rng = np.random.default_rng(0)
+    obs = (rng.random((300, 270)) < 0.1).astype(np.float32)
+    priv = rng.random((300, 120)).astype(np.float32)
+    lg, v = tr.model.forward(obs, priv)
+    d = O.ctde_desc(270, 120, 49, 256, 2, 512, 3)
+    lo, vo = O.net_forward(d, params, obs, priv)
+    assert np.array_equal(_bits(lg), _bits(lo))
+    assert np.array_equal(_bits(v.reshape(-1)), _bits(vo))
+    tr.close()
