@@ -117,8 +117,10 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     TRY(dalloc(c, &c->d_m1, np));
     TRY(dalloc(c, &c->d_m2, np));
     TRY(dalloc(c, &c->d_grad, np + 64));
-    c->slab_rows = 256 * 4;   // one 4-wave block per CU, persistent over the minibatch
+    c->slab_rows = 256 * 8;   // one 8-wave (MFMA) or 4-wave block per CU, persistent over the minibatch
+    c->relu_mfma = cfg->relu ? 1 : 0;
     if (!c->wide) TRY(dalloc(c, &c->d_slab, c->slab_rows * (np + 64)));
+    if (!c->wide) TRY(dalloc(c, &c->d_slab_part, (size_t)32 * (np + 64)));
     TRY(dalloc(c, &c->d_cp, (size_t)4 * c->N));
     TRY(dalloc(c, &c->d_steps, (size_t)c->N));
     TRY(dalloc(c, &c->d_env_pos, (size_t)c->N));
@@ -183,7 +185,7 @@ extern "C" void bppo_destroy(bppo_ctx *c) {
     c->shuf.shutdown();
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     wide_free(c);
-    void *ptrs[] = {c->d_params, c->d_m1, c->d_m2, c->d_grad, c->d_slab, c->d_cp, c->d_steps,
+    void *ptrs[] = {c->d_params, c->d_m1, c->d_m2, c->d_grad, c->d_slab, c->d_slab_part, c->d_cp, c->d_steps,
                     c->d_env_pos, c->d_ep_ret, c->d_ep_len, c->d_obs, c->d_rew, c->d_rew_raw,
                     c->d_done, c->d_val, c->d_logp, c->d_adv, c->d_ret, c->d_act, c->d_X, c->d_on,
                     c->d_obs_part, c->d_rn_returns, c->d_rn_stats, c->d_scan_agg, c->d_last_v,

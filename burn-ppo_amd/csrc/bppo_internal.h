@@ -119,7 +119,10 @@ struct bppo_ctx {
     float *d_grad = nullptr;          // [n_params + metric slots]
     double *d_grad64 = nullptr;
     float *d_slab = nullptr;          // per-wave partial gradients
+    double *d_slab_part = nullptr;    // row-group partials of the slab reduction [32][np + 64]
     size_t slab_rows = 0;
+    int slab_used = 0;                // waves that wrote a row in the last minibatch launch
+    int relu_mfma = 1;                // CfgB net (64x2 relu): the MFMA minibatch kernel
     // env state (CartPole SoA)
     float *d_cp = nullptr;            // x, x_dot, theta, theta_dot  [4][N]
     int32_t *d_steps = nullptr;

@@ -52,14 +52,28 @@ __global__ void __launch_bounds__(256) k_adv_pass(const float *adv, const uint32
 }
 
 // mb_stats: [0] mean (f32), [1] std (f32, unbiased), [2] min, [3] max
-__global__ void k_adv_finalize(const double *part, int nblk, uint32_t n, int pass, float *mb_stats) {
-    if (threadIdx.x != 0) return;
+// 256 threads: strided partial sums, then a fixed-order LDS tree (deterministic)
+__global__ void __launch_bounds__(256) k_adv_finalize(const double *part, int nblk, uint32_t n, int pass,
+                                                      float *mb_stats) {
+    __shared__ double ss[256], smn[256], smx[256];
     double s = 0.0, mn = INFINITY, mx = -INFINITY;
-    for (int b = 0; b < nblk; b++) {
+    for (int b = threadIdx.x; b < nblk; b += blockDim.x) {
         s += part[b * 3];
         mn = fmin(mn, part[b * 3 + 1]);
         mx = fmax(mx, part[b * 3 + 2]);
     }
+    ss[threadIdx.x] = s; smn[threadIdx.x] = mn; smx[threadIdx.x] = mx;
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+        if (threadIdx.x < st) {
+            ss[threadIdx.x] += ss[threadIdx.x + st];
+            smn[threadIdx.x] = fmin(smn[threadIdx.x], smn[threadIdx.x + st]);
+            smx[threadIdx.x] = fmax(smx[threadIdx.x], smx[threadIdx.x + st]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x != 0) return;
+    s = ss[0]; mn = smn[0]; mx = smx[0];
     if (pass == 0) {
         mb_stats[0] = (float)(s / (double)n);
         mb_stats[2] = (float)mn;
@@ -326,34 +340,374 @@ __global__ void __launch_bounds__(256, 1) k_minibatch(MbArgs g) {
     }
 }
 
-// fixed-order reduction of the wave partials: grad[p] = sum_w slab[w][p]
-__global__ void k_slab_reduce(const float *slab, int rows, int width, float *grad) {
+// ================================================ MFMA minibatch (H=64, NL=2) ==
+// The CfgB network (5 -> 64 -> 64 -> {2, 1}, relu) per wave tile of 32 rows on
+// v_mfma_f32_32x32x2_f32:
+//   forward   H1 = relu(X W0 + b0), H2 = relu(H1 W1 + b1): natural k order (the
+//             MFMA is a k-ordered fma chain), so values equal the rollout's VALU
+//             forward bit for bit and the first-minibatch ratio is exactly 1;
+//             the heads run on the VALU, lane = row, in k order.
+//   backward  dW1 += H1^T dZ2 takes both accumulators straight from the C/D
+//             layout (rows in registers: a permuted but fixed row order inside
+//             the gradient sum); dZ1 = (dZ2 W1^T) * [H1 > 0] on MFMA after one
+//             LDS transpose of dZ2; dW0, biases and the head gradients on the VALU.
+// 8 waves per block (2 per SIMD), one block per CU, persistent over the minibatch.
+namespace mmb {
+constexpr int H = 64, RS = 65, TR = 32;          // hidden width, LDS row stride, rows per wave tile
+struct Params {
+    float W0[6 * H];      // [d][k], d = 5 is a zero pad row (K 5 -> 6)
+    float b0[H];
+    float W1[H * RS];     // [k][o], row stride 65: conflict-free for both operand reads
+    float b1[H];
+    float Wp[H * 2];
+    float bp[2];
+    float Wv[H];
+    float bv[2];
+};
+struct Wave {
+    float X[TR * 9];      // [row][d]
+    float T[TR * RS];     // transpose staging: H1 -> H2 -> dZ2, [row][col]
+    float dl[TR * 4];     // dL/d(logit0, logit1, value) per row
+};
+constexpr int WAVES = 8;
+constexpr size_t LDS = sizeof(Params) + WAVES * sizeof(Wave);
+}  // namespace mmb
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+
+__global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
+    using namespace mmb;
+    constexpr CpOffsets O = cp_offsets<64, 2>();
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    Params &S = *reinterpret_cast<Params *>(smem);
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    Wave &B = reinterpret_cast<Wave *>(smem + sizeof(Params) / 4)[wv];
+    for (int i = tid; i < 6 * H; i += blockDim.x) S.W0[i] = i < 5 * H ? g.params[O.w0 + i] : 0.0f;
+    for (int i = tid; i < H * H; i += blockDim.x) S.W1[(i / H) * RS + (i % H)] = g.params[O.w1 + i];
+    for (int i = tid; i < H; i += blockDim.x) {
+        S.b0[i] = g.params[O.b0 + i]; S.b1[i] = g.params[O.b1 + i]; S.Wv[i] = g.params[O.wv + i];
+        S.Wp[2 * i] = g.params[O.wp + 2 * i]; S.Wp[2 * i + 1] = g.params[O.wp + 2 * i + 1];
+    }
+    if (tid < 2) S.bp[tid] = g.params[O.bp + tid];
+    if (tid == 0) S.bv[0] = g.params[O.bv];
+    __syncthreads();
+
+    const int c = lane & 31, h = lane >> 5;
+    const int gwave = blockIdx.x * WAVES + wv, nwaves = gridDim.x * WAVES;
+    const float mean = g.mb_stats[0], denom = g.mb_stats[1] + 1e-8f;
+    float b0k[2], b1k[2], wpk0[2], wpk1[2], wvk[2];
+#pragma unroll
+    for (int ct = 0; ct < 2; ct++) {
+        const int k = c + 32 * ct;
+        b0k[ct] = S.b0[k]; b1k[ct] = S.b1[k];
+        wpk0[ct] = S.Wp[2 * k]; wpk1[ct] = S.Wp[2 * k + 1]; wvk[ct] = S.Wv[k];
+    }
+    f32x16_t dW1[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+#pragma unroll
+            for (int q = 0; q < 16; q++) dW1[i][j][q] = 0.0f;
+    float gW0[5][2], gb0[2] = {0, 0}, gb1[2] = {0, 0}, gP0[2] = {0, 0}, gP1[2] = {0, 0}, gV[2] = {0, 0};
+#pragma unroll
+    for (int d = 0; d < 5; d++) gW0[d][0] = gW0[d][1] = 0.0f;
+    float gbp0 = 0, gbp1 = 0, gbv = 0;
+    float m_pl = 0, m_vl = 0, m_h = 0, m_kl = 0, m_cf = 0, m_v = 0, m_r = 0, m_ve = 0, m_ve2 = 0;
+    float m_vemax = -INFINITY, m_n = 0;
+
+    for (uint32_t base = (uint32_t)gwave * TR; base < g.n; base += (uint32_t)nwaves * TR) {
+        const uint32_t r = base + c;
+        const bool valid = h == 0 && r < g.n;
+        float x[5] = {0, 0, 0, 0, 0};
+        int a = 0;
+        float olp = 0.0f, A = 0.0f, R = 0.0f, ov = 0.0f;
+        if (valid) {
+            const uint32_t idx = g.perm[g.start + r];
+#pragma unroll
+            for (int d = 0; d < 5; d++) x[d] = g.obs[(size_t)idx * 5 + d];
+            a = g.act[idx]; olp = g.logp[idx]; A = g.adv[idx]; R = g.ret[idx];
+            if (g.clip_value) ov = g.val[idx];
+        }
+        if (h == 0) {
+#pragma unroll
+            for (int d = 0; d < 5; d++) B.X[c * 9 + d] = x[d];
+            B.X[c * 9 + 5] = 0.0f;
+        }
+        wave_sync();
+        // ---- layer 1 (K = 5 padded to 6)
+        f32x16_t h1[2];
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++)
+#pragma unroll
+            for (int q = 0; q < 16; q++) h1[ct][q] = 0.0f;
+#pragma unroll
+        for (int s = 0; s < 3; s++) {
+            const float av = B.X[c * 9 + 2 * s + h];
+#pragma unroll
+            for (int ct = 0; ct < 2; ct++)
+                h1[ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, S.W0[(2 * s + h) * H + c + 32 * ct], h1[ct], 0, 0, 0);
+        }
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++)
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const float v = __fadd_rn(h1[ct][q], b0k[ct]);
+                h1[ct][q] = v > 0.0f ? v : 0.0f;
+                B.T[((q & 3) + 8 * (q >> 2) + 4 * h) * RS + c + 32 * ct] = h1[ct][q];
+            }
+        wave_sync();
+        // ---- layer 2 (K = 64)
+        f32x16_t h2[2];
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++)
+#pragma unroll
+            for (int q = 0; q < 16; q++) h2[ct][q] = 0.0f;
+#pragma unroll 8
+        for (int s = 0; s < 32; s++) {
+            const float av = B.T[c * RS + 2 * s + h];
+            const float bv0 = S.W1[(2 * s + h) * RS + c], bv1 = S.W1[(2 * s + h) * RS + c + 32];
+            h2[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv0, h2[0], 0, 0, 0);
+            h2[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv1, h2[1], 0, 0, 0);
+        }
+        wave_sync();
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++)
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const float v = __fadd_rn(h2[ct][q], b1k[ct]);
+                h2[ct][q] = v > 0.0f ? v : 0.0f;
+                B.T[((q & 3) + 8 * (q >> 2) + 4 * h) * RS + c + 32 * ct] = h2[ct][q];
+            }
+        wave_sync();
+        // ---- heads + loss, lane = row (rows 0..31 on the low half-wave)
+        if (h == 0) {
+            float l0 = 0.0f, l1 = 0.0f, vv = 0.0f;
+            const float *hr = B.T + c * RS;
+#pragma unroll 16
+            for (int k = 0; k < H; k++) {
+                const float hk = hr[k];
+                l0 = __builtin_fmaf(hk, S.Wp[2 * k], l0);
+                l1 = __builtin_fmaf(hk, S.Wp[2 * k + 1], l1);
+                vv = __builtin_fmaf(hk, S.Wv[k], vv);
+            }
+            const float lg0 = __fadd_rn(l0, S.bp[0]), lg1 = __fadd_rn(l1, S.bp[1]), v = __fadd_rn(vv, S.bv[0]);
+            const float An = __fdiv_rn(__fsub_rn(A, mean), denom);   // utils.rs:88
+            const float mx = lg0 > lg1 ? lg0 : lg1;
+            const float e0 = bppo_math::expf_glibc(__fsub_rn(lg0, mx));
+            const float e1 = bppo_math::expf_glibc(__fsub_rn(lg1, mx));
+            const float lse = bppo_math::logf_glibc(__fadd_rn(e0, e1));
+            const float ls0 = __fsub_rn(__fsub_rn(lg0, mx), lse);
+            const float ls1 = __fsub_rn(__fsub_rn(lg1, mx), lse);
+            const float p0 = bppo_math::expf_glibc(ls0), p1 = bppo_math::expf_glibc(ls1);
+            const float Hn = -__fadd_rn(__fmul_rn(p0, ls0), __fmul_rn(p1, ls1));
+            const float newlp = a == 1 ? ls1 : ls0;
+            const float log_ratio = __fsub_rn(newlp, olp);
+            const float ratio = bppo_math::expf_glibc(log_ratio);
+            const float na = -An;
+            const float pl1 = __fmul_rn(na, ratio);
+            const float rc = ratio < g.lo ? g.lo : (ratio > g.hi ? g.hi : ratio);
+            const float pl2 = __fmul_rn(na, rc);
+            const bool rhs = pl1 < pl2;
+            const float pl = rhs ? pl2 : pl1;
+            float vl, dvl;
+            if (g.clip_value) {
+                const float dlt = __fsub_rn(v, ov);
+                const float dc = dlt < -g.ceps ? -g.ceps : (dlt > g.ceps ? g.ceps : dlt);
+                const float vc = __fadd_rn(ov, dc);
+                const float q1 = __fmul_rn(__fsub_rn(v, R), __fsub_rn(v, R));
+                const float q2 = __fmul_rn(__fsub_rn(vc, R), __fsub_rn(vc, R));
+                if (q1 < q2) { vl = q2; dvl = (dlt >= -g.ceps && dlt <= g.ceps) ? 2.0f * __fsub_rn(vc, R) : 0.0f; }
+                else { vl = q1; dvl = 2.0f * __fsub_rn(v, R); }
+            } else {
+                vl = __fmul_rn(__fsub_rn(v, R), __fsub_rn(v, R));
+                dvl = 2.0f * __fsub_rn(v, R);
+            }
+            const float g_ratio = (!rhs || (ratio >= g.lo && ratio <= g.hi)) ? -An * g.inv_mb : 0.0f;
+            const float g_lr = g_ratio * ratio;
+            const float ec = g.ent_coef * g.inv_mb;
+            float dl0 = g_lr * ((a == 0 ? 1.0f : 0.0f) - p0) + ec * p0 * (ls0 + Hn);
+            float dl1 = g_lr * ((a == 1 ? 1.0f : 0.0f) - p1) + ec * p1 * (ls1 + Hn);
+            float dv = g.value_coef * 0.5f * g.inv_mb * dvl;
+            if (!valid) { dl0 = dl1 = dv = 0.0f; }
+            else {
+                const float ve = fabsf(__fsub_rn(v, R));
+                m_pl += pl; m_vl += vl; m_h += Hn; m_kl += (ratio - 1.0f) - log_ratio;
+                m_cf += fabsf(ratio - 1.0f) > g.ceps ? 1.0f : 0.0f;
+                m_v += v; m_r += R; m_ve += ve; m_ve2 += ve * ve; m_vemax = fmaxf(m_vemax, ve);
+                m_n += 1.0f;
+            }
+            gbp0 += dl0; gbp1 += dl1; gbv += dv;
+            B.dl[c * 4 + 0] = dl0; B.dl[c * 4 + 1] = dl1; B.dl[c * 4 + 2] = dv;
+        }
+        wave_sync();
+        // ---- head gradients and dZ2 = ([dl | dv] [Wp | Wv]^T) * [H2 > 0], C/D layout
+        f32x16_t dz2[2];
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            const int row = (q & 3) + 8 * (q >> 2) + 4 * h;
+            const float d0 = B.dl[row * 4], d1 = B.dl[row * 4 + 1], dvr = B.dl[row * 4 + 2];
+#pragma unroll
+            for (int ct = 0; ct < 2; ct++) {
+                const float hv = h2[ct][q];
+                gP0[ct] = __builtin_fmaf(hv, d0, gP0[ct]);
+                gP1[ct] = __builtin_fmaf(hv, d1, gP1[ct]);
+                gV[ct] = __builtin_fmaf(hv, dvr, gV[ct]);
+                float sacc = __builtin_fmaf(d0, wpk0[ct], 0.0f);
+                sacc = __builtin_fmaf(d1, wpk1[ct], sacc);
+                sacc = __builtin_fmaf(dvr, wvk[ct], sacc);
+                dz2[ct][q] = hv > 0.0f ? sacc : 0.0f;
+                gb1[ct] += dz2[ct][q];
+            }
+        }
+        // dW1 += H1^T dZ2 over this tile's rows (both operands in C/D layout)
+#pragma unroll
+        for (int q = 0; q < 16; q++)
+#pragma unroll
+            for (int it = 0; it < 2; it++)
+#pragma unroll
+                for (int jt = 0; jt < 2; jt++)
+                    dW1[it][jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(h1[it][q], dz2[jt][q], dW1[it][jt], 0, 0, 0);
+        // dZ2 -> LDS [row][o] for dZ1 = dZ2 W1^T (sums over dZ2's column index)
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++)
+#pragma unroll
+            for (int q = 0; q < 16; q++)
+                B.T[((q & 3) + 8 * (q >> 2) + 4 * h) * RS + c + 32 * ct] = dz2[ct][q];
+        wave_sync();
+        f32x16_t dz1[2];
+#pragma unroll
+        for (int jt = 0; jt < 2; jt++)
+#pragma unroll
+            for (int q = 0; q < 16; q++) dz1[jt][q] = 0.0f;
+#pragma unroll 8
+        for (int s = 0; s < 32; s++) {
+            const float av = B.T[c * RS + 2 * s + h];
+            const float bw0 = S.W1[c * RS + 2 * s + h], bw1 = S.W1[(c + 32) * RS + 2 * s + h];
+            dz1[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bw0, dz1[0], 0, 0, 0);
+            dz1[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bw1, dz1[1], 0, 0, 0);
+        }
+        // dZ1 masked by relu'(H1); dW0 and db0 on the VALU (lane = hidden unit)
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            const int row = (q & 3) + 8 * (q >> 2) + 4 * h;
+            float xr[5];
+#pragma unroll
+            for (int d = 0; d < 5; d++) xr[d] = B.X[row * 9 + d];
+#pragma unroll
+            for (int jt = 0; jt < 2; jt++) {
+                const float dzv = h1[jt][q] > 0.0f ? dz1[jt][q] : 0.0f;
+                gb0[jt] += dzv;
+#pragma unroll
+                for (int d = 0; d < 5; d++) gW0[d][jt] = __builtin_fmaf(xr[d], dzv, gW0[d][jt]);
+            }
+        }
+        wave_sync();
+    }
+    // ---- this wave's partial gradient row (lane halves hold different rows: combine)
+#pragma unroll
+    for (int ct = 0; ct < 2; ct++) {
+        gb0[ct] += __shfl_xor(gb0[ct], 32, 64); gb1[ct] += __shfl_xor(gb1[ct], 32, 64);
+        gP0[ct] += __shfl_xor(gP0[ct], 32, 64); gP1[ct] += __shfl_xor(gP1[ct], 32, 64);
+        gV[ct] += __shfl_xor(gV[ct], 32, 64);
+#pragma unroll
+        for (int d = 0; d < 5; d++) gW0[d][ct] += __shfl_xor(gW0[d][ct], 32, 64);
+    }
+    float *row = g.slab + (size_t)gwave * (g.np + NUM_M);
+    if (h == 0) {
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++) {
+            const int k = c + 32 * ct;
+#pragma unroll
+            for (int d = 0; d < 5; d++) row[O.w0 + d * H + k] = gW0[d][ct];
+            row[O.b0 + k] = gb0[ct];
+            row[O.b1 + k] = gb1[ct];
+            row[O.wp + 2 * k] = gP0[ct];
+            row[O.wp + 2 * k + 1] = gP1[ct];
+            row[O.wv + k] = gV[ct];
+        }
+    }
+    // dW1[k][o]: accumulator (it, jt) row k = (q&3) + 8(q>>2) + 4h + 32 it, col o = c + 32 jt
+#pragma unroll
+    for (int it = 0; it < 2; it++)
+#pragma unroll
+        for (int jt = 0; jt < 2; jt++)
+#pragma unroll
+            for (int q = 0; q < 16; q++)
+                row[O.w1 + ((q & 3) + 8 * (q >> 2) + 4 * h + 32 * it) * H + c + 32 * jt] = dW1[it][jt][q];
+    const float s_bp0 = wave_sum(gbp0), s_bp1 = wave_sum(gbp1), s_bv = wave_sum(gbv);
+    const float s_pl = wave_sum(m_pl), s_vl = wave_sum(m_vl), s_h = wave_sum(m_h);
+    const float s_kl = wave_sum(m_kl), s_cf = wave_sum(m_cf), s_v = wave_sum(m_v);
+    const float s_r = wave_sum(m_r), s_ve = wave_sum(m_ve), s_ve2 = wave_sum(m_ve2);
+    const float s_mx = wave_max(m_vemax), s_n = wave_sum(m_n);
+    if (lane == 0) {
+        row[O.bp] = s_bp0; row[O.bp + 1] = s_bp1; row[O.bv] = s_bv;
+        float *mm = row + g.np;
+        mm[M_PL] = s_pl; mm[M_VL] = s_vl; mm[M_H] = s_h; mm[M_KL] = s_kl; mm[M_CF] = s_cf;
+        mm[M_V] = s_v; mm[M_R] = s_r; mm[M_VE] = s_ve; mm[M_VE2] = s_ve2; mm[M_VEMAX] = s_mx;
+        mm[M_N] = s_n;
+    }
+}
+
+// fixed-order reduction of the wave partials: grad[p] = sum_w slab[w][p], in two
+// passes (SLAB_GROUPS row groups in parallel, then the groups in order)
+constexpr int SLAB_GROUPS = 32;
+__global__ void k_slab_reduce_groups(const float *slab, int rows, int width, double *part) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= width) return;
-    if (p == width - NUM_M + M_VEMAX) {
-        float m = -INFINITY;
-        for (int w = 0; w < rows; w++) m = fmaxf(m, slab[(size_t)w * width + p]);
-        grad[p] = m;
-        return;
+    const int per = (rows + SLAB_GROUPS - 1) / SLAB_GROUPS, g = blockIdx.y;
+    const int w0 = g * per, w1 = min(rows, w0 + per);
+    const bool is_max = p == width - NUM_M + M_VEMAX;
+    double s = is_max ? -INFINITY : 0.0;
+    for (int w = w0; w < w1; w++) {
+        const double v = slab[(size_t)w * width + p];
+        s = is_max ? fmax(s, v) : s + v;
     }
-    double s = 0.0;
-    for (int w = 0; w < rows; w++) s += (double)slab[(size_t)w * width + p];
+    part[(size_t)g * width + p] = s;
+}
+__global__ void k_slab_reduce(const double *part, int width, float *grad) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= width) return;
+    const bool is_max = p == width - NUM_M + M_VEMAX;
+    double s = is_max ? -INFINITY : 0.0;
+    for (int g = 0; g < SLAB_GROUPS; g++) {
+        const double v = part[(size_t)g * width + p];
+        s = is_max ? fmax(s, v) : s + v;
+    }
     grad[p] = (float)s;
 }
 
-// per-tensor norm clip + Adam (burn-optim 0.20 restated; one block per tensor)
+// per-tensor norm clip + Adam (burn-optim 0.20 restated).  Each tensor is cut
+// into ADAM_CHUNK-element blocks: pass 1 writes every block's sum of squares,
+// pass 2 sums its tensor's partials in block order (deterministic) and updates.
+constexpr int ADAM_CHUNK = 4096;
 struct AdamTensor { int off, len; float c1, c2; };
 struct AdamArgs {
     float *params, *grad, *m1, *m2;
+    double *part;
     AdamTensor t[32];
+    int blk0[33];          // first block of tensor i; blk0[nt] = total blocks
     int nt;
     float lr, max_norm, eps, inv_world;
 };
-__global__ void __launch_bounds__(256) k_adam(AdamArgs a) {
+__device__ __forceinline__ int adam_tensor_of(const AdamArgs &a, int b) {
+    int t = 0;
+    while (t + 1 < a.nt && a.blk0[t + 1] <= b) t++;
+    return t;
+}
+__global__ void __launch_bounds__(256) k_adam_norm(AdamArgs a) {
     __shared__ double red[256];
-    const AdamTensor T = a.t[blockIdx.x];
+    const int ti = adam_tensor_of(a, blockIdx.x);
+    const AdamTensor T = a.t[ti];
+    const int i0 = (blockIdx.x - a.blk0[ti]) * ADAM_CHUNK, i1 = min(T.len, i0 + ADAM_CHUNK);
     double ss = 0.0;
-    for (int i = threadIdx.x; i < T.len; i += blockDim.x) {
+    for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
         const float gi = a.grad[T.off + i] * a.inv_world;
         ss += (double)gi * (double)gi;
     }
@@ -363,11 +717,24 @@ __global__ void __launch_bounds__(256) k_adam(AdamArgs a) {
         if (threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
         __syncthreads();
     }
-    const float norm = (float)sqrt(red[0]);
+    if (threadIdx.x == 0) a.part[blockIdx.x] = red[0];
+}
+__global__ void __launch_bounds__(256) k_adam(AdamArgs a) {
+    __shared__ double tot;
+    const int ti = adam_tensor_of(a, blockIdx.x);
+    const AdamTensor T = a.t[ti];
+    if (threadIdx.x == 0) {
+        double s = 0.0;
+        for (int b = a.blk0[ti]; b < a.blk0[ti + 1]; b++) s += a.part[b];
+        tot = s;
+    }
+    __syncthreads();
+    const int i0 = (blockIdx.x - a.blk0[ti]) * ADAM_CHUNK, i1 = min(T.len, i0 + ADAM_CHUNK);
+    const float norm = (float)sqrt(tot);
     const float scale = norm > a.max_norm ? __fdiv_rn(a.max_norm, norm) : 1.0f;
     const bool clip = norm > a.max_norm;
     const float b1 = 0.9f, b2 = 0.999f, f1 = 1.0f - 0.9f, f2 = 1.0f - 0.999f;
-    for (int i = threadIdx.x; i < T.len; i += blockDim.x) {
+    for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
         float gi = a.grad[T.off + i] * a.inv_world;
         if (clip) gi = __fmul_rn(gi, scale);
         const float m1 = __fadd_rn(__fmul_rn(a.m1[T.off + i], b1), __fmul_rn(gi, f1));
@@ -405,7 +772,7 @@ bppo_status launch_adv_stats(bppo_ctx *c, uint32_t start, uint32_t n) {
     for (int pass = 0; pass < 2; pass++) {
         hipLaunchKernelGGL(k_adv_pass, dim3(STAT_BLOCKS), dim3(256), 0, c->stream, c->d_adv, c->d_perm,
                            start, n, c->d_mb_stats, pass, c->d_red);
-        hipLaunchKernelGGL(k_adv_finalize, dim3(1), dim3(64), 0, c->stream, c->d_red, STAT_BLOCKS, n,
+        hipLaunchKernelGGL(k_adv_finalize, dim3(1), dim3(256), 0, c->stream, c->d_red, STAT_BLOCKS, n,
                            pass, c->d_mb_stats);
     }
     BPPO_HIP(c, hipGetLastError());
@@ -425,11 +792,16 @@ bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_
     g.ceps = (float)c->cfg.clip_epsilon;
     g.inv_mb = (float)(1.0 / (double)n); g.ent_coef = ent_coef; g.value_coef = (float)c->cfg.value_coef;
     g.clip_value = c->cfg.clip_value;
-    const int blocks = (int)(c->slab_rows / 4);
+    int blocks = 256;
     const size_t params_bytes = ((c->net.n_params + 3) & ~(size_t)3) * sizeof(float);
+    if (h == 64 && nl == 2 && c->relu_mfma) {
+        c->slab_used = blocks * mmb::WAVES;
+        hipLaunchKernelGGL(k_minibatch_mfma, dim3(blocks), dim3(64 * mmb::WAVES), mmb::LDS, c->stream, g);
+    } else
 #define L(H_, NL_)                                                                                 \
     if (h == H_ && nl == NL_) {                                                                     \
         size_t lds = params_bytes + 4 * sizeof(WaveStage<H_>);                                      \
+        c->slab_used = blocks * 4;                                                                  \
         hipLaunchKernelGGL((k_minibatch<H_, NL_>), dim3(blocks), dim3(256), lds, c->stream, g);    \
     } else
     L(16, 1) L(16, 2) L(32, 1) L(32, 2) L(64, 1) L(64, 2) {
@@ -439,8 +811,10 @@ bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_
 #undef L
     BPPO_HIP(c, hipGetLastError());
     const int width = (int)c->net.n_params + NUM_M;
-    hipLaunchKernelGGL(k_slab_reduce, dim3((width + 255) / 256), dim3(256), 0, c->stream, c->d_slab,
-                       (int)c->slab_rows, width, c->d_grad);
+    hipLaunchKernelGGL(k_slab_reduce_groups, dim3((width + 255) / 256, SLAB_GROUPS), dim3(256), 0, c->stream,
+                       c->d_slab, c->slab_used, width, c->d_slab_part);
+    hipLaunchKernelGGL(k_slab_reduce, dim3((width + 255) / 256), dim3(256), 0, c->stream, c->d_slab_part,
+                       width, c->d_grad);
     BPPO_HIP(c, hipGetLastError());
     return BPPO_OK;
 }
@@ -455,7 +829,12 @@ bppo_status launch_adam(bppo_ctx *c, float lr, const float *c1, const float *c2)
     }
     a.lr = lr; a.max_norm = (float)c->cfg.max_grad_norm; a.eps = (float)c->cfg.adam_epsilon;
     a.inv_world = 1.0f / (float)c->world;
-    hipLaunchKernelGGL(k_adam, dim3(a.nt), dim3(256), 0, c->stream, a);
+    a.part = c->d_red;
+    int nb = 0;
+    for (int t = 0; t < a.nt; t++) { a.blk0[t] = nb; nb += (a.t[t].len + ADAM_CHUNK - 1) / ADAM_CHUNK; }
+    a.blk0[a.nt] = nb;
+    hipLaunchKernelGGL(k_adam_norm, dim3(nb), dim3(256), 0, c->stream, a);
+    hipLaunchKernelGGL(k_adam, dim3(nb), dim3(256), 0, c->stream, a);
     BPPO_HIP(c, hipGetLastError());
     return BPPO_OK;
 }

@@ -314,16 +314,21 @@ __global__ void __launch_bounds__(256) k_wide_loss(LossArgs g) {
 }
 
 // fixed-order reduction of the loss partials into the metric slots after the
-// gradient (d_grad[np + k]), where the all-reduce callback picks them up
-__global__ void k_wide_metric_reduce(const double *part, int nblk, float *out) {
-    const int k = threadIdx.x;
-    if (k >= WM_COUNT) return;
-    double v = k == WM_VEMAX ? -INFINITY : 0.0;
-    for (int b = 0; b < nblk; b++) {
+// gradient (d_grad[np + k]), where the all-reduce callback picks them up: one
+// wave per metric, lane-strided sums then a fixed shuffle tree
+__global__ void __launch_bounds__(64) k_wide_metric_reduce(const double *part, int nblk, float *out) {
+    const int k = blockIdx.x, lane = threadIdx.x;
+    const bool is_max = k == WM_VEMAX;
+    double v = is_max ? -INFINITY : 0.0;
+    for (int b = lane; b < nblk; b += 64) {
         const double x = part[(size_t)b * WM_COUNT + k];
-        v = k == WM_VEMAX ? fmax(v, x) : v + x;
+        v = is_max ? fmax(v, x) : v + x;
     }
-    out[k] = (float)v;
+    for (int off = 32; off > 0; off >>= 1) {
+        const double o = __shfl_xor(v, off, 64);
+        v = is_max ? fmax(v, o) : v + o;
+    }
+    if (lane == 0) out[k] = (float)v;
 }
 
 // ------------------------------------------------------------- launchers --
@@ -392,7 +397,7 @@ hipError_t wide_loss(int A, hipStream_t st, const LossArgs &g, int blocks, float
     else return hipErrorInvalidValue;
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_wide_metric_reduce, dim3(1), dim3(64), 0, st, g.part, blocks, metrics_out);
+    hipLaunchKernelGGL(k_wide_metric_reduce, dim3(WM_COUNT), dim3(64), 0, st, g.part, blocks, metrics_out);
     return hipGetLastError();
 }
 

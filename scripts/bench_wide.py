@@ -1,0 +1,66 @@
+"""Throughput of the multi-player workloads (SURVEY CfgC / CfgD) on one MI355X.
+
+    python scripts/bench_wide.py --workload cfgC|cfgD [--steps K --warmup W]
+
+Not the driver's bench line (bench.py measures BASELINE.json's CfgB): this
+prints one JSON line per workload with env-steps/s of a full update (rollout +
+bootstrap/GAE + PPO update) and per-phase device times, for DESIGN.md."""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "burn-ppo_amd"))
+
+WORKLOADS = {
+    # configs/connect_four.toml at num_envs=16384, T=128 (opponent pool off), 6 epochs x 4 minibatches
+    "cfgC": dict(preset="connect_four", num_envs=16384, num_steps=128),
+    # configs/liars_dice_ctde.toml at num_envs=32768, T=128, 4 epochs x 8 minibatches
+    "cfgD": dict(preset="liars_dice_ctde", num_envs=32768, num_steps=128),
+}
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--workload", default="cfgC", choices=sorted(WORKLOADS))
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--num-envs", type=int, default=None)
+    p.add_argument("--no-kl-stop", action="store_true", help="run every epoch (target_kl off)")
+    a = p.parse_args()
+    import torch
+    import bppo
+    w = dict(WORKLOADS[a.workload])
+    if a.num_envs:
+        w["num_envs"] = a.num_envs
+    over = {"target_kl": None} if a.no_kl_stop else {}
+    cfg = bppo.make_config(w["preset"], num_envs=w["num_envs"], num_steps=w["num_steps"], **over)
+    torch.cuda.set_device(0)
+    tr = bppo.Trainer(cfg, init_seed=0)
+    for _ in range(a.warmup):
+        tr.train_update()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ph = {"rollout": 0.0, "gae": 0.0, "update": 0.0}
+    ups = 0
+    for _ in range(a.steps):
+        m = tr.train_update()
+        ups += m["num_updates"]
+        for k in ph:
+            ph[k] += tr.ctx.kernel_ms(k)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    B = w["num_envs"] * w["num_steps"]
+    out = {"workload": a.workload, "env_steps_per_sec": round(B * a.steps / dt, 1),
+           "ms_per_update": round(dt / a.steps * 1000, 2), "num_envs": w["num_envs"],
+           "num_steps": w["num_steps"], "minibatches_per_update": ups / a.steps,
+           "phase_ms_per_update": {k: round(v / a.steps, 2) for k, v in ph.items()},
+           "last": {k: round(v, 5) for k, v in m.items() if isinstance(v, float)}}
+    print(json.dumps(out), flush=True)
+    tr.close()
+
+
+if __name__ == "__main__":
+    main()
