@@ -111,7 +111,8 @@ def main():
     if dist:
         dist.barrier()
     t0 = time.perf_counter()
-    phase = {"rollout": 0.0, "return_norm": 0.0, "gae": 0.0, "minibatch": 0.0, "shuffle": 0.0}
+    phase = {"rollout": 0.0, "return_norm": 0.0, "gae": 0.0, "minibatch": 0.0, "shuffle": 0.0, "update": 0.0,
+             "shuffle_walk": 0.0, "shuffle_wait": 0.0, "shuffle_met": 0.0}
     last = None
     for _ in range(args.steps):
         last = tr.train_update()
@@ -138,7 +139,7 @@ def main():
     achieved = flops / (mb_ms * 1e-3) / 1e12
     roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None,
-            "kernel": "k_minibatch<64,2>", "launch_ms": round(mb_ms, 4),
+            "kernel": "k_minibatch_mfma", "launch_ms": round(mb_ms, 4),
             "algorithmic": f"{mb_rows} rows x {FLOP_PER_ROW_FWD_BWD} FLOP"}
     gae_ms = phase["gae"] / args.steps
     gae_bytes = N * T * GAE_BYTES_PER_ELEM

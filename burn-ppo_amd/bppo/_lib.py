@@ -68,7 +68,7 @@ EXPORTS = (
     "bppo_collect_rollouts", "bppo_rollout_episodes", "bppo_compute_gae", "bppo_ppo_update",
     "bppo_set_allreduce", "bppo_buffer_get", "bppo_buffer_set", "bppo_gae_device",
     "bppo_gae_mp_device", "bppo_last_kernel_ms", "bppo_debug_libm", "bppo_debug_shuffle_chain",
-    "bppo_debug_fisher_yates", "bppo_debug_gemm",
+    "bppo_debug_fisher_yates", "bppo_debug_gemm", "bppo_debug_shuffle_engine",
 )
 
 _lib = None
@@ -79,6 +79,13 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
+    # One HIP runtime per process: the PyTorch wheel ships its own libamdhip64.
+    # Loading torch first makes libbppo bind to that already-loaded runtime; the
+    # other order leaves torch unable to see the GPU ("No HIP GPUs are available").
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"{LIB_PATH} is missing; build it with `make -C burn-ppo_amd` "
                            f"(or __graft_entry__.build())")
@@ -120,6 +127,7 @@ def lib():
         "bppo_debug_shuffle_chain": (i32, [u64, u64, u64, C.c_uint32, vp, C.POINTER(u64)]),
         "bppo_debug_fisher_yates": (i32, [i32, vp, C.c_uint32, vp]),
         "bppo_debug_gemm": (i32, [i32, i32, i32, i32, vp, vp, vp, i32, vp, vp]),
+        "bppo_debug_shuffle_engine": (i32, [u64, u64, u64, C.c_uint32, i32, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -2,6 +2,7 @@
 // host-side orchestration of one update (collect_rollouts -> bootstrap + GAE ->
 // ppo_update, main.rs:724-963), the rand-0.8 shuffle chain thread, parity hooks.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -481,11 +482,16 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
     std::vector<float> rows;          // per minibatch: NM metric sums + 4 adv stats
     int epochs_run = 0;
     bool stop = false;
+    double wait_ms = 0.0;
     tm_begin(c, TM_UPDATE);
     float fw_ms = 0, sh_ms = 0;
     for (int ep = 0; ep < c->cfg.num_epochs && !stop; ep++) {
         epochs_run++;
-        c->shuf.wait_epoch(slot, ep);
+        {
+            auto w0 = std::chrono::steady_clock::now();
+            c->shuf.wait_epoch(slot, ep);
+            wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
+        }
         BPPO_HIP(c, hipStreamWaitEvent(c->stream, c->shuf.ev[slot][ep], 0));
         hipEvent_t s0 = c->ev[TM_SHUFFLE][0], s1 = c->ev[TM_SHUFFLE][1];
         (void)hipEventRecord(s0, c->stream);
@@ -536,6 +542,13 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
     }
     tm_end(c, TM_UPDATE);
     c->rng_pos = c->shuf.end_pos[slot][epochs_run - 1];   // only started epochs consumed words
+    c->last_wait_ms = wait_ms;
+    c->last_walk_ms = 0.0;
+    c->last_met = 0;
+    for (int e = 0; e < epochs_run; e++) {
+        c->last_walk_ms += c->shuf.walk_ms[slot][e];
+        c->last_met += c->shuf.coalesced[slot][e] >= 0 && e > 0;
+    }
     c->shuf_slot = -1;
     // the next update's shuffles begin after its rollout's T*N*A Gumbel words
     c->shuf.ensure(c->rng_pos + (uint64_t)c->T * c->N * (uint64_t)c->A);
@@ -656,6 +669,11 @@ extern "C" bppo_status bppo_last_kernel_ms(bppo_ctx *c, const char *k, float *ms
                                    "adam", "bootstrap"};
     for (int i = 0; i < 8; i++)
         if (!strcmp(k, names[i])) { *ms = c->last_ms[i]; return BPPO_OK; }
+    // host side of the shuffle: draw-chain walk of the last update's epochs, and the
+    // time ppo_update blocked waiting for it
+    if (!strcmp(k, "shuffle_walk")) { *ms = (float)c->last_walk_ms; return BPPO_OK; }
+    if (!strcmp(k, "shuffle_wait")) { *ms = (float)c->last_wait_ms; return BPPO_OK; }
+    if (!strcmp(k, "shuffle_met")) { *ms = (float)c->last_met; return BPPO_OK; }   // epochs resolved by speculation
     return BPPO_ERR_ARG;
 }
 
@@ -694,6 +712,32 @@ extern "C" bppo_status bppo_debug_shuffle_chain(uint64_t seed, uint64_t stream, 
     const uint64_t e = shuffle_walk_host(key, stream, word_pos, n, J);
     if (end_pos) *end_pos = e;
     return BPPO_OK;
+}
+
+// the full shuffle engine (GPU-made words, speculative walks) for `epochs`
+// consecutive shuffles of n from word position start: J [epochs][n] as uploaded to
+// HBM, end positions, and per epoch the checkpoints the true walk needed before it
+// met a speculative walk (-1: walked the whole epoch)
+extern "C" bppo_status bppo_debug_shuffle_engine(uint64_t seed, uint64_t stream, uint64_t start, uint32_t n,
+                                                 int32_t epochs, uint32_t *J, uint64_t *ends, int32_t *met) {
+    if (!J || !ends || n < 2 || epochs < 1 || epochs > SHUF_MAX_EPOCHS) return BPPO_ERR_ARG;
+    ShuffleEngine *e = new ShuffleEngine();
+    std::string err;
+    bppo_status s = e->init(0, seed_key(seed), stream, n, epochs, err);
+    if (s == BPPO_OK) {
+        const int slot = e->ensure(start);
+        for (int k = 0; k < epochs; k++) e->wait_epoch(slot, k);
+        if (hipStreamSynchronize(e->copy) != hipSuccess ||
+            hipMemcpy(J, e->d_J[slot], sizeof(uint32_t) * (size_t)n * epochs, hipMemcpyDeviceToHost) != hipSuccess)
+            s = BPPO_ERR_HIP;
+        for (int k = 0; k < epochs; k++) {
+            ends[k] = e->end_pos[slot][k];
+            if (met) met[k] = e->coalesced[slot][k];
+        }
+    }
+    e->shutdown();
+    delete e;
+    return s;
 }
 
 extern "C" bppo_status bppo_debug_fisher_yates(int32_t device, const uint32_t *J, uint32_t n, uint32_t *perm) {

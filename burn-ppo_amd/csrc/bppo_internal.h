@@ -10,6 +10,7 @@
 #include <mutex>
 #include <condition_variable>
 #include <atomic>
+#include <memory>
 #include "../../include/bppo.h"
 #include "bppo_device.h"
 
@@ -40,62 +41,71 @@ struct Welford { double n, mean, m2; };
 // -------------------------------------------------------------- shuffle -----
 // rand 0.8.5 SliceRandom::shuffle (ppo.rs:1816) on the main StdRng.  The draw
 // chain (every draw may reject, so each draw's word position depends on all
-// earlier ones) is walked on a host thread (shuffle_host.cpp) from ChaCha12
-// words made by producer threads; each epoch's swap targets J[i] go to HBM on a
-// copy stream and the GPU turns them into the permutation (k_shuffle.hip).
-// The thread runs ahead: the next update's shuffles start at a position known
-// in advance (the rollout consumes exactly T*N*A words), so the chain overlaps
-// the rollout, the GAE and the previous epochs' minibatches.
+// earlier ones) is walked on host threads (shuffle_host.cpp) over ChaCha12 words
+// made on the GPU; each epoch's swap targets J[i] go to HBM on a copy stream and
+// the GPU turns them into the permutation (k_shuffle.hip).  Epoch e >= 1 starts
+// where epoch e-1 ends, which is known only after walking it, so K speculative
+// walks per epoch start at once near the expected boundary; the true walk of
+// epoch e runs from the real boundary only until its state (word position,
+// remaining range) meets one of them, after which both are the same walk.
 constexpr int SHUF_MAX_EPOCHS = 32;
+constexpr int SHUF_MAX_SPEC = 16;
+constexpr uint64_t SHUF_CK = 4096;               // checkpoint spacing (words)
+constexpr uint64_t SHUF_CHUNK = (uint64_t)1 << 20; // words per GPU->host copy
 
-struct WordRing {              // ChaCha12 words in fixed chunks, filled ahead of the walker
-    static constexpr size_t C = (size_t)1 << 18;  // words per chunk
-    static constexpr int R = 40;                  // chunks in the ring
-    uint32_t *buf = nullptr;                      // [R][C]
-    int64_t chunk_id[R];
-    Key8 key{};
-    uint64_t stream = 0;
-    std::mutex mu;
-    std::condition_variable cv;
-    int64_t next = 0, floor = 0;                  // next chunk to produce; consumer done below floor
-    uint64_t gen = 0;
-    int inflight = 0;
-    bool quit = false;
-    std::vector<std::thread> producers;
-    void start(const Key8 &k, uint64_t strm, int nthreads);
-    void reset(int64_t first_chunk);              // drop everything, restart at first_chunk
-    const uint32_t *get(int64_t chunk);           // blocks until produced
-    void release_below(int64_t chunk);
-    void stop();
+struct SpecWalk {
+    uint64_t start = 0, end = 0;
+    int epoch = 0;
+    uint32_t *J = nullptr;                        // pinned [n]
+    std::vector<uint32_t> ck;                     // remaining range at checkpoint c (q = wbase + c*CK)
+    std::atomic<int64_t> progress{-1};            // last checkpoint index written
+    std::atomic<int> done{0};
 };
 
 struct ShuffleEngine {
     int dev = 0;
     uint32_t n = 0;
     int epochs = 0;
-    WordRing words;
+    Key8 key{};
+    uint64_t stream = 0;
+    double Ew = 0.0, sigma = 0.0;                 // expected words per shuffle, its std dev
+    int K = 0;                                    // speculative walks per epoch
+    // words of the current job [wbase, wbase + wlen), made on the GPU, copied in chunks
+    uint32_t *d_words = nullptr, *h_words = nullptr;
+    uint64_t wbase = 0, wlen = 0, wcap = 0;
+    std::vector<hipEvent_t> chunk_ev;
+    std::unique_ptr<std::atomic<int>[]> chunk_ok;
+    // speculative walkers
+    SpecWalk spec[SHUF_MAX_SPEC];
+    std::vector<std::thread> workers;
+    uint64_t gen = 0;                             // job generation (workers follow it)
+    int nspec = 0, busy = 0;
+    // job control
     std::thread th;
     std::mutex mu;
     std::condition_variable cv;
     bool quit = false;
-    // job: the shuffles of one update, starting at word position job_start
     bool job_pending = false, job_running = false, job_valid = false;
     uint64_t job_start = 0;
     int job_slot = 1;
-    bool cancel = false;
-    int ready[2] = {0, 0};                    // epochs of the slot's job already on the device
+    std::atomic<bool> cancel{false};
+    int ready[2] = {0, 0};                        // epochs of the slot's job already on the device
     uint64_t end_pos[2][SHUF_MAX_EPOCHS];
-    uint32_t *J_host[2] = {nullptr, nullptr}; // pinned [epochs][n]
-    uint32_t *d_J[2] = {nullptr, nullptr};    // device [epochs][n]
+    uint32_t *J_host[2] = {nullptr, nullptr};     // pinned [epochs][n]
+    uint32_t *d_J[2] = {nullptr, nullptr};        // device [epochs][n]
     hipEvent_t ev[2][SHUF_MAX_EPOCHS] = {};
     bool ev_used[2][SHUF_MAX_EPOCHS] = {};
     hipStream_t copy = nullptr;
     double walk_ms[2][SHUF_MAX_EPOCHS] = {};
+    int coalesced[2][SHUF_MAX_EPOCHS] = {};       // checkpoints walked before meeting a speculative walk (-1: none)
     bppo_status init(int device, const Key8 &key, uint64_t stream, uint32_t n_, int epochs_, std::string &err);
     int ensure(uint64_t start);               // job for this start (reused if already running/done) -> slot
     void wait_epoch(int slot, int e);
     void shutdown();
     void run();
+    void worker(int i);
+    const uint32_t *words(uint64_t pos, uint64_t len, std::vector<uint32_t> &scratch);
+    uint64_t walk_piece(uint64_t pos, uint32_t *r, uint32_t *J, std::vector<uint32_t> &scratch);
 };
 uint64_t shuffle_walk_host(const Key8 &key, uint64_t stream, uint64_t pos, uint32_t n, uint32_t *J);
 
@@ -195,6 +205,8 @@ struct bppo_ctx {
     // timing
     hipEvent_t ev[8][2] = {};
     float last_ms[8] = {0};
+    double last_walk_ms = 0.0, last_wait_ms = 0.0;
+    int last_met = 0;
     int collected = 0, gae_done = 0;
 };
 

@@ -64,3 +64,30 @@ def test_device_fisher_yates_matches_sequential(n):
     ref = np.arange(n, dtype=np.uint32)
     O.lib().or_apply_swaps(J, ref, n)
     assert np.array_equal(perm, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,start,n,epochs", [
+    (42, 1_000_003, 1 << 23, 4),        # CfgB: 4 epochs of 2^23 (speculative walks meet the true walk)
+    (7, 5, 100_003, 6),                 # small n, many epochs
+    (3, 0, 2, 3),                       # degenerate
+    (11, 12_345, (1 << 20) + 1, 2),
+])
+def test_shuffle_engine_equals_sequential_walks(seed, start, n, epochs):
+    """The engine (GPU-made words, speculative walks spliced at a meeting
+    checkpoint) returns exactly the chained single-thread walks."""
+    J = np.zeros(n * epochs, np.uint32)
+    ends = np.zeros(epochs, np.uint64)
+    met = np.zeros(epochs, np.int32)
+    assert L.lib().bppo_debug_shuffle_engine(seed, 0, start, n, epochs, J.ctypes.data, ends.ctypes.data,
+                                             met.ctypes.data) == 0
+    pos = start
+    for e in range(epochs):
+        Je = np.zeros(n, np.uint32)
+        end = C.c_uint64()
+        assert L.lib().bppo_debug_shuffle_chain(seed, 0, pos, n, Je.ctypes.data, C.byref(end)) == 0
+        assert ends[e] == end.value, (e, met)
+        assert np.array_equal(J[e * n:(e + 1) * n], Je), (e, met)
+        pos = end.value
+    if n == 1 << 23:
+        assert (met[1:] >= 0).any(), met      # at CfgB size the speculation does meet
