@@ -5,6 +5,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include "bppo_internal.h"
 #include "bppo_wide.h"
@@ -137,6 +138,8 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     TRY(dalloc(c, &c->d_ret, TN));
     TRY(dalloc(c, &c->d_act, TN));
     if (!c->wide) TRY(dalloc(c, &c->d_X, TN));
+    if (!c->wide && cfg->hidden_size == 64 && cfg->num_hidden == 2 && cfg->relu && !getenv("BPPO_VALU_ROLLOUT"))
+        TRY(dalloc(c, &c->d_gumbel, TN * 2));
     TRY(dalloc(c, &c->d_on, (size_t)2 * c->D + 1));
     if (!c->wide) TRY(dalloc(c, &c->d_obs_part, (size_t)c->N * 2 * c->D));
     TRY(dalloc(c, &c->d_rn_returns, (size_t)c->N * c->P));
@@ -191,7 +194,7 @@ extern "C" void bppo_destroy(bppo_ctx *c) {
                     c->d_done, c->d_val, c->d_logp, c->d_adv, c->d_ret, c->d_act, c->d_X, c->d_on,
                     c->d_obs_part, c->d_rn_returns, c->d_rn_stats, c->d_scan_agg, c->d_last_v,
                     c->d_eps, c->d_ep_count, c->d_err, c->d_perm, c->d_fy, c->d_scan,
-                    c->d_red, c->d_mb_stats};
+                    c->d_red, c->d_mb_stats, c->d_gumbel};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     if (c->h_red) (void)hipHostFree(c->h_red);
     for (int i = 0; i < 8; i++) {

@@ -145,6 +145,7 @@ struct bppo_ctx {
     float *d_val = nullptr, *d_logp = nullptr, *d_adv = nullptr, *d_ret = nullptr;
     int32_t *d_act = nullptr;
     double *d_X = nullptr;            // rolling returns per (t,e) for the return-normalizer scan
+    float *d_gumbel = nullptr;        // CfgB MFMA rollout: Gumbel noise [T][N][2], made ahead of it
     // normalizers
     double *d_on = nullptr;           // [3][D]: mean, M2, (count in slot) ; host mirror below
     std::vector<double> on_mean, on_m2;

@@ -1,0 +1,53 @@
+// bppo_mlp64.h — shared pieces of the MFMA kernels for the CfgB network
+// (5 -> 64 -> 64 -> {2, 1}, relu; configs/cartpole.toml): parameter staging in
+// LDS with conflict-free row strides, the per-wave transpose buffers, and the
+// v_mfma_f32_32x32x2_f32 C/D layout helpers.
+#pragma once
+#include "bppo_device.h"
+
+namespace bppo {
+namespace mmb {
+constexpr int H = 64, RS = 65, TR = 32;          // hidden width, LDS row stride, rows per wave tile
+struct Params {
+    float W0[6 * H];      // [d][k], d = 5 is a zero pad row (K 5 -> 6)
+    float b0[H];
+    float W1[H * RS];     // [k][o], row stride 65: conflict-free for both operand reads
+    float b1[H];
+    float Wp[H * 2];
+    float bp[2];
+    float Wv[H];
+    float bv[2];
+};
+struct Wave {
+    float X[TR * 9];      // [row][d]
+    float T[TR * RS];     // transpose staging: H1 -> H2 -> dZ2, [row][col]
+    float dl[TR * 4];     // dL/d(logit0, logit1, value) per row
+};
+constexpr int WAVES = 8;
+constexpr size_t LDS = sizeof(Params) + WAVES * sizeof(Wave);
+
+// whole block: flat Burn-order params -> LDS layout
+__device__ __forceinline__ void load_params(Params &S, const float *__restrict__ P) {
+    constexpr CpOffsets O = cp_offsets<64, 2>();
+    for (int i = threadIdx.x; i < 6 * H; i += blockDim.x) S.W0[i] = i < 5 * H ? P[O.w0 + i] : 0.0f;
+    for (int i = threadIdx.x; i < H * H; i += blockDim.x) S.W1[(i / H) * RS + (i % H)] = P[O.w1 + i];
+    for (int i = threadIdx.x; i < H; i += blockDim.x) {
+        S.b0[i] = P[O.b0 + i]; S.b1[i] = P[O.b1 + i]; S.Wv[i] = P[O.wv + i];
+        S.Wp[2 * i] = P[O.wp + 2 * i]; S.Wp[2 * i + 1] = P[O.wp + 2 * i + 1];
+    }
+    if (threadIdx.x < 2) S.bp[threadIdx.x] = P[O.bp + threadIdx.x];
+    if (threadIdx.x == 0) S.bv[0] = P[O.bv];
+}
+
+// C/D row of accumulator register q for lane half h
+__device__ __forceinline__ int cd_row(int q, int h) { return (q & 3) + 8 * (q >> 2) + 4 * h; }
+}  // namespace mmb
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+}  // namespace bppo

@@ -9,6 +9,7 @@
 // cartpole.rs:272-301).  Raw rewards are written; the return normaliser runs as
 // a post-pass scan (k_gae.hip) because normalised rewards only feed GAE.
 #include "bppo_internal.h"
+#include "bppo_mlp64.h"
 
 namespace bppo {
 
@@ -170,6 +171,178 @@ __global__ void __launch_bounds__(256) k_cartpole_rollout(RolloutArgs a) {
         a.obs_part[(size_t)e * 10 + 5 + d] = wM2[d];
     }
     if (bad) atomicOr(a.err, 1);
+}
+
+// Gumbel noise of a whole rollout, ahead of it (utils.rs:10-31): g[i] for the
+// word at base + i, i < count (row-major [t][env][action], one word per draw).
+// One ChaCha12 block per thread; the rollout reads two floats per env-step.
+__global__ void k_gumbel_words(Key8 key, uint64_t stream, uint64_t base, uint64_t count, float *g) {
+    const uint64_t b = (base >> 4) + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    const uint64_t w0 = b * 16;
+    if (w0 >= base + count) return;
+    uint32_t blk[16];
+    chacha12_block(key, b, stream, blk);
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const uint64_t w = w0 + j;
+        if (w >= base && w < base + count) g[w - base] = gumbel_from_word(blk[j]);
+    }
+}
+
+// The CfgB rollout (64x2 relu MLP) with the MLP on v_mfma_f32_32x32x2_f32: each
+// wave owns 32 envs for all T steps (lanes 0-31 hold the env state; all 64
+// lanes run the MFMAs), 8 waves per block, 2 per SIMD.  Per step: obs ->
+// normalise (lagged stats) -> H1, H2 on MFMA in natural k order (bit-equal to
+// the VALU chain) -> heads on the VALU -> Gumbel-max with the precomputed noise
+// -> log-prob -> CartPole step / auto-reset; same outputs as k_cartpole_rollout.
+__global__ void __launch_bounds__(512, 2) k_cartpole_rollout_mfma(RolloutArgs a, const float *__restrict__ gum) {
+    using namespace mmb;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    Params &S = *reinterpret_cast<Params *>(smem);
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    Wave &B = reinterpret_cast<Wave *>(smem + sizeof(Params) / 4)[wv];
+    load_params(S, a.params);
+    __syncthreads();
+    const int c = lane & 31, h = lane >> 5;
+    const int N = a.N;
+    const int e = (blockIdx.x * WAVES + wv) * TR + c;
+    const bool mine = h == 0 && e < N;
+    float b0k[2], b1k[2];
+#pragma unroll
+    for (int ct = 0; ct < 2; ct++) { b0k[ct] = S.b0[c + 32 * ct]; b1k[ct] = S.b1[c + 32 * ct]; }
+    CartPoleState s{};
+    WordCursor ec;
+    float ep_ret = 0.0f;
+    int32_t ep_len = 0;
+    if (mine) {
+        load_state(a.cp, a.steps, N, e, s);
+        ec.init(seed_key(a.seed_base + (uint64_t)e), 0, a.env_pos[e]);
+        ep_ret = a.ep_ret[e];
+        ep_len = a.ep_len[e];
+    }
+    double wm[5] = {0, 0, 0, 0, 0}, wM2[5] = {0, 0, 0, 0, 0};
+    int32_t bad = 0;
+#pragma unroll 1
+    for (int t = 0; t < a.T; t++) {
+        const size_t row = (size_t)t * N + e;
+        if (h == 0) {
+            float x[5] = {0, 0, 0, 0, 0};
+            if (mine) {
+                float raw[5];
+                cartpole_obs(s, raw);
+                const double cnt = (double)(t + 1);
+#pragma unroll
+                for (int d = 0; d < 5; d++) {             // per-env Welford partial (raw obs)
+                    const double xv = (double)raw[d];
+                    const double delta = xv - wm[d];
+                    wm[d] += delta / cnt;
+                    wM2[d] += delta * (xv - wm[d]);
+                }
+                normalize_obs5(a.on, a.norm_on, raw, x);
+#pragma unroll
+                for (int d = 0; d < 5; d++) a.obs[row * 5 + d] = x[d];
+            }
+#pragma unroll
+            for (int d = 0; d < 5; d++) B.X[c * 9 + d] = x[d];
+            B.X[c * 9 + 5] = 0.0f;
+        }
+        wave_sync();
+        f32x16_t h1[2];
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++)
+#pragma unroll
+            for (int q = 0; q < 16; q++) h1[ct][q] = 0.0f;
+#pragma unroll
+        for (int st = 0; st < 3; st++) {
+            const float av = B.X[c * 9 + 2 * st + h];
+#pragma unroll
+            for (int ct = 0; ct < 2; ct++)
+                h1[ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, S.W0[(2 * st + h) * H + c + 32 * ct], h1[ct], 0, 0, 0);
+        }
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++)
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const float v = __fadd_rn(h1[ct][q], b0k[ct]);
+                B.T[cd_row(q, h) * RS + c + 32 * ct] = v > 0.0f ? v : 0.0f;
+            }
+        wave_sync();
+        f32x16_t h2[2];
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++)
+#pragma unroll
+            for (int q = 0; q < 16; q++) h2[ct][q] = 0.0f;
+#pragma unroll 8
+        for (int st = 0; st < 32; st++) {
+            const float av = B.T[c * RS + 2 * st + h];
+            h2[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, S.W1[(2 * st + h) * RS + c], h2[0], 0, 0, 0);
+            h2[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, S.W1[(2 * st + h) * RS + c + 32], h2[1], 0, 0, 0);
+        }
+        wave_sync();
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++)
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const float v = __fadd_rn(h2[ct][q], b1k[ct]);
+                B.T[cd_row(q, h) * RS + c + 32 * ct] = v > 0.0f ? v : 0.0f;
+            }
+        wave_sync();
+        if (mine) {
+            float l0 = 0.0f, l1 = 0.0f, vv = 0.0f;
+            const float *hr = B.T + c * RS;
+#pragma unroll 16
+            for (int k = 0; k < H; k++) {
+                const float hk = hr[k];
+                l0 = __builtin_fmaf(hk, S.Wp[2 * k], l0);
+                l1 = __builtin_fmaf(hk, S.Wp[2 * k + 1], l1);
+                vv = __builtin_fmaf(hk, S.Wv[k], vv);
+            }
+            float lg[2];
+            lg[0] = __fadd_rn(l0, S.bp[0]);
+            lg[1] = __fadd_rn(l1, S.bp[1]);
+            const float v = __fadd_rn(vv, S.bv[0]);
+            const float n0 = __fadd_rn(lg[0], gum[row * 2]);
+            const float n1 = __fadd_rn(lg[1], gum[row * 2 + 1]);
+            const int act = n1 > n0 ? 1 : 0;               // argmax, first maximum
+            const float lp = log_prob_row<2>(lg, act);
+            bad |= !isfinite(lp);
+            float r;
+            const bool done = cartpole_step(s, act, r);
+            ep_ret = __fadd_rn(ep_ret, r);
+            ep_len += 1;
+            if (done) {
+                const int32_t k = atomicAdd(a.ep_count, 1);
+                if (k < a.eps_cap) {
+                    EpisodeRec rec;
+                    rec.total_reward[0] = ep_ret; rec.total_reward[1] = rec.total_reward[2] =
+                        rec.total_reward[3] = 0.0f;
+                    rec.length = ep_len; rec.env_index = e; rec.step = t; rec.pad = 0;
+                    a.eps[k] = rec;
+                }
+                cartpole_reset(s, ec);
+                ep_ret = 0.0f;
+                ep_len = 0;
+            }
+            a.act[row] = act;
+            a.rew_raw[row] = r;
+            a.done[row] = done ? 1.0f : 0.0f;
+            a.val[row] = v;
+            a.logp[row] = lp;
+        }
+        wave_sync();
+    }
+    if (mine) {
+        store_state(a.cp, a.steps, N, e, s);
+        a.env_pos[e] = ec.pos;
+        a.ep_ret[e] = ep_ret;
+        a.ep_len[e] = ep_len;
+#pragma unroll
+        for (int d = 0; d < 5; d++) {
+            a.obs_part[(size_t)e * 10 + d] = wm[d];
+            a.obs_part[(size_t)e * 10 + 5 + d] = wM2[d];
+        }
+        if (bad) atomicOr(a.err, 1);
+    }
 }
 
 // VecEnv::step surface (env.rs:400-487) for host-driven stepping.
@@ -336,6 +509,18 @@ bppo_status launch_cartpole_rollout(bppo_ctx *c, uint64_t base_pos, const double
     a.obs = c->d_obs; a.rew_raw = c->d_rew_raw; a.done = c->d_done; a.val = c->d_val;
     a.logp = c->d_logp; a.act = c->d_act; a.obs_part = c->d_obs_part; a.eps = c->d_eps;
     a.ep_count = c->d_ep_count; a.eps_cap = c->eps_cap; a.err = c->d_err;
+    if (h == 64 && nl == 2 && c->d_gumbel) {
+        // Gumbel noise for every (t, env, action) first, then the MFMA rollout
+        const uint64_t count = (uint64_t)c->T * c->N * 2;
+        const uint64_t blocks = ((base_pos + count + 15) >> 4) - (base_pos >> 4);
+        hipLaunchKernelGGL(k_gumbel_words, dim3((unsigned)((blocks + 255) / 256)), dim3(256), 0, c->stream, c->rng_key,
+                           (uint64_t)c->cfg.rng_stream, base_pos, count, c->d_gumbel);
+        const int waves = (c->N + mmb::TR - 1) / mmb::TR;
+        hipLaunchKernelGGL(k_cartpole_rollout_mfma, dim3((waves + mmb::WAVES - 1) / mmb::WAVES), dim3(64 * mmb::WAVES),
+                           mmb::LDS, c->stream, a, (const float *)c->d_gumbel);
+        BPPO_HIP(c, hipGetLastError());
+        return BPPO_OK;
+    }
     dim3 grid((c->N + 255) / 256), blk(256);
     size_t lds = c->net.n_params * sizeof(float);
 #define L(H_, NL_) hipLaunchKernelGGL((k_cartpole_rollout<H_, NL_>), grid, blk, lds, c->stream, a)

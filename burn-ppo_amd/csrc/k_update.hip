@@ -8,6 +8,7 @@
 //    gradients reduced in fixed order (deterministic), per-tensor norm clip +
 //    Adam (main.rs:264-268).
 #include "bppo_internal.h"
+#include "bppo_mlp64.h"
 
 namespace bppo {
 
@@ -352,35 +353,6 @@ __global__ void __launch_bounds__(256, 1) k_minibatch(MbArgs g) {
 //             the gradient sum); dZ1 = (dZ2 W1^T) * [H1 > 0] on MFMA after one
 //             LDS transpose of dZ2; dW0, biases and the head gradients on the VALU.
 // 8 waves per block (2 per SIMD), one block per CU, persistent over the minibatch.
-namespace mmb {
-constexpr int H = 64, RS = 65, TR = 32;          // hidden width, LDS row stride, rows per wave tile
-struct Params {
-    float W0[6 * H];      // [d][k], d = 5 is a zero pad row (K 5 -> 6)
-    float b0[H];
-    float W1[H * RS];     // [k][o], row stride 65: conflict-free for both operand reads
-    float b1[H];
-    float Wp[H * 2];
-    float bp[2];
-    float Wv[H];
-    float bv[2];
-};
-struct Wave {
-    float X[TR * 9];      // [row][d]
-    float T[TR * RS];     // transpose staging: H1 -> H2 -> dZ2, [row][col]
-    float dl[TR * 4];     // dL/d(logit0, logit1, value) per row
-};
-constexpr int WAVES = 8;
-constexpr size_t LDS = sizeof(Params) + WAVES * sizeof(Wave);
-}  // namespace mmb
-
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-typedef float f32x16_t __attribute__((ext_vector_type(16)));
-
 __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
     using namespace mmb;
     constexpr CpOffsets O = cp_offsets<64, 2>();
@@ -388,14 +360,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
     Params &S = *reinterpret_cast<Params *>(smem);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     Wave &B = reinterpret_cast<Wave *>(smem + sizeof(Params) / 4)[wv];
-    for (int i = tid; i < 6 * H; i += blockDim.x) S.W0[i] = i < 5 * H ? g.params[O.w0 + i] : 0.0f;
-    for (int i = tid; i < H * H; i += blockDim.x) S.W1[(i / H) * RS + (i % H)] = g.params[O.w1 + i];
-    for (int i = tid; i < H; i += blockDim.x) {
-        S.b0[i] = g.params[O.b0 + i]; S.b1[i] = g.params[O.b1 + i]; S.Wv[i] = g.params[O.wv + i];
-        S.Wp[2 * i] = g.params[O.wp + 2 * i]; S.Wp[2 * i + 1] = g.params[O.wp + 2 * i + 1];
-    }
-    if (tid < 2) S.bp[tid] = g.params[O.bp + tid];
-    if (tid == 0) S.bv[0] = g.params[O.bv];
+    load_params(S, g.params);
     __syncthreads();
 
     const int c = lane & 31, h = lane >> 5;
