@@ -127,7 +127,7 @@ def lib():
         "bppo_debug_shuffle_chain": (i32, [u64, u64, u64, C.c_uint32, vp, C.POINTER(u64)]),
         "bppo_debug_fisher_yates": (i32, [i32, vp, C.c_uint32, vp]),
         "bppo_debug_gemm": (i32, [i32, i32, i32, i32, vp, vp, vp, i32, vp, vp]),
-        "bppo_debug_shuffle_engine": (i32, [u64, u64, u64, C.c_uint32, i32, vp, vp, vp]),
+        "bppo_debug_shuffle_engine": (i32, [u64, u64, u64, C.c_uint32, i32, u64, i32, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -162,7 +162,7 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     }
     c->rng_key = seed_key(cfg->seed);
     c->rng_pos = 0;
-    TRY(c->shuf.init(dev, c->rng_key, cfg->rng_stream, (uint32_t)TN, cfg->num_epochs, c->err));
+    TRY(c->shuf.init(dev, c->rng_key, cfg->rng_stream, (uint32_t)TN, cfg->num_epochs, TN * (uint64_t)c->A, c->err));
     c->on_mean.assign(c->D, 0.0); c->on_m2.assign(c->D, 0.0); c->on_count = 0;
     if (c->wide) {
         TRY(wide_init(c));
@@ -553,7 +553,9 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
         c->last_met += c->shuf.coalesced[slot][e] >= 0 && e > 0;
     }
     c->shuf_slot = -1;
-    // the next update's shuffles begin after its rollout's T*N*A Gumbel words
+    // this update's reads of the J slot are enqueued; the next update's shuffles
+    // begin after its rollout's T*N*A Gumbel words (usually chained already)
+    c->shuf.release(slot, c->stream);
     c->shuf.ensure(c->rng_pos + (uint64_t)c->T * c->N * (uint64_t)c->A);
     double ev4[4];
     TRY(launch_explained_variance(c, ev4));
@@ -717,26 +719,32 @@ extern "C" bppo_status bppo_debug_shuffle_chain(uint64_t seed, uint64_t stream, 
     return BPPO_OK;
 }
 
-// the full shuffle engine (GPU-made words, speculative walks) for `epochs`
-// consecutive shuffles of n from word position start: J [epochs][n] as uploaded to
-// HBM, end positions, and per epoch the checkpoints the true walk needed before it
-// met a speculative walk (-1: walked the whole epoch)
+// the full shuffle engine (GPU-made words, speculative walks) for `jobs`
+// consecutive updates of `epochs` shuffles of n, the first starting at word
+// position start and each next one `gap` words after the previous update's last
+// shuffle (the rollout's draws): J [jobs][epochs][n] as rebuilt in HBM, end
+// positions [jobs][epochs], and per epoch the checkpoints the true walk needed
+// before it met a speculative walk (-1: walked the whole epoch)
 extern "C" bppo_status bppo_debug_shuffle_engine(uint64_t seed, uint64_t stream, uint64_t start, uint32_t n,
-                                                 int32_t epochs, uint32_t *J, uint64_t *ends, int32_t *met) {
-    if (!J || !ends || n < 2 || epochs < 1 || epochs > SHUF_MAX_EPOCHS) return BPPO_ERR_ARG;
+                                                 int32_t epochs, uint64_t gap, int32_t jobs, uint32_t *J,
+                                                 uint64_t *ends, int32_t *met) {
+    if (!J || !ends || n < 2 || epochs < 1 || epochs > SHUF_MAX_EPOCHS || jobs < 1) return BPPO_ERR_ARG;
     ShuffleEngine *e = new ShuffleEngine();
     std::string err;
-    bppo_status s = e->init(0, seed_key(seed), stream, n, epochs, err);
-    if (s == BPPO_OK) {
-        const int slot = e->ensure(start);
+    bppo_status s = e->init(0, seed_key(seed), stream, n, epochs, gap, err);
+    uint64_t pos = start;
+    for (int j = 0; j < jobs && s == BPPO_OK; j++) {
+        const int slot = e->ensure(pos);
         for (int k = 0; k < epochs; k++) e->wait_epoch(slot, k);
+        const size_t o = (size_t)j * epochs;
         if (hipStreamSynchronize(e->copy) != hipSuccess ||
-            hipMemcpy(J, e->d_J[slot], sizeof(uint32_t) * (size_t)n * epochs, hipMemcpyDeviceToHost) != hipSuccess)
+            hipMemcpy(J + o * n, e->d_J[slot], sizeof(uint32_t) * (size_t)n * epochs, hipMemcpyDeviceToHost) != hipSuccess)
             s = BPPO_ERR_HIP;
         for (int k = 0; k < epochs; k++) {
-            ends[k] = e->end_pos[slot][k];
-            if (met) met[k] = e->coalesced[slot][k];
+            ends[o + k] = e->end_pos[slot][k];
+            if (met) met[o + k] = e->coalesced[slot][k];
         }
+        pos = e->end_pos[slot][epochs - 1] + gap;
     }
     e->shutdown();
     delete e;

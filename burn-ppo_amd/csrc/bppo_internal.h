@@ -49,17 +49,28 @@ struct Welford { double n, mean, m2; };
 // epoch e runs from the real boundary only until its state (word position,
 // remaining range) meets one of them, after which both are the same walk.
 constexpr int SHUF_MAX_EPOCHS = 32;
-constexpr int SHUF_MAX_SPEC = 16;
+constexpr int SHUF_MAX_SPEC = 40;
 constexpr uint64_t SHUF_CK = 4096;               // checkpoint spacing (words)
 constexpr uint64_t SHUF_CHUNK = (uint64_t)1 << 20; // words per GPU->host copy
 
 struct SpecWalk {
-    uint64_t start = 0, end = 0;
-    int epoch = 0;
-    uint32_t *J = nullptr;                        // pinned [n]
-    std::vector<uint32_t> ck;                     // remaining range at checkpoint c (q = wbase + c*CK)
+    uint64_t start = 0, end = 0, ck_base = 0;     // checkpoint c is word position ck_base + c*CK
+    int wbuf = 0;                                 // word buffer it reads
+    std::vector<uint32_t> ck;                     // remaining range at checkpoint c
     std::atomic<int64_t> progress{-1};            // last checkpoint index written
-    std::atomic<int> done{0};
+    std::atomic<int> done{1};
+    std::atomic<bool> stop{false};
+    uint64_t gen = 0;                             // assignment counter (the worker follows it)
+    bool running = false;                         // guarded by the engine mutex
+};
+
+struct WordBuf {                                  // ChaCha12 words made on the GPU for one job
+    uint32_t *d = nullptr, *h = nullptr;
+    uint64_t cap = 0;                             // words
+    struct Region { uint64_t base = 0, len = 0, off = 0; } reg[2];
+    int nreg = 0;
+    std::vector<hipEvent_t> ev;                   // per SHUF_CHUNK chunk of h
+    std::unique_ptr<std::atomic<int>[]> ok;
 };
 
 struct ShuffleEngine {
@@ -68,44 +79,60 @@ struct ShuffleEngine {
     int epochs = 0;
     Key8 key{};
     uint64_t stream = 0;
+    uint64_t gap = 0;                             // words between an update's last shuffle and the next update's first
     double Ew = 0.0, sigma = 0.0;                 // expected words per shuffle, its std dev
-    int K = 0;                                    // speculative walks per epoch
-    // words of the current job [wbase, wbase + wlen), made on the GPU, copied in chunks
-    uint32_t *d_words = nullptr, *h_words = nullptr;
-    uint64_t wbase = 0, wlen = 0, wcap = 0;
-    std::vector<hipEvent_t> chunk_ev;
-    std::unique_ptr<std::atomic<int>[]> chunk_ok;
-    // speculative walkers
+    int K = 0;                                    // speculative walks per epoch boundary
+    WordBuf wb[2];                                // double-buffered by job parity
+    // walker slots: [0, ncur) K per epoch 1..E-1 of the current job; then two
+    // carry sets of K for the next job's first epoch (alternating by job parity)
     SpecWalk spec[SHUF_MAX_SPEC];
+    int nspec = 0, ncur = 0;
     std::vector<std::thread> workers;
-    uint64_t gen = 0;                             // job generation (workers follow it)
-    int nspec = 0, busy = 0;
-    // job control
+    uint64_t seq = 0;                             // jobs started
+    bool carry_valid[2] = {false, false};
+    // job control: a job = one update's shuffles in a J slot.  The engine chains
+    // the next job (start = last end + gap) as soon as one is resolved, at most
+    // one job ahead of the job the caller consumes.
     std::thread th;
     std::mutex mu;
     std::condition_variable cv;
     bool quit = false;
-    bool job_pending = false, job_running = false, job_valid = false;
-    uint64_t job_start = 0;
-    int job_slot = 1;
+    bool slot_valid[2] = {false, false};          // slot holds (or is computing) the job for slot_start
+    uint64_t slot_start[2] = {0, 0};
+    int pending = -1, running = -1;               // slot queued / being computed
+    int consumer = -1;                            // slot the caller last asked for
+    int chain_from = -1;                          // resolved slot whose successor may be chained
+    uint64_t chain_start = 0;
+    int last_slot = 1;
+    hipEvent_t consumed[2] = {nullptr, nullptr};  // recorded by the caller after its last read of d_J[slot]
+    bool consumed_used[2] = {false, false};
     std::atomic<bool> cancel{false};
     int ready[2] = {0, 0};                        // epochs of the slot's job already on the device
     uint64_t end_pos[2][SHUF_MAX_EPOCHS];
-    uint32_t *J_host[2] = {nullptr, nullptr};     // pinned [epochs][n]
+    // each epoch's walk as segments (start position, start range, end position),
+    // one per checkpoint interval; the GPU rebuilds J from them (k_expand_J)
+    struct Seg { uint64_t pos0, pos1; uint32_t r0, pad; };
+    int maxseg = 0;
+    Seg *seg_host[2] = {nullptr, nullptr};        // pinned [epochs][maxseg]
+    Seg *d_seg[2] = {nullptr, nullptr};
     uint32_t *d_J[2] = {nullptr, nullptr};        // device [epochs][n]
     hipEvent_t ev[2][SHUF_MAX_EPOCHS] = {};
     bool ev_used[2][SHUF_MAX_EPOCHS] = {};
     hipStream_t copy = nullptr;
     double walk_ms[2][SHUF_MAX_EPOCHS] = {};
     int coalesced[2][SHUF_MAX_EPOCHS] = {};       // checkpoints walked before meeting a speculative walk (-1: none)
-    bppo_status init(int device, const Key8 &key, uint64_t stream, uint32_t n_, int epochs_, std::string &err);
+    bppo_status init(int device, const Key8 &key, uint64_t stream, uint32_t n_, int epochs_, uint64_t gap_,
+                     std::string &err);
     int ensure(uint64_t start);               // job for this start (reused if already running/done) -> slot
+    void release(int slot, hipStream_t st);   // the caller is done enqueuing reads of d_J[slot] on st
     void wait_epoch(int slot, int e);
     void shutdown();
     void run();
     void worker(int i);
-    const uint32_t *words(uint64_t pos, uint64_t len, std::vector<uint32_t> &scratch);
-    uint64_t walk_piece(uint64_t pos, uint32_t *r, uint32_t *J, std::vector<uint32_t> &scratch);
+    void launch_walk(int i, uint64_t start, int wbuf);   // mu held
+    void stop_walks(int lo, int hi);                     // stop and wait (mu not held)
+    const uint32_t *words(int b, uint64_t pos, uint64_t len, std::vector<uint32_t> &scratch);
+    uint64_t walk_piece(int b, uint64_t pos, uint32_t *r, std::vector<uint32_t> &scratch);
 };
 uint64_t shuffle_walk_host(const Key8 &key, uint64_t stream, uint64_t pos, uint32_t n, uint32_t *J);
 

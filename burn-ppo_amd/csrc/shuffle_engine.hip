@@ -7,14 +7,18 @@
 //   true walk  : the sequential rejection chain -> J[i] = gen_range(0..i+1),
 //                i = n-1..1 (shuffle_host.cpp), epoch by epoch;
 //   speculation: epoch e >= 1 starts where epoch e-1 ends, known only after
-//                walking it.  K walkers start every epoch e >= 1 at once, at
-//                guesses spread around the expected boundary, recording the
+//                walking it, and the next update's first epoch starts `gap`
+//                words (the rollout's T*N*A Gumbel draws) after this update's
+//                last one.  K walkers start at every such boundary at once, at
+//                guesses spread around the expected position, recording the
 //                remaining range r at every SHUF_CK-th word position.  The true
-//                walk of epoch e runs from the real boundary only until, at a
+//                walk of an epoch runs from the real boundary only until, at a
 //                checkpoint, its r equals a speculative walk's r at the same
 //                position: from there the two walks are the same walk, so the
 //                epoch's end and J[0 .. r) come from the speculative one.  With
-//                no meeting the true walk finishes the epoch itself.
+//                no meeting the true walk finishes the epoch itself.  The walks
+//                for the next update's first epoch ("carry" set) run during this
+//                update's job, on this job's word buffer (double-buffered).
 //   copy stream: each epoch's J to HBM; an event per epoch lets the compute
 //                stream wait for exactly that epoch.
 //
@@ -57,6 +61,37 @@ __global__ void k_chacha_words(Key8 key, uint64_t stream, uint64_t base, uint64_
     o[3] = make_uint4(blk[12], blk[13], blk[14], blk[15]);
 }
 
+// J from walk segments: thread i re-walks words [pos0, pos1) of segment i from
+// range r0 and writes J[r-1] = hi(w * r) for every ACCEPTED word (each r is
+// accepted exactly once, so segments never write the same slot).  Words come
+// from the jobs' device word buffers when a region holds the segment, else
+// from ChaCha12 here.
+struct WordRegions {
+    const uint32_t *ptr[4];
+    uint64_t base[4], len[4];
+    int n;
+};
+__global__ void __launch_bounds__(64) k_expand_J(Key8 key, uint64_t stream, const ShuffleEngine::Seg *segs, int ns,
+                                                 WordRegions wr, uint32_t *J) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) J[0] = 0;
+    if (i >= ns) return;
+    const ShuffleEngine::Seg g = segs[i];
+    uint32_t r = g.r0;
+    const uint32_t *src = nullptr;
+    for (int k = 0; k < wr.n; k++)
+        if (g.pos0 >= wr.base[k] && g.pos1 <= wr.base[k] + wr.len[k]) src = wr.ptr[k] + (g.pos0 - wr.base[k]);
+    WordCursor c;
+    c.init(key, stream, g.pos0);
+    const uint64_t nw = g.pos1 - g.pos0;
+    for (uint64_t p = 0; p < nw && r >= 2; p++) {
+        const uint32_t w = src ? src[p] : c.next();
+        const uint64_t m = (uint64_t)w * r;
+        const uint32_t z = (r << __clz(r)) - 1u;
+        if ((uint32_t)m <= z) { J[r - 1] = (uint32_t)(m >> 32); r--; }
+    }
+}
+
 // expected words per shuffle of n and its std dev: draw with range R accepts with
 // probability a = (R << lz(R)) / 2^32 (uniform.rs zone), geometric word count
 static void shuffle_word_stats(uint32_t n, double &mean, double &sd) {
@@ -70,20 +105,25 @@ static void shuffle_word_stats(uint32_t n, double &mean, double &sd) {
     sd = std::sqrt(v);
 }
 
-bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32_t n_, int epochs_,
+bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32_t n_, int epochs_, uint64_t gap_,
                                 std::string &err) {
-    dev = device; n = n_; epochs = epochs_; key = k; stream = strm;
+    dev = device; n = n_; epochs = epochs_; key = k; stream = strm; gap = gap_;
     if (epochs > SHUF_MAX_EPOCHS) { err = "num_epochs > 32 not supported by the shuffle engine"; return BPPO_ERR_UNSUPPORTED; }
     shuffle_word_stats(n, Ew, sigma);
-    // speculative walks per epoch (BPPO_SHUFFLE_SPEC, default: about 12 walker threads in all)
-    K = epochs > 1 ? std::max(1, std::min(4, 12 / (epochs - 1))) : 0;
-    if (const char *e = getenv("BPPO_SHUFFLE_SPEC")) K = std::max(0, std::min(SHUF_MAX_SPEC, atoi(e)));
-    nspec = std::min(SHUF_MAX_SPEC, K * std::max(0, epochs - 1));
-    K = epochs > 1 ? nspec / (epochs - 1) : 0;
-    nspec = K * std::max(0, epochs - 1);
+    // K walkers per epoch boundary: epochs 1..E-1 of a job plus the next job's
+    // first epoch (two alternating carry sets); about 12 run at once
+    // (BPPO_SHUFFLE_SPEC overrides; 0 = sequential walk only)
+    K = std::max(1, 12 / std::max(epochs, 1));
+    if (const char *e = getenv("BPPO_SHUFFLE_SPEC")) K = std::max(0, atoi(e));
+    K = std::min(K, SHUF_MAX_SPEC / (std::max(epochs - 1, 0) + 2));
+    ncur = K * std::max(epochs - 1, 0);
+    nspec = ncur + 2 * K;
     const size_t bytes = sizeof(uint32_t) * (size_t)n * epochs;
+    maxseg = (int)((Ew + 48.0 * sigma) / SHUF_CK) + 16;
+    const size_t sbytes = sizeof(Seg) * (size_t)maxseg * epochs;
     for (int s = 0; s < 2; s++) {
-        if (hipHostMalloc((void **)&J_host[s], bytes, hipHostMallocDefault) != hipSuccess ||
+        if (hipHostMalloc((void **)&seg_host[s], sbytes, hipHostMallocDefault) != hipSuccess ||
+            hipMalloc((void **)&d_seg[s], sbytes) != hipSuccess ||
             hipMalloc((void **)&d_J[s], bytes) != hipSuccess) {
             err = "shuffle buffers: allocation failed";
             return BPPO_ERR_HIP;
@@ -94,37 +134,41 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
                 return BPPO_ERR_HIP;
             }
     }
+    for (int s = 0; s < 2; s++)
+        if (hipEventCreateWithFlags(&consumed[s], hipEventDisableTiming) != hipSuccess) {
+            err = "shuffle events: creation failed";
+            return BPPO_ERR_HIP;
+        }
     if (hipStreamCreateWithFlags(&copy, hipStreamNonBlocking) != hipSuccess) {
         err = "shuffle copy stream: creation failed";
         return BPPO_ERR_HIP;
     }
-    // word buffer: all epochs plus 12 sigma of slack, whole chunks
-    const double need = epochs * Ew + 12.0 * sigma * std::sqrt((double)epochs) + 4.0 * SHUF_CK + 64.0;
-    wcap = ((uint64_t)need + SHUF_CHUNK - 1) / SHUF_CHUNK * SHUF_CHUNK + SHUF_CHUNK;
-    if (hipMalloc((void **)&d_words, wcap * 4) != hipSuccess ||
-        hipHostMalloc((void **)&h_words, wcap * 4, hipHostMallocDefault) != hipSuccess) {
-        err = "shuffle word buffers: allocation failed";
-        return BPPO_ERR_HIP;
-    }
-    const size_t nch = wcap / SHUF_CHUNK;
-    chunk_ev.assign(nch, nullptr);
-    chunk_ok.reset(new std::atomic<int>[nch]);
-    for (size_t c = 0; c < nch; c++) {
-        chunk_ok[c] = 0;
-        if (hipEventCreateWithFlags(&chunk_ev[c], hipEventDisableTiming) != hipSuccess) {
-            err = "shuffle chunk events: creation failed";
+    // word buffers: the job's epochs plus the carry region, 12 sigma of slack each
+    auto chunks = [](double w) { return ((uint64_t)std::max(w, 1.0) + SHUF_CHUNK - 1) / SHUF_CHUNK * SHUF_CHUNK; };
+    const double sE = sigma * std::sqrt((double)std::max(epochs, 1));
+    const uint64_t cap0 = chunks(epochs * Ew + 12.0 * sE + 4.0 * SHUF_CK) + SHUF_CHUNK;
+    const uint64_t cap1 = K ? chunks(Ew + 6.0 * sE + 12.0 * sigma + 8.0 * SHUF_CK) + SHUF_CHUNK : 0;
+    for (int b = 0; b < 2; b++) {
+        WordBuf &w = wb[b];
+        w.cap = cap0 + cap1;
+        if (hipMalloc((void **)&w.d, w.cap * 4) != hipSuccess ||
+            hipHostMalloc((void **)&w.h, w.cap * 4, hipHostMallocDefault) != hipSuccess) {
+            err = "shuffle word buffers: allocation failed";
             return BPPO_ERR_HIP;
         }
-    }
-    const uint64_t nck = wcap / SHUF_CK + 2;
-    for (int i = 0; i < nspec; i++) {
-        if (hipHostMalloc((void **)&spec[i].J, sizeof(uint32_t) * (size_t)n, hipHostMallocDefault) != hipSuccess) {
-            err = "shuffle speculative buffers: allocation failed";
-            return BPPO_ERR_HIP;
+        const size_t nch = w.cap / SHUF_CHUNK;
+        w.ev.assign(nch, nullptr);
+        w.ok.reset(new std::atomic<int>[nch]);
+        for (size_t c = 0; c < nch; c++) {
+            w.ok[c] = 0;
+            if (hipEventCreateWithFlags(&w.ev[c], hipEventDisableTiming) != hipSuccess) {
+                err = "shuffle chunk events: creation failed";
+                return BPPO_ERR_HIP;
+            }
         }
-        spec[i].ck.assign(nck, 0xFFFFFFFFu);
-        spec[i].done = 1;
     }
+    const uint64_t nck = (uint64_t)((Ew + 24.0 * sigma) / SHUF_CK) + 4;
+    for (int i = 0; i < nspec; i++) spec[i].ck.assign(nck, 0xFFFFFFFFu);
     for (int i = 0; i < nspec; i++) workers.emplace_back([this, i]() { worker(i); });
     th = std::thread([this]() { run(); });
     return BPPO_OK;
@@ -132,38 +176,61 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
 
 int ShuffleEngine::ensure(uint64_t start) {
     std::unique_lock<std::mutex> lk(mu);
-    if (job_valid && job_start == start) return job_slot;
-    if (job_running || job_pending) {
+    for (int sl = 0; sl < 2; sl++)
+        if (slot_valid[sl] && slot_start[sl] == start) {
+            consumer = sl;
+            lk.unlock();
+            cv.notify_all();
+            return sl;
+        }
+    // a start the engine did not predict (KL early stop, rng_set): drop everything
+    if (running >= 0 || pending >= 0) {
         cancel = true;
+        pending = -1;
         cv.notify_all();
-        cv.wait(lk, [&] { return !job_running && !job_pending; });
+        cv.wait(lk, [&] { return running < 0; });
         cancel = false;
     }
-    job_slot ^= 1;
-    job_start = start;
-    job_pending = true;
-    job_valid = true;
-    ready[job_slot] = 0;
+    chain_from = -1;
+    slot_valid[0] = slot_valid[1] = false;
+    const int sl = last_slot ^ 1;
+    last_slot = sl;
+    slot_start[sl] = start;
+    slot_valid[sl] = true;
+    ready[sl] = 0;
+    pending = sl;
+    consumer = sl;
     lk.unlock();
     cv.notify_all();
-    return job_slot;
+    return sl;
 }
 
 void ShuffleEngine::wait_epoch(int slot, int e) {
     std::unique_lock<std::mutex> lk(mu);
-    cv.wait(lk, [&] { return ready[slot] > e; });
+    cv.wait(lk, [&] { return ready[slot] > e || !slot_valid[slot]; });
 }
 
-// words [pos, pos + len) of the current job (one checkpoint piece: never crosses
-// a chunk); outside the GPU-made range (never at the usual sizes) they are made here
-const uint32_t *ShuffleEngine::words(uint64_t pos, uint64_t len, std::vector<uint32_t> &scratch) {
-    if (pos >= wbase && pos + len <= wbase + wlen) {
-        const size_t c = (size_t)((pos - wbase) / SHUF_CHUNK);
-        if (!chunk_ok[c].load(std::memory_order_acquire)) {
-            (void)hipEventSynchronize(chunk_ev[c]);
-            chunk_ok[c].store(1, std::memory_order_release);
+void ShuffleEngine::release(int slot, hipStream_t st) {
+    (void)hipEventRecord(consumed[slot], st);
+    std::lock_guard<std::mutex> lk(mu);
+    consumed_used[slot] = true;
+}
+
+// words [pos, pos + len) of word buffer b (one checkpoint piece: never crosses a
+// chunk); outside its regions (not at the usual sizes) they are made here
+const uint32_t *ShuffleEngine::words(int b, uint64_t pos, uint64_t len, std::vector<uint32_t> &scratch) {
+    WordBuf &w = wb[b];
+    for (int g = 0; g < w.nreg; g++) {
+        const WordBuf::Region &R = w.reg[g];
+        if (pos >= R.base && pos + len <= R.base + R.len) {
+            const uint64_t o = R.off + (pos - R.base);
+            const size_t c = (size_t)(o / SHUF_CHUNK);
+            if (!w.ok[c].load(std::memory_order_acquire)) {
+                (void)hipEventSynchronize(w.ev[c]);
+                w.ok[c].store(1, std::memory_order_release);
+            }
+            return w.h + o;
         }
-        return h_words + (pos - wbase);
     }
     scratch.resize(len);
     bppo_host::chacha12_words(key.k, stream, pos, scratch.data(), len);
@@ -171,43 +238,67 @@ const uint32_t *ShuffleEngine::words(uint64_t pos, uint64_t len, std::vector<uin
 }
 
 // walk from pos up to the next checkpoint boundary (or the end of the shuffle)
-uint64_t ShuffleEngine::walk_piece(uint64_t pos, uint32_t *r, uint32_t *J, std::vector<uint32_t> &scratch) {
+uint64_t ShuffleEngine::walk_piece(int b, uint64_t pos, uint32_t *r, std::vector<uint32_t> &scratch) {
     const uint64_t q = (pos / SHUF_CK + 1) * SHUF_CK;
-    const uint32_t *w = words(pos, q - pos, scratch);
-    return pos + bppo_host::chain_walk(w, (size_t)(q - pos), r, J);
+    const uint32_t *w = words(b, pos, q - pos, scratch);
+    return pos + bppo_host::chain_walk_nj(w, (size_t)(q - pos), r);
+}
+
+void ShuffleEngine::launch_walk(int i, uint64_t start, int wbuf) {
+    SpecWalk &s = spec[i];
+    s.start = start;
+    s.ck_base = start / SHUF_CK * SHUF_CK;
+    s.wbuf = wbuf;
+    s.end = 0;
+    std::fill(s.ck.begin(), s.ck.end(), 0xFFFFFFFFu);
+    s.progress.store(-1, std::memory_order_relaxed);
+    s.stop.store(false, std::memory_order_relaxed);
+    s.done.store(0, std::memory_order_release);
+    s.running = true;
+    s.gen++;
+}
+
+void ShuffleEngine::stop_walks(int lo, int hi) {
+    std::unique_lock<std::mutex> lk(mu);
+    for (int i = lo; i < hi; i++) spec[i].stop.store(true, std::memory_order_relaxed);
+    cv.notify_all();
+    cv.wait(lk, [&] {
+        if (quit) return true;
+        for (int i = lo; i < hi; i++) if (spec[i].running) return false;
+        return true;
+    });
 }
 
 void ShuffleEngine::worker(int i) {
     (void)hipSetDevice(dev);
     std::vector<uint32_t> scratch;
     uint64_t seen = 0;
+    SpecWalk &s = spec[i];
     for (;;) {
         {
             std::unique_lock<std::mutex> lk(mu);
-            cv.wait(lk, [&] { return quit || gen != seen; });
-            if (quit) return;
-            seen = gen;
+            cv.wait(lk, [&] { return quit || s.gen != seen; });
+            if (quit) { s.running = false; cv.notify_all(); return; }
+            seen = s.gen;
         }
-        SpecWalk &s = spec[i];
         uint64_t pos = s.start;
         uint32_t r = n;
-        while (r >= 2 && !cancel.load(std::memory_order_relaxed)) {
+        while (r >= 2 && !s.stop.load(std::memory_order_relaxed)) {
             const uint64_t q = (pos / SHUF_CK + 1) * SHUF_CK;
-            pos = walk_piece(pos, &r, s.J, scratch);
+            pos = walk_piece(s.wbuf, pos, &r, scratch);
             if (pos == q) {
-                const int64_t c = (int64_t)((q - wbase) / SHUF_CK);
+                const int64_t c = (int64_t)((q - s.ck_base) / SHUF_CK);
                 if (c < (int64_t)s.ck.size()) {
                     s.ck[c] = r;
                     s.progress.store(c, std::memory_order_release);
                 }
             }
         }
-        if (n) s.J[0] = 0;
         s.end = pos;
         {
             std::lock_guard<std::mutex> lk(mu);
             s.done.store(1, std::memory_order_release);
-            busy--;
+            s.running = false;
         }
         cv.notify_all();
     }
@@ -219,129 +310,207 @@ void ShuffleEngine::run() {
     for (;;) {
         uint64_t start;
         int slot;
+        bool wait_consumed = false;
         {
             std::unique_lock<std::mutex> lk(mu);
-            cv.wait(lk, [&] { return quit || job_pending; });
+            cv.wait(lk, [&] { return quit || pending >= 0 || (chain_from >= 0 && consumer == chain_from); });
             if (quit) return;
-            job_pending = false;
-            job_running = true;
-            start = job_start;
-            slot = job_slot;
+            if (pending < 0) {
+                // chain: the caller consumes the job just resolved, so the other slot is
+                // free on the host; its GPU readers are ordered by the `consumed` event
+                slot = chain_from ^ 1;
+                chain_from = -1;
+                last_slot = slot;
+                slot_start[slot] = chain_start;
+                slot_valid[slot] = true;
+                ready[slot] = 0;
+            } else {
+                slot = pending;
+                pending = -1;
+            }
+            running = slot;
+            start = slot_start[slot];
+            wait_consumed = consumed_used[slot];
         }
-        SHUF_LOG("[shuf] job start=%llu slot=%d\n", (unsigned long long)start, slot);
-        // uploads still reading the speculative J buffers / host words have finished
-        (void)hipStreamSynchronize(copy);
-        // ---- words of the whole job, made on the GPU, copied in need order
-        wbase = start / SHUF_CK * SHUF_CK;
+        if (wait_consumed) (void)hipStreamWaitEvent(copy, consumed[slot], 0);
+        seq++;
+        const int b = (int)(seq & 1);                 // word buffer and carry set of this job
+        const int cs = 1 - b;                         // carry set the previous job launched for us
+        const int cur0 = 0, cur1 = ncur;
+        const int cn0 = ncur + b * K, cn1 = cn0 + K;  // carry set launched now (next job)
+        const int cp0 = ncur + cs * K, cp1 = cp0 + K; // carry set for this job's epoch 0
+        SHUF_LOG("[shuf] job %llu start=%llu slot=%d carry=%d\n", (unsigned long long)seq, (unsigned long long)start,
+                 slot, (int)carry_valid[cs]);
+        // walks of two jobs ago still on this buffer / carry slots have stopped
+        stop_walks(cn0, cn1);
+        // ---- words: this job's epochs, then the region of the next job's first epoch
+        WordBuf &W = wb[b];
+        const double sE = sigma * std::sqrt((double)std::max(epochs, 1));
         {
-            const double need = (double)(start - wbase) + epochs * Ew +
-                                10.0 * sigma * std::sqrt((double)std::max(epochs, 1)) + 4.0 * SHUF_CK;
-            wlen = std::min(wcap, ((uint64_t)need + SHUF_CHUNK - 1) / SHUF_CHUNK * SHUF_CHUNK);
+            auto chunks = [](double w) { return ((uint64_t)std::max(w, 1.0) + SHUF_CHUNK - 1) / SHUF_CHUNK * SHUF_CHUNK; };
+            W.nreg = 1;
+            W.reg[0].base = start / SHUF_CK * SHUF_CK;
+            W.reg[0].off = 0;
+            W.reg[0].len = std::min(W.cap, chunks((double)(start - W.reg[0].base) + epochs * Ew + 10.0 * sE + 4.0 * SHUF_CK));
+            if (K > 0) {
+                const double lo = (double)start + epochs * Ew + (double)gap - 3.0 * sE - 4.0 * SHUF_CK;
+                uint64_t b1 = (uint64_t)std::max(lo, 0.0) / SHUF_CK * SHUF_CK;
+                b1 = std::max(b1, W.reg[0].base + W.reg[0].len);
+                const uint64_t len1 = std::min(W.cap - W.reg[0].len, chunks(Ew + 6.0 * sE + 12.0 * sigma + 8.0 * SHUF_CK));
+                if (len1 > 0) {
+                    W.reg[1].base = b1; W.reg[1].off = W.reg[0].len; W.reg[1].len = len1;
+                    W.nreg = 2;
+                }
+            }
         }
-        const size_t nch = (size_t)(wlen / SHUF_CHUNK);
-        hipLaunchKernelGGL(k_chacha_words, dim3((unsigned)((wlen / 16 + 255) / 256)), dim3(256), 0, copy, key,
-                           stream, wbase, wlen, d_words);
-        std::vector<std::pair<double, size_t>> order(nch);
-        for (size_t c = 0; c < nch; c++) {
-            chunk_ok[c] = 0;
-            const double off = std::max(0.0, (double)(wbase + c * SHUF_CHUNK) - (double)start);
-            order[c] = {std::fmod(off, std::max(Ew, 1.0)), c};
+        std::vector<std::pair<double, size_t>> order;
+        for (int g = 0; g < W.nreg; g++) {
+            const WordBuf::Region &R = W.reg[g];
+            hipLaunchKernelGGL(k_chacha_words, dim3((unsigned)((R.len / 16 + 255) / 256)), dim3(256), 0, copy, key,
+                               stream, R.base, R.len, W.d + R.off);
+            for (uint64_t o = 0; o < R.len; o += SHUF_CHUNK) {
+                const size_t c = (size_t)((R.off + o) / SHUF_CHUNK);
+                W.ok[c] = 0;
+                const double p = (double)(R.base + o);
+                const double org = g == 0 ? (double)start : (double)start + epochs * Ew + (double)gap;
+                const double key_t = std::fmod(std::max(0.0, p - org + 4.0 * sE), std::max(Ew, 1.0));
+                order.push_back({key_t, c});
+            }
         }
         std::sort(order.begin(), order.end());
         for (auto &oc : order) {
             const size_t c = oc.second;
-            (void)hipMemcpyAsync(h_words + c * SHUF_CHUNK, d_words + c * SHUF_CHUNK, SHUF_CHUNK * 4,
-                                 hipMemcpyDeviceToHost, copy);
-            (void)hipEventRecord(chunk_ev[c], copy);
+            (void)hipMemcpyAsync(W.h + c * SHUF_CHUNK, W.d + c * SHUF_CHUNK, SHUF_CHUNK * 4, hipMemcpyDeviceToHost, copy);
+            (void)hipEventRecord(W.ev[c], copy);
         }
-        // ---- speculative walks of epochs 1 .. E-1
+        // ---- speculative walks: epochs 1 .. E-1 of this job, and the next job's first epoch
         {
             std::lock_guard<std::mutex> lk(mu);
+            auto guess = [&](double centre, double sd, int k) {
+                return (uint64_t)std::max((double)start, std::floor(centre + ((k + 0.5) / K - 0.5) * 3.0 * sd));
+            };
             for (int e = 1; e < epochs; e++)
-                for (int k = 0; k < K; k++) {
-                    SpecWalk &s = spec[(e - 1) * K + k];
-                    const double spread = 3.0 * sigma * std::sqrt((double)e);
-                    const double guess = (double)start + e * Ew + ((k + 0.5) / K - 0.5) * spread;
-                    s.start = (uint64_t)std::max((double)start, std::floor(guess));
-                    s.epoch = e;
-                    s.end = 0;
-                    s.progress.store(-1, std::memory_order_relaxed);
-                    s.done.store(0, std::memory_order_relaxed);
-                    std::fill(s.ck.begin(), s.ck.end(), 0xFFFFFFFFu);
-                }
-            busy = nspec;
-            gen++;
+                for (int k = 0; k < K; k++)
+                    launch_walk(cur0 + (e - 1) * K + k, guess((double)start + e * Ew, sigma * std::sqrt((double)e), k), b);
+            for (int k = 0; k < K; k++)
+                launch_walk(cn0 + k, guess((double)start + epochs * Ew + (double)gap, sE, k), b);
+            carry_valid[b] = K > 0;
         }
         cv.notify_all();
-        // ---- true walks
+        // ---- true walks (checkpoint states only; J is rebuilt on the GPU)
         uint64_t pos = start;
         bool cancelled = false;
+        std::vector<std::pair<uint64_t, uint32_t>> tck;
         for (int e = 0; e < epochs && !cancelled; e++) {
             auto t0 = std::chrono::steady_clock::now();
             if (ev_used[slot][e]) (void)hipEventSynchronize(ev[slot][e]);   // previous upload of this buffer
-            uint32_t *J = J_host[slot] + (size_t)e * n;
             uint32_t r = n;
-            int met = -1;
-            int walked = 0;
+            int met = -1, walked = 0;
+            int s0 = 0, s1 = 0;                        // candidate speculative walks for this epoch
+            if (e == 0) { if (carry_valid[cs]) { s0 = cp0; s1 = cp1; } }
+            else { s0 = cur0 + (e - 1) * K; s1 = s0 + K; }
+            tck.clear();
+            tck.push_back({pos, r});
             while (r >= 2) {
                 const uint64_t q = (pos / SHUF_CK + 1) * SHUF_CK;
-                pos = walk_piece(pos, &r, J, scratch);
+                pos = walk_piece(b, pos, &r, scratch);
                 if (cancel.load(std::memory_order_relaxed)) { cancelled = true; break; }
-                if (pos != q || r < 2 || e == 0 || K == 0) continue;
+                if (pos != q || r < 2) continue;
+                tck.push_back({q, r});
+                if (s0 == s1) continue;
                 walked++;
-                const int64_t c = (int64_t)((q - wbase) / SHUF_CK);
-                for (int k = 0; k < K && met < 0; k++) {
-                    SpecWalk &s = spec[(e - 1) * K + k];
-                    if (s.start > q || c >= (int64_t)s.ck.size()) continue;
-                    // wait until that walk has passed q (or finished before it)
-                    while (s.progress.load(std::memory_order_acquire) < c && !s.done.load(std::memory_order_acquire) &&
+                for (int i = s0; i < s1 && met < 0; i++) {
+                    SpecWalk &sp = spec[i];
+                    if (q <= sp.start) continue;
+                    const int64_t c = (int64_t)((q - sp.ck_base) / SHUF_CK);
+                    if (c >= (int64_t)sp.ck.size()) continue;
+                    // wait until that walk has passed q (or stopped before it)
+                    while (sp.progress.load(std::memory_order_acquire) < c && !sp.done.load(std::memory_order_acquire) &&
                            !cancel.load(std::memory_order_relaxed))
                         std::this_thread::yield();
-                    if (s.progress.load(std::memory_order_acquire) >= c && s.ck[c] == r) met = (e - 1) * K + k;
+                    if (sp.progress.load(std::memory_order_acquire) >= c && sp.ck[c] == r) met = i;
                 }
                 if (met >= 0) break;
             }
             if (cancelled) break;
-            uint32_t *dJ = d_J[slot] + (size_t)e * n;
+            Seg *S = seg_host[slot] + (size_t)e * maxseg;
+            int ns = 0;
+            bool overflow = false;
+            auto add = [&](uint64_t p0, uint64_t p1, uint32_t r0) {
+                if (p1 <= p0 || r0 < 2) return;
+                if (ns >= maxseg) { overflow = true; return; }
+                S[ns++] = Seg{p0, p1, r0, 0};
+            };
+            for (size_t i = 0; i + 1 < tck.size(); i++) add(tck[i].first, tck[i + 1].first, tck[i].second);
             if (met >= 0) {
-                SpecWalk &s = spec[met];
-                while (!s.done.load(std::memory_order_acquire) && !cancel.load(std::memory_order_relaxed))
+                SpecWalk &sp = spec[met];
+                while (!sp.done.load(std::memory_order_acquire) && !cancel.load(std::memory_order_relaxed))
                     std::this_thread::yield();
-                if (!s.done.load(std::memory_order_acquire)) { cancelled = true; break; }
-                pos = s.end;
-                // J[r .. n) from the true walk, J[0 .. r) from the speculative walk
-                (void)hipMemcpyAsync(dJ + r, J + r, sizeof(uint32_t) * (size_t)(n - r), hipMemcpyHostToDevice, copy);
-                (void)hipMemcpyAsync(dJ, s.J, sizeof(uint32_t) * (size_t)r, hipMemcpyHostToDevice, copy);
+                if (cancel.load(std::memory_order_relaxed)) { cancelled = true; break; }
+                // from the meeting checkpoint on, the speculative walk's states
+                const int64_t last = sp.progress.load(std::memory_order_acquire);
+                for (int64_t c = (int64_t)((tck.back().first - sp.ck_base) / SHUF_CK); c <= last; c++) {
+                    const uint64_t q0 = sp.ck_base + (uint64_t)c * SHUF_CK;
+                    if (q0 >= sp.end) break;
+                    add(q0, std::min(q0 + SHUF_CK, sp.end), sp.ck[c]);
+                }
+                pos = sp.end;
                 coalesced[slot][e] = walked;
             } else {
-                if (n) J[0] = 0;
-                (void)hipMemcpyAsync(dJ, J, sizeof(uint32_t) * n, hipMemcpyHostToDevice, copy);
+                add(tck.back().first, pos, tck.back().second);
                 coalesced[slot][e] = -1;
+            }
+            if (overflow) {   // never at sane sizes: fall back to the sequential walk of the epoch
+                std::vector<uint32_t> Jh(n);
+                const uint64_t e0 = shuffle_walk_host(key, stream, tck.front().first, n, Jh.data());
+                (void)hipMemcpyAsync(d_J[slot] + (size_t)e * n, Jh.data(), 4ull * n, hipMemcpyHostToDevice, copy);
+                (void)hipStreamSynchronize(copy);
+                pos = e0;
+            } else {
+                WordRegions wr{};
+                for (int bb = 0; bb < 2; bb++)
+                    for (int g = 0; g < wb[bb].nreg; g++) {
+                        wr.ptr[wr.n] = wb[bb].d + wb[bb].reg[g].off;
+                        wr.base[wr.n] = wb[bb].reg[g].base;
+                        wr.len[wr.n] = wb[bb].reg[g].len;
+                        wr.n++;
+                    }
+                Seg *dS = d_seg[slot] + (size_t)e * maxseg;
+                (void)hipMemcpyAsync(dS, S, sizeof(Seg) * (size_t)std::max(ns, 1), hipMemcpyHostToDevice, copy);
+                hipLaunchKernelGGL(k_expand_J, dim3((unsigned)((std::max(ns, 1) + 63) / 64)), dim3(64), 0, copy, key,
+                                   stream, (const Seg *)dS, ns, wr, d_J[slot] + (size_t)e * n);
             }
             end_pos[slot][e] = pos;
             (void)hipEventRecord(ev[slot][e], copy);
             ev_used[slot][e] = true;
             walk_ms[slot][e] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-            SHUF_LOG("[shuf] epoch %d end=%llu met=%d (%.2f ms)\n", e, (unsigned long long)pos, coalesced[slot][e],
-                     walk_ms[slot][e]);
+            SHUF_LOG("[shuf] epoch %d end=%llu met=%d segs=%d (%.2f ms)\n", e, (unsigned long long)pos,
+                     coalesced[slot][e], ns, walk_ms[slot][e]);
             {
                 std::lock_guard<std::mutex> lk(mu);
                 ready[slot] = e + 1;
             }
             cv.notify_all();
+            if (K > 0) stop_walks(s0, s1);        // this epoch's walks have served
+            if (e == 0) carry_valid[cs] = false;
         }
-        SHUF_LOG("[shuf] job done cancelled=%d, stopping walkers\n", (int)cancelled);
-        // leftover speculative walks matter only until their epoch is resolved:
-        // stop them and wait, so the next job can reuse their buffers
+        SHUF_LOG("[shuf] job done cancelled=%d\n", (int)cancelled);
+        // this job's in-update walks are done with; the carry set keeps running for
+        // the next job (all of it is dropped on a cancel)
+        stop_walks(cur0, cur1);
+        if (cancelled) {
+            stop_walks(0, nspec);
+            carry_valid[0] = carry_valid[1] = false;
+        }
         {
-            std::unique_lock<std::mutex> lk(mu);
-            cancel = true;
-            cv.notify_all();
-            // (at shutdown, workers that never picked up this job just exit)
-            cv.wait(lk, [&] { return busy == 0 || quit; });
-            cancel = false;
-            job_running = false;
-            if (cancelled) job_valid = false;
+            std::lock_guard<std::mutex> lk(mu);
+            running = -1;
+            if (cancelled) {
+                slot_valid[slot] = false;
+            } else {
+                chain_from = slot;                     // next job: gap words after this one's end
+                chain_start = end_pos[slot][epochs - 1] + gap;
+            }
         }
         cv.notify_all();
     }
@@ -353,6 +522,7 @@ void ShuffleEngine::shutdown() {
             std::lock_guard<std::mutex> lk(mu);
             quit = true;
             cancel = true;
+            for (int i = 0; i < nspec; i++) spec[i].stop = true;
         }
         cv.notify_all();
         th.join();
@@ -361,15 +531,18 @@ void ShuffleEngine::shutdown() {
     }
     if (copy) { (void)hipStreamSynchronize(copy); (void)hipStreamDestroy(copy); copy = nullptr; }
     for (int s = 0; s < 2; s++) {
+        if (consumed[s]) { (void)hipEventDestroy(consumed[s]); consumed[s] = nullptr; }
         for (int e = 0; e < epochs; e++) if (ev[s][e]) { (void)hipEventDestroy(ev[s][e]); ev[s][e] = nullptr; }
-        if (J_host[s]) { (void)hipHostFree(J_host[s]); J_host[s] = nullptr; }
+        if (seg_host[s]) { (void)hipHostFree(seg_host[s]); seg_host[s] = nullptr; }
+        if (d_seg[s]) { (void)hipFree(d_seg[s]); d_seg[s] = nullptr; }
         if (d_J[s]) { (void)hipFree(d_J[s]); d_J[s] = nullptr; }
     }
-    for (auto &e : chunk_ev) if (e) (void)hipEventDestroy(e);
-    chunk_ev.clear();
-    for (int i = 0; i < SHUF_MAX_SPEC; i++) if (spec[i].J) { (void)hipHostFree(spec[i].J); spec[i].J = nullptr; }
-    if (d_words) { (void)hipFree(d_words); d_words = nullptr; }
-    if (h_words) { (void)hipHostFree(h_words); h_words = nullptr; }
+    for (int b = 0; b < 2; b++) {
+        for (auto &e : wb[b].ev) if (e) (void)hipEventDestroy(e);
+        wb[b].ev.clear();
+        if (wb[b].d) { (void)hipFree(wb[b].d); wb[b].d = nullptr; }
+        if (wb[b].h) { (void)hipHostFree(wb[b].h); wb[b].h = nullptr; }
+    }
 }
 
 // single-shot host walk (parity hook): J for one shuffle of n from word position pos

@@ -225,6 +225,72 @@ static size_t walk_avx512(const u32 *w, size_t nw, u32 *rp, u32 *J) {
     return p;
 }
 
+// the same chain without the J stores: only the range r advances (speculative
+// and true walks record checkpoint states; the GPU rebuilds J from them)
+static inline size_t walk_scalar_nj(const u32 *w, size_t nw, u32 *rp) {
+    u32 r = *rp;
+    size_t p = 0;
+    while (r >= 2 && p < nw) {
+        const int lz = __builtin_clz(r);
+        const u32 lowr = 1u << (31 - lz), s = 1u << lz;
+        u32 z = (r << lz) - 1u;
+        while (r >= lowr && r >= 2 && p < nw) {
+            const u32 lo = w[p++] * r;
+            const u32 acc = lo <= z;
+            r -= acc;
+            z -= acc ? s : 0u;
+        }
+    }
+    *rp = r;
+    return p;
+}
+
+__attribute__((target("avx512f,avx512bw,avx512vl,avx512dq,bmi,bmi2,popcnt")))
+static size_t walk_avx512_nj(const u32 *w, size_t nw, u32 *rp) {
+    u32 r = *rp;
+    size_t p = 0;
+    const __m512i kidx = _mm512_setr_epi32(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+    while (r >= 2 && p < nw) {
+        const int lz = __builtin_clz(r);
+        const u32 lowr = 1u << (31 - lz), s = 1u << lz;
+        while (r >= lowr + 24 && p + 16 <= nw) {
+            const u32 z = (r << lz) - 1u;
+            const __m512i wv = _mm512_loadu_si512((const void *)(w + p));
+            const __m512i rk = _mm512_sub_epi32(_mm512_set1_epi32((int)r), kidx);
+            __m512i lo = _mm512_mullo_epi32(wv, rk);
+            __m512i zz = _mm512_sub_epi32(_mm512_set1_epi32((int)z), _mm512_slli_epi32(kidx, lz));
+            const __m512i sv = _mm512_set1_epi32((int)s);
+            u64 M[8];
+            for (int j = 0; j < 8; j++) {
+                M[j] = (u64)_mm512_cmple_epu32_mask(lo, zz);
+                lo = _mm512_add_epi32(lo, wv);
+                zz = _mm512_add_epi32(zz, sv);
+            }
+            u64 k = 0, rejmask = 0;
+            for (int j = 0; j < 8; j++) {
+                const u64 rej = ((~M[j]) & 0xFFFFull & (~0ull << k)) | (1ull << 16);
+                const u64 kz = (u64)__builtin_ctzll(rej);
+                rejmask |= 1ull << kz;
+                k = kz + 1;
+            }
+            const u32 stop = k > 16 ? 16u : (u32)k;
+            const u32 valid = (u32)((1u << stop) - 1u);
+            r -= (u32)__builtin_popcount((~(u32)rejmask) & valid);
+            p += stop;
+        }
+        u32 z = (r << lz) - 1u;
+        while (r >= lowr && r >= 2 && p < nw) {
+            const u32 lo = w[p++] * r;
+            const u32 a = lo <= z;
+            r -= a;
+            z -= a ? s : 0u;
+            if (r >= lowr + 24 && p + 16 <= nw) break;
+        }
+    }
+    *rp = r;
+    return p;
+}
+
 static int isa_level() {
     static int v = -1;
     if (v < 0) {
@@ -236,6 +302,11 @@ static int isa_level() {
 }
 
 int chain_walk_isa() { return isa_level(); }
+
+size_t chain_walk_nj(const u32 *w, size_t nw, u32 *r) {
+    if (isa_level() == 2) return walk_avx512_nj(w, nw, r);
+    return walk_scalar_nj(w, nw, r);
+}
 
 size_t chain_walk(const u32 *w, size_t nw, u32 *r, u32 *J) {
     if (isa_level() == 2) return walk_avx512(w, nw, r, J);

@@ -21,6 +21,9 @@ void chacha12_words(const uint32_t key[8], uint64_t stream, uint64_t pos, uint32
 // 16 words where the CPU has it, else the scalar band loop.
 size_t chain_walk(const uint32_t *w, size_t nw, uint32_t *r, uint32_t *J);
 
+// chain_walk without writing J (the range r advances exactly the same way)
+size_t chain_walk_nj(const uint32_t *w, size_t nw, uint32_t *r);
+
 // 2 = AVX-512 walker, 1 = scalar
 int chain_walk_isa();
 

@@ -174,12 +174,14 @@ bppo_status bppo_debug_libm(int32_t which, int32_t device, const float *x, float
 bppo_status bppo_debug_shuffle_chain(uint64_t seed, uint64_t stream, uint64_t word_pos, uint32_t n,
                                      uint32_t *J, uint64_t *end_pos);
 bppo_status bppo_debug_fisher_yates(int32_t device, const uint32_t *J, uint32_t n, uint32_t *perm);
-/* the whole shuffle engine (GPU-made ChaCha words, speculative walks) for `epochs`
- * consecutive shuffles of n from word position start: J [epochs][n], end word
- * positions [epochs], met [epochs] = checkpoints walked before meeting a
- * speculative walk (-1 = none; may be NULL).  Must equal chained shuffle_chain calls. */
+/* the whole shuffle engine (GPU-made ChaCha words, speculative walks, J rebuilt on
+ * the GPU) for `jobs` updates of `epochs` shuffles of n: the first from word
+ * position start, each next update `gap` words after the previous one's last
+ * shuffle.  J [jobs][epochs][n], end word positions [jobs][epochs], met = checkpoints
+ * walked before meeting a speculative walk (-1 = none; may be NULL).  Must equal
+ * chained shuffle_chain calls. */
 bppo_status bppo_debug_shuffle_engine(uint64_t seed, uint64_t stream, uint64_t start, uint32_t n, int32_t epochs,
-                                      uint32_t *J, uint64_t *ends, int32_t *met);
+                                      uint64_t gap, int32_t jobs, uint32_t *J, uint64_t *ends, int32_t *met);
 
 /* GEMM engine parity hook (host buffers).  mode 0: out[M][N] = act(A[M][K] B[K][N] + bias[N])
  * with matrixmultiply's KC=256 fma-chain order (Burn Linear forward, mlp.rs:140-206);

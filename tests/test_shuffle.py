@@ -67,27 +67,31 @@ def test_device_fisher_yates_matches_sequential(n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed,start,n,epochs", [
-    (42, 1_000_003, 1 << 23, 4),        # CfgB: 4 epochs of 2^23 (speculative walks meet the true walk)
-    (7, 5, 100_003, 6),                 # small n, many epochs
-    (3, 0, 2, 3),                       # degenerate
-    (11, 12_345, (1 << 20) + 1, 2),
+@pytest.mark.parametrize("seed,start,n,epochs,gap,jobs", [
+    (42, 1_000_003, 1 << 23, 4, 16_777_216, 3),   # CfgB: 3 updates (the 2nd and 3rd meet speculative walks)
+    (7, 5, 100_003, 6, 700_000, 3),                # small n, many epochs
+    (3, 0, 2, 3, 5, 2),                            # degenerate
+    (11, 12_345, (1 << 20) + 1, 2, 0, 2),
 ])
-def test_shuffle_engine_equals_sequential_walks(seed, start, n, epochs):
-    """The engine (GPU-made words, speculative walks spliced at a meeting
-    checkpoint) returns exactly the chained single-thread walks."""
-    J = np.zeros(n * epochs, np.uint32)
-    ends = np.zeros(epochs, np.uint64)
-    met = np.zeros(epochs, np.int32)
-    assert L.lib().bppo_debug_shuffle_engine(seed, 0, start, n, epochs, J.ctypes.data, ends.ctypes.data,
-                                             met.ctypes.data) == 0
+def test_shuffle_engine_equals_sequential_walks(seed, start, n, epochs, gap, jobs):
+    """The engine (GPU-made words, speculative walks for the next update spliced
+    at a meeting checkpoint, J rebuilt on the GPU from checkpoint states) returns
+    exactly the chained single-thread walks."""
+    J = np.zeros(n * epochs * jobs, np.uint32)
+    ends = np.zeros(epochs * jobs, np.uint64)
+    met = np.zeros(epochs * jobs, np.int32)
+    assert L.lib().bppo_debug_shuffle_engine(seed, 0, start, n, epochs, gap, jobs, J.ctypes.data,
+                                             ends.ctypes.data, met.ctypes.data) == 0
     pos = start
-    for e in range(epochs):
-        Je = np.zeros(n, np.uint32)
-        end = C.c_uint64()
-        assert L.lib().bppo_debug_shuffle_chain(seed, 0, pos, n, Je.ctypes.data, C.byref(end)) == 0
-        assert ends[e] == end.value, (e, met)
-        assert np.array_equal(J[e * n:(e + 1) * n], Je), (e, met)
-        pos = end.value
+    for j in range(jobs):
+        for e in range(epochs):
+            k = j * epochs + e
+            Je = np.zeros(n, np.uint32)
+            end = C.c_uint64()
+            assert L.lib().bppo_debug_shuffle_chain(seed, 0, pos, n, Je.ctypes.data, C.byref(end)) == 0
+            assert ends[k] == end.value, (j, e, met)
+            assert np.array_equal(J[k * n:(k + 1) * n], Je), (j, e, met)
+            pos = end.value
+        pos += gap
     if n == 1 << 23:
-        assert (met[1:] >= 0).any(), met      # at CfgB size the speculation does meet
+        assert (met[epochs:] >= 0).any(), met      # at CfgB size the speculation does meet
