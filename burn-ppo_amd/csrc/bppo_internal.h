@@ -50,7 +50,7 @@ struct Welford { double n, mean, m2; };
 // remaining range) meets one of them, after which both are the same walk.
 constexpr int SHUF_MAX_EPOCHS = 32;
 constexpr int SHUF_MAX_SPEC = 40;
-constexpr uint64_t SHUF_CK = 4096;               // checkpoint spacing (words)
+constexpr uint64_t SHUF_CK = 1024;               // checkpoint spacing (words) = GPU J segment length
 constexpr uint64_t SHUF_CHUNK = (uint64_t)1 << 20; // words per GPU->host copy
 
 struct SpecWalk {

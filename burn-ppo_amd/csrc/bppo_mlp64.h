@@ -43,10 +43,12 @@ __device__ __forceinline__ void load_params(Params &S, const float *__restrict__
 __device__ __forceinline__ int cd_row(int q, int h) { return (q & 3) + 8 * (q >> 2) + 4 * h; }
 }  // namespace mmb
 
+// LDS hand-off between the lanes of ONE wave: wait for this wave's LDS
+// operations only (lgkmcnt), not for its outstanding global loads (a wavefront
+// release fence would also drain vmcnt and stall the prefetched gathers)
 __device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 typedef float f32x16_t __attribute__((ext_vector_type(16)));

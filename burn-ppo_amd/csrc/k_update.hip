@@ -387,19 +387,42 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
     float m_pl = 0, m_vl = 0, m_h = 0, m_kl = 0, m_cf = 0, m_v = 0, m_r = 0, m_ve = 0, m_ve2 = 0;
     float m_vemax = -INFINITY, m_n = 0;
 
-    for (uint32_t base = (uint32_t)gwave * TR; base < g.n; base += (uint32_t)nwaves * TR) {
+    // software pipeline of the gather (ppo.rs:1833-1857): the shuffled index two
+    // tiles ahead, the row data one tile ahead, so the dependent loads of the next
+    // tile run under this tile's MFMAs
+    const uint32_t stride = (uint32_t)nwaves * TR;
+    auto idx_of = [&](uint32_t b) -> uint32_t {
+        const uint32_t rr = b + c;
+        return (h == 0 && rr < g.n) ? g.perm[g.start + rr] : 0xFFFFFFFFu;
+    };
+    struct RowData { float x[5]; int a; float olp, A, R, ov; };
+    auto load_row = [&](uint32_t idx, RowData &d) {
+        if (idx != 0xFFFFFFFFu) {
+#pragma unroll
+            for (int k = 0; k < 5; k++) d.x[k] = g.obs[(size_t)idx * 5 + k];
+            d.a = g.act[idx]; d.olp = g.logp[idx]; d.A = g.adv[idx]; d.R = g.ret[idx];
+            d.ov = g.clip_value ? g.val[idx] : 0.0f;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 5; k++) d.x[k] = 0.0f;
+            d.a = 0; d.olp = d.A = d.R = d.ov = 0.0f;
+        }
+    };
+    RowData nxt;
+    uint32_t idx_next = idx_of((uint32_t)gwave * TR + stride);
+    load_row(idx_of((uint32_t)gwave * TR), nxt);
+    for (uint32_t base = (uint32_t)gwave * TR; base < g.n; base += stride) {
         const uint32_t r = base + c;
         const bool valid = h == 0 && r < g.n;
-        float x[5] = {0, 0, 0, 0, 0};
-        int a = 0;
-        float olp = 0.0f, A = 0.0f, R = 0.0f, ov = 0.0f;
-        if (valid) {
-            const uint32_t idx = g.perm[g.start + r];
+        const RowData cur = nxt;
+        const uint32_t idx_after = idx_of(base + 2 * stride);
+        load_row(idx_next, nxt);
+        idx_next = idx_after;
+        float x[5];
 #pragma unroll
-            for (int d = 0; d < 5; d++) x[d] = g.obs[(size_t)idx * 5 + d];
-            a = g.act[idx]; olp = g.logp[idx]; A = g.adv[idx]; R = g.ret[idx];
-            if (g.clip_value) ov = g.val[idx];
-        }
+        for (int d = 0; d < 5; d++) x[d] = cur.x[d];
+        const int a = cur.a;
+        const float olp = cur.olp, A = cur.A, R = cur.R, ov = cur.ov;
         if (h == 0) {
 #pragma unroll
             for (int d = 0; d < 5; d++) B.X[c * 9 + d] = x[d];

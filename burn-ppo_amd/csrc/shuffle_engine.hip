@@ -71,8 +71,8 @@ struct WordRegions {
     uint64_t base[4], len[4];
     int n;
 };
-__global__ void __launch_bounds__(64) k_expand_J(Key8 key, uint64_t stream, const ShuffleEngine::Seg *segs, int ns,
-                                                 WordRegions wr, uint32_t *J) {
+__global__ void __launch_bounds__(256) k_expand_J(Key8 key, uint64_t stream, const ShuffleEngine::Seg *segs, int ns,
+                                                  WordRegions wr, uint32_t *J) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i == 0) J[0] = 0;
     if (i >= ns) return;
@@ -81,15 +81,30 @@ __global__ void __launch_bounds__(64) k_expand_J(Key8 key, uint64_t stream, cons
     const uint32_t *src = nullptr;
     for (int k = 0; k < wr.n; k++)
         if (g.pos0 >= wr.base[k] && g.pos1 <= wr.base[k] + wr.len[k]) src = wr.ptr[k] + (g.pos0 - wr.base[k]);
-    WordCursor c;
-    c.init(key, stream, g.pos0);
     const uint64_t nw = g.pos1 - g.pos0;
-    for (uint64_t p = 0; p < nw && r >= 2; p++) {
-        const uint32_t w = src ? src[p] : c.next();
+    auto step = [&](uint32_t w) {
         const uint64_t m = (uint64_t)w * r;
         const uint32_t z = (r << __clz(r)) - 1u;
         if ((uint32_t)m <= z) { J[r - 1] = (uint32_t)(m >> 32); r--; }
+    };
+    if (!src) {
+        WordCursor c;
+        c.init(key, stream, g.pos0);
+        for (uint64_t p = 0; p < nw && r >= 2; p++) step(c.next());
+        return;
     }
+    // head up to 16-byte alignment, then 16 words per iteration (4 x 16-byte loads)
+    uint64_t p = 0;
+    while (p < nw && (((uintptr_t)(src + p)) & 15) && r >= 2) step(src[p++]);
+    for (; p + 16 <= nw && r >= 2; p += 16) {
+        const uint4 *v = reinterpret_cast<const uint4 *>(src + p);
+        const uint4 a0 = v[0], a1 = v[1], a2 = v[2], a3 = v[3];
+        const uint32_t w[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
+                                a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+#pragma unroll
+        for (int j = 0; j < 16; j++) if (r >= 2) step(w[j]);
+    }
+    for (; p < nw && r >= 2; p++) step(src[p]);
 }
 
 // expected words per shuffle of n and its std dev: draw with range R accepts with
@@ -479,7 +494,7 @@ void ShuffleEngine::run() {
                     }
                 Seg *dS = d_seg[slot] + (size_t)e * maxseg;
                 (void)hipMemcpyAsync(dS, S, sizeof(Seg) * (size_t)std::max(ns, 1), hipMemcpyHostToDevice, copy);
-                hipLaunchKernelGGL(k_expand_J, dim3((unsigned)((std::max(ns, 1) + 63) / 64)), dim3(64), 0, copy, key,
+                hipLaunchKernelGGL(k_expand_J, dim3((unsigned)((std::max(ns, 1) + 255) / 256)), dim3(256), 0, copy, key,
                                    stream, (const Seg *)dS, ns, wr, d_J[slot] + (size_t)e * n);
             }
             end_pos[slot][e] = pos;
