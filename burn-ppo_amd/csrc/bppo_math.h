@@ -64,7 +64,8 @@ BPPO_TABLE uint64_t kExp2fTab[32] = {
         0x3fef5818dcfba487ULL, 0x3fef7c97337b9b5fULL, 0x3fefa4afa2a490daULL, 0x3fefd0765b6e4540ULL};
 
 // ------------------------------------------------------------------ logf ----
-BPPO_HD float logf_glibc(float x) {
+// (the _tab forms take the tables from a caller-chosen copy, e.g. in LDS)
+BPPO_HD float logf_glibc_tab(float x, const double *invc_t, const double *logc_t) {
     // __logf_data (LOGF_TABLE_BITS = 4): {invc, logc}
             const double Ln2 = 0x1.62e42fefa39efp-1;
     const double A0 = -0x1.00ea348b88334p-2, A1 = 0x1.5575b0be00b6ap-2,
@@ -82,7 +83,7 @@ BPPO_HD float logf_glibc(float x) {
     int i = (int)((tmp >> (23 - 4)) % 16);
     int k = (int32_t)tmp >> 23;
     uint32_t iz = ix - (tmp & (0x1ffu << 23));
-    double invc = kLogfInvc[i], logc = kLogfLogc[i];
+    double invc = invc_t[i], logc = logc_t[i];
     double z = (double)asfloat(iz);
     double r = fma(z, invc, -1.0);
     double y0 = fma((double)k, Ln2, logc);
@@ -92,6 +93,7 @@ BPPO_HD float logf_glibc(float x) {
     y = fma(y, r2, y0 + r);
     return (float)y;
 }
+BPPO_HD float logf_glibc(float x) { return logf_glibc_tab(x, kLogfInvc, kLogfLogc); }
 
 // ---------------------------------------------------------- sinf / cosf ----
 struct sincos_t {
@@ -211,7 +213,7 @@ BPPO_HD float cosf_glibc(float y) {
 BPPO_HD uint64_t asuint64(double f) { uint64_t u; memcpy(&u, &f, 8); return u; }
 BPPO_HD double asdouble(uint64_t u) { double f; memcpy(&f, &u, 8); return f; }
 
-BPPO_HD float expf_glibc(float x) {
+BPPO_HD float expf_glibc_tab(float x, const uint64_t *tab) {
         const double SHIFT = 0x1.8p+52, InvLn2N = 0x1.71547652b82fep+5;
     const double C0 = 0x1.c6af84b912394p-20, C1 = 0x1.ebfce50fac4f3p-13, C2 = 0x1.62e42ff0c52d6p-6;
     double xd = (double)x;
@@ -227,7 +229,7 @@ BPPO_HD float expf_glibc(float x) {
     uint64_t ki = asuint64(kd);
     kd -= SHIFT;
     double r = fma(InvLn2N, xd, -kd);   // glibc's -mfma build contracts z - kd
-    uint64_t t = kExp2fTab[ki % 32];
+    uint64_t t = tab[ki % 32];
     t += ki << (52 - 5);
     double s = asdouble(t);
     double zz = fma(C0, r, C1);
@@ -237,5 +239,7 @@ BPPO_HD float expf_glibc(float x) {
     y = y * s;
     return (float)y;
 }
+
+BPPO_HD float expf_glibc(float x) { return expf_glibc_tab(x, kExp2fTab); }
 
 }  // namespace bppo_math

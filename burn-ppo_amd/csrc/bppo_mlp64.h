@@ -4,11 +4,16 @@
 // v_mfma_f32_32x32x2_f32 C/D layout helpers.
 #pragma once
 #include "bppo_device.h"
+#include "bppo_math.h"
 
 namespace bppo {
 namespace mmb {
 constexpr int H = 64, RS = 65, TR = 32;          // hidden width, LDS row stride, rows per wave tile
 struct Params {
+    // glibc expf / logf tables (bppo_math.h) in LDS: the loss's five expf and
+    // one logf per row read them at LDS latency instead of from the L2
+    uint64_t exp2tab[32];
+    double linvc[16], llogc[16];
     float W0[6 * H];      // [d][k], d = 5 is a zero pad row (K 5 -> 6)
     float b0[H];
     float W1[H * RS];     // [k][o], row stride 65: conflict-free for both operand reads
@@ -17,6 +22,8 @@ struct Params {
     float bp[2];
     float Wv[H];
     float bv[2];
+    __device__ __forceinline__ float expf(float x) const { return bppo_math::expf_glibc_tab(x, exp2tab); }
+    __device__ __forceinline__ float logf(float x) const { return bppo_math::logf_glibc_tab(x, linvc, llogc); }
 };
 struct Wave {
     float X[TR * 9];      // [row][d]
@@ -26,6 +33,28 @@ struct Wave {
 constexpr int WAVES = 8;
 constexpr size_t LDS = sizeof(Params) + WAVES * sizeof(Wave);
 
+// per-wave LDS of the minibatch kernel: H1 and H2 -> dZ2 both stay in LDS
+// (neither is held in registers through the backward); X at stride 5
+// (conflict-free: 5c mod 64 is distinct over 32 lanes)
+struct WaveB {
+    float X[TR * 5];
+    float T1[TR * RS];    // H1 [row][k]
+    float T2[TR * RS];    // H2, then dZ2 in place [row][o]
+    float dl[TR * 4];
+};
+constexpr size_t LDSB = sizeof(Params) + WAVES * sizeof(WaveB);
+static_assert(LDSB <= 160 * 1024, "minibatch kernel LDS over the gfx950 limit");
+
+// 64-row tiles (two 32-row MFMA tiles per wave, one wave per SIMD, 512 VGPRs)
+constexpr int TR64 = 64;
+struct Wave64 {
+    float X[TR64 * 9];
+    float T[TR64 * RS];
+    float dl[TR64 * 4];
+};
+constexpr int WAVES64 = 4;
+constexpr size_t LDS64 = sizeof(Params) + WAVES64 * sizeof(Wave64);
+
 // whole block: flat Burn-order params -> LDS layout
 __device__ __forceinline__ void load_params(Params &S, const float *__restrict__ P) {
     constexpr CpOffsets O = cp_offsets<64, 2>();
@@ -34,6 +63,11 @@ __device__ __forceinline__ void load_params(Params &S, const float *__restrict__
     for (int i = threadIdx.x; i < H; i += blockDim.x) {
         S.b0[i] = P[O.b0 + i]; S.b1[i] = P[O.b1 + i]; S.Wv[i] = P[O.wv + i];
         S.Wp[2 * i] = P[O.wp + 2 * i]; S.Wp[2 * i + 1] = P[O.wp + 2 * i + 1];
+    }
+    if (threadIdx.x < 32) S.exp2tab[threadIdx.x] = bppo_math::kExp2fTab[threadIdx.x];
+    if (threadIdx.x < 16) {
+        S.linvc[threadIdx.x] = bppo_math::kLogfInvc[threadIdx.x];
+        S.llogc[threadIdx.x] = bppo_math::kLogfLogc[threadIdx.x];
     }
     if (threadIdx.x < 2) S.bp[threadIdx.x] = P[O.bp + threadIdx.x];
     if (threadIdx.x == 0) S.bv[0] = P[O.bv];
