@@ -153,6 +153,7 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     TRY(dalloc(c, &c->d_perm, TN));
     TRY(dalloc(c, &c->d_fy, 4 * TN));
     TRY(dalloc(c, &c->d_scan, TN / 8192 + 2));
+    BPPO_HIP(c, fy_ranges_init(c->fyr, (uint32_t)TN));
     TRY(dalloc(c, &c->d_red, 4 * 1024 + 64));
     TRY(dalloc(c, &c->d_mb_stats, 8));
     BPPO_HIP(c, hipHostMalloc((void **)&c->h_red, sizeof(double) * (4 * 1024 + 64), hipHostMallocDefault));
@@ -196,6 +197,7 @@ extern "C" void bppo_destroy(bppo_ctx *c) {
                     c->d_eps, c->d_ep_count, c->d_err, c->d_perm, c->d_fy, c->d_scan,
                     c->d_red, c->d_mb_stats, c->d_gumbel};
     for (void *p : ptrs) if (p) (void)hipFree(p);
+    fy_ranges_free(c->fyr);
     if (c->h_red) (void)hipHostFree(c->h_red);
     for (int i = 0; i < 8; i++) {
         if (c->ev[i][0]) (void)hipEventDestroy(c->ev[i][0]);
@@ -755,13 +757,16 @@ extern "C" bppo_status bppo_debug_fisher_yates(int32_t device, const uint32_t *J
     if (!J || !perm) return BPPO_ERR_ARG;
     if (hipSetDevice(device) != hipSuccess) return BPPO_ERR_HIP;
     uint32_t *dJ = nullptr, *dP = nullptr, *dS = nullptr, *dC = nullptr;
+    FyRanges rg;
     bppo_status s = BPPO_ERR_HIP;
     if (hipMalloc((void **)&dJ, 4ull * n + 4) == hipSuccess && hipMalloc((void **)&dP, 4ull * n + 4) == hipSuccess &&
         hipMalloc((void **)&dS, 16ull * n + 16) == hipSuccess && hipMalloc((void **)&dC, 4ull * (n / 8192 + 2)) == hipSuccess &&
         hipMemcpy(dJ, J, 4ull * n, hipMemcpyHostToDevice) == hipSuccess &&
-        fisher_yates_device(dJ, n, dS, dC, dP, nullptr) == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
+        fy_ranges_init(rg, n) == hipSuccess &&
+        fisher_yates_device(dJ, n, dS, dC, dP, nullptr, &rg) == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
         hipMemcpy(perm, dP, 4ull * n, hipMemcpyDeviceToHost) == hipSuccess)
         s = BPPO_OK;
     (void)hipFree(dJ); (void)hipFree(dP); (void)hipFree(dS); (void)hipFree(dC);
+    fy_ranges_free(rg);
     return s;
 }

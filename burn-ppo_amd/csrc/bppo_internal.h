@@ -73,6 +73,14 @@ struct WordBuf {                                  // ChaCha12 words made on the 
     std::unique_ptr<std::atomic<int>[]> ok;
 };
 
+// target-range table of the ranged Fisher-Yates bucketing (k_shuffle.hip)
+struct FyRanges {
+    uint32_t *x = nullptr;            // device [nb + 1] range boundaries
+    uint32_t *cb = nullptr;           // device [ncb] first range of each 2^11-target block
+    int nb = 0, ncb = 0;              // nb = 0: direct bucketing only
+    uint32_t n = 0;
+};
+
 struct ShuffleEngine {
     int dev = 0;
     uint32_t n = 0;
@@ -196,6 +204,7 @@ struct bppo_ctx {
     uint32_t *d_perm = nullptr;       // shuffled indices of the current epoch
     uint32_t *d_fy = nullptr;         // Fisher-Yates scratch [4][TN]: count/offset, bucket, succ, fw
     uint32_t *d_scan = nullptr;       // scan block sums
+    bppo::FyRanges fyr;               // target ranges of the ranged Fisher-Yates bucketing
     int shuf_slot = -1;               // engine slot holding this update's J
     // scratch
     double *d_red = nullptr;          // reduction scratch
@@ -264,7 +273,9 @@ bppo_status launch_return_norm(bppo_ctx *c);
 // (k_update.hip)
 bppo_status launch_fisher_yates(bppo_ctx *c, const uint32_t *d_J, uint32_t n);
 hipError_t fisher_yates_device(const uint32_t *d_J, uint32_t n, uint32_t *scratch, uint32_t *scan, uint32_t *perm,
-                               hipStream_t st);
+                               hipStream_t st, const FyRanges *rg);
+hipError_t fy_ranges_init(FyRanges &r, uint32_t n);
+void fy_ranges_free(FyRanges &r);
 bppo_status launch_adv_stats(bppo_ctx *c, uint32_t start, uint32_t n);
 bppo_status launch_minibatch(bppo_ctx *c, uint32_t mb_start, uint32_t mb_size, float ent_coef,
                              double *h_stats_out);

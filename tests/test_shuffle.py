@@ -50,7 +50,7 @@ def test_host_chain_full_cfgb_epoch():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [1, 2, 3, 17, 1000, 8193, 100_003, 1 << 23])
+@pytest.mark.parametrize("n", [1, 2, 3, 17, 1000, 8193, 100_003, (1 << 20) - 1, 1 << 20, 3_000_017, 1 << 23])
 def test_device_fisher_yates_matches_sequential(n):
     rng = np.random.default_rng(n)
     i = np.arange(n, dtype=np.uint64)
@@ -59,6 +59,32 @@ def test_device_fisher_yates_matches_sequential(n):
     if n > 10:
         J[n // 2] = n // 2            # self-swaps
         J[n - 1] = 0                  # a long bucket at 0
+    perm = np.zeros(n, np.uint32)
+    assert L.lib().bppo_debug_fisher_yates(0, J.ctypes.data, n, perm.ctypes.data) == 0
+    ref = np.arange(n, dtype=np.uint32)
+    O.lib().or_apply_swaps(J, ref, n)
+    assert np.array_equal(perm, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["identity", "half", "front"])
+def test_device_fisher_yates_skewed_targets(kind):
+    """Inputs far from J[i] ~ U[0, i]: target ranges overflow their LDS capacity
+    (front: every step targets the first 4096 positions) and the gated direct
+    bucketing must produce the permutation; identity / half stay in the ranged
+    path.  n = 2^20 (the ranged path's minimum).  (The direct path orders each
+    target's steps by insertion sort: quadratic in the largest bucket, which is
+    ~ln n for RNG-drawn J; a J with 10^5+ steps on one target is not a case.)"""
+    n = 1 << 20
+    i = np.arange(n, dtype=np.uint64)
+    if kind == "identity":
+        J = i.astype(np.uint32)
+    elif kind == "half":
+        J = (i // 2).astype(np.uint32)
+    else:                                   # every step targets one of the first 4096 positions
+        rng = np.random.default_rng(5)
+        J = np.minimum(rng.integers(0, 4096, n, dtype=np.uint64), i).astype(np.uint32)
+    J[0] = 0
     perm = np.zeros(n, np.uint32)
     assert L.lib().bppo_debug_fisher_yates(0, J.ctypes.data, n, perm.ctypes.data) == 0
     ref = np.arange(n, dtype=np.uint32)
