@@ -460,6 +460,10 @@ void ShuffleEngine::run() {
             };
             for (size_t i = 0; i + 1 < tck.size(); i++) add(tck[i].first, tck[i + 1].first, tck[i].second);
             if (met >= 0) {
+                // the other walks of this boundary cannot serve any more: free their CPUs
+                // for the met one (it still has to finish the epoch) and the later epochs
+                for (int i = s0; i < s1; i++)
+                    if (i != met) spec[i].stop.store(true, std::memory_order_relaxed);
                 SpecWalk &sp = spec[met];
                 while (!sp.done.load(std::memory_order_acquire) && !cancel.load(std::memory_order_relaxed))
                     std::this_thread::yield();

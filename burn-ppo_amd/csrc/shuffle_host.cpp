@@ -245,38 +245,46 @@ static inline size_t walk_scalar_nj(const u32 *w, size_t nw, u32 *rp) {
     return p;
 }
 
+// 32 words per block, 16 hypotheses m = rejections so far (r_j = r - j + m).
+// M[m] = acceptance of every word under hypothesis m.  The resolution keeps the
+// mask L of positions consumed so far: the next rejection under hypothesis m is
+// the lowest bit of Z_m = ~M[m] above L, so L' = blsmsk(Z_m & ~L) — two 1-cycle
+// ops per step.  Bits >= 32 of Z are set (virtual rejections past the block),
+// so after the 16 steps P = popcount(L) gives the block exactly:
+//   consumed = min(P, 32), accepted = P - 16
+// (16 rejections inside the block: P = last one + 1; fewer: P = 32 + the
+// virtual ones).
 __attribute__((target("avx512f,avx512bw,avx512vl,avx512dq,bmi,bmi2,popcnt")))
 static size_t walk_avx512_nj(const u32 *w, size_t nw, u32 *rp) {
     u32 r = *rp;
     size_t p = 0;
     const __m512i kidx = _mm512_setr_epi32(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+    const __m512i kidx16 = _mm512_add_epi32(kidx, _mm512_set1_epi32(16));
     while (r >= 2 && p < nw) {
         const int lz = __builtin_clz(r);
         const u32 lowr = 1u << (31 - lz), s = 1u << lz;
-        while (r >= lowr + 24 && p + 16 <= nw) {
+        const __m512i sv = _mm512_set1_epi32((int)s);
+        const __m512i kz = _mm512_slli_epi32(kidx, lz), kz16 = _mm512_slli_epi32(kidx16, lz);
+        while (r >= lowr + 48 && p + 32 <= nw) {
             const u32 z = (r << lz) - 1u;
-            const __m512i wv = _mm512_loadu_si512((const void *)(w + p));
-            const __m512i rk = _mm512_sub_epi32(_mm512_set1_epi32((int)r), kidx);
-            __m512i lo = _mm512_mullo_epi32(wv, rk);
-            __m512i zz = _mm512_sub_epi32(_mm512_set1_epi32((int)z), _mm512_slli_epi32(kidx, lz));
-            const __m512i sv = _mm512_set1_epi32((int)s);
-            u64 M[8];
-            for (int j = 0; j < 8; j++) {
-                M[j] = (u64)_mm512_cmple_epu32_mask(lo, zz);
-                lo = _mm512_add_epi32(lo, wv);
-                zz = _mm512_add_epi32(zz, sv);
+            const __m512i w0 = _mm512_loadu_si512((const void *)(w + p));
+            const __m512i w1 = _mm512_loadu_si512((const void *)(w + p + 16));
+            const __m512i rv = _mm512_set1_epi32((int)r), zv = _mm512_set1_epi32((int)z);
+            __m512i lo0 = _mm512_mullo_epi32(w0, _mm512_sub_epi32(rv, kidx));
+            __m512i lo1 = _mm512_mullo_epi32(w1, _mm512_sub_epi32(rv, kidx16));
+            __m512i zz0 = _mm512_sub_epi32(zv, kz), zz1 = _mm512_sub_epi32(zv, kz16);
+            u64 Z[16];
+            for (int j = 0; j < 16; j++) {
+                const u32 m = (u32)_mm512_cmple_epu32_mask(lo0, zz0) | ((u32)_mm512_cmple_epu32_mask(lo1, zz1) << 16);
+                Z[j] = (u64)(~m) | 0xFFFFFFFF00000000ull;
+                lo0 = _mm512_add_epi32(lo0, w0); lo1 = _mm512_add_epi32(lo1, w1);
+                zz0 = _mm512_add_epi32(zz0, sv); zz1 = _mm512_add_epi32(zz1, sv);
             }
-            u64 k = 0, rejmask = 0;
-            for (int j = 0; j < 8; j++) {
-                const u64 rej = ((~M[j]) & 0xFFFFull & (~0ull << k)) | (1ull << 16);
-                const u64 kz = (u64)__builtin_ctzll(rej);
-                rejmask |= 1ull << kz;
-                k = kz + 1;
-            }
-            const u32 stop = k > 16 ? 16u : (u32)k;
-            const u32 valid = (u32)((1u << stop) - 1u);
-            r -= (u32)__builtin_popcount((~(u32)rejmask) & valid);
-            p += stop;
+            u64 L = 0;
+            for (int j = 0; j < 16; j++) L = _blsmsk_u64(Z[j] & ~L);
+            const u32 P = (u32)__builtin_popcountll(L);
+            r -= P - 16;
+            p += P < 32 ? P : 32;
         }
         u32 z = (r << lz) - 1u;
         while (r >= lowr && r >= 2 && p < nw) {
@@ -284,7 +292,7 @@ static size_t walk_avx512_nj(const u32 *w, size_t nw, u32 *rp) {
             const u32 a = lo <= z;
             r -= a;
             z -= a ? s : 0u;
-            if (r >= lowr + 24 && p + 16 <= nw) break;
+            if (r >= lowr + 48 && p + 32 <= nw) break;
         }
     }
     *rp = r;
