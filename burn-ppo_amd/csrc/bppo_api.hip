@@ -156,6 +156,7 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     BPPO_HIP(c, fy_ranges_init(c->fyr, (uint32_t)TN));
     TRY(dalloc(c, &c->d_red, 4 * 1024 + 64));
     TRY(dalloc(c, &c->d_mb_stats, 8));
+    TRY(dalloc(c, &c->d_rows, (size_t)cfg->num_epochs * cfg->num_minibatches * (WM_COUNT + 4)));
     BPPO_HIP(c, hipHostMalloc((void **)&c->h_red, sizeof(double) * (4 * 1024 + 64), hipHostMallocDefault));
     for (int i = 0; i < 8; i++) {
         BPPO_HIP(c, hipEventCreate(&c->ev[i][0]));
@@ -195,7 +196,7 @@ extern "C" void bppo_destroy(bppo_ctx *c) {
                     c->d_done, c->d_val, c->d_logp, c->d_adv, c->d_ret, c->d_act, c->d_X, c->d_on,
                     c->d_obs_part, c->d_rn_returns, c->d_rn_stats, c->d_scan_agg, c->d_last_v,
                     c->d_eps, c->d_ep_count, c->d_err, c->d_perm, c->d_fy, c->d_scan,
-                    c->d_red, c->d_mb_stats, c->d_gumbel};
+                    c->d_red, c->d_mb_stats, c->d_gumbel, c->d_rows};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     fy_ranges_free(c->fyr);
     if (c->h_red) (void)hipHostFree(c->h_red);
@@ -490,6 +491,11 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
     double wait_ms = 0.0;
     tm_begin(c, TM_UPDATE);
     float fw_ms = 0, sh_ms = 0;
+    // without a KL early stop or a host all-reduce nothing in the loop needs the
+    // metrics on the host: the minibatches are enqueued back to back and the rows
+    // are read once after the last one (no per-minibatch stream drain)
+    const bool deferred = c->cfg.target_kl < 0 && !(c->allreduce && c->world > 1);
+    int nrow = 0;
     for (int ep = 0; ep < c->cfg.num_epochs && !stop; ep++) {
         epochs_run++;
         {
@@ -529,21 +535,34 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
             }
             TRY(launch_adam(c, (float)lr, c1, c2));
             if (c->wide) TRY(wide_pack(c));
-            // metric row: grad[np .. np+NM) and adv stats
-            std::vector<float> row(NM + 4);
-            BPPO_HIP(c, hipMemcpyAsync(row.data(), c->d_grad + np, sizeof(float) * NM, hipMemcpyDeviceToHost, c->stream));
-            BPPO_HIP(c, hipMemcpyAsync(row.data() + NM, c->d_mb_stats, sizeof(float) * 4, hipMemcpyDeviceToHost, c->stream));
-            BPPO_HIP(c, hipStreamSynchronize(c->stream));
-            float ms = 0;
-            if (hipEventElapsedTime(&ms, c->ev[TM_FWDBWD][0], c->ev[TM_FWDBWD][1]) == hipSuccess) fw_ms = ms;
-            if (mb == 0 && hipEventElapsedTime(&ms, s0, s1) == hipSuccess) sh_ms = ms;
-            rows.insert(rows.end(), row.begin(), row.end());
-            if (c->cfg.target_kl >= 0) {
+            // metric row: grad[np .. np+NM) and adv stats, into the update's device rows
+            TRY(launch_metric_row(c, c->d_rows + (size_t)nrow * (NM + 4), NM));
+            nrow++;
+            if (!deferred) {
+                std::vector<float> row(NM + 4);
+                BPPO_HIP(c, hipMemcpyAsync(row.data(), c->d_rows + (size_t)(nrow - 1) * (NM + 4), sizeof(float) * (NM + 4),
+                                           hipMemcpyDeviceToHost, c->stream));
+                BPPO_HIP(c, hipStreamSynchronize(c->stream));
+                float ms = 0;
+                if (hipEventElapsedTime(&ms, c->ev[TM_FWDBWD][0], c->ev[TM_FWDBWD][1]) == hipSuccess) fw_ms = ms;
+                if (mb == 0 && hipEventElapsedTime(&ms, s0, s1) == hipSuccess) sh_ms = ms;
+                rows.insert(rows.end(), row.begin(), row.end());
+            }
+            if (!deferred && c->cfg.target_kl >= 0) {
+                const float *row = &rows[rows.size() - (NM + 4)];
                 const float n = row[10] > 0 ? row[10] : 1.0f;
                 if (row[3] / n > (float)c->cfg.target_kl) { stop = true; break; }   // ppo.rs:2019-2023
             }
             start += sz;
         }
+    }
+    if (deferred && nrow > 0) {
+        rows.resize((size_t)nrow * (NM + 4));
+        BPPO_HIP(c, hipMemcpyAsync(rows.data(), c->d_rows, sizeof(float) * rows.size(), hipMemcpyDeviceToHost, c->stream));
+        BPPO_HIP(c, hipStreamSynchronize(c->stream));
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, c->ev[TM_FWDBWD][0], c->ev[TM_FWDBWD][1]) == hipSuccess) fw_ms = ms;
+        if (hipEventElapsedTime(&ms, c->ev[TM_SHUFFLE][0], c->ev[TM_SHUFFLE][1]) == hipSuccess) sh_ms = ms;
     }
     tm_end(c, TM_UPDATE);
     c->rng_pos = c->shuf.end_pos[slot][epochs_run - 1];   // only started epochs consumed words

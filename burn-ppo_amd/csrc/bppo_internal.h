@@ -210,6 +210,7 @@ struct bppo_ctx {
     double *d_red = nullptr;          // reduction scratch
     double *h_red = nullptr;          // pinned mirror
     float *d_mb_stats = nullptr;      // [mean, inv_std...] per minibatch
+    float *d_rows = nullptr;          // per-minibatch metric rows of one update [E*M][WM_COUNT + 4]
     // all-reduce hook
     bppo_allreduce_fn allreduce = nullptr;
     void *allreduce_user = nullptr;
@@ -280,6 +281,7 @@ bppo_status launch_adv_stats(bppo_ctx *c, uint32_t start, uint32_t n);
 bppo_status launch_minibatch(bppo_ctx *c, uint32_t mb_start, uint32_t mb_size, float ent_coef,
                              double *h_stats_out);
 bppo_status launch_adam(bppo_ctx *c, float lr, const float *c1, const float *c2);
+bppo_status launch_metric_row(bppo_ctx *c, float *dst, int nm);
 bppo_status launch_explained_variance(bppo_ctx *c, double *out6);
 // (wide_api.hip) multi-player path
 bppo_status wide_init(bppo_ctx *c);

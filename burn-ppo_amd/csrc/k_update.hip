@@ -1123,6 +1123,19 @@ bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_
     return BPPO_OK;
 }
 
+// one minibatch's metric sums (grad tail) and advantage stats into the update's rows
+__global__ void k_metric_row(const float *gtail, const float *mb_stats, int nm, float *dst) {
+    const int i = threadIdx.x;
+    if (i < nm) dst[i] = gtail[i];
+    else if (i < nm + 4) dst[i] = mb_stats[i - nm];
+}
+bppo_status launch_metric_row(bppo_ctx *c, float *dst, int nm) {
+    hipLaunchKernelGGL(k_metric_row, dim3(1), dim3(64), 0, c->stream, c->d_grad + c->net.n_params, c->d_mb_stats, nm,
+                       dst);
+    BPPO_HIP(c, hipGetLastError());
+    return BPPO_OK;
+}
+
 bppo_status launch_adam(bppo_ctx *c, float lr, const float *c1, const float *c2) {
     AdamArgs a;
     a.params = c->d_params; a.grad = c->d_grad; a.m1 = c->d_m1; a.m2 = c->d_m2;
