@@ -155,7 +155,8 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     TRY(dalloc(c, &c->d_scan, TN / 8192 + 2));
     BPPO_HIP(c, fy_ranges_init(c->fyr, (uint32_t)TN));
     TRY(dalloc(c, &c->d_red, 4 * 1024 + 64));
-    TRY(dalloc(c, &c->d_mb_stats, 8));
+    TRY(dalloc(c, &c->d_mb_stats, (size_t)4 * std::max(cfg->num_minibatches, 2)));
+    c->d_mb_cur = c->d_mb_stats;
     TRY(dalloc(c, &c->d_rows, (size_t)cfg->num_epochs * cfg->num_minibatches * (WM_COUNT + 4)));
     BPPO_HIP(c, hipHostMalloc((void **)&c->h_red, sizeof(double) * (4 * 1024 + 64), hipHostMallocDefault));
     for (int i = 0; i < 8; i++) {
@@ -508,13 +509,14 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
         (void)hipEventRecord(s0, c->stream);
         TRY(launch_fisher_yates(c, c->shuf.d_J[slot] + (size_t)ep * B, (uint32_t)B));
         (void)hipEventRecord(s1, c->stream);
+        TRY(launch_epoch_adv_stats(c, (uint32_t)B, M));
         size_t start = 0;
         for (int mb = 0; mb < M; mb++) {
             const size_t sz = base_mb + ((size_t)mb < rem ? 1 : 0);
             if (sz == 0) continue;
             (void)hipEventRecord(c->ev[TM_FWDBWD][0], c->stream);
+            c->d_mb_cur = c->d_mb_stats + 4 * mb;
             if (c->wide) {
-                TRY(launch_adv_stats(c, (uint32_t)start, (uint32_t)sz));
                 TRY(wide_minibatch(c, (uint32_t)start, (uint32_t)sz, (float)ent_coef));
             } else {
                 TRY(launch_minibatch(c, (uint32_t)start, (uint32_t)sz, (float)ent_coef, nullptr));

@@ -209,7 +209,8 @@ struct bppo_ctx {
     // scratch
     double *d_red = nullptr;          // reduction scratch
     double *h_red = nullptr;          // pinned mirror
-    float *d_mb_stats = nullptr;      // [mean, inv_std...] per minibatch
+    float *d_mb_stats = nullptr;      // advantage [mean, std, min, max] of each minibatch of the epoch [M][4]
+    float *d_mb_cur = nullptr;        // the current minibatch's row of d_mb_stats
     float *d_rows = nullptr;          // per-minibatch metric rows of one update [E*M][WM_COUNT + 4]
     // all-reduce hook
     bppo_allreduce_fn allreduce = nullptr;
@@ -277,7 +278,7 @@ hipError_t fisher_yates_device(const uint32_t *d_J, uint32_t n, uint32_t *scratc
                                hipStream_t st, const FyRanges *rg);
 hipError_t fy_ranges_init(FyRanges &r, uint32_t n);
 void fy_ranges_free(FyRanges &r);
-bppo_status launch_adv_stats(bppo_ctx *c, uint32_t start, uint32_t n);
+bppo_status launch_epoch_adv_stats(bppo_ctx *c, uint32_t B, int M);
 bppo_status launch_minibatch(bppo_ctx *c, uint32_t mb_start, uint32_t mb_size, float ent_coef,
                              double *h_stats_out);
 bppo_status launch_adam(bppo_ctx *c, float lr, const float *c1, const float *c2);

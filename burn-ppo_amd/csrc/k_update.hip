@@ -12,78 +12,7 @@
 
 namespace bppo {
 
-// ============================================================ adv stats ====
-// two-pass, f64 accumulation, fixed-order final reduction
-constexpr int STAT_BLOCKS = 1024;
-
-__global__ void __launch_bounds__(256) k_adv_pass(const float *adv, const uint32_t *perm,
-                                                  uint32_t start, uint32_t n, const float *mb_stats,
-                                                  int pass, double *part) {
-    __shared__ double s0[256], s1[256];
-    __shared__ float smin[256], smax[256];
-    double a0 = 0.0;
-    float mn = INFINITY, mx = -INFINITY;
-    const float mean = pass ? mb_stats[0] : 0.0f;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        float a = adv[perm[start + i]];
-        if (pass == 0) {
-            a0 += (double)a;
-            mn = fminf(mn, a); mx = fmaxf(mx, a);
-        } else {
-            double d = (double)a - (double)mean;
-            a0 += d * d;
-        }
-    }
-    s0[threadIdx.x] = a0; smin[threadIdx.x] = mn; smax[threadIdx.x] = mx;
-    __syncthreads();
-    for (int st = 128; st > 0; st >>= 1) {
-        if (threadIdx.x < st) {
-            s0[threadIdx.x] += s0[threadIdx.x + st];
-            smin[threadIdx.x] = fminf(smin[threadIdx.x], smin[threadIdx.x + st]);
-            smax[threadIdx.x] = fmaxf(smax[threadIdx.x], smax[threadIdx.x + st]);
-        }
-        __syncthreads();
-    }
-    (void)s1;
-    if (threadIdx.x == 0) {
-        part[blockIdx.x * 3 + 0] = s0[0];
-        part[blockIdx.x * 3 + 1] = (double)smin[0];
-        part[blockIdx.x * 3 + 2] = (double)smax[0];
-    }
-}
-
-// mb_stats: [0] mean (f32), [1] std (f32, unbiased), [2] min, [3] max
-// 256 threads: strided partial sums, then a fixed-order LDS tree (deterministic)
-__global__ void __launch_bounds__(256) k_adv_finalize(const double *part, int nblk, uint32_t n, int pass,
-                                                      float *mb_stats) {
-    __shared__ double ss[256], smn[256], smx[256];
-    double s = 0.0, mn = INFINITY, mx = -INFINITY;
-    for (int b = threadIdx.x; b < nblk; b += blockDim.x) {
-        s += part[b * 3];
-        mn = fmin(mn, part[b * 3 + 1]);
-        mx = fmax(mx, part[b * 3 + 2]);
-    }
-    ss[threadIdx.x] = s; smn[threadIdx.x] = mn; smx[threadIdx.x] = mx;
-    __syncthreads();
-    for (int st = 128; st > 0; st >>= 1) {
-        if (threadIdx.x < st) {
-            ss[threadIdx.x] += ss[threadIdx.x + st];
-            smn[threadIdx.x] = fmin(smn[threadIdx.x], smn[threadIdx.x + st]);
-            smx[threadIdx.x] = fmax(smx[threadIdx.x], smx[threadIdx.x + st]);
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x != 0) return;
-    s = ss[0]; mn = smn[0]; mx = smx[0];
-    if (pass == 0) {
-        mb_stats[0] = (float)(s / (double)n);
-        mb_stats[2] = (float)mn;
-        mb_stats[3] = (float)mx;
-    } else {
-        float var = n > 1 ? (float)(s / (double)(n - 1)) : NAN;
-        mb_stats[1] = sqrtf(var);
-    }
-}
+constexpr int STAT_BLOCKS = 1024;   // partial blocks of the explained-variance sums
 
 // =========================================================== fwd + bwd ====
 // metric slots appended after the parameters in the gradient slab
@@ -1065,14 +994,90 @@ __global__ void __launch_bounds__(256) k_ev(size_t n, const float *val, const fl
 }
 
 // ------------------------------------------------------------- launchers ---
-// raw advantage stats of the minibatch (ppo.rs:1905-1913, utils.rs:80-89) -> d_mb_stats
-bppo_status launch_adv_stats(bppo_ctx *c, uint32_t start, uint32_t n) {
-    for (int pass = 0; pass < 2; pass++) {
-        hipLaunchKernelGGL(k_adv_pass, dim3(STAT_BLOCKS), dim3(256), 0, c->stream, c->d_adv, c->d_perm,
-                           start, n, c->d_mb_stats, pass, c->d_red);
-        hipLaunchKernelGGL(k_adv_finalize, dim3(1), dim3(256), 0, c->stream, c->d_red, STAT_BLOCKS, n,
-                           pass, c->d_mb_stats);
+// advantage stats of every minibatch of one epoch in one pass (ppo.rs:1905-1913,
+// utils.rs:80-89): f64 sum and sum of squares, min, max over each minibatch's
+// shuffled rows.  Block b owns positions [b C, (b + 1) C) with C no larger than
+// the smallest minibatch, so it touches at most two minibatches; the final pass
+// adds the block partials of each minibatch in block order (deterministic).
+struct EpochSplit { uint32_t B, base, rem, M; };   // minibatch m has base + (m < rem) rows
+__device__ __forceinline__ uint32_t mb_of(uint32_t i, const EpochSplit &s) {
+    const uint32_t big = s.rem * (s.base + 1);
+    return i < big ? i / (s.base + 1) : s.rem + (i - big) / s.base;
+}
+__global__ void __launch_bounds__(256) k_adv_epoch(const float *adv, const uint32_t *perm, EpochSplit sp, uint32_t C,
+                                                   double *part) {
+    __shared__ double ss[2][256], sq[2][256];
+    __shared__ float smn[2][256], smx[2][256];
+    const uint32_t i0 = blockIdx.x * C, i1 = min(sp.B, i0 + C);
+    const uint32_t m0 = mb_of(i0, sp);
+    double s[2] = {0.0, 0.0}, q[2] = {0.0, 0.0};
+    float mn[2] = {INFINITY, INFINITY}, mx[2] = {-INFINITY, -INFINITY};
+    for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+        const float a = adv[perm[i]];
+        const double d = (double)a;
+        if (mb_of(i, sp) != m0) { s[1] += d; q[1] += d * d; mn[1] = fminf(mn[1], a); mx[1] = fmaxf(mx[1], a); }
+        else { s[0] += d; q[0] += d * d; mn[0] = fminf(mn[0], a); mx[0] = fmaxf(mx[0], a); }
     }
+    for (int k = 0; k < 2; k++) {
+        ss[k][threadIdx.x] = s[k]; sq[k][threadIdx.x] = q[k]; smn[k][threadIdx.x] = mn[k]; smx[k][threadIdx.x] = mx[k];
+    }
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+        if (threadIdx.x < st)
+            for (int k = 0; k < 2; k++) {
+                ss[k][threadIdx.x] += ss[k][threadIdx.x + st];
+                sq[k][threadIdx.x] += sq[k][threadIdx.x + st];
+                smn[k][threadIdx.x] = fminf(smn[k][threadIdx.x], smn[k][threadIdx.x + st]);
+                smx[k][threadIdx.x] = fmaxf(smx[k][threadIdx.x], smx[k][threadIdx.x + st]);
+            }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0)
+        for (int k = 0; k < 2; k++) {
+            double *o = part + ((size_t)blockIdx.x * 2 + k) * 4;
+            o[0] = ss[k][0]; o[1] = sq[k][0]; o[2] = smn[k][0]; o[3] = smx[k][0];
+        }
+}
+// one block per minibatch: its rows' partials in block order -> [mean, std, min, max]
+__global__ void __launch_bounds__(256) k_adv_epoch_final(const double *part, int nblk, uint32_t C, EpochSplit sp,
+                                                         float *stats) {
+    __shared__ double ss[256], sq[256], smn[256], smx[256];
+    const uint32_t m = blockIdx.x;
+    double s = 0.0, q = 0.0, mn = INFINITY, mx = -INFINITY;
+    for (int b = threadIdx.x; b < nblk; b += blockDim.x) {
+        const uint32_t m0 = mb_of((uint32_t)b * C, sp);
+        if (m != m0 && m != m0 + 1) continue;
+        const double *o = part + ((size_t)b * 2 + (m != m0)) * 4;
+        s += o[0]; q += o[1]; mn = fmin(mn, o[2]); mx = fmax(mx, o[3]);
+    }
+    ss[threadIdx.x] = s; sq[threadIdx.x] = q; smn[threadIdx.x] = mn; smx[threadIdx.x] = mx;
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+        if (threadIdx.x < st) {
+            ss[threadIdx.x] += ss[threadIdx.x + st]; sq[threadIdx.x] += sq[threadIdx.x + st];
+            smn[threadIdx.x] = fmin(smn[threadIdx.x], smn[threadIdx.x + st]);
+            smx[threadIdx.x] = fmax(smx[threadIdx.x], smx[threadIdx.x + st]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x != 0) return;
+    const double n = (double)(sp.base + (m < sp.rem ? 1u : 0u));
+    const double mean = ss[0] / n;
+    stats[m * 4 + 0] = (float)mean;
+    stats[m * 4 + 1] = n > 1.0 ? sqrtf((float)(fmax(sq[0] - ss[0] * mean, 0.0) / (n - 1.0))) : NAN;
+    stats[m * 4 + 2] = (float)smn[0];
+    stats[m * 4 + 3] = (float)smx[0];
+}
+
+bppo_status launch_epoch_adv_stats(bppo_ctx *c, uint32_t B, int M) {
+    EpochSplit sp{B, B / (uint32_t)M, B % (uint32_t)M, (uint32_t)M};
+    uint32_t C = (B + 511) / 512;
+    if (sp.base > 0 && C > sp.base) C = sp.base;
+    if (sp.base == 0) C = 1;
+    const uint32_t nblk = (B + C - 1) / C;
+    if ((size_t)nblk * 8 > 4 * 1024 + 64) { c->err = "epoch advantage stats: too many minibatches"; return BPPO_ERR_UNSUPPORTED; }
+    hipLaunchKernelGGL(k_adv_epoch, dim3(nblk), dim3(256), 0, c->stream, c->d_adv, c->d_perm, sp, C, c->d_red);
+    hipLaunchKernelGGL(k_adv_epoch_final, dim3(M), dim3(256), 0, c->stream, c->d_red, (int)nblk, C, sp, c->d_mb_stats);
     BPPO_HIP(c, hipGetLastError());
     return BPPO_OK;
 }
@@ -1080,12 +1085,10 @@ bppo_status launch_adv_stats(bppo_ctx *c, uint32_t start, uint32_t n) {
 bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_coef,
                              double *) {
     const int h = c->cfg.hidden_size, nl = c->cfg.num_hidden;
-    bppo_status st = launch_adv_stats(c, start, n);
-    if (st != BPPO_OK) return st;
     MbArgs g;
     g.obs = c->d_obs; g.logp = c->d_logp; g.adv = c->d_adv; g.ret = c->d_ret; g.val = c->d_val;
     g.act = c->d_act; g.perm = c->d_perm; g.start = start; g.n = n; g.params = c->d_params;
-    g.mb_stats = c->d_mb_stats; g.slab = c->d_slab; g.np = (int)c->net.n_params;
+    g.mb_stats = c->d_mb_cur; g.slab = c->d_slab; g.np = (int)c->net.n_params;
     g.lo = (float)(1.0 - c->cfg.clip_epsilon); g.hi = (float)(1.0 + c->cfg.clip_epsilon);
     g.ceps = (float)c->cfg.clip_epsilon;
     g.inv_mb = (float)(1.0 / (double)n); g.ent_coef = ent_coef; g.value_coef = (float)c->cfg.value_coef;
@@ -1130,7 +1133,7 @@ __global__ void k_metric_row(const float *gtail, const float *mb_stats, int nm, 
     else if (i < nm + 4) dst[i] = mb_stats[i - nm];
 }
 bppo_status launch_metric_row(bppo_ctx *c, float *dst, int nm) {
-    hipLaunchKernelGGL(k_metric_row, dim3(1), dim3(64), 0, c->stream, c->d_grad + c->net.n_params, c->d_mb_stats, nm,
+    hipLaunchKernelGGL(k_metric_row, dim3(1), dim3(64), 0, c->stream, c->d_grad + c->net.n_params, c->d_mb_cur, nm,
                        dst);
     BPPO_HIP(c, hipGetLastError());
     return BPPO_OK;

@@ -212,7 +212,7 @@ bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, float ent_c
     LossArgs g;
     g.perm = c->d_perm; g.start = start; g.n = mb; g.act = c->d_act; g.logp = c->d_logp; g.adv = c->d_adv;
     g.ret = c->d_ret; g.val = c->d_val; g.mask = c->d_mask; g.logits = c->d_logits; g.values = c->d_values;
-    g.mb_stats = c->d_mb_stats; g.dout = c->d_dout; g.part = c->d_mpart;
+    g.mb_stats = c->d_mb_cur; g.dout = c->d_dout; g.part = c->d_mpart;
     g.lo = (float)(1.0 - c->cfg.clip_epsilon); g.hi = (float)(1.0 + c->cfg.clip_epsilon);
     g.ceps = (float)c->cfg.clip_epsilon; g.inv_mb = (float)(1.0 / (double)mb); g.ent_coef = ent_coef;
     g.value_coef = (float)c->cfg.value_coef; g.clip_value = c->cfg.clip_value;
