@@ -92,6 +92,14 @@ extern "C" const char *bppo_version(void) { return "bppo-mi355x 0.1 (gfx950)"; }
 
 extern "C" const char *bppo_last_error(const bppo_ctx *c) { return c ? c->err.c_str() : "null ctx"; }
 
+// wait for the context stream on a blocking-sync event: the host thread sleeps
+// instead of polling (polling eats the CPU quota the shuffle walkers run on)
+static hipError_t sync_stream(bppo_ctx *c) {
+    if (!c->ev_block) return hipStreamSynchronize(c->stream);
+    hipError_t e = hipEventRecord(c->ev_block, c->stream);
+    return e == hipSuccess ? hipEventSynchronize(c->ev_block) : e;
+}
+
 static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *stream) {
     c->cfg = *cfg;
     c->dev = dev;
@@ -159,6 +167,7 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     c->d_mb_cur = c->d_mb_stats;
     TRY(dalloc(c, &c->d_rows, (size_t)cfg->num_epochs * cfg->num_minibatches * (WM_COUNT + 4)));
     BPPO_HIP(c, hipHostMalloc((void **)&c->h_red, sizeof(double) * (4 * 1024 + 64), hipHostMallocDefault));
+    BPPO_HIP(c, hipEventCreateWithFlags(&c->ev_block, hipEventDisableTiming | hipEventBlockingSync));
     for (int i = 0; i < 8; i++) {
         BPPO_HIP(c, hipEventCreate(&c->ev[i][0]));
         BPPO_HIP(c, hipEventCreate(&c->ev[i][1]));
@@ -174,7 +183,7 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     } else {
         TRY(launch_cartpole_reset(c));
     }
-    BPPO_HIP(c, hipStreamSynchronize(c->stream));
+    BPPO_HIP(c, sync_stream(c));
     return BPPO_OK;
 }
 
@@ -201,6 +210,7 @@ extern "C" void bppo_destroy(bppo_ctx *c) {
     for (void *p : ptrs) if (p) (void)hipFree(p);
     fy_ranges_free(c->fyr);
     if (c->h_red) (void)hipHostFree(c->h_red);
+    if (c->ev_block) (void)hipEventDestroy(c->ev_block);
     for (int i = 0; i < 8; i++) {
         if (c->ev[i][0]) (void)hipEventDestroy(c->ev[i][0]);
         if (c->ev[i][1]) (void)hipEventDestroy(c->ev[i][1]);
@@ -215,14 +225,14 @@ extern "C" bppo_status bppo_params_set(bppo_ctx *c, const float *h, size_t n) {
     if (!c || !h || n != c->net.n_params) { if (c) c->err = "params_set: size mismatch"; return BPPO_ERR_ARG; }
     BPPO_HIP(c, hipMemcpyAsync(c->d_params, h, n * 4, hipMemcpyHostToDevice, c->stream));
     if (c->wide) TRY(wide_pack(c));
-    BPPO_HIP(c, hipStreamSynchronize(c->stream));
+    BPPO_HIP(c, sync_stream(c));
     return BPPO_OK;
 }
 
 extern "C" bppo_status bppo_params_get(bppo_ctx *c, float *h, size_t n) {
     if (!c || !h || n != c->net.n_params) { if (c) c->err = "params_get: size mismatch"; return BPPO_ERR_ARG; }
     BPPO_HIP(c, hipMemcpyAsync(h, c->d_params, n * 4, hipMemcpyDeviceToHost, c->stream));
-    BPPO_HIP(c, hipStreamSynchronize(c->stream));
+    BPPO_HIP(c, sync_stream(c));
     return BPPO_OK;
 }
 
@@ -239,7 +249,7 @@ extern "C" bppo_status bppo_forward(bppo_ctx *c, const float *obs, const float *
     if (s == BPPO_OK) {
         if (logits) BPPO_HIP(c, hipMemcpyAsync(logits, d_l, sizeof(float) * (size_t)B * c->A, hipMemcpyDeviceToHost, c->stream));
         if (values) BPPO_HIP(c, hipMemcpyAsync(values, d_v, sizeof(float) * (size_t)B, hipMemcpyDeviceToHost, c->stream));
-        BPPO_HIP(c, hipStreamSynchronize(c->stream));
+        BPPO_HIP(c, sync_stream(c));
     }
     (void)hipFree(d_o); (void)hipFree(d_l); (void)hipFree(d_v);
     return s;
@@ -260,7 +270,7 @@ extern "C" bppo_status bppo_rng_set(bppo_ctx *c, uint64_t p) {
 extern "C" bppo_status bppo_vecenv_reset(bppo_ctx *c) {
     if (!c) return BPPO_ERR_ARG;
     TRY(c->wide ? wide_reset(c) : launch_cartpole_reset(c));
-    BPPO_HIP(c, hipStreamSynchronize(c->stream));
+    BPPO_HIP(c, sync_stream(c));
     return BPPO_OK;
 }
 
@@ -274,7 +284,7 @@ extern "C" bppo_status bppo_vecenv_observe(bppo_ctx *c, float *obs, int32_t *pla
         BPPO_HIP(c, hipMalloc((void **)&d, sizeof(float) * (size_t)c->N * c->D));
         TRY(launch_cartpole_observe(c, d));
         BPPO_HIP(c, hipMemcpyAsync(obs, d, sizeof(float) * (size_t)c->N * c->D, hipMemcpyDeviceToHost, c->stream));
-        BPPO_HIP(c, hipStreamSynchronize(c->stream));
+        BPPO_HIP(c, sync_stream(c));
         (void)hipFree(d);
     }
     if (players) std::fill(players, players + c->N, 0);
@@ -317,7 +327,7 @@ extern "C" bppo_status bppo_vecenv_step(bppo_ctx *c, const int32_t *actions, flo
     if (obs) BPPO_HIP(c, hipMemcpyAsync(obs, d_o, sizeof(float) * (size_t)N * c->D, hipMemcpyDeviceToHost, c->stream));
     int32_t cnt = 0;
     BPPO_HIP(c, hipMemcpyAsync(&cnt, c->d_ep_count, 4, hipMemcpyDeviceToHost, c->stream));
-    BPPO_HIP(c, hipStreamSynchronize(c->stream));
+    BPPO_HIP(c, sync_stream(c));
     if (n_eps) *n_eps = cnt;
     if (eps && cap > 0 && cnt > 0) {
         std::vector<EpisodeRec> recs(std::min(cnt, c->eps_cap));
@@ -345,7 +355,7 @@ extern "C" bppo_status bppo_obs_norm_get(bppo_ctx *c, double *mean, double *m2, 
     if (!c) return BPPO_ERR_ARG;
     std::vector<double> h(2 * c->D + 1);
     BPPO_HIP(c, hipMemcpyAsync(h.data(), c->d_on, sizeof(double) * h.size(), hipMemcpyDeviceToHost, c->stream));
-    BPPO_HIP(c, hipStreamSynchronize(c->stream));
+    BPPO_HIP(c, sync_stream(c));
     if (mean) std::memcpy(mean, h.data(), sizeof(double) * c->D);
     if (m2) std::memcpy(m2, h.data() + c->D, sizeof(double) * c->D);
     if (count) *count = h[2 * c->D];
@@ -359,7 +369,7 @@ extern "C" bppo_status bppo_obs_norm_set(bppo_ctx *c, const double *mean, const 
     std::memcpy(h.data() + c->D, m2, sizeof(double) * c->D);
     h[2 * c->D] = count;
     BPPO_HIP(c, hipMemcpyAsync(c->d_on, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice, c->stream));
-    BPPO_HIP(c, hipStreamSynchronize(c->stream));
+    BPPO_HIP(c, sync_stream(c));
     return BPPO_OK;
 }
 
@@ -367,7 +377,7 @@ extern "C" bppo_status bppo_ret_norm_get(bppo_ctx *c, double *mvc, double *retur
     if (!c) return BPPO_ERR_ARG;
     if (mvc) BPPO_HIP(c, hipMemcpyAsync(mvc, c->d_rn_stats, sizeof(double) * 3, hipMemcpyDeviceToHost, c->stream));
     if (returns) BPPO_HIP(c, hipMemcpyAsync(returns, c->d_rn_returns, sizeof(double) * (size_t)c->N * c->P, hipMemcpyDeviceToHost, c->stream));
-    BPPO_HIP(c, hipStreamSynchronize(c->stream));
+    BPPO_HIP(c, sync_stream(c));
     return BPPO_OK;
 }
 
@@ -375,7 +385,7 @@ extern "C" bppo_status bppo_ret_norm_set(bppo_ctx *c, const double *mvc, const d
     if (!c) return BPPO_ERR_ARG;
     if (mvc) BPPO_HIP(c, hipMemcpyAsync(c->d_rn_stats, mvc, sizeof(double) * 3, hipMemcpyHostToDevice, c->stream));
     if (returns) BPPO_HIP(c, hipMemcpyAsync(c->d_rn_returns, returns, sizeof(double) * (size_t)c->N * c->P, hipMemcpyHostToDevice, c->stream));
-    BPPO_HIP(c, hipStreamSynchronize(c->stream));
+    BPPO_HIP(c, sync_stream(c));
     return BPPO_OK;
 }
 
@@ -408,7 +418,7 @@ extern "C" bppo_status bppo_collect_rollouts(bppo_ctx *c, bppo_rollout_info *inf
     int32_t hv[2] = {0, 0};
     BPPO_HIP(c, hipMemcpyAsync(&hv[0], c->d_ep_count, 4, hipMemcpyDeviceToHost, c->stream));
     BPPO_HIP(c, hipMemcpyAsync(&hv[1], c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
-    BPPO_HIP(c, hipStreamSynchronize(c->stream));
+    BPPO_HIP(c, sync_stream(c));
     tm_read(c, TM_ROLLOUT); tm_read(c, TM_RETNORM);
     c->collected = 1; c->gae_done = 0;
     c->global_step += TN;
@@ -456,7 +466,7 @@ extern "C" bppo_status bppo_compute_gae(bppo_ctx *c) {
         tm_begin(c, TM_GAE);
         TRY(wide_bootstrap_gae(c));
         tm_end(c, TM_GAE);
-        BPPO_HIP(c, hipStreamSynchronize(c->stream));
+        BPPO_HIP(c, sync_stream(c));
         tm_read(c, TM_GAE);
         c->gae_done = 1;
         return BPPO_OK;
@@ -470,7 +480,7 @@ extern "C" bppo_status bppo_compute_gae(bppo_ctx *c) {
                                   c->stream);
     tm_end(c, TM_GAE);
     if (s != BPPO_OK) { c->err = "gae launch failed"; return s; }
-    BPPO_HIP(c, hipStreamSynchronize(c->stream));
+    BPPO_HIP(c, sync_stream(c));
     tm_read(c, TM_BOOT); tm_read(c, TM_GAE);
     c->gae_done = 1;
     return BPPO_OK;
@@ -523,7 +533,7 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
             }
             (void)hipEventRecord(c->ev[TM_FWDBWD][1], c->stream);
             if (c->allreduce && c->world > 1) {
-                BPPO_HIP(c, hipStreamSynchronize(c->stream));
+                BPPO_HIP(c, sync_stream(c));
                 if (c->allreduce(c->d_grad, (size_t)np + NM, c->allreduce_user) != 0) {
                     c->err = "all-reduce callback failed";
                     return BPPO_ERR_COMM;
@@ -544,7 +554,7 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
                 std::vector<float> row(NM + 4);
                 BPPO_HIP(c, hipMemcpyAsync(row.data(), c->d_rows + (size_t)(nrow - 1) * (NM + 4), sizeof(float) * (NM + 4),
                                            hipMemcpyDeviceToHost, c->stream));
-                BPPO_HIP(c, hipStreamSynchronize(c->stream));
+                BPPO_HIP(c, sync_stream(c));
                 float ms = 0;
                 if (hipEventElapsedTime(&ms, c->ev[TM_FWDBWD][0], c->ev[TM_FWDBWD][1]) == hipSuccess) fw_ms = ms;
                 if (mb == 0 && hipEventElapsedTime(&ms, s0, s1) == hipSuccess) sh_ms = ms;
@@ -561,7 +571,7 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
     if (deferred && nrow > 0) {
         rows.resize((size_t)nrow * (NM + 4));
         BPPO_HIP(c, hipMemcpyAsync(rows.data(), c->d_rows, sizeof(float) * rows.size(), hipMemcpyDeviceToHost, c->stream));
-        BPPO_HIP(c, hipStreamSynchronize(c->stream));
+        BPPO_HIP(c, sync_stream(c));
         float ms = 0;
         if (hipEventElapsedTime(&ms, c->ev[TM_FWDBWD][0], c->ev[TM_FWDBWD][1]) == hipSuccess) fw_ms = ms;
         if (hipEventElapsedTime(&ms, c->ev[TM_SHUFFLE][0], c->ev[TM_SHUFFLE][1]) == hipSuccess) sh_ms = ms;
@@ -661,7 +671,7 @@ extern "C" bppo_status bppo_buffer_get(bppo_ctx *c, const char *name, void *host
     BufDesc b = find_buf(c, name);
     if (!b.ptr || bytes < b.bytes) { c->err = std::string("buffer_get: unknown buffer or too small: ") + name; return BPPO_ERR_ARG; }
     BPPO_HIP(c, hipMemcpyAsync(host, b.ptr, b.bytes, hipMemcpyDeviceToHost, c->stream));
-    BPPO_HIP(c, hipStreamSynchronize(c->stream));
+    BPPO_HIP(c, sync_stream(c));
     return BPPO_OK;
 }
 
@@ -670,7 +680,7 @@ extern "C" bppo_status bppo_buffer_set(bppo_ctx *c, const char *name, const void
     BufDesc b = find_buf(c, name);
     if (!b.ptr || bytes != b.bytes) { c->err = std::string("buffer_set: unknown buffer or size mismatch: ") + name; return BPPO_ERR_ARG; }
     BPPO_HIP(c, hipMemcpyAsync(b.ptr, host, b.bytes, hipMemcpyHostToDevice, c->stream));
-    BPPO_HIP(c, hipStreamSynchronize(c->stream));
+    BPPO_HIP(c, sync_stream(c));
     if (!strcmp(name, "advantages") || !strcmp(name, "returns")) c->gae_done = c->collected = 1;
     return BPPO_OK;
 }

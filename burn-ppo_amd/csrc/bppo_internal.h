@@ -60,6 +60,8 @@ struct SpecWalk {
     std::atomic<int64_t> progress{-1};            // last checkpoint index written
     std::atomic<int> done{1};
     std::atomic<bool> stop{false};
+    std::atomic<int> merged_to{-1};               // left neighbour it coalesced with (then stopped)
+    uint64_t merge_q = 0;                         // word position of that checkpoint (set before merged_to)
     uint64_t gen = 0;                             // assignment counter (the worker follows it)
     bool running = false;                         // guarded by the engine mutex
 };
@@ -96,6 +98,15 @@ struct ShuffleEngine {
     SpecWalk spec[SHUF_MAX_SPEC];
     int nspec = 0, ncur = 0;
     std::vector<std::thread> workers;
+    // host word producers: the job's ChaCha12 words into the pinned word buffer,
+    // chunk by chunk in the order the walks need them (no device -> host copies)
+    std::vector<std::thread> gens;
+    std::vector<std::pair<uint64_t, size_t>> gen_order;   // (word position, chunk) of the current job
+    WordBuf *gen_buf = nullptr;
+    std::atomic<size_t> gen_next{0};
+    uint64_t gen_job = 0;
+    int gen_active = 0;                           // producers inside a job's list (mu)
+    void generator();
     uint64_t seq = 0;                             // jobs started
     bool carry_valid[2] = {false, false};
     // job control: a job = one update's shuffles in a J slot.  The engine chains
@@ -141,6 +152,7 @@ struct ShuffleEngine {
     void stop_walks(int lo, int hi);                     // stop and wait (mu not held)
     const uint32_t *words(int b, uint64_t pos, uint64_t len, std::vector<uint32_t> &scratch);
     uint64_t walk_piece(int b, uint64_t pos, uint32_t *r, std::vector<uint32_t> &scratch);
+    int peek(int i, uint64_t q, uint32_t *r);     // walk i's range at checkpoint q: 1 known, 0 not yet, -1 never
 };
 uint64_t shuffle_walk_host(const Key8 &key, uint64_t stream, uint64_t pos, uint32_t n, uint32_t *J);
 
@@ -243,6 +255,7 @@ struct bppo_ctx {
     uint8_t *d_scr_d = nullptr;       // VecEnv::step dones [N]
     // timing
     hipEvent_t ev[8][2] = {};
+    hipEvent_t ev_block = nullptr;    // blocking-sync event for host waits on the stream
     float last_ms[8] = {0};
     double last_walk_ms = 0.0, last_wait_ms = 0.0;
     int last_met = 0;

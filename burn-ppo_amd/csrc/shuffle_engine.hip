@@ -2,8 +2,9 @@
 // (ppo.rs:1816 `indices.shuffle(rng)`, rand 0.8.5 SliceRandom::shuffle):
 //
 //   words      : the ChaCha12 words of the main StdRng stream for one update's
-//                shuffles, made by a GPU kernel and copied to pinned host
-//                memory in chunks (ordered by when the walkers reach them);
+//                shuffles: made on the host by producer threads into pinned
+//                memory in chunks, in the order the walkers reach them, and
+//                independently on the GPU (device copy for the J expansion);
 //   true walk  : the sequential rejection chain -> J[i] = gen_range(0..i+1),
 //                i = n-1..1 (shuffle_host.cpp), epoch by epoch;
 //   speculation: epoch e >= 1 starts where epoch e-1 ends, known only after
@@ -33,6 +34,9 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <sys/resource.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 #include "bppo_internal.h"
 #include "shuffle_host.h"
 
@@ -146,13 +150,13 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
             return BPPO_ERR_HIP;
         }
         for (int e = 0; e < epochs; e++)
-            if (hipEventCreateWithFlags(&ev[s][e], hipEventDisableTiming) != hipSuccess) {
+            if (hipEventCreateWithFlags(&ev[s][e], hipEventDisableTiming | hipEventBlockingSync) != hipSuccess) {
                 err = "shuffle events: creation failed";
                 return BPPO_ERR_HIP;
             }
     }
     for (int s = 0; s < 2; s++)
-        if (hipEventCreateWithFlags(&consumed[s], hipEventDisableTiming) != hipSuccess) {
+        if (hipEventCreateWithFlags(&consumed[s], hipEventDisableTiming | hipEventBlockingSync) != hipSuccess) {
             err = "shuffle events: creation failed";
             return BPPO_ERR_HIP;
         }
@@ -178,7 +182,7 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
         w.ok.reset(new std::atomic<int>[nch]);
         for (size_t c = 0; c < nch; c++) {
             w.ok[c] = 0;
-            if (hipEventCreateWithFlags(&w.ev[c], hipEventDisableTiming) != hipSuccess) {
+            if (hipEventCreateWithFlags(&w.ev[c], hipEventDisableTiming | hipEventBlockingSync) != hipSuccess) {
                 err = "shuffle chunk events: creation failed";
                 return BPPO_ERR_HIP;
             }
@@ -187,6 +191,9 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
     const uint64_t nck = (uint64_t)((Ew + 24.0 * sigma) / SHUF_CK) + 4;
     for (int i = 0; i < nspec; i++) spec[i].ck.assign(nck, 0xFFFFFFFFu);
     for (int i = 0; i < nspec; i++) workers.emplace_back([this, i]() { worker(i); });
+    int ngen = 4;
+    if (const char *e = getenv("BPPO_SHUFFLE_GEN")) ngen = std::max(1, atoi(e));
+    for (int i = 0; i < ngen; i++) gens.emplace_back([this]() { generator(); });
     th = std::thread([this]() { run(); });
     return BPPO_OK;
 }
@@ -242,11 +249,11 @@ const uint32_t *ShuffleEngine::words(int b, uint64_t pos, uint64_t len, std::vec
         if (pos >= R.base && pos + len <= R.base + R.len) {
             const uint64_t o = R.off + (pos - R.base);
             const size_t c = (size_t)(o / SHUF_CHUNK);
-            if (!w.ok[c].load(std::memory_order_acquire)) {
-                (void)hipEventSynchronize(w.ev[c]);
-                w.ok[c].store(1, std::memory_order_release);
-            }
-            return w.h + o;
+            // (on shutdown the producers are gone: make the piece here instead)
+            while (!w.ok[c].load(std::memory_order_acquire) && !quit && !cancel.load(std::memory_order_relaxed))
+                std::this_thread::sleep_for(std::chrono::microseconds(10));
+            if (w.ok[c].load(std::memory_order_acquire)) return w.h + o;
+            break;
         }
     }
     scratch.resize(len);
@@ -270,6 +277,8 @@ void ShuffleEngine::launch_walk(int i, uint64_t start, int wbuf) {
     std::fill(s.ck.begin(), s.ck.end(), 0xFFFFFFFFu);
     s.progress.store(-1, std::memory_order_relaxed);
     s.stop.store(false, std::memory_order_relaxed);
+    s.merged_to.store(-1, std::memory_order_relaxed);
+    s.merge_q = 0;
     s.done.store(0, std::memory_order_release);
     s.running = true;
     s.gen++;
@@ -286,8 +295,34 @@ void ShuffleEngine::stop_walks(int lo, int hi) {
     });
 }
 
+// Walks of one boundary start at increasing guesses and never cross (a walk
+// started earlier has the smaller or equal range at every position), so once two
+// neighbours hold the same range at a checkpoint they are one walk: the right one
+// stops and records which walk carries on from there.  peek() follows those links.
+int ShuffleEngine::peek(int i, uint64_t q, uint32_t *r) {
+    for (;;) {
+        SpecWalk &t = spec[i];
+        if (q <= t.start) return -1;
+        const int mt = t.merged_to.load(std::memory_order_acquire);
+        if (mt >= 0 && q >= t.merge_q) { i = mt; continue; }
+        const int64_t c = (int64_t)((q - t.ck_base) / SHUF_CK);
+        if (c >= (int64_t)t.ck.size()) return -1;
+        if (t.progress.load(std::memory_order_acquire) >= c) { *r = t.ck[c]; return 1; }
+        if (t.done.load(std::memory_order_acquire) && t.merged_to.load(std::memory_order_acquire) < 0) return -1;
+        return 0;
+    }
+}
+
 void ShuffleEngine::worker(int i) {
     (void)hipSetDevice(dev);
+    // CPU priority by when a walk is needed: epoch 1's walks first, then epoch
+    // 2's, ..., the next job's carry set last (16 CPUs run ~K (E + 1) walks; the
+    // scheduler otherwise shares them evenly and delays the walk needed first)
+    {
+        static const int nice_step = getenv("BPPO_SHUFFLE_NICE") ? atoi(getenv("BPPO_SHUFFLE_NICE")) : 3;
+        const int g = i < ncur ? i / std::max(K, 1) : std::max(epochs - 1, 0);
+        if (nice_step > 0 && g > 0) (void)setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), std::min(19, nice_step * g));
+    }
     std::vector<uint32_t> scratch;
     uint64_t seen = 0;
     SpecWalk &s = spec[i];
@@ -309,6 +344,12 @@ void ShuffleEngine::worker(int i) {
                     s.ck[c] = r;
                     s.progress.store(c, std::memory_order_release);
                 }
+                uint32_t rl;
+                if (i % K != 0 && peek(i - 1, q, &rl) == 1 && rl == r) {   // coalesced with the left neighbour
+                    s.merge_q = q;
+                    s.merged_to.store(i - 1, std::memory_order_release);
+                    break;
+                }
             }
         }
         s.end = pos;
@@ -316,6 +357,33 @@ void ShuffleEngine::worker(int i) {
             std::lock_guard<std::mutex> lk(mu);
             s.done.store(1, std::memory_order_release);
             s.running = false;
+        }
+        cv.notify_all();
+    }
+}
+
+void ShuffleEngine::generator() {
+    uint64_t seen = 0;
+    for (;;) {
+        WordBuf *W;
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return quit || gen_job != seen; });
+            if (quit) return;
+            seen = gen_job;
+            W = gen_buf;
+            gen_active++;
+        }
+        for (;;) {
+            const size_t k = gen_next.fetch_add(1, std::memory_order_relaxed);
+            if (k >= gen_order.size()) break;
+            const auto pc = gen_order[k];
+            bppo_host::chacha12_words(key.k, stream, pc.first, W->h + pc.second * SHUF_CHUNK, SHUF_CHUNK);
+            W->ok[pc.second].store(1, std::memory_order_release);
+        }
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            gen_active--;
         }
         cv.notify_all();
     }
@@ -395,11 +463,24 @@ void ShuffleEngine::run() {
             }
         }
         std::sort(order.begin(), order.end());
-        for (auto &oc : order) {
-            const size_t c = oc.second;
-            (void)hipMemcpyAsync(W.h + c * SHUF_CHUNK, W.d + c * SHUF_CHUNK, SHUF_CHUNK * 4, hipMemcpyDeviceToHost, copy);
-            (void)hipEventRecord(W.ev[c], copy);
+        {
+            // the host copy of the words: made by the producer threads in need order
+            // (the previous job's list is finished: producers run far ahead of walks)
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return gen_active == 0 || quit; });
+            gen_order.clear();
+            for (auto &oc : order) {
+                const size_t c = oc.second;
+                const WordBuf::Region *R = nullptr;
+                for (int g = 0; g < W.nreg; g++)
+                    if (c * SHUF_CHUNK >= W.reg[g].off && c * SHUF_CHUNK < W.reg[g].off + W.reg[g].len) R = &W.reg[g];
+                if (R) gen_order.push_back({R->base + (c * SHUF_CHUNK - R->off), c});
+            }
+            gen_buf = &W;
+            gen_next.store(0, std::memory_order_relaxed);
+            gen_job++;
         }
+        cv.notify_all();
         // ---- speculative walks: epochs 1 .. E-1 of this job, and the next job's first epoch
         {
             std::lock_guard<std::mutex> lk(mu);
@@ -437,15 +518,13 @@ void ShuffleEngine::run() {
                 if (s0 == s1) continue;
                 walked++;
                 for (int i = s0; i < s1 && met < 0; i++) {
-                    SpecWalk &sp = spec[i];
-                    if (q <= sp.start) continue;
-                    const int64_t c = (int64_t)((q - sp.ck_base) / SHUF_CK);
-                    if (c >= (int64_t)sp.ck.size()) continue;
-                    // wait until that walk has passed q (or stopped before it)
-                    while (sp.progress.load(std::memory_order_acquire) < c && !sp.done.load(std::memory_order_acquire) &&
-                           !cancel.load(std::memory_order_relaxed))
-                        std::this_thread::yield();
-                    if (sp.progress.load(std::memory_order_acquire) >= c && sp.ck[c] == r) met = i;
+                    // wait until that walk (or the one it coalesced with) has passed q
+                    uint32_t rs = 0;
+                    int st;
+                    // (sleep, not spin: the process runs under a CPU quota that spinning eats)
+                    while ((st = peek(i, q, &rs)) == 0 && !cancel.load(std::memory_order_relaxed))
+                        std::this_thread::sleep_for(std::chrono::microseconds(20));
+                    if (st == 1 && rs == r) met = i;
                 }
                 if (met >= 0) break;
             }
@@ -462,20 +541,32 @@ void ShuffleEngine::run() {
             if (met >= 0) {
                 // the other walks of this boundary cannot serve any more: free their CPUs
                 // for the met one (it still has to finish the epoch) and the later epochs
-                for (int i = s0; i < s1; i++)
-                    if (i != met) spec[i].stop.store(true, std::memory_order_relaxed);
-                SpecWalk &sp = spec[met];
-                while (!sp.done.load(std::memory_order_acquire) && !cancel.load(std::memory_order_relaxed))
-                    std::this_thread::yield();
-                if (cancel.load(std::memory_order_relaxed)) { cancelled = true; break; }
-                // from the meeting checkpoint on, the speculative walk's states
-                const int64_t last = sp.progress.load(std::memory_order_acquire);
-                for (int64_t c = (int64_t)((tck.back().first - sp.ck_base) / SHUF_CK); c <= last; c++) {
-                    const uint64_t q0 = sp.ck_base + (uint64_t)c * SHUF_CK;
-                    if (q0 >= sp.end) break;
-                    add(q0, std::min(q0 + SHUF_CK, sp.end), sp.ck[c]);
+                // (walks only coalesce leftwards, so the ones right of the met walk
+                // can never carry its states)
+                for (int i = met + 1; i < s1; i++) spec[i].stop.store(true, std::memory_order_relaxed);
+                // the walk that finishes the epoch: follow the links until one ends on its own
+                int fin = met;
+                for (;;) {
+                    SpecWalk &sp = spec[fin];
+                    {
+                        std::unique_lock<std::mutex> lk(mu);
+                        cv.wait(lk, [&] {
+                            return sp.done.load(std::memory_order_acquire) || cancel.load(std::memory_order_relaxed) || quit;
+                        });
+                    }
+                    const int mt = sp.merged_to.load(std::memory_order_acquire);
+                    if (mt < 0 || cancel.load(std::memory_order_relaxed)) break;
+                    fin = mt;
                 }
-                pos = sp.end;
+                if (cancel.load(std::memory_order_relaxed)) { cancelled = true; break; }
+                // from the meeting checkpoint on, the speculative walks' states
+                const uint64_t endp = spec[fin].end;
+                for (uint64_t q0 = tck.back().first; q0 < endp; q0 += SHUF_CK) {
+                    uint32_t r0 = 0;
+                    if (peek(met, q0, &r0) != 1) { overflow = true; break; }   // cannot happen: all walks done
+                    add(q0, std::min(q0 + SHUF_CK, endp), r0);
+                }
+                pos = endp;
                 coalesced[slot][e] = walked;
             } else {
                 add(tck.back().first, pos, tck.back().second);
@@ -549,6 +640,8 @@ void ShuffleEngine::shutdown() {
         th.join();
         for (auto &w : workers) w.join();
         workers.clear();
+        for (auto &g : gens) g.join();
+        gens.clear();
     }
     if (copy) { (void)hipStreamSynchronize(copy); (void)hipStreamDestroy(copy); copy = nullptr; }
     for (int s = 0; s < 2; s++) {
