@@ -186,12 +186,27 @@ __device__ Welford block_exclusive_scan(Welford mine, Welford *sh) {
     return excl;
 }
 
+// the block's RN_SEG returns staged through LDS with coalesced loads; thread t
+// then walks its RN_IPT consecutive values (one pad double per RN_IPT keeps the
+// per-thread rows on distinct banks)
+constexpr int RN_PAD = RN_IPT + 1;
+__device__ __forceinline__ void rn_stage(size_t n, const double *X, double *xs) {
+    const size_t base = (size_t)blockIdx.x * RN_SEG;
+    for (int k = threadIdx.x; k < RN_SEG; k += RN_BLOCK) {
+        const size_t i = base + k;
+        xs[(k / RN_IPT) * RN_PAD + (k % RN_IPT)] = i < n ? X[i] : 0.0;
+    }
+    __syncthreads();
+}
+
 __global__ void __launch_bounds__(RN_BLOCK) k_rn_block_agg(size_t n, const double *X, Welford *agg) {
     __shared__ Welford sh[RN_BLOCK];
+    __shared__ double xs[RN_BLOCK * RN_PAD];
+    rn_stage(n, X, xs);
     const size_t base = (size_t)blockIdx.x * RN_SEG + (size_t)threadIdx.x * RN_IPT;
     Welford s{0, 0, 0};
     for (int k = 0; k < RN_IPT; k++)
-        if (base + k < n) wpush(s, X[base + k]);
+        if (base + k < n) wpush(s, xs[threadIdx.x * RN_PAD + k]);
     Welford ex = block_exclusive_scan(s, sh);
     if (threadIdx.x == blockDim.x - 1) agg[blockIdx.x] = wmerge(ex, s);
 }
@@ -221,16 +236,19 @@ __global__ void __launch_bounds__(RN_BLOCK) k_rn_apply(size_t n, const double *X
                                                        const float *rew_raw, const Welford *agg,
                                                        float clip, float *rew) {
     __shared__ Welford sh[RN_BLOCK];
+    __shared__ double xs[RN_BLOCK * RN_PAD];
+    __shared__ float rs[RN_BLOCK * RN_PAD];
+    rn_stage(n, X, xs);
     const size_t base = (size_t)blockIdx.x * RN_SEG + (size_t)threadIdx.x * RN_IPT;
     Welford s{0, 0, 0};
     for (int k = 0; k < RN_IPT; k++)
-        if (base + k < n) wpush(s, X[base + k]);
+        if (base + k < n) wpush(s, xs[threadIdx.x * RN_PAD + k]);
     Welford ex = block_exclusive_scan(s, sh);
     Welford run = wmerge(agg[blockIdx.x], ex);
     for (int k = 0; k < RN_IPT; k++) {
         const size_t i = base + k;
         if (i >= n) break;
-        wpush(run, X[i]);
+        wpush(run, xs[threadIdx.x * RN_PAD + k]);
         float r = rew_raw[i];
         if (run.n >= 2.0) {                                  // normalization.rs:187-197
             const double sd = sqrt(run.m2 / run.n + 1e-8);
@@ -239,8 +257,12 @@ __global__ void __launch_bounds__(RN_BLOCK) k_rn_apply(size_t n, const double *X
             z = z > clip ? clip : z;
             r = z;
         }
-        rew[i] = r;
+        rs[threadIdx.x * RN_PAD + k] = r;
     }
+    __syncthreads();
+    const size_t b0 = (size_t)blockIdx.x * RN_SEG;
+    for (int k = threadIdx.x; k < RN_SEG; k += RN_BLOCK)
+        if (b0 + k < n) rew[b0 + k] = rs[(k / RN_IPT) * RN_PAD + (k % RN_IPT)];
 }
 
 bppo_status launch_return_norm(bppo_ctx *c) {

@@ -434,47 +434,70 @@ __global__ void __launch_bounds__(256) k_cartpole_forward_rows(int B, const floa
 
 // Merge per-env Welford partials (count T each) into the running stats
 // (normalization.rs:37-53 is a sequential Welford over T*N rows; Chan merges
-// give the same statistics to f64 rounding).  One block, fixed merge order.
-__global__ void __launch_bounds__(1024) k_obs_norm_merge(int N, int D, double T,
-                                                         const double *part, double *on) {
-    __shared__ double sm[1024][2];
-    __shared__ double sn[1024];
-    for (int d = 0; d < D; d++) {
-        double n = 0, mean = 0, m2 = 0;
-        for (int e = threadIdx.x; e < N; e += blockDim.x) {
-            double mb = part[(size_t)e * 2 * D + d], m2b = part[(size_t)e * 2 * D + D + d];
-            double nn = n + T, delta = mb - mean;
-            mean += delta * (T / nn);
-            m2 += m2b + delta * delta * (n * T / nn);
-            n = nn;
+// give the same statistics to f64 rounding).  Two passes with a fixed merge
+// order: OBS_PART_BLOCKS blocks each merge a contiguous range of envs (thread-
+// sequential, then a block tree), then one thread per dim merges the block
+// results in block order into the running stats.
+constexpr int OBS_PART_BLOCKS = 64, OBS_MAX_D = 8;
+__global__ void __launch_bounds__(256) k_obs_norm_part(int N, int D, double T, const double *part, double *bp) {
+    __shared__ double sn[256], sm[256][OBS_MAX_D], sq[256][OBS_MAX_D];
+    const int per = (N + gridDim.x - 1) / gridDim.x;
+    const int e0 = blockIdx.x * per, e1 = min(N, e0 + per);
+    double n = 0.0, mean[OBS_MAX_D], m2[OBS_MAX_D];
+    for (int d = 0; d < OBS_MAX_D; d++) mean[d] = m2[d] = 0.0;
+    for (int e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
+        const double *pe = part + (size_t)e * 2 * D;
+        const double nn = n + T, f = T / nn, g = n * T / nn;
+        for (int d = 0; d < D; d++) {
+            const double delta = pe[d] - mean[d];
+            mean[d] += delta * f;
+            m2[d] += pe[D + d] + delta * delta * g;
         }
-        sn[threadIdx.x] = n; sm[threadIdx.x][0] = mean; sm[threadIdx.x][1] = m2;
-        __syncthreads();
-        for (int st = blockDim.x / 2; st > 0; st >>= 1) {
-            if (threadIdx.x < st) {
-                double na = sn[threadIdx.x], nb = sn[threadIdx.x + st];
-                double nn = na + nb;
-                if (nb > 0) {
-                    double delta = sm[threadIdx.x + st][0] - sm[threadIdx.x][0];
-                    double f = na > 0 ? nb / nn : 1.0;
-                    sm[threadIdx.x][0] += delta * f;
-                    sm[threadIdx.x][1] += sm[threadIdx.x + st][1] + delta * delta * (na * nb / nn);
-                    sn[threadIdx.x] = nn;
+        n = nn;
+    }
+    sn[threadIdx.x] = n;
+    for (int d = 0; d < D; d++) { sm[threadIdx.x][d] = mean[d]; sq[threadIdx.x][d] = m2[d]; }
+    __syncthreads();
+    for (int st = blockDim.x / 2; st > 0; st >>= 1) {
+        if (threadIdx.x < st) {
+            const double na = sn[threadIdx.x], nb = sn[threadIdx.x + st], nn = na + nb;
+            if (nb > 0) {
+                const double f = na > 0 ? nb / nn : 1.0, g = na * nb / nn;
+                for (int d = 0; d < D; d++) {
+                    const double delta = sm[threadIdx.x + st][d] - sm[threadIdx.x][d];
+                    sm[threadIdx.x][d] += delta * f;
+                    sq[threadIdx.x][d] += sq[threadIdx.x + st][d] + delta * delta * g;
                 }
+                sn[threadIdx.x] = nn;
             }
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) {
-            // old stats (count on[2D]) merged with the batch
-            double na = on[2 * D], nb = sn[0], nn = na + nb;
-            double ma = on[d], mb = sm[0][0];
-            double delta = mb - ma;
-            on[d] = na > 0 ? ma + delta * (nb / nn) : mb;
-            on[D + d] = on[D + d] + sm[0][1] + (na > 0 ? delta * delta * (na * nb / nn) : 0.0);
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0) on[2 * D] += (double)N * T;
+    if (threadIdx.x < D) {
+        double *o = bp + ((size_t)blockIdx.x * OBS_MAX_D + threadIdx.x) * 3;
+        o[0] = sn[0]; o[1] = sm[0][threadIdx.x]; o[2] = sq[0][threadIdx.x];
+    }
+}
+__global__ void k_obs_norm_final(int D, int nblk, const double *bp, double *on) {
+    const int d = threadIdx.x;
+    if (d >= D) return;
+    double n = 0.0, mean = 0.0, m2 = 0.0;
+    for (int b = 0; b < nblk; b++) {
+        const double *o = bp + ((size_t)b * OBS_MAX_D + d) * 3;
+        const double nb = o[0];
+        if (nb <= 0) continue;
+        const double nn = n + nb, delta = o[1] - mean;
+        mean = n > 0 ? mean + delta * (nb / nn) : o[1];
+        m2 += o[2] + (n > 0 ? delta * delta * (n * nb / nn) : 0.0);
+        n = nn;
+    }
+    // old stats (count on[2D]) merged with the batch
+    const double na = on[2 * D], nn = na + n, delta = mean - on[d];
+    const double ma = on[d];
+    on[d] = na > 0 ? ma + delta * (n / nn) : mean;
+    on[D + d] = on[D + d] + m2 + (na > 0 ? delta * delta * (na * n / nn) : 0.0);
+    __syncthreads();
+    if (d == 0) on[2 * D] = nn;
 }
 
 // ------------------------------------------------------------- launchers ---
@@ -577,8 +600,11 @@ bppo_status launch_cartpole_observe(bppo_ctx *c, float *d_obs_out) {
 }
 
 bppo_status launch_obs_norm_merge(bppo_ctx *c) {
-    hipLaunchKernelGGL(k_obs_norm_merge, dim3(1), dim3(1024), 0, c->stream, c->N, c->D,
-                       (double)c->T, c->d_obs_part, c->d_on);
+    if (c->D > OBS_MAX_D) { c->err = "observation normalizer: obs dim > 8"; return BPPO_ERR_UNSUPPORTED; }
+    const int nblk = std::min(OBS_PART_BLOCKS, std::max(1, (c->N + 255) / 256));
+    hipLaunchKernelGGL(k_obs_norm_part, dim3(nblk), dim3(256), 0, c->stream, c->N, c->D, (double)c->T,
+                       c->d_obs_part, c->d_red);
+    hipLaunchKernelGGL(k_obs_norm_final, dim3(1), dim3(64), 0, c->stream, c->D, nblk, c->d_red, c->d_on);
     BPPO_HIP(c, hipGetLastError());
     return BPPO_OK;
 }
