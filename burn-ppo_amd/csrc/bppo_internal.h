@@ -49,7 +49,7 @@ struct Welford { double n, mean, m2; };
 // epoch e runs from the real boundary only until its state (word position,
 // remaining range) meets one of them, after which both are the same walk.
 constexpr int SHUF_MAX_EPOCHS = 32;
-constexpr int SHUF_MAX_SPEC = 40;
+constexpr int SHUF_MAX_SPEC = 64;
 constexpr uint64_t SHUF_CK = 1024;               // checkpoint spacing (words) = GPU J segment length
 constexpr uint64_t SHUF_CHUNK = (uint64_t)1 << 20; // words per GPU->host copy
 
@@ -93,10 +93,12 @@ struct ShuffleEngine {
     double Ew = 0.0, sigma = 0.0;                 // expected words per shuffle, its std dev
     int K = 0;                                    // speculative walks per epoch boundary
     WordBuf wb[2];                                // double-buffered by job parity
-    // walker slots: [0, ncur) K per epoch 1..E-1 of the current job; then two
+    // walker slots: [0, ncur) K per epoch C..E-1 of the current job; then two
+    // (by job parity) carry groups of C*K for the next job's epochs 0..C-1
     // carry sets of K for the next job's first epoch (alternating by job parity)
     SpecWalk spec[SHUF_MAX_SPEC];
     int nspec = 0, ncur = 0;
+    int C = 1;                                    // leading epochs of the next job speculated during this one
     std::vector<std::thread> workers;
     // host word producers: the job's ChaCha12 words into the pinned word buffer,
     // chunk by chunk in the order the walks need them (no device -> host copies)

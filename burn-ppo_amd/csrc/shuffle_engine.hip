@@ -136,9 +136,13 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
     // (BPPO_SHUFFLE_SPEC overrides; 0 = sequential walk only)
     K = 6;
     if (const char *e = getenv("BPPO_SHUFFLE_SPEC")) K = std::max(0, atoi(e));
-    K = std::min(K, SHUF_MAX_SPEC / (std::max(epochs - 1, 0) + 2));
-    ncur = K * std::max(epochs - 1, 0);
-    nspec = ncur + 2 * K;
+    // C leading epochs of the next job are speculated during this job (their walks
+    // get a whole job of head start; later epochs' walks start with their job)
+    C = std::min(2, std::max(epochs, 1));
+    if (const char *e = getenv("BPPO_SHUFFLE_CARRY")) C = std::max(1, std::min(epochs, atoi(e)));
+    K = std::min(K, SHUF_MAX_SPEC / (std::max(epochs - C, 0) + 2 * C));
+    ncur = K * std::max(epochs - C, 0);
+    nspec = ncur + 2 * C * K;
     const size_t bytes = sizeof(uint32_t) * (size_t)n * epochs;
     maxseg = (int)((Ew + 48.0 * sigma) / SHUF_CK) + 16;
     const size_t sbytes = sizeof(Seg) * (size_t)maxseg * epochs;
@@ -168,7 +172,8 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
     auto chunks = [](double w) { return ((uint64_t)std::max(w, 1.0) + SHUF_CHUNK - 1) / SHUF_CHUNK * SHUF_CHUNK; };
     const double sE = sigma * std::sqrt((double)std::max(epochs, 1));
     const uint64_t cap0 = chunks(epochs * Ew + 12.0 * sE + 4.0 * SHUF_CK) + SHUF_CHUNK;
-    const uint64_t cap1 = K ? chunks(Ew + 6.0 * sE + 12.0 * sigma + 8.0 * SHUF_CK) + SHUF_CHUNK : 0;
+    const double sC = sigma * std::sqrt((double)(epochs + C));
+    const uint64_t cap1 = K ? chunks(C * Ew + 8.0 * sC + 12.0 * sigma + 8.0 * SHUF_CK) + SHUF_CHUNK : 0;
     for (int b = 0; b < 2; b++) {
         WordBuf &w = wb[b];
         w.cap = cap0 + cap1;
@@ -320,7 +325,7 @@ void ShuffleEngine::worker(int i) {
     // scheduler otherwise shares them evenly and delays the walk needed first)
     {
         static const int nice_step = getenv("BPPO_SHUFFLE_NICE") ? atoi(getenv("BPPO_SHUFFLE_NICE")) : 3;
-        const int g = i < ncur ? i / std::max(K, 1) : std::max(epochs - 1, 0);
+        const int g = i < ncur ? i / std::max(K, 1) : std::max(epochs - C, 0);
         if (nice_step > 0 && g > 0) (void)setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), std::min(19, nice_step * g));
     }
     std::vector<uint32_t> scratch;
@@ -422,8 +427,8 @@ void ShuffleEngine::run() {
         const int b = (int)(seq & 1);                 // word buffer and carry set of this job
         const int cs = 1 - b;                         // carry set the previous job launched for us
         const int cur0 = 0, cur1 = ncur;
-        const int cn0 = ncur + b * K, cn1 = cn0 + K;  // carry set launched now (next job)
-        const int cp0 = ncur + cs * K, cp1 = cp0 + K; // carry set for this job's epoch 0
+        const int cn0 = ncur + b * C * K, cn1 = cn0 + C * K;   // carry group launched now (next job)
+        const int cp0 = ncur + cs * C * K;                     // carry group for this job's epochs 0..C-1
         SHUF_LOG("[shuf] job %llu start=%llu slot=%d carry=%d\n", (unsigned long long)seq, (unsigned long long)start,
                  slot, (int)carry_valid[cs]);
         // walks of two jobs ago still on this buffer / carry slots have stopped
@@ -438,10 +443,11 @@ void ShuffleEngine::run() {
             W.reg[0].off = 0;
             W.reg[0].len = std::min(W.cap, chunks((double)(start - W.reg[0].base) + epochs * Ew + 10.0 * sE + 4.0 * SHUF_CK));
             if (K > 0) {
-                const double lo = (double)start + epochs * Ew + (double)gap - 3.0 * sE - 4.0 * SHUF_CK;
+                const double sC = sigma * std::sqrt((double)(epochs + C));
+                const double lo = (double)start + epochs * Ew + (double)gap - 4.0 * sC - 4.0 * SHUF_CK;
                 uint64_t b1 = (uint64_t)std::max(lo, 0.0) / SHUF_CK * SHUF_CK;
                 b1 = std::max(b1, W.reg[0].base + W.reg[0].len);
-                const uint64_t len1 = std::min(W.cap - W.reg[0].len, chunks(Ew + 6.0 * sE + 12.0 * sigma + 8.0 * SHUF_CK));
+                const uint64_t len1 = std::min(W.cap - W.reg[0].len, chunks(C * Ew + 8.0 * sC + 12.0 * sigma + 8.0 * SHUF_CK));
                 if (len1 > 0) {
                     W.reg[1].base = b1; W.reg[1].off = W.reg[0].len; W.reg[1].len = len1;
                     W.nreg = 2;
@@ -484,14 +490,18 @@ void ShuffleEngine::run() {
         // ---- speculative walks: epochs 1 .. E-1 of this job, and the next job's first epoch
         {
             std::lock_guard<std::mutex> lk(mu);
+            // K guesses evenly over centre +- spread*sd
+            static const double spread = getenv("BPPO_SHUFFLE_SPREAD") ? atof(getenv("BPPO_SHUFFLE_SPREAD")) : 2.0;
             auto guess = [&](double centre, double sd, int k) {
-                return (uint64_t)std::max((double)start, std::floor(centre + ((k + 0.5) / K - 0.5) * 3.0 * sd));
+                return (uint64_t)std::max((double)start, std::floor(centre + ((k + 0.5) / K - 0.5) * 2.0 * spread * sd));
             };
-            for (int e = 1; e < epochs; e++)
+            for (int e = C; e < epochs; e++)
                 for (int k = 0; k < K; k++)
-                    launch_walk(cur0 + (e - 1) * K + k, guess((double)start + e * Ew, sigma * std::sqrt((double)e), k), b);
-            for (int k = 0; k < K; k++)
-                launch_walk(cn0 + k, guess((double)start + epochs * Ew + (double)gap, sE, k), b);
+                    launch_walk(cur0 + (e - C) * K + k, guess((double)start + e * Ew, sigma * std::sqrt((double)e), k), b);
+            for (int c = 0; c < C; c++)
+                for (int k = 0; k < K; k++)
+                    launch_walk(cn0 + c * K + k, guess((double)start + (epochs + c) * Ew + (double)gap,
+                                                       sigma * std::sqrt((double)(epochs + c)), k), b);
             carry_valid[b] = K > 0;
         }
         cv.notify_all();
@@ -505,8 +515,8 @@ void ShuffleEngine::run() {
             uint32_t r = n;
             int met = -1, walked = 0;
             int s0 = 0, s1 = 0;                        // candidate speculative walks for this epoch
-            if (e == 0) { if (carry_valid[cs]) { s0 = cp0; s1 = cp1; } }
-            else { s0 = cur0 + (e - 1) * K; s1 = s0 + K; }
+            if (e < C) { if (carry_valid[cs]) { s0 = cp0 + e * K; s1 = s0 + K; } }
+            else { s0 = cur0 + (e - C) * K; s1 = s0 + K; }
             tck.clear();
             tck.push_back({pos, r});
             while (r >= 2) {
@@ -604,7 +614,7 @@ void ShuffleEngine::run() {
             }
             cv.notify_all();
             if (K > 0) stop_walks(s0, s1);        // this epoch's walks have served
-            if (e == 0) carry_valid[cs] = false;
+            if (e == C - 1) carry_valid[cs] = false;
         }
         SHUF_LOG("[shuf] job done cancelled=%d\n", (int)cancelled);
         // this job's in-update walks are done with; the carry set keeps running for

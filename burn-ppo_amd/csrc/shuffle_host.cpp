@@ -8,6 +8,7 @@
 #include "shuffle_host.h"
 
 #include <immintrin.h>
+#include <cstdlib>
 #include <string.h>
 
 namespace bppo_host {
@@ -245,17 +246,20 @@ static inline size_t walk_scalar_nj(const u32 *w, size_t nw, u32 *rp) {
     return p;
 }
 
-// 32 words per block, 16 hypotheses m = rejections so far (r_j = r - j + m).
+// 32 words per block, NH hypotheses m = rejections so far (r_j = r - j + m).
 // M[m] = acceptance of every word under hypothesis m.  The resolution keeps the
 // mask L of positions consumed so far: the next rejection under hypothesis m is
 // the lowest bit of Z_m = ~M[m] above L, so L' = blsmsk(Z_m & ~L) — two 1-cycle
 // ops per step.  Bits >= 32 of Z are set (virtual rejections past the block),
-// so after the 16 steps P = popcount(L) gives the block exactly:
-//   consumed = min(P, 32), accepted = P - 16
-// (16 rejections inside the block: P = last one + 1; fewer: P = 32 + the
-// virtual ones).
+// so after the NH steps P = popcount(L) gives the block exactly:
+//   consumed = min(P, 32), accepted = P - NH
+// (NH rejections inside the block: P = last one + 1; fewer: P = 32 + the
+// virtual ones).  9 rejections are expected per 32 words; NH = 10 (measured
+// fastest on the EPYC 9575F: 0.48 ns/word vs 0.57 at NH = 16) ends the blocks
+// with more rejections early, at their 10th.
+template <int NH>
 __attribute__((target("avx512f,avx512bw,avx512vl,avx512dq,bmi,bmi2,popcnt")))
-static size_t walk_avx512_nj(const u32 *w, size_t nw, u32 *rp) {
+static size_t walk_avx512_nj_t(const u32 *w, size_t nw, u32 *rp) {
     u32 r = *rp;
     size_t p = 0;
     const __m512i kidx = _mm512_setr_epi32(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
@@ -273,17 +277,17 @@ static size_t walk_avx512_nj(const u32 *w, size_t nw, u32 *rp) {
             __m512i lo0 = _mm512_mullo_epi32(w0, _mm512_sub_epi32(rv, kidx));
             __m512i lo1 = _mm512_mullo_epi32(w1, _mm512_sub_epi32(rv, kidx16));
             __m512i zz0 = _mm512_sub_epi32(zv, kz), zz1 = _mm512_sub_epi32(zv, kz16);
-            u64 Z[16];
-            for (int j = 0; j < 16; j++) {
-                const u32 m = (u32)_mm512_cmple_epu32_mask(lo0, zz0) | ((u32)_mm512_cmple_epu32_mask(lo1, zz1) << 16);
-                Z[j] = (u64)(~m) | 0xFFFFFFFF00000000ull;
+            u64 Z[NH];
+            for (int j = 0; j < NH; j++) {
+                const __mmask32 m = _mm512_kunpackw(_mm512_cmple_epu32_mask(lo1, zz1), _mm512_cmple_epu32_mask(lo0, zz0));
+                Z[j] = (u64)(u32)~_cvtmask32_u32(m) | 0xFFFFFFFF00000000ull;
                 lo0 = _mm512_add_epi32(lo0, w0); lo1 = _mm512_add_epi32(lo1, w1);
                 zz0 = _mm512_add_epi32(zz0, sv); zz1 = _mm512_add_epi32(zz1, sv);
             }
             u64 L = 0;
-            for (int j = 0; j < 16; j++) L = _blsmsk_u64(Z[j] & ~L);
+            for (int j = 0; j < NH; j++) L = _blsmsk_u64(Z[j] & ~L);
             const u32 P = (u32)__builtin_popcountll(L);
-            r -= P - 16;
+            r -= P - NH;
             p += P < 32 ? P : 32;
         }
         u32 z = (r << lz) - 1u;
@@ -297,6 +301,16 @@ static size_t walk_avx512_nj(const u32 *w, size_t nw, u32 *rp) {
     }
     *rp = r;
     return p;
+}
+static size_t walk_avx512_nj(const u32 *w, size_t nw, u32 *rp) {
+    static const int nh = getenv("BPPO_WALK_NH") ? atoi(getenv("BPPO_WALK_NH")) : 10;
+    switch (nh) {
+    case 8: return walk_avx512_nj_t<8>(w, nw, rp);
+    case 10: return walk_avx512_nj_t<10>(w, nw, rp);
+    case 14: return walk_avx512_nj_t<14>(w, nw, rp);
+    case 16: return walk_avx512_nj_t<16>(w, nw, rp);
+    default: return walk_avx512_nj_t<12>(w, nw, rp);
+    }
 }
 
 static int isa_level() {
