@@ -545,7 +545,11 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
 #pragma unroll
         for (int d = 0; d < 5; d++) gW0[d][ct] += __shfl_xor(gW0[d][ct], 32, 64);
     }
-    float *row = g.slab + (size_t)gwave * (g.np + NUM_M);
+    // the block's 8 wave rows meet in LDS (all tiles done: the staging is free)
+    // and are summed in wave order into one slab row per block
+    const int W_ = g.np + NUM_M;
+    __syncthreads();
+    float *row = smem + (size_t)wv * W_;
     if (h == 0) {
 #pragma unroll
         for (int ct = 0; ct < 2; ct++) {
@@ -578,6 +582,16 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
         mm[M_PL] = s_pl; mm[M_VL] = s_vl; mm[M_H] = s_h; mm[M_KL] = s_kl; mm[M_CF] = s_cf;
         mm[M_V] = s_v; mm[M_R] = s_r; mm[M_VE] = s_ve; mm[M_VE2] = s_ve2; mm[M_VEMAX] = s_mx;
         mm[M_N] = s_n;
+    }
+    __syncthreads();
+    for (int p = tid; p < W_; p += blockDim.x) {
+        float acc = smem[p];
+        if (p == g.np + M_VEMAX) {
+            for (int w = 1; w < WAVES; w++) acc = fmaxf(acc, smem[(size_t)w * W_ + p]);
+        } else {
+            for (int w = 1; w < WAVES; w++) acc += smem[(size_t)w * W_ + p];
+        }
+        g.slab[(size_t)blockIdx.x * W_ + p] = acc;
     }
 }
 
@@ -1102,7 +1116,11 @@ bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_
         c->slab_used = blocks * mmb::WAVES64;
         hipLaunchKernelGGL(k_minibatch_mfma64, dim3(blocks), dim3(64 * mmb::WAVES64), mmb::LDS64, c->stream, g);
     } else if (h == 64 && nl == 2 && c->relu_mfma) {
-        c->slab_used = blocks * mmb::WAVES;
+        if ((size_t)mmb::WAVES * (c->net.n_params + NUM_M) * sizeof(float) > mmb::LDSB) {
+            c->err = "minibatch kernel: gradient rows exceed LDS";
+            return BPPO_ERR_UNSUPPORTED;
+        }
+        c->slab_used = blocks;
         hipLaunchKernelGGL(k_minibatch_mfma, dim3(blocks), dim3(64 * mmb::WAVES), mmb::LDSB, c->stream, g);
     } else
 #define L(H_, NL_)                                                                                 \
