@@ -166,6 +166,8 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     TRY(dalloc(c, &c->d_mb_stats, (size_t)4 * std::max(cfg->num_minibatches, 2)));
     c->d_mb_cur = c->d_mb_stats;
     TRY(dalloc(c, &c->d_rows, (size_t)cfg->num_epochs * cfg->num_minibatches * (WM_COUNT + 4)));
+    if (!c->wide && cfg->hidden_size == 64 && cfg->num_hidden == 2 && cfg->relu && c->D == 5)
+        BPPO_HIP(c, hipMalloc((void **)&c->d_mbrow, sizeof(float4) * 4 * TN));
     BPPO_HIP(c, hipHostMalloc((void **)&c->h_red, sizeof(double) * (4 * 1024 + 64), hipHostMallocDefault));
     BPPO_HIP(c, hipEventCreateWithFlags(&c->ev_block, hipEventDisableTiming | hipEventBlockingSync));
     for (int i = 0; i < 8; i++) {
@@ -206,7 +208,7 @@ extern "C" void bppo_destroy(bppo_ctx *c) {
                     c->d_done, c->d_val, c->d_logp, c->d_adv, c->d_ret, c->d_act, c->d_X, c->d_on,
                     c->d_obs_part, c->d_rn_returns, c->d_rn_stats, c->d_scan_agg, c->d_last_v,
                     c->d_eps, c->d_ep_count, c->d_err, c->d_perm, c->d_fy, c->d_scan,
-                    c->d_red, c->d_mb_stats, c->d_gumbel, c->d_rows};
+                    c->d_red, c->d_mb_stats, c->d_gumbel, c->d_rows, c->d_mbrow};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     fy_ranges_free(c->fyr);
     if (c->h_red) (void)hipHostFree(c->h_red);
@@ -501,6 +503,7 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
     bool stop = false;
     double wait_ms = 0.0;
     tm_begin(c, TM_UPDATE);
+    if (c->d_mbrow) TRY(launch_pack_rows(c));
     float fw_ms = 0, sh_ms = 0;
     // without a KL early stop or a host all-reduce nothing in the loop needs the
     // metrics on the host: the minibatches are enqueued back to back and the rows

@@ -226,6 +226,7 @@ struct bppo_ctx {
     float *d_mb_stats = nullptr;      // advantage [mean, std, min, max] of each minibatch of the epoch [M][4]
     float *d_mb_cur = nullptr;        // the current minibatch's row of d_mb_stats
     float *d_rows = nullptr;          // per-minibatch metric rows of one update [E*M][WM_COUNT + 4]
+    float4 *d_mbrow = nullptr;        // CfgB net: the update's rows packed 64 B each [B][4] (k_pack_rows)
     // all-reduce hook
     bppo_allreduce_fn allreduce = nullptr;
     void *allreduce_user = nullptr;
@@ -298,6 +299,7 @@ bppo_status launch_minibatch(bppo_ctx *c, uint32_t mb_start, uint32_t mb_size, f
                              double *h_stats_out);
 bppo_status launch_adam(bppo_ctx *c, float lr, const float *c1, const float *c2);
 bppo_status launch_metric_row(bppo_ctx *c, float *dst, int nm);
+bppo_status launch_pack_rows(bppo_ctx *c);
 bppo_status launch_explained_variance(bppo_ctx *c, double *out6);
 // (wide_api.hip) multi-player path
 bppo_status wide_init(bppo_ctx *c);

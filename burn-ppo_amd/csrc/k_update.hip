@@ -31,6 +31,7 @@ struct MbArgs {
     float inv_mb, ent_coef, value_coef;
     int clip_value;
     int dbg_seq;           // timing experiment only: rows read in index order (no shuffle gather)
+    const float4 *rows;    // packed rows [B][4 x float4] (k_pack_rows) or nullptr
 };
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -283,14 +284,46 @@ struct RowData {
 __device__ __forceinline__ RowData load_row(const MbArgs &g, uint32_t idx) {
     const bool ok = idx != 0xFFFFFFFFu;
     const size_t i = ok ? idx : 0;
-    const float *o = g.obs + i * 5;
     RowData d;
+    if (g.rows) {                     // one 64-byte line per row
+        const float4 a = g.rows[i * 4], b = g.rows[i * 4 + 1];
+        const float2 c = *reinterpret_cast<const float2 *>(g.rows + i * 4 + 2);
+        d.x0 = ok ? a.x : 0.0f; d.x1 = ok ? a.y : 0.0f; d.x2 = ok ? a.z : 0.0f; d.x3 = ok ? a.w : 0.0f;
+        d.x4 = ok ? b.x : 0.0f;
+        d.a = ok ? __float_as_int(b.y) : 0;
+        d.olp = ok ? b.z : 0.0f; d.A = ok ? b.w : 0.0f; d.R = ok ? c.x : 0.0f;
+        d.ov = (ok && g.clip_value) ? c.y : 0.0f;
+        return d;
+    }
+    const float *o = g.obs + i * 5;
     d.x0 = ok ? o[0] : 0.0f; d.x1 = ok ? o[1] : 0.0f; d.x2 = ok ? o[2] : 0.0f;
     d.x3 = ok ? o[3] : 0.0f; d.x4 = ok ? o[4] : 0.0f;
     d.a = ok ? g.act[i] : 0;
     d.olp = ok ? g.logp[i] : 0.0f; d.A = ok ? g.adv[i] : 0.0f; d.R = ok ? g.ret[i] : 0.0f;
     d.ov = (ok && g.clip_value) ? g.val[i] : 0.0f;
     return d;
+}
+
+// the update's rows packed once per update into 64-byte records
+// [obs 0..4, action, log-prob, advantage, return, value, pad] so the shuffled
+// minibatch gather touches one cache line per row instead of six
+__global__ void __launch_bounds__(256) k_pack_rows(size_t B, const float *obs, const int32_t *act, const float *logp,
+                                                   const float *adv, const float *ret, const float *val,
+                                                   float4 *rows) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < B; i += (size_t)gridDim.x * blockDim.x) {
+        const float *o = obs + i * 5;
+        rows[i * 4] = make_float4(o[0], o[1], o[2], o[3]);
+        rows[i * 4 + 1] = make_float4(o[4], __int_as_float(act[i]), logp[i], adv[i]);
+        rows[i * 4 + 2] = make_float4(ret[i], val[i], 0.0f, 0.0f);
+        rows[i * 4 + 3] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+}
+bppo_status launch_pack_rows(bppo_ctx *c) {
+    const size_t B = (size_t)c->T * c->N;
+    hipLaunchKernelGGL(k_pack_rows, dim3(2048), dim3(256), 0, c->stream, B, c->d_obs, c->d_act, c->d_logp, c->d_adv,
+                       c->d_ret, c->d_val, c->d_mbrow);
+    BPPO_HIP(c, hipGetLastError());
+    return BPPO_OK;
 }
 
 // ================================================ MFMA minibatch (H=64, NL=2) ==
@@ -1109,6 +1142,7 @@ bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_
     g.clip_value = c->cfg.clip_value;
     static const bool dbg_seq = getenv("BPPO_DBG_MB_SEQ") != nullptr;
     g.dbg_seq = dbg_seq;
+    g.rows = c->d_mbrow;
     int blocks = 256;
     const size_t params_bytes = ((c->net.n_params + 3) & ~(size_t)3) * sizeof(float);
     static const bool mb64 = getenv("BPPO_MB64") != nullptr;
