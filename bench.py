@@ -7,7 +7,8 @@ i.e. 8,388,608 env-steps per GPU per step, synthetic fixed-seed data (seed 42).
 
 N>1 runs as one process per GPU (torch.distributed.run): each rank owns its own
 65536 envs (global env index rank*65536 + i) and the gradient is all-reduced
-(RCCL over xGMI) once per minibatch; weak scaling.
+(RCCL over xGMI) once per minibatch, enqueued on the context's stream (the host
+never waits per minibatch); weak scaling.
 
 Prints ONE JSON line (rank 0).  `roofline` is the dominant kernel's (the fused
 minibatch forward/backward) algorithmic FLOP rate against the FP32 dense peak;
@@ -42,16 +43,6 @@ def parse():
     p.add_argument("--cpu-envs", type=int, default=1024, help="CPU baseline sample size (envs)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
-
-
-def hip_memcpy_d2d(dst, src, nbytes):
-    lib = getattr(hip_memcpy_d2d, "lib", None)
-    if lib is None:
-        lib = C.CDLL("libamdhip64.so")
-        lib.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
-        lib.hipMemcpy.restype = C.c_int
-        hip_memcpy_d2d.lib = lib
-    assert lib.hipMemcpy(dst, src, nbytes, 3) == 0
 
 
 def cpu_baseline(args):
@@ -95,15 +86,11 @@ def main():
     cfg = bppo.make_config("cartpole", num_envs=N * world, num_steps=T)
     tr = bppo.Trainer(cfg, device=local, init_seed=0, rank=rank, world=world, envs_per_rank=N)
     if world > 1:
-        gbuf = torch.zeros(tr.ctx.n_params + 64, device="cuda")
-
-        def allreduce(ptr, n):
-            hip_memcpy_d2d(gbuf.data_ptr(), ptr, n * 4)
-            dist.all_reduce(gbuf[:n])
-            torch.cuda.synchronize()
-            hip_memcpy_d2d(ptr, gbuf.data_ptr(), n * 4)
-
-        tr.ctx.set_allreduce(allreduce, world)
+        # RCCL all-reduce of the gradient enqueued on the context's stream: no
+        # host wait per minibatch (bppo_set_allreduce_async)
+        from bppo.dist import make_allreduce
+        fn = make_allreduce(dist, mode="device_async", max_elems=tr.ctx.n_params + 64, stream=tr.ctx.stream)
+        tr.ctx.set_allreduce(fn, world, stream_ordered=True)
 
     for _ in range(args.warmup):
         tr.train_update()

@@ -9,6 +9,9 @@ size before clip + Adam, so all ranks apply the same step and stay in sync.
 `make_allreduce` builds the callback libbppo invokes (bppo_set_allreduce):
   mode "device": the buffer is HIP device memory; all-reduce a torch CUDA
                  tensor (backend "nccl" = RCCL over xGMI) staged by D2D copy;
+  mode "device_async": stream-ordered (bppo_set_allreduce_async): D2D copy,
+                 RCCL all-reduce and D2D copy all enqueued on the context's
+                 stream (torch.cuda.ExternalStream); the host never waits;
   mode "host_staged": D2H copy, CPU all-reduce (gloo), H2D copy — lets several
                  ranks share one GPU in tests;
   mode "host":   the pointer is host memory (CPU-only tests of the plumbing).
@@ -37,9 +40,33 @@ def _memcpy(dst, src, nbytes, kind):
         raise RuntimeError(f"hipMemcpy failed ({st})")
 
 
-def make_allreduce(dist, mode="device", max_elems=1 << 20):
-    """Return fn(ptr:int, n:int) that leaves the sum over ranks in place."""
+def _memcpy_async(dst, src, nbytes, stream):
+    lib = _hip()
+    if not hasattr(lib, "_async"):
+        lib.hipMemcpyAsync.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
+        lib.hipMemcpyAsync.restype = C.c_int
+        lib._async = True
+    st = lib.hipMemcpyAsync(dst, src, nbytes, _D2D, stream)
+    if st != 0:
+        raise RuntimeError(f"hipMemcpyAsync failed ({st})")
+
+
+def make_allreduce(dist, mode="device", max_elems=1 << 20, stream=None, reduce=None):
+    """Return fn(ptr:int, n:int) that leaves the sum over ranks in place.
+    device_async needs the context's stream; `reduce(tensor)` replaces
+    dist.all_reduce (tests)."""
     import torch
+    if mode == "device_async":
+        buf = torch.zeros(max_elems, device="cuda")
+        ext = torch.cuda.ExternalStream(stream)
+        red = reduce or (lambda t: dist.all_reduce(t))
+
+        def fn(ptr, n):
+            _memcpy_async(buf.data_ptr(), ptr, n * 4, stream)
+            with torch.cuda.stream(ext):
+                red(buf[:n])
+            _memcpy_async(ptr, buf.data_ptr(), n * 4, stream)
+        return fn
     if mode == "device":
         buf = torch.zeros(max_elems, device="cuda")
 

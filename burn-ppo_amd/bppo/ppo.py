@@ -108,8 +108,10 @@ class Context:
         self._chk(L.lib().bppo_last_kernel_ms(self.h, name.encode(), C.byref(f)))
         return f.value
 
-    def set_allreduce(self, fn, world):
-        """fn(device_ptr:int, n:int) -> None must leave the SUM over ranks in place."""
+    def set_allreduce(self, fn, world, stream_ordered=False):
+        """fn(device_ptr:int, n:int) -> None must leave the SUM over ranks in place.
+        stream_ordered: fn only enqueues the reduction on `self.stream` (no host
+        wait per minibatch; bppo_set_allreduce_async)."""
         def _cb(p, n, user):
             try:
                 fn(p, n)
@@ -117,7 +119,15 @@ class Context:
             except Exception:
                 return 1
         self._ar_keep = L.ALLREDUCE_FN(_cb)
-        self._chk(L.lib().bppo_set_allreduce(self.h, self._ar_keep, None, world))
+        setter = L.lib().bppo_set_allreduce_async if stream_ordered else L.lib().bppo_set_allreduce
+        self._chk(setter(self.h, self._ar_keep, None, world))
+
+    @property
+    def stream(self):
+        """The context's HIP stream (hipStream_t as int)."""
+        s = C.c_void_p()
+        self._chk(L.lib().bppo_get_stream(self.h, C.byref(s)))
+        return s.value or 0
 
 
 class VecEnv:

@@ -508,7 +508,7 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
     // without a KL early stop or a host all-reduce nothing in the loop needs the
     // metrics on the host: the minibatches are enqueued back to back and the rows
     // are read once after the last one (no per-minibatch stream drain)
-    const bool deferred = c->cfg.target_kl < 0 && !(c->allreduce && c->world > 1);
+    const bool deferred = c->cfg.target_kl < 0 && !(c->allreduce && c->world > 1 && !c->allreduce_async);
     int nrow = 0;
     for (int ep = 0; ep < c->cfg.num_epochs && !stop; ep++) {
         epochs_run++;
@@ -536,7 +536,7 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
             }
             (void)hipEventRecord(c->ev[TM_FWDBWD][1], c->stream);
             if (c->allreduce && c->world > 1) {
-                BPPO_HIP(c, sync_stream(c));
+                if (!c->allreduce_async) BPPO_HIP(c, sync_stream(c));
                 if (c->allreduce(c->d_grad, (size_t)np + NM, c->allreduce_user) != 0) {
                     c->err = "all-reduce callback failed";
                     return BPPO_ERR_COMM;
@@ -641,7 +641,19 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
 
 extern "C" bppo_status bppo_set_allreduce(bppo_ctx *c, bppo_allreduce_fn fn, void *user, int32_t world) {
     if (!c || world < 1) return BPPO_ERR_ARG;
-    c->allreduce = fn; c->allreduce_user = user; c->world = world;
+    c->allreduce = fn; c->allreduce_user = user; c->world = world; c->allreduce_async = 0;
+    return BPPO_OK;
+}
+
+extern "C" bppo_status bppo_set_allreduce_async(bppo_ctx *c, bppo_allreduce_fn fn, void *user, int32_t world) {
+    if (!c || world < 1) return BPPO_ERR_ARG;
+    c->allreduce = fn; c->allreduce_user = user; c->world = world; c->allreduce_async = 1;
+    return BPPO_OK;
+}
+
+extern "C" bppo_status bppo_get_stream(bppo_ctx *c, void **stream) {
+    if (!c || !stream) return BPPO_ERR_ARG;
+    *stream = (void *)c->stream;
     return BPPO_OK;
 }
 

@@ -231,6 +231,7 @@ struct bppo_ctx {
     bppo_allreduce_fn allreduce = nullptr;
     void *allreduce_user = nullptr;
     int world = 1;
+    int allreduce_async = 0;          // callback enqueues on the stream (no host sync per minibatch)
     // ---- multi-player ("wide") path: Connect Four / Liar's Dice (wide_api.hip)
     int wide = 0;                     // env_kind != CartPole
     int L = 0;                        // rollout row length G + D: [priv | obs]

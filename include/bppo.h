@@ -141,6 +141,15 @@ bppo_status bppo_ppo_update(bppo_ctx *ctx, double lr, double ent_coef, bppo_upda
 typedef int (*bppo_allreduce_fn)(float *device_buf, size_t n, void *user);
 bppo_status bppo_set_allreduce(bppo_ctx *ctx, bppo_allreduce_fn fn, void *user, int32_t world_size);
 
+/* stream-ordered variant: fn is called WITHOUT draining the stream, right after
+ * the minibatch's gradient kernels are enqueued; it must enqueue the SUM
+ * all-reduce of device_buf on the context's stream (bppo_get_stream) and
+ * return.  Clip + Adam are enqueued after it, so the host never waits per
+ * minibatch (replaces the ncclAllReduce-on-stream call a Rust host would make
+ * in ppo.rs's update loop; the reference has no multi-GPU path). */
+bppo_status bppo_set_allreduce_async(bppo_ctx *ctx, bppo_allreduce_fn fn, void *user, int32_t world_size);
+bppo_status bppo_get_stream(bppo_ctx *ctx, void **hip_stream);
+
 /* parity hooks: export / import a RolloutBuffer field.  names: "obs", "priv",
  * "actions" (i32), "rewards", "dones", "values", "log_probs", "advantages",
  * "returns", "players" (i32), "all_rewards", "masks", "last_v_pp", "perm" (u32,

@@ -105,3 +105,29 @@ def test_two_ranks_identical_shards_match_single_rank():
     assert np.array_equal(res[0][1], res[1][1]), "ranks diverged"
     assert np.array_equal(res[0][1], p_solo)
     assert abs(res[0][2] - ms[-1]["policy_loss"]) <= 1e-6 + 1e-5 * abs(ms[-1]["policy_loss"])
+
+
+@pytest.mark.gpu
+def test_stream_ordered_allreduce_matches_single_rank():
+    """bppo_set_allreduce_async: the callback only ENQUEUES its reduction on the
+    context's stream (staging copies + a torch op on an ExternalStream), with no
+    host wait per minibatch.  An emulated 2-rank SUM of identical shards (x2,
+    then libbppo's /2) must reproduce the single-rank parameters bit for bit,
+    which fails if any of the enqueued steps ran out of order."""
+    import torch
+    from bppo.dist import make_allreduce
+    updates = 3
+    cfg = bppo.make_config("cartpole", num_envs=256, num_steps=32)
+    solo = bppo.Trainer(cfg, device=0, init_seed=3)
+    for _ in range(updates):
+        solo.train_update()
+    p_solo = solo.model.get_params()
+    solo.close()
+    tr = bppo.Trainer(cfg, device=0, init_seed=3)
+    fn = make_allreduce(None, mode="device_async", stream=tr.ctx.stream, reduce=lambda t: t.mul_(2.0))
+    tr.ctx.set_allreduce(fn, 2, stream_ordered=True)
+    for _ in range(updates):
+        tr.train_update()
+    p = tr.model.get_params()
+    tr.close()
+    assert np.array_equal(p, p_solo)
