@@ -14,26 +14,62 @@
 namespace bppo {
 
 // ObsNormalizer::normalize_batch (normalization.rs:58-75) from device stats
-// on = {mean[D], M2[D], count}
-__device__ __forceinline__ void normalize_obs5(const double *__restrict__ on, int norm_on,
-                                               const float (&raw)[5], float (&out)[5]) {
-    const double cnt = on[10];
-    if (!norm_on || cnt < 2.0) {
+// on = {mean[D], M2[D], count}.  The stats are fixed for a whole rollout, so
+// the per-dim std is derived once (same f64 ops as per call) and each step only
+// does (raw - mean) / sd.
+struct ObsNorm5 {
+    double mean[5], sd[5];
+    bool on;
+    __device__ __forceinline__ void load(const double *__restrict__ st, int norm_on) {
+        const double cnt = st[10];
+        on = norm_on && cnt >= 2.0;
 #pragma unroll
-        for (int d = 0; d < 5; d++) out[d] = raw[d];
-        return;
+        for (int d = 0; d < 5; d++) {
+            const double var = st[5 + d] / cnt;
+            double s = sqrt(var);
+            sd[d] = s < 1e-8 ? 1e-8 : s;
+            mean[d] = st[d];
+        }
     }
+    __device__ __forceinline__ void apply(const float (&raw)[5], float (&out)[5]) const {
 #pragma unroll
-    for (int d = 0; d < 5; d++) {
-        double var = on[5 + d] / cnt;
-        double sd = sqrt(var);
-        sd = sd < 1e-8 ? 1e-8 : sd;
-        float z = (float)(((double)raw[d] - on[d]) / sd);
-        z = z < -10.0f ? -10.0f : z;
-        z = z > 10.0f ? 10.0f : z;
-        out[d] = z;
+        for (int d = 0; d < 5; d++) {
+            if (!on) { out[d] = raw[d]; continue; }
+            float z = (float)(((double)raw[d] - mean[d]) / sd[d]);
+            z = z < -10.0f ? -10.0f : z;
+            z = z > 10.0f ? 10.0f : z;
+            out[d] = z;
+        }
     }
-}
+};
+
+// per-env raw-observation statistics of one rollout (count T) for the
+// normalizer update (normalization.rs:37-53): sums shifted by the first
+// observation, no division per step; mean / M2 at the end match the
+// sequential Welford values to f64 rounding (Chan-merged afterwards)
+struct ObsAcc5 {
+    double x0[5], s1[5], s2[5];
+    __device__ __forceinline__ void init(const float (&raw)[5]) {
+#pragma unroll
+        for (int d = 0; d < 5; d++) { x0[d] = (double)raw[d]; s1[d] = s2[d] = 0.0; }
+    }
+    __device__ __forceinline__ void push(const float (&raw)[5]) {
+#pragma unroll
+        for (int d = 0; d < 5; d++) {
+            const double dd = (double)raw[d] - x0[d];
+            s1[d] += dd;
+            s2[d] += dd * dd;
+        }
+    }
+    __device__ __forceinline__ void store(double T, double *part) const {
+#pragma unroll
+        for (int d = 0; d < 5; d++) {
+            part[d] = x0[d] + s1[d] / T;
+            const double m2 = s2[d] - s1[d] * s1[d] / T;
+            part[5 + d] = m2 > 0.0 ? m2 : 0.0;
+        }
+    }
+};
 
 __device__ __forceinline__ void load_state(const float *cp, const int32_t *steps, int N, int e,
                                            CartPoleState &s) {
@@ -96,21 +132,21 @@ __global__ void __launch_bounds__(256) k_cartpole_rollout(RolloutArgs a) {
     ec.init(seed_key(a.seed_base + (uint64_t)e), 0, a.env_pos[e]);
     float ep_ret = a.ep_ret[e];
     int32_t ep_len = a.ep_len[e];
-    double wm[5] = {0, 0, 0, 0, 0}, wM2[5] = {0, 0, 0, 0, 0};
+    ObsNorm5 nz;
+    nz.load(a.on, a.norm_on);
+    ObsAcc5 oa;
+    {
+        float raw0[5];
+        cartpole_obs(s, raw0);
+        oa.init(raw0);
+    }
     int32_t bad = 0;
 #pragma unroll 1
     for (int t = 0; t < a.T; t++) {
         float raw[5], x[5];
         cartpole_obs(s, raw);
-        const double cnt = (double)(t + 1);
-#pragma unroll
-        for (int d = 0; d < 5; d++) {                 // per-env Welford partial (raw obs)
-            double xv = (double)raw[d];
-            double delta = xv - wm[d];
-            wm[d] += delta / cnt;
-            wM2[d] += delta * (xv - wm[d]);
-        }
-        normalize_obs5(a.on, a.norm_on, raw, x);
+        oa.push(raw);
+        nz.apply(raw, x);
         const size_t row = (size_t)t * N + e;
 #pragma unroll
         for (int d = 0; d < 5; d++) a.obs[row * 5 + d] = x[d];
@@ -165,11 +201,7 @@ __global__ void __launch_bounds__(256) k_cartpole_rollout(RolloutArgs a) {
     a.env_pos[e] = ec.pos;
     a.ep_ret[e] = ep_ret;
     a.ep_len[e] = ep_len;
-#pragma unroll
-    for (int d = 0; d < 5; d++) {
-        a.obs_part[(size_t)e * 10 + d] = wm[d];
-        a.obs_part[(size_t)e * 10 + 5 + d] = wM2[d];
-    }
+    oa.store((double)a.T, a.obs_part + (size_t)e * 10);
     if (bad) atomicOr(a.err, 1);
 }
 
@@ -220,7 +252,14 @@ __global__ void __launch_bounds__(512, 2) k_cartpole_rollout_mfma(RolloutArgs a,
         ep_ret = a.ep_ret[e];
         ep_len = a.ep_len[e];
     }
-    double wm[5] = {0, 0, 0, 0, 0}, wM2[5] = {0, 0, 0, 0, 0};
+    ObsNorm5 nz;
+    nz.load(a.on, a.norm_on);
+    ObsAcc5 oa;
+    if (mine) {
+        float raw0[5];
+        cartpole_obs(s, raw0);
+        oa.init(raw0);
+    }
     int32_t bad = 0;
 #pragma unroll 1
     for (int t = 0; t < a.T; t++) {
@@ -230,15 +269,8 @@ __global__ void __launch_bounds__(512, 2) k_cartpole_rollout_mfma(RolloutArgs a,
             if (mine) {
                 float raw[5];
                 cartpole_obs(s, raw);
-                const double cnt = (double)(t + 1);
-#pragma unroll
-                for (int d = 0; d < 5; d++) {             // per-env Welford partial (raw obs)
-                    const double xv = (double)raw[d];
-                    const double delta = xv - wm[d];
-                    wm[d] += delta / cnt;
-                    wM2[d] += delta * (xv - wm[d]);
-                }
-                normalize_obs5(a.on, a.norm_on, raw, x);
+                oa.push(raw);
+                nz.apply(raw, x);
 #pragma unroll
                 for (int d = 0; d < 5; d++) a.obs[row * 5 + d] = x[d];
             }
@@ -336,11 +368,7 @@ __global__ void __launch_bounds__(512, 2) k_cartpole_rollout_mfma(RolloutArgs a,
         a.env_pos[e] = ec.pos;
         a.ep_ret[e] = ep_ret;
         a.ep_len[e] = ep_len;
-#pragma unroll
-        for (int d = 0; d < 5; d++) {
-            a.obs_part[(size_t)e * 10 + d] = wm[d];
-            a.obs_part[(size_t)e * 10 + 5 + d] = wM2[d];
-        }
+        oa.store((double)a.T, a.obs_part + (size_t)e * 10);
         if (bad) atomicOr(a.err, 1);
     }
 }
@@ -409,7 +437,9 @@ __global__ void __launch_bounds__(256) k_cartpole_bootstrap(int N, const float *
     load_state(cp, steps, N, e, s);
     float raw[5], x[5], lg[2], v;
     cartpole_obs(s, raw);
-    normalize_obs5(on, norm_on, raw, x);
+    ObsNorm5 nz;
+    nz.load(on, norm_on);
+    nz.apply(raw, x);
     cp_forward<H, NL>(sP, x, lg, v);
     last_v[e] = v;
 }
