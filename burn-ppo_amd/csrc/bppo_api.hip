@@ -548,10 +548,10 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
                 c1[t] = 1.0f - powi_f32(0.9f, ti);
                 c2[t] = 1.0f - powi_f32(0.999f, ti);
             }
-            TRY(launch_adam(c, (float)lr, c1, c2));
+            // clip + Adam; the metric row (grad[np .. np+NM) and adv stats) into the
+            // update's device rows
+            TRY(launch_adam(c, (float)lr, c1, c2, c->d_rows + (size_t)nrow * (NM + 4), NM));
             if (c->wide) TRY(wide_pack(c));
-            // metric row: grad[np .. np+NM) and adv stats, into the update's device rows
-            TRY(launch_metric_row(c, c->d_rows + (size_t)nrow * (NM + 4), NM));
             nrow++;
             if (!deferred) {
                 std::vector<float> row(NM + 4);

@@ -298,7 +298,8 @@ void fy_ranges_free(FyRanges &r);
 bppo_status launch_epoch_adv_stats(bppo_ctx *c, uint32_t B, int M);
 bppo_status launch_minibatch(bppo_ctx *c, uint32_t mb_start, uint32_t mb_size, float ent_coef,
                              double *h_stats_out);
-bppo_status launch_adam(bppo_ctx *c, float lr, const float *c1, const float *c2);
+bppo_status launch_adam(bppo_ctx *c, float lr, const float *c1, const float *c2, float *metric_dst = nullptr,
+                        int nm = 0);
 bppo_status launch_metric_row(bppo_ctx *c, float *dst, int nm);
 bppo_status launch_pack_rows(bppo_ctx *c);
 bppo_status launch_explained_variance(bppo_ctx *c, double *out6);

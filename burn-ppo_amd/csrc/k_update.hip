@@ -1021,6 +1021,47 @@ __global__ void __launch_bounds__(256) k_adam(AdamArgs a) {
     }
 }
 
+// every tensor within one ADAM_CHUNK (the CfgB net): one block per tensor does
+// pass 1 (the same per-thread sums and tree as k_adam_norm) and pass 2 (the
+// update) back to back; block 0 also copies the minibatch's metric row
+__global__ void __launch_bounds__(256) k_adam1(AdamArgs a, const float *gtail, const float *mb_stats, int nm,
+                                               float *metric_dst) {
+    __shared__ double red[256];
+    const AdamTensor T = a.t[blockIdx.x];
+    double ss = 0.0;
+    for (int i = threadIdx.x; i < T.len; i += blockDim.x) {
+        const float gi = a.grad[T.off + i] * a.inv_world;
+        ss += (double)gi * (double)gi;
+    }
+    red[threadIdx.x] = ss;
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+        if (threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+        __syncthreads();
+    }
+    const double tot = red[0];
+    const float norm = (float)sqrt(tot);
+    const float scale = norm > a.max_norm ? __fdiv_rn(a.max_norm, norm) : 1.0f;
+    const bool clip = norm > a.max_norm;
+    const float b1 = 0.9f, b2 = 0.999f, f1 = 1.0f - 0.9f, f2 = 1.0f - 0.999f;
+    for (int i = threadIdx.x; i < T.len; i += blockDim.x) {
+        float gi = a.grad[T.off + i] * a.inv_world;
+        if (clip) gi = __fmul_rn(gi, scale);
+        const float m1 = __fadd_rn(__fmul_rn(a.m1[T.off + i], b1), __fmul_rn(gi, f1));
+        const float m2 = __fadd_rn(__fmul_rn(a.m2[T.off + i], b2), __fmul_rn(__fmul_rn(gi, gi), f2));
+        a.m1[T.off + i] = m1;
+        a.m2[T.off + i] = m2;
+        const float m1c = __fdiv_rn(m1, T.c1), m2c = __fdiv_rn(m2, T.c2);
+        const float upd = __fdiv_rn(m1c, __fadd_rn(__fsqrt_rn(m2c), a.eps));
+        a.params[T.off + i] = __fsub_rn(a.params[T.off + i], __fmul_rn(upd, a.lr));
+    }
+    if (blockIdx.x == 0 && metric_dst) {
+        const int i = threadIdx.x;
+        if (i < nm) metric_dst[i] = gtail[i];
+        else if (i < nm + 4) metric_dst[i] = mb_stats[i - nm];
+    }
+}
+
 // explained variance partial sums (ppo.rs:1268-1294)
 __global__ void __launch_bounds__(256) k_ev(size_t n, const float *val, const float *ret, double *part) {
     __shared__ double sh[4][256];
@@ -1191,7 +1232,7 @@ bppo_status launch_metric_row(bppo_ctx *c, float *dst, int nm) {
     return BPPO_OK;
 }
 
-bppo_status launch_adam(bppo_ctx *c, float lr, const float *c1, const float *c2) {
+bppo_status launch_adam(bppo_ctx *c, float lr, const float *c1, const float *c2, float *metric_dst, int nm) {
     AdamArgs a;
     a.params = c->d_params; a.grad = c->d_grad; a.m1 = c->d_m1; a.m2 = c->d_m2;
     a.nt = 2 * c->net.n_layers;
@@ -1205,9 +1246,16 @@ bppo_status launch_adam(bppo_ctx *c, float lr, const float *c1, const float *c2)
     int nb = 0;
     for (int t = 0; t < a.nt; t++) { a.blk0[t] = nb; nb += (a.t[t].len + ADAM_CHUNK - 1) / ADAM_CHUNK; }
     a.blk0[a.nt] = nb;
+    if (nb == a.nt && metric_dst) {       // one chunk per tensor: fused
+        hipLaunchKernelGGL(k_adam1, dim3(nb), dim3(256), 0, c->stream, a, c->d_grad + c->net.n_params, c->d_mb_cur, nm,
+                           metric_dst);
+        BPPO_HIP(c, hipGetLastError());
+        return BPPO_OK;
+    }
     hipLaunchKernelGGL(k_adam_norm, dim3(nb), dim3(256), 0, c->stream, a);
     hipLaunchKernelGGL(k_adam, dim3(nb), dim3(256), 0, c->stream, a);
     BPPO_HIP(c, hipGetLastError());
+    if (metric_dst) return launch_metric_row(c, metric_dst, nm);
     return BPPO_OK;
 }
 
