@@ -36,7 +36,7 @@ GAE_BYTES_PER_ELEM = 20        # r, d, v in; adv, ret out (f32)
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--num-envs", type=int, default=65536, help="envs per GPU")
     p.add_argument("--num-steps", type=int, default=128)

@@ -502,29 +502,49 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
                 m_n += 1.0f;
             }
             gbp0 += dl0; gbp1 += dl1; gbv += dv;
-            B.dl[c * 4 + 0] = dl0; B.dl[c * 4 + 1] = dl1; B.dl[c * 4 + 2] = dv;
+            B.dl[c * 4 + 0] = dl0; B.dl[c * 4 + 1] = dl1; B.dl[c * 4 + 2] = dv; B.dl[c * 4 + 3] = 0.0f;
         }
         wave_sync();
-        // ---- head gradients; dZ2 = ([dl | dv] [Wp | Wv]^T) * [H2 > 0] over H2 in
-        // place (each lane rewrites only its own C/D elements)
+        // ---- head weight gradients dWp, dWv += H2^T [dl | dv] (lane = hidden unit)
 #pragma unroll 4
         for (int q = 0; q < 16; q++) {
             const int row = cd_row(q, h);
             const float d0 = B.dl[row * 4], d1 = B.dl[row * 4 + 1], dvr = B.dl[row * 4 + 2];
 #pragma unroll
             for (int ct = 0; ct < 2; ct++) {
-                const int ad = row * RS + c + 32 * ct;
-                const float hv = B.T2[ad];
+                const float hv = B.T2[row * RS + c + 32 * ct];
                 gP0[ct] = __builtin_fmaf(hv, d0, gP0[ct]);
                 gP1[ct] = __builtin_fmaf(hv, d1, gP1[ct]);
                 gV[ct] = __builtin_fmaf(hv, dvr, gV[ct]);
-                float sacc = __builtin_fmaf(d0, wpk0[ct], 0.0f);
-                sacc = __builtin_fmaf(d1, wpk1[ct], sacc);
-                sacc = __builtin_fmaf(dvr, wvk[ct], sacc);
-                const float dz = hv > 0.0f ? sacc : 0.0f;
+            }
+        }
+        // ---- dZ2 before the relu mask: [dl0 dl1 dv 0] [Wp0; Wp1; Wv; 0] per (row, k)
+        // as two k-steps of the MFMA (the same k-ordered fma chain as the VALU
+        // form d0*wp0 -> +d1*wp1 -> +dv*wv), already in the C/D layout
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++)
+#pragma unroll
+            for (int q = 0; q < 16; q++) acc[ct][q] = 0.0f;
+        {
+            const float a0 = B.dl[c * 4 + h], a1 = B.dl[c * 4 + 2 + h];
+#pragma unroll
+            for (int ct = 0; ct < 2; ct++) {
+                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, h ? wpk1[ct] : wpk0[ct], acc[ct], 0, 0, 0);
+                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, h ? 0.0f : wvk[ct], acc[ct], 0, 0, 0);
+            }
+        }
+        // dZ2 = that * [H2 > 0], over H2 in place (each lane rewrites only its own
+        // C/D elements)
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+#pragma unroll
+            for (int ct = 0; ct < 2; ct++) {
+                const int ad = cd_row(q, h) * RS + c + 32 * ct;
+                const float dz = B.T2[ad] > 0.0f ? acc[ct][q] : 0.0f;
                 gb1[ct] += dz;
                 B.T2[ad] = dz;
             }
+            if ((q & 3) == 3) __builtin_amdgcn_sched_barrier(0);   // bound the LDS read hoisting
         }
         wave_sync();
         // ---- dZ1 = dZ2 W1^T (32 k-steps) interleaved with dW1 += H1^T dZ2 (16
