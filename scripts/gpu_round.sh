@@ -8,6 +8,6 @@ if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 900 python -m pytest tests -m gpu -q -x --timeout 600 > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -40 gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 600 python bench.py --steps 3 --warmup 1 --cpu-envs 256 > gpurun_out/bench.log 2>&1
+timeout -k 10 600 python bench.py > gpurun_out/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -20 gpurun_out/bench.log
 exit $rc
