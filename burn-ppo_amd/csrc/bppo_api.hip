@@ -49,6 +49,7 @@ __global__ void k_libm(int which, const float *x, float *y, size_t n) {
     case 1: y[i] = bppo_math::sinf_glibc(v); break;
     case 2: y[i] = bppo_math::cosf_glibc(v); break;
     case 3: y[i] = -bppo_math::logf_glibc(-bppo_math::logf_glibc(v)); break;
+    case 5: y[i] = bppo_math::tanhf_glibc_bf(v); break;   // the form the MLP kernels use
     default: y[i] = bppo_math::expf_glibc(v); break;
     }
 }
@@ -740,6 +741,7 @@ extern "C" bppo_status bppo_debug_libm(int32_t which, int32_t device, const floa
             case 1: y[i] = bppo_math::sinf_glibc(v); break;
             case 2: y[i] = bppo_math::cosf_glibc(v); break;
             case 3: y[i] = -bppo_math::logf_glibc(-bppo_math::logf_glibc(v)); break;
+            case 5: y[i] = bppo_math::tanhf_glibc(v); break;
             default: y[i] = bppo_math::expf_glibc(v); break;
             }
         }

@@ -182,11 +182,33 @@ __device__ __forceinline__ float log_prob_row(const float x[A], int a) {
 }
 
 // ------------------------------------------------------------------- MLP ----
+// hidden activation (mlp.rs:79, :187-191): relu if configured, else tanh
+enum { ACT_NONE = 0, ACT_RELU = 1, ACT_TANH = 2 };
+template <int ACT>
+__device__ __forceinline__ float act_fwd(float v) {
+    if constexpr (ACT == ACT_RELU) return v > 0.0f ? v : 0.0f;
+    else if constexpr (ACT == ACT_TANH) return bppo_math::tanhf_glibc_bf(v);
+    else return v;
+}
+// Burn autodiff backward through the activation given its OUTPUT y:
+// relu -> g where y > 0; tanh -> g * (1 - y^2) (powi 2, neg, add 1, mul)
+template <int ACT>
+__device__ __forceinline__ float act_bwd(float g, float y) {
+    if constexpr (ACT == ACT_RELU) return y > 0.0f ? g : 0.0f;
+    else if constexpr (ACT == ACT_TANH) return __fmul_rn(g, __fsub_rn(1.0f, __fmul_rn(y, y)));
+    else return g;
+}
+
 // y[o] = act( (sum_k x[k] W[k][o], k-ordered fma chain from 0) + b[o] )
 // W row-major [IN][OUT] in LDS (or global).  IN <= 256 (one matrixmultiply KC block).
-template <int IN, int OUT, bool RELU>
+// tanh: the OUT pre-activations go through this thread's column of an LDS stage
+// (element o at stage[o * ss], ss = threads sharing the stage, so a wave's
+// accesses are conflict-free) and one rolled loop applies tanh; an unrolled
+// per-unit tanh is too large to schedule without spilling.
+template <int IN, int OUT, int ACT>
 __device__ __forceinline__ void linear_fwd(const float *__restrict__ W, const float *__restrict__ b,
-                                           const float (&x)[IN], float (&y)[OUT]) {
+                                           const float (&x)[IN], float (&y)[OUT],
+                                           float *stage = nullptr, int ss = 0) {
     static_assert(IN <= 256, "K > KC needs the split-chain path");
 #pragma unroll
     for (int o = 0; o < OUT; o++) y[o] = 0.0f;
@@ -203,10 +225,16 @@ __device__ __forceinline__ void linear_fwd(const float *__restrict__ W, const fl
 #pragma unroll
         for (int o = 0; o < OUT; o++) y[o] = __builtin_fmaf(xk, Wk[o], y[o]);
     }
+    if constexpr (ACT == ACT_TANH) {
 #pragma unroll
-    for (int o = 0; o < OUT; o++) {
-        const float v = __fadd_rn(y[o], b[o]);
-        y[o] = RELU ? (v > 0.0f ? v : 0.0f) : v;
+        for (int o = 0; o < OUT; o++) stage[o * ss] = __fadd_rn(y[o], b[o]);
+#pragma unroll 1
+        for (int o = 0; o < OUT; o++) stage[o * ss] = bppo_math::tanhf_glibc_bf(stage[o * ss]);
+#pragma unroll
+        for (int o = 0; o < OUT; o++) y[o] = stage[o * ss];
+    } else {
+#pragma unroll
+        for (int o = 0; o < OUT; o++) y[o] = act_fwd<ACT>(__fadd_rn(y[o], b[o]));
     }
 }
 
@@ -228,23 +256,33 @@ __host__ __device__ constexpr CpOffsets cp_offsets() {
     return o;
 }
 
+// dynamic LDS of the per-env forward kernels: the parameters, then (tanh) the
+// activation stage [H][threads]
 template <int H, int NL>
+__host__ __device__ constexpr int cp_stage_ofs() { return (cp_offsets<H, NL>().n + 3) & ~3; }
+template <int H, int NL>
+inline size_t cp_lds(int act, int threads) {
+    return (size_t)(cp_stage_ofs<H, NL>() + (act == ACT_TANH ? H * threads : 0)) * sizeof(float);
+}
+
+// (stage/ss: the tanh LDS stage of linear_fwd, unused for relu)
+template <int H, int NL, int ACT>
 __device__ __forceinline__ void cp_forward(const float *__restrict__ P, const float (&x)[5],
-                                           float (&lg)[2], float &v) {
+                                           float (&lg)[2], float &v, float *stage = nullptr, int ss = 0) {
     constexpr CpOffsets O = cp_offsets<H, NL>();
     float h[H];
-    linear_fwd<5, H, true>(P + O.w0, P + O.b0, x, h);
+    linear_fwd<5, H, ACT>(P + O.w0, P + O.b0, x, h, stage, ss);
     if constexpr (NL == 2) {
         float h2[H];
-        linear_fwd<H, H, true>(P + O.w1, P + O.b1, h, h2);
-        linear_fwd<H, 2, false>(P + O.wp, P + O.bp, h2, lg);
+        linear_fwd<H, H, ACT>(P + O.w1, P + O.b1, h, h2, stage, ss);
+        linear_fwd<H, 2, ACT_NONE>(P + O.wp, P + O.bp, h2, lg);
         float vv[1];
-        linear_fwd<H, 1, false>(P + O.wv, P + O.bv, h2, vv);
+        linear_fwd<H, 1, ACT_NONE>(P + O.wv, P + O.bv, h2, vv);
         v = vv[0];
     } else {
-        linear_fwd<H, 2, false>(P + O.wp, P + O.bp, h, lg);
+        linear_fwd<H, 2, ACT_NONE>(P + O.wp, P + O.bp, h, lg);
         float vv[1];
-        linear_fwd<H, 1, false>(P + O.wv, P + O.bv, h, vv);
+        linear_fwd<H, 1, ACT_NONE>(P + O.wv, P + O.bv, h, vv);
         v = vv[0];
     }
 }

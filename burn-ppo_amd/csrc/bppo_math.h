@@ -242,4 +242,155 @@ BPPO_HD float expf_glibc_tab(float x, const uint64_t *tab) {
 
 BPPO_HD float expf_glibc(float x) { return expf_glibc_tab(x, kExp2fTab); }
 
+// ---------------------------------------------------------------- tanhf ---
+// The tanh activation (mlp.rs:187-191, Burn ndarray -> f32::tanh -> tanhf).
+// glibc 2.35 tanhf/expm1f are the fdlibm single-precision routines
+// (sysdeps/ieee754/flt-32/s_tanhf.c, s_expm1f.c) with no FMA ifunc variant: pure
+// float arithmetic, every product and sum rounded on its own.  Restated from the
+// published fdlibm algorithm; a one-off run over all 2^32 non-NaN floats found
+// zero mismatches against this image's glibc, and
+// tests/test_libm_restatement.py re-checks dense and random samples.
+// expm1f for the arguments tanhf passes (finite, |x| < 44); the overflow branch
+// is kept for completeness.
+BPPO_HD float expm1f_glibc(float x) {
+    const float ln2_hi = 6.9313812256e-01f, ln2_lo = 9.0580006145e-06f, invln2 = 1.4426950216e+00f;
+    const float Q1 = -3.3333335072e-02f, Q2 = 1.5873016091e-03f, Q3 = -7.9365076090e-05f,
+                Q4 = 4.0082177293e-06f, Q5 = -2.0109921195e-07f;
+    uint32_t hx = asuint(x);
+    const uint32_t neg = hx >> 31;
+    hx &= 0x7fffffffu;
+    if (hx >= 0x4195b844u) {                        // |x| >= 27 ln2
+        if (hx >= 0x42b17218u) {                    // |x| >= 88.72
+            if (hx > 0x7f800000u) return x + x;
+            if (hx == 0x7f800000u) return neg ? -1.0f : x;
+            if (x > 8.8721679688e+01f) return INFINITY;
+        }
+        if (neg) return 1.0e-30f - 1.0f;            // -1 (inexact)
+    }
+    float hi, lo, c = 0.0f, t;
+    int32_t k;
+    if (hx > 0x3eb17218u) {                         // |x| > ln2 / 2: reduce by k ln2
+        if (hx < 0x3F851592u) {                     // and |x| < 1.5 ln2
+            if (!neg) { hi = x - ln2_hi; lo = ln2_lo; k = 1; }
+            else { hi = x + ln2_hi; lo = -ln2_lo; k = -1; }
+        } else {
+            k = (int32_t)(invln2 * x + (neg ? -0.5f : 0.5f));
+            t = (float)k;
+            hi = x - t * ln2_hi;                    // exact
+            lo = t * ln2_lo;
+        }
+        x = hi - lo;
+        c = (hi - x) - lo;
+    } else if (hx < 0x33000000u) {                  // |x| < 2^-25
+        return x;
+    } else {
+        k = 0;
+    }
+    const float hfx = 0.5f * x, hxs = x * hfx;
+    const float r1 = 1.0f + hxs * (Q1 + hxs * (Q2 + hxs * (Q3 + hxs * (Q4 + hxs * Q5))));
+    t = 3.0f - r1 * hfx;
+    float e = hxs * ((r1 - t) / (6.0f - x * t));
+    if (k == 0) return x - (x * e - hxs);
+    e = (x * (e - c) - c);
+    e -= hxs;
+    if (k == -1) return 0.5f * (x - e) - 0.5f;
+    if (k == 1) return x < -0.25f ? -2.0f * (e - (x + 0.5f)) : 1.0f + 2.0f * (x - e);
+    float y;
+    if (k <= -2 || k > 56) {                        // exp(x) - 1 ~ exp(x)
+        y = 1.0f - (e - x);
+        y = asfloat(asuint(y) + ((uint32_t)k << 23));
+        return y - 1.0f;
+    }
+    if (k < 23) {
+        t = asfloat(0x3f800000u - (0x1000000u >> k));   // 1 - 2^-k
+        y = t - (e - x);
+    } else {
+        t = asfloat((uint32_t)(0x7f - k) << 23);         // 2^-k
+        y = x - (e + t);
+        y += 1.0f;
+    }
+    return asfloat(asuint(y) + ((uint32_t)k << 23));
+}
+
+BPPO_HD float tanhf_glibc(float x) {
+    const uint32_t jx = asuint(x), ix = jx & 0x7fffffffu;
+    if (ix >= 0x7f800000u) return (jx >> 31) ? 1.0f / x - 1.0f : 1.0f / x + 1.0f;   // +-inf, NaN
+    float z;
+    if (ix < 0x41b00000u) {                          // |x| < 22
+        if (ix == 0) return x;
+        if (ix < 0x24000000u) return x * (1.0f + x); // |x| < 2^-55
+        if (ix >= 0x3f800000u) {                     // |x| >= 1
+            const float t = expm1f_glibc(2.0f * fabsf(x));
+            z = 1.0f - 2.0f / (t + 2.0f);
+        } else {
+            const float t = expm1f_glibc(-2.0f * fabsf(x));
+            z = -t / (t + 2.0f);
+        }
+    } else {
+        z = 1.0f - 1.0e-30f;                         // +-1 (inexact)
+    }
+    return (jx >> 31) ? -z : z;
+}
+
+// The same arithmetic as tanhf_glibc with every branch turned into a select
+// (each candidate is computed exactly as its branch would compute it), for
+// straight-line use inside fully unrolled per-unit loops on the device.  The
+// expm1f argument a = +-2|x| lies in (-2, 44): only the reductions k = 0, -1
+// and the general k path occur, and the result paths k <= -2 / k > 56,
+// 2 <= k < 23 and k >= 23.
+BPPO_HD float tanhf_glibc_bf(float x) {
+    const float ln2_hi = 6.9313812256e-01f, ln2_lo = 9.0580006145e-06f, invln2 = 1.4426950216e+00f;
+    const float Q1 = -3.3333335072e-02f, Q2 = 1.5873016091e-03f, Q3 = -7.9365076090e-05f,
+                Q4 = 4.0082177293e-06f, Q5 = -2.0109921195e-07f;
+    const uint32_t jx = asuint(x), ix = jx & 0x7fffffffu;
+    const float ax = asfloat(ix);
+    const bool big = ix >= 0x3f800000u;
+    const float a = big ? 2.0f * ax : -2.0f * ax;           // expm1f argument
+    const uint32_t ha = asuint(a) & 0x7fffffffu;
+    const bool aneg = !big;
+    // argument reduction
+    const bool red = ha > 0x3eb17218u, near1 = ha < 0x3F851592u;
+    const int32_t kg = (int32_t)(invln2 * a + (aneg ? -0.5f : 0.5f));
+    const float tg = (float)kg;
+    const float hi = near1 ? (aneg ? a + ln2_hi : a - ln2_hi) : a - tg * ln2_hi;
+    const float lo = near1 ? (aneg ? -ln2_lo : ln2_lo) : tg * ln2_lo;
+    const int32_t k = red ? (near1 ? (aneg ? -1 : 1) : kg) : 0;
+    const float xr_red = hi - lo;
+    const float xr = red ? xr_red : a;
+    const float c = red ? (hi - xr_red) - lo : 0.0f;
+    // primary range
+    const float hfx = 0.5f * xr, hxs = xr * hfx;
+    const float r1 = 1.0f + hxs * (Q1 + hxs * (Q2 + hxs * (Q3 + hxs * (Q4 + hxs * Q5))));
+    const float t = 3.0f - r1 * hfx;
+    const float e0 = hxs * ((r1 - t) / (6.0f - xr * t));
+    const float res_k0 = xr - (xr * e0 - hxs);
+    float e = (xr * (e0 - c) - c);
+    e -= hxs;
+    const float res_m1 = 0.5f * (xr - e) - 0.5f;
+    const uint32_t ksh = (uint32_t)k << 23;
+    const float ya = 1.0f - (e - xr);
+    const float res_a = asfloat(asuint(ya) + ksh) - 1.0f;                 // k <= -2 or k > 56
+    const int32_t kb = k < 1 ? 1 : (k > 24 ? 24 : k);                    // keep the shifts in range
+    const float yb = asfloat(0x3f800000u - (0x1000000u >> kb)) - (e - xr);
+    const float res_b = asfloat(asuint(yb) + ksh);                         // 2 <= k < 23
+    const int32_t kc = k > 126 ? 126 : (k < 0 ? 0 : k);
+    float yc = xr - (e + asfloat((uint32_t)(0x7f - kc) << 23));
+    yc += 1.0f;
+    const float res_c = asfloat(asuint(yc) + ksh);                         // k >= 23
+    float tm = k < 23 ? res_b : res_c;
+    tm = (k <= -2 || k > 56) ? res_a : tm;
+    tm = k == -1 ? res_m1 : tm;
+    tm = k == 0 ? res_k0 : tm;
+    tm = ha < 0x33000000u ? a : tm;                                        // |a| < 2^-25
+    // tanh from expm1
+    const float q = (big ? 2.0f : -tm) / (tm + 2.0f);
+    float z = big ? 1.0f - q : q;
+    z = ix >= 0x41b00000u ? 1.0f - 1.0e-30f : z;                          // |x| >= 22
+    z = (jx >> 31) ? -z : z;
+    z = ix < 0x24000000u ? x * (1.0f + x) : z;                             // |x| < 2^-55 (and +-0)
+    // +-inf already gives +-1 above; NaN -> quiet NaN (glibc: 1/x +- 1)
+    z = ix > 0x7f800000u ? x + x : z;
+    return z;
+}
+
 }  // namespace bppo_math

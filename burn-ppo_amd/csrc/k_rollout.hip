@@ -117,7 +117,7 @@ struct RolloutArgs {
     int32_t *err;
 };
 
-template <int H, int NL>
+template <int H, int NL, int ACT>
 __global__ void __launch_bounds__(256) k_cartpole_rollout(RolloutArgs a) {
     extern __shared__ __attribute__((aligned(16))) float sP[];
     constexpr CpOffsets O = cp_offsets<H, NL>();
@@ -153,7 +153,7 @@ __global__ void __launch_bounds__(256) k_cartpole_rollout(RolloutArgs a) {
         float lg[2], v;
         int zero = 0;
         asm volatile("" : "+v"(zero));   // keep weight reads inside the step loop (no LICM spill)
-        cp_forward<H, NL>(sP + zero, x, lg, v);
+        cp_forward<H, NL, ACT>(sP + zero, x, lg, v, sP + cp_stage_ofs<H, NL>() + threadIdx.x, blockDim.x);
         // Gumbel-max: words base + row*2 + {0,1}
         const uint64_t p0 = a.base_pos + row * 2;
         uint32_t blk[16];
@@ -422,7 +422,7 @@ __global__ void k_cartpole_observe(int N, const float *cp, const int32_t *steps,
 }
 
 // bootstrap (main.rs:878-896): current obs normalised with the UPDATED stats
-template <int H, int NL>
+template <int H, int NL, int ACT>
 __global__ void __launch_bounds__(256) k_cartpole_bootstrap(int N, const float *cp,
                                                             const int32_t *steps,
                                                             const float *params, const double *on,
@@ -440,11 +440,11 @@ __global__ void __launch_bounds__(256) k_cartpole_bootstrap(int N, const float *
     ObsNorm5 nz;
     nz.load(on, norm_on);
     nz.apply(raw, x);
-    cp_forward<H, NL>(sP, x, lg, v);
+    cp_forward<H, NL, ACT>(sP, x, lg, v, sP + cp_stage_ofs<H, NL>() + threadIdx.x, blockDim.x);
     last_v[e] = v;
 }
 
-template <int H, int NL>
+template <int H, int NL, int ACT>
 __global__ void __launch_bounds__(256) k_cartpole_forward_rows(int B, const float *obs,
                                                                const float *params, float *logits,
                                                                float *values) {
@@ -456,7 +456,7 @@ __global__ void __launch_bounds__(256) k_cartpole_forward_rows(int B, const floa
     if (r >= B) return;
     float x[5], lg[2], v;
     for (int d = 0; d < 5; d++) x[d] = obs[(size_t)r * 5 + d];
-    cp_forward<H, NL>(sP, x, lg, v);
+    cp_forward<H, NL, ACT>(sP, x, lg, v, sP + cp_stage_ofs<H, NL>() + threadIdx.x, blockDim.x);
     logits[(size_t)r * 2] = lg[0];
     logits[(size_t)r * 2 + 1] = lg[1];
     values[r] = v;
@@ -531,8 +531,12 @@ __global__ void k_obs_norm_final(int D, int nblk, const double *bp, double *on) 
 }
 
 // ------------------------------------------------------------- launchers ---
-#define CP_DISPATCH(H_, NL_, CALL)                                               \
-    if (h == H_ && nl == NL_) { CALL(H_, NL_); return BPPO_OK; }
+// shape x activation: relu (configs/*.toml) or tanh (config.rs:990-992 default)
+#define CP_DISPATCH(H_, NL_, CALL)                                                 \
+    if (h == H_ && nl == NL_) {                                                    \
+        if (c->cfg.relu) CALL(H_, NL_, ACT_RELU); else CALL(H_, NL_, ACT_TANH);   \
+        return BPPO_OK;                                                            \
+    }
 
 static bool cp_supported(int h, int nl) {
     return (h == 16 || h == 32 || h == 64) && (nl == 1 || nl == 2);
@@ -550,8 +554,8 @@ bppo_status launch_cartpole_reset(bppo_ctx *c) {
 bppo_status launch_cartpole_rollout(bppo_ctx *c, uint64_t base_pos, const double *, const double *,
                                     int norm_on) {
     const int h = c->cfg.hidden_size, nl = c->cfg.num_hidden;
-    if (!cp_supported(h, nl) || !c->cfg.relu) {
-        c->err = "CartPole rollout kernel supports relu MLPs with hidden in {16,32,64} x {1,2} layers";
+    if (!cp_supported(h, nl)) {
+        c->err = "CartPole rollout kernel supports MLPs with hidden in {16,32,64} x {1,2} layers";
         return BPPO_ERR_UNSUPPORTED;
     }
     RolloutArgs a;
@@ -562,7 +566,7 @@ bppo_status launch_cartpole_rollout(bppo_ctx *c, uint64_t base_pos, const double
     a.obs = c->d_obs; a.rew_raw = c->d_rew_raw; a.done = c->d_done; a.val = c->d_val;
     a.logp = c->d_logp; a.act = c->d_act; a.obs_part = c->d_obs_part; a.eps = c->d_eps;
     a.ep_count = c->d_ep_count; a.eps_cap = c->eps_cap; a.err = c->d_err;
-    if (h == 64 && nl == 2 && c->d_gumbel) {
+    if (h == 64 && nl == 2 && c->cfg.relu && c->d_gumbel) {
         // Gumbel noise for every (t, env, action) first, then the MFMA rollout
         const uint64_t count = (uint64_t)c->T * c->N * 2;
         const uint64_t blocks = ((base_pos + count + 15) >> 4) - (base_pos >> 4);
@@ -575,8 +579,7 @@ bppo_status launch_cartpole_rollout(bppo_ctx *c, uint64_t base_pos, const double
         return BPPO_OK;
     }
     dim3 grid((c->N + 255) / 256), blk(256);
-    size_t lds = c->net.n_params * sizeof(float);
-#define L(H_, NL_) hipLaunchKernelGGL((k_cartpole_rollout<H_, NL_>), grid, blk, lds, c->stream, a)
+#define L(H_, NL_, A_) hipLaunchKernelGGL((k_cartpole_rollout<H_, NL_, A_>), grid, blk, (cp_lds<H_, NL_>(A_, 256)), c->stream, a)
     CP_DISPATCH(16, 1, L) CP_DISPATCH(16, 2, L) CP_DISPATCH(32, 1, L) CP_DISPATCH(32, 2, L)
     CP_DISPATCH(64, 1, L) CP_DISPATCH(64, 2, L)
 #undef L
@@ -586,9 +589,8 @@ bppo_status launch_cartpole_rollout(bppo_ctx *c, uint64_t base_pos, const double
 bppo_status launch_bootstrap(bppo_ctx *c, const double *, const double *, int norm_on) {
     const int h = c->cfg.hidden_size, nl = c->cfg.num_hidden;
     dim3 grid((c->N + 255) / 256), blk(256);
-    size_t lds = c->net.n_params * sizeof(float);
-#define L(H_, NL_)                                                                              \
-    hipLaunchKernelGGL((k_cartpole_bootstrap<H_, NL_>), grid, blk, lds, c->stream, c->N, c->d_cp, \
+#define L(H_, NL_, A_)                                                                          \
+    hipLaunchKernelGGL((k_cartpole_bootstrap<H_, NL_, A_>), grid, blk, (cp_lds<H_, NL_>(A_, 256)), c->stream, c->N, c->d_cp, \
                        c->d_steps, c->d_params, c->d_on, norm_on, c->d_last_v)
     CP_DISPATCH(16, 1, L) CP_DISPATCH(16, 2, L) CP_DISPATCH(32, 1, L) CP_DISPATCH(32, 2, L)
     CP_DISPATCH(64, 1, L) CP_DISPATCH(64, 2, L)
@@ -600,9 +602,8 @@ bppo_status launch_forward_rows(bppo_ctx *c, const float *d_obs, int B, float *d
                                 float *d_values) {
     const int h = c->cfg.hidden_size, nl = c->cfg.num_hidden;
     dim3 grid((B + 255) / 256), blk(256);
-    size_t lds = c->net.n_params * sizeof(float);
-#define L(H_, NL_)                                                                                \
-    hipLaunchKernelGGL((k_cartpole_forward_rows<H_, NL_>), grid, blk, lds, c->stream, B, d_obs, \
+#define L(H_, NL_, A_)                                                                            \
+    hipLaunchKernelGGL((k_cartpole_forward_rows<H_, NL_, A_>), grid, blk, (cp_lds<H_, NL_>(A_, 256)), c->stream, B, d_obs, \
                        c->d_params, d_logits, d_values)
     CP_DISPATCH(16, 1, L) CP_DISPATCH(16, 2, L) CP_DISPATCH(32, 1, L) CP_DISPATCH(32, 2, L)
     CP_DISPATCH(64, 1, L) CP_DISPATCH(64, 2, L)

@@ -56,7 +56,7 @@ struct WaveStage {
     __device__ __forceinline__ static int at(int row, int col) { return row * H + (col ^ (row & (H - 1))); }
 };
 
-template <int H, int NL>
+template <int H, int NL, int ACT>
 __global__ void __launch_bounds__(256, 1) k_minibatch(MbArgs g) {
     constexpr CpOffsets O = cp_offsets<H, NL>();
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -99,13 +99,14 @@ __global__ void __launch_bounds__(256, 1) k_minibatch(MbArgs g) {
         const float An = __fdiv_rn(__fsub_rn(A, mean), denom);   // utils.rs:88
         // ---- forward (same code path as the rollout: ratio == 1 at first mb)
         float h1[H];
-        linear_fwd<5, H, true>(sP + O.w0, sP + O.b0, x, h1);
+        linear_fwd<5, H, ACT>(sP + O.w0, sP + O.b0, x, h1, S.a + lane, 64);   // tanh stage: S.a column-major
+        // relu: the backward needs only the sign bits; tanh re-reads y from LDS
         uint64_t m1 = 0, m2 = 0;
 #pragma unroll
         for (int k = 0; k < H; k++) m1 |= (h1[k] > 0.0f ? 1ull : 0ull) << k;
         float hl[H];
         if constexpr (NL == 2) {
-            linear_fwd<H, H, true>(sP + O.w1, sP + O.b1, h1, hl);
+            linear_fwd<H, H, ACT>(sP + O.w1, sP + O.b1, h1, hl, S.a + lane, 64);
         } else {
 #pragma unroll
             for (int k = 0; k < H; k++) hl[k] = h1[k];
@@ -113,8 +114,8 @@ __global__ void __launch_bounds__(256, 1) k_minibatch(MbArgs g) {
 #pragma unroll
         for (int k = 0; k < H; k++) m2 |= (hl[k] > 0.0f ? 1ull : 0ull) << k;
         float lg[2], vv[1];
-        linear_fwd<H, 2, false>(sP + O.wp, sP + O.bp, hl, lg);
-        linear_fwd<H, 1, false>(sP + O.wv, sP + O.bv, hl, vv);
+        linear_fwd<H, 2, ACT_NONE>(sP + O.wp, sP + O.bp, hl, lg);
+        linear_fwd<H, 1, ACT_NONE>(sP + O.wv, sP + O.bv, hl, vv);
         const float v = vv[0];
         // ---- loss terms (ppo.rs:1444-1487)
         float mx = lg[0] > lg[1] ? lg[0] : lg[1];
@@ -187,7 +188,9 @@ __global__ void __launch_bounds__(256, 1) k_minibatch(MbArgs g) {
             float s = __builtin_fmaf(dl0, sP[O.wp + o * 2], 0.0f);
             s = __builtin_fmaf(dl1, sP[O.wp + o * 2 + 1], s);
             s = __builtin_fmaf(dv, sP[O.wv + o], s);
-            dz[o] = ((m2 >> o) & 1ull) ? s : 0.0f;
+            // S.a still holds this lane's row of hl (0 for an absent row, whose s is 0)
+            if constexpr (ACT == ACT_RELU) dz[o] = ((m2 >> o) & 1ull) ? s : 0.0f;
+            else dz[o] = act_bwd<ACT>(s, S.a[WaveStage<H>::at(lane, o)]);
         }
         __builtin_amdgcn_wave_barrier();
         float dz1[H];
@@ -207,7 +210,7 @@ __global__ void __launch_bounds__(256, 1) k_minibatch(MbArgs g) {
                     for (int k = 0; k < H; k++) gW1[k] = __builtin_fmaf(S.a[WaveStage<H>::at(rr, k)], dzo, gW1[k]);
                 }
             }
-            // dh1 = dz2 W1^T, dz1 = dh1 * relu'(h1)
+            // dh1 = dz2 W1^T, dz1 = dh1 * act'(h1) (S.a holds h1 now)
             float prev = 0.0f;
 #pragma unroll
             for (int k = 0; k < H; k++) {
@@ -217,7 +220,8 @@ __global__ void __launch_bounds__(256, 1) k_minibatch(MbArgs g) {
                 float s = 0.0f;
 #pragma unroll
                 for (int o = 0; o < H; o++) s = __builtin_fmaf(dz[o], Wk[o], s);
-                dz1[k] = ((m1 >> k) & 1ull) ? s : 0.0f;
+                if constexpr (ACT == ACT_RELU) dz1[k] = ((m1 >> k) & 1ull) ? s : 0.0f;
+                else dz1[k] = act_bwd<ACT>(s, S.a[WaveStage<H>::at(lane, k)]);
                 prev = s;
             }
             __builtin_amdgcn_wave_barrier();
@@ -1222,7 +1226,10 @@ bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_
     if (h == H_ && nl == NL_) {                                                                     \
         size_t lds = params_bytes + 4 * sizeof(WaveStage<H_>);                                      \
         c->slab_used = blocks * 4;                                                                  \
-        hipLaunchKernelGGL((k_minibatch<H_, NL_>), dim3(blocks), dim3(256), lds, c->stream, g);    \
+        if (c->cfg.relu)                                                                            \
+            hipLaunchKernelGGL((k_minibatch<H_, NL_, ACT_RELU>), dim3(blocks), dim3(256), lds, c->stream, g); \
+        else                                                                                        \
+            hipLaunchKernelGGL((k_minibatch<H_, NL_, ACT_TANH>), dim3(blocks), dim3(256), lds, c->stream, g); \
     } else
     L(16, 1) L(16, 2) L(32, 1) L(32, 2) L(64, 1) L(64, 2) {
         c->err = "minibatch kernel: unsupported MLP shape";

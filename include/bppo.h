@@ -172,7 +172,7 @@ bppo_status bppo_gae_mp_device(const float *all_rewards, const int32_t *players,
 /* device timing of the last call of each phase kernel (ms), for bench.py's roofline */
 bppo_status bppo_last_kernel_ms(bppo_ctx *ctx, const char *kernel, float *ms);
 
-/* libm parity hook: which 0 = logf, 1 = sinf, 2 = cosf, 3 = gumbel(-ln(-ln u));
+/* libm parity hook: which 0 = logf, 1 = sinf, 2 = cosf, 3 = gumbel(-ln(-ln u)), 4 = expf, 5 = tanhf;
  * device = 0 runs the host build of the same source, 1 runs the HIP kernel */
 bppo_status bppo_debug_libm(int32_t which, int32_t device, const float *x, float *y, size_t n);
 

@@ -30,6 +30,15 @@ size_t mismatch_sincos(const float *x, size_t n, float *rs, float *gs, float *rc
     }
     return bad;
 }
+size_t mismatch_tanhf(const float *x, size_t n, float *ref, float *got) {
+    size_t bad = 0;
+    for (size_t i = 0; i < n; i++) {
+        ref[i] = tanhf(x[i]); got[i] = bppo_math::tanhf_glibc(x[i]);
+        bad += bppo_math::asuint(ref[i]) != bppo_math::asuint(got[i]);
+        bad += bppo_math::asuint(ref[i]) != bppo_math::asuint(bppo_math::tanhf_glibc_bf(x[i]));   // device form
+    }
+    return bad;
+}
 // every Gumbel draw of utils.rs:20-25: u = gen_range(1e-10f32..1.0) from word w,
 // g = -ln(-ln(u)); k = w >> 9 indexes all 2^23 distinct u.
 size_t mismatch_gumbel_all(void) {

@@ -23,7 +23,7 @@ def _torch():
 
 
 # ----------------------------------------------------------------- libm ---
-@pytest.mark.parametrize("which", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("which", [0, 1, 2, 3, 4, 5])
 def test_device_libm_matches_host(which):
     rng = np.random.default_rng(which)
     if which == 3:   # every Gumbel input u
@@ -34,6 +34,9 @@ def test_device_libm_matches_host(which):
         x = np.concatenate([rng.uniform(-0.5, 0.5, 2_000_000), rng.uniform(-200, 200, 500_000)]).astype(np.float32)
     elif which == 4:
         x = rng.uniform(-100, 20, 2_000_000).astype(np.float32)
+    elif which == 5:   # every 16th float with |x| < 22, both signs
+        lo = np.arange(0, np.float32(22.0).view(np.uint32), 16, dtype=np.uint32).view(np.float32)
+        x = np.concatenate([lo, -lo])
     else:
         x = rng.integers(0, 0x7F800000, 2_000_000, dtype=np.uint32).view(np.float32)
     yh = np.zeros_like(x)
@@ -135,6 +138,7 @@ def _pair(N, T, seed=42, **kw):
     tr = bppo.Trainer(cfg, params=params)
     ocfg = O.train_cfg(num_envs=N, num_steps=T, seed=seed, lr=1e-3,
                        hidden=cfg["hidden_size"], num_hidden=cfg["num_hidden"],
+                       relu=cfg["activation"] == "relu",
                        num_epochs=cfg["num_epochs"], num_minibatches=cfg["num_minibatches"])
     ot = O.Trainer(ocfg, params)
     return cfg, tr, ot
@@ -242,3 +246,54 @@ def test_training_improves_cartpole_return():
         rets.append(m["mean_return"])
     tr.close()
     assert rets[-1] > 3 * max(rets[0], 10.0), rets
+
+
+# ------------------------------------------------------ tanh activation ---
+# config.rs:990-992 default activation (every shipped config says relu):
+# mlp.rs:187-191 tanh through glibc tanhf, restated bit-exactly on the device
+TANH_NETS = [(64, 2), (32, 1), (16, 2)]
+
+
+@pytest.mark.parametrize("H,NL", TANH_NETS)
+def test_tanh_first_rollout_bit_exact(H, NL):
+    cfg, tr, ot = _pair(64, 32, activation="tanh", hidden_size=H, num_hidden=NL)
+    bppo.collect_rollouts(tr.ctx); ot.collect()
+    _cmp_rollout(tr, ot)
+    tr.close(); ot.close()
+
+
+@pytest.mark.parametrize("H,NL", TANH_NETS)
+def test_tanh_update_matches_oracle(H, NL):
+    cfg, tr, ot = _pair(64, 32, activation="tanh", hidden_size=H, num_hidden=NL,
+                        num_minibatches=4, num_epochs=2)
+    bppo.collect_rollouts(tr.ctx); ot.collect()
+    bppo.compute_gae(tr.ctx); ot.gae()
+    tr.ctx.set_buffer("advantages", ot.buffer("advantages"))
+    tr.ctx.set_buffer("returns", ot.buffer("returns"))
+    m = bppo.ppo_update(tr.ctx, 1e-3, 0.01)
+    om = ot.update()
+    assert tr.ctx.rng_pos() == ot.rng_pos()
+    for k in ("policy_loss", "value_loss", "entropy", "approx_kl", "clip_fraction"):
+        assert abs(m[k] - om[k]) <= 1e-5 + 1e-4 * abs(om[k]), (k, m[k], om[k])
+    np.testing.assert_allclose(tr.model.get_params(), ot.params(), rtol=1e-4, atol=2e-5)
+    tr.close(); ot.close()
+
+
+def test_tanh_second_rollout_and_forward_rows_bit_exact():
+    N, T = 128, 32
+    cfg, tr, ot = _pair(N, T, activation="tanh")
+    bppo.collect_rollouts(tr.ctx); ot.collect()
+    bppo.compute_gae(tr.ctx); ot.gae()
+    bppo.ppo_update(tr.ctx, 1e-3, 0.01); ot.update()
+    tr.model.set_params(ot.params())
+    m, v, c = ot.obs_norm_state(5)
+    tr.ctx.set_obs_norm(m, v, c)
+    tr.ctx.set_ret_norm(ot.ret_norm_state(), tr.ctx.ret_norm()[1])
+    bppo.collect_rollouts(tr.ctx); ot.collect()
+    _cmp_rollout(tr, ot)
+    # the batched forward entry on the rollout's own observations reproduces
+    # the values the rollout stored
+    obs = tr.buffer.observations.reshape(-1, 5)
+    lg, vals = tr.model.forward(obs)
+    assert np.array_equal(vals.reshape(-1).view(np.uint32), ot.buffer("values").view(np.uint32))
+    tr.close(); ot.close()

@@ -28,6 +28,8 @@ def chk(tmp_path_factory):
     L.mismatch_expf.argtypes = [f32, C.c_size_t, f32, f32]
     L.mismatch_sincos.restype = C.c_size_t
     L.mismatch_sincos.argtypes = [f32, C.c_size_t, f32, f32, f32, f32]
+    L.mismatch_tanhf.restype = C.c_size_t
+    L.mismatch_tanhf.argtypes = [f32, C.c_size_t, f32, f32]
     L.mismatch_gumbel_all.restype = C.c_size_t
     return L
 
@@ -89,3 +91,20 @@ def test_expf_samples(chk):
     dense = np.linspace(-30, 0, 1_000_001, dtype=np.float32)
     r = np.empty_like(dense); g = np.empty_like(dense)
     assert chk.mismatch_expf(dense, dense.size, r, g) == 0
+
+
+def test_tanhf_samples(chk):
+    """tanh activation (mlp.rs:187-191): every 7th float with |x| < 22 (both
+    signs, every expm1f branch), random bit patterns, and the specials."""
+    lo = np.arange(0, np.float32(22.0).view(np.uint32), 7, dtype=np.uint32).view(np.float32)
+    for x in (lo, -lo):
+        xs = np.ascontiguousarray(x); r = np.empty_like(xs); g = np.empty_like(xs)
+        assert chk.mismatch_tanhf(xs, xs.size, r, g) == 0
+    rng = np.random.default_rng(3)
+    x = rng.integers(0, 2**32, size=2_000_000, dtype=np.uint64).astype(np.uint32).view(np.float32)
+    x = np.ascontiguousarray(x[~np.isnan(x)])
+    r = np.empty_like(x); g = np.empty_like(x)
+    assert chk.mismatch_tanhf(x, x.size, r, g) == 0
+    sp = np.array([0.0, -0.0, np.inf, -np.inf, 1e-45, -1e-40, 2.0**-56, 22.0, -22.0, 1.0, -1.0], np.float32)
+    r = np.empty_like(sp); g = np.empty_like(sp)
+    assert chk.mismatch_tanhf(sp, sp.size, r, g) == 0
