@@ -9,12 +9,14 @@ constexpr int GEMM_MAX_SPLITS = 256;
 // Y = act(X W + b): X [M][K] (ldx), W [K][N] (ldw), bias [N]; columns [0, n0)
 // go to out0 (ld0), [n0, N) to out1 (ld1) when out1 != nullptr.  Bit-exact
 // with matrixmultiply's KC=256 k-ordered fma chains (see k_gemm.hip).
+// act: 0 none, 1 relu, 2 tanh (glibc tanhf, bit-exact).
 hipError_t gemm_fwd(hipStream_t st, int M, int N, int K, const float *X, int ldx, const float *W,
-                    int ldw, const float *bias, int relu, float *out0, int ld0, int n0, float *out1,
+                    int ldw, const float *bias, int act, float *out0, int ld0, int n0, float *out1,
                     int ld1);
-// out = (dZ W^T) masked by H > 0 (H may be null): dZ [M][K] (ldz), W [N][K] (ldw)
+// out = (dZ W^T) * act'(H) given the layer OUTPUT H (may be null: no factor):
+// act 2 tanh -> (1 - H^2), otherwise relu -> [H > 0].  dZ [M][K] (ldz), W [N][K] (ldw)
 hipError_t gemm_dx(hipStream_t st, int M, int N, int K, const float *dZ, int ldz, const float *W,
-                   int ldw, const float *H, int ldh, float *out, int ldo);
+                   int ldw, const float *H, int ldh, int act, float *out, int ldo);
 // dW = X^T dZ over `rows` rows: X [rows][Kin] (ldx), dZ [rows][N] (ldz).
 // Columns [0, n0) -> dW0 [Kin][ldw0], [n0, N) -> dW1 [Kin][ldw1] (when dW1);
 // bias gradient (column sums of dZ) -> db0 / db1 likewise (either may be null).

@@ -20,6 +20,7 @@
 // next stage prefetched into registers while the MFMAs of the current run.
 #include "bppo_internal.h"
 #include "bppo_gemm.h"
+#include <algorithm>
 
 namespace bppo {
 
@@ -74,11 +75,12 @@ struct GemmArgs {
     const float *B; int ldb;
     int M, N, K;                 // C is M x N, reduction K
     // FWD epilogue
-    const float *bias; int act;  // act: 1 relu, 0 none
+    const float *bias; int act;  // act: 1 relu, 0 none (tanh: none here + k_tanh_inplace)
     float *out0; int ld0; int n0;   // cols [0, n0) -> out0[row*ld0 + col]
     float *out1; int ld1;           // cols [n0, N) -> out1[row*ld1 + col - n0]
-    // DX epilogue: relu mask from H [M][ldh] (nullptr: no mask)
-    const float *H; int ldh;
+    // DX epilogue: activation derivative from the layer output H [M][ldh]
+    // (nullptr: none): dact 1 relu mask [H > 0], 2 tanh (1 - H^2)
+    const float *H; int ldh; int dact;
     // WG: partial slab [split][M][N] and column sums [split][N]; rows of the
     // reduction per split
     float *part; float *colsum; int k_per_split;
@@ -197,7 +199,11 @@ __global__ void __launch_bounds__(256, 2) k_gemm(GemmArgs g) {
                     if (col < g.n0) g.out0[(size_t)row * g.ld0 + col] = v;
                     else g.out1[(size_t)row * g.ld1 + (col - g.n0)] = v;
                 } else if constexpr (MODE == GEMM_DX) {
-                    if (g.H && !(g.H[(size_t)row * g.ldh + col] > 0.0f)) v = 0.0f;
+                    if (g.H) {
+                        const float hv = g.H[(size_t)row * g.ldh + col];
+                        if (g.dact == 2) v = __fmul_rn(v, __fsub_rn(1.0f, __fmul_rn(hv, hv)));
+                        else if (!(hv > 0.0f)) v = 0.0f;
+                    }
                     g.out0[(size_t)row * g.ld0 + col] = v;
                 } else {
                     g.part[((size_t)blockIdx.z * g.M + row) * g.N + col] = v;
@@ -230,6 +236,25 @@ __global__ void k_split_reduce(const float *__restrict__ part, int splits, int M
     else out1[(size_t)r * ld1 + (c - n0)] = (float)s;
 }
 
+// tanh activation of a FWD output block [M][cols] (ld), in place: the
+// elementwise pass after the GEMM (mlp.rs:187-191 -> glibc tanhf, restated
+// bit-exactly in bppo_math.h).  HBM-bound: 8 B per element.
+__global__ void __launch_bounds__(256) k_tanh_inplace(float *__restrict__ y, int M, int cols, int ld) {
+    const size_t n = (size_t)M * cols;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = i / cols, c = i % cols;
+        float *p = y + r * ld + c;
+        *p = bppo_math::tanhf_glibc_bf(*p);
+    }
+}
+static hipError_t tanh_inplace(hipStream_t st, float *y, int M, int cols, int ld) {
+    if (M <= 0 || cols <= 0) return hipSuccess;
+    const size_t n = (size_t)M * cols;
+    const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_tanh_inplace, dim3(blocks), dim3(256), 0, st, y, M, cols, ld);
+    return hipGetLastError();
+}
+
 // -------------------------------------------------------------- launchers --
 template <int MODE, int BM, int BN, int WM, int WN>
 static hipError_t launch(const GemmArgs &g, int splits, hipStream_t st) {
@@ -246,22 +271,25 @@ static hipError_t launch_by_width(const GemmArgs &g, int splits, hipStream_t st)
 }
 
 hipError_t gemm_fwd(hipStream_t st, int M, int N, int K, const float *X, int ldx, const float *W,
-                    int ldw, const float *bias, int relu, float *out0, int ld0, int n0, float *out1,
+                    int ldw, const float *bias, int act, float *out0, int ld0, int n0, float *out1,
                     int ld1) {
     if (M <= 0 || N <= 0) return hipSuccess;
     GemmArgs g{};
     g.A = X; g.lda = ldx; g.B = W; g.ldb = ldw; g.M = M; g.N = N; g.K = K;
-    g.bias = bias; g.act = relu ? 1 : 0;
+    g.bias = bias; g.act = act == 1 ? 1 : 0;
     g.out0 = out0; g.ld0 = ld0; g.n0 = out1 ? n0 : N; g.out1 = out1; g.ld1 = ld1;
-    return launch_by_width<GEMM_FWD>(g, 1, st);
+    hipError_t e = launch_by_width<GEMM_FWD>(g, 1, st);
+    if (e != hipSuccess || act != 2) return e;
+    if ((e = tanh_inplace(st, out0, M, g.n0, ld0)) != hipSuccess) return e;
+    return out1 ? tanh_inplace(st, out1, M, N - g.n0, ld1) : hipSuccess;
 }
 
 hipError_t gemm_dx(hipStream_t st, int M, int N, int K, const float *dZ, int ldz, const float *W,
-                   int ldw, const float *H, int ldh, float *out, int ldo) {
+                   int ldw, const float *H, int ldh, int act, float *out, int ldo) {
     if (M <= 0 || N <= 0) return hipSuccess;
     GemmArgs g{};
     g.A = dZ; g.lda = ldz; g.B = W; g.ldb = ldw; g.M = M; g.N = N; g.K = K;
-    g.H = H; g.ldh = ldh; g.out0 = out; g.ld0 = ldo; g.n0 = N;
+    g.H = H; g.ldh = ldh; g.dact = act == 2 ? 2 : 1; g.out0 = out; g.ld0 = ldo; g.n0 = N;
     return launch_by_width<GEMM_DX>(g, 1, st);
 }
 
@@ -303,10 +331,11 @@ hipError_t gemm_wgrad(hipStream_t st, int Kin, int N, int rows, const float *X, 
 }  // namespace bppo
 
 // ------------------------------------------------------------ parity hook ---
-// bppo_debug_gemm: host buffers in/out; mode 0 FWD (bias, relu), 1 DX (H mask
-// optional), 2 WG (out = [Kin][N] weight grad, out2 = [N] bias grad).
+// bppo_debug_gemm: host buffers in/out; mode 0 FWD (bias, act 0 none / 1 relu /
+// 2 tanh), 1 DX (H optional: act 2 tanh derivative, else relu mask), 2 WG
+// (out = [Kin][N] weight grad, out2 = [N] bias grad).
 extern "C" bppo_status bppo_debug_gemm(int32_t mode, int32_t M, int32_t N, int32_t K, const float *A,
-                                       const float *B, const float *bias_or_H, int32_t relu, float *out,
+                                       const float *B, const float *bias_or_H, int32_t act, float *out,
                                        float *out2) {
     using namespace bppo;
     if (!A || !B || !out || M <= 0 || N <= 0 || K <= 0 || mode < 0 || mode > 2) return BPPO_ERR_ARG;
@@ -328,9 +357,9 @@ extern "C" bppo_status bppo_debug_gemm(int32_t mode, int32_t M, int32_t N, int32
         hipError_t e;
         if (mode == 0) {
             if (!dX) break;
-            e = gemm_fwd(nullptr, M, N, K, dA, K, dB, N, dX, relu, dO, N, N, nullptr, 0);
+            e = gemm_fwd(nullptr, M, N, K, dA, K, dB, N, dX, act, dO, N, N, nullptr, 0);
         } else if (mode == 1) {
-            e = gemm_dx(nullptr, M, N, K, dA, K, dB, K, dX, N, dO, N);
+            e = gemm_dx(nullptr, M, N, K, dA, K, dB, K, dX, N, act, dO, N);
         } else {
             if (hipMalloc((void **)&dO2, (size_t)N * 4) != hipSuccess) break;
             if (hipMalloc((void **)&dP, (size_t)splits * M * N * 4) != hipSuccess) break;

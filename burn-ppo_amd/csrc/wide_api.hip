@@ -45,7 +45,6 @@ static bool is_hidden(const NetLayout &n, int l) {
 
 bppo_status wide_init(bppo_ctx *c) {
     const bppo_config &cfg = c->cfg;
-    if (!cfg.relu) { c->err = "wide path: only relu activations are implemented"; return BPPO_ERR_UNSUPPORTED; }
     if (cfg.normalize_obs || cfg.normalize_returns) {
         c->err = "wide path: obs/return normalisation not implemented for multi-player envs "
                  "(the reference default for them is off)";
@@ -134,7 +133,7 @@ bppo_status wide_forward(bppo_ctx *c, int rows, const float *xc, int ldxc, float
     int ldx = ldxc;
     for (int l = 0; l < n.n_actor_hidden; l++) {
         float *h = c->d_hbuf + c->hoff[l];
-        WHIP(c, gemm_fwd(c->stream, rows, n.out[l], n.in[l], x, ldx, P + n.w[l], n.out[l], P + n.b[l], 1, h,
+        WHIP(c, gemm_fwd(c->stream, rows, n.out[l], n.in[l], x, ldx, P + n.w[l], n.out[l], P + n.b[l], c->cfg.relu ? 1 : 2, h,
                          n.out[l], n.out[l], nullptr, 0));
         x = h; ldx = n.out[l];
     }
@@ -150,7 +149,7 @@ bppo_status wide_forward(bppo_ctx *c, int rows, const float *xc, int ldxc, float
     int ldq = ldxc;
     for (int l = n.critic_first; l < n.value; l++) {
         float *h = c->d_hbuf + c->hoff[l];
-        WHIP(c, gemm_fwd(c->stream, rows, n.out[l], n.in[l], xq, ldq, P + n.w[l], n.out[l], P + n.b[l], 1, h,
+        WHIP(c, gemm_fwd(c->stream, rows, n.out[l], n.in[l], xq, ldq, P + n.w[l], n.out[l], P + n.b[l], c->cfg.relu ? 1 : 2, h,
                          n.out[l], n.out[l], nullptr, 0));
         xq = h; ldq = n.out[l];
     }
@@ -204,6 +203,7 @@ bppo_status wide_bootstrap_gae(bppo_ctx *c) {
 // metrics -> d_grad[np, np + WM_COUNT)
 bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, float ent_coef) {
     const NetLayout &n = c->net;
+    const int hact = c->cfg.relu ? 1 : 2;   // hidden activation derivative in the DX epilogues
     const int A = c->A, L = c->L, rows = (int)mb;
     const float *P = c->d_params;
     float *G = c->d_grad;
@@ -235,7 +235,7 @@ bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, float ent_c
                        G + n.b[l], nullptr));
             if (l > first) {
                 WHIP(c, gemm_dx(c->stream, rows, n.in[l], n.out[l], dz, n.out[l], P + n.w[l], n.out[l],
-                                c->d_hbuf + c->hoff[l - 1], n.out[l - 1], dz2, n.in[l]));
+                                c->d_hbuf + c->hoff[l - 1], n.out[l - 1], hact, dz2, n.in[l]));
                 std::swap(dz, dz2);
             }
         }
@@ -248,13 +248,13 @@ bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, float ent_c
         // heads: dW = H^T [dlogits | dv] split into policy / value tensors
         WTRY(wgrad(Wa, A + 1, Ha, Wa, c->d_dout, A + 1, G + n.w[n.policy], A, A, G + n.w[n.value], 1,
                    G + n.b[n.policy], G + n.b[n.value]));
-        WHIP(c, gemm_dx(c->stream, rows, Wa, A + 1, c->d_dout, A + 1, c->d_heads, A + 1, Ha, Wa, dz, Wa));
+        WHIP(c, gemm_dx(c->stream, rows, Wa, A + 1, c->d_dout, A + 1, c->d_heads, A + 1, Ha, Wa, hact, dz, Wa));
         WTRY(hidden_chain(0, la, c->d_xcg + c->G, L));
         return BPPO_OK;
     }
     // CTDE actor
     WTRY(wgrad(Wa, A, Ha, Wa, c->d_dout, A + 1, G + n.w[n.policy], A, A, nullptr, 0, G + n.b[n.policy], nullptr));
-    WHIP(c, gemm_dx(c->stream, rows, Wa, A, c->d_dout, A + 1, P + n.w[n.policy], A, Ha, Wa, dz, Wa));
+    WHIP(c, gemm_dx(c->stream, rows, Wa, A, c->d_dout, A + 1, P + n.w[n.policy], A, Ha, Wa, hact, dz, Wa));
     WTRY(hidden_chain(0, la, c->d_xcg + c->G, L));
     // CTDE critic
     const int lc = n.value - 1;
@@ -262,7 +262,7 @@ bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, float ent_c
     const int Wc = n.out[lc];
     dz = c->d_dz[0]; dz2 = c->d_dz[1];
     WTRY(wgrad(Wc, 1, Hc, Wc, c->d_dout + A, A + 1, G + n.w[n.value], 1, 1, nullptr, 0, G + n.b[n.value], nullptr));
-    WHIP(c, gemm_dx(c->stream, rows, Wc, 1, c->d_dout + A, A + 1, P + n.w[n.value], 1, Hc, Wc, dz, Wc));
+    WHIP(c, gemm_dx(c->stream, rows, Wc, 1, c->d_dout + A, A + 1, P + n.w[n.value], 1, Hc, Wc, hact, dz, Wc));
     WTRY(hidden_chain(n.critic_first, lc, c->d_xcg, L));
     return BPPO_OK;
 }

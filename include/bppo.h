@@ -194,10 +194,11 @@ bppo_status bppo_debug_shuffle_engine(uint64_t seed, uint64_t stream, uint64_t s
 
 /* GEMM engine parity hook (host buffers).  mode 0: out[M][N] = act(A[M][K] B[K][N] + bias[N])
  * with matrixmultiply's KC=256 fma-chain order (Burn Linear forward, mlp.rs:140-206);
- * mode 1: out[M][N] = (A[M][K] B[N][K]^T) * [H[M][N] > 0] (H = bias_or_H, may be NULL);
+ * (act: 0 none, 1 relu, 2 tanh); mode 1: out[M][N] = (A[M][K] B[N][K]^T) * act'(H) with H = bias_or_H
+ * the layer output (may be NULL): act 2 -> (1 - H^2), otherwise [H > 0];
  * mode 2: out[M][N] = A[K][M]^T B[K][N] (weight gradient), out2[N] = column sums of B */
 bppo_status bppo_debug_gemm(int32_t mode, int32_t M, int32_t N, int32_t K, const float *A, const float *B,
-                            const float *bias_or_H, int32_t relu, float *out, float *out2);
+                            const float *bias_or_H, int32_t act, float *out, float *out2);
 
 #ifdef __cplusplus
 }

@@ -44,6 +44,31 @@ def test_gemm_forward_bit_exact(M, N, K, relu):
     assert np.array_equal(y, y_ref), f"max |diff| {np.abs(y - y_ref).max()}"
 
 
+@pytest.mark.parametrize("M,N,K", [(257, 512, 86), (300, 512, 512), (33, 130, 600)])
+def test_gemm_forward_tanh_bit_exact(M, N, K):
+    """tanh hidden layers (config.rs:990-992 default): GEMM + elementwise glibc tanhf"""
+    rng = np.random.default_rng(M + 5 * N + K)
+    X = rng.standard_normal((M, K)).astype(np.float32)
+    W = (rng.standard_normal((K, N)) / np.sqrt(K) * 2.0).astype(np.float32)
+    b = rng.standard_normal(N).astype(np.float32) * 0.1
+    y_ref = O.linear(X, W, b, 0)          # oracle act 0 = tanhf
+    y, _ = _gemm(0, M, N, K, X, W, b, relu=2)
+    assert np.array_equal(y.view(np.uint32), y_ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 512, 512), (129, 86, 8)])
+def test_gemm_dx_tanh(M, N, K):
+    rng = np.random.default_rng(M + N + K + 1)
+    dZ = rng.standard_normal((M, K)).astype(np.float32)
+    W = rng.standard_normal((N, K)).astype(np.float32)
+    H = np.tanh(rng.standard_normal((M, N))).astype(np.float32)
+    g = (dZ.astype(np.float64) @ W.astype(np.float64).T)
+    mag = np.abs(dZ.astype(np.float64)) @ np.abs(W.astype(np.float64)).T
+    ref = g * (1.0 - H.astype(np.float64) ** 2)
+    out, _ = _gemm(1, M, N, K, dZ, W, H, relu=2)
+    assert np.all(np.abs(out - ref) <= 2e-5 * mag + 1e-30)
+
+
 @pytest.mark.parametrize("M,N,K", [(300, 512, 512), (257, 86, 512), (100, 256, 49), (70, 512, 1),
                                    (129, 512, 8)])
 def test_gemm_dx(M, N, K):

@@ -82,7 +82,7 @@ def _pair(env, N, T, seed=42, ctde=None, **kw):
     tr = bppo.Trainer(cfg, params=params)
     is_ctde = cfg["network_type"] == "ctde"
     ocfg = O.train_cfg(env_kind=kind, num_envs=N, num_steps=T, seed=seed, hidden=cfg["hidden_size"],
-                       num_hidden=cfg["num_hidden"], ctde=is_ctde,
+                       num_hidden=cfg["num_hidden"], ctde=is_ctde, relu=cfg["activation"] == "relu",
                        critic_hidden=cfg["critic_hidden_size"] or 0,
                        critic_num_hidden=cfg["critic_num_hidden"] or 0, normalize_obs=False,
                        normalize_returns=False, gamma=cfg["gamma"], gae_lambda=cfg["gae_lambda"],
@@ -169,3 +169,27 @@ def test_forward_matches_oracle_ctde():
     assert np.array_equal(_bits(lg), _bits(lo))
     assert np.array_equal(_bits(v.reshape(-1)), _bits(vo))
     tr.close()
+
+
+# tanh hidden layers (config.rs:990-992 default) on the GEMM path: the rollout
+# stays bit-exact, the update within the same tolerance as relu
+TANH_CASES = [("connect_four", 64, 12, None), ("liars_dice", 40, 10, None)]
+
+
+@pytest.mark.parametrize("env,N,T,ctde", TANH_CASES)
+def test_tanh_rollout_update_second_rollout(env, N, T, ctde):
+    cfg, tr, ot = _pair(env, N, T, ctde=ctde, activation="tanh")
+    bppo.collect_rollouts(tr.ctx); ot.collect()
+    _cmp_rollout(env, tr, ot)
+    bppo.compute_gae(tr.ctx); ot.gae()
+    assert np.array_equal(_bits(tr.buffer.advantages.reshape(-1)), _bits(ot.buffer("advantages")))
+    m = bppo.ppo_update(tr.ctx, bppo.schedule_get(cfg["learning_rate"], 0), bppo.schedule_get(cfg["entropy_coef"], 0))
+    om = ot.update()
+    assert m["epochs_run"] == om["epochs_run"]
+    for k in ("policy_loss", "value_loss", "entropy", "approx_kl", "clip_fraction"):
+        assert abs(m[k] - om[k]) <= 2e-5 + 1e-4 * abs(om[k]), (k, m[k], om[k])
+    np.testing.assert_allclose(tr.model.get_params(), ot.params(), rtol=1e-4, atol=2e-5)
+    tr.model.set_params(ot.params())
+    bppo.collect_rollouts(tr.ctx); ot.collect()
+    _cmp_rollout(env, tr, ot)
+    tr.close(); ot.close()
