@@ -95,12 +95,15 @@ class Context:
         self._chk(L.lib().bppo_obs_norm_set(self.h, mean.ctypes.data, m2.ctypes.data, float(count)))
 
     def ret_norm(self):
-        mvc = np.zeros(3); r = np.zeros(self.N)
+        """-> ([mean, M2, count], rolling returns [N * num_players]) (normalization.rs:121-134)"""
+        mvc = np.zeros(3); r = np.zeros(self.N * self.num_players)
         self._chk(L.lib().bppo_ret_norm_get(self.h, mvc.ctypes.data, r.ctypes.data))
         return mvc, r
 
     def set_ret_norm(self, mvc, returns):
         mvc = np.ascontiguousarray(mvc, np.float64); r = np.ascontiguousarray(returns, np.float64)
+        if r.size != self.N * self.num_players:
+            raise ValueError(f"returns must hold num_envs * num_players = {self.N * self.num_players} values")
         self._chk(L.lib().bppo_ret_norm_set(self.h, mvc.ctypes.data, r.ctypes.data))
 
     def kernel_ms(self, name):

@@ -146,7 +146,7 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     TRY(dalloc(c, &c->d_adv, TN));
     TRY(dalloc(c, &c->d_ret, TN));
     TRY(dalloc(c, &c->d_act, TN));
-    if (!c->wide) TRY(dalloc(c, &c->d_X, TN));
+    if (!c->wide || cfg->normalize_returns) TRY(dalloc(c, &c->d_X, TN));
     if (!c->wide && cfg->hidden_size == 64 && cfg->num_hidden == 2 && cfg->relu && !getenv("BPPO_VALU_ROLLOUT"))
         TRY(dalloc(c, &c->d_gumbel, TN * 2));
     TRY(dalloc(c, &c->d_on, (size_t)2 * c->D + 1));

@@ -238,6 +238,9 @@ struct bppo_ctx {
     int rows_max = 0;                 // max(N, largest minibatch): rows of the activation buffers
     void *d_wstate = nullptr;         // per-env state structs [N]
     float *d_xc = nullptr;            // rollout rows [T][N][L]
+    float *d_obs_raw = nullptr;       // normalize_obs: raw obs rows [T][N][D] for the stats update
+    double *d_obsw_part = nullptr;    // normalize_obs: per-chunk partial stats [256][D][3]
+    size_t obsw_part_n = 0;
     uint8_t *d_mask = nullptr;        // action masks [T][N][A] (0/1)
     int32_t *d_players = nullptr;     // acting player [T][N]
     float *d_allr = nullptr;          // all_rewards [T][N][P]
@@ -279,6 +282,7 @@ bppo_status launch_cartpole_vecenv_step(bppo_ctx *c, const int32_t *d_actions, f
                                         uint8_t *d_done, float *d_obs_out);
 bppo_status launch_cartpole_observe(bppo_ctx *c, float *d_obs_out);
 bppo_status launch_obs_norm_merge(bppo_ctx *c);
+bppo_status launch_obs_norm_rows(bppo_ctx *c, int rows, float *x, int ld, float *raw);
 bppo_status launch_bootstrap(bppo_ctx *c, const double *mean, const double *sd, int norm_on);
 bppo_status launch_forward_rows(bppo_ctx *c, const float *d_obs, int B, float *d_logits,
                                 float *d_values);

@@ -13,6 +13,7 @@
 // rolling return per (env) is a per-env scan; its Welford statistics are a
 // global inclusive scan in (t, e) order, done here as a Chan-merge scan in f64.
 #include "bppo_internal.h"
+#include <algorithm>
 
 namespace bppo {
 
@@ -168,6 +169,37 @@ __global__ void k_rn_returns(int T, int N, double gamma, const float *rew_raw, c
     returns_state[e] = x;
 }
 
+// multi-player (ppo.rs:388-408): one rolling return per (env, player), updated
+// and pushed for the ACTING player only (normalization.rs:163-186), reset for
+// that player when the step ends the episode.  X in (t, e) order as above.
+__global__ void k_rn_returns_mp(int T, int N, int P, double gamma, const float *rew_raw, const float *done,
+                                const int32_t *players, double *returns_state, double *X) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= N) return;
+    double R0 = returns_state[(size_t)e * P], R1 = P > 1 ? returns_state[(size_t)e * P + 1] : 0.0;
+    double R2 = P > 2 ? returns_state[(size_t)e * P + 2] : 0.0, R3 = P > 3 ? returns_state[(size_t)e * P + 3] : 0.0;
+    for (int t = 0; t < T; t++) {
+        const size_t i = (size_t)t * N + e;
+        const int p = players[i];
+        double x = p == 0 ? R0 : p == 1 ? R1 : p == 2 ? R2 : R3;
+        x = x * gamma + (double)rew_raw[i];
+        X[i] = x;
+        if (done[i] != 0.0f) x = 0.0;
+        R0 = p == 0 ? x : R0; R1 = p == 1 ? x : R1; R2 = p == 2 ? x : R2; R3 = p == 3 ? x : R3;
+    }
+    returns_state[(size_t)e * P] = R0;
+    if (P > 1) returns_state[(size_t)e * P + 1] = R1;
+    if (P > 2) returns_state[(size_t)e * P + 2] = R2;
+    if (P > 3) returns_state[(size_t)e * P + 3] = R3;
+}
+
+// ppo.rs:412-428: the acting player's entry of all_rewards is the normalized
+// acting reward; the other players keep their raw rewards
+__global__ void k_rn_scatter_acting(size_t n, int P, const int32_t *players, const float *rew, float *all_r) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        all_r[i * P + players[i]] = rew[i];
+}
+
 // block-level exclusive scan of Welford states held one per thread (Hillis-Steele)
 __device__ Welford block_exclusive_scan(Welford mine, Welford *sh) {
     sh[threadIdx.x] = mine;
@@ -268,14 +300,21 @@ __global__ void __launch_bounds__(RN_BLOCK) k_rn_apply(size_t n, const double *X
 bppo_status launch_return_norm(bppo_ctx *c) {
     const size_t n = (size_t)c->T * c->N;
     const int nb = (int)((n + RN_SEG - 1) / RN_SEG);
-    hipLaunchKernelGGL(k_rn_returns, dim3((c->N + 255) / 256), dim3(256), 0, c->stream, c->T, c->N,
-                       c->cfg.gamma, c->d_rew_raw, c->d_done, c->d_rn_returns, c->d_X);
+    if (c->wide)
+        hipLaunchKernelGGL(k_rn_returns_mp, dim3((c->N + 255) / 256), dim3(256), 0, c->stream, c->T, c->N, c->P,
+                           c->cfg.gamma, c->d_rew_raw, c->d_done, c->d_players, c->d_rn_returns, c->d_X);
+    else
+        hipLaunchKernelGGL(k_rn_returns, dim3((c->N + 255) / 256), dim3(256), 0, c->stream, c->T, c->N,
+                           c->cfg.gamma, c->d_rew_raw, c->d_done, c->d_rn_returns, c->d_X);
     hipLaunchKernelGGL(k_rn_block_agg, dim3(nb), dim3(RN_BLOCK), 0, c->stream, n, c->d_X,
                        c->d_scan_agg);
     hipLaunchKernelGGL(k_rn_agg_scan, dim3(1), dim3(1024), 0, c->stream, nb, c->d_scan_agg,
                        c->d_rn_stats);
     hipLaunchKernelGGL(k_rn_apply, dim3(nb), dim3(RN_BLOCK), 0, c->stream, n, c->d_X, c->d_rew_raw,
                        c->d_scan_agg, (float)c->cfg.return_clip, c->d_rew);
+    if (c->wide)
+        hipLaunchKernelGGL(k_rn_scatter_acting, dim3((unsigned)std::min<size_t>((n + 255) / 256, 4096)), dim3(256), 0,
+                           c->stream, n, c->P, c->d_players, c->d_rew, c->d_allr);
     BPPO_HIP(c, hipGetLastError());
     return BPPO_OK;
 }

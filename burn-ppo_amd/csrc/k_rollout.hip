@@ -630,7 +630,91 @@ bppo_status launch_cartpole_observe(bppo_ctx *c, float *d_obs_out) {
     return BPPO_OK;
 }
 
+// ---- multi-player envs (D = 86 / 270): the obs columns of the [priv | obs]
+// rows normalized in place with the lagged stats (normalization.rs:57-74,
+// ppo.rs:292-294; privileged obs stay raw), the raw values kept for the update
+__global__ void __launch_bounds__(256) k_obs_norm_rows(int rows, int D, int ld, float *x, float *raw,
+                                                       const double *on, float clip) {
+    const double cnt = on[2 * D];
+    const size_t n = (size_t)rows * D;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = i / D;
+        const int d = (int)(i - r * D);
+        float *p = x + r * ld + d;
+        const float v = *p;
+        if (raw) raw[i] = v;
+        if (cnt >= 2.0) {
+            double sd = sqrt(on[D + d] / cnt);
+            sd = sd < 1e-8 ? 1e-8 : sd;
+            float z = (float)(((double)v - on[d]) / sd);
+            z = z < -clip ? -clip : z;
+            z = z > clip ? clip : z;
+            *p = z;
+        }
+    }
+}
+bppo_status launch_obs_norm_rows(bppo_ctx *c, int rows, float *x, int ld, float *raw) {
+    const size_t n = (size_t)rows * c->D;
+    hipLaunchKernelGGL(k_obs_norm_rows, dim3((unsigned)std::min<size_t>((n + 255) / 256, 8192)), dim3(256), 0,
+                       c->stream, rows, c->D, ld, x, raw, c->d_on, 10.0f);
+    BPPO_HIP(c, hipGetLastError());
+    return BPPO_OK;
+}
+
+// update_batch over all T*N raw rows (normalization.rs:37-53): column-parallel
+// per chunk of rows (thread = dim, coalesced along the row), sums shifted by the
+// chunk's first row, then the chunks Chan-merged in order into the running stats
+constexpr int OBSW_CHUNKS = 256;
+__global__ void __launch_bounds__(256) k_obsw_part(size_t rows, int D, const float *raw, double *part) {
+    const int d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= D) return;
+    const size_t per = (rows + gridDim.y - 1) / gridDim.y;
+    const size_t r0 = blockIdx.y * per, r1 = r0 + per < rows ? r0 + per : rows;
+    double n = 0.0, s1 = 0.0, s2 = 0.0, k = 0.0;
+    if (r0 < r1) k = raw[r0 * D + d];
+    for (size_t r = r0; r < r1; r++) {
+        const double y = (double)raw[r * D + d] - k;
+        s1 += y;
+        s2 += y * y;
+        n += 1.0;
+    }
+    double *o = part + ((size_t)blockIdx.y * D + d) * 3;
+    o[0] = n;
+    o[1] = n > 0 ? k + s1 / n : 0.0;
+    o[2] = n > 0 ? s2 - s1 * (s1 / n) : 0.0;
+}
+__global__ void k_obsw_final(int D, int nchunk, const double *part, double *on) {
+    const int d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= D) return;
+    double n = 0.0, mean = 0.0, m2 = 0.0;
+    for (int b = 0; b < nchunk; b++) {
+        const double *o = part + ((size_t)b * D + d) * 3;
+        const double nb = o[0];
+        if (nb <= 0) continue;
+        const double nn = n + nb, delta = o[1] - mean;
+        mean = n > 0 ? mean + delta * (nb / nn) : o[1];
+        m2 += o[2] + (n > 0 ? delta * delta * (n * nb / nn) : 0.0);
+        n = nn;
+    }
+    const double na = on[2 * D], nn = na + n, delta = mean - on[d];
+    const double ma = on[d];
+    on[d] = na > 0 ? ma + delta * (n / nn) : mean;
+    on[D + d] = on[D + d] + m2 + (na > 0 ? delta * delta * (na * n / nn) : 0.0);
+}
+__global__ void k_obsw_count(int D, double add, double *on) { on[2 * D] += add; }
+
 bppo_status launch_obs_norm_merge(bppo_ctx *c) {
+    if (c->wide) {
+        const size_t rows = (size_t)c->T * c->N;
+        if ((size_t)OBSW_CHUNKS * c->D * 3 > c->obsw_part_n) { c->err = "obs normalizer scratch too small"; return BPPO_ERR_ARG; }
+        hipLaunchKernelGGL(k_obsw_part, dim3((c->D + 255) / 256, OBSW_CHUNKS), dim3(256), 0, c->stream, rows, c->D,
+                           c->d_obs_raw, c->d_obsw_part);
+        hipLaunchKernelGGL(k_obsw_final, dim3((c->D + 255) / 256), dim3(256), 0, c->stream, c->D, OBSW_CHUNKS,
+                           c->d_obsw_part, c->d_on);
+        hipLaunchKernelGGL(k_obsw_count, dim3(1), dim3(1), 0, c->stream, c->D, (double)rows, c->d_on);
+        BPPO_HIP(c, hipGetLastError());
+        return BPPO_OK;
+    }
     if (c->D > OBS_MAX_D) { c->err = "observation normalizer: obs dim > 8"; return BPPO_ERR_UNSUPPORTED; }
     const int nblk = std::min(OBS_PART_BLOCKS, std::max(1, (c->N + 255) / 256));
     hipLaunchKernelGGL(k_obs_norm_part, dim3(nblk), dim3(256), 0, c->stream, c->N, c->D, (double)c->T,

@@ -45,11 +45,6 @@ static bool is_hidden(const NetLayout &n, int l) {
 
 bppo_status wide_init(bppo_ctx *c) {
     const bppo_config &cfg = c->cfg;
-    if (cfg.normalize_obs || cfg.normalize_returns) {
-        c->err = "wide path: obs/return normalisation not implemented for multi-player envs "
-                 "(the reference default for them is off)";
-        return BPPO_ERR_UNSUPPORTED;
-    }
     if (cfg.ctde && cfg.env_kind != BPPO_ENV_LIARS_DICE) { c->err = "CTDE needs privileged obs"; return BPPO_ERR_ARG; }
     if (!cfg.ctde) c->G = 0;
     c->L = c->G + c->D;
@@ -98,6 +93,11 @@ bppo_status wide_init(bppo_ctx *c) {
     WTRY(walloc(c, &c->d_act_in, (size_t)c->N));
     WTRY(walloc(c, &c->d_scr_r, (size_t)c->N * c->P));
     WTRY(walloc(c, &c->d_scr_d, (size_t)c->N));
+    if (cfg.normalize_obs) {
+        WTRY(walloc(c, &c->d_obs_raw, TN * c->D));
+        c->obsw_part_n = (size_t)256 * c->D * 3;
+        WTRY(walloc(c, &c->d_obsw_part, c->obsw_part_n));
+    }
     return BPPO_OK;
 }
 
@@ -105,7 +105,7 @@ void wide_free(bppo_ctx *c) {
     void *ptrs[] = {c->d_wstate, c->d_xc, c->d_mask, c->d_players, c->d_allr, c->d_lvpp, c->d_hbuf,
                     c->d_logits, c->d_values, c->d_xcg, c->d_dout, c->d_dz[0], c->d_dz[1], c->d_heads,
                     c->d_heads_b, c->d_part, c->d_colsum, c->d_mpart, c->d_bxc, c->d_bmask, c->d_bplayers,
-                    c->d_act_in, c->d_scr_r, c->d_scr_d};
+                    c->d_act_in, c->d_scr_r, c->d_scr_d, c->d_obs_raw, c->d_obsw_part};
     for (void *p : ptrs) if (p) (void)hipFree(p);
 }
 
@@ -158,7 +158,10 @@ bppo_status wide_forward(bppo_ctx *c, int rows, const float *xc, int ldxc, float
     return BPPO_OK;
 }
 
-// collect_rollouts (ppo.rs:213-500), self-play path, normalisers off
+// collect_rollouts (ppo.rs:213-500), self-play path.  Observation normalizer:
+// each step's obs columns normalized in place with the lagged stats (raw copy
+// kept, stats updated after the rollout); return normalizer: the env writes
+// the raw acting rewards, launch_return_norm normalizes them after the rollout
 bppo_status wide_collect(bppo_ctx *c, uint64_t base) {
     const int N = c->N, A = c->A, P = c->P, L = c->L;
     WHIP(c, hipMemsetAsync(c->d_lvpp, 0, sizeof(float) * (size_t)N * P, c->stream));
@@ -167,6 +170,7 @@ bppo_status wide_collect(bppo_ctx *c, uint64_t base) {
         float *xc = c->d_xc + r0 * L;
         WHIP(c, wide_env_observe(c->cfg.env_kind, c->G > 0, c->stream, N, c->d_wstate, xc, c->d_mask + r0 * A,
                                  c->d_players + r0));
+        if (c->cfg.normalize_obs) WTRY(launch_obs_norm_rows(c, N, xc + c->G, L, c->d_obs_raw + r0 * c->D));
         WTRY(wide_forward(c, N, xc, L, c->d_logits, c->d_values));
         SampleArgs s;
         s.N = N; s.P = P; s.logits = c->d_logits; s.values = c->d_values; s.mask = c->d_mask + r0 * A;
@@ -177,7 +181,7 @@ bppo_status wide_collect(bppo_ctx *c, uint64_t base) {
         WideStepArgs w;
         w.N = N; w.t = t; w.state = c->d_wstate; w.env_pos = c->d_env_pos; w.seed_base = c->cfg.env_seed_base;
         w.actions = c->d_act + r0; w.shaping = (float)c->cfg.reward_shaping_coef;
-        w.all_r = c->d_allr + r0 * P; w.rew_act = c->d_rew + r0; w.done_f = c->d_done + r0; w.done_u8 = nullptr;
+        w.all_r = c->d_allr + r0 * P; w.rew_act = (c->cfg.normalize_returns ? c->d_rew_raw : c->d_rew) + r0; w.done_f = c->d_done + r0; w.done_u8 = nullptr;
         w.ep_ret = c->d_ep_ret; w.ep_len = c->d_ep_len; w.eps = c->d_eps; w.ep_count = c->d_ep_count;
         w.eps_cap = c->eps_cap;
         WHIP(c, wide_env_step(c->cfg.env_kind, c->stream, w));
@@ -190,6 +194,7 @@ bppo_status wide_collect(bppo_ctx *c, uint64_t base) {
 bppo_status wide_bootstrap_gae(bppo_ctx *c) {
     const int N = c->N;
     WHIP(c, wide_env_observe(c->cfg.env_kind, c->G > 0, c->stream, N, c->d_wstate, c->d_bxc, c->d_bmask, c->d_bplayers));
+    if (c->cfg.normalize_obs) WTRY(launch_obs_norm_rows(c, N, c->d_bxc + c->G, c->L, nullptr));   // updated stats
     WTRY(wide_forward(c, N, c->d_bxc, c->L, c->d_logits, c->d_values));
     WHIP(c, wide_boot_lvpp(c->stream, N, c->P, c->d_values, c->d_bplayers, c->d_lvpp));
     WHIP(c, hipMemcpyAsync(c->d_last_v, c->d_values, sizeof(float) * N, hipMemcpyDeviceToDevice, c->stream));

@@ -17,6 +17,10 @@ LIB_PATH = os.path.join(ORACLE_DIR, "build", "liboracle.so")
 ENV_CARTPOLE, ENV_CONNECT_FOUR, ENV_LIARS_DICE = 0, 1, 2
 
 
+def _num_players(kind):
+    return {ENV_CARTPOLE: 1, ENV_CONNECT_FOUR: 2, ENV_LIARS_DICE: 4}[kind]
+
+
 def build():
     subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
 
@@ -334,10 +338,14 @@ class Trainer:
         lib().or_trainer_obs_norm_state(self.h, mean, var, C.byref(cnt))
         return mean, var, cnt.value
 
-    def ret_norm_state(self):
+    def ret_norm_state(self, returns=False):
         mvc = np.zeros(3, np.float64)
-        lib().or_trainer_ret_norm_state(self.h, mvc, None)
-        return mvc
+        if not returns:
+            lib().or_trainer_ret_norm_state(self.h, mvc, None)
+            return mvc
+        r = np.zeros(self.cfg.num_envs * _num_players(self.cfg.env_kind), np.float64)
+        lib().or_trainer_ret_norm_state(self.h, mvc, r.ctypes.data)
+        return mvc, r
 
     def phase_seconds(self, ph):
         return lib().or_trainer_last_phase_seconds(self.h, ph)

@@ -84,8 +84,9 @@ def _pair(env, N, T, seed=42, ctde=None, **kw):
     ocfg = O.train_cfg(env_kind=kind, num_envs=N, num_steps=T, seed=seed, hidden=cfg["hidden_size"],
                        num_hidden=cfg["num_hidden"], ctde=is_ctde, relu=cfg["activation"] == "relu",
                        critic_hidden=cfg["critic_hidden_size"] or 0,
-                       critic_num_hidden=cfg["critic_num_hidden"] or 0, normalize_obs=False,
-                       normalize_returns=False, gamma=cfg["gamma"], gae_lambda=cfg["gae_lambda"],
+                       critic_num_hidden=cfg["critic_num_hidden"] or 0,
+                       normalize_obs=bool(cfg["normalize_obs"]),
+                       normalize_returns=bool(cfg["normalize_returns"]), gamma=cfg["gamma"], gae_lambda=cfg["gae_lambda"],
                        lr=bppo.schedule_get(cfg["learning_rate"], 0),
                        ent_coef=bppo.schedule_get(cfg["entropy_coef"], 0),
                        reward_shaping=cfg["reward_shaping_coef"], num_epochs=cfg["num_epochs"],
@@ -99,7 +100,7 @@ def _bits(a):
     return np.ascontiguousarray(a, np.float32).view(np.uint32)
 
 
-def _cmp_rollout(env, tr, ot):
+def _cmp_rollout(env, tr, ot, rew_rtol=0.0):
     kind, D, A, P, G = ENV[env]
     b = tr.buffer
     assert np.array_equal(b.acting_players.reshape(-1), ot.buffer("players", np.int32))
@@ -111,8 +112,14 @@ def _cmp_rollout(env, tr, ot):
     assert np.array_equal(_bits(b.values.reshape(-1)), _bits(ot.buffer("values")))
     assert np.array_equal(_bits(b.log_probs.reshape(-1)), _bits(ot.buffer("log_probs")))
     assert np.array_equal(b.dones.reshape(-1), ot.buffer("dones"))
-    assert np.array_equal(_bits(b.rewards.reshape(-1)), _bits(ot.buffer("rewards")))
-    assert np.array_equal(_bits(b.all_rewards.reshape(-1)), _bits(ot.buffer("all_rewards")))
+    if rew_rtol:
+        # return normalizer: f64 Welford block scan vs the sequential update
+        # (merge order) -> normalized rewards identical up to rare last-ulp ties
+        np.testing.assert_allclose(b.rewards.reshape(-1), ot.buffer("rewards"), rtol=rew_rtol, atol=0)
+        np.testing.assert_allclose(b.all_rewards.reshape(-1), ot.buffer("all_rewards"), rtol=rew_rtol, atol=0)
+    else:
+        assert np.array_equal(_bits(b.rewards.reshape(-1)), _bits(ot.buffer("rewards")))
+        assert np.array_equal(_bits(b.all_rewards.reshape(-1)), _bits(ot.buffer("all_rewards")))
     assert tr.ctx.rng_pos() == ot.rng_pos()
 
 
@@ -192,4 +199,44 @@ def test_tanh_rollout_update_second_rollout(env, N, T, ctde):
     tr.model.set_params(ot.params())
     bppo.collect_rollouts(tr.ctx); ot.collect()
     _cmp_rollout(env, tr, ot)
+    tr.close(); ot.close()
+
+
+# observation + return normalizers on the multi-player path (main.rs:235-254:
+# off by default for P > 1, available by config): lagged obs stats, per
+# (env, player) rolling returns for the acting player, the normalized acting
+# reward in all_rewards
+NORM_CASES = [("connect_four", 64, 12, None), ("liars_dice", 48, 10, None), ("liars_dice", 40, 8, False)]
+
+
+@pytest.mark.parametrize("env,N,T,ctde", NORM_CASES)
+def test_normalizers_rollout_update_second_rollout(env, N, T, ctde):
+    kind, D, A, P, G = ENV[env]
+    cfg, tr, ot = _pair(env, N, T, ctde=ctde, normalize_obs=True, normalize_returns=True)
+    # first rollout: obs stats still empty (count < 2), rewards normalized from step 1
+    bppo.collect_rollouts(tr.ctx); ot.collect()
+    _cmp_rollout(env, tr, ot, rew_rtol=2e-7)
+    m, v, c = tr.ctx.obs_norm()
+    mo, vo, co = ot.obs_norm_state(D)
+    assert c == co == N * T
+    np.testing.assert_allclose(m, mo, rtol=1e-12, atol=1e-15)
+    np.testing.assert_allclose(v, vo, rtol=1e-10, atol=1e-12)
+    mvc, rets = tr.ctx.ret_norm()
+    omvc, orets = ot.ret_norm_state(returns=True)
+    assert np.array_equal(rets, orets)
+    np.testing.assert_allclose(mvc, omvc, rtol=1e-12)
+    bppo.compute_gae(tr.ctx); ot.gae()
+    np.testing.assert_allclose(tr.buffer.advantages.reshape(-1), ot.buffer("advantages"), rtol=1e-5, atol=1e-6)
+    m_ = bppo.ppo_update(tr.ctx, bppo.schedule_get(cfg["learning_rate"], 0), bppo.schedule_get(cfg["entropy_coef"], 0))
+    om = ot.update()
+    for k in ("policy_loss", "value_loss", "entropy", "approx_kl"):
+        assert abs(m_[k] - om[k]) <= 2e-5 + 1e-4 * abs(om[k]), (k, m_[k], om[k])
+    # second rollout from the oracle's params and normalizer state: normalized
+    # observations (now count >= 2) and rewards bit-exact again
+    tr.model.set_params(ot.params())
+    mo, vo, co = ot.obs_norm_state(D)
+    tr.ctx.set_obs_norm(mo, vo, co)
+    tr.ctx.set_ret_norm(omvc, orets)
+    bppo.collect_rollouts(tr.ctx); ot.collect()
+    _cmp_rollout(env, tr, ot, rew_rtol=2e-7)
     tr.close(); ot.close()
