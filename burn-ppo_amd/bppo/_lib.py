@@ -66,7 +66,7 @@ EXPORTS = (
     "bppo_vecenv_reset", "bppo_vecenv_observe", "bppo_vecenv_step", "bppo_vecenv_set_step",
     "bppo_obs_norm_get", "bppo_obs_norm_set", "bppo_ret_norm_get", "bppo_ret_norm_set",
     "bppo_collect_rollouts", "bppo_rollout_episodes", "bppo_compute_gae", "bppo_ppo_update",
-    "bppo_set_allreduce", "bppo_set_allreduce_async", "bppo_get_stream", "bppo_buffer_get", "bppo_buffer_set", "bppo_gae_device",
+    "bppo_set_allreduce", "bppo_set_allreduce_async", "bppo_get_stream", "bppo_opponents_set", "bppo_opponents_get_envs", "bppo_buffer_get", "bppo_buffer_set", "bppo_gae_device",
     "bppo_gae_mp_device", "bppo_last_kernel_ms", "bppo_debug_libm", "bppo_debug_shuffle_chain",
     "bppo_debug_fisher_yates", "bppo_debug_gemm", "bppo_debug_shuffle_engine",
 )
@@ -119,6 +119,8 @@ def lib():
         "bppo_set_allreduce": (i32, [vp, ALLREDUCE_FN, vp, i32]),
         "bppo_set_allreduce_async": (i32, [vp, ALLREDUCE_FN, vp, i32]),
         "bppo_get_stream": (i32, [vp, C.POINTER(vp)]),
+        "bppo_opponents_set": (i32, [vp, i32, vp, vp, vp, vp, i32, vp, vp, vp]),
+        "bppo_opponents_get_envs": (i32, [vp, vp, vp]),
         "bppo_buffer_get": (i32, [vp, C.c_char_p, vp, sz]),
         "bppo_buffer_set": (i32, [vp, C.c_char_p, vp, sz]),
         "bppo_gae_device": (i32, [vp, vp, vp, vp, i32, i32, C.c_float, C.c_float, vp, vp, vp]),

@@ -106,6 +106,32 @@ class Context:
             raise ValueError(f"returns must hold num_envs * num_players = {self.N * self.num_players} values")
         self._chk(L.lib().bppo_ret_norm_set(self.h, mvc.ctypes.data, r.ctypes.data))
 
+    def set_opponents(self, params, norms, num_opponent_envs, learner_pos, pos_to_opp, current_opp):
+        """Opponent-pool rollouts (ppo.rs:537-1063): params [K, n_params] of the
+        loaded opponents, norms[k] = (mean, m2, count) or None, seat state of envs
+        [0, num_opponent_envs) (EnvState, opponent_pool.rs:80-124), current_opp
+        [P - 1] = OpponentPool::sample_all_slots."""
+        params = np.ascontiguousarray(params, np.float32).reshape(-1, self.n_params)
+        K, D, P = params.shape[0], self.obs_dim, self.num_players
+        mean = np.zeros((max(K, 1), D)); m2 = np.zeros((max(K, 1), D)); cnt = np.zeros(max(K, 1))
+        for k, nm in enumerate(norms or []):
+            if nm is not None:
+                mean[k], m2[k], cnt[k] = nm
+        lp = np.ascontiguousarray(learner_pos, np.int32)
+        po = np.ascontiguousarray(pos_to_opp, np.int32)
+        co = np.ascontiguousarray(current_opp, np.int32)
+        self._chk(L.lib().bppo_opponents_set(self.h, K, params.ctypes.data, mean.ctypes.data, m2.ctypes.data,
+                                             cnt.ctypes.data, int(num_opponent_envs), lp.ctypes.data,
+                                             po.ctypes.data, co.ctypes.data))
+        self._n_opp = int(num_opponent_envs)
+
+    def opponent_envs(self):
+        """-> (learner_pos [n_opp], pos_to_opp [n_opp, P]) after the last rollout"""
+        n = getattr(self, "_n_opp", 0)
+        lp = np.zeros(max(n, 1), np.int32); po = np.zeros(max(n, 1) * self.num_players, np.int32)
+        self._chk(L.lib().bppo_opponents_get_envs(self.h, lp.ctypes.data, po.ctypes.data))
+        return lp[:n], po[:n * self.num_players].reshape(n, self.num_players)
+
     def kernel_ms(self, name):
         f = C.c_float()
         self._chk(L.lib().bppo_last_kernel_ms(self.h, name.encode(), C.byref(f)))

@@ -410,9 +410,14 @@ extern "C" bppo_status bppo_collect_rollouts(bppo_ctx *c, bppo_rollout_info *inf
     if (c->wide) TRY(wide_collect(c, base));
     else TRY(launch_cartpole_rollout(c, base, nullptr, nullptr, c->cfg.normalize_obs));
     tm_end(c, TM_ROLLOUT);
-    c->rng_pos = base + TN * (uint64_t)c->A;   // one word per (env, action) per step
-    // this update's shuffles start here; the engine usually began them already
-    c->shuf_slot = c->shuf.ensure(c->rng_pos);
+    if (opp_active(c)) {
+        // opponent pool: seat reshuffles drew a data-dependent number of words
+        TRY(opp_rollout_end(c));
+    } else {
+        c->rng_pos = base + TN * (uint64_t)c->A;   // one word per (env, action) per step
+        // this update's shuffles start here; the engine usually began them already
+        c->shuf_slot = c->shuf.ensure(c->rng_pos);
+    }
     if (c->cfg.normalize_obs) TRY(launch_obs_norm_merge(c));       // ppo.rs:495-497
     tm_begin(c, TM_RETNORM);
     if (c->cfg.normalize_returns) TRY(launch_return_norm(c));      // ppo.rs:390-408
@@ -492,9 +497,16 @@ extern "C" bppo_status bppo_compute_gae(bppo_ctx *c) {
 // ppo_update (ppo.rs:1661-2112)
 extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, bppo_update_metrics *m) {
     if (!c || !c->gae_done) { if (c) c->err = "ppo_update before compute_gae"; return BPPO_ERR_ARG; }
-    if (c->shuf_slot < 0) c->shuf_slot = c->shuf.ensure(c->rng_pos);
+    // opponent pool: train on the learner rows only (ppo.rs:1696-1720); their count
+    // varies per update, so each epoch's swap targets come from the sequential
+    // host walk instead of the speculating shuffle engine
+    const bool opp = opp_active(c);
+    if (opp) TRY(opp_compact_valid(c));
+    if (!opp && c->shuf_slot < 0) c->shuf_slot = c->shuf.ensure(c->rng_pos);
     const int slot = c->shuf_slot;
-    const size_t B = (size_t)c->T * c->N;
+    const size_t B = opp ? (size_t)c->n_valid : (size_t)c->T * c->N;
+    std::vector<uint32_t> Jh(opp ? std::max<size_t>(B, 1) * c->cfg.num_epochs : 0);
+    uint64_t opp_pos = c->rng_pos;
     const int M = c->cfg.num_minibatches;
     const size_t base_mb = B / M, rem = B % M;
     const int np = (int)c->net.n_params;
@@ -513,16 +525,28 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
     int nrow = 0;
     for (int ep = 0; ep < c->cfg.num_epochs && !stop; ep++) {
         epochs_run++;
-        {
-            auto w0 = std::chrono::steady_clock::now();
-            c->shuf.wait_epoch(slot, ep);
-            wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
-        }
-        BPPO_HIP(c, hipStreamWaitEvent(c->stream, c->shuf.ev[slot][ep], 0));
         hipEvent_t s0 = c->ev[TM_SHUFFLE][0], s1 = c->ev[TM_SHUFFLE][1];
-        (void)hipEventRecord(s0, c->stream);
-        TRY(launch_fisher_yates(c, c->shuf.d_J[slot] + (size_t)ep * B, (uint32_t)B));
-        (void)hipEventRecord(s1, c->stream);
+        if (opp) {
+            uint32_t *J = Jh.data() + (size_t)ep * B;
+            auto w0 = std::chrono::steady_clock::now();
+            opp_pos = shuffle_walk_host(c->rng_key, c->cfg.rng_stream, opp_pos, (uint32_t)B, J);   // ppo.rs:1816
+            wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
+            BPPO_HIP(c, hipMemcpyAsync(c->d_Jopp, J, sizeof(uint32_t) * B, hipMemcpyHostToDevice, c->stream));
+            (void)hipEventRecord(s0, c->stream);
+            if (B) TRY(launch_fisher_yates(c, c->d_Jopp, (uint32_t)B));
+            if (B) TRY(opp_map_perm(c, (uint32_t)B));
+            (void)hipEventRecord(s1, c->stream);
+        } else {
+            {
+                auto w0 = std::chrono::steady_clock::now();
+                c->shuf.wait_epoch(slot, ep);
+                wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
+            }
+            BPPO_HIP(c, hipStreamWaitEvent(c->stream, c->shuf.ev[slot][ep], 0));
+            (void)hipEventRecord(s0, c->stream);
+            TRY(launch_fisher_yates(c, c->shuf.d_J[slot] + (size_t)ep * B, (uint32_t)B));
+            (void)hipEventRecord(s1, c->stream);
+        }
         TRY(launch_epoch_adv_stats(c, (uint32_t)B, M));
         size_t start = 0;
         for (int mb = 0; mb < M; mb++) {
@@ -581,21 +605,27 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
         if (hipEventElapsedTime(&ms, c->ev[TM_SHUFFLE][0], c->ev[TM_SHUFFLE][1]) == hipSuccess) sh_ms = ms;
     }
     tm_end(c, TM_UPDATE);
-    c->rng_pos = c->shuf.end_pos[slot][epochs_run - 1];   // only started epochs consumed words
     c->last_wait_ms = wait_ms;
     c->last_walk_ms = 0.0;
     c->last_met = 0;
-    for (int e = 0; e < epochs_run; e++) {
-        c->last_walk_ms += c->shuf.walk_ms[slot][e];
-        c->last_met += c->shuf.coalesced[slot][e] >= 0 && e > 0;
+    if (opp) {
+        c->rng_pos = opp_pos;                               // the epochs walked (early stop: started ones)
+        c->last_walk_ms = wait_ms;
+        BPPO_HIP(c, hipStreamSynchronize(c->stream));      // Jh's copies done
+    } else {
+        c->rng_pos = c->shuf.end_pos[slot][epochs_run - 1];   // only started epochs consumed words
+        for (int e = 0; e < epochs_run; e++) {
+            c->last_walk_ms += c->shuf.walk_ms[slot][e];
+            c->last_met += c->shuf.coalesced[slot][e] >= 0 && e > 0;
+        }
+        c->shuf_slot = -1;
+        // this update's reads of the J slot are enqueued; the next update's shuffles
+        // begin after its rollout's T*N*A Gumbel words (usually chained already)
+        c->shuf.release(slot, c->stream);
+        c->shuf.ensure(c->rng_pos + (uint64_t)c->T * c->N * (uint64_t)c->A);
     }
-    c->shuf_slot = -1;
-    // this update's reads of the J slot are enqueued; the next update's shuffles
-    // begin after its rollout's T*N*A Gumbel words (usually chained already)
-    c->shuf.release(slot, c->stream);
-    c->shuf.ensure(c->rng_pos + (uint64_t)c->T * c->N * (uint64_t)c->A);
     double ev4[4];
-    TRY(launch_explained_variance(c, ev4));
+    TRY(launch_explained_variance(c, ev4, opp ? c->d_valid : nullptr));
     tm_read(c, TM_UPDATE);
     c->last_ms[TM_FWDBWD] = fw_ms;
     c->last_ms[TM_SHUFFLE] = sh_ms;
@@ -665,6 +695,7 @@ static BufDesc find_buf(bppo_ctx *c, const char *name) {
     if (!strcmp(name, "actions")) return {c->d_act, TN * 4};
     if (!strcmp(name, "rewards")) return {c->d_rew, TN * 4};
     if (!strcmp(name, "raw_rewards")) return {c->d_rew_raw, TN * 4};
+    if (!strcmp(name, "valid")) return {c->d_valid, c->d_valid ? TN * 4 : 0};
     if (!strcmp(name, "dones")) return {c->d_done, TN * 4};
     if (!strcmp(name, "values")) return {c->d_val, TN * 4};
     if (!strcmp(name, "log_probs")) return {c->d_logp, TN * 4};

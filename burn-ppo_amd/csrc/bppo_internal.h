@@ -239,6 +239,19 @@ struct bppo_ctx {
     void *d_wstate = nullptr;         // per-env state structs [N]
     float *d_xc = nullptr;            // rollout rows [T][N][L]
     float *d_obs_raw = nullptr;       // normalize_obs: raw obs rows [T][N][D] for the stats update
+    // opponent pool (ppo.rs:537-1063): K opponent models, envs [0, n_opp) play them
+    int opp_K = 0, n_opp = 0;
+    float *d_opp_params = nullptr;    // [K][n_params]
+    double *d_opp_on = nullptr;       // [K][2D + 1] obs normalizer per model
+    std::vector<int> opp_has_norm;
+    int32_t *d_lpos = nullptr, *d_p2o = nullptr, *d_curopp = nullptr;   // [n_opp], [n_opp][P], [P - 1]
+    int32_t *d_group = nullptr, *d_gpos = nullptr;                        // per step [N]
+    float *d_valid = nullptr;         // learner-turn flags [T][N]
+    uint64_t *d_rngpos = nullptr;     // main RNG word position during an opponent rollout
+    float *d_oraw = nullptr, *d_oxc = nullptr, *d_ologits = nullptr;     // [N][L], [N][L], [N][A]
+    uint32_t *d_vidx = nullptr, *d_Jopp = nullptr;                         // [T N]
+    uint32_t *d_nvalid = nullptr;
+    uint32_t n_valid = 0;
     double *d_obsw_part = nullptr;    // normalize_obs: per-chunk partial stats [256][D][3]
     size_t obsw_part_n = 0;
     uint8_t *d_mask = nullptr;        // action masks [T][N][A] (0/1)
@@ -283,6 +296,7 @@ bppo_status launch_cartpole_vecenv_step(bppo_ctx *c, const int32_t *d_actions, f
 bppo_status launch_cartpole_observe(bppo_ctx *c, float *d_obs_out);
 bppo_status launch_obs_norm_merge(bppo_ctx *c);
 bppo_status launch_obs_norm_rows(bppo_ctx *c, int rows, float *x, int ld, float *raw);
+bppo_status launch_obs_norm_rows_on(bppo_ctx *c, int rows, float *x, int ld, float *raw, const double *on);
 bppo_status launch_bootstrap(bppo_ctx *c, const double *mean, const double *sd, int norm_on);
 bppo_status launch_forward_rows(bppo_ctx *c, const float *d_obs, int B, float *d_logits,
                                 float *d_values);
@@ -306,13 +320,25 @@ bppo_status launch_adam(bppo_ctx *c, float lr, const float *c1, const float *c2,
                         int nm = 0);
 bppo_status launch_metric_row(bppo_ctx *c, float *dst, int nm);
 bppo_status launch_pack_rows(bppo_ctx *c);
-bppo_status launch_explained_variance(bppo_ctx *c, double *out6);
+bppo_status launch_explained_variance(bppo_ctx *c, double *out6, const float *valid = nullptr);
 // (wide_api.hip) multi-player path
 bppo_status wide_init(bppo_ctx *c);
 void wide_free(bppo_ctx *c);
 bppo_status wide_reset(bppo_ctx *c);
 bppo_status wide_pack(bppo_ctx *c);
 bppo_status wide_forward(bppo_ctx *c, int rows, const float *xc, int ldxc, float *logits, float *values);
+bppo_status wide_forward_actor(bppo_ctx *c, int rows, const float *xc, int ldxc, const float *params, float *logits);
+// opponent pool (opponents.hip)
+bool opp_active(const bppo_ctx *c);
+bppo_status opp_alloc(bppo_ctx *c);
+void opp_free(bppo_ctx *c);
+bppo_status opp_rollout_begin(bppo_ctx *c, uint64_t base);
+bppo_status opp_step_group(bppo_ctx *c, int t);
+bppo_status opp_step_forwards(bppo_ctx *c);
+bppo_status opp_step_seats(bppo_ctx *c, int t);
+bppo_status opp_rollout_end(bppo_ctx *c);
+bppo_status opp_compact_valid(bppo_ctx *c);
+bppo_status opp_map_perm(bppo_ctx *c, uint32_t n);
 bppo_status wide_collect(bppo_ctx *c, uint64_t base);
 bppo_status wide_bootstrap_gae(bppo_ctx *c);
 bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_coef);

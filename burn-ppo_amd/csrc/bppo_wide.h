@@ -37,6 +37,10 @@ struct SampleArgs {
     int32_t *act;
     float *logp, *val, *lvpp;
     int32_t *err;        // bit 0: non-finite log-prob, bit 1: empty mask
+    // opponent pool: row group (0 learner, 1 + model) and its position in the
+    // step's draw order; the step's first word position from device memory
+    const int32_t *group = nullptr, *gpos = nullptr;
+    const uint64_t *dbase = nullptr;
 };
 
 // metric slots written after the gradient (d_grad[np + k]); the first 11 are

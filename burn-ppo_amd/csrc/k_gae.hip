@@ -172,8 +172,10 @@ __global__ void k_rn_returns(int T, int N, double gamma, const float *rew_raw, c
 // multi-player (ppo.rs:388-408): one rolling return per (env, player), updated
 // and pushed for the ACTING player only (normalization.rs:163-186), reset for
 // that player when the step ends the episode.  X in (t, e) order as above.
+// valid (opponent pool, nullable): only learner turns enter the variance stats
+// (ppo.rs:982-989); other rows carry a NaN in X, which the scan skips
 __global__ void k_rn_returns_mp(int T, int N, int P, double gamma, const float *rew_raw, const float *done,
-                                const int32_t *players, double *returns_state, double *X) {
+                                const int32_t *players, const float *valid, double *returns_state, double *X) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= N) return;
     double R0 = returns_state[(size_t)e * P], R1 = P > 1 ? returns_state[(size_t)e * P + 1] : 0.0;
@@ -183,7 +185,7 @@ __global__ void k_rn_returns_mp(int T, int N, int P, double gamma, const float *
         const int p = players[i];
         double x = p == 0 ? R0 : p == 1 ? R1 : p == 2 ? R2 : R3;
         x = x * gamma + (double)rew_raw[i];
-        X[i] = x;
+        X[i] = (valid && !(valid[i] > 0.5f)) ? __longlong_as_double(0x7ff8000000000000ll) : x;
         if (done[i] != 0.0f) x = 0.0;
         R0 = p == 0 ? x : R0; R1 = p == 1 ? x : R1; R2 = p == 2 ? x : R2; R3 = p == 3 ? x : R3;
     }
@@ -238,7 +240,7 @@ __global__ void __launch_bounds__(RN_BLOCK) k_rn_block_agg(size_t n, const doubl
     const size_t base = (size_t)blockIdx.x * RN_SEG + (size_t)threadIdx.x * RN_IPT;
     Welford s{0, 0, 0};
     for (int k = 0; k < RN_IPT; k++)
-        if (base + k < n) wpush(s, xs[threadIdx.x * RN_PAD + k]);
+        if (base + k < n && !isnan(xs[threadIdx.x * RN_PAD + k])) wpush(s, xs[threadIdx.x * RN_PAD + k]);
     Welford ex = block_exclusive_scan(s, sh);
     if (threadIdx.x == blockDim.x - 1) agg[blockIdx.x] = wmerge(ex, s);
 }
@@ -274,13 +276,13 @@ __global__ void __launch_bounds__(RN_BLOCK) k_rn_apply(size_t n, const double *X
     const size_t base = (size_t)blockIdx.x * RN_SEG + (size_t)threadIdx.x * RN_IPT;
     Welford s{0, 0, 0};
     for (int k = 0; k < RN_IPT; k++)
-        if (base + k < n) wpush(s, xs[threadIdx.x * RN_PAD + k]);
+        if (base + k < n && !isnan(xs[threadIdx.x * RN_PAD + k])) wpush(s, xs[threadIdx.x * RN_PAD + k]);
     Welford ex = block_exclusive_scan(s, sh);
     Welford run = wmerge(agg[blockIdx.x], ex);
     for (int k = 0; k < RN_IPT; k++) {
         const size_t i = base + k;
         if (i >= n) break;
-        wpush(run, xs[threadIdx.x * RN_PAD + k]);
+        if (!isnan(xs[threadIdx.x * RN_PAD + k])) wpush(run, xs[threadIdx.x * RN_PAD + k]);
         float r = rew_raw[i];
         if (run.n >= 2.0) {                                  // normalization.rs:187-197
             const double sd = sqrt(run.m2 / run.n + 1e-8);
@@ -302,7 +304,8 @@ bppo_status launch_return_norm(bppo_ctx *c) {
     const int nb = (int)((n + RN_SEG - 1) / RN_SEG);
     if (c->wide)
         hipLaunchKernelGGL(k_rn_returns_mp, dim3((c->N + 255) / 256), dim3(256), 0, c->stream, c->T, c->N, c->P,
-                           c->cfg.gamma, c->d_rew_raw, c->d_done, c->d_players, c->d_rn_returns, c->d_X);
+                           c->cfg.gamma, c->d_rew_raw, c->d_done, c->d_players, c->n_opp ? c->d_valid : nullptr,
+                           c->d_rn_returns, c->d_X);
     else
         hipLaunchKernelGGL(k_rn_returns, dim3((c->N + 255) / 256), dim3(256), 0, c->stream, c->T, c->N,
                            c->cfg.gamma, c->d_rew_raw, c->d_done, c->d_rn_returns, c->d_X);

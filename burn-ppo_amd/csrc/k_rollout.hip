@@ -654,9 +654,12 @@ __global__ void __launch_bounds__(256) k_obs_norm_rows(int rows, int D, int ld, 
     }
 }
 bppo_status launch_obs_norm_rows(bppo_ctx *c, int rows, float *x, int ld, float *raw) {
+    return launch_obs_norm_rows_on(c, rows, x, ld, raw, c->d_on);
+}
+bppo_status launch_obs_norm_rows_on(bppo_ctx *c, int rows, float *x, int ld, float *raw, const double *on) {
     const size_t n = (size_t)rows * c->D;
     hipLaunchKernelGGL(k_obs_norm_rows, dim3((unsigned)std::min<size_t>((n + 255) / 256, 8192)), dim3(256), 0,
-                       c->stream, rows, c->D, ld, x, raw, c->d_on, 10.0f);
+                       c->stream, rows, c->D, ld, x, raw, on, 10.0f);
     BPPO_HIP(c, hipGetLastError());
     return BPPO_OK;
 }

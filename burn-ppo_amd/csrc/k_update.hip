@@ -1087,10 +1087,12 @@ __global__ void __launch_bounds__(256) k_adam1(AdamArgs a, const float *gtail, c
 }
 
 // explained variance partial sums (ppo.rs:1268-1294)
-__global__ void __launch_bounds__(256) k_ev(size_t n, const float *val, const float *ret, double *part) {
+__global__ void __launch_bounds__(256) k_ev(size_t n, const float *val, const float *ret, const float *valid,
+                                             double *part) {
     __shared__ double sh[4][256];
     double s[4] = {0, 0, 0, 0};
     for (size_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        if (valid && !(valid[i] > 0.5f)) continue;      // opponent pool: learner rows only (ppo.rs:2047-2056)
         const double R = ret[i], res = (double)(ret[i] - val[i]);
         s[0] += R; s[1] += R * R; s[2] += res; s[3] += res * res;
     }
@@ -1286,9 +1288,9 @@ bppo_status launch_adam(bppo_ctx *c, float lr, const float *c1, const float *c2,
     return BPPO_OK;
 }
 
-bppo_status launch_explained_variance(bppo_ctx *c, double *out4) {
+bppo_status launch_explained_variance(bppo_ctx *c, double *out4, const float *valid) {
     const size_t n = (size_t)c->T * c->N;
-    hipLaunchKernelGGL(k_ev, dim3(STAT_BLOCKS), dim3(256), 0, c->stream, n, c->d_val, c->d_ret, c->d_red);
+    hipLaunchKernelGGL(k_ev, dim3(STAT_BLOCKS), dim3(256), 0, c->stream, n, c->d_val, c->d_ret, valid, c->d_red);
     BPPO_HIP(c, hipMemcpyAsync(c->h_red, c->d_red, sizeof(double) * 4 * STAT_BLOCKS,
                                hipMemcpyDeviceToHost, c->stream));
     BPPO_HIP(c, hipStreamSynchronize(c->stream));

@@ -161,7 +161,8 @@ __global__ void k_sample_masked(SampleArgs g) {
     }
     if (!any) { atomicOr(g.err, 2); return; }   // utils.rs:115-123 "Empty action mask"
     WordCursor c;
-    c.init(g.key, g.stream, g.base + (uint64_t)e * A);
+    const uint64_t row = g.gpos ? (uint64_t)g.gpos[e] : (uint64_t)e;   // ppo.rs:737 / :850 batch order
+    c.init(g.key, g.stream, (g.dbase ? *g.dbase : g.base) + row * A);
     int best = 0;
     float bv = 0.0f;
 #pragma unroll
@@ -169,10 +170,15 @@ __global__ void k_sample_masked(SampleArgs g) {
         const float v = __fadd_rn(x[a], gumbel_from_word(c.next()));
         if (a == 0 || v > bv) { bv = v; best = a; }
     }
+    g.act[e] = best;
+    if (g.group && g.group[e] != 0) {              // opponent's move: no log-prob / value (ppo.rs:849-861)
+        g.logp[e] = 0.0f;
+        g.val[e] = 0.0f;
+        return;
+    }
     const float lp = log_prob_row<A>(x, best);
     if (!isfinite(lp)) atomicOr(g.err, 1);       // ppo.rs:363-366
     const float v = g.values[e];
-    g.act[e] = best;
     g.logp[e] = lp;
     g.val[e] = v;
     const int p = g.players[e];

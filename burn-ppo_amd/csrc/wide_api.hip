@@ -107,6 +107,7 @@ void wide_free(bppo_ctx *c) {
                     c->d_heads_b, c->d_part, c->d_colsum, c->d_mpart, c->d_bxc, c->d_bmask, c->d_bplayers,
                     c->d_act_in, c->d_scr_r, c->d_scr_d, c->d_obs_raw, c->d_obsw_part};
     for (void *p : ptrs) if (p) (void)hipFree(p);
+    opp_free(c);
 }
 
 bppo_status wide_reset(bppo_ctx *c) {
@@ -158,25 +159,48 @@ bppo_status wide_forward(bppo_ctx *c, int rows, const float *xc, int ldxc, float
     return BPPO_OK;
 }
 
-// collect_rollouts (ppo.rs:213-500), self-play path.  Observation normalizer:
+// actor logits only, with caller-given parameters (an opponent model,
+// ppo.rs:827-843: forward_actor for CTDE, the shared trunk + policy head for MLP)
+bppo_status wide_forward_actor(bppo_ctx *c, int rows, const float *xc, int ldxc, const float *P, float *logits) {
+    const NetLayout &n = c->net;
+    const float *x = xc + c->G;
+    int ldx = ldxc;
+    for (int l = 0; l < n.n_actor_hidden; l++) {
+        float *h = c->d_hbuf + c->hoff[l];
+        WHIP(c, gemm_fwd(c->stream, rows, n.out[l], n.in[l], x, ldx, P + n.w[l], n.out[l], P + n.b[l],
+                         c->cfg.relu ? 1 : 2, h, n.out[l], n.out[l], nullptr, 0));
+        x = h; ldx = n.out[l];
+    }
+    WHIP(c, gemm_fwd(c->stream, rows, c->A, n.in[n.policy], x, ldx, P + n.w[n.policy], c->A, P + n.b[n.policy], 0,
+                     logits, c->A, c->A, nullptr, 0));
+    return BPPO_OK;
+}
+
+// collect_rollouts (ppo.rs:213-500), self-play path; with an opponent pool
+// (opponents.hip) collect_rollouts_with_opponents (ppo.rs:537-1063).  Observation normalizer:
 // each step's obs columns normalized in place with the lagged stats (raw copy
 // kept, stats updated after the rollout); return normalizer: the env writes
 // the raw acting rewards, launch_return_norm normalizes them after the rollout
 bppo_status wide_collect(bppo_ctx *c, uint64_t base) {
     const int N = c->N, A = c->A, P = c->P, L = c->L;
+    const bool opp = opp_active(c);
     WHIP(c, hipMemsetAsync(c->d_lvpp, 0, sizeof(float) * (size_t)N * P, c->stream));
+    if (opp) WTRY(opp_rollout_begin(c, base));
     for (int t = 0; t < c->T; t++) {
         const size_t r0 = (size_t)t * N;
         float *xc = c->d_xc + r0 * L;
         WHIP(c, wide_env_observe(c->cfg.env_kind, c->G > 0, c->stream, N, c->d_wstate, xc, c->d_mask + r0 * A,
                                  c->d_players + r0));
+        if (opp) WTRY(opp_step_group(c, t));
         if (c->cfg.normalize_obs) WTRY(launch_obs_norm_rows(c, N, xc + c->G, L, c->d_obs_raw + r0 * c->D));
         WTRY(wide_forward(c, N, xc, L, c->d_logits, c->d_values));
+        if (opp) WTRY(opp_step_forwards(c));
         SampleArgs s;
         s.N = N; s.P = P; s.logits = c->d_logits; s.values = c->d_values; s.mask = c->d_mask + r0 * A;
         s.players = c->d_players + r0; s.key = c->rng_key; s.stream = c->cfg.rng_stream;
         s.base = base + r0 * (uint64_t)A;
         s.act = c->d_act + r0; s.logp = c->d_logp + r0; s.val = c->d_val + r0; s.lvpp = c->d_lvpp; s.err = c->d_err;
+        if (opp) { s.group = c->d_group; s.gpos = c->d_gpos; s.dbase = c->d_rngpos; }
         WHIP(c, wide_sample(A, c->stream, s));
         WideStepArgs w;
         w.N = N; w.t = t; w.state = c->d_wstate; w.env_pos = c->d_env_pos; w.seed_base = c->cfg.env_seed_base;
@@ -185,6 +209,7 @@ bppo_status wide_collect(bppo_ctx *c, uint64_t base) {
         w.ep_ret = c->d_ep_ret; w.ep_len = c->d_ep_len; w.eps = c->d_eps; w.ep_count = c->d_ep_count;
         w.eps_cap = c->eps_cap;
         WHIP(c, wide_env_step(c->cfg.env_kind, c->stream, w));
+        if (opp) WTRY(opp_step_seats(c, t));
     }
     return BPPO_OK;
 }

@@ -150,6 +150,29 @@ bppo_status bppo_set_allreduce(bppo_ctx *ctx, bppo_allreduce_fn fn, void *user, 
 bppo_status bppo_set_allreduce_async(bppo_ctx *ctx, bppo_allreduce_fn fn, void *user, int32_t world_size);
 bppo_status bppo_get_stream(bppo_ctx *ctx, void **hip_stream);
 
+/* Opponent-pool training (multi-player envs): replaces collect_rollouts_with_opponents
+ * (ppo.rs:537-1063) and the learner-row filter of ppo_update (ppo.rs:165-180,
+ * 1696-1753).  The host keeps the pool (OpponentPool, opponent_pool.rs: checkpoint
+ * loading, win-rate sampling, rotation) and hands over the loaded models:
+ *   n_models (<= 15) parameter vectors of the learner's architecture, packed
+ *   [n_models][n_params]; per model an optional observation normalizer
+ *   (norm_mean/norm_m2 [n_models][obs_dim], norm_count [n_models]; count < 2 or
+ *   NULL arrays = none);
+ *   envs [0, num_opponent_envs) play against them (main.rs:621-637), with seat
+ *   state learner_pos [num_opponent_envs] and pos_to_opp [num_opponent_envs][P]
+ *   (model index per seat, -1 on the learner's seat) (EnvState, opponent_pool.rs:80-124);
+ *   current_opp [P - 1]: OpponentPool::sample_all_slots, the models a finished game
+ *   is given before its seats are reshuffled from the main RNG.
+ * Opponent batches sample in ascending model index (the reference iterates a
+ * HashMap, whose order is unspecified).  num_opponent_envs = 0 switches it off.
+ * Buffer "valid" holds the learner-turn flags of the last rollout; ppo_update
+ * trains on those rows only. */
+bppo_status bppo_opponents_set(bppo_ctx *ctx, int32_t n_models, const float *params, const double *norm_mean,
+                               const double *norm_m2, const double *norm_count, int32_t num_opponent_envs,
+                               const int32_t *learner_pos, const int32_t *pos_to_opp, const int32_t *current_opp);
+/* the seat state after the last rollout's reshuffles */
+bppo_status bppo_opponents_get_envs(bppo_ctx *ctx, int32_t *learner_pos, int32_t *pos_to_opp);
+
 /* parity hooks: export / import a RolloutBuffer field.  names: "obs", "priv",
  * "actions" (i32), "rewards", "dones", "values", "log_probs", "advantages",
  * "returns", "players" (i32), "all_rewards", "masks", "last_v_pp", "perm" (u32,

@@ -53,6 +53,7 @@ void or_rng_fill_bytes(or_rng *r, uint8_t *dst, size_t n);
 float or_gen_range_f32(or_rng *r, float low, float high);
 uint32_t or_gen_range_u32(or_rng *r, uint32_t low, uint32_t high);     /* [low, high) */
 uint8_t or_gen_range_u8_incl(or_rng *r, uint8_t low, uint8_t high);    /* [low, high] */
+uint64_t or_gen_range_u64(or_rng *r, uint64_t low, uint64_t high);     /* [low, high), usize */
 void or_shuffle_u32(or_rng *r, uint32_t *v, size_t n);
 void or_shuffle_targets(or_rng *r, uint32_t *J, size_t n);
 void or_apply_swaps(const uint32_t *J, uint32_t *v, size_t n);
@@ -283,6 +284,20 @@ size_t or_trainer_buffer(const or_trainer *t, const char *name, void *out, size_
 void or_trainer_obs_norm_state(const or_trainer *t, double *mean, double *var, double *count);
 void or_trainer_ret_norm_state(const or_trainer *t, double *mean_var_count3, double *returns);
 int or_trainer_episodes(const or_trainer *t, or_episode *out, int cap);  /* last collect */
+/* Opponent-pool training (ppo.rs:537-1063, main.rs:621-651): K opponent
+ * parameter sets of the learner's architecture, each with an optional
+ * observation normalizer (count < 2: none); envs [0, n_opp) are opponent envs
+ * with seat state learner_pos [n_opp], pos_to_opp [n_opp * P] (model index, -1
+ * for the learner's seat); current_opp [P - 1] is OpponentPool::sample_all_slots
+ * (the models a finished game is reassigned).  Opponent batches run in
+ * ascending model index (the reference iterates a HashMap).  n_opp = 0 turns
+ * it off.  The update then trains on the learner rows only (buffer "valid"). */
+void or_trainer_set_opponents(or_trainer *t, int K, const float *params, const double *mean,
+                              const double *m2, const double *count, int n_opp, const int32_t *learner_pos,
+                              const int32_t *pos_to_opp, const int32_t *current_opp);
+void or_trainer_opponent_envs(const or_trainer *t, int32_t *learner_pos, int32_t *pos_to_opp);
+/* EnvState::shuffle_positions (opponent_pool.rs:107-123) on caller state */
+void or_shuffle_positions(or_rng *r, int P, const int32_t *assigned, int32_t *learner_pos, int32_t *pos_to_opp);
 double or_trainer_last_phase_seconds(const or_trainer *t, int phase);   /* 0 rollout, 1 gae, 2 update */
 
 #ifdef __cplusplus

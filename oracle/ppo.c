@@ -101,6 +101,13 @@ struct or_trainer {
     or_episode *eps;
     int n_eps, eps_cap;
     double phase_s[3];
+    /* opponent pool (ppo.rs:537-1063) */
+    int K, n_opp;
+    float *opp_params;
+    or_obs_norm *opp_on;
+    int *opp_has_norm;
+    int32_t *lpos, *p2o, *curopp;
+    float *valid;
 };
 
 static double now_s(void) {
@@ -153,7 +160,62 @@ void or_trainer_free(or_trainer *t) {
     or_vecenv_free(t->env); or_adam_free(&t->adam); or_obs_norm_free(&t->on); or_ret_norm_free(&t->rn);
     free(t->params); free(t->obs); free(t->raw); free(t->priv); free(t->rewards); free(t->dones);
     free(t->values); free(t->logp); free(t->all_r); free(t->masks); free(t->adv); free(t->ret);
-    free(t->actions); free(t->players); free(t->lvpp); free(t->eps); free(t);
+    free(t->actions); free(t->players); free(t->lvpp); free(t->eps);
+    for (int k = 0; k < t->K; k++) or_obs_norm_free(&t->opp_on[k]);
+    free(t->opp_on); free(t->opp_has_norm); free(t->opp_params);
+    free(t->lpos); free(t->p2o); free(t->curopp); free(t->valid); free(t);
+}
+
+/* opponent_pool.rs:107-123 EnvState::shuffle_positions: the learner's seat is
+ * gen_range(0..P) (usize -> u64 draw), the other seats ascending, shuffled
+ * (u32 gen_index), then mapped to the assigned opponents in order */
+void or_shuffle_positions(or_rng *r, int P, const int32_t *assigned, int32_t *learner_pos, int32_t *pos_to_opp) {
+    const int lp = (int)or_gen_range_u64(r, 0, (uint64_t)P);
+    uint32_t other[8];
+    int no = 0;
+    for (int p = 0; p < P; p++) if (p != lp) other[no++] = (uint32_t)p;
+    or_shuffle_u32(r, other, (size_t)no);
+    *learner_pos = lp;
+    for (int p = 0; p < P; p++) pos_to_opp[p] = -1;
+    for (int i = 0; i < no; i++) pos_to_opp[other[i]] = assigned[i];
+}
+
+void or_trainer_set_opponents(or_trainer *t, int K, const float *params, const double *mean,
+                              const double *m2, const double *count, int n_opp, const int32_t *learner_pos,
+                              const int32_t *pos_to_opp, const int32_t *current_opp) {
+    for (int k = 0; k < t->K; k++) or_obs_norm_free(&t->opp_on[k]);
+    free(t->opp_on); free(t->opp_has_norm); free(t->opp_params);
+    free(t->lpos); free(t->p2o); free(t->curopp);
+    const size_t np = t->net.n_params;
+    t->K = K; t->n_opp = n_opp;
+    t->opp_params = malloc(sizeof(float) * np * (K > 0 ? K : 1));
+    if (K) memcpy(t->opp_params, params, sizeof(float) * np * K);
+    t->opp_on = calloc(K > 0 ? K : 1, sizeof(or_obs_norm));
+    t->opp_has_norm = calloc(K > 0 ? K : 1, sizeof(int));
+    for (int k = 0; k < K; k++) {
+        or_obs_norm_init(&t->opp_on[k], t->D, 10.0f);
+        if (count && count[k] >= 2.0) {
+            memcpy(t->opp_on[k].mean, mean + (size_t)k * t->D, sizeof(double) * t->D);
+            memcpy(t->opp_on[k].var, m2 + (size_t)k * t->D, sizeof(double) * t->D);
+            t->opp_on[k].count = count[k];
+            t->opp_has_norm[k] = 1;
+        }
+    }
+    t->lpos = malloc(sizeof(int32_t) * (n_opp > 0 ? n_opp : 1));
+    t->p2o = malloc(sizeof(int32_t) * (size_t)(n_opp > 0 ? n_opp : 1) * t->P);
+    t->curopp = malloc(sizeof(int32_t) * t->P);
+    if (n_opp) {
+        memcpy(t->lpos, learner_pos, sizeof(int32_t) * n_opp);
+        memcpy(t->p2o, pos_to_opp, sizeof(int32_t) * (size_t)n_opp * t->P);
+    }
+    memcpy(t->curopp, current_opp, sizeof(int32_t) * (t->P - 1));
+    if (!t->valid) t->valid = malloc(sizeof(float) * (size_t)t->T * t->N);
+}
+
+void or_trainer_opponent_envs(const or_trainer *t, int32_t *learner_pos, int32_t *pos_to_opp) {
+    if (!t->n_opp) return;
+    if (learner_pos) memcpy(learner_pos, t->lpos, sizeof(int32_t) * t->n_opp);
+    if (pos_to_opp) memcpy(pos_to_opp, t->p2o, sizeof(int32_t) * (size_t)t->n_opp * t->P);
 }
 
 size_t or_trainer_num_params(const or_trainer *t) { return t->net.n_params; }
@@ -167,8 +229,123 @@ static void forward_rows(or_trainer *t, const float *obs, const float *priv, siz
     or_net_forward(&t->net, t->params, obs, priv, B, logits, values);
 }
 
+/* one masked categorical draw per row of a group (ppo.rs:337-339 / :735-737 / :849-850):
+ * -inf masking (panics on an empty mask), Gumbel-max from the main RNG */
+static void mask_rows(float *logits, const uint8_t *mk, const int32_t *rows, int n, int A) {
+    for (int j = 0; j < n; j++) {
+        const uint8_t *m = mk + (size_t)rows[j] * A;
+        int any = 0;
+        for (int a = 0; a < A; a++) any |= m[a];
+        if (!any) { fprintf(stderr, "Empty action mask: env %d\n", rows[j]); abort(); }
+        for (int a = 0; a < A; a++) logits[(size_t)j * A + a] += m[a] ? 0.0f : -INFINITY;
+    }
+}
+
+/* ppo.rs:537-1063 collect_rollouts_with_opponents.  Per step: partition into the
+ * learner's rows (self-play envs and opponent envs on the learner's seat) and
+ * each opponent model's rows; the learner batch samples first, then the
+ * opponent batches in ascending model index, all from the main RNG; env step;
+ * every finished opponent game gets the current opponents and reshuffled seats
+ * (main RNG, env order); then every row is stored, with the learner-turn flag
+ * evaluated against the seats AFTER that reshuffle (ppo.rs:904-911: the
+ * reference's order, replicated). */
+static int collect_opp(or_trainer *t) {
+    double t0 = now_s();
+    const int N = t->N, D = t->D, A = t->A, P = t->P, G = t->G;
+    const size_t np = t->net.n_params;
+    float *raw = malloc(sizeof(float) * N * D), *xo = malloc(sizeof(float) * N * D);
+    float *xp = G ? malloc(sizeof(float) * N * G) : NULL, *privs = G ? malloc(sizeof(float) * N * G) : NULL;
+    float *logits = malloc(sizeof(float) * N * A), *vals = malloc(sizeof(float) * N);
+    float *rw = malloc(sizeof(float) * N * P), *alogp = malloc(sizeof(float) * N), *aval = malloc(sizeof(float) * N);
+    uint8_t *dn = malloc(N), *mk = malloc((size_t)N * A);
+    int32_t *cp = malloc(sizeof(int32_t) * N), *act = malloc(sizeof(int32_t) * N);
+    int32_t *rows = malloc(sizeof(int32_t) * N), *sact = malloc(sizeof(int32_t) * N);
+    t->n_eps = 0;
+    memset(t->lvpp, 0, sizeof(float) * (size_t)N * P);
+    for (int s = 0; s < t->T; s++) {
+        const size_t base = (size_t)s * N;
+        or_vecenv_get_players(t->env, cp);                                   /* :614 */
+        or_vecenv_get_obs(t->env, raw);                                      /* :617 */
+        memcpy(t->raw + base * D, raw, sizeof(float) * N * D);               /* :620-622 */
+        if (G) { or_vecenv_get_priv(t->env, privs); memcpy(t->priv + base * G, privs, sizeof(float) * N * G); }
+        int hm = or_vecenv_get_masks(t->env, mk);                            /* :647 */
+        t->has_masks = hm;
+        if (!hm) memset(mk, 1, (size_t)N * A);
+        if (hm) for (size_t q = 0; q < (size_t)N * A; q++) t->masks[base * A + q] = mk[q] ? 1.0f : 0.0f;
+        for (int e = 0; e < N; e++) { act[e] = 0; alogp[e] = 0.0f; aval[e] = 0.0f; }
+        /* learner batch (:636-640, :668-775) */
+        int n = 0;
+        for (int e = 0; e < N; e++) if (e >= t->n_opp || cp[e] == t->lpos[e]) rows[n++] = e;
+        if (n) {
+            for (int j = 0; j < n; j++) {
+                memcpy(xo + (size_t)j * D, raw + (size_t)rows[j] * D, sizeof(float) * D);
+                if (G) memcpy(xp + (size_t)j * G, privs + (size_t)rows[j] * G, sizeof(float) * G);
+            }
+            if (t->c.normalize_obs) or_obs_norm_normalize_batch(&t->on, xo, n);
+            forward_rows(t, xo, xp, n, logits, vals);
+            if (hm) mask_rows(logits, mk, rows, n, A);
+            or_sample_categorical(&t->rng, logits, n, A, sact);
+            for (int j = 0; j < n; j++) {
+                const int e = rows[j];
+                float lp = or_log_prob(logits + (size_t)j * A, A, sact[j]);
+                if (!isfinite(lp)) { fprintf(stderr, "NaN/Inf in log probs\n"); abort(); }
+                act[e] = sact[j]; alogp[e] = lp; aval[e] = vals[j];
+                t->lvpp[(size_t)e * P + cp[e]] = vals[j];                    /* :770-772 */
+            }
+        }
+        /* opponent batches (:777-864), ascending model index */
+        for (int k = 0; k < t->K; k++) {
+            n = 0;
+            for (int e = 0; e < t->n_opp; e++)
+                if (cp[e] != t->lpos[e] && t->p2o[(size_t)e * P + cp[e]] == k) rows[n++] = e;
+            if (!n) continue;
+            for (int j = 0; j < n; j++) {
+                memcpy(xo + (size_t)j * D, raw + (size_t)rows[j] * D, sizeof(float) * D);
+                if (G) memcpy(xp + (size_t)j * G, privs + (size_t)rows[j] * G, sizeof(float) * G);
+            }
+            if (t->opp_has_norm[k]) or_obs_norm_normalize_batch(&t->opp_on[k], xo, n);
+            or_net_forward(&t->net, t->opp_params + (size_t)k * np, xo, xp, n, logits, vals);
+            if (hm) mask_rows(logits, mk, rows, n, A);
+            or_sample_categorical(&t->rng, logits, n, A, sact);
+            for (int j = 0; j < n; j++) act[rows[j]] = sact[j];
+        }
+        int cap = t->eps_cap - t->n_eps;
+        int ne = or_vecenv_step(t->env, act, NULL, rw, dn, t->eps + t->n_eps, cap);   /* :867-871 */
+        t->n_eps += ne < cap ? ne : cap;
+        for (int e = 0; e < t->n_opp; e++)                                   /* :874-925 */
+            if (dn[e]) or_shuffle_positions(&t->rng, P, t->curopp, &t->lpos[e], &t->p2o[(size_t)e * P]);
+        for (int e = 0; e < N; e++) {                                        /* :928-1003 */
+            const int cur = cp[e];
+            const int valid = e >= t->n_opp || cur == t->lpos[e];
+            t->valid[base + e] = valid ? 1.0f : 0.0f;
+            float r = rw[(size_t)e * P + cur];
+            if (t->c.normalize_returns) {
+                or_ret_norm_update_return(&t->rn, e, cur, r);
+                if (valid) or_ret_norm_update_variance(&t->rn, e, cur);
+                r = or_ret_norm_normalize(&t->rn, r);
+                if (dn[e]) or_ret_norm_reset_player(&t->rn, e, cur);
+            }
+            t->rewards[base + e] = r;
+            for (int q = 0; q < P; q++) t->all_r[(base + e) * P + q] = q == cur ? r : rw[(size_t)e * P + q];
+            t->actions[base + e] = act[e];
+            t->logp[base + e] = alogp[e];
+            t->values[base + e] = aval[e];
+            t->dones[base + e] = dn[e] ? 1.0f : 0.0f;
+            t->players[base + e] = cur;
+        }
+        memcpy(t->obs + base * D, raw, sizeof(float) * N * D);              /* :943-948 learner-normalized */
+        if (t->c.normalize_obs) or_obs_norm_normalize_batch(&t->on, t->obs + base * D, N);
+    }
+    if (t->c.normalize_obs) or_obs_norm_update_batch(&t->on, t->raw, (size_t)t->T * N);   /* :1058-1060 */
+    free(raw); free(xo); free(xp); free(privs); free(logits); free(vals); free(rw); free(alogp); free(aval);
+    free(dn); free(mk); free(cp); free(act); free(rows); free(sact);
+    t->phase_s[0] = now_s() - t0;
+    return t->n_eps;
+}
+
 /* ppo.rs:213-500 collect_rollouts (self-play / single-player path). */
 int or_trainer_collect(or_trainer *t) {
+    if (t->n_opp > 0) return collect_opp(t);
     double t0 = now_s();
     const int N = t->N, D = t->D, A = t->A, P = t->P, G = t->G;
     float *obs = malloc(sizeof(float) * N * D);
@@ -269,7 +446,15 @@ void or_trainer_gae(or_trainer *t) {
 /* ppo.rs:1661-2112 ppo_update (no pool, no PopArt). */
 void or_trainer_update(or_trainer *t, or_update_metrics *m) {
     double t0 = now_s();
-    const size_t B = (size_t)t->T * t->N;
+    size_t B = (size_t)t->T * t->N;
+    /* opponent-pool training: only the learner rows, in (t, e) order (ppo.rs:1696-1720) */
+    uint32_t *vidx = NULL;
+    if (t->n_opp > 0) {
+        vidx = malloc(sizeof(uint32_t) * B);
+        size_t nv = 0;
+        for (size_t i = 0; i < B; i++) if (t->valid[i] > 0.5f) vidx[nv++] = (uint32_t)i;
+        B = nv;
+    }
     const int D = t->D, A = t->A, G = t->G;
     const or_ppo_cfg *c = &t->c.ppo;
     uint32_t *idx = malloc(sizeof(uint32_t) * B);
@@ -295,7 +480,7 @@ void or_trainer_update(or_trainer *t, or_update_metrics *m) {
             size_t sz = base + ((size_t)mbi < rem ? 1 : 0);
             if (sz == 0) continue;
             for (size_t q = 0; q < sz; q++) {                    /* :1833-1857 gather */
-                size_t r = idx[start + q];
+                size_t r = vidx ? vidx[idx[start + q]] : idx[start + q];
                 memcpy(mo + q * D, t->obs + r * D, sizeof(float) * D);
                 if (G) memcpy(mp + q * G, t->priv + r * G, sizeof(float) * G);
                 if (mm) memcpy(mm + q * A, t->masks + r * A, sizeof(float) * A);
@@ -327,7 +512,14 @@ void or_trainer_update(or_trainer *t, or_update_metrics *m) {
         m->policy_loss = tp / n; m->value_loss = tv / n; m->entropy = th / n;
         m->entropy_scaled = m->entropy / logf((float)A);
         m->approx_kl = tk / n; m->clip_fraction = tc / n;
-        m->explained_variance = or_explained_variance(t->values, t->ret, B);
+        if (vidx) {                                                   /* ppo.rs:2047-2056 */
+            float *fv = malloc(sizeof(float) * (B ? B : 1)), *fr = malloc(sizeof(float) * (B ? B : 1));
+            for (size_t i = 0; i < B; i++) { fv[i] = t->values[vidx[i]]; fr[i] = t->ret[vidx[i]]; }
+            m->explained_variance = or_explained_variance(fv, fr, B);
+            free(fv); free(fr);
+        } else {
+            m->explained_variance = or_explained_variance(t->values, t->ret, B);
+        }
         m->total_loss = tl / n; m->value_mean = tvm / n; m->returns_mean = trm / n;
         m->adv_mean_raw = tam / n; m->adv_std_raw = tas / n; m->adv_min_raw = tamin; m->adv_max_raw = tamax;
         m->value_error_mean = tvem / n; m->value_error_std = tves / n; m->value_error_max = tvemax;
@@ -335,7 +527,7 @@ void or_trainer_update(or_trainer *t, or_update_metrics *m) {
         m->entropy_valid_pct = t->has_masks ? tevp / n : 0.0f;
         m->num_updates = nup; m->epochs_run = epochs_run;
     }
-    free(idx); free(grads); free(mo); free(mp); free(mm); free(ma); free(mlp); free(madv);
+    free(vidx); free(idx); free(grads); free(mo); free(mp); free(mm); free(ma); free(mlp); free(madv);
     free(mret); free(mov); free(madvn);
     t->phase_s[2] = now_s() - t0;
 }
@@ -357,6 +549,7 @@ size_t or_trainer_buffer(const or_trainer *t, const char *name, void *out, size_
     else if (!strcmp(name, "all_rewards")) { src = t->all_r; n = TN * t->P * 4; }
     else if (!strcmp(name, "masks")) { src = t->masks; n = t->masks ? TN * t->A * 4 : 0; }
     else if (!strcmp(name, "last_v_pp")) { src = t->lvpp; n = (size_t)t->N * t->P * 4; }
+    else if (!strcmp(name, "valid")) { src = t->valid; n = t->valid ? TN * 4 : 0; }
     if (!src) return 0;
     if (out && bytes >= n) memcpy(out, src, n);
     return n;

@@ -117,6 +117,21 @@ uint32_t or_gen_range_u32(or_rng *r, uint32_t low, uint32_t high) {
     }
 }
 
+/* rand 0.8.5 UniformInt<u64>::sample_single ([low, high)), the form
+ * `gen_range(0..n)` takes for usize on 64-bit targets (opponent_pool.rs:109):
+ * next_u64 (two words, low first), 64x64 -> 128 widening multiply, zone
+ * (range << lz(range)) - 1.  Restated, verify. */
+uint64_t or_gen_range_u64(or_rng *r, uint64_t low, uint64_t high) {
+    uint64_t range = high - 1 - low + 1;
+    if (range == 0) return or_rng_next_u64(r);
+    uint64_t zone = (range << __builtin_clzll(range)) - 1u;
+    for (;;) {
+        unsigned __int128 m = (unsigned __int128)or_rng_next_u64(r) * range;
+        uint64_t lo = (uint64_t)m, hi = (uint64_t)(m >> 64);
+        if (lo <= zone) return low + hi;
+    }
+}
+
 /* UniformInt<u8>::sample_single_inclusive: u32 arithmetic, modulus zone. */
 uint8_t or_gen_range_u8_incl(or_rng *r, uint8_t low, uint8_t high) {
     uint32_t range = (uint32_t)(uint8_t)(high - low) + 1u;

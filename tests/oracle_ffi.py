@@ -178,6 +178,11 @@ def lib():
             "or_trainer_ret_norm_state": (None, [C.c_void_p, f64, C.c_void_p]),
             "or_trainer_episodes": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
             "or_trainer_last_phase_seconds": (C.c_double, [C.c_void_p, C.c_int]),
+            "or_trainer_set_opponents": (None, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                                C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]),
+            "or_trainer_opponent_envs": (None, [C.c_void_p, C.c_void_p, C.c_void_p]),
+            "or_shuffle_positions": (None, [C.c_void_p, C.c_int, i32, C.c_void_p, i32]),
+            "or_gen_range_u64": (C.c_uint64, [C.c_void_p, C.c_uint64, C.c_uint64]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -346,6 +351,28 @@ class Trainer:
         r = np.zeros(self.cfg.num_envs * _num_players(self.cfg.env_kind), np.float64)
         lib().or_trainer_ret_norm_state(self.h, mvc, r.ctypes.data)
         return mvc, r
+
+    def set_opponents(self, params, norms, n_opp, learner_pos, pos_to_opp, current_opp):
+        """ppo.rs:537-1063 opponent pool: params [K, n_params]; norms: per model
+        (mean [D], m2 [D], count) or None; seat state of envs [0, n_opp)."""
+        params = np.ascontiguousarray(params, np.float32)
+        K = params.shape[0] if params.ndim == 2 else 0
+        D = lib().or_trainer_buffer(self.h, b"obs", None, 0) // 4 // (self.cfg.num_steps * self.cfg.num_envs)
+        mean = np.zeros((max(K, 1), D)); m2 = np.zeros((max(K, 1), D)); cnt = np.zeros(max(K, 1))
+        for k, nm in enumerate(norms or []):
+            if nm is not None:
+                mean[k], m2[k], cnt[k] = nm
+        self._keep = [params, mean, m2, cnt, np.ascontiguousarray(learner_pos, np.int32),
+                      np.ascontiguousarray(pos_to_opp, np.int32), np.ascontiguousarray(current_opp, np.int32)]
+        k = self._keep
+        lib().or_trainer_set_opponents(self.h, K, k[0].ctypes.data, k[1].ctypes.data, k[2].ctypes.data,
+                                       k[3].ctypes.data, n_opp, k[4].ctypes.data, k[5].ctypes.data,
+                                       k[6].ctypes.data)
+
+    def opponent_envs(self, n_opp, P):
+        lp = np.zeros(max(n_opp, 1), np.int32); po = np.zeros(max(n_opp, 1) * P, np.int32)
+        lib().or_trainer_opponent_envs(self.h, lp.ctypes.data, po.ctypes.data)
+        return lp[:n_opp], po[:n_opp * P]
 
     def phase_seconds(self, ph):
         return lib().or_trainer_last_phase_seconds(self.h, ph)

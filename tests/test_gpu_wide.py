@@ -240,3 +240,66 @@ def test_normalizers_rollout_update_second_rollout(env, N, T, ctde):
     bppo.collect_rollouts(tr.ctx); ot.collect()
     _cmp_rollout(env, tr, ot, rew_rtol=2e-7)
     tr.close(); ot.close()
+
+
+# ------------------------------------------------------- opponent pool ---
+# collect_rollouts_with_opponents (ppo.rs:537-1063) + the learner-row filter of
+# ppo_update (ppo.rs:1696-1753).  Oracle and device get the same opponent
+# models (one with its own obs normalizer), seats and current opponents.
+def _opponent_setup(cfg, tr, ot, env, n_opp, K, seed=3):
+    kind, D, A, P, G = ENV[env]
+    rng = np.random.default_rng(seed)
+    params = np.stack([bppo.orthogonal_init(cfg, seed=100 + k) for k in range(K)])
+    norms = [None] * K
+    norms[K - 1] = (rng.normal(size=D) * 0.1, (rng.random(D) + 0.5) * 500.0, 500.0)
+    lp = rng.integers(0, P, n_opp).astype(np.int32)
+    po = np.full((n_opp, P), -1, np.int32)
+    for e in range(n_opp):
+        for p in range(P):
+            if p != lp[e]:
+                po[e, p] = rng.integers(0, K)
+    co = rng.integers(0, K, P - 1).astype(np.int32)
+    tr.ctx.set_opponents(params, norms, n_opp, lp, po, co)
+    ot.set_opponents(params, norms, n_opp, lp, po.reshape(-1), co)
+    return P
+
+
+OPP_CASES = [("connect_four", 64, 16, None, 40, 2, False), ("liars_dice", 48, 12, None, 48, 3, False),
+             ("liars_dice", 40, 10, False, 25, 2, False), ("connect_four", 64, 16, None, 40, 3, True),
+             ("liars_dice", 48, 10, None, 30, 2, True)]
+
+
+@pytest.mark.parametrize("env,N,T,ctde,n_opp,K,norm", OPP_CASES)
+def test_opponent_pool_rollout_update_bit_exact(env, N, T, ctde, n_opp, K, norm):
+    kw = dict(normalize_obs=True, normalize_returns=True) if norm else {}
+    cfg, tr, ot = _pair(env, N, T, ctde=ctde, **kw)
+    P = _opponent_setup(cfg, tr, ot, env, n_opp, K)
+    for rnd in range(2):
+        if norm and rnd:                       # layered: the oracle's normalizer state
+            kind, D, A, P_, G = ENV[env]
+            tr.ctx.set_obs_norm(*ot.obs_norm_state(D))
+            tr.ctx.set_ret_norm(*ot.ret_norm_state(returns=True))
+        bppo.collect_rollouts(tr.ctx); ot.collect()
+        _cmp_rollout(env, tr, ot, rew_rtol=2e-7 if norm else 0.0)   # includes the main RNG position
+        assert np.array_equal(tr.ctx.buffer("valid"), ot.buffer("valid"))
+        lp, po = tr.ctx.opponent_envs()
+        olp, opo = ot.opponent_envs(n_opp, P)
+        assert np.array_equal(lp, olp) and np.array_equal(po.reshape(-1), opo)
+        v = tr.ctx.buffer("valid").reshape(T, N)
+        assert (n_opp == N or v[:, n_opp:].min() == 1.0) and 0.0 < v[:, :n_opp].mean() < 1.0
+        bppo.compute_gae(tr.ctx); ot.gae()
+        if norm:
+            np.testing.assert_allclose(tr.buffer.advantages.reshape(-1), ot.buffer("advantages"), rtol=1e-5, atol=1e-6)
+        else:
+            assert np.array_equal(_bits(tr.buffer.advantages.reshape(-1)), _bits(ot.buffer("advantages")))
+        lr = bppo.schedule_get(cfg["learning_rate"], 0)
+        ent = bppo.schedule_get(cfg["entropy_coef"], 0)
+        m = bppo.ppo_update(tr.ctx, lr, ent)
+        om = ot.update()
+        assert m["epochs_run"] == om["epochs_run"] and m["num_updates"] == om["num_updates"]
+        assert tr.ctx.rng_pos() == ot.rng_pos()     # shuffles over the learner rows only
+        for k in ("policy_loss", "value_loss", "entropy", "approx_kl", "clip_fraction", "explained_variance"):
+            assert abs(m[k] - om[k]) <= 2e-5 + 1e-4 * abs(om[k]), (k, m[k], om[k])
+        np.testing.assert_allclose(tr.model.get_params(), ot.params(), rtol=1e-4, atol=2e-5)
+        tr.model.set_params(ot.params())
+    tr.close(); ot.close()
