@@ -252,6 +252,7 @@ struct bppo_ctx {
     uint32_t *d_vidx = nullptr, *d_Jopp = nullptr;                         // [T N]
     uint32_t *d_nvalid = nullptr;
     uint32_t n_valid = 0;
+    int32_t *d_gbase = nullptr, *h_gbase = nullptr;   // per step: draw-order base of each mover group
     double *d_obsw_part = nullptr;    // normalize_obs: per-chunk partial stats [256][D][3]
     size_t obsw_part_n = 0;
     uint8_t *d_mask = nullptr;        // action masks [T][N][A] (0/1)

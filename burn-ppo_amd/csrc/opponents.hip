@@ -42,7 +42,7 @@ __global__ void k_set_u64(uint64_t *p, uint64_t v) { *p = v; }
 // exclusive prefix per group, group bases in group order.
 __global__ void __launch_bounds__(OG_THREADS) k_opp_group(int N, int n_opp, int P, int G, const int32_t *players,
                                                           const int32_t *lpos, const int32_t *p2o, int32_t *group,
-                                                          int32_t *gpos, int32_t *err) {
+                                                          int32_t *gpos, int32_t *gbase, int32_t *err) {
     __shared__ int cnt[OPP_MAX_MODELS + 1][OG_THREADS];
     __shared__ int base[OPP_MAX_MODELS + 2];
     const int tid = threadIdx.x;
@@ -71,6 +71,7 @@ __global__ void __launch_bounds__(OG_THREADS) k_opp_group(int N, int n_opp, int 
     if (tid == 0) {
         base[0] = 0;
         for (int g = 1; g <= G; g++) base[g] += base[g - 1];
+        for (int g = 0; g <= G; g++) gbase[g] = base[g];
     }
     __syncthreads();
     for (int e = e0; e < e1; e++) {
@@ -79,16 +80,49 @@ __global__ void __launch_bounds__(OG_THREADS) k_opp_group(int N, int n_opp, int 
     }
 }
 
-// model k's logits into the step's logits for its rows
-__global__ void k_opp_select(int N, int A, const int32_t *group, int gsel, const float *src, float *dst) {
+// the step's raw rows in draw order: each model's rows become one contiguous slice
+__global__ void k_opp_sort_rows(int N, int L, const int32_t *group, const int32_t *gpos, const float *src, float *dst) {
+    const size_t n = (size_t)N * L;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t e = i / L, k = i - e * L;
+        if (group[e] != 0) dst[(size_t)gpos[e] * L + k] = src[i];
+    }
+}
+
+// the opponents' logits (draw order) into the step's logits for their rows
+__global__ void k_opp_select(int N, int A, const int32_t *group, const int32_t *gpos, const float *src, float *dst) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N * A) return;
-    if (group[i / A] == gsel) dst[i] = src[i];
+    const int e = i / A;
+    if (group[e] != 0) dst[i] = src[(size_t)gpos[e] * A + (i - e * A)];
 }
+
+// main-stream words from an LDS window [base, end) filled in parallel by the
+// block; a position past the window (an env whose rejections run past it)
+// falls back to computing its ChaCha block
+struct WindowCursor {
+    const uint32_t *buf;
+    uint64_t base, end, pos;
+    Key8 key;
+    uint64_t stream;
+    __device__ __forceinline__ uint32_t next() {
+        uint32_t w;
+        if (pos < end) {
+            w = buf[pos - base];
+        } else {
+            uint32_t blk[16];
+            chacha12_block(key, pos >> 4, stream, blk);
+            w = blk[pos & 15];
+        }
+        pos++;
+        return w;
+    }
+};
 
 // rand 0.8.5 UniformInt<u64> / <u32>::sample_single on the counter-based main
 // stream (same restatement as oracle/rng.c)
-__device__ __forceinline__ uint64_t dev_range_u64(WordCursor &c, uint64_t range) {
+template <class Cur>
+__device__ __forceinline__ uint64_t dev_range_u64(Cur &c, uint64_t range) {
     const uint64_t zone = (range << __clzll((long long)range)) - 1ull;
     for (;;) {
         const uint64_t lo32 = c.next(), hi32 = c.next();
@@ -97,7 +131,8 @@ __device__ __forceinline__ uint64_t dev_range_u64(WordCursor &c, uint64_t range)
         if (lo <= zone) return hi;
     }
 }
-__device__ __forceinline__ uint32_t dev_range_u32(WordCursor &c, uint32_t range) {
+template <class Cur>
+__device__ __forceinline__ uint32_t dev_range_u32(Cur &c, uint32_t range) {
     const uint32_t zone = (range << __clz((int)range)) - 1u;
     for (;;) {
         const uint64_t m = (uint64_t)c.next() * range;
@@ -108,31 +143,73 @@ __device__ __forceinline__ uint32_t dev_range_u32(WordCursor &c, uint32_t range)
 // after the env step: the step's N*A sampling words, then the seat reshuffle of
 // every finished opponent game (env order, main RNG), then the learner-turn
 // flags against the new seats (ppo.rs:874-925, 928-937)
-__global__ void __launch_bounds__(256) k_opp_seats(int N, int n_opp, int P, int A, const float *done,
-                                                   const int32_t *players, Key8 key, uint64_t stream,
-                                                   const int32_t *curopp, uint64_t *rngpos, int32_t *lpos,
-                                                   int32_t *p2o, float *valid) {
-    if (threadIdx.x == 0) {
-        WordCursor c;
-        c.init(key, stream, *rngpos + (uint64_t)N * A);
-        for (int e = 0; e < n_opp; e++) {
-            if (done[e] == 0.0f) continue;
-            const int lp = (int)dev_range_u64(c, (uint64_t)P);            // opponent_pool.rs:109
-            int other[4], no = 0;
-            for (int p = 0; p < P; p++) if (p != lp) other[no++] = p;
-            for (int i = no - 1; i >= 1; i--) {                              // :114-115 SliceRandom::shuffle
-                const int j = (int)dev_range_u32(c, (uint32_t)(i + 1));
-                const int t = other[i]; other[i] = other[j]; other[j] = t;
-            }
-            lpos[e] = lp;
-            int32_t *row = p2o + (size_t)e * P;
-            for (int p = 0; p < P; p++) row[p] = -1;
-            for (int i = 0; i < no; i++) row[other[i]] = curopp[i];
+constexpr int SEAT_THREADS = 1024, SEAT_CHUNK = 8192, SEAT_WORDS = 4096, SEAT_MARGIN = 64;
+__global__ void __launch_bounds__(SEAT_THREADS) k_opp_seats(int N, int n_opp, int P, int A, const float *done,
+                                                            const int32_t *players, Key8 key, uint64_t stream,
+                                                            const int32_t *curopp, uint64_t *rngpos, int32_t *lpos,
+                                                            int32_t *p2o, float *valid) {
+    __shared__ int list[SEAT_CHUNK];
+    __shared__ int cnt[SEAT_THREADS];
+    __shared__ uint32_t words[SEAT_WORDS];
+    __shared__ uint64_t pos;
+    __shared__ int qnext;
+    const int tid = threadIdx.x;
+    if (tid == 0) pos = *rngpos + (uint64_t)N * A;
+    // finished opponent games in env order, chunk by chunk: flags read in
+    // parallel and compacted, the draws (sequential in the RNG) on one thread
+    for (int c0 = 0; c0 < n_opp; c0 += SEAT_CHUNK) {
+        const int c1 = min(n_opp, c0 + SEAT_CHUNK);
+        const int per = (c1 - c0 + SEAT_THREADS - 1) / SEAT_THREADS;
+        const int e0 = c0 + tid * per, e1 = min(c1, e0 + per);
+        int k = 0;
+        for (int e = e0; e < e1; e++) k += done[e] != 0.0f;
+        cnt[tid] = k;
+        __syncthreads();
+        if (tid == 0) {
+            int run = 0;
+            for (int q = 0; q < SEAT_THREADS; q++) { const int v = cnt[q]; cnt[q] = run; run += v; }
+            list[SEAT_CHUNK - 1] = run;   // count (list slot reused after the writes below)
         }
-        *rngpos = c.pos;
+        __syncthreads();
+        const int nd = list[SEAT_CHUNK - 1];
+        __syncthreads();
+        int o = cnt[tid];
+        for (int e = e0; e < e1; e++) if (done[e] != 0.0f) list[o++] = e;
+        __syncthreads();
+        if (tid == 0) qnext = 0;
+        __syncthreads();
+        while (qnext < nd) {
+            // the next SEAT_WORDS words from pos's block on, one ChaCha block per thread
+            const uint64_t wbase = (pos >> 4) << 4;
+            if (tid < SEAT_WORDS / 16) chacha12_block(key, (wbase >> 4) + tid, stream, (uint32_t *)&words[tid * 16]);
+            __syncthreads();
+            if (tid == 0) {
+                WindowCursor c{words, wbase, wbase + SEAT_WORDS, pos, key, stream};
+                int q = qnext;
+                for (; q < nd && c.pos + SEAT_MARGIN <= c.end; q++) {
+                    const int e = list[q];
+                    const int lp = (int)dev_range_u64(c, (uint64_t)P);        // opponent_pool.rs:109
+                    int other[4], no = 0;
+                    for (int p = 0; p < P; p++) if (p != lp) other[no++] = p;
+                    for (int i = no - 1; i >= 1; i--) {                          // :114-115 SliceRandom::shuffle
+                        const int j = (int)dev_range_u32(c, (uint32_t)(i + 1));
+                        const int t = other[i]; other[i] = other[j]; other[j] = t;
+                    }
+                    lpos[e] = lp;
+                    int32_t *row = p2o + (size_t)e * P;
+                    for (int p = 0; p < P; p++) row[p] = -1;
+                    for (int i = 0; i < no; i++) row[other[i]] = curopp[i];
+                }
+                pos = c.pos;
+                qnext = q;
+            }
+            __syncthreads();
+        }
     }
+    if (tid == 0) *rngpos = pos;
+    __threadfence_block();
     __syncthreads();
-    for (int e = threadIdx.x; e < N; e += blockDim.x)
+    for (int e = tid; e < N; e += blockDim.x)
         valid[e] = (e >= n_opp || players[e] == lpos[e]) ? 1.0f : 0.0f;
 }
 
@@ -168,8 +245,11 @@ bool opp_active(const bppo_ctx *c) { return c->wide && c->n_opp > 0 && c->opp_K 
 
 void opp_free(bppo_ctx *c) {
     void *ptrs[] = {c->d_opp_params, c->d_opp_on, c->d_lpos, c->d_p2o, c->d_curopp, c->d_group, c->d_gpos,
-                    c->d_valid, c->d_rngpos, c->d_oraw, c->d_oxc, c->d_ologits, c->d_vidx, c->d_Jopp, c->d_nvalid};
+                    c->d_valid, c->d_rngpos, c->d_oraw, c->d_oxc, c->d_ologits, c->d_vidx, c->d_Jopp, c->d_nvalid,
+                    c->d_gbase};
     for (void *p : ptrs) if (p) (void)hipFree(p);
+    if (c->h_gbase) (void)hipHostFree(c->h_gbase);
+    c->h_gbase = nullptr; c->d_gbase = nullptr;
     c->d_opp_params = nullptr; c->d_opp_on = nullptr; c->d_lpos = c->d_p2o = c->d_curopp = nullptr;
     c->d_group = c->d_gpos = nullptr; c->d_valid = nullptr; c->d_rngpos = nullptr;
     c->d_oraw = c->d_oxc = c->d_ologits = nullptr; c->d_vidx = c->d_Jopp = c->d_nvalid = nullptr;
@@ -196,6 +276,8 @@ bppo_status opp_alloc(bppo_ctx *c) {
     TRY(oalloc(c, &c->d_Jopp, TN));
     TRY(oalloc(c, &c->d_nvalid, 1));
     TRY(oalloc(c, &c->d_curopp, 4));
+    TRY(oalloc(c, &c->d_gbase, OPP_MAX_MODELS + 2));
+    if (!c->h_gbase) BPPO_HIP(c, hipHostMalloc((void **)&c->h_gbase, sizeof(int32_t) * (OPP_MAX_MODELS + 2)));
     return BPPO_OK;
 }
 
@@ -211,8 +293,12 @@ bppo_status opp_step_group(bppo_ctx *c, int t) {
     BPPO_HIP(c, hipMemcpyAsync(c->d_oraw, c->d_xc + r0 * c->L, sizeof(float) * (size_t)c->N * c->L,
                                hipMemcpyDeviceToDevice, c->stream));
     hipLaunchKernelGGL(k_opp_group, dim3(1), dim3(OG_THREADS), 0, c->stream, c->N, c->n_opp, c->P, c->opp_K + 1,
-                       c->d_players + r0, c->d_lpos, c->d_p2o, c->d_group, c->d_gpos, c->d_err);
+                       c->d_players + r0, c->d_lpos, c->d_p2o, c->d_group, c->d_gpos, c->d_gbase, c->d_err);
     BPPO_HIP(c, hipGetLastError());
+    // the per-model row counts size the opponents' GEMMs: one small read per step
+    BPPO_HIP(c, hipMemcpyAsync(c->h_gbase, c->d_gbase, sizeof(int32_t) * (c->opp_K + 2), hipMemcpyDeviceToHost,
+                               c->stream));
+    BPPO_HIP(c, hipStreamSynchronize(c->stream));
     return BPPO_OK;
 }
 
@@ -220,24 +306,32 @@ bppo_status opp_step_group(bppo_ctx *c, int t) {
 // rows; its rows' logits replace the learner's in d_logits
 bppo_status opp_step_forwards(bppo_ctx *c) {
     const size_t np = c->net.n_params;
-    for (int k = 0; k < c->opp_K; k++) {
-        BPPO_HIP(c, hipMemcpyAsync(c->d_oxc, c->d_oraw, sizeof(float) * (size_t)c->N * c->L, hipMemcpyDeviceToDevice,
-                                   c->stream));
-        if (c->opp_has_norm[k])
-            TRY(launch_obs_norm_rows_on(c, c->N, c->d_oxc + c->G, c->L, nullptr,
-                                        c->d_opp_on + (size_t)k * (2 * c->D + 1)));
-        TRY(wide_forward_actor(c, c->N, c->d_oxc, c->L, c->d_opp_params + (size_t)k * np, c->d_ologits));
-        const int n = c->N * c->A;
-        hipLaunchKernelGGL(k_opp_select, dim3((n + 255) / 256), dim3(256), 0, c->stream, c->N, c->A, c->d_group, k + 1,
-                           c->d_ologits, c->d_logits);
+    const int32_t *gb = c->h_gbase;            // group g owns draw rows [gb[g], gb[g + 1])
+    if (gb[c->opp_K + 1] == gb[1]) return BPPO_OK;   // no opponent moves this step
+    {
+        const size_t n = (size_t)c->N * c->L;
+        hipLaunchKernelGGL(k_opp_sort_rows, dim3((unsigned)std::min<size_t>((n + 255) / 256, 8192)), dim3(256), 0,
+                           c->stream, c->N, c->L, c->d_group, c->d_gpos, c->d_oraw, c->d_oxc);
         BPPO_HIP(c, hipGetLastError());
     }
+    for (int k = 0; k < c->opp_K; k++) {
+        const int r0 = gb[k + 1], rows = gb[k + 2] - gb[k + 1];
+        if (rows <= 0) continue;
+        float *x = c->d_oxc + (size_t)r0 * c->L;
+        if (c->opp_has_norm[k])
+            TRY(launch_obs_norm_rows_on(c, rows, x + c->G, c->L, nullptr, c->d_opp_on + (size_t)k * (2 * c->D + 1)));
+        TRY(wide_forward_actor(c, rows, x, c->L, c->d_opp_params + (size_t)k * np, c->d_ologits + (size_t)r0 * c->A));
+    }
+    const int n = c->N * c->A;
+    hipLaunchKernelGGL(k_opp_select, dim3((n + 255) / 256), dim3(256), 0, c->stream, c->N, c->A, c->d_group,
+                       c->d_gpos, c->d_ologits, c->d_logits);
+    BPPO_HIP(c, hipGetLastError());
     return BPPO_OK;
 }
 
 bppo_status opp_step_seats(bppo_ctx *c, int t) {
     const size_t r0 = (size_t)t * c->N;
-    hipLaunchKernelGGL(k_opp_seats, dim3(1), dim3(256), 0, c->stream, c->N, c->n_opp, c->P, c->A, c->d_done + r0,
+    hipLaunchKernelGGL(k_opp_seats, dim3(1), dim3(SEAT_THREADS), 0, c->stream, c->N, c->n_opp, c->P, c->A, c->d_done + r0,
                        c->d_players + r0, c->rng_key, (uint64_t)c->cfg.rng_stream, c->d_curopp, c->d_rngpos,
                        c->d_lpos, c->d_p2o, c->d_valid + r0);
     BPPO_HIP(c, hipGetLastError());

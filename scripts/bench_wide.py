@@ -1,6 +1,7 @@
 """Throughput of the multi-player workloads (SURVEY CfgC / CfgD) on one MI355X.
 
     python scripts/bench_wide.py --workload cfgC|cfgD [--steps K --warmup W]
+                                 [--opponents K --opponent-frac F]
 
 Not the driver's bench line (bench.py measures BASELINE.json's CfgB): this
 prints one JSON line per workload with env-steps/s of a full update (rollout +
@@ -29,6 +30,10 @@ def main():
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--num-envs", type=int, default=None)
     p.add_argument("--no-kl-stop", action="store_true", help="run every epoch (target_kl off)")
+    p.add_argument("--opponents", type=int, default=0,
+                   help="opponent-pool rollouts (ppo.rs:537-1063) against K loaded models")
+    p.add_argument("--opponent-frac", type=float, default=0.25,
+                   help="opponent_pool_fraction (configs/liars_dice*.toml: 0.25)")
     a = p.parse_args()
     import torch
     import bppo
@@ -39,6 +44,16 @@ def main():
     cfg = bppo.make_config(w["preset"], num_envs=w["num_envs"], num_steps=w["num_steps"], **over)
     torch.cuda.set_device(0)
     tr = bppo.Trainer(cfg, init_seed=0)
+    if a.opponents:
+        import numpy as np
+        P = tr.ctx.num_players
+        n_opp = max(1, int(w["num_envs"] * a.opponent_frac))          # main.rs:621-637
+        rng = np.random.default_rng(0)
+        opp = np.stack([bppo.orthogonal_init(cfg, seed=50 + k) for k in range(a.opponents)])
+        lp = rng.integers(0, P, n_opp).astype(np.int32)
+        po = np.where(np.arange(P)[None, :] == lp[:, None], -1,
+                      rng.integers(0, a.opponents, (n_opp, P))).astype(np.int32)
+        tr.ctx.set_opponents(opp, None, n_opp, lp, po, rng.integers(0, a.opponents, P - 1))
     for _ in range(a.warmup):
         tr.train_update()
     torch.cuda.synchronize()
@@ -53,7 +68,8 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     B = w["num_envs"] * w["num_steps"]
-    out = {"workload": a.workload, "env_steps_per_sec": round(B * a.steps / dt, 1),
+    out = {"workload": a.workload + (f"+opponents{a.opponents}@{a.opponent_frac}" if a.opponents else ""),
+           "env_steps_per_sec": round(B * a.steps / dt, 1),
            "ms_per_update": round(dt / a.steps * 1000, 2), "num_envs": w["num_envs"],
            "num_steps": w["num_steps"], "minibatches_per_update": ups / a.steps,
            "phase_ms_per_update": {k: round(v / a.steps, 2) for k, v in ph.items()},
