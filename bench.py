@@ -31,6 +31,11 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md: FP32 vector / matrix dense peak
 FLOP_PER_ROW_FWD_BWD = 27_008  # CfgB forward + backward per env-step (per minibatch row)
 GAE_BYTES_PER_ELEM = 20        # r, d, v in; adv, ret out (f32)
+# rocprofv3 PMC, CfgB, per launch (profiles/r01k_pmc_traffic.txt). FETCH_SIZE/WRITE_SIZE are KiB;
+# k_gae_1p's 16-B/lane streaming reads take the gfx950 x2 FETCH_SIZE correction, the minibatch
+# kernel's 64-B row gathers do not (raw FETCH = 1.03 x the 2097152 x 64 B packed rows).
+MB_TRAFFIC_BYTES = int((134902.7 + 4756.0) * 1024)
+GAE_TRAFFIC_BYTES = int((2 * 49302.0 + 65536.0) * 1024)
 
 
 def parse():
@@ -124,15 +129,21 @@ def main():
     mb_ms = phase["minibatch"] / args.steps          # last minibatch launch of each update
     flops = mb_rows * FLOP_PER_ROW_FWD_BWD
     achieved = flops / (mb_ms * 1e-3) / 1e12
+    # HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes on CfgB
+    # (scripts/pmc_traffic.sh, profiles/r01k_pmc_traffic.txt); PMC cannot be read live here,
+    # so it is reported only for the configuration it was measured on.
+    pmc_cfg = (N == 65536 and T == 128 and cfg["num_minibatches"] == 4)
     roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None,
+            "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
+            "traffic": MB_TRAFFIC_BYTES if pmc_cfg else None, "traffic_unit": "B/launch",
             "kernel": "k_minibatch_mfma", "launch_ms": round(mb_ms, 4),
             "algorithmic": f"{mb_rows} rows x {FLOP_PER_ROW_FWD_BWD} FLOP"}
     gae_ms = phase["gae"] / args.steps
     gae_bytes = N * T * GAE_BYTES_PER_ELEM
     gae_gbs = gae_bytes / (gae_ms * 1e-3) / 1e9
     gae_roof = {"bound": "hbm", "achieved": round(gae_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(gae_gbs / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "k_gae_1p",
+                "frac": round(gae_gbs / HBM_PEAK_GBS, 4), "traffic": GAE_TRAFFIC_BYTES if pmc_cfg else None,
+                "traffic_unit": "B/launch", "kernel": "k_gae_1p",
                 "launch_ms": round(gae_ms, 4), "algorithmic": f"{N * T} x {GAE_BYTES_PER_ELEM} B"}
     out = {"metric": METRIC, "value": round(value, 1), "unit": "env-steps/sec", "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
