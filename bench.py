@@ -1,25 +1,39 @@
 """bench.py — env-steps/sec of burn-ppo's hot path (rollout + GAE + PPO update)
-on MI355X.
+on MI355X, plus the CartPole steps-to-475 learning metric.
 
 One "step" = one full PPO update of CfgB: CartPole, num_envs=65536
 per GPU, num_steps=128, 2x64 relu MLP, 4 epochs x 4 minibatches (configs/cartpole.toml),
 i.e. 8,388,608 env-steps per GPU per step, synthetic fixed-seed data (seed 42).
 
-N>1 runs as one process per GPU (torch.distributed.run): each rank owns its own
-65536 envs (global env index rank*65536 + i) and the gradient is all-reduced
-(RCCL over xGMI) once per minibatch, enqueued on the context's stream (the host
-never waits per minibatch); weak scaling.
+N>1 runs as one process per GPU.  `python bench.py --gpus N` starts the N ranks
+itself (a torch.distributed.run child process) when it is not already running
+under a launcher; each rank owns its own 65536 envs (global env index
+rank*65536 + i) and the gradient is all-reduced (RCCL over xGMI, the
+torch.distributed "nccl" backend) once per minibatch, enqueued on the context's
+stream (the host never waits per minibatch); weak scaling.
 
-Prints ONE JSON line (rank 0).  `roofline` is the dominant kernel's (the fused
-minibatch forward/backward) algorithmic FLOP rate against the FP32 dense peak;
-`gae_roofline` the GAE scan's algorithmic HBM rate; `cpu_baseline` the CPU
-oracle (a restatement of the reference's ndarray path) timed on a bounded sample
-of the same workload on this host.
+Prints ONE JSON line (rank 0):
+  roofline      the dominant kernel (fused minibatch forward/loss/backward):
+                algorithmic FLOP rate against the FP32 dense peak, timed with HIP
+                events on the context's stream; `traffic` = HBM bytes per launch
+                from the rocprofv3 PMC passes in pmc_traffic.json, reported only
+                when that profile was taken of the current kernel source;
+  gae_roofline  the GAE scan's algorithmic HBM rate (north star: >= 40 %);
+  steps_to_475  global_step at which the 100-episode rolling mean return
+                (main.rs:842-853) first reaches 475 (CartPole-v1 solved, max 500),
+                for CfgB and for configs/cartpole.toml (N=32, T=128), trained
+                outside the timed region (rank 0, N=1 only);
+  cpu_baseline  the CPU oracle (C restatement of the reference's ndarray path)
+                timed on a bounded sample of the same workload on this host.
+`--selftest` runs the launcher, rank plumbing, barrier and max-over-ranks
+timing with gloo and no GPU work (the CPU test of the N>1 harness).
 """
 import argparse
-import ctypes as C
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -31,11 +45,8 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md: FP32 vector / matrix dense peak
 FLOP_PER_ROW_FWD_BWD = 27_008  # CfgB forward + backward per env-step (per minibatch row)
 GAE_BYTES_PER_ELEM = 20        # r, d, v in; adv, ret out (f32)
-# rocprofv3 PMC, CfgB, per launch (profiles/r01k_pmc_traffic.txt). FETCH_SIZE/WRITE_SIZE are KiB;
-# k_gae_1p's 16-B/lane streaming reads take the gfx950 x2 FETCH_SIZE correction, the minibatch
-# kernel's 64-B row gathers do not (raw FETCH = 1.03 x the 2097152 x 64 B packed rows).
-MB_TRAFFIC_BYTES = int((134902.7 + 4756.0) * 1024)
-GAE_TRAFFIC_BYTES = int((2 * 49302.0 + 65536.0) * 1024)
+TRAFFIC_JSON = os.path.join(ROOT, "pmc_traffic.json")   # copy of a scripts/pmc_traffic.sh summary
+CSRC = os.path.join(ROOT, "burn-ppo_amd", "csrc")
 
 
 def parse():
@@ -45,39 +56,158 @@ def parse():
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--num-envs", type=int, default=65536, help="envs per GPU")
     p.add_argument("--num-steps", type=int, default=128)
-    p.add_argument("--cpu-envs", type=int, default=1024, help="CPU baseline sample size (envs)")
+    p.add_argument("--cpu-envs", type=int, default=2048, help="CPU baseline sample size (envs)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-learning", action="store_true", help="skip the steps-to-475 runs")
+    p.add_argument("--selftest", action="store_true", help="N>1 harness check with gloo and no GPU work")
     return p.parse_args()
 
 
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """--gpus N without a launcher: run N ranks under torch.distributed.run as a
+    CHILD process (nothing here has touched the GPU) and exit with its code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def host_cpu_budget(local_world):
+    """CPUs this rank may use for the shuffle engine's host threads: the CPUs
+    the process may run on (affinity, cgroup quota) / ranks on this node."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n // max(1, local_world))
+
+
+def traffic_for(kernel, source):
+    """HBM bytes per launch from the committed PMC summary, only if it profiled
+    the current source of the kernel."""
+    try:
+        prof = json.load(open(TRAFFIC_JSON))
+        e = prof["kernels"][kernel]
+    except (OSError, KeyError, ValueError):
+        return None, "no PMC profile"
+    sha = hashlib.sha256(open(os.path.join(CSRC, source), "rb").read()).hexdigest()[:16]
+    if e.get("source_sha") != sha or "traffic_bytes" not in e:
+        return None, f"PMC profile {prof.get('tag')} is of other {source} source"
+    return e["traffic_bytes"], f"rocprofv3 FETCH_SIZE x{e['fetch_correction']:g} + WRITE_SIZE ({prof.get('tag')})"
+
+
 def cpu_baseline(args):
-    """The oracle (CPU restatement of the reference ndarray path) on a bounded
-    sample: same config, num_envs = --cpu-envs, one full update."""
+    """The oracle (C restatement of the reference ndarray path) on a bounded
+    sample: CfgB's config at num_envs = --cpu-envs, 1 warm-up update then 2
+    timed full updates.  Env stepping OpenMP over all host threads (rayon in the
+    reference); MLP, GAE, normalizers, sampling and shuffle single-threaded (the
+    reference's matrixmultiply sgemm and serial loops).  Every phase is linear in
+    T*N, so env-steps/s at this N stands for CfgB's."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import numpy as np
     import oracle_ffi as O
     import bppo
     n = args.cpu_envs
     cfg = bppo.make_config("cartpole", num_envs=n, num_steps=args.num_steps)
     params = bppo.orthogonal_init(cfg, seed=0)
+    O.lib().or_set_mlp_parallel(0)
     ot = O.Trainer(O.train_cfg(num_envs=n, num_steps=args.num_steps, lr=1e-3), params)
+    ot.collect(); ot.gae(); ot.update()          # warm-up
     t0 = time.perf_counter()
-    ot.collect(); ot.gae(); ot.update()
+    for _ in range(2):
+        ot.collect(); ot.gae(); ot.update()
     dt = time.perf_counter() - t0
     ot.close()
+    O.lib().or_set_mlp_parallel(1)
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    return {"value": n * args.num_steps / dt, "unit": "env-steps/sec", "cores": threads,
-            "kind": "port",
-            "sample": f"1 full update (rollout+GAE+4x4 PPO) of CfgB at num_envs={n}, T={args.num_steps}; "
-                      f"env stepping OpenMP x{threads}, MLP/GAE/shuffle single-threaded; {dt:.1f}s"}
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": 2 * n * args.num_steps / dt, "unit": "env-steps/sec", "cores": threads, "kind": "port",
+            "cpu": model,
+            "sample": f"CfgB config (cartpole.toml, 2x64 relu, 4x4 PPO) at num_envs={n}, T={args.num_steps}: "
+                      f"1 warm-up + 2 timed full updates (rollout+GAE+update) = {2 * n * args.num_steps} env-steps "
+                      f"in {dt:.1f}s; env stepping OpenMP x{threads}, MLP/GAE/normalizers/sampling/shuffle "
+                      f"single-threaded as in the reference; per-env-step cost is independent of N"}
+
+
+def steps_to_475(bppo, preset_over, max_steps, init_seed=0):
+    """Train until the 100-episode rolling mean return (main.rs:842-853) reaches
+    475; -> global_step after that rollout, or None within max_steps."""
+    cfg = bppo.make_config("cartpole", **preset_over)
+    tr = bppo.Trainer(cfg, init_seed=init_seed)
+    T, N = cfg["num_steps"], cfg["num_envs"]
+    step, best, reached, t0 = 0, 0.0, None, time.perf_counter()
+    try:
+        while step < max_steps:
+            tr.train_update(track_returns=True)
+            step += T * N
+            mr = tr.mean_recent_return()
+            best = max(best, mr)
+            if len(tr.recent_returns) == 100 and mr >= 475.0:
+                reached = step
+                break
+    finally:
+        tr.close()
+    return {"steps": reached, "best_mean_return": round(best, 2), "updates": step // (T * N),
+            "num_envs": N, "num_steps": T, "seconds": round(time.perf_counter() - t0, 2)}
+
+
+def selftest_main(args, world, rank):
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    x = torch.ones(4)
+    for _ in range(args.warmup):
+        dist.all_reduce(x)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dist.all_reduce(x)
+    dist.barrier()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        assert world == args.gpus, (world, args.gpus)
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "env-steps/sec", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "ms_per_step": float(t.item()) / args.steps * 1e3,
+                          "higher_is_better": True, "scaling": "weak", "selftest": True,
+                          "data": "selftest: launcher + gloo ranks, no GPU work",
+                          "config": {"parallelism": f"dp{world}", "backend": "gloo"}}), flush=True)
+    dist.destroy_process_group()
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    import numpy as np
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
+    if args.selftest:
+        return selftest_main(args, world, rank)
+    os.environ.setdefault("BPPO_HOST_THREADS", str(host_cpu_budget(local_world)))
     import torch
     import bppo
     dist = None
@@ -118,6 +248,7 @@ def main():
         t = torch.tensor([dt], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    tr.close()
     if rank != 0:
         dist.destroy_process_group()
         return
@@ -127,24 +258,20 @@ def main():
     # dominant kernel: the fused minibatch forward/loss/backward (16 launches per update)
     mb_rows = N * T // cfg["num_minibatches"]
     mb_ms = phase["minibatch"] / args.steps          # last minibatch launch of each update
-    flops = mb_rows * FLOP_PER_ROW_FWD_BWD
-    achieved = flops / (mb_ms * 1e-3) / 1e12
-    # HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes on CfgB
-    # (scripts/pmc_traffic.sh, profiles/r01k_pmc_traffic.txt); PMC cannot be read live here,
-    # so it is reported only for the configuration it was measured on.
-    pmc_cfg = (N == 65536 and T == 128 and cfg["num_minibatches"] == 4)
+    achieved = mb_rows * FLOP_PER_ROW_FWD_BWD / (mb_ms * 1e-3) / 1e12
+    cfgB = (N == 65536 and T == 128)
+    mb_tr, mb_src = traffic_for("k_minibatch_mfma", "k_update.hip") if cfgB else (None, "not the profiled shape")
     roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
-            "traffic": MB_TRAFFIC_BYTES if pmc_cfg else None, "traffic_unit": "B/launch",
-            "kernel": "k_minibatch_mfma", "launch_ms": round(mb_ms, 4),
+            "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": mb_tr, "traffic_unit": "B/launch",
+            "traffic_source": mb_src, "kernel": "k_minibatch_mfma", "launch_ms": round(mb_ms, 4),
             "algorithmic": f"{mb_rows} rows x {FLOP_PER_ROW_FWD_BWD} FLOP"}
     gae_ms = phase["gae"] / args.steps
-    gae_bytes = N * T * GAE_BYTES_PER_ELEM
-    gae_gbs = gae_bytes / (gae_ms * 1e-3) / 1e9
+    gae_gbs = N * T * GAE_BYTES_PER_ELEM / (gae_ms * 1e-3) / 1e9
+    g_tr, g_src = traffic_for("k_gae_1p_seg", "k_gae.hip") if cfgB else (None, "not the profiled shape")
     gae_roof = {"bound": "hbm", "achieved": round(gae_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(gae_gbs / HBM_PEAK_GBS, 4), "traffic": GAE_TRAFFIC_BYTES if pmc_cfg else None,
-                "traffic_unit": "B/launch", "kernel": "k_gae_1p",
-                "launch_ms": round(gae_ms, 4), "algorithmic": f"{N * T} x {GAE_BYTES_PER_ELEM} B"}
+                "frac": round(gae_gbs / HBM_PEAK_GBS, 4), "traffic": g_tr, "traffic_unit": "B/launch",
+                "traffic_source": g_src, "kernel": "k_gae_1p_seg", "launch_ms": round(gae_ms, 4),
+                "algorithmic": f"{N * T} x {GAE_BYTES_PER_ELEM} B"}
     out = {"metric": METRIC, "value": round(value, 1), "unit": "env-steps/sec", "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
@@ -152,18 +279,26 @@ def main():
            "config": {"workload": "CfgB: CartPole num_envs=65536/GPU num_steps=128, 2x64 relu MLP, "
                                   "4 epochs x 4 minibatches (configs/cartpole.toml)",
                       "num_envs_per_gpu": N, "num_steps": T, "env_steps_per_update": N * T * world,
-                      "parallelism": f"dp{world}"},
+                      "parallelism": f"dp{world}",
+                      "collective": ("RCCL all-reduce (torch.distributed nccl) of the gradient, 1 per minibatch, "
+                                     "stream-ordered" if world > 1 else None),
+                      "w_gt_1_semantics": ("per-rank obs/return normalizers and per-rank minibatch advantage "
+                                           "stats (SURVEY 8e); parity is defined at N=1" if world > 1 else None),
+                      "host_cpus_per_rank": int(os.environ["BPPO_HOST_THREADS"])},
            "roofline": roof, "gae_roofline": gae_roof,
            "phase_ms_per_update": {k: round(v / args.steps, 3) for k, v in phase.items()},
            "last_update": {k: (round(v, 5) if isinstance(v, float) else v) for k, v in last.items()
                            if k in ("policy_loss", "value_loss", "entropy", "approx_kl", "mean_return",
                                     "episodes", "explained_variance")}}
-    if not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args)
+    if world == 1 and not args.no_learning:
+        out["steps_to_475"] = {
+            "window": "100 episodes (main.rs:842-853), checked after each rollout",
+            "cfgB": steps_to_475(bppo, dict(num_envs=N, num_steps=T), max_steps=40 * N * T),
+            "cartpole_toml": steps_to_475(bppo, dict(num_envs=32, num_steps=128), max_steps=1_000_000)}
     else:
-        out["cpu_baseline"] = None
+        out["steps_to_475"] = None
+    out["cpu_baseline"] = None if args.no_cpu_baseline else cpu_baseline(args)
     print(json.dumps(out), flush=True)
-    tr.close()
     if dist:
         dist.destroy_process_group()
 

@@ -68,7 +68,7 @@ EXPORTS = (
     "bppo_collect_rollouts", "bppo_rollout_episodes", "bppo_compute_gae", "bppo_ppo_update",
     "bppo_set_allreduce", "bppo_set_allreduce_async", "bppo_get_stream", "bppo_opponents_set", "bppo_opponents_get_envs", "bppo_buffer_get", "bppo_buffer_set", "bppo_gae_device",
     "bppo_gae_mp_device", "bppo_last_kernel_ms", "bppo_debug_libm", "bppo_debug_shuffle_chain",
-    "bppo_debug_fisher_yates", "bppo_debug_gemm", "bppo_debug_shuffle_engine",
+    "bppo_debug_fisher_yates", "bppo_debug_gemm", "bppo_debug_shuffle_engine", "bppo_debug_sample",
 )
 
 _lib = None
@@ -132,6 +132,7 @@ def lib():
         "bppo_debug_fisher_yates": (i32, [i32, vp, C.c_uint32, vp]),
         "bppo_debug_gemm": (i32, [i32, i32, i32, i32, vp, vp, vp, i32, vp, vp]),
         "bppo_debug_shuffle_engine": (i32, [u64, u64, u64, C.c_uint32, i32, u64, i32, vp, vp, vp]),
+        "bppo_debug_sample": (i32, [i32, i32, vp, vp, u64, u64, u64, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

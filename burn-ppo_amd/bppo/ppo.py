@@ -16,6 +16,7 @@ marshal host arrays.  Errors that the reference panics on (NaN log-probs,
 empty action masks) raise BppoError.
 """
 import ctypes as C
+from collections import deque
 
 import numpy as np
 
@@ -289,6 +290,21 @@ def collect_rollouts(ctx):
     return info
 
 
+def rollout_episodes(ctx):
+    """EpisodeStats of the last rollout in the reference's order: by step, then
+    env index (env.rs:470-483 appends completed envs in env order each step)."""
+    n = C.c_int32()
+    ctx._chk(L.lib().bppo_rollout_episodes(ctx.h, None, 0, C.byref(n)))
+    cap = n.value
+    if cap == 0:
+        return []
+    eps = (L.Episode * cap)()
+    ctx._chk(L.lib().bppo_rollout_episodes(ctx.h, eps, cap, C.byref(n)))
+    P = ctx.num_players
+    return [dict(total_rewards=list(eps[i].total_reward[:P]), length=eps[i].length, env_index=eps[i].env_index,
+                 step=eps[i].step) for i in range(min(n.value, cap))]
+
+
 def compute_gae(ctx):
     """main.rs:877-947 bootstrap (updated obs stats) + ppo.rs:1069-1124."""
     ctx._chk(L.lib().bppo_compute_gae(ctx.h))
@@ -316,13 +332,22 @@ class Trainer:
         self.buffer = RolloutBuffer(self.ctx)
         self.model.set_params(orthogonal_init(self.cfg, init_seed) if params is None else params)
         self.global_step = 0
-        self.recent_returns = []
+        # main.rs:850-853: the last 100 completed episodes' returns (player 0)
+        self.recent_returns = deque(maxlen=100)
 
-    def train_update(self):
+    def mean_recent_return(self):
+        return float(np.mean(self.recent_returns)) if self.recent_returns else float("nan")
+
+    def train_update(self, track_returns=False):
+        """one iteration of main.rs:684-988.  track_returns: push this rollout's
+        completed episodes into the 100-episode window (main.rs:842-853)."""
         lr = schedule_get(self.cfg["learning_rate"], self.global_step)         # main.rs:706
         ent = schedule_get(self.cfg["entropy_coef"], self.global_step)         # main.rs:716
         self.vec_env.set_step(self.global_step)
         info = collect_rollouts(self.ctx)
+        if track_returns:
+            for ep in rollout_episodes(self.ctx):
+                self.recent_returns.append(ep["total_rewards"][0])
         compute_gae(self.ctx)
         metrics = ppo_update(self.ctx, lr, ent)
         self.global_step += self.ctx.T * self.ctx.N                           # main.rs:988

@@ -147,10 +147,16 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     TRY(dalloc(c, &c->d_ret, TN));
     TRY(dalloc(c, &c->d_act, TN));
     if (!c->wide || cfg->normalize_returns) TRY(dalloc(c, &c->d_X, TN));
-    if (!c->wide && cfg->hidden_size == 64 && cfg->num_hidden == 2 && cfg->relu && !getenv("BPPO_VALU_ROLLOUT"))
+    if (!c->wide && cfg->hidden_size == 64 && cfg->num_hidden == 2 && cfg->relu)
         TRY(dalloc(c, &c->d_gumbel, TN * 2));
     TRY(dalloc(c, &c->d_on, (size_t)2 * c->D + 1));
     if (!c->wide) TRY(dalloc(c, &c->d_obs_part, (size_t)c->N * 2 * c->D));
+    if (!c->wide) {   // VecEnv::step / get_observations scratch (freed by wide_free with the rest)
+        TRY(dalloc(c, &c->d_act_in, (size_t)c->N));
+        TRY(dalloc(c, &c->d_scr_r, (size_t)c->N));
+        TRY(dalloc(c, &c->d_bxc, (size_t)c->N * c->D));
+        BPPO_HIP(c, hipMalloc((void **)&c->d_scr_d, (size_t)c->N));
+    }
     TRY(dalloc(c, &c->d_rn_returns, (size_t)c->N * c->P));
     TRY(dalloc(c, &c->d_rn_stats, 4));
     TRY(dalloc(c, &c->d_scan_agg, (TN + 4095) / 4096 + 1));
@@ -283,12 +289,9 @@ extern "C" bppo_status bppo_vecenv_observe(bppo_ctx *c, float *obs, int32_t *pla
     if (!c) return BPPO_ERR_ARG;
     if (c->wide) return wide_observe_host(c, obs, players, masks, priv);
     if (obs) {
-        float *d = nullptr;
-        BPPO_HIP(c, hipMalloc((void **)&d, sizeof(float) * (size_t)c->N * c->D));
-        TRY(launch_cartpole_observe(c, d));
-        BPPO_HIP(c, hipMemcpyAsync(obs, d, sizeof(float) * (size_t)c->N * c->D, hipMemcpyDeviceToHost, c->stream));
+        TRY(launch_cartpole_observe(c, c->d_bxc));
+        BPPO_HIP(c, hipMemcpyAsync(obs, c->d_bxc, sizeof(float) * (size_t)c->N * c->D, hipMemcpyDeviceToHost, c->stream));
         BPPO_HIP(c, sync_stream(c));
-        (void)hipFree(d);
     }
     if (players) std::fill(players, players + c->N, 0);
     return BPPO_OK;
@@ -317,11 +320,8 @@ extern "C" bppo_status bppo_vecenv_step(bppo_ctx *c, const int32_t *actions, flo
         c->global_step += N;
         return BPPO_OK;
     }
-    int32_t *d_a = nullptr; float *d_r = nullptr, *d_o = nullptr; uint8_t *d_d = nullptr;
-    BPPO_HIP(c, hipMalloc((void **)&d_a, sizeof(int32_t) * N));
-    BPPO_HIP(c, hipMalloc((void **)&d_r, sizeof(float) * N));
-    BPPO_HIP(c, hipMalloc((void **)&d_d, N));
-    BPPO_HIP(c, hipMalloc((void **)&d_o, sizeof(float) * (size_t)N * c->D));
+    // persistent scratch (ctx_init): no allocator round-trip per step
+    int32_t *d_a = c->d_act_in; float *d_r = c->d_scr_r, *d_o = c->d_bxc; uint8_t *d_d = c->d_scr_d;
     BPPO_HIP(c, hipMemcpyAsync(d_a, actions, sizeof(int32_t) * N, hipMemcpyHostToDevice, c->stream));
     BPPO_HIP(c, hipMemsetAsync(c->d_ep_count, 0, 4, c->stream));
     TRY(launch_cartpole_vecenv_step(c, d_a, d_r, d_d, d_o));
@@ -344,7 +344,6 @@ extern "C" bppo_status bppo_vecenv_step(bppo_ctx *c, const int32_t *actions, flo
         }
     }
     c->global_step += N;
-    (void)hipFree(d_a); (void)hipFree(d_r); (void)hipFree(d_d); (void)hipFree(d_o);
     return BPPO_OK;
 }
 
@@ -430,8 +429,12 @@ extern "C" bppo_status bppo_collect_rollouts(bppo_ctx *c, bppo_rollout_info *inf
     tm_read(c, TM_ROLLOUT); tm_read(c, TM_RETNORM);
     c->collected = 1; c->gae_done = 0;
     c->global_step += TN;
+    // device error bits: 1 non-finite log-prob, 2 empty action mask, 4 opponent seat
+    // table names a model outside [0, n_models)
     if (hv[1] & 2) { c->err = "Empty action mask: an env has no valid action"; return BPPO_ERR_EMPTY_MASK; }
-    if (hv[1]) { c->err = "NaN/Inf in log probs — model producing corrupt logits"; return BPPO_ERR_NONFINITE; }
+    if (hv[1] & 1) { c->err = "NaN/Inf in log probs — model producing corrupt logits"; return BPPO_ERR_NONFINITE; }
+    if (hv[1] & 4) { c->err = "opponent pool: pos_to_opp names a model index outside [0, n_models)"; return BPPO_ERR_ARG; }
+    if (hv[1]) { c->err = "collect_rollouts: unknown device error flag"; return BPPO_ERR_HIP; }
     if (info) {
         info->episodes = hv[0];
         info->rng_word_pos = c->rng_pos;
@@ -451,10 +454,14 @@ extern "C" bppo_status bppo_collect_rollouts(bppo_ctx *c, bppo_rollout_info *inf
 extern "C" bppo_status bppo_rollout_episodes(bppo_ctx *c, bppo_episode *eps, int32_t cap, int32_t *n) {
     if (!c) return BPPO_ERR_ARG;
     int32_t cnt = 0;
-    BPPO_HIP(c, hipMemcpy(&cnt, c->d_ep_count, 4, hipMemcpyDeviceToHost));
+    BPPO_HIP(c, hipMemcpyAsync(&cnt, c->d_ep_count, 4, hipMemcpyDeviceToHost, c->stream));
+    BPPO_HIP(c, sync_stream(c));
     int m = std::min(cnt, c->eps_cap);
     std::vector<EpisodeRec> recs(m);
-    if (m) BPPO_HIP(c, hipMemcpy(recs.data(), c->d_eps, sizeof(EpisodeRec) * m, hipMemcpyDeviceToHost));
+    if (m) {
+        BPPO_HIP(c, hipMemcpyAsync(recs.data(), c->d_eps, sizeof(EpisodeRec) * m, hipMemcpyDeviceToHost, c->stream));
+        BPPO_HIP(c, sync_stream(c));
+    }
     // reference order: by step, then env index (env.rs:470-483 collects in env order per step)
     std::sort(recs.begin(), recs.end(), [](const EpisodeRec &a, const EpisodeRec &b) {
         return a.step != b.step ? a.step < b.step : a.env_index < b.env_index; });
@@ -547,6 +554,9 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
             TRY(launch_fisher_yates(c, c->shuf.d_J[slot] + (size_t)ep * B, (uint32_t)B));
             (void)hipEventRecord(s1, c->stream);
         }
+        // no learner rows (opponent pool): the reference shuffles an empty index
+        // list (no RNG words) and skips every minibatch (ppo.rs:1815-1831)
+        if (B == 0) continue;
         TRY(launch_epoch_adv_stats(c, (uint32_t)B, M));
         size_t start = 0;
         for (int mb = 0; mb < M; mb++) {
@@ -652,7 +662,8 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
             tam += r[NM]; tas += r[NM + 1];
             tamin = std::min(tamin, r[NM + 2]); tamax = std::max(tamax, r[NM + 3]);
         }
-        const float n = (float)std::max(nup, 1);
+        // averaged over the minibatches run; none run -> 0/0 = NaN as in ppo.rs:2071-2090
+        const float n = (float)nup;
         m->policy_loss = tp / n; m->value_loss = tv / n; m->entropy = th / n;
         m->entropy_scaled = m->entropy / logf((float)c->A);
         m->approx_kl = tk / n; m->clip_fraction = tc / n; m->total_loss = tl / n;
@@ -662,7 +673,8 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
         const double Bn = (double)B;
         const double mr = ev4[0] / Bn, vr = ev4[1] / Bn - mr * mr;
         const double mres = ev4[2] / Bn, vres = ev4[3] / Bn - mres * mres;
-        m->explained_variance = vr < 1e-8 ? 0.0f : (float)(1.0 - vres / vr);
+        // ppo.rs:1268-1294 (fewer than 2 rows or Var(R) < 1e-8 -> 0)
+        m->explained_variance = (B < 2 || vr < 1e-8) ? 0.0f : (float)(1.0 - vres / vr);
         if (c->wide) { m->avg_valid_actions = tav / n; m->entropy_valid_pct = tevp / n; }
         m->num_updates = nup; m->epochs_run = epochs_run;
     }
@@ -847,5 +859,44 @@ extern "C" bppo_status bppo_debug_fisher_yates(int32_t device, const uint32_t *J
         s = BPPO_OK;
     (void)hipFree(dJ); (void)hipFree(dP); (void)hipFree(dS); (void)hipFree(dC);
     fy_ranges_free(rg);
+    return s;
+}
+
+// apply_action_mask + sample_categorical + log_prob_categorical (utils.rs:10-45,
+// 96-135) on host rows through the device sampler the multi-player rollout uses
+// (k_sample_masked): Gumbel words of StdRng(seed) stream `stream` from word_pos,
+// row-major [row][action]; masks may be NULL (all valid)
+extern "C" bppo_status bppo_debug_sample(int32_t A, int32_t B, const float *logits, const uint8_t *masks,
+                                         uint64_t seed, uint64_t stream, uint64_t word_pos, int32_t *actions,
+                                         float *log_probs) {
+    if (!logits || !actions || B <= 0 || (A != 2 && A != 7 && A != 49)) return BPPO_ERR_ARG;
+    const size_t nA = (size_t)B * A;
+    float *d_l = nullptr, *d_v = nullptr, *d_lp = nullptr, *d_val = nullptr, *d_lv = nullptr;
+    uint8_t *d_m = nullptr;
+    int32_t *d_p = nullptr, *d_a = nullptr, *d_e = nullptr;
+    bppo_status s = BPPO_ERR_HIP;
+    std::vector<uint8_t> ones;
+    if (!masks) { ones.assign(nA, 1); masks = ones.data(); }
+    int32_t err = 0;
+    if (hipMalloc((void **)&d_l, nA * 4) == hipSuccess && hipMalloc((void **)&d_m, nA) == hipSuccess &&
+        hipMalloc((void **)&d_v, 4ull * B) == hipSuccess && hipMalloc((void **)&d_lp, 4ull * B) == hipSuccess &&
+        hipMalloc((void **)&d_val, 4ull * B) == hipSuccess && hipMalloc((void **)&d_lv, 4ull * B) == hipSuccess &&
+        hipMalloc((void **)&d_p, 4ull * B) == hipSuccess && hipMalloc((void **)&d_a, 4ull * B) == hipSuccess &&
+        hipMalloc((void **)&d_e, 4) == hipSuccess && hipMemset(d_v, 0, 4ull * B) == hipSuccess &&
+        hipMemset(d_p, 0, 4ull * B) == hipSuccess && hipMemset(d_e, 0, 4) == hipSuccess &&
+        hipMemcpy(d_l, logits, nA * 4, hipMemcpyHostToDevice) == hipSuccess &&
+        hipMemcpy(d_m, masks, nA, hipMemcpyHostToDevice) == hipSuccess) {
+        SampleArgs g;
+        g.N = B; g.P = 1; g.logits = d_l; g.values = d_v; g.mask = d_m; g.players = d_p;
+        g.key = seed_key(seed); g.stream = stream; g.base = word_pos;
+        g.act = d_a; g.logp = d_lp; g.val = d_val; g.lvpp = d_lv; g.err = d_e;
+        if (wide_sample(A, nullptr, g) == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
+            hipMemcpy(actions, d_a, 4ull * B, hipMemcpyDeviceToHost) == hipSuccess &&
+            (!log_probs || hipMemcpy(log_probs, d_lp, 4ull * B, hipMemcpyDeviceToHost) == hipSuccess) &&
+            hipMemcpy(&err, d_e, 4, hipMemcpyDeviceToHost) == hipSuccess)
+            s = (err & 2) ? BPPO_ERR_EMPTY_MASK : (err & 1) ? BPPO_ERR_NONFINITE : BPPO_OK;
+    }
+    void *ptrs[] = {d_l, d_m, d_v, d_lp, d_val, d_lv, d_p, d_a, d_e};
+    for (void *q : ptrs) if (q) (void)hipFree(q);
     return s;
 }

@@ -92,6 +92,7 @@ struct ShuffleEngine {
     uint64_t gap = 0;                             // words between an update's last shuffle and the next update's first
     double Ew = 0.0, sigma = 0.0;                 // expected words per shuffle, its std dev
     int K = 0;                                    // speculative walks per epoch boundary
+    int host_cpus = 16;                           // CPU budget of this rank (BPPO_HOST_THREADS)
     WordBuf wb[2];                                // double-buffered by job parity
     // walker slots: [0, ncur) K per epoch C..E-1 of the current job; then two
     // (by job parity) carry groups of C*K for the next job's epochs 0..C-1

@@ -45,16 +45,6 @@ struct WaveB {
 constexpr size_t LDSB = sizeof(Params) + WAVES * sizeof(WaveB);
 static_assert(LDSB <= 160 * 1024, "minibatch kernel LDS over the gfx950 limit");
 
-// 64-row tiles (two 32-row MFMA tiles per wave, one wave per SIMD, 512 VGPRs)
-constexpr int TR64 = 64;
-struct Wave64 {
-    float X[TR64 * 9];
-    float T[TR64 * RS];
-    float dl[TR64 * 4];
-};
-constexpr int WAVES64 = 4;
-constexpr size_t LDS64 = sizeof(Params) + WAVES64 * sizeof(Wave64);
-
 // whole block: flat Burn-order params -> LDS layout
 __device__ __forceinline__ void load_params(Params &S, const float *__restrict__ P) {
     constexpr CpOffsets O = cp_offsets<64, 2>();

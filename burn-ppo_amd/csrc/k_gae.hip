@@ -60,6 +60,79 @@ __global__ void __launch_bounds__(256) k_gae_1p(const float *__restrict__ r,
     }
 }
 
+// The CfgB shape (N % 4 == 0, T <= GSEG_WAVES * GSEG_L): one block per 256 envs
+// (each lane owns 4 consecutive envs: dwordx4 loads and stores), T cut into
+// GSEG_WAVES contiguous segments of L steps, one wave per segment.  Every wave
+// issues all of its segment's loads at once (3 L + 1 dwordx4 per lane), turns
+// them into delta_t and c_t = gamma*lambda*(1-d_t) elementwise, then the serial
+// chain A_t = fma(c_t, A_{t+1}, delta_t) runs segment by segment from the last
+// (the carry between waves goes through LDS), so each element sees exactly the
+// reference's op sequence and the result is bit-identical to k_gae_1p.  16
+// waves per block keep ~16 waves per CU and ~25 x 1 KB loads in flight per wave.
+constexpr int GSEG_WAVES = 16, GSEG_L = 8;
+__global__ void __launch_bounds__(GSEG_WAVES * 64) k_gae_1p_seg(const float4 *__restrict__ r,
+                                                                 const float4 *__restrict__ d,
+                                                                 const float4 *__restrict__ v,
+                                                                 const float4 *__restrict__ lv, int T, int N4,
+                                                                 int L, float gamma, float lambda,
+                                                                 float4 *__restrict__ adv, float4 *__restrict__ ret) {
+    __shared__ float4 carry[GSEG_WAVES][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int g = blockIdx.x * 64 + lane;
+    const bool ok = g < N4;
+    const int t0 = w * L, n = max(0, min(T, t0 + L) - t0);   // this wave's steps [t0, t0 + n)
+    const float gl = gamma * lambda;
+    float4 x0[GSEG_L], x1[GSEG_L], vv[GSEG_L], vnext = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (ok) {
+#pragma unroll
+        for (int u = 0; u < GSEG_L; u++)
+            if (u < n) {
+                const size_t i = (size_t)(t0 + u) * N4 + g;
+                x0[u] = r[i]; x1[u] = d[i]; vv[u] = v[i];
+            }
+        if (n > 0) vnext = t0 + n < T ? v[(size_t)(t0 + n) * N4 + g] : lv[g];
+    }
+    // elementwise: x0 <- delta_t = fma(gamma * v_{t+1}, 1 - d_t, r_t) - v_t, x1 <- gamma*lambda*(1 - d_t)
+#pragma unroll
+    for (int u = 0; u < GSEG_L; u++) {
+        if (u >= n) continue;
+        const float4 nv = u + 1 < n ? vv[u + 1 < GSEG_L ? u + 1 : u] : vnext;
+        float4 &a = x0[u], &b = x1[u];
+        const float4 vu = vv[u];
+        float om;
+        om = 1.0f - b.x; a.x = __fsub_rn(__builtin_fmaf(gamma * nv.x, om, a.x), vu.x); b.x = gl * om;
+        om = 1.0f - b.y; a.y = __fsub_rn(__builtin_fmaf(gamma * nv.y, om, a.y), vu.y); b.y = gl * om;
+        om = 1.0f - b.z; a.z = __fsub_rn(__builtin_fmaf(gamma * nv.z, om, a.z), vu.z); b.z = gl * om;
+        om = 1.0f - b.w; a.w = __fsub_rn(__builtin_fmaf(gamma * nv.w, om, a.w), vu.w); b.w = gl * om;
+    }
+    // the serial chain, last segment first
+    for (int k = GSEG_WAVES - 1; k >= 0; k--) {
+        if (w == k) {
+            float4 A = k == GSEG_WAVES - 1 ? make_float4(0.f, 0.f, 0.f, 0.f) : carry[k + 1][lane];
+#pragma unroll
+            for (int u = GSEG_L - 1; u >= 0; u--) {
+                if (u >= n) continue;
+                A.x = __builtin_fmaf(x1[u].x, A.x, x0[u].x);
+                A.y = __builtin_fmaf(x1[u].y, A.y, x0[u].y);
+                A.z = __builtin_fmaf(x1[u].z, A.z, x0[u].z);
+                A.w = __builtin_fmaf(x1[u].w, A.w, x0[u].w);
+                x0[u] = A;
+            }
+            carry[k][lane] = A;
+        }
+        __syncthreads();
+    }
+    if (!ok) return;
+#pragma unroll
+    for (int u = 0; u < GSEG_L; u++) {
+        if (u >= n) continue;
+        const size_t i = (size_t)(t0 + u) * N4 + g;
+        const float4 A = x0[u], vu = vv[u];
+        adv[i] = A;
+        ret[i] = make_float4(__fadd_rn(A.x, vu.x), __fadd_rn(A.y, vu.y), __fadd_rn(A.z, vu.z), __fadd_rn(A.w, vu.w));
+    }
+}
+
 template <int P>
 __global__ void __launch_bounds__(256) k_gae_mp(const float *__restrict__ ar,
                                                 const int32_t *__restrict__ pl,
@@ -113,8 +186,16 @@ __global__ void __launch_bounds__(256) k_gae_mp(const float *__restrict__ ar,
 bppo_status launch_gae_1p(const float *r, const float *d, const float *v, const float *lv, int T,
                           int N, float gamma, float lambda, float *adv, float *ret, hipStream_t s) {
     if (T <= 0 || N <= 0) return BPPO_OK;
-    hipLaunchKernelGGL(k_gae_1p, dim3((N + 255) / 256), dim3(256), 0, s, r, d, v, lv, T, N, gamma,
-                       lambda, adv, ret);
+    const bool al = ((uintptr_t)r | (uintptr_t)d | (uintptr_t)v | (uintptr_t)lv | (uintptr_t)adv | (uintptr_t)ret) % 16 == 0;
+    if (N % 4 == 0 && T <= GSEG_WAVES * GSEG_L && al) {
+        const int N4 = N / 4, L = (T + GSEG_WAVES - 1) / GSEG_WAVES;
+        hipLaunchKernelGGL(k_gae_1p_seg, dim3((N4 + 63) / 64), dim3(GSEG_WAVES * 64), 0, s, (const float4 *)r,
+                           (const float4 *)d, (const float4 *)v, (const float4 *)lv, T, N4, L, gamma, lambda,
+                           (float4 *)adv, (float4 *)ret);
+    } else {
+        hipLaunchKernelGGL(k_gae_1p, dim3((N + 255) / 256), dim3(256), 0, s, r, d, v, lv, T, N, gamma,
+                           lambda, adv, ret);
+    }
     return hipGetLastError() == hipSuccess ? BPPO_OK : BPPO_ERR_HIP;
 }
 

@@ -30,7 +30,6 @@ struct MbArgs {
     float lo, hi, ceps;    // clip bounds
     float inv_mb, ent_coef, value_coef;
     int clip_value;
-    int dbg_seq;           // timing experiment only: rows read in index order (no shuffle gather)
     const float4 *rows;    // packed rows [B][4 x float4] (k_pack_rows) or nullptr
 };
 
@@ -382,7 +381,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
     const uint32_t stride = (uint32_t)nwaves * TR;
     auto idx_of = [&](uint32_t b) -> uint32_t {
         const uint32_t rr = b + c;
-        return (h == 0 && rr < g.n) ? (g.dbg_seq ? g.start + rr : g.perm[g.start + rr]) : 0xFFFFFFFFu;
+        return (h == 0 && rr < g.n) ? g.perm[g.start + rr] : 0xFFFFFFFFu;
     };
     RowData nxt;
     uint32_t idx_next = idx_of((uint32_t)gwave * TR + stride);
@@ -652,307 +651,6 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
     }
 }
 
-// The same network on 64-row wave tiles: one wave per SIMD (4 per block, one
-// block per CU) with the whole 512-VGPR file, two 32-row MFMA tiles per wave so
-// every GEMM runs 4 independent accumulator chains, and all 64 lanes own a row
-// in the heads / loss.  Forward values are the same k-ordered chains as above
-// (bit-identical); the gradient sums visit the rows in another fixed order.
-__global__ void __launch_bounds__(256, 1) k_minibatch_mfma64(MbArgs g) {
-    using namespace mmb;
-    constexpr CpOffsets O = cp_offsets<64, 2>();
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    Params &S = *reinterpret_cast<Params *>(smem);
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    Wave64 &B = reinterpret_cast<Wave64 *>(smem + sizeof(Params) / 4)[wv];
-    load_params(S, g.params);
-    __syncthreads();
-
-    const int c = lane & 31, h = lane >> 5;
-    const int gwave = blockIdx.x * WAVES64 + wv, nwaves = gridDim.x * WAVES64;
-    const float mean = g.mb_stats[0], denom = g.mb_stats[1] + 1e-8f;
-    float b0k[2], b1k[2], wpk0[2], wpk1[2], wvk[2];
-#pragma unroll
-    for (int ct = 0; ct < 2; ct++) {
-        const int k = c + 32 * ct;
-        b0k[ct] = S.b0[k]; b1k[ct] = S.b1[k];
-        wpk0[ct] = S.Wp[2 * k]; wpk1[ct] = S.Wp[2 * k + 1]; wvk[ct] = S.Wv[k];
-    }
-    f32x16_t dW1[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; i++)
-#pragma unroll
-        for (int j = 0; j < 2; j++)
-#pragma unroll
-            for (int q = 0; q < 16; q++) dW1[i][j][q] = 0.0f;
-    float gW0[5][2], gb0[2] = {0, 0}, gb1[2] = {0, 0}, gP0[2] = {0, 0}, gP1[2] = {0, 0}, gV[2] = {0, 0};
-#pragma unroll
-    for (int d = 0; d < 5; d++) gW0[d][0] = gW0[d][1] = 0.0f;
-    float gbp0 = 0, gbp1 = 0, gbv = 0;
-    float m_pl = 0, m_vl = 0, m_h = 0, m_kl = 0, m_cf = 0, m_v = 0, m_r = 0, m_ve = 0, m_ve2 = 0;
-    float m_vemax = -INFINITY, m_n = 0;
-
-    // gather pipeline (ppo.rs:1833-1857): shuffled index two tiles ahead, row
-    // data one tile ahead; lane = row
-    const uint32_t stride = (uint32_t)nwaves * TR64;
-    auto idx_of = [&](uint32_t b) -> uint32_t {
-        const uint32_t rr = b + lane;
-        return rr < g.n ? (g.dbg_seq ? g.start + rr : g.perm[g.start + rr]) : 0xFFFFFFFFu;
-    };
-    RowData nxt;
-    uint32_t idx_next = idx_of((uint32_t)gwave * TR64 + stride);
-    nxt = load_row(g, idx_of((uint32_t)gwave * TR64));
-    for (uint32_t base = (uint32_t)gwave * TR64; base < g.n; base += stride) {
-        const bool valid = base + lane < g.n;
-        const RowData cur = nxt;
-        const uint32_t idx_after = idx_of(base + 2 * stride);
-        nxt = load_row(g, idx_next);
-        idx_next = idx_after;
-#pragma unroll
-        for (int d = 0; d < 5; d++) B.X[lane * 9 + d] = cur.x(d);
-        B.X[lane * 9 + 5] = 0.0f;
-        wave_sync();
-        // ---- layer 1 (K = 5 padded to 6)
-        f32x16_t h1[2][2];   // [row tile][col tile]
-#pragma unroll
-        for (int rt = 0; rt < 2; rt++)
-#pragma unroll
-            for (int ct = 0; ct < 2; ct++)
-#pragma unroll
-                for (int q = 0; q < 16; q++) h1[rt][ct][q] = 0.0f;
-#pragma unroll
-        for (int s = 0; s < 3; s++) {
-            const float bw0 = S.W0[(2 * s + h) * H + c], bw1 = S.W0[(2 * s + h) * H + c + 32];
-#pragma unroll
-            for (int rt = 0; rt < 2; rt++) {
-                const float av = B.X[(32 * rt + c) * 9 + 2 * s + h];
-                h1[rt][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bw0, h1[rt][0], 0, 0, 0);
-                h1[rt][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bw1, h1[rt][1], 0, 0, 0);
-            }
-        }
-#pragma unroll
-        for (int rt = 0; rt < 2; rt++)
-#pragma unroll
-            for (int ct = 0; ct < 2; ct++)
-#pragma unroll
-                for (int q = 0; q < 16; q++) {
-                    const float v = __fadd_rn(h1[rt][ct][q], b0k[ct]);
-                    h1[rt][ct][q] = v > 0.0f ? v : 0.0f;
-                    B.T[(32 * rt + cd_row(q, h)) * RS + c + 32 * ct] = h1[rt][ct][q];
-                }
-        wave_sync();
-        // ---- layer 2 (K = 64)
-        f32x16_t h2[2][2];
-#pragma unroll
-        for (int rt = 0; rt < 2; rt++)
-#pragma unroll
-            for (int ct = 0; ct < 2; ct++)
-#pragma unroll
-                for (int q = 0; q < 16; q++) h2[rt][ct][q] = 0.0f;
-#pragma unroll 8
-        for (int s = 0; s < 32; s++) {
-            const float bv0 = S.W1[(2 * s + h) * RS + c], bv1 = S.W1[(2 * s + h) * RS + c + 32];
-#pragma unroll
-            for (int rt = 0; rt < 2; rt++) {
-                const float av = B.T[(32 * rt + c) * RS + 2 * s + h];
-                h2[rt][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv0, h2[rt][0], 0, 0, 0);
-                h2[rt][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv1, h2[rt][1], 0, 0, 0);
-            }
-        }
-        wave_sync();
-#pragma unroll
-        for (int rt = 0; rt < 2; rt++)
-#pragma unroll
-            for (int ct = 0; ct < 2; ct++)
-#pragma unroll
-                for (int q = 0; q < 16; q++) {
-                    const float v = __fadd_rn(h2[rt][ct][q], b1k[ct]);
-                    h2[rt][ct][q] = v > 0.0f ? v : 0.0f;
-                    B.T[(32 * rt + cd_row(q, h)) * RS + c + 32 * ct] = h2[rt][ct][q];
-                }
-        wave_sync();
-        // ---- heads + loss, lane = row
-        {
-            float l0 = 0.0f, l1 = 0.0f, vv = 0.0f;
-            const float *hr = B.T + lane * RS;
-#pragma unroll 16
-            for (int k = 0; k < H; k++) {
-                const float hk = hr[k];
-                l0 = __builtin_fmaf(hk, S.Wp[2 * k], l0);
-                l1 = __builtin_fmaf(hk, S.Wp[2 * k + 1], l1);
-                vv = __builtin_fmaf(hk, S.Wv[k], vv);
-            }
-            const int a = cur.a;
-            const float olp = cur.olp, A = cur.A, R = cur.R, ov = cur.ov;
-            const float lg0 = __fadd_rn(l0, S.bp[0]), lg1 = __fadd_rn(l1, S.bp[1]), v = __fadd_rn(vv, S.bv[0]);
-            const float An = __fdiv_rn(__fsub_rn(A, mean), denom);   // utils.rs:88
-            const float mx = lg0 > lg1 ? lg0 : lg1;
-            const float e0 = S.expf(__fsub_rn(lg0, mx));
-            const float e1 = S.expf(__fsub_rn(lg1, mx));
-            const float lse = S.logf(__fadd_rn(e0, e1));
-            const float ls0 = __fsub_rn(__fsub_rn(lg0, mx), lse);
-            const float ls1 = __fsub_rn(__fsub_rn(lg1, mx), lse);
-            const float p0 = S.expf(ls0), p1 = S.expf(ls1);
-            const float Hn = -__fadd_rn(__fmul_rn(p0, ls0), __fmul_rn(p1, ls1));
-            const float newlp = a == 1 ? ls1 : ls0;
-            const float log_ratio = __fsub_rn(newlp, olp);
-            const float ratio = S.expf(log_ratio);
-            const float na = -An;
-            const float pl1 = __fmul_rn(na, ratio);
-            const float rc = ratio < g.lo ? g.lo : (ratio > g.hi ? g.hi : ratio);
-            const float pl2 = __fmul_rn(na, rc);
-            const bool rhs = pl1 < pl2;
-            const float pl = rhs ? pl2 : pl1;
-            float vl, dvl;
-            if (g.clip_value) {
-                const float dlt = __fsub_rn(v, ov);
-                const float dc = dlt < -g.ceps ? -g.ceps : (dlt > g.ceps ? g.ceps : dlt);
-                const float vc = __fadd_rn(ov, dc);
-                const float q1 = __fmul_rn(__fsub_rn(v, R), __fsub_rn(v, R));
-                const float q2 = __fmul_rn(__fsub_rn(vc, R), __fsub_rn(vc, R));
-                if (q1 < q2) { vl = q2; dvl = (dlt >= -g.ceps && dlt <= g.ceps) ? 2.0f * __fsub_rn(vc, R) : 0.0f; }
-                else { vl = q1; dvl = 2.0f * __fsub_rn(v, R); }
-            } else {
-                vl = __fmul_rn(__fsub_rn(v, R), __fsub_rn(v, R));
-                dvl = 2.0f * __fsub_rn(v, R);
-            }
-            const float g_ratio = (!rhs || (ratio >= g.lo && ratio <= g.hi)) ? -An * g.inv_mb : 0.0f;
-            const float g_lr = g_ratio * ratio;
-            const float ec = g.ent_coef * g.inv_mb;
-            float dl0 = g_lr * ((a == 0 ? 1.0f : 0.0f) - p0) + ec * p0 * (ls0 + Hn);
-            float dl1 = g_lr * ((a == 1 ? 1.0f : 0.0f) - p1) + ec * p1 * (ls1 + Hn);
-            float dv = g.value_coef * 0.5f * g.inv_mb * dvl;
-            if (!valid) { dl0 = dl1 = dv = 0.0f; }
-            else {
-                const float ve = fabsf(__fsub_rn(v, R));
-                m_pl += pl; m_vl += vl; m_h += Hn; m_kl += (ratio - 1.0f) - log_ratio;
-                m_cf += fabsf(ratio - 1.0f) > g.ceps ? 1.0f : 0.0f;
-                m_v += v; m_r += R; m_ve += ve; m_ve2 += ve * ve; m_vemax = fmaxf(m_vemax, ve);
-                m_n += 1.0f;
-            }
-            gbp0 += dl0; gbp1 += dl1; gbv += dv;
-            B.dl[lane * 4 + 0] = dl0; B.dl[lane * 4 + 1] = dl1; B.dl[lane * 4 + 2] = dv;
-        }
-        wave_sync();
-        // ---- head gradients and dZ2 = ([dl | dv] [Wp | Wv]^T) * [H2 > 0], C/D layout
-        f32x16_t dz2[2][2];
-#pragma unroll
-        for (int rt = 0; rt < 2; rt++)
-#pragma unroll
-            for (int q = 0; q < 16; q++) {
-                const int row = 32 * rt + cd_row(q, h);
-                const float d0 = B.dl[row * 4], d1 = B.dl[row * 4 + 1], dvr = B.dl[row * 4 + 2];
-#pragma unroll
-                for (int ct = 0; ct < 2; ct++) {
-                    const float hv = h2[rt][ct][q];
-                    gP0[ct] = __builtin_fmaf(hv, d0, gP0[ct]);
-                    gP1[ct] = __builtin_fmaf(hv, d1, gP1[ct]);
-                    gV[ct] = __builtin_fmaf(hv, dvr, gV[ct]);
-                    float sacc = __builtin_fmaf(d0, wpk0[ct], 0.0f);
-                    sacc = __builtin_fmaf(d1, wpk1[ct], sacc);
-                    sacc = __builtin_fmaf(dvr, wvk[ct], sacc);
-                    dz2[rt][ct][q] = hv > 0.0f ? sacc : 0.0f;
-                    gb1[ct] += dz2[rt][ct][q];
-                }
-            }
-        // dZ2 -> LDS [row][o] for dZ1 = dZ2 W1^T (sums over dZ2's column index)
-#pragma unroll
-        for (int rt = 0; rt < 2; rt++)
-#pragma unroll
-            for (int ct = 0; ct < 2; ct++)
-#pragma unroll
-                for (int q = 0; q < 16; q++)
-                    B.T[(32 * rt + cd_row(q, h)) * RS + c + 32 * ct] = dz2[rt][ct][q];
-        // dW1 += H1^T dZ2 over this tile's rows (both operands in C/D layout)
-#pragma unroll
-        for (int rt = 0; rt < 2; rt++)
-#pragma unroll
-            for (int q = 0; q < 16; q++)
-#pragma unroll
-                for (int it = 0; it < 2; it++)
-#pragma unroll
-                    for (int jt = 0; jt < 2; jt++)
-                        dW1[it][jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(h1[rt][it][q], dz2[rt][jt][q], dW1[it][jt], 0, 0, 0);
-        wave_sync();
-        f32x16_t dz1[2][2];
-#pragma unroll
-        for (int rt = 0; rt < 2; rt++)
-#pragma unroll
-            for (int jt = 0; jt < 2; jt++)
-#pragma unroll
-                for (int q = 0; q < 16; q++) dz1[rt][jt][q] = 0.0f;
-#pragma unroll 8
-        for (int s = 0; s < 32; s++) {
-            const float bw0 = S.W1[c * RS + 2 * s + h], bw1 = S.W1[(c + 32) * RS + 2 * s + h];
-#pragma unroll
-            for (int rt = 0; rt < 2; rt++) {
-                const float av = B.T[(32 * rt + c) * RS + 2 * s + h];
-                dz1[rt][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bw0, dz1[rt][0], 0, 0, 0);
-                dz1[rt][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bw1, dz1[rt][1], 0, 0, 0);
-            }
-        }
-        // dZ1 masked by relu'(H1); dW0 and db0 on the VALU (lane = hidden unit)
-#pragma unroll
-        for (int rt = 0; rt < 2; rt++)
-#pragma unroll
-            for (int q = 0; q < 16; q++) {
-                const int row = 32 * rt + cd_row(q, h);
-                float xr[5];
-#pragma unroll
-                for (int d = 0; d < 5; d++) xr[d] = B.X[row * 9 + d];
-#pragma unroll
-                for (int jt = 0; jt < 2; jt++) {
-                    const float dzv = h1[rt][jt][q] > 0.0f ? dz1[rt][jt][q] : 0.0f;
-                    gb0[jt] += dzv;
-#pragma unroll
-                    for (int d = 0; d < 5; d++) gW0[d][jt] = __builtin_fmaf(xr[d], dzv, gW0[d][jt]);
-                }
-            }
-        wave_sync();
-    }
-    // ---- this wave's partial gradient row (lane halves hold different rows: combine)
-#pragma unroll
-    for (int ct = 0; ct < 2; ct++) {
-        gb0[ct] += __shfl_xor(gb0[ct], 32, 64); gb1[ct] += __shfl_xor(gb1[ct], 32, 64);
-        gP0[ct] += __shfl_xor(gP0[ct], 32, 64); gP1[ct] += __shfl_xor(gP1[ct], 32, 64);
-        gV[ct] += __shfl_xor(gV[ct], 32, 64);
-#pragma unroll
-        for (int d = 0; d < 5; d++) gW0[d][ct] += __shfl_xor(gW0[d][ct], 32, 64);
-    }
-    float *row = g.slab + (size_t)gwave * (g.np + NUM_M);
-    if (h == 0) {
-#pragma unroll
-        for (int ct = 0; ct < 2; ct++) {
-            const int k = c + 32 * ct;
-#pragma unroll
-            for (int d = 0; d < 5; d++) row[O.w0 + d * H + k] = gW0[d][ct];
-            row[O.b0 + k] = gb0[ct];
-            row[O.b1 + k] = gb1[ct];
-            row[O.wp + 2 * k] = gP0[ct];
-            row[O.wp + 2 * k + 1] = gP1[ct];
-            row[O.wv + k] = gV[ct];
-        }
-    }
-#pragma unroll
-    for (int it = 0; it < 2; it++)
-#pragma unroll
-        for (int jt = 0; jt < 2; jt++)
-#pragma unroll
-            for (int q = 0; q < 16; q++)
-                row[O.w1 + (cd_row(q, h) + 32 * it) * H + c + 32 * jt] = dW1[it][jt][q];
-    const float s_bp0 = wave_sum(gbp0), s_bp1 = wave_sum(gbp1), s_bv = wave_sum(gbv);
-    const float s_pl = wave_sum(m_pl), s_vl = wave_sum(m_vl), s_h = wave_sum(m_h);
-    const float s_kl = wave_sum(m_kl), s_cf = wave_sum(m_cf), s_v = wave_sum(m_v);
-    const float s_r = wave_sum(m_r), s_ve = wave_sum(m_ve), s_ve2 = wave_sum(m_ve2);
-    const float s_mx = wave_max(m_vemax), s_n = wave_sum(m_n);
-    if (lane == 0) {
-        row[O.bp] = s_bp0; row[O.bp + 1] = s_bp1; row[O.bv] = s_bv;
-        float *mm = row + g.np;
-        mm[M_PL] = s_pl; mm[M_VL] = s_vl; mm[M_H] = s_h; mm[M_KL] = s_kl; mm[M_CF] = s_cf;
-        mm[M_V] = s_v; mm[M_R] = s_r; mm[M_VE] = s_ve; mm[M_VE2] = s_ve2; mm[M_VEMAX] = s_mx;
-        mm[M_N] = s_n;
-    }
-}
-
 // fixed-order reduction of the wave partials: grad[p] = sum_w slab[w][p], in two
 // passes (SLAB_GROUPS row groups in parallel, then the groups in order)
 constexpr int SLAB_GROUPS = 32;
@@ -1207,16 +905,10 @@ bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_
     g.ceps = (float)c->cfg.clip_epsilon;
     g.inv_mb = (float)(1.0 / (double)n); g.ent_coef = ent_coef; g.value_coef = (float)c->cfg.value_coef;
     g.clip_value = c->cfg.clip_value;
-    static const bool dbg_seq = getenv("BPPO_DBG_MB_SEQ") != nullptr;
-    g.dbg_seq = dbg_seq;
     g.rows = c->d_mbrow;
     int blocks = 256;
     const size_t params_bytes = ((c->net.n_params + 3) & ~(size_t)3) * sizeof(float);
-    static const bool mb64 = getenv("BPPO_MB64") != nullptr;
-    if (h == 64 && nl == 2 && c->relu_mfma && mb64) {
-        c->slab_used = blocks * mmb::WAVES64;
-        hipLaunchKernelGGL(k_minibatch_mfma64, dim3(blocks), dim3(64 * mmb::WAVES64), mmb::LDS64, c->stream, g);
-    } else if (h == 64 && nl == 2 && c->relu_mfma) {
+    if (h == 64 && nl == 2 && c->relu_mfma) {
         if ((size_t)mmb::WAVES * (c->net.n_params + NUM_M) * sizeof(float) > mmb::LDSB) {
             c->err = "minibatch kernel: gradient rows exceed LDS";
             return BPPO_ERR_UNSUPPORTED;

@@ -371,7 +371,8 @@ hipError_t wide_env_step(int kind, hipStream_t st, const WideStepArgs &a) {
 
 hipError_t wide_sample(int A, hipStream_t st, const SampleArgs &g) {
     const dim3 grid((g.N + 127) / 128), block(128);
-    if (A == C4_ACT) hipLaunchKernelGGL(k_sample_masked<C4_ACT>, grid, block, 0, st, g);
+    if (A == 2) hipLaunchKernelGGL(k_sample_masked<2>, grid, block, 0, st, g);   // CartPole (bppo_debug_sample)
+    else if (A == C4_ACT) hipLaunchKernelGGL(k_sample_masked<C4_ACT>, grid, block, 0, st, g);
     else if (A == LD_ACT) hipLaunchKernelGGL(k_sample_masked<LD_ACT>, grid, block, 0, st, g);
     else return hipErrorInvalidValue;
     return hipGetLastError();

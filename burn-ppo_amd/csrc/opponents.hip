@@ -408,7 +408,11 @@ extern "C" bppo_status bppo_opponents_set(bppo_ctx *c, int32_t n_models, const f
     TRY(oalloc(c, &c->d_opp_on, (size_t)(2 * D + 1) * std::max(n_models, 1)));
     TRY(oalloc(c, &c->d_lpos, (size_t)std::max(num_opponent_envs, 1)));
     TRY(oalloc(c, &c->d_p2o, (size_t)std::max(num_opponent_envs, 1) * P));
-    if (n_models > 0) BPPO_HIP(c, hipMemcpy(c->d_opp_params, params, sizeof(float) * np * n_models, hipMemcpyHostToDevice));
+    // uploads are ordered on the context stream after oalloc's zeroing memsets (a
+    // blocking hipMemcpy on the null stream would not wait for that non-blocking
+    // stream); the stream is drained before the host arrays may go away
+    if (n_models > 0)
+        BPPO_HIP(c, hipMemcpyAsync(c->d_opp_params, params, sizeof(float) * np * n_models, hipMemcpyHostToDevice, c->stream));
     std::vector<double> on((size_t)(2 * D + 1) * std::max(n_models, 1), 0.0);
     for (int k = 0; k < n_models; k++) {
         if (!norm_count || norm_count[k] < 2.0 || !norm_mean || !norm_m2) continue;
@@ -417,11 +421,12 @@ extern "C" bppo_status bppo_opponents_set(bppo_ctx *c, int32_t n_models, const f
         std::memcpy(&on[(size_t)k * (2 * D + 1) + D], norm_m2 + (size_t)k * D, sizeof(double) * D);
         on[(size_t)k * (2 * D + 1) + 2 * D] = norm_count[k];
     }
-    BPPO_HIP(c, hipMemcpy(c->d_opp_on, on.data(), sizeof(double) * on.size(), hipMemcpyHostToDevice));
+    BPPO_HIP(c, hipMemcpyAsync(c->d_opp_on, on.data(), sizeof(double) * on.size(), hipMemcpyHostToDevice, c->stream));
     if (num_opponent_envs > 0) {
-        BPPO_HIP(c, hipMemcpy(c->d_lpos, learner_pos, sizeof(int32_t) * num_opponent_envs, hipMemcpyHostToDevice));
-        BPPO_HIP(c, hipMemcpy(c->d_p2o, pos_to_opp, sizeof(int32_t) * (size_t)num_opponent_envs * P, hipMemcpyHostToDevice));
-        BPPO_HIP(c, hipMemcpy(c->d_curopp, current_opp, sizeof(int32_t) * (P - 1), hipMemcpyHostToDevice));
+        BPPO_HIP(c, hipMemcpyAsync(c->d_lpos, learner_pos, sizeof(int32_t) * num_opponent_envs, hipMemcpyHostToDevice, c->stream));
+        BPPO_HIP(c, hipMemcpyAsync(c->d_p2o, pos_to_opp, sizeof(int32_t) * (size_t)num_opponent_envs * P,
+                                   hipMemcpyHostToDevice, c->stream));
+        BPPO_HIP(c, hipMemcpyAsync(c->d_curopp, current_opp, sizeof(int32_t) * (P - 1), hipMemcpyHostToDevice, c->stream));
     }
     BPPO_HIP(c, hipStreamSynchronize(c->stream));
     return BPPO_OK;
@@ -430,8 +435,9 @@ extern "C" bppo_status bppo_opponents_set(bppo_ctx *c, int32_t n_models, const f
 extern "C" bppo_status bppo_opponents_get_envs(bppo_ctx *c, int32_t *learner_pos, int32_t *pos_to_opp) {
     if (!c) return BPPO_ERR_ARG;
     if (!c->n_opp) return BPPO_OK;
+    if (learner_pos) BPPO_HIP(c, hipMemcpyAsync(learner_pos, c->d_lpos, sizeof(int32_t) * c->n_opp, hipMemcpyDeviceToHost, c->stream));
+    if (pos_to_opp)
+        BPPO_HIP(c, hipMemcpyAsync(pos_to_opp, c->d_p2o, sizeof(int32_t) * (size_t)c->n_opp * c->P, hipMemcpyDeviceToHost, c->stream));
     BPPO_HIP(c, hipStreamSynchronize(c->stream));
-    if (learner_pos) BPPO_HIP(c, hipMemcpy(learner_pos, c->d_lpos, sizeof(int32_t) * c->n_opp, hipMemcpyDeviceToHost));
-    if (pos_to_opp) BPPO_HIP(c, hipMemcpy(pos_to_opp, c->d_p2o, sizeof(int32_t) * (size_t)c->n_opp * c->P, hipMemcpyDeviceToHost));
     return BPPO_OK;
 }

@@ -134,7 +134,12 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
     // 16-CPU share (K = 2/4/5/6: 281/284/311/316 M env-steps/s): more starting
     // points meet the true walk sooner even oversubscribed.
     // (BPPO_SHUFFLE_SPEC overrides; 0 = sequential walk only)
-    K = 6;
+    // BPPO_HOST_THREADS: this rank's CPU budget (bench.py: the CPUs this process may
+    // use / ranks on the node), so 8 ranks of one node do not oversubscribe it.
+    // K and the word producers scale with it; 16 CPUs (one GPU's share) -> K = 6.
+    host_cpus = 16;
+    if (const char *e = getenv("BPPO_HOST_THREADS")) host_cpus = std::max(1, atoi(e));
+    K = std::max(1, std::min(6, (6 * host_cpus + 8) / 16));
     if (const char *e = getenv("BPPO_SHUFFLE_SPEC")) K = std::max(0, atoi(e));
     // C leading epochs of the next job are speculated during this job (their walks
     // get a whole job of head start; later epochs' walks start with their job)
@@ -196,7 +201,7 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
     const uint64_t nck = (uint64_t)((Ew + 24.0 * sigma) / SHUF_CK) + 4;
     for (int i = 0; i < nspec; i++) spec[i].ck.assign(nck, 0xFFFFFFFFu);
     for (int i = 0; i < nspec; i++) workers.emplace_back([this, i]() { worker(i); });
-    int ngen = 4;
+    int ngen = std::max(1, std::min(4, host_cpus / 4));
     if (const char *e = getenv("BPPO_SHUFFLE_GEN")) ngen = std::max(1, atoi(e));
     for (int i = 0; i < ngen; i++) gens.emplace_back([this]() { generator(); });
     th = std::thread([this]() { run(); });

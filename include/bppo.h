@@ -215,6 +215,15 @@ bppo_status bppo_debug_fisher_yates(int32_t device, const uint32_t *J, uint32_t 
 bppo_status bppo_debug_shuffle_engine(uint64_t seed, uint64_t stream, uint64_t start, uint32_t n, int32_t epochs,
                                       uint64_t gap, int32_t jobs, uint32_t *J, uint64_t *ends, int32_t *met);
 
+/* sampling parity hook: apply_action_mask + sample_categorical + log_prob_categorical
+ * (utils.rs:10-45, 96-135) for B host rows of A logits (A in {2, 7, 49}) on the device
+ * sampler; Gumbel words from StdRng(seed) stream `stream` at word_pos, row-major;
+ * masks [B*A] 0/1 or NULL.  Returns BPPO_ERR_EMPTY_MASK for a row with no valid
+ * action (the reference panics, utils.rs:115-123) and BPPO_ERR_NONFINITE for a
+ * non-finite log-prob (ppo.rs:363-366). */
+bppo_status bppo_debug_sample(int32_t A, int32_t B, const float *logits, const uint8_t *masks, uint64_t seed,
+                              uint64_t stream, uint64_t word_pos, int32_t *actions, float *log_probs);
+
 /* GEMM engine parity hook (host buffers).  mode 0: out[M][N] = act(A[M][K] B[K][N] + bias[N])
  * with matrixmultiply's KC=256 fma-chain order (Burn Linear forward, mlp.rs:140-206);
  * (act: 0 none, 1 relu, 2 tanh); mode 1: out[M][N] = (A[M][K] B[N][K]^T) * act'(H) with H = bias_or_H

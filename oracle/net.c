@@ -19,6 +19,12 @@
 
 #define KC 256
 
+/* MLP row parallelism: on for the parity tests (speed), off for the timed CPU
+ * baseline, whose plan keeps the MLP single-threaded as the
+ * reference's matrixmultiply sgemm is; results do not depend on it */
+static int g_mlp_parallel = 1;
+void or_set_mlp_parallel(int on) { g_mlp_parallel = on; }
+
 typedef struct { int in, out; size_t w, b; } layer_t;
 
 /* parameter layout = Burn record order (mlp.rs:47-62, ctde.rs:26-44) */
@@ -53,22 +59,36 @@ size_t or_net_num_params(const or_net_desc *d) {
 
 static float act_fwd(float y, int relu) { return relu ? (y > 0.0f ? y : 0.0f) : tanhf(y); }
 
-/* One Burn Linear: y = x.matmul(W) + b (matrixmultiply k-ordered fma chain). */
+/* One Burn Linear: y = x.matmul(W) + b (matrixmultiply k-ordered fma chain).
+ * Each (row, o) element is the chain acc = fmaf(x[k], W[k][o], acc) from 0 over
+ * one KC block, blocks summed in order, then + b[o].  The loops run o innermost
+ * (independent chains, vectorisable) and rows in parallel: the arithmetic of
+ * every element is unchanged, so the result does not depend on the thread count. */
 void or_linear(const float *x, const float *W, const float *b, size_t B, int in, int out,
                int relu, float *y) {
-    for (size_t r = 0; r < B; r++) {
-        const float *xr = x + r * in;
-        for (int o = 0; o < out; o++) {
-            float tot = 0.0f;
+#pragma omp parallel if (g_mlp_parallel && B * (size_t)in * (size_t)out > (1u << 18))
+    {
+        float *acc = malloc(sizeof(float) * (size_t)out), *tot = malloc(sizeof(float) * (size_t)out);
+#pragma omp for schedule(static)
+        for (size_t r = 0; r < B; r++) {
+            const float *xr = x + r * in;
             for (int kb = 0; kb < in; kb += KC) {
                 int ke = kb + KC < in ? kb + KC : in;
-                float acc = 0.0f;
-                for (int k = kb; k < ke; k++) acc = fmaf(xr[k], W[(size_t)k * out + o], acc);
-                tot = kb == 0 ? acc : tot + acc;
+                for (int o = 0; o < out; o++) acc[o] = 0.0f;
+                for (int k = kb; k < ke; k++) {
+                    const float xk = xr[k];
+                    const float *wk = W + (size_t)k * out;
+                    for (int o = 0; o < out; o++) acc[o] = fmaf(xk, wk[o], acc[o]);
+                }
+                if (kb == 0) for (int o = 0; o < out; o++) tot[o] = acc[o];
+                else for (int o = 0; o < out; o++) tot[o] = tot[o] + acc[o];
             }
-            float v = tot + b[o];
-            y[r * out + o] = relu >= 0 ? act_fwd(v, relu) : v;
+            for (int o = 0; o < out; o++) {
+                float v = tot[o] + b[o];
+                y[r * out + o] = relu >= 0 ? act_fwd(v, relu) : v;
+            }
         }
+        free(acc); free(tot);
     }
 }
 
@@ -127,10 +147,14 @@ void or_net_forward(const or_net_desc *d, const float *params, const float *obs,
 }
 
 /* backward of one Linear + activation given the post-activation output y:
- * dW += x^T dz (f64 accumulation), db += sum dz, dx = dz W^T (f32 fma chain). */
+ * dW += x^T dz (f64, each element summed over rows in row order), db += sum dz,
+ * dx = dz W^T (f32 fma chain over o).  Parallel over k (dW) and rows (dx):
+ * per-element arithmetic and order are fixed, independent of the thread count. */
 static void linear_bwd(const float *x, const float *y, const float *dy, const float *W,
                        size_t B, int in, int out, int act, double *gW, double *gb, float *dx) {
     float *dz = malloc(sizeof(float) * B * out);
+    const int big = g_mlp_parallel && B * (size_t)in * (size_t)out > (1u << 18);
+#pragma omp parallel for schedule(static) if (big)
     for (size_t r = 0; r < B; r++)
         for (int o = 0; o < out; o++) {
             float g = dy[r * out + o];
@@ -139,19 +163,37 @@ static void linear_bwd(const float *x, const float *y, const float *dy, const fl
             dz[r * out + o] = g;
         }
     for (size_t r = 0; r < B; r++)
-        for (int o = 0; o < out; o++) {
-            double g = dz[r * out + o];
-            gb[o] += g;
-            if (g != 0.0)
-                for (int k = 0; k < in; k++) gW[(size_t)k * out + o] += (double)x[r * in + k] * g;
+        for (int o = 0; o < out; o++) gb[o] += (double)dz[r * out + o];
+#pragma omp parallel for schedule(dynamic, 1) if (big)
+    for (int k = 0; k < in; k++) {
+        double *gk = gW + (size_t)k * out;
+        for (size_t r = 0; r < B; r++) {
+            const double xk = (double)x[r * in + k];
+            const float *dzr = dz + r * out;
+            for (int o = 0; o < out; o++) gk[o] += xk * (double)dzr[o];
         }
-    if (dx)
-        for (size_t r = 0; r < B; r++)
-            for (int k = 0; k < in; k++) {
-                float acc = 0.0f;
-                for (int o = 0; o < out; o++) acc = fmaf(dz[r * out + o], W[(size_t)k * out + o], acc);
-                dx[r * in + k] = acc;
+    }
+    if (dx) {
+        float *WT = malloc(sizeof(float) * (size_t)in * out);
+        for (int k = 0; k < in; k++)
+            for (int o = 0; o < out; o++) WT[(size_t)o * in + k] = W[(size_t)k * out + o];
+#pragma omp parallel if (big)
+        {
+            float *acc = malloc(sizeof(float) * (size_t)in);
+#pragma omp for schedule(static)
+            for (size_t r = 0; r < B; r++) {
+                for (int k = 0; k < in; k++) acc[k] = 0.0f;
+                for (int o = 0; o < out; o++) {
+                    const float g = dz[r * out + o];
+                    const float *wo = WT + (size_t)o * in;
+                    for (int k = 0; k < in; k++) acc[k] = fmaf(g, wo[k], acc[k]);
+                }
+                for (int k = 0; k < in; k++) dx[r * in + k] = acc[k];
             }
+            free(acc);
+        }
+        free(WT);
+    }
     free(dz);
 }
 

@@ -188,6 +188,8 @@ size_t or_net_num_params(const or_net_desc *d);
 /* forward for B rows; logits [B*A], values [B] */
 void or_net_forward(const or_net_desc *d, const float *params, const float *obs,
                     const float *priv, size_t B, float *logits, float *values);
+/* MLP forward/backward row parallelism (OpenMP); off = single-threaded MLP */
+void or_set_mlp_parallel(int on);
 /* one linear layer y = x W + b with the matrixmultiply summation order */
 void or_linear(const float *x, const float *W, const float *b, size_t B, int in, int out,
                int relu, float *y);
@@ -275,7 +277,7 @@ void or_trainer_get_params(const or_trainer *t, float *out);
 void or_trainer_set_params(or_trainer *t, const float *in);
 uint64_t or_trainer_rng_pos(const or_trainer *t);
 /* phases of one update, so tests can compare buffers phase by phase */
-int or_trainer_collect(or_trainer *t);                     /* returns episodes completed */
+int or_trainer_collect(or_trainer *t);                     /* returns episodes completed (all, not only those stored) */
 void or_trainer_gae(or_trainer *t);
 void or_trainer_update(or_trainer *t, or_update_metrics *m);
 /* buffer export: name in {"obs","actions","rewards","dones","values","log_probs",

@@ -100,6 +100,7 @@ struct or_trainer {
     int has_masks;
     or_episode *eps;
     int n_eps, eps_cap;
+    long n_eps_total;        /* episodes completed in the last collect (n_eps of them stored) */
     double phase_s[3];
     /* opponent pool (ppo.rs:537-1063) */
     int K, n_opp;
@@ -260,7 +261,7 @@ static int collect_opp(or_trainer *t) {
     uint8_t *dn = malloc(N), *mk = malloc((size_t)N * A);
     int32_t *cp = malloc(sizeof(int32_t) * N), *act = malloc(sizeof(int32_t) * N);
     int32_t *rows = malloc(sizeof(int32_t) * N), *sact = malloc(sizeof(int32_t) * N);
-    t->n_eps = 0;
+    t->n_eps = 0; t->n_eps_total = 0;
     memset(t->lvpp, 0, sizeof(float) * (size_t)N * P);
     for (int s = 0; s < t->T; s++) {
         const size_t base = (size_t)s * N;
@@ -312,6 +313,7 @@ static int collect_opp(or_trainer *t) {
         int cap = t->eps_cap - t->n_eps;
         int ne = or_vecenv_step(t->env, act, NULL, rw, dn, t->eps + t->n_eps, cap);   /* :867-871 */
         t->n_eps += ne < cap ? ne : cap;
+        t->n_eps_total += ne;
         for (int e = 0; e < t->n_opp; e++)                                   /* :874-925 */
             if (dn[e]) or_shuffle_positions(&t->rng, P, t->curopp, &t->lpos[e], &t->p2o[(size_t)e * P]);
         for (int e = 0; e < N; e++) {                                        /* :928-1003 */
@@ -340,7 +342,7 @@ static int collect_opp(or_trainer *t) {
     free(raw); free(xo); free(xp); free(privs); free(logits); free(vals); free(rw); free(alogp); free(aval);
     free(dn); free(mk); free(cp); free(act); free(rows); free(sact);
     t->phase_s[0] = now_s() - t0;
-    return t->n_eps;
+    return (int)t->n_eps_total;
 }
 
 /* ppo.rs:213-500 collect_rollouts (self-play / single-player path). */
@@ -356,7 +358,7 @@ int or_trainer_collect(or_trainer *t) {
     uint8_t *mk = malloc((size_t)N * A);
     int32_t *cp = malloc(sizeof(int32_t) * N);
     int32_t *act = malloc(sizeof(int32_t) * N);
-    t->n_eps = 0;
+    t->n_eps = 0; t->n_eps_total = 0;
     memset(t->lvpp, 0, sizeof(float) * (size_t)N * P);
     for (int s = 0; s < t->T; s++) {
         size_t base = (size_t)s * N;
@@ -388,6 +390,7 @@ int or_trainer_collect(or_trainer *t) {
         int ne = or_vecenv_step(t->env, act, NULL, rw, dn, t->eps + t->n_eps,
                                 t->eps_cap - t->n_eps);         /* :374-378 */
         t->n_eps += ne < t->eps_cap - t->n_eps ? ne : t->eps_cap - t->n_eps;
+        t->n_eps_total += ne;
         for (int e = 0; e < N; e++) {                            /* :382-408 */
             int p = cp[e];
             float r = rw[(size_t)e * P + p];
@@ -413,7 +416,7 @@ int or_trainer_collect(or_trainer *t) {
     if (t->c.normalize_obs) or_obs_norm_update_batch(&t->on, t->raw, (size_t)t->T * N); /* :495-497 */
     free(obs); free(logits); free(vals); free(rw); free(dn); free(mk); free(cp); free(act);
     t->phase_s[0] = now_s() - t0;
-    return t->n_eps;
+    return (int)t->n_eps_total;
 }
 
 /* main.rs:877-947 bootstrap (UPDATED normalizer stats) then GAE dispatch. */

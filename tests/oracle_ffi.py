@@ -183,6 +183,7 @@ def lib():
             "or_trainer_opponent_envs": (None, [C.c_void_p, C.c_void_p, C.c_void_p]),
             "or_shuffle_positions": (None, [C.c_void_p, C.c_int, i32, C.c_void_p, i32]),
             "or_gen_range_u64": (C.c_uint64, [C.c_void_p, C.c_uint64, C.c_uint64]),
+            "or_set_mlp_parallel": (None, [C.c_int]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)

@@ -1,0 +1,145 @@
+"""Shared parity helpers: device (libbppo.so) vs oracle trainers on identical
+seeds and the stated tolerances.
+
+Tolerances (north_star: "fp32 returns/advantages/loss within 1e-5 relative"):
+  * every UpdateMetrics field (ppo.rs:1342-1369) within 1e-5 relative to
+    max(|oracle|, floor): the floor is the magnitude of the summands for the
+    signed means that cancel to ~0 — policy_loss / total_loss are means of
+    -A_n * ratio with E|A_n| ~ 0.8 (floor 1.0); adv_mean_raw is a mean of raw
+    advantages (floor adv_std_raw); value_mean / returns_mean (floor
+    value_error_mean + |returns_mean|).  Both sides accumulate in f64 per
+    minibatch, so what is left is per-row f32 rounding of the later minibatches,
+    whose parameters differ in the last bits (gradient reduction order);
+  * explained_variance: the reference sums in f32 sequentially
+    (ppo.rs:1268-1294); at 10^6 rows that sum drifts by ~1e-3 absolute on the
+    result (measured: 0.014473 vs the exact 0.013404 at B = 1,048,576).  The
+    device computes it in f64 (a deliberate deviation: the metric is logged,
+    it feeds nothing back).  So the device must equal the exact f64 explained
+    variance of the same buffers within 1e-6, and the oracle's f32 value must
+    equal a second restatement of the reference's f32 sequential sums
+    (ev_f32_sequential) bit for bit;
+  * parameters after Adam: rtol 1e-4 / atol 2e-5 (Adam divides by sqrt(v): a
+    gradient entry near 0 moves by ~lr either way, so the parameter check is
+    looser than the loss check).
+"""
+import numpy as np
+
+import bppo
+import oracle_ffi as O
+
+METRICS = ("policy_loss", "value_loss", "entropy", "entropy_scaled", "approx_kl", "clip_fraction",
+           "explained_variance", "total_loss", "value_mean", "returns_mean", "adv_mean_raw", "adv_std_raw",
+           "adv_min_raw", "adv_max_raw", "value_error_mean", "value_error_std", "value_error_max",
+           "avg_valid_actions", "entropy_valid_pct")
+RTOL = 1e-5
+PARAM_RTOL, PARAM_ATOL = 1e-4, 2e-5
+
+
+def _floor(k, om):
+    if k in ("policy_loss", "total_loss"):
+        return 1.0
+    if k == "adv_mean_raw":
+        return abs(om["adv_std_raw"])
+    if k in ("value_mean", "returns_mean"):
+        return abs(om["value_error_mean"]) + abs(om["returns_mean"])
+    return 0.0
+
+
+def ev_f64(values, returns):
+    """ppo.rs:1268-1294 in f64 (population variances)."""
+    v = np.asarray(values, np.float64)
+    r = np.asarray(returns, np.float64)
+    if v.size < 2:
+        return 0.0
+    vr = r.var()
+    if vr < 1e-8:
+        return 0.0
+    return 1.0 - (r - v).var() / vr
+
+
+def _seq_sum_f32(x):
+    return np.cumsum(np.ascontiguousarray(x, np.float32), dtype=np.float32)[-1] if x.size else np.float32(0)
+
+
+def ev_f32_sequential(values, returns):
+    """ppo.rs:1268-1294 as the reference computes it: f32 iterator sums in order."""
+    v = np.ascontiguousarray(values, np.float32)
+    r = np.ascontiguousarray(returns, np.float32)
+    n = np.float32(v.size)
+    if n < 2:
+        return np.float32(0)
+    mr = _seq_sum_f32(r) / n
+    q = (r - mr).astype(np.float32)
+    vr = _seq_sum_f32(q * q) / n
+    if vr < np.float32(1e-8):
+        return np.float32(0)
+    res = (r - v).astype(np.float32)
+    mres = _seq_sum_f32(res) / n
+    q = (res - mres).astype(np.float32)
+    vres = _seq_sum_f32(q * q) / n
+    return np.float32(np.float32(1) - np.float32(vres / vr))
+
+
+def assert_metrics_close(m, om, values=None, returns=None, skip=()):
+    """All 19 UpdateMetrics fields plus num_updates / epochs_run.  values /
+    returns: the buffers the explained variance is taken over (learner rows
+    only under an opponent pool)."""
+    assert m["num_updates"] == om["num_updates"], (m["num_updates"], om["num_updates"])
+    assert m["epochs_run"] == om["epochs_run"], (m["epochs_run"], om["epochs_run"])
+    bad = []
+    for k in METRICS:
+        if k in skip:
+            continue
+        d, o = float(m[k]), float(om[k])
+        if k == "explained_variance" and values is not None:
+            ex = ev_f64(values, returns)
+            ref32 = float(ev_f32_sequential(values, returns))
+            if abs(d - ex) > 1e-6 or o != ref32:
+                bad.append((k, d, o, ex, ref32))
+            continue
+        if np.isnan(o) and np.isnan(d):
+            continue
+        tol = RTOL * max(abs(o), _floor(k, om))
+        if not abs(d - o) <= tol:
+            bad.append((k, d, o, abs(d - o) / max(abs(o), 1e-30)))
+    assert not bad, bad
+
+
+def assert_params_close(pg, po):
+    np.testing.assert_allclose(pg, po, rtol=PARAM_RTOL, atol=PARAM_ATOL)
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def cartpole_pair(N, T, preset="cartpole", seed=42, init_seed=1, **kw):
+    """Device trainer + oracle trainer of one CartPole config (same params, seeds)."""
+    cfg = bppo.make_config(preset, num_envs=N, num_steps=T, seed=seed, **kw)
+    params = bppo.orthogonal_init(cfg, seed=init_seed)
+    tr = bppo.Trainer(cfg, params=params)
+    nr = cfg["normalize_returns"]
+    ocfg = O.train_cfg(num_envs=N, num_steps=T, seed=seed, lr=bppo.schedule_get(cfg["learning_rate"], 0),
+                       ent_coef=bppo.schedule_get(cfg["entropy_coef"], 0),
+                       hidden=cfg["hidden_size"], num_hidden=cfg["num_hidden"],
+                       relu=cfg["activation"] == "relu", normalize_obs=bool(cfg["normalize_obs"]),
+                       normalize_returns=True if nr is None else bool(nr), gamma=cfg["gamma"],
+                       gae_lambda=cfg["gae_lambda"], num_epochs=cfg["num_epochs"],
+                       num_minibatches=cfg["num_minibatches"], clip=cfg["clip_epsilon"],
+                       value_coef=cfg["value_coef"], max_grad_norm=cfg["max_grad_norm"],
+                       target_kl=cfg["target_kl"])
+    ot = O.Trainer(ocfg, params)
+    return cfg, tr, ot
+
+
+def cmp_cartpole_rollout(tr, ot):
+    b = tr.buffer
+    assert np.array_equal(b.actions.reshape(-1), ot.buffer("actions", np.int32))
+    assert np.array_equal(b.dones.reshape(-1), ot.buffer("dones"))
+    assert np.array_equal(bits(b.observations.reshape(-1)), bits(ot.buffer("obs")))
+    assert np.array_equal(bits(b.values.reshape(-1)), bits(ot.buffer("values")))
+    assert np.array_equal(bits(b.log_probs.reshape(-1)), bits(ot.buffer("log_probs")))
+    # return normalizer: f64 block scan vs the sequential Welford update ->
+    # normalized f32 rewards equal up to rare last-ulp ties
+    np.testing.assert_allclose(b.rewards.reshape(-1), ot.buffer("rewards"), rtol=2e-7, atol=0)
+    assert tr.ctx.rng_pos() == ot.rng_pos()

@@ -131,3 +131,21 @@ def test_stream_ordered_allreduce_matches_single_rank():
     p = tr.model.get_params()
     tr.close()
     assert np.array_equal(p, p_solo)
+
+
+def test_bench_launcher_starts_world_size_ranks_gloo():
+    """`bench.py --gpus N` must start N ranks itself (a
+    torch.distributed.run child) and report n_gpus = N; --selftest runs the
+    launcher, rank plumbing, barrier and max-over-ranks timing with gloo."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--selftest", "--steps", "3", "--warmup", "1"],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["selftest"] and d["config"]["parallelism"] == "dp2"

@@ -126,3 +126,16 @@ def test_explained_variance_cases():               # ppo.rs:2776-2830
 def test_minibatch_split(B, M, expected):           # ppo.rs:2946-3038
     import bppo.host as H
     assert H.minibatch_sizes(B, M) == expected
+
+
+def test_explained_variance_f32_sequential_restatement():
+    """The oracle's f32 sums (ppo.rs:1268-1294) equal a second restatement bit
+    for bit, at a size where f32 sequential drift is visible (vs f64)."""
+    from parity_util import ev_f32_sequential, ev_f64
+    rng = np.random.default_rng(3)
+    n = 300_000
+    r = rng.normal(20.0, 5.0, n).astype(np.float32)
+    v = (r + rng.normal(0.0, 4.0, n)).astype(np.float32)
+    o = O.lib().or_explained_variance(v, r, n)
+    assert np.float32(o) == ev_f32_sequential(v, r)
+    assert abs(o - ev_f64(v, r)) < 0.05
