@@ -69,6 +69,8 @@ EXPORTS = (
     "bppo_set_allreduce", "bppo_set_allreduce_async", "bppo_get_stream", "bppo_opponents_set", "bppo_opponents_get_envs", "bppo_buffer_get", "bppo_buffer_set", "bppo_gae_device",
     "bppo_gae_mp_device", "bppo_last_kernel_ms", "bppo_debug_libm", "bppo_debug_shuffle_chain",
     "bppo_debug_fisher_yates", "bppo_debug_gemm", "bppo_debug_shuffle_engine", "bppo_debug_sample",
+    "bppo_rng_fill_bytes", "bppo_rng_from_seed", "bppo_rng_key_get", "bppo_num_param_tensors",
+    "bppo_optimizer_get", "bppo_optimizer_set",
 )
 
 _lib = None
@@ -133,6 +135,12 @@ def lib():
         "bppo_debug_gemm": (i32, [i32, i32, i32, i32, vp, vp, vp, i32, vp, vp]),
         "bppo_debug_shuffle_engine": (i32, [u64, u64, u64, C.c_uint32, i32, u64, i32, vp, vp, vp]),
         "bppo_debug_sample": (i32, [i32, i32, vp, vp, u64, u64, u64, vp, vp]),
+        "bppo_rng_fill_bytes": (i32, [vp, vp, sz]),
+        "bppo_rng_from_seed": (i32, [vp, vp]),
+        "bppo_rng_key_get": (i32, [vp, vp]),
+        "bppo_num_param_tensors": (sz, [vp]),
+        "bppo_optimizer_get": (i32, [vp, vp, vp, vp, sz]),
+        "bppo_optimizer_set": (i32, [vp, vp, vp, vp, sz]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

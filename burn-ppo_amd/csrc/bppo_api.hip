@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <new>
 #include "bppo_internal.h"
 #include "bppo_wide.h"
 
@@ -275,6 +276,77 @@ extern "C" bppo_status bppo_rng_set(bppo_ctx *c, uint64_t p) {
     c->rng_pos = p;
     return BPPO_OK;
 }
+
+// checkpoint.rs:390-400 save_rng_state: rng.fill_bytes(&mut [u8; 32]) — rand_core
+// 0.6 BlockRng::fill_bytes takes ceil(n / 4) whole words, little-endian
+extern "C" bppo_status bppo_rng_fill_bytes(bppo_ctx *c, uint8_t *dst, size_t n) {
+    if (!c || (!dst && n)) return BPPO_ERR_ARG;
+    const size_t nw = (n + 3) / 4;
+    uint32_t blk[16];
+    uint64_t cached = ~0ull;
+    for (size_t i = 0; i < nw; i++) {
+        const uint64_t pos = c->rng_pos + i;
+        if ((pos >> 4) != cached) { chacha12_block(c->rng_key, pos >> 4, c->cfg.rng_stream, blk); cached = pos >> 4; }
+        const uint32_t w = blk[pos & 15];
+        for (int b = 0; b < 4 && 4 * i + b < n; b++) dst[4 * i + b] = (uint8_t)(w >> (8 * b));
+    }
+    c->rng_pos += nw;
+    c->shuf_slot = -1;
+    return BPPO_OK;
+}
+
+// checkpoint.rs:405-426 load_rng_state: StdRng::from_seed(seed) — the 32 seed bytes
+// are the ChaCha12 key (8 little-endian words), block counter 0.  The shuffle
+// engine precomputes words of the old key, so it is restarted on the new one.
+extern "C" bppo_status bppo_rng_from_seed(bppo_ctx *c, const uint8_t *seed) {
+    if (!c || !seed) return BPPO_ERR_ARG;
+    Key8 k;
+    for (int i = 0; i < 8; i++)
+        k.k[i] = (uint32_t)seed[4 * i] | ((uint32_t)seed[4 * i + 1] << 8) | ((uint32_t)seed[4 * i + 2] << 16) |
+                 ((uint32_t)seed[4 * i + 3] << 24);
+    BPPO_HIP(c, sync_stream(c));
+    c->shuf.shutdown();
+    c->shuf.~ShuffleEngine();
+    new (&c->shuf) ShuffleEngine();
+    c->rng_key = k;
+    c->rng_pos = 0;
+    c->shuf_slot = -1;
+    const size_t TN = (size_t)c->T * c->N;
+    TRY(c->shuf.init(c->dev, c->rng_key, c->cfg.rng_stream, (uint32_t)TN, c->cfg.num_epochs, TN * (uint64_t)c->A, c->err));
+    return BPPO_OK;
+}
+
+extern "C" bppo_status bppo_rng_key_get(bppo_ctx *c, uint32_t *key) {
+    if (!c || !key) return BPPO_ERR_ARG;
+    for (int i = 0; i < 8; i++) key[i] = c->rng_key.k[i];
+    return BPPO_OK;
+}
+
+// Adam state (burn-optim AdamState: moment_1, moment_2, time per parameter tensor):
+// m1/m2 flat like the parameters, steps [2 * layers] in record order (W, b per Linear)
+extern "C" bppo_status bppo_optimizer_get(bppo_ctx *c, float *m1, float *m2, int32_t *steps, size_t n) {
+    if (!c || n != c->net.n_params) { if (c) c->err = "optimizer_get: size mismatch"; return BPPO_ERR_ARG; }
+    if (m1) BPPO_HIP(c, hipMemcpyAsync(m1, c->d_m1, n * 4, hipMemcpyDeviceToHost, c->stream));
+    if (m2) BPPO_HIP(c, hipMemcpyAsync(m2, c->d_m2, n * 4, hipMemcpyDeviceToHost, c->stream));
+    BPPO_HIP(c, sync_stream(c));
+    if (steps) for (size_t t = 0; t < c->adam_t.size(); t++) steps[t] = c->adam_t[t];
+    return BPPO_OK;
+}
+
+extern "C" bppo_status bppo_optimizer_set(bppo_ctx *c, const float *m1, const float *m2, const int32_t *steps,
+                                          size_t n) {
+    if (!c || !m1 || !m2 || !steps || n != c->net.n_params) {
+        if (c) c->err = "optimizer_set: size mismatch";
+        return BPPO_ERR_ARG;
+    }
+    BPPO_HIP(c, hipMemcpyAsync(c->d_m1, m1, n * 4, hipMemcpyHostToDevice, c->stream));
+    BPPO_HIP(c, hipMemcpyAsync(c->d_m2, m2, n * 4, hipMemcpyHostToDevice, c->stream));
+    BPPO_HIP(c, sync_stream(c));
+    for (size_t t = 0; t < c->adam_t.size(); t++) c->adam_t[t] = steps[t];
+    return BPPO_OK;
+}
+
+extern "C" size_t bppo_num_param_tensors(const bppo_ctx *c) { return c ? c->adam_t.size() : 0; }
 
 extern "C" bppo_status bppo_vecenv_reset(bppo_ctx *c) {
     if (!c) return BPPO_ERR_ARG;

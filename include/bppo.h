@@ -16,7 +16,8 @@
  *                                                            main.rs:877-947, ppo.rs:1069-1264
  *   bppo_ppo_update               ppo_update (+ Adam/clip)   ppo.rs:1661-2112, main.rs:264-268
  *   bppo_gae_device               compute_gae on caller device buffers  ppo.rs:1069-1124
- *   bppo_rng_*                    the shared &mut StdRng     main.rs:189
+ *   bppo_rng_*                    the shared &mut StdRng     main.rs:189, checkpoint.rs:390-426
+ *   bppo_optimizer_*              Adam record (checkpoint)   checkpoint.rs:291-335
  *   bppo_obs_norm_* / ret_norm_*  ObsNormalizer / ReturnNormalizer  normalization.rs:12-260
  */
 #ifndef BPPO_H
@@ -109,6 +110,19 @@ bppo_status bppo_forward(bppo_ctx *ctx, const float *obs, const float *priv, int
 /* ---- main RNG (StdRng = ChaCha12; state = seed key + word position) ------- */
 bppo_status bppo_rng_get(bppo_ctx *ctx, uint64_t *word_pos);
 bppo_status bppo_rng_set(bppo_ctx *ctx, uint64_t word_pos);
+/* checkpoint.rs:390-400 save_rng_state: fill_bytes from the main RNG (ceil(n/4)
+ * words, little-endian; advances the position like the reference's draw) */
+bppo_status bppo_rng_fill_bytes(bppo_ctx *ctx, uint8_t *dst, size_t n);
+/* checkpoint.rs:405-426 load_rng_state: the main RNG becomes StdRng::from_seed(seed[32]) */
+bppo_status bppo_rng_from_seed(bppo_ctx *ctx, const uint8_t *seed);
+bppo_status bppo_rng_key_get(bppo_ctx *ctx, uint32_t key[8]);
+
+/* ---- optimizer (Adam) state, for checkpoint.rs save/load_optimizer ------- */
+/* m1, m2 flat like the parameters; steps[bppo_num_param_tensors] = Adam time per
+ * parameter tensor (W then b of every Linear, record order) */
+size_t bppo_num_param_tensors(const bppo_ctx *ctx);
+bppo_status bppo_optimizer_get(bppo_ctx *ctx, float *m1, float *m2, int32_t *steps, size_t n);
+bppo_status bppo_optimizer_set(bppo_ctx *ctx, const float *m1, const float *m2, const int32_t *steps, size_t n);
 
 /* ---- VecEnv ------------------------------------------------------------- */
 bppo_status bppo_vecenv_reset(bppo_ctx *ctx);  /* VecEnv::new: factory(i) + reset() */

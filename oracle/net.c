@@ -238,6 +238,19 @@ void or_sample_categorical(or_rng *rng, const float *logits, size_t B, int A, in
     }
 }
 
+/* utils.rs:96-135 apply_action_mask: 0 for a valid action, -inf otherwise;
+ * returns the first row with no valid action (the reference panics,
+ * utils.rs:115-123), or -1 */
+long or_apply_action_mask(float *logits, const uint8_t *mask, size_t B, int A) {
+    for (size_t r = 0; r < B; r++) {
+        int any = 0;
+        for (int a = 0; a < A; a++) any |= mask[r * A + a];
+        if (!any) return (long)r;
+    }
+    for (size_t q = 0; q < B * (size_t)A; q++) logits[q] += mask[q] ? 0.0f : -INFINITY;
+    return -1;
+}
+
 /* utils.rs:80-89: (a - mean) / (sqrt(var_unbiased) + 1e-8); raw stats ppo.rs:1905-1913.
  * Reductions accumulate in f64 (the reference's ndarray f32 order is unknowable). */
 void or_normalize_advantages(const float *adv, size_t n, float *out, float *mean_o, float *std_o,

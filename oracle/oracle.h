@@ -169,6 +169,8 @@ void or_ret_norm_update_return(or_ret_norm *n, int env, int player, float r);
 void or_ret_norm_update_variance(or_ret_norm *n, int env, int player);
 float or_ret_norm_normalize(const or_ret_norm *n, float r);
 void or_ret_norm_reset_player(or_ret_norm *n, int env, int player);
+void or_ret_norm_reset_env(or_ret_norm *n, int env);
+void or_ret_norm_update_and_normalize_all(or_ret_norm *n, float *rewards, const uint8_t *dones);
 
 /* ----------------------------------------------------------- networks ---- */
 /* Flat parameter layout = Burn module record order: for every Linear, W[in][out]
@@ -196,6 +198,7 @@ void or_linear(const float *x, const float *W, const float *b, size_t B, int in,
 
 /* ------------------------------------------------------------- policy ---- */
 void or_sample_categorical(or_rng *rng, const float *logits, size_t B, int A, int32_t *actions);
+long or_apply_action_mask(float *logits, const uint8_t *mask, size_t B, int A);   /* -1 ok, else empty row */
 void or_log_softmax_row(const float *x, int A, float *out);
 float or_log_prob(const float *logits, int A, int32_t a);
 float or_entropy(const float *logits, int A);
@@ -276,6 +279,11 @@ size_t or_trainer_num_params(const or_trainer *t);
 void or_trainer_get_params(const or_trainer *t, float *out);
 void or_trainer_set_params(or_trainer *t, const float *in);
 uint64_t or_trainer_rng_pos(const or_trainer *t);
+void or_trainer_set_rng(or_trainer *t, const uint32_t key[8], uint64_t pos);
+void or_trainer_set_adam(or_trainer *t, const float *m1, const float *m2, const int32_t *steps, int n_tensors);
+void or_trainer_get_adam(const or_trainer *t, float *m1, float *m2, int32_t *steps, int n_tensors);
+void or_trainer_set_norms(or_trainer *t, const double *mean, const double *m2, double count, const double *mvc,
+                          const double *returns);
 /* phases of one update, so tests can compare buffers phase by phase */
 int or_trainer_collect(or_trainer *t);                     /* returns episodes completed (all, not only those stored) */
 void or_trainer_gae(or_trainer *t);

@@ -219,6 +219,36 @@ void or_trainer_opponent_envs(const or_trainer *t, int32_t *learner_pos, int32_t
     if (pos_to_opp) memcpy(pos_to_opp, t->p2o, sizeof(int32_t) * (size_t)t->n_opp * t->P);
 }
 
+/* resume hooks (checkpoint.rs:405-465 load_*): main RNG = StdRng::from_seed(key
+ * bytes) at word position pos, Adam moments + per-tensor steps, normalizer state */
+void or_trainer_set_rng(or_trainer *t, const uint32_t key[8], uint64_t pos) {
+    or_rng_from_key(&t->rng, key, 12);
+    t->rng.word_pos = pos;
+}
+void or_trainer_set_adam(or_trainer *t, const float *m1, const float *m2, const int32_t *steps, int n_tensors) {
+    memcpy(t->adam.m1, m1, sizeof(float) * t->net.n_params);
+    memcpy(t->adam.m2, m2, sizeof(float) * t->net.n_params);
+    for (int i = 0; i < n_tensors; i++) t->adam.time[i] = steps[i];
+    t->adam.has_state = 1;
+}
+void or_trainer_get_adam(const or_trainer *t, float *m1, float *m2, int32_t *steps, int n_tensors) {
+    memcpy(m1, t->adam.m1, sizeof(float) * t->net.n_params);
+    memcpy(m2, t->adam.m2, sizeof(float) * t->net.n_params);
+    for (int i = 0; i < n_tensors; i++) steps[i] = t->adam.time[i];
+}
+void or_trainer_set_norms(or_trainer *t, const double *mean, const double *m2, double count, const double *mvc,
+                          const double *returns) {
+    if (mean) {
+        memcpy(t->on.mean, mean, sizeof(double) * t->D);
+        memcpy(t->on.var, m2, sizeof(double) * t->D);
+        t->on.count = count;
+    }
+    if (mvc) {
+        t->rn.mean = mvc[0]; t->rn.var = mvc[1]; t->rn.count = mvc[2];
+        if (returns) memcpy(t->rn.returns, returns, sizeof(double) * (size_t)t->N * t->P);
+    }
+}
+
 size_t or_trainer_num_params(const or_trainer *t) { return t->net.n_params; }
 void or_trainer_get_params(const or_trainer *t, float *o) { memcpy(o, t->params, sizeof(float) * t->net.n_params); }
 void or_trainer_set_params(or_trainer *t, const float *i) { memcpy(t->params, i, sizeof(float) * t->net.n_params); }
@@ -373,13 +403,8 @@ int or_trainer_collect(or_trainer *t) {
             for (size_t q = 0; q < (size_t)N * A; q++) t->masks[base * A + q] = mk[q] ? 1.0f : 0.0f;
         forward_rows(t, obs, G ? t->priv + base * G : NULL, N, logits, vals);  /* :322-333 */
         if (hm) {                                                /* :337 apply_action_mask */
-            for (int e = 0; e < N; e++) {
-                int any = 0;
-                for (int a = 0; a < A; a++) any |= mk[(size_t)e * A + a];
-                if (!any) { fprintf(stderr, "Empty action mask: env %d\n", e); abort(); }
-                for (int a = 0; a < A; a++)
-                    logits[(size_t)e * A + a] += mk[(size_t)e * A + a] ? 0.0f : -INFINITY;
-            }
+            long bad = or_apply_action_mask(logits, mk, (size_t)N, A);
+            if (bad >= 0) { fprintf(stderr, "Empty action mask: env %ld\n", bad); abort(); }
         }
         or_sample_categorical(&t->rng, logits, N, A, act);       /* :338 */
         for (int e = 0; e < N; e++) {                            /* :339 */

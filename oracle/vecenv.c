@@ -217,3 +217,18 @@ float or_ret_norm_normalize(const or_ret_norm *n, float r) {
 void or_ret_norm_reset_player(or_ret_norm *n, int e, int p) {
     n->returns[(size_t)e * n->num_players + p] = 0.0;
 }
+/* normalization.rs:202-210 */
+void or_ret_norm_reset_env(or_ret_norm *n, int e) {
+    for (int p = 0; p < n->num_players; p++) n->returns[(size_t)e * n->num_players + p] = 0.0;
+}
+/* normalization.rs:220-243 (single-player convenience): per env update the
+ * rolling return, the variance stats, normalize in place, reset on done */
+void or_ret_norm_update_and_normalize_all(or_ret_norm *n, float *rewards, const uint8_t *dones) {
+    for (int e = 0; e < n->num_envs; e++) {
+        const float r = rewards[e];
+        or_ret_norm_update_return(n, e, 0, r);
+        or_ret_norm_update_variance(n, e, 0);
+        rewards[e] = or_ret_norm_normalize(n, r);
+        if (dones[e]) or_ret_norm_reset_player(n, e, 0);
+    }
+}

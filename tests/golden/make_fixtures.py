@@ -1,0 +1,131 @@
+"""Generates the committed golden fixtures of SURVEY.md 8(c) (oracle plan item 5)
+from the CPU oracle (oracle/, a restatement of the reference path):
+
+  cartpole_traj_16x32.npz   a 16-env x 32-step CartPole rollout (CfgB net, both
+                            normalizers) + bootstrap + GAE from fixed params
+                            (collect_rollouts ppo.rs:213-500, GAE ppo.rs:1069-1124)
+  c4_scripted.npz           Connect Four VecEnv driven by a scripted action matrix
+  ld_scripted.npz           Liar's Dice VecEnv (with privileged obs) the same way
+                            (env.rs:400-487, connect_four.rs, liars_dice.rs)
+  minibatch_cfgB.npz        one minibatch (512 rows, CfgB net) through
+                            compute_minibatch_loss + backward + Adam with per-tensor
+                            clip (ppo.rs:1385-1592, main.rs:264-268): metrics, the
+                            gradient and the parameters after the step
+
+Inputs and expected outputs only (data, no reference source).  Regenerate with
+    python tests/golden/make_fixtures.py
+Tests: tests/test_golden.py (oracle, CPU) and tests/test_gpu_golden.py (device).
+"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "burn-ppo_amd"))
+
+import oracle_ffi as O  # noqa: E402
+from bppo.host import make_config, orthogonal_init  # noqa: E402
+
+
+def cartpole_traj():
+    N, T = 16, 32
+    cfg = make_config("cartpole", num_envs=N, num_steps=T)
+    params = orthogonal_init(cfg, seed=1)
+    ot = O.Trainer(O.train_cfg(num_envs=N, num_steps=T, lr=1e-3), params)
+    n_eps = ot.collect()
+    ot.gae()
+    out = dict(params=params, num_envs=N, num_steps=T, seed=cfg["seed"], episodes=n_eps, rng_pos=ot.rng_pos())
+    for k, dt in (("obs", np.float32), ("actions", np.int32), ("rewards", np.float32), ("dones", np.float32),
+                  ("values", np.float32), ("log_probs", np.float32), ("advantages", np.float32),
+                  ("returns", np.float32)):
+        out[k] = ot.buffer(k, dt)
+    m, v, c = ot.obs_norm_state(5)
+    out.update(obs_norm_mean=m, obs_norm_m2=v, obs_norm_count=c, ret_norm=ot.ret_norm_state())
+    ot.close()
+    return out
+
+
+def scripted(kind, N, steps, D, A, P, G, shaping):
+    v = O.lib().or_vecenv_new(kind, N, 42)
+    O.lib().or_vecenv_set_shaping(v, shaping)
+    rng = np.random.default_rng(kind)
+    obs = np.zeros(N * D, np.float32)
+    mk = np.zeros(N * A, np.uint8)
+    pl = np.zeros(N, np.int32)
+    g = np.zeros(max(N * G, 1), np.float32)
+    rw = np.zeros(N * P, np.float32)
+    dn = np.zeros(N, np.uint8)
+    eps = (O.Episode * N)()
+    rec = {k: [] for k in ("obs", "masks", "players", "priv", "actions", "rewards", "dones", "next_obs")}
+    for _ in range(steps):
+        O.lib().or_vecenv_get_obs(v, obs)
+        O.lib().or_vecenv_get_masks(v, mk)
+        O.lib().or_vecenv_get_players(v, pl)
+        if G:
+            O.lib().or_vecenv_get_priv(v, g)
+        m = mk.reshape(N, A).astype(bool)
+        a = np.array([rng.choice(np.flatnonzero(row)) for row in m], np.int32)
+        rec["obs"].append(obs.copy()); rec["masks"].append(mk.copy()); rec["players"].append(pl.copy())
+        rec["priv"].append(g.copy()); rec["actions"].append(a)
+        O.lib().or_vecenv_step(v, a, obs, rw, dn, eps, N)
+        rec["rewards"].append(rw.copy()); rec["dones"].append(dn.copy()); rec["next_obs"].append(obs.copy())
+    O.lib().or_vecenv_free(v)
+    out = {k: np.stack(x) for k, x in rec.items()}
+    out.update(num_envs=N, seed=42, shaping=shaping)
+    return out
+
+
+def minibatch():
+    N, T = 16, 32
+    cfg = make_config("cartpole", num_envs=N, num_steps=T, num_epochs=1, num_minibatches=1)
+    params = orthogonal_init(cfg, seed=4)
+    ot = O.Trainer(O.train_cfg(num_envs=N, num_steps=T, lr=1e-3, num_epochs=1, num_minibatches=1), params)
+    ot.collect()
+    ot.gae()
+    # the buffers one minibatch reads, made less trivial than a first rollout:
+    # old log-probs / values perturbed so that ratio != 1 and the clip is hit
+    rng = np.random.default_rng(9)
+    B = N * T
+    obs = ot.buffer("obs").reshape(B, 5)
+    act = ot.buffer("actions", np.int32)
+    logp = (ot.buffer("log_probs") + rng.normal(0, 0.3, B)).astype(np.float32)
+    adv = ot.buffer("advantages")
+    ret = ot.buffer("returns")
+    val = (ot.buffer("values") + rng.normal(0, 0.2, B)).astype(np.float32)
+    ot.close()
+    # loss + gradient on the whole buffer (one minibatch; row order only moves
+    # the f64 summation)
+    desc = O.mlp_desc(5, 2, 64, 2, True)
+    advn = np.zeros(B, np.float32)
+    st = [C.c_float() for _ in range(4)]
+    O.lib().or_normalize_advantages(adv, B, advn, *[C.byref(x) for x in st])
+    grads = np.zeros(desc.n_params, np.float32)
+    ms = O.MbStats()
+    pc = O.ppo_cfg(num_epochs=1, num_minibatches=1)
+    O.lib().or_minibatch_loss_grad(C.byref(desc), params, B, obs.reshape(-1), None, act, logp, advn, ret, val,
+                                   None, C.byref(pc), 0.01, grads, C.byref(ms))
+    # per-tensor norm clip + Adam step 1 (main.rs:264-268)
+    adam = O.Adam()
+    O.lib().or_adam_init(C.byref(adam), C.byref(desc))
+    after = params.copy()
+    O.lib().or_adam_step(C.byref(desc), C.byref(adam), after, grads.copy(), 1e-3, 0.5, 1e-5)
+    O.lib().or_adam_free(C.byref(adam))
+    return dict(params=params, obs=obs, actions=act, log_probs=logp, advantages=adv, returns=ret, values=val,
+                grads=grads, params_after=after, loss=ms.loss, policy_loss=ms.policy_loss, value_loss=ms.value_loss,
+                entropy=ms.entropy, approx_kl=ms.approx_kl, clip_fraction=ms.clip_fraction,
+                adv_mean=st[0].value, adv_std=st[1].value, lr=1e-3, ent_coef=0.01, max_grad_norm=0.5)
+
+
+def main():
+    np.savez_compressed(os.path.join(HERE, "cartpole_traj_16x32.npz"), **cartpole_traj())
+    np.savez_compressed(os.path.join(HERE, "c4_scripted.npz"), **scripted(O.ENV_CONNECT_FOUR, 6, 60, 86, 7, 2, 0, 0.0))
+    np.savez_compressed(os.path.join(HERE, "ld_scripted.npz"), **scripted(O.ENV_LIARS_DICE, 4, 80, 270, 49, 4, 120, 0.05))
+    np.savez_compressed(os.path.join(HERE, "minibatch_cfgB.npz"), **minibatch())
+
+
+if __name__ == "__main__":
+    main()

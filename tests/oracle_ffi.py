@@ -50,6 +50,22 @@ class LiarsDice(C.Structure):
                 ("global_step", C.c_uint64), ("rng", Rng)]
 
 
+class ObsNorm(C.Structure):
+    _fields_ = [("dim", C.c_int), ("mean", C.POINTER(C.c_double)), ("var", C.POINTER(C.c_double)),
+                ("count", C.c_double), ("clip", C.c_float)]
+
+
+class RetNorm(C.Structure):
+    _fields_ = [("num_envs", C.c_int), ("num_players", C.c_int), ("returns", C.POINTER(C.c_double)),
+                ("var", C.c_double), ("mean", C.c_double), ("count", C.c_double), ("gamma", C.c_double),
+                ("epsilon", C.c_double), ("clip", C.c_float)]
+
+
+class Adam(C.Structure):
+    _fields_ = [("m1", C.POINTER(C.c_float)), ("m2", C.POINTER(C.c_float)), ("time", C.POINTER(C.c_int32)),
+                ("has_state", C.c_int)]
+
+
 class Episode(C.Structure):
     _fields_ = [("total_rewards", C.c_float * 4), ("length", C.c_int32), ("env_index", C.c_int32)]
 
@@ -184,6 +200,28 @@ def lib():
             "or_shuffle_positions": (None, [C.c_void_p, C.c_int, i32, C.c_void_p, i32]),
             "or_gen_range_u64": (C.c_uint64, [C.c_void_p, C.c_uint64, C.c_uint64]),
             "or_set_mlp_parallel": (None, [C.c_int]),
+            "or_obs_norm_init": (None, [C.POINTER(ObsNorm), C.c_int, C.c_float]),
+            "or_obs_norm_free": (None, [C.POINTER(ObsNorm)]),
+            "or_obs_norm_update_batch": (None, [C.POINTER(ObsNorm), f32, C.c_size_t]),
+            "or_obs_norm_normalize_batch": (None, [C.POINTER(ObsNorm), f32, C.c_size_t]),
+            "or_ret_norm_init": (None, [C.POINTER(RetNorm), C.c_int, C.c_int, C.c_double, C.c_float]),
+            "or_ret_norm_free": (None, [C.POINTER(RetNorm)]),
+            "or_ret_norm_update_return": (None, [C.POINTER(RetNorm), C.c_int, C.c_int, C.c_float]),
+            "or_ret_norm_update_variance": (None, [C.POINTER(RetNorm), C.c_int, C.c_int]),
+            "or_ret_norm_normalize": (C.c_float, [C.POINTER(RetNorm), C.c_float]),
+            "or_ret_norm_reset_player": (None, [C.POINTER(RetNorm), C.c_int, C.c_int]),
+            "or_ret_norm_reset_env": (None, [C.POINTER(RetNorm), C.c_int]),
+            "or_ret_norm_update_and_normalize_all": (None, [C.POINTER(RetNorm), f32, u8]),
+            "or_apply_action_mask": (C.c_long, [f32, u8, C.c_size_t, C.c_int]),
+            "or_trainer_set_rng": (None, [C.c_void_p, u32, C.c_uint64]),
+            "or_trainer_set_adam": (None, [C.c_void_p, f32, f32, i32, C.c_int]),
+            "or_trainer_get_adam": (None, [C.c_void_p, f32, f32, i32, C.c_int]),
+            "or_trainer_set_norms": (None, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_double, C.c_void_p,
+                                            C.c_void_p]),
+            "or_adam_init": (None, [C.POINTER(Adam), C.POINTER(NetDesc)]),
+            "or_adam_free": (None, [C.POINTER(Adam)]),
+            "or_adam_step": (None, [C.POINTER(NetDesc), C.POINTER(Adam), f32, f32, C.c_double, C.c_float,
+                                    C.c_float]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
