@@ -56,7 +56,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--num-envs", type=int, default=65536, help="envs per GPU")
     p.add_argument("--num-steps", type=int, default=128)
-    p.add_argument("--cpu-envs", type=int, default=2048, help="CPU baseline sample size (envs)")
+    p.add_argument("--cpu-envs", type=int, default=8192, help="CPU baseline sample size (envs)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-learning", action="store_true", help="skip the steps-to-475 runs")
     p.add_argument("--selftest", action="store_true", help="N>1 harness check with gloo and no GPU work")

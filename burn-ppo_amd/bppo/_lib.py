@@ -33,7 +33,9 @@ class Config(C.Structure):
                 ("value_coef", C.c_double), ("max_grad_norm", C.c_double), ("adam_epsilon", C.c_double),
                 ("target_kl", C.c_double), ("return_clip", C.c_double),
                 ("reward_shaping_coef", C.c_double), ("seed", C.c_uint64), ("env_seed_base", C.c_uint64),
-                ("rng_stream", C.c_uint64)]
+                ("rng_stream", C.c_uint64),
+                ("cnn", C.c_int32), ("num_conv_layers", C.c_int32), ("conv_channels", C.c_int32 * 4),
+                ("kernel_size", C.c_int32), ("cnn_fc_hidden_size", C.c_int32), ("cnn_num_fc_layers", C.c_int32)]
 
 
 class Episode(C.Structure):

@@ -169,7 +169,13 @@ class CheckpointMetadata:
         act = {"cartpole": 2, "connect_four": 7, "liars_dice": 49}[cfg["env"]]
         P = {"cartpole": 1, "connect_four": 2, "liars_dice": 4}[cfg["env"]]
         ctde = cfg["network_type"] == "ctde"
-        return cls(step=int(step), avg_return=float(avg_return), rng_seed=int(cfg["seed"]),
+        cnn = {}
+        if cfg["network_type"] == "cnn":
+            from .host import conv_channels
+            cnn = dict(num_conv_layers=cfg["num_conv_layers"], conv_channels=conv_channels(cfg),
+                       kernel_size=cfg["kernel_size"], cnn_fc_hidden_size=cfg["cnn_fc_hidden_size"],
+                       cnn_num_fc_layers=cfg["cnn_num_fc_layers"], obs_shape=(6, 7, 2))
+        return cls(**cnn, step=int(step), avg_return=float(avg_return), rng_seed=int(cfg["seed"]),
                    best_avg_return=best_avg_return, recent_returns=[float(x) for x in recent_returns],
                    forked_from=forked_from, obs_dim=obs, action_count=act, num_players=P,
                    hidden_size=cfg["hidden_size"], num_hidden=cfg["num_hidden"], activation=cfg["activation"],
@@ -221,6 +227,23 @@ def model_record(cfg, params):
     """ActorCriticNetwork record item (enum variant -> {"Mlp"|"Ctde": {...}})"""
     lin = _split(cfg, np.asarray(params, np.float32))
     nh = cfg["num_hidden"]
+    if cfg["network_type"] == "cnn":
+        # cnn.rs:24-50: Conv2d {weight [Cout][Cin][k][k], bias}, then Linear layers
+        from .host import conv_channels
+        ch, ks = conv_channels(cfg), cfg["kernel_size"]
+        nc, nf = len(ch), cfg["cnn_num_fc_layers"]
+        conv = []
+        for i, (W, b) in enumerate(lin[:nc]):
+            cin = W.shape[0] // (ks * ks)
+            conv.append({"weight": {"id": _param_id(f"conv_layers.{i}.weight"),
+                                    "param": _tensor(W.reshape(-1).reshape(ch[i], cin, ks, ks))},
+                         "bias": {"id": _param_id(f"conv_layers.{i}.bias"), "param": _tensor(b)}})
+        item = {"Cnn": {"conv_layers": conv,
+                        "fc_layers": [_linear(W, b, f"fc_layers.{i}") for i, (W, b) in enumerate(lin[nc:nc + nf])],
+                        "critic_conv_layers": [], "critic_fc_layers": [],
+                        "policy_head": _linear(*lin[nc + nf], "policy_head"),
+                        "value_head": _linear(*lin[nc + nf + 1], "value_head")}}
+        return {"metadata": BURN_METADATA, "item": item}
     if cfg["network_type"] == "ctde":
         nc = cfg["critic_num_hidden"] or nh
         item = {"Ctde": {"actor_layers": [_linear(W, b, f"actor_layers.{i}") for i, (W, b) in enumerate(lin[:nh])],
@@ -238,6 +261,10 @@ def model_record(cfg, params):
 
 def _linears_in_order(item):
     (kind, rec), = item.items()
+    if kind == "Cnn":
+        if rec["critic_conv_layers"] or rec["critic_fc_layers"]:
+            raise ValueError("split_networks CNN checkpoints are not supported by the device path")
+        return rec["conv_layers"] + rec["fc_layers"] + [rec["policy_head"], rec["value_head"]]
     if kind == "Ctde":
         seq = rec["actor_layers"] + [rec["policy_head"]] + rec["critic_layers"] + [rec["value_head"]]
     elif kind == "Mlp":

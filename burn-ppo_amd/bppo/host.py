@@ -32,7 +32,9 @@ BASE = dict(env="cartpole", num_envs=32, num_steps=128, hidden_size=64, num_hidd
             num_minibatches=4, normalize_obs=False, normalize_returns=None, clip_value=False, gamma=0.99,
             gae_lambda=0.95, clip_epsilon=0.2, value_coef=0.5, max_grad_norm=0.5, adam_epsilon=1e-5,
             target_kl=None, return_clip=10.0, reward_shaping_coef=0.0, learning_rate=[(2.5e-4, 0)],
-            entropy_coef=[(0.01, 0)], seed=42)
+            entropy_coef=[(0.01, 0)], seed=42,
+            # network_type = "cnn" (config.rs:996-1010 defaults)
+            num_conv_layers=2, conv_channels=[8, 8], kernel_size=3, cnn_fc_hidden_size=32, cnn_num_fc_layers=1)
 
 PRESETS = {
     # configs/test.toml (CfgA runs it with --num-envs 8 --num-steps 128)
@@ -90,19 +92,50 @@ def to_struct(c, rank=0, world=1, envs_per_rank=None):
         setattr(s, k, float(c[k]))
     s.target_kl = -1.0 if c["target_kl"] is None else float(c["target_kl"])
     s.seed = c["seed"]
+    s.cnn = int(c["network_type"] == "cnn")
+    if s.cnn:
+        s.num_conv_layers = c["num_conv_layers"]
+        ch = conv_channels(c)
+        for i in range(4):
+            s.conv_channels[i] = ch[min(i, len(ch) - 1)]
+        s.kernel_size = c["kernel_size"]
+        s.cnn_fc_hidden_size = c["cnn_fc_hidden_size"]
+        s.cnn_num_fc_layers = c["cnn_num_fc_layers"]
     # W > 1: global env index = rank * n + i; main RNG stream = rank
     s.env_seed_base, s.rng_stream = shard(c, rank, world, n)
     return s
 
 
+def conv_channels(c):
+    """cnn.rs:84-90: channels of conv layer i, the last entry repeated"""
+    ch = list(c["conv_channels"])
+    if not ch:
+        raise ValueError("conv_channels must not be empty")          # config.rs:1575-1577
+    return [ch[min(i, len(ch) - 1)] for i in range(c["num_conv_layers"])]
+
+
 def layer_shapes(c):
     """Burn record order: hidden..., policy head, value head (MLP) /
-    actor hidden..., policy, critic hidden..., value (CTDE)."""
+    actor hidden..., policy, critic hidden..., value (CTDE) /
+    conv layers (as (Cin*k*k, Cout)), FC layers, policy, value (CNN)."""
     obs = {"cartpole": 5, "connect_four": 86, "liars_dice": 270}[c["env"]]
     act = {"cartpole": 2, "connect_four": 7, "liars_dice": 49}[c["env"]]
     shapes, gains = [], []
     hg = np.sqrt(2.0) if c["activation"] == "relu" else 1.0
     i = obs
+    if c["network_type"] == "cnn":
+        if c["env"] != "connect_four":
+            raise ValueError("CNN requires OBSERVATION_SHAPE")          # cnn.rs:73-74
+        H, W, C0 = 6, 7, 2                                              # connect_four.rs:217
+        cin = C0
+        for co in conv_channels(c):
+            shapes.append((cin * c["kernel_size"] ** 2, co)); gains.append(None); cin = co
+        i = H * W * cin + (obs - H * W * C0)
+        for _ in range(c["cnn_num_fc_layers"]):
+            shapes.append((i, c["cnn_fc_hidden_size"])); gains.append(hg); i = c["cnn_fc_hidden_size"]
+        shapes.append((i, act)); gains.append(0.01)
+        shapes.append((i, 1)); gains.append(1.0)
+        return shapes, gains
     for _ in range(c["num_hidden"]):
         shapes.append((i, c["hidden_size"])); gains.append(hg); i = c["hidden_size"]
     shapes.append((i, act)); gains.append(0.01)
@@ -125,6 +158,13 @@ def orthogonal_init(c, seed=0):
     out = []
     shapes, gains = layer_shapes(c)
     for (i, o), g in zip(shapes, gains):
+        if g is None:
+            # Conv2d (Burn default KaimingUniform, gain 1/sqrt(3)): U(-1/sqrt(fan_in), 1/sqrt(fan_in))
+            # for the weight [Cout][Cin][k][k] and the bias
+            bound = 1.0 / np.sqrt(i)
+            out.append(rng.uniform(-bound, bound, o * i).astype(np.float32))
+            out.append(rng.uniform(-bound, bound, o).astype(np.float32))
+            continue
         a = rng.standard_normal((max(i, o), min(i, o)))
         q, r = np.linalg.qr(a)
         q = q * np.sign(np.diag(r))

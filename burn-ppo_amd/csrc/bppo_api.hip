@@ -25,8 +25,28 @@ NetLayout make_layout(const bppo_config &c, int obs_dim, int priv_dim, int act_d
         return i;
     };
     int in = obs_dim;
-    for (int l = 0; l < c.num_hidden; l++) { add(in, c.hidden_size); in = c.hidden_size; }
-    L.n_actor_hidden = c.num_hidden;
+    if (c.cnn) {
+        // cnn.rs:66-150: conv stack on the (H, W, C) spatial part, FC layers on
+        // [flattened conv output | extra features], heads of cnn_fc_hidden_size
+        L.H = 6; L.W = 7; L.C = 2;                     // connect_four.rs:217 OBSERVATION_SHAPE
+        L.E = obs_dim - L.H * L.W * L.C;
+        L.ksize = c.kernel_size;
+        int cin = L.C;
+        for (int l = 0; l < c.num_conv_layers; l++) {
+            const int co = c.conv_channels[l < 4 ? l : 3];
+            L.conv_cin[l] = cin;
+            add(cin * L.ksize * L.ksize, co);
+            cin = co;
+        }
+        L.n_conv = c.num_conv_layers;
+        L.fdim = L.H * L.W * cin + L.E;
+        in = L.fdim;
+        for (int l = 0; l < c.cnn_num_fc_layers; l++) { add(in, c.cnn_fc_hidden_size); in = c.cnn_fc_hidden_size; }
+        L.n_actor_hidden = L.n_conv + c.cnn_num_fc_layers;
+    } else {
+        for (int l = 0; l < c.num_hidden; l++) { add(in, c.hidden_size); in = c.hidden_size; }
+        L.n_actor_hidden = c.num_hidden;
+    }
     L.policy = add(in, act_dim);
     if (c.ctde) {
         int cin = priv_dim + obs_dim;
@@ -121,6 +141,17 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     }
     c->wide = cfg->env_kind != BPPO_ENV_CARTPOLE;
     if (c->wide && !cfg->ctde) c->G = 0;
+    if (cfg->cnn) {
+        // cnn.rs:73-74 "CNN requires OBSERVATION_SHAPE" (only Connect Four has one)
+        if (cfg->env_kind != BPPO_ENV_CONNECT_FOUR || cfg->ctde) { c->err = "CNN requires OBSERVATION_SHAPE (Connect Four)"; return BPPO_ERR_ARG; }
+        if (cfg->num_conv_layers < 1 || cfg->num_conv_layers > 4 || cfg->kernel_size < 1 || cfg->kernel_size > 7 ||
+            !(cfg->kernel_size & 1) || cfg->cnn_num_fc_layers < 1 || cfg->cnn_fc_hidden_size < 1) {
+            c->err = "CNN: 1-4 conv layers, odd kernel_size <= 7 (same padding), >= 1 FC layer";
+            return BPPO_ERR_UNSUPPORTED;
+        }
+        for (int l = 0; l < cfg->num_conv_layers; l++)
+            if (cfg->conv_channels[l < 4 ? l : 3] < 1) { c->err = "conv_channels must be positive"; return BPPO_ERR_ARG; }
+    }
     c->net = make_layout(*cfg, c->D, c->G, c->A);
     const size_t np = c->net.n_params;
     const size_t TN = (size_t)c->T * c->N;

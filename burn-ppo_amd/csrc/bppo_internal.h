@@ -26,6 +26,11 @@ struct NetLayout {
     int critic_first = -1;        // CTDE critic hidden layers [critic_first, value)
     int ctde = 0, relu = 1;
     size_t n_params = 0;
+    // CNN (network/cnn.rs): layers [0, n_conv) are the conv layers (in = Cin k k,
+    // out = Cout; weight [Cout][Cin][k][k] then bias in Burn record order), then the
+    // FC layers [n_conv, n_actor_hidden), policy, value
+    int n_conv = 0, ksize = 3, H = 0, W = 0, C = 0, E = 0, fdim = 0;
+    int conv_cin[4] = {0, 0, 0, 0};
 };
 NetLayout make_layout(const bppo_config &c, int obs_dim, int priv_dim, int act_dim);
 
@@ -269,6 +274,13 @@ struct bppo_ctx {
     float *d_heads = nullptr, *d_heads_b = nullptr; // packed shared-trunk heads [W][A+1], [A+1]
     float *d_part = nullptr, *d_colsum = nullptr;   // split-K weight-grad scratch
     double *d_mpart = nullptr;        // loss-metric partials
+    // CNN actor-critic (cnn.hip): conv outputs (post-relu, NHWC rows) per conv layer,
+    // im2col scratch, the flattened NCHW features + extra [rows][fdim], backward
+    // scratch, conv weights packed [k k Cin][Cout] (GEMM operand) and their gradient
+    float *d_cnn_y[4] = {nullptr, nullptr, nullptr, nullptr};
+    float *d_cnn_a = nullptr, *d_cnn_f = nullptr, *d_cnn_dy[2] = {nullptr, nullptr};
+    float *d_cnn_wt = nullptr, *d_cnn_owt = nullptr, *d_cnn_dwt = nullptr;
+    size_t cnn_wt_off[4] = {0, 0, 0, 0};
     float *d_bxc = nullptr;           // bootstrap / VecEnv scratch rows [N][L]
     uint8_t *d_bmask = nullptr;
     int32_t *d_bplayers = nullptr;
@@ -330,6 +342,13 @@ bppo_status wide_reset(bppo_ctx *c);
 bppo_status wide_pack(bppo_ctx *c);
 bppo_status wide_forward(bppo_ctx *c, int rows, const float *xc, int ldxc, float *logits, float *values);
 bppo_status wide_forward_actor(bppo_ctx *c, int rows, const float *xc, int ldxc, const float *params, float *logits);
+// CNN trunk (cnn.hip): conv stack + flatten of `rows` obs rows -> d_cnn_f; backward
+// of the conv stack from dF (dL/d features, [rows][fdim]) into the gradient
+bppo_status cnn_alloc(bppo_ctx *c);
+void cnn_free(bppo_ctx *c);
+bppo_status cnn_pack(bppo_ctx *c, const float *params, float *wt);
+bppo_status cnn_features(bppo_ctx *c, int rows, const float *x, int ldx, const float *params, const float *wt);
+bppo_status cnn_backward(bppo_ctx *c, int rows, const float *x, int ldx, float *dF, float *grad);
 // opponent pool (opponents.hip)
 bool opp_active(const bppo_ctx *c);
 bppo_status opp_alloc(bppo_ctx *c);

@@ -39,8 +39,10 @@ static bppo_status walloc(bppo_ctx *c, T **p, size_t n) {
         if (_s != BPPO_OK) return _s;          \
     } while (0)
 
+// fully connected hidden layers (their activations live in d_hbuf); CNN conv
+// layers [0, n_conv) keep theirs in d_cnn_y (cnn.hip)
 static bool is_hidden(const NetLayout &n, int l) {
-    return l < n.n_actor_hidden || (n.ctde && l >= n.critic_first && l < n.value);
+    return (l >= n.n_conv && l < n.n_actor_hidden) || (n.ctde && l >= n.critic_first && l < n.value);
 }
 
 bppo_status wide_init(bppo_ctx *c) {
@@ -80,7 +82,8 @@ bppo_status wide_init(bppo_ctx *c) {
         if (!n.ctde && l == n.policy) N = c->A + 1;
         if (!n.ctde && l == n.value) continue;
         const int Kin = (!n.ctde && l == n.policy) ? n.in[l] : n.in[l];
-        const int s = gemm_wg_splits(Kin, N, mb_max);
+        const int rows_l = l < n.n_conv ? mb_max * n.H * n.W : mb_max;   // conv GEMMs: one row per position
+        const int s = gemm_wg_splits(Kin, N, rows_l);
         part = std::max(part, (size_t)s * Kin * N);
         cs = std::max(cs, (size_t)s * N);
     }
@@ -93,6 +96,7 @@ bppo_status wide_init(bppo_ctx *c) {
     WTRY(walloc(c, &c->d_act_in, (size_t)c->N));
     WTRY(walloc(c, &c->d_scr_r, (size_t)c->N * c->P));
     WTRY(walloc(c, &c->d_scr_d, (size_t)c->N));
+    if (n.n_conv) WTRY(cnn_alloc(c));
     if (cfg.normalize_obs) {
         WTRY(walloc(c, &c->d_obs_raw, TN * c->D));
         c->obsw_part_n = (size_t)256 * c->D * 3;
@@ -107,6 +111,7 @@ void wide_free(bppo_ctx *c) {
                     c->d_heads_b, c->d_part, c->d_colsum, c->d_mpart, c->d_bxc, c->d_bmask, c->d_bplayers,
                     c->d_act_in, c->d_scr_r, c->d_scr_d, c->d_obs_raw, c->d_obsw_part};
     for (void *p : ptrs) if (p) (void)hipFree(p);
+    cnn_free(c);
     opp_free(c);
 }
 
@@ -119,6 +124,7 @@ bppo_status wide_reset(bppo_ctx *c) {
 // shared-trunk heads packed as one [W][A+1] GEMM operand (after every params change)
 bppo_status wide_pack(bppo_ctx *c) {
     const NetLayout &n = c->net;
+    if (n.n_conv) WTRY(cnn_pack(c, c->d_params, c->d_cnn_wt));
     if (n.ctde) return BPPO_OK;
     WHIP(c, wide_pack_heads(c->stream, c->d_params, n.in[n.policy], c->A, n.w[n.policy], n.b[n.policy],
                             n.w[n.value], n.b[n.value], c->d_heads, c->d_heads_b));
@@ -132,7 +138,11 @@ bppo_status wide_forward(bppo_ctx *c, int rows, const float *xc, int ldxc, float
     const float *P = c->d_params;
     const float *x = xc + c->G;
     int ldx = ldxc;
-    for (int l = 0; l < n.n_actor_hidden; l++) {
+    if (n.n_conv) {                                  // CNN trunk (cnn.rs:241-330) -> features [rows][fdim]
+        WTRY(cnn_features(c, rows, x, ldx, P, c->d_cnn_wt));
+        x = c->d_cnn_f; ldx = n.fdim;
+    }
+    for (int l = n.n_conv; l < n.n_actor_hidden; l++) {
         float *h = c->d_hbuf + c->hoff[l];
         WHIP(c, gemm_fwd(c->stream, rows, n.out[l], n.in[l], x, ldx, P + n.w[l], n.out[l], P + n.b[l], c->cfg.relu ? 1 : 2, h,
                          n.out[l], n.out[l], nullptr, 0));
@@ -165,7 +175,12 @@ bppo_status wide_forward_actor(bppo_ctx *c, int rows, const float *xc, int ldxc,
     const NetLayout &n = c->net;
     const float *x = xc + c->G;
     int ldx = ldxc;
-    for (int l = 0; l < n.n_actor_hidden; l++) {
+    if (n.n_conv) {
+        WTRY(cnn_pack(c, P, c->d_cnn_owt));
+        WTRY(cnn_features(c, rows, x, ldx, P, c->d_cnn_owt));
+        x = c->d_cnn_f; ldx = n.fdim;
+    }
+    for (int l = n.n_conv; l < n.n_actor_hidden; l++) {
         float *h = c->d_hbuf + c->hoff[l];
         WHIP(c, gemm_fwd(c->stream, rows, n.out[l], n.in[l], x, ldx, P + n.w[l], n.out[l], P + n.b[l],
                          c->cfg.relu ? 1 : 2, h, n.out[l], n.out[l], nullptr, 0));
@@ -279,7 +294,18 @@ bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, float ent_c
         WTRY(wgrad(Wa, A + 1, Ha, Wa, c->d_dout, A + 1, G + n.w[n.policy], A, A, G + n.w[n.value], 1,
                    G + n.b[n.policy], G + n.b[n.value]));
         WHIP(c, gemm_dx(c->stream, rows, Wa, A + 1, c->d_dout, A + 1, c->d_heads, A + 1, Ha, Wa, hact, dz, Wa));
-        WTRY(hidden_chain(0, la, c->d_xcg + c->G, L));
+        if (!n.n_conv) {
+            WTRY(hidden_chain(0, la, c->d_xcg + c->G, L));
+            return BPPO_OK;
+        }
+        // CNN: FC layers down to the features, dF = dz W^T * [F > 0] (the conv
+        // part of F is relu output), then the conv stack
+        const int f0 = n.n_conv;
+        WTRY(hidden_chain(f0, la, c->d_cnn_f, n.fdim));
+        float *dF = c->d_cnn_dy[0];
+        WHIP(c, gemm_dx(c->stream, rows, n.fdim, n.out[f0], dz, n.out[f0], P + n.w[f0], n.out[f0], c->d_cnn_f, n.fdim, 1,
+                        dF, n.fdim));
+        WTRY(cnn_backward(c, rows, c->d_xcg + c->G, L, dF, G));
         return BPPO_OK;
     }
     // CTDE actor

@@ -58,6 +58,11 @@ typedef struct {
     uint64_t seed;               /* main StdRng seed (main.rs:189) */
     uint64_t env_seed_base;      /* env i is seeded env_seed_base + i (main.rs:1964) */
     uint64_t rng_stream;         /* ChaCha stream id of the main RNG: 0 = reference; rank for W>1 */
+    /* network_type = "cnn" (network/cnn.rs:24-50; Connect Four, OBSERVATION_SHAPE (6, 7, 2)):
+     * num_conv_layers conv layers (stride 1, same padding, odd kernel_size, relu),
+     * conv_channels per layer (the last repeated past the list, cnn.rs:84-90),
+     * cnn_num_fc_layers FC layers of cnn_fc_hidden_size, then the heads */
+    int32_t cnn, num_conv_layers, conv_channels[4], kernel_size, cnn_fc_hidden_size, cnn_num_fc_layers;
 } bppo_config;
 
 typedef struct {

@@ -30,6 +30,17 @@ typedef struct { int in, out; size_t w, b; } layer_t;
 /* parameter layout = Burn record order (mlp.rs:47-62, ctde.rs:26-44) */
 static int net_layers(const or_net_desc *d, layer_t *L, int *n_actor_total) {
     int n = 0; size_t off = 0; int in = d->obs_dim;
+    if (d->cnn) {
+        /* conv layers first (Burn record order: weight [Cout][Cin][k][k], bias),
+         * as layers with in = Cin k k, out = Cout; the FC stack then reads the
+         * flattened conv output + the extra features */
+        int cin = d->C;
+        for (int i = 0; i < d->n_conv; i++) {
+            L[n].in = cin * d->ksize * d->ksize; L[n].out = d->conv_ch[i]; L[n].w = off;
+            off += (size_t)L[n].in * L[n].out; L[n].b = off; off += L[n].out; cin = d->conv_ch[i]; n++;
+        }
+        in = d->H * d->W * cin + (d->obs_dim - d->H * d->W * d->C);
+    }
     for (int i = 0; i < d->n_actor; i++) {
         L[n].in = in; L[n].out = d->actor_width; L[n].w = off; off += (size_t)in * L[n].out;
         L[n].b = off; off += L[n].out; in = d->actor_width; n++;
@@ -97,13 +108,73 @@ typedef struct {
     float *buf[32];
 } acts_t;
 
+/* ------------------------------------------------------------------ CNN --
+ * cnn.rs:241-330 with Burn Conv2d as im2col + the same Linear chain order:
+ * A[b*HW + hw][(ci*k + kh)*k + kw] (zero padded), Y = relu(A Wt + bias), Wt[k][co]
+ * = weight[co][k]; the input of layer 0 is obs[:, :HWC] read channels-last
+ * ([B, H, W, C] then permuted, cnn.rs:252-262) although the observation is
+ * plane-major; activations NHWC rows; flatten NCHW (c*HW + hw) + extra features. */
+static void im2col(const or_net_desc *d, int layer, const float *src, int ld, size_t B, int cin, float *A) {
+    const int ks = d->ksize, pad = ks / 2, HW = d->H * d->W, K = cin * ks * ks;
+    for (size_t b = 0; b < B; b++)
+        for (int hw = 0; hw < HW; hw++)
+            for (int k = 0; k < K; k++) {
+                const int ci = k / (ks * ks), kh = (k % (ks * ks)) / ks, kw = k % ks;
+                const int h = hw / d->W + kh - pad, w = hw % d->W + kw - pad;
+                float v = 0.0f;
+                if (h >= 0 && h < d->H && w >= 0 && w < d->W) {
+                    const int hw2 = h * d->W + w;
+                    v = layer == 0 ? src[b * ld + (size_t)hw2 * cin + ci] : src[(b * HW + hw2) * cin + ci];
+                }
+                A[(b * HW + hw) * K + k] = v;
+            }
+}
+
+static float *conv_wt(const float *w, int cout, int K) {   /* [Cout][K] -> [K][Cout] */
+    float *t = malloc(sizeof(float) * (size_t)cout * K);
+    for (int co = 0; co < cout; co++)
+        for (int k = 0; k < K; k++) t[(size_t)k * cout + co] = w[(size_t)co * K + k];
+    return t;
+}
+
+/* conv stack + flatten: A->buf[16 + l] = conv outputs, A->buf[30] = features F */
+static void cnn_trunk(const or_net_desc *d, const layer_t *L, const float *p, const float *obs, size_t B, acts_t *A) {
+    const int HW = d->H * d->W;
+    const float *src = obs;
+    int cin = d->C;
+    for (int l = 0; l < d->n_conv; l++) {
+        const int K = L[l].in, co = L[l].out;
+        float *a = malloc(sizeof(float) * B * HW * K);
+        im2col(d, l, src, d->obs_dim, B, cin, a);
+        float *wt = conv_wt(p + L[l].w, co, K);
+        float *y = malloc(sizeof(float) * B * HW * co);
+        or_linear(a, wt, p + L[l].b, B * HW, K, co, 1, y);
+        free(a); free(wt);
+        A->buf[16 + l] = y;
+        src = y; cin = co;
+    }
+    const int E = d->obs_dim - HW * d->C, fd = HW * cin + E;
+    float *F = malloc(sizeof(float) * B * fd);
+    for (size_t b = 0; b < B; b++) {
+        for (int c = 0; c < cin; c++)
+            for (int hw = 0; hw < HW; hw++) F[b * fd + (size_t)c * HW + hw] = src[(b * HW + hw) * cin + c];
+        for (int j = 0; j < E; j++) F[b * fd + (size_t)HW * cin + j] = obs[b * d->obs_dim + (size_t)HW * d->C + j];
+    }
+    A->buf[30] = F;
+}
+
 static void forward_cached(const or_net_desc *d, const float *p, const float *obs,
                            const float *priv, size_t B, float *logits, float *values,
                            acts_t *A) {
     layer_t L[32]; int na;
     int n = net_layers(d, L, &na);
     const float *x = obs;
-    for (int i = 0; i < na - 1; i++) {
+    const int l0 = d->cnn ? d->n_conv : 0;
+    if (d->cnn) {
+        cnn_trunk(d, L, p, obs, B, A);
+        x = A->buf[30];
+    }
+    for (int i = l0; i < na - 1; i++) {
         float *y = malloc(sizeof(float) * B * L[i].out);
         or_linear(x, p + L[i].w, p + L[i].b, B, L[i].in, L[i].out, d->relu, y);
         if (A) A->buf[i] = y;
@@ -195,6 +266,55 @@ static void linear_bwd(const float *x, const float *y, const float *dy, const fl
         free(WT);
     }
     free(dz);
+}
+
+/* conv stack backward from dF = dL/d[features]: relu' of the last conv output,
+ * un-flatten, then per layer dWt = A^T dY (f64), db = sum dY, dA = dY Wt^T and the
+ * col2im gather (taps in (kh, kw) order, f32 adds) times relu' of the input */
+static void cnn_bwd(const or_net_desc *d, const layer_t *L, const float *p, const float *obs, size_t B,
+                    const acts_t *A, const float *dF, double *g) {
+    const int HW = d->H * d->W, last = d->n_conv - 1, ks = d->ksize, pad = ks / 2;
+    const int cl = L[last].out, E = d->obs_dim - HW * d->C, fd = HW * cl + E;
+    float *dy = malloc(sizeof(float) * B * HW * cl);
+    const float *yl = A->buf[16 + last];
+    for (size_t b = 0; b < B; b++)
+        for (int hw = 0; hw < HW; hw++)
+            for (int c = 0; c < cl; c++) {
+                const size_t r = (b * HW + hw) * cl + c;
+                dy[r] = yl[r] > 0.0f ? dF[b * fd + (size_t)c * HW + hw] : 0.0f;
+            }
+    for (int l = last; l >= 0; l--) {
+        const int K = L[l].in, co = L[l].out, cin = l ? L[l - 1].out : d->C;
+        float *a = malloc(sizeof(float) * B * HW * K);
+        im2col(d, l, l ? A->buf[16 + l - 1] : obs, d->obs_dim, B, cin, a);
+        float *wt = conv_wt(p + L[l].w, co, K);
+        double *gwt = calloc((size_t)K * co, sizeof(double));
+        float *da = l ? malloc(sizeof(float) * B * HW * K) : NULL;
+        linear_bwd(a, NULL, dy, wt, B * HW, K, co, -1, gwt, g + L[l].b, da);
+        for (int c = 0; c < co; c++)
+            for (int k = 0; k < K; k++) g[L[l].w + (size_t)c * K + k] += gwt[(size_t)k * co + c];
+        free(a); free(wt); free(gwt); free(dy);
+        dy = NULL;
+        if (!l) break;
+        const float *yp = A->buf[16 + l - 1];
+        dy = malloc(sizeof(float) * B * HW * cin);
+        for (size_t b = 0; b < B; b++)
+            for (int hw = 0; hw < HW; hw++)
+                for (int ci = 0; ci < cin; ci++) {
+                    const int h = hw / d->W, w = hw % d->W;
+                    float s = 0.0f;
+                    for (int kh = 0; kh < ks; kh++)
+                        for (int kw = 0; kw < ks; kw++) {
+                            const int ho = h - kh + pad, wo = w - kw + pad;
+                            if (ho < 0 || ho >= d->H || wo < 0 || wo >= d->W) continue;
+                            s += da[(b * HW + ho * d->W + wo) * K + (ci * ks + kh) * ks + kw];
+                        }
+                    const size_t r = (b * HW + hw) * cin + ci;
+                    dy[r] = yp[r] > 0.0f ? s : 0.0f;
+                }
+        free(da);
+    }
+    free(dy);
 }
 
 /* ---------------------------------------------------------------- policy -- */
@@ -400,14 +520,16 @@ void or_minibatch_loss_grad(const or_net_desc *d, const float *p, size_t mb, con
                 if (dh) for (size_t q = 0; q < mb * (size_t)L[vi].in; q++) dh[q] += dx2[q];
                 free(dx2);
             }
-            for (int l = li - 1; l >= 0; l--) {
-                const float *xl = l > 0 ? acts.buf[l - 1] : obs;
-                float *dxl = l > 0 ? malloc(sizeof(float) * mb * L[l].in) : NULL;
+            const int l0 = d->cnn ? d->n_conv : 0;     /* first FC layer */
+            for (int l = li - 1; l >= l0; l--) {
+                const float *xl = l > l0 ? acts.buf[l - 1] : (d->cnn ? acts.buf[30] : obs);
+                float *dxl = (l > l0 || d->cnn) ? malloc(sizeof(float) * mb * L[l].in) : NULL;
                 linear_bwd(xl, acts.buf[l], dh, p + L[l].w, mb, L[l].in, L[l].out, d->relu,
                            g + L[l].w, g + L[l].b, dxl);
                 free(dh);
                 dh = dxl;
             }
+            if (d->cnn) cnn_bwd(d, L, p, obs, mb, &acts, dh, g);   /* dh = dL/dF */
             free(dh);
         }
         if (d->ctde) {

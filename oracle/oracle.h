@@ -185,6 +185,10 @@ typedef struct {
     int n_critic;             /* CTDE critic hidden layers (0 for MLP) */
     int critic_width;
     size_t n_params;
+    /* CNN (network/cnn.rs; Connect Four OBSERVATION_SHAPE (H, W, C) = (6, 7, 2)):
+     * n_conv conv layers of conv_ch[l] channels, odd kernel ksize, stride 1, same
+     * padding, relu; then n_actor FC layers of actor_width, then the heads */
+    int cnn, n_conv, conv_ch[4], ksize, H, W, C;
 } or_net_desc;
 size_t or_net_num_params(const or_net_desc *d);
 /* forward for B rows; logits [B*A], values [B] */
@@ -272,6 +276,7 @@ typedef struct {
     or_ppo_cfg ppo;
     uint64_t seed;
     int threads;             /* env-step threads (rayon equivalent); 0 = all */
+    int cnn, num_conv, conv_ch[4], ksize;   /* network_type = "cnn" (Connect Four) */
 } or_train_cfg;
 or_trainer *or_trainer_new(const or_train_cfg *c, const float *init_params);
 void or_trainer_free(or_trainer *t);

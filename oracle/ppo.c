@@ -129,6 +129,11 @@ or_trainer *or_trainer_new(const or_train_cfg *c, const float *init_params) {
     t->net.relu = c->relu; t->net.n_actor = c->num_hidden; t->net.actor_width = c->hidden;
     t->net.n_critic = c->ctde ? c->critic_num_hidden : 0;
     t->net.critic_width = c->ctde ? c->critic_hidden : 0;
+    if (c->cnn) {   /* cnn.rs:66-150 */
+        t->net.cnn = 1; t->net.n_conv = c->num_conv; t->net.ksize = c->ksize;
+        for (int l = 0; l < 4; l++) t->net.conv_ch[l] = c->conv_ch[l];
+        t->net.H = 6; t->net.W = 7; t->net.C = 2;
+    }
     t->net.n_params = or_net_num_params(&t->net);
     t->params = malloc(sizeof(float) * t->net.n_params);
     memcpy(t->params, init_params, sizeof(float) * t->net.n_params);

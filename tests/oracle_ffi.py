@@ -73,7 +73,9 @@ class Episode(C.Structure):
 class NetDesc(C.Structure):
     _fields_ = [("ctde", C.c_int), ("obs_dim", C.c_int), ("priv_dim", C.c_int), ("act_dim", C.c_int),
                 ("relu", C.c_int), ("n_actor", C.c_int), ("actor_width", C.c_int),
-                ("n_critic", C.c_int), ("critic_width", C.c_int), ("n_params", C.c_size_t)]
+                ("n_critic", C.c_int), ("critic_width", C.c_int), ("n_params", C.c_size_t),
+                ("cnn", C.c_int), ("n_conv", C.c_int), ("conv_ch", C.c_int * 4), ("ksize", C.c_int),
+                ("H", C.c_int), ("W", C.c_int), ("C", C.c_int)]
 
 
 class PpoCfg(C.Structure):
@@ -90,7 +92,8 @@ class TrainCfg(C.Structure):
                 ("normalize_obs", C.c_int), ("normalize_returns", C.c_int),
                 ("return_clip", C.c_float), ("gamma", C.c_double), ("gae_lambda", C.c_double),
                 ("lr", C.c_double), ("ent_coef", C.c_double), ("reward_shaping", C.c_double),
-                ("ppo", PpoCfg), ("seed", C.c_uint64), ("threads", C.c_int)]
+                ("ppo", PpoCfg), ("seed", C.c_uint64), ("threads", C.c_int),
+                ("cnn", C.c_int), ("num_conv", C.c_int), ("conv_ch", C.c_int * 4), ("ksize", C.c_int)]
 
 
 class UpdateMetrics(C.Structure):
@@ -263,6 +266,16 @@ def mlp_desc(obs_dim, act_dim, hidden, num_hidden, relu=True):
     return d
 
 
+def cnn_desc(act_dim, conv_ch, ksize, fc_hidden, n_fc, relu=True):
+    """Connect Four CNN (obs 86, shape (6, 7, 2))"""
+    d = NetDesc(ctde=0, obs_dim=86, priv_dim=0, act_dim=act_dim, relu=int(relu), n_actor=n_fc,
+                actor_width=fc_hidden, n_critic=0, critic_width=0, cnn=1, n_conv=len(conv_ch),
+                conv_ch=(C.c_int * 4)(*[conv_ch[min(i, len(conv_ch) - 1)] for i in range(4)]), ksize=ksize,
+                H=6, W=7, C=2)
+    d.n_params = lib().or_net_num_params(C.byref(d))
+    return d
+
+
 def ctde_desc(obs_dim, priv_dim, act_dim, hidden, num_hidden, critic_hidden, critic_num_hidden,
               relu=True):
     d = NetDesc(ctde=1, obs_dim=obs_dim, priv_dim=priv_dim, act_dim=act_dim, relu=int(relu),
@@ -326,8 +339,15 @@ def ppo_cfg(num_epochs=4, num_minibatches=4, clip=0.2, value_coef=0.5, max_grad_
 def train_cfg(env_kind=ENV_CARTPOLE, num_envs=8, num_steps=128, hidden=64, num_hidden=2, relu=True,
               ctde=False, critic_hidden=0, critic_num_hidden=0, normalize_obs=True,
               normalize_returns=True, return_clip=10.0, gamma=0.99, gae_lambda=0.95, lr=1e-3,
-              ent_coef=0.01, reward_shaping=0.0, seed=42, threads=0, **ppo):
-    return TrainCfg(env_kind=env_kind, num_envs=num_envs, num_steps=num_steps, hidden=hidden,
+              ent_coef=0.01, reward_shaping=0.0, seed=42, threads=0, cnn=None, **ppo):
+    """cnn: None, or (conv_channels per layer, kernel_size); hidden / num_hidden are
+    then cnn_fc_hidden_size / cnn_num_fc_layers"""
+    extra = {}
+    if cnn is not None:
+        ch, ks = cnn
+        extra = dict(cnn=1, num_conv=len(ch), conv_ch=(C.c_int * 4)(*[ch[min(i, len(ch) - 1)] for i in range(4)]),
+                     ksize=ks)
+    return TrainCfg(**extra, env_kind=env_kind, num_envs=num_envs, num_steps=num_steps, hidden=hidden,
                     num_hidden=num_hidden, relu=int(relu), ctde=int(ctde), critic_hidden=critic_hidden,
                     critic_num_hidden=critic_num_hidden, normalize_obs=int(normalize_obs),
                     normalize_returns=int(normalize_returns), return_clip=return_clip, gamma=gamma,

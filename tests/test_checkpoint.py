@@ -58,6 +58,7 @@ def test_metadata_required_fields_and_defaults():
 
 
 @pytest.mark.parametrize("preset,over", [("cartpole", {}), ("connect_four", {}), ("liars_dice_ctde", {}),
+                                         ("connect_four", {"network_type": "cnn"}),
                                          ("liars_dice_ctde", {"network_type": "mlp", "hidden_size": 128})])
 def test_model_record_round_trip(tmp_path, preset, over):
     cfg = bppo.make_config(preset, **over)
@@ -69,7 +70,7 @@ def test_model_record_round_trip(tmp_path, preset, over):
     rec = K.model_record(cfg, p)
     assert set(rec) == {"metadata", "item"} and rec["metadata"]["float"] == "f32"
     (kind, body), = rec["item"].items()
-    assert kind == ("Ctde" if cfg["network_type"] == "ctde" else "Mlp")
+    assert kind == {"ctde": "Ctde", "cnn": "Cnn", "mlp": "Mlp"}[cfg["network_type"]]
     lin = body["policy_head"]
     assert set(lin) == {"weight", "bias"} and lin["weight"]["param"]["dtype"] == "F32"
 

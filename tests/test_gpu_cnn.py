@@ -1,0 +1,98 @@
+"""CNN actor-critic (network/cnn.rs) on the device: implicit-GEMM
+convolutions on the f32 MFMA engine (cnn.hip) against the oracle's im2col
+restatement (oracle/net.c cnn_trunk / cnn_bwd, itself checked against torch
+autograd in tests/test_oracle_backward.py).  Bit-exact: forward logits/values,
+the whole rollout (actions, log-probs, values), GAE; the update within
+tests/parity_util.py's tolerances; the next rollout from the oracle's params
+bit-exact again."""
+import numpy as np
+import pytest
+
+import bppo
+import oracle_ffi as O
+from parity_util import assert_metrics_close, assert_params_close, bits
+
+pytestmark = pytest.mark.gpu
+
+NETS = [dict(num_conv_layers=2, conv_channels=[8, 8], kernel_size=3, cnn_fc_hidden_size=32, cnn_num_fc_layers=1),
+        dict(num_conv_layers=1, conv_channels=[8], kernel_size=3, cnn_fc_hidden_size=16, cnn_num_fc_layers=1),
+        dict(num_conv_layers=2, conv_channels=[64, 64], kernel_size=3, cnn_fc_hidden_size=128, cnn_num_fc_layers=2),
+        dict(num_conv_layers=2, conv_channels=[16], kernel_size=5, cnn_fc_hidden_size=32, cnn_num_fc_layers=1,
+             activation="tanh")]
+
+
+def _cfg(N, T, net, **kw):
+    return bppo.make_config("connect_four", num_envs=N, num_steps=T, network_type="cnn", **net, **kw)
+
+
+def _pair(N, T, net, **kw):
+    cfg = _cfg(N, T, net, **kw)
+    params = bppo.orthogonal_init(cfg, seed=7)
+    tr = bppo.Trainer(cfg, params=params)
+    ch = [net["conv_channels"][min(i, len(net["conv_channels"]) - 1)] for i in range(net["num_conv_layers"])]
+    ocfg = O.train_cfg(env_kind=O.ENV_CONNECT_FOUR, num_envs=N, num_steps=T, seed=cfg["seed"],
+                       hidden=net["cnn_fc_hidden_size"], num_hidden=net["cnn_num_fc_layers"],
+                       relu=cfg["activation"] == "relu", normalize_obs=False, normalize_returns=False,
+                       gamma=cfg["gamma"], gae_lambda=cfg["gae_lambda"],
+                       lr=bppo.schedule_get(cfg["learning_rate"], 0), ent_coef=bppo.schedule_get(cfg["entropy_coef"], 0),
+                       num_epochs=cfg["num_epochs"], num_minibatches=cfg["num_minibatches"], clip=cfg["clip_epsilon"],
+                       value_coef=cfg["value_coef"], target_kl=cfg["target_kl"], cnn=(ch, net["kernel_size"]))
+    ot = O.Trainer(ocfg, params)
+    return cfg, tr, ot
+
+
+def _cmp(tr, ot):
+    b = tr.buffer
+    assert np.array_equal(b.acting_players.reshape(-1), ot.buffer("players", np.int32))
+    assert np.array_equal(bits(b.observations.reshape(-1)), bits(ot.buffer("obs")))
+    assert np.array_equal(b.actions.reshape(-1), ot.buffer("actions", np.int32))
+    assert np.array_equal(bits(b.values.reshape(-1)), bits(ot.buffer("values")))
+    assert np.array_equal(bits(b.log_probs.reshape(-1)), bits(ot.buffer("log_probs")))
+    assert np.array_equal(bits(b.all_rewards.reshape(-1)), bits(ot.buffer("all_rewards")))
+    assert tr.ctx.rng_pos() == ot.rng_pos()
+
+
+@pytest.mark.parametrize("net", NETS)
+def test_cnn_forward_bit_exact(net):
+    cfg = _cfg(16, 2, net)
+    params = bppo.orthogonal_init(cfg, seed=3)
+    tr = bppo.Trainer(cfg, params=params)
+    rng = np.random.default_rng(0)
+    obs = (rng.random((300, 86)) < 0.3).astype(np.float32)
+    obs[:, 84:] = 0.0
+    obs[np.arange(300), 84 + rng.integers(0, 2, 300)] = 1.0
+    lg, v = tr.model.forward(obs)
+    ch = [net["conv_channels"][min(i, len(net["conv_channels"]) - 1)] for i in range(net["num_conv_layers"])]
+    d = O.cnn_desc(7, ch, net["kernel_size"], net["cnn_fc_hidden_size"], net["cnn_num_fc_layers"],
+                   relu=cfg["activation"] == "relu")
+    lo, vo = O.net_forward(d, params, obs)
+    assert np.array_equal(bits(lg), bits(lo))
+    assert np.array_equal(bits(v.reshape(-1)), bits(vo))
+    tr.close()
+
+
+@pytest.mark.parametrize("net,N,T", [(NETS[0], 64, 16), (NETS[1], 64, 12), (NETS[2], 1024, 8), (NETS[3], 48, 10)])
+def test_cnn_rollout_update_second_rollout(net, N, T):
+    cfg, tr, ot = _pair(N, T, net)
+    bppo.collect_rollouts(tr.ctx); ot.collect()
+    _cmp(tr, ot)
+    bppo.compute_gae(tr.ctx); ot.gae()
+    assert np.array_equal(bits(tr.buffer.advantages.reshape(-1)), bits(ot.buffer("advantages")))
+    m = bppo.ppo_update(tr.ctx, bppo.schedule_get(cfg["learning_rate"], 0), bppo.schedule_get(cfg["entropy_coef"], 0))
+    om = ot.update()
+    assert tr.ctx.rng_pos() == ot.rng_pos()
+    assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"))
+    assert_params_close(tr.model.get_params(), ot.params())
+    tr.model.set_params(ot.params())
+    bppo.collect_rollouts(tr.ctx); ot.collect()
+    _cmp(tr, ot)
+    tr.close(); ot.close()
+
+
+def test_cnn_requires_observation_shape():
+    """cnn.rs:430-438 (#[should_panic] "CNN requires OBSERVATION_SHAPE")"""
+    import bppo._lib as L
+    cfg = bppo.make_config("liars_dice_ctde", num_envs=8, network_type="cnn")
+    cfg["network_type"] = "cnn"
+    with pytest.raises((L.BppoError, ValueError)):
+        bppo.Trainer(cfg)

@@ -13,6 +13,11 @@ import oracle_ffi as O
 def layer_shapes(desc):
     shapes = []
     i = desc.obs_dim
+    if desc.cnn:
+        cin = desc.C
+        for l in range(desc.n_conv):
+            shapes.append((cin * desc.ksize ** 2, desc.conv_ch[l])); cin = desc.conv_ch[l]
+        i = desc.H * desc.W * cin + desc.obs_dim - desc.H * desc.W * desc.C
     for _ in range(desc.n_actor):
         shapes.append((i, desc.actor_width)); i = desc.actor_width
     shapes.append((i, desc.act_dim))
@@ -38,6 +43,20 @@ def torch_loss(desc, params, obs, priv, actions, old_logp, adv_n, returns, old_v
     act = torch.relu if desc.relu else torch.tanh
     x = torch.tensor(obs, dtype=torch.float64)
     h = x
+    if desc.cnn:
+        # cnn.rs:241-330: obs[:, :HWC] reshaped [B, H, W, C] and permuted to NCHW,
+        # conv (weight [Cout][Cin][k][k], same padding) + relu, flatten NCHW, cat extra
+        Hh, Ww, Cc = desc.H, desc.W, desc.C
+        sp = x[:, :Hh * Ww * Cc].reshape(-1, Hh, Ww, Cc).permute(0, 3, 1, 2)
+        cin = Cc
+        for l in range(desc.n_conv):
+            W, b = Ws[l]
+            co = desc.conv_ch[l]
+            sp = torch.relu(torch.nn.functional.conv2d(sp, W.reshape(co, cin, desc.ksize, desc.ksize), b,
+                                                       padding=desc.ksize // 2))
+            cin = co
+        h = torch.cat([sp.reshape(sp.shape[0], -1), x[:, Hh * Ww * Cc:]], 1)
+        Ws = Ws[desc.n_conv:]
     for W, b in Ws[:desc.n_actor]:
         h = act(h @ W + b)
     logits = h @ Ws[desc.n_actor][0] + Ws[desc.n_actor][1]
@@ -116,3 +135,12 @@ def test_clip_value_branch():
 
 def test_tanh_activation():
     run_case(O.mlp_desc(5, 2, 16, 2, relu=False), mb=100, seed=4)
+
+
+def test_cnn_connect_four_shape():
+    """network/cnn.rs: 2 conv layers (8, 16 channels), 3x3 same, 1 FC layer of 24"""
+    run_case(O.cnn_desc(7, [8, 16], 3, 24, 1), mb=33, masks=True, seed=5)
+
+
+def test_cnn_one_conv_tanh_fc_kernel5():
+    run_case(O.cnn_desc(7, [6], 5, 16, 2, relu=False), mb=20, masks=True, seed=6)
