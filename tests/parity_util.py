@@ -80,7 +80,7 @@ def ev_f32_sequential(values, returns):
     return np.float32(np.float32(1) - np.float32(vres / vr))
 
 
-def assert_metrics_close(m, om, values=None, returns=None, skip=()):
+def assert_metrics_close(m, om, values=None, returns=None, skip=(), rtol=RTOL):
     """All 19 UpdateMetrics fields plus num_updates / epochs_run.  values /
     returns: the buffers the explained variance is taken over (learner rows
     only under an opponent pool)."""
@@ -99,7 +99,7 @@ def assert_metrics_close(m, om, values=None, returns=None, skip=()):
             continue
         if np.isnan(o) and np.isnan(d):
             continue
-        tol = RTOL * max(abs(o), _floor(k, om))
+        tol = rtol * max(abs(o), _floor(k, om))
         if not abs(d - o) <= tol:
             bad.append((k, d, o, abs(d - o) / max(abs(o), 1e-30)))
     assert not bad, bad
