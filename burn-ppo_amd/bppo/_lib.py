@@ -35,7 +35,8 @@ class Config(C.Structure):
                 ("reward_shaping_coef", C.c_double), ("seed", C.c_uint64), ("env_seed_base", C.c_uint64),
                 ("rng_stream", C.c_uint64),
                 ("cnn", C.c_int32), ("num_conv_layers", C.c_int32), ("conv_channels", C.c_int32 * 4),
-                ("kernel_size", C.c_int32), ("cnn_fc_hidden_size", C.c_int32), ("cnn_num_fc_layers", C.c_int32)]
+                ("kernel_size", C.c_int32), ("cnn_fc_hidden_size", C.c_int32), ("cnn_num_fc_layers", C.c_int32),
+                ("normalize_values", C.c_int32)]
 
 
 class Episode(C.Structure):
@@ -54,9 +55,14 @@ METRIC_NAMES = ("policy_loss", "value_loss", "entropy", "entropy_scaled", "appro
                 "value_error_max", "avg_valid_actions", "entropy_valid_pct")
 
 
+# PopArt metrics (ppo.rs:2061-2068; NaN when the reference's Option is None)
+POPART_METRICS = ("value_norm_target_mean", "value_norm_target_std", "value_norm_rescale_mag")
+
+
 class UpdateMetrics(C.Structure):
     _fields_ = [(n, C.c_float) for n in METRIC_NAMES] + [("num_updates", C.c_int32),
-                                                          ("epochs_run", C.c_int32)]
+                                                          ("epochs_run", C.c_int32)] + \
+        [(n, C.c_float) for n in POPART_METRICS]
 
 
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_size_t, C.c_void_p)
@@ -72,7 +78,7 @@ EXPORTS = (
     "bppo_gae_mp_device", "bppo_last_kernel_ms", "bppo_debug_libm", "bppo_debug_shuffle_chain",
     "bppo_debug_fisher_yates", "bppo_debug_gemm", "bppo_debug_shuffle_engine", "bppo_debug_sample",
     "bppo_rng_fill_bytes", "bppo_rng_from_seed", "bppo_rng_key_get", "bppo_num_param_tensors",
-    "bppo_optimizer_get", "bppo_optimizer_set",
+    "bppo_optimizer_get", "bppo_optimizer_set", "bppo_popart_get", "bppo_popart_set",
 )
 
 _lib = None
@@ -143,6 +149,8 @@ def lib():
         "bppo_num_param_tensors": (sz, [vp]),
         "bppo_optimizer_get": (i32, [vp, vp, vp, vp, sz]),
         "bppo_optimizer_set": (i32, [vp, vp, vp, vp, sz]),
+        "bppo_popart_get": (i32, [vp, vp]),
+        "bppo_popart_set": (i32, [vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -10,6 +10,7 @@
   save/load_optimizer               checkpoint.rs:291-335
   save/load_normalizer              checkpoint.rs:340-375 (ObsNormalizer JSON)
   save/load_return_normalizer       checkpoint.rs:430-465
+  save/load_popart_normalizer       checkpoint.rs:468-490
   save_rng_state / load_rng_state   checkpoint.rs:380-426: 32 bytes drawn from the
                                     main RNG (advances it by 8 words, as the reference
                                     does at every periodic checkpoint, main.rs:1307);
@@ -385,6 +386,23 @@ def load_return_normalizer(ctx, path_dir):
     return True
 
 
+def save_popart_normalizer(ctx, path_dir):
+    """checkpoint.rs:468-476: PopArtNormalizer serde {mean, var (M2), count, epsilon}"""
+    st = ctx.popart()
+    d = {"mean": float(st[0]), "var": float(st[1]), "count": float(st[2]), "epsilon": float(st[3])}
+    with open(os.path.join(path_dir, "popart_normalizer.json"), "w") as f:
+        f.write(to_json_pretty(d))
+
+
+def load_popart_normalizer(ctx, path_dir):
+    p = os.path.join(path_dir, "popart_normalizer.json")
+    if not os.path.exists(p):
+        return False
+    d = json.load(open(p))
+    ctx.set_popart([d["mean"], d["var"], d["count"], d["epsilon"]])
+    return True
+
+
 # -------------------------------------------------------------------- RNG ---
 def save_rng_state(ctx, path_dir):
     """checkpoint.rs:390-400: 32 bytes from the main RNG (8 words) -> rng_state.bin"""
@@ -466,6 +484,8 @@ def save_training_checkpoint(manager, ctx, params, metadata, update_best=True):
     nr = ctx.cfg["normalize_returns"]
     if (ctx.num_players == 1) if nr is None else nr:
         save_return_normalizer(ctx, path)
+    if ctx.cfg.get("normalize_values"):
+        save_popart_normalizer(ctx, path)
     save_rng_state(ctx, path)
     return path
 
@@ -478,5 +498,6 @@ def resume_training_checkpoint(ctx, ckpt_dir):
     load_optimizer(ctx, ckpt_dir)
     load_normalizer(ctx, ckpt_dir)
     load_return_normalizer(ctx, ckpt_dir)
+    load_popart_normalizer(ctx, ckpt_dir)
     load_rng_state(ctx, ckpt_dir)
     return meta

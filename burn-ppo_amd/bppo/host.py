@@ -92,6 +92,7 @@ def to_struct(c, rank=0, world=1, envs_per_rank=None):
         setattr(s, k, float(c[k]))
     s.target_kl = -1.0 if c["target_kl"] is None else float(c["target_kl"])
     s.seed = c["seed"]
+    s.normalize_values = int(bool(c.get("normalize_values", False)))
     s.cnn = int(c["network_type"] == "cnn")
     if s.cnn:
         s.num_conv_layers = c["num_conv_layers"]

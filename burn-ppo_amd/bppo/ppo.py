@@ -107,6 +107,16 @@ class Context:
             raise ValueError(f"returns must hold num_envs * num_players = {self.N * self.num_players} values")
         self._chk(L.lib().bppo_ret_norm_set(self.h, mvc.ctypes.data, r.ctypes.data))
 
+    def popart(self):
+        """PopArtNormalizer state [mean, M2, count, epsilon] (normalization.rs:275-284)"""
+        st = np.zeros(4)
+        self._chk(L.lib().bppo_popart_get(self.h, st.ctypes.data))
+        return st
+
+    def set_popart(self, st):
+        st = np.ascontiguousarray(st, np.float64)
+        self._chk(L.lib().bppo_popart_set(self.h, st.ctypes.data))
+
     def set_opponents(self, params, norms, num_opponent_envs, learner_pos, pos_to_opp, current_opp):
         """Opponent-pool rollouts (ppo.rs:537-1063): params [K, n_params] of the
         loaded opponents, norms[k] = (mean, m2, count) or None, seat state of envs
@@ -314,7 +324,7 @@ def ppo_update(ctx, learning_rate, entropy_coef):
     """ppo.rs:1661-2112 -> UpdateMetrics dict."""
     m = L.UpdateMetrics()
     ctx._chk(L.lib().bppo_ppo_update(ctx.h, float(learning_rate), float(entropy_coef), C.byref(m)))
-    d = {k: getattr(m, k) for k in L.METRIC_NAMES}
+    d = {k: getattr(m, k) for k in L.METRIC_NAMES + L.POPART_METRICS}
     d["num_updates"] = m.num_updates
     d["epochs_run"] = m.epochs_run
     return d

@@ -217,6 +217,8 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     c->rng_pos = 0;
     TRY(c->shuf.init(dev, c->rng_key, cfg->rng_stream, (uint32_t)TN, cfg->num_epochs, TN * (uint64_t)c->A, c->err));
     c->on_mean.assign(c->D, 0.0); c->on_m2.assign(c->D, 0.0); c->on_count = 0;
+    c->u_ret = c->d_ret; c->u_val = c->d_val;
+    if (cfg->normalize_values) TRY(popart_alloc(c));
     if (c->wide) {
         TRY(wide_init(c));
         TRY(wide_reset(c));
@@ -242,6 +244,7 @@ extern "C" void bppo_destroy(bppo_ctx *c) {
     c->shuf.shutdown();
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     wide_free(c);
+    popart_free(c);
     void *ptrs[] = {c->d_params, c->d_m1, c->d_m2, c->d_grad, c->d_slab, c->d_slab_part, c->d_cp, c->d_steps,
                     c->d_env_pos, c->d_ep_ret, c->d_ep_len, c->d_obs, c->d_rew, c->d_rew_raw,
                     c->d_done, c->d_val, c->d_logp, c->d_adv, c->d_ret, c->d_act, c->d_X, c->d_on,
@@ -494,6 +497,18 @@ extern "C" bppo_status bppo_ret_norm_set(bppo_ctx *c, const double *mvc, const d
     return BPPO_OK;
 }
 
+extern "C" bppo_status bppo_popart_get(bppo_ctx *c, double *st) {
+    if (!c || !st) return BPPO_ERR_ARG;
+    st[0] = c->pa_mean; st[1] = c->pa_m2; st[2] = c->pa_count; st[3] = c->pa_eps;
+    return BPPO_OK;
+}
+
+extern "C" bppo_status bppo_popart_set(bppo_ctx *c, const double *st) {
+    if (!c || !st) return BPPO_ERR_ARG;
+    c->pa_mean = st[0]; c->pa_m2 = st[1]; c->pa_count = st[2]; c->pa_eps = st[3];
+    return BPPO_OK;
+}
+
 static void tm_begin(bppo_ctx *c, int slot) { (void)hipEventRecord(c->ev[slot][0], c->stream); }
 static void tm_end(bppo_ctx *c, int slot) { (void)hipEventRecord(c->ev[slot][1], c->stream); }
 static void tm_read(bppo_ctx *c, int slot) {
@@ -510,7 +525,10 @@ extern "C" bppo_status bppo_collect_rollouts(bppo_ctx *c, bppo_rollout_info *inf
     const uint64_t base = c->rng_pos;
     tm_begin(c, TM_ROLLOUT);
     if (c->wide) TRY(wide_collect(c, base));
-    else TRY(launch_cartpole_rollout(c, base, nullptr, nullptr, c->cfg.normalize_obs));
+    else {
+        TRY(launch_cartpole_rollout(c, base, nullptr, nullptr, c->cfg.normalize_obs));
+        TRY(popart_denorm(c, c->d_val, TN));            // ppo.rs:355-359 (multi-player: in the sampler)
+    }
     tm_end(c, TM_ROLLOUT);
     if (opp_active(c)) {
         // opponent pool: seat reshuffles drew a data-dependent number of words
@@ -591,6 +609,7 @@ extern "C" bppo_status bppo_compute_gae(bppo_ctx *c) {
     }
     tm_begin(c, TM_BOOT);
     TRY(launch_bootstrap(c, nullptr, nullptr, c->cfg.normalize_obs));
+    TRY(popart_denorm(c, c->d_last_v, (size_t)c->N));   // main.rs:898-907
     tm_end(c, TM_BOOT);
     tm_begin(c, TM_GAE);
     bppo_status s = launch_gae_1p(c->d_rew, c->d_done, c->d_val, c->d_last_v, c->T, c->N,
@@ -626,6 +645,7 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
     bool stop = false;
     double wait_ms = 0.0;
     tm_begin(c, TM_UPDATE);
+    TRY(popart_update_begin(c, opp ? c->d_valid : nullptr));   // ppo.rs:1787-1808
     if (c->d_mbrow) TRY(launch_pack_rows(c));
     float fw_ms = 0, sh_ms = 0;
     // without a KL early stop or a host all-reduce nothing in the loop needs the
@@ -633,6 +653,7 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
     // are read once after the last one (no per-minibatch stream drain)
     const bool deferred = c->cfg.target_kl < 0 && !(c->allreduce && c->world > 1 && !c->allreduce_async);
     int nrow = 0;
+    size_t rows_done = 0;                 // rows of the KL-stopped epoch's minibatches that ran
     for (int ep = 0; ep < c->cfg.num_epochs && !stop; ep++) {
         epochs_run++;
         hipEvent_t s0 = c->ev[TM_SHUFFLE][0], s1 = c->ev[TM_SHUFFLE][1];
@@ -704,7 +725,7 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
             if (!deferred && c->cfg.target_kl >= 0) {
                 const float *row = &rows[rows.size() - (NM + 4)];
                 const float n = row[10] > 0 ? row[10] : 1.0f;
-                if (row[3] / n > (float)c->cfg.target_kl) { stop = true; break; }   // ppo.rs:2019-2023
+                if (row[3] / n > (float)c->cfg.target_kl) { stop = true; rows_done = start + sz; break; }   // ppo.rs:2019-2023
             }
             start += sz;
         }
@@ -737,6 +758,7 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
         c->shuf.release(slot, c->stream);
         c->shuf.ensure(c->rng_pos + (uint64_t)c->T * c->N * (uint64_t)c->A);
     }
+    TRY(popart_target_stats(c, stop ? epochs_run - 1 : epochs_run, rows_done, opp ? c->d_valid : nullptr));
     double ev4[4];
     TRY(launch_explained_variance(c, ev4, opp ? c->d_valid : nullptr));
     tm_read(c, TM_UPDATE);
@@ -780,6 +802,14 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
         m->explained_variance = (B < 2 || vr < 1e-8) ? 0.0f : (float)(1.0 - vres / vr);
         if (c->wide) { m->avg_valid_actions = tav / n; m->entropy_valid_pct = tevp / n; }
         m->num_updates = nup; m->epochs_run = epochs_run;
+        // PopArt metrics (ppo.rs:2061-2068): None -> NaN
+        m->value_norm_target_mean = m->value_norm_target_std = NAN;
+        m->value_norm_rescale_mag = c->pa_rescale_mag;
+        if (c->cfg.normalize_values && c->pa_tcount > 0) {
+            const double mean = c->pa_tsum / c->pa_tcount, var = c->pa_tsq / c->pa_tcount - mean * mean;
+            m->value_norm_target_mean = (float)mean;
+            m->value_norm_target_std = (float)std::sqrt(std::max(var, 0.0));
+        }
     }
     c->collected = 0; c->gae_done = 0;
     return BPPO_OK;

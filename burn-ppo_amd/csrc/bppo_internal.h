@@ -281,6 +281,14 @@ struct bppo_ctx {
     float *d_cnn_a = nullptr, *d_cnn_f = nullptr, *d_cnn_dy[2] = {nullptr, nullptr};
     float *d_cnn_wt = nullptr, *d_cnn_owt = nullptr, *d_cnn_dwt = nullptr;
     size_t cnn_wt_off[4] = {0, 0, 0, 0};
+    // PopArt value normalization (popart.hip, normalization.rs:262-366): running
+    // statistics on the host, normalized update buffers, the update's views
+    double pa_mean = 0.0, pa_m2 = 0.0, pa_count = 0.0, pa_eps = 1e-4;
+    float pa_rescale_mag = 0.0f;
+    double pa_tsum = 0.0, pa_tsq = 0.0, pa_tcount = 0.0;
+    float *d_ret_n = nullptr, *d_val_n = nullptr;
+    double *d_pa_part = nullptr;
+    const float *u_ret = nullptr, *u_val = nullptr;   // returns / old values the minibatches read
     float *d_bxc = nullptr;           // bootstrap / VecEnv scratch rows [N][L]
     uint8_t *d_bmask = nullptr;
     int32_t *d_bplayers = nullptr;
@@ -369,6 +377,13 @@ bppo_status wide_step_host(bppo_ctx *c, const int32_t *actions, float *obs, floa
 bppo_status wide_forward_host(bppo_ctx *c, const float *obs, const float *priv, int B, float *logits,
                               float *values);
 bppo_status wide_buffer_get(bppo_ctx *c, const char *name, void *host, size_t bytes, bool *handled);
+// PopArt (popart.hip)
+double popart_std(const bppo_ctx *c);
+bppo_status popart_alloc(bppo_ctx *c);
+void popart_free(bppo_ctx *c);
+bppo_status popart_denorm(bppo_ctx *c, float *v, size_t n);
+bppo_status popart_update_begin(bppo_ctx *c, const float *valid);
+bppo_status popart_target_stats(bppo_ctx *c, int full_epochs, size_t rows_done, const float *valid);
 // libm device check
 bppo_status launch_libm(int which, const float *d_x, float *d_y, size_t n);
 

@@ -41,6 +41,9 @@ struct SampleArgs {
     // step's draw order; the step's first word position from device memory
     const int32_t *group = nullptr, *gpos = nullptr;
     const uint64_t *dbase = nullptr;
+    // PopArt (ppo.rs:355-359): stored values denormalized, v * std + mean in f64
+    int pa_on = 0;
+    double pa_mean = 0.0, pa_std = 1.0;
 };
 
 // metric slots written after the gradient (d_grad[np + k]); the first 11 are

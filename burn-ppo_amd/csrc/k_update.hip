@@ -324,7 +324,7 @@ __global__ void __launch_bounds__(256) k_pack_rows(size_t B, const float *obs, c
 bppo_status launch_pack_rows(bppo_ctx *c) {
     const size_t B = (size_t)c->T * c->N;
     hipLaunchKernelGGL(k_pack_rows, dim3(2048), dim3(256), 0, c->stream, B, c->d_obs, c->d_act, c->d_logp, c->d_adv,
-                       c->d_ret, c->d_val, c->d_mbrow);
+                       c->u_ret, c->u_val, c->d_mbrow);
     BPPO_HIP(c, hipGetLastError());
     return BPPO_OK;
 }
@@ -898,7 +898,7 @@ bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_
                              double *) {
     const int h = c->cfg.hidden_size, nl = c->cfg.num_hidden;
     MbArgs g;
-    g.obs = c->d_obs; g.logp = c->d_logp; g.adv = c->d_adv; g.ret = c->d_ret; g.val = c->d_val;
+    g.obs = c->d_obs; g.logp = c->d_logp; g.adv = c->d_adv; g.ret = c->u_ret; g.val = c->u_val;
     g.act = c->d_act; g.perm = c->d_perm; g.start = start; g.n = n; g.params = c->d_params;
     g.mb_stats = c->d_mb_cur; g.slab = c->d_slab; g.np = (int)c->net.n_params;
     g.lo = (float)(1.0 - c->cfg.clip_epsilon); g.hi = (float)(1.0 + c->cfg.clip_epsilon);

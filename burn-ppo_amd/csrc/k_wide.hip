@@ -178,7 +178,8 @@ __global__ void k_sample_masked(SampleArgs g) {
     }
     const float lp = log_prob_row<A>(x, best);
     if (!isfinite(lp)) atomicOr(g.err, 1);       // ppo.rs:363-366
-    const float v = g.values[e];
+    float v = g.values[e];
+    if (g.pa_on) v = (float)((double)v * g.pa_std + g.pa_mean);
     g.logp[e] = lp;
     g.val[e] = v;
     const int p = g.players[e];

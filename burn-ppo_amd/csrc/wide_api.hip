@@ -216,6 +216,7 @@ bppo_status wide_collect(bppo_ctx *c, uint64_t base) {
         s.base = base + r0 * (uint64_t)A;
         s.act = c->d_act + r0; s.logp = c->d_logp + r0; s.val = c->d_val + r0; s.lvpp = c->d_lvpp; s.err = c->d_err;
         if (opp) { s.group = c->d_group; s.gpos = c->d_gpos; s.dbase = c->d_rngpos; }
+        if (c->cfg.normalize_values && c->pa_count >= 2.0) { s.pa_on = 1; s.pa_mean = c->pa_mean; s.pa_std = popart_std(c); }
         WHIP(c, wide_sample(A, c->stream, s));
         WideStepArgs w;
         w.N = N; w.t = t; w.state = c->d_wstate; w.env_pos = c->d_env_pos; w.seed_base = c->cfg.env_seed_base;
@@ -236,6 +237,7 @@ bppo_status wide_bootstrap_gae(bppo_ctx *c) {
     WHIP(c, wide_env_observe(c->cfg.env_kind, c->G > 0, c->stream, N, c->d_wstate, c->d_bxc, c->d_bmask, c->d_bplayers));
     if (c->cfg.normalize_obs) WTRY(launch_obs_norm_rows(c, N, c->d_bxc + c->G, c->L, nullptr));   // updated stats
     WTRY(wide_forward(c, N, c->d_bxc, c->L, c->d_logits, c->d_values));
+    WTRY(popart_denorm(c, c->d_values, (size_t)N));    // main.rs:898-907
     WHIP(c, wide_boot_lvpp(c->stream, N, c->P, c->d_values, c->d_bplayers, c->d_lvpp));
     WHIP(c, hipMemcpyAsync(c->d_last_v, c->d_values, sizeof(float) * N, hipMemcpyDeviceToDevice, c->stream));
     bppo_status s = launch_gae_mp(c->d_allr, c->d_players, c->d_done, c->d_val, c->d_lvpp, c->T, N, c->P,
@@ -256,7 +258,7 @@ bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, float ent_c
     WTRY(wide_forward(c, rows, c->d_xcg, L, c->d_logits, c->d_values));
     LossArgs g;
     g.perm = c->d_perm; g.start = start; g.n = mb; g.act = c->d_act; g.logp = c->d_logp; g.adv = c->d_adv;
-    g.ret = c->d_ret; g.val = c->d_val; g.mask = c->d_mask; g.logits = c->d_logits; g.values = c->d_values;
+    g.ret = c->u_ret; g.val = c->u_val; g.mask = c->d_mask; g.logits = c->d_logits; g.values = c->d_values;
     g.mb_stats = c->d_mb_cur; g.dout = c->d_dout; g.part = c->d_mpart;
     g.lo = (float)(1.0 - c->cfg.clip_epsilon); g.hi = (float)(1.0 + c->cfg.clip_epsilon);
     g.ceps = (float)c->cfg.clip_epsilon; g.inv_mb = (float)(1.0 / (double)mb); g.ent_coef = ent_coef;

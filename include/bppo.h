@@ -63,6 +63,9 @@ typedef struct {
      * conv_channels per layer (the last repeated past the list, cnn.rs:84-90),
      * cnn_num_fc_layers FC layers of cnn_fc_hidden_size, then the heads */
     int32_t cnn, num_conv_layers, conv_channels[4], kernel_size, cnn_fc_hidden_size, cnn_num_fc_layers;
+    /* normalize_values (config.rs:827-832, default false): PopArt value normalization
+     * with value-head rescaling (normalization.rs:262-366, ppo.rs:1599-1653) */
+    int32_t normalize_values;
 } bppo_config;
 
 typedef struct {
@@ -89,6 +92,8 @@ typedef struct {
     float value_error_mean, value_error_std, value_error_max;
     float avg_valid_actions, entropy_valid_pct;
     int32_t num_updates, epochs_run;
+    /* PopArt (ppo.rs:2061-2068, 1799-1804): NaN when the reference's Option is None */
+    float value_norm_target_mean, value_norm_target_std, value_norm_rescale_mag;
 } bppo_update_metrics;
 
 typedef struct bppo_ctx bppo_ctx;
@@ -146,6 +151,9 @@ bppo_status bppo_obs_norm_set(bppo_ctx *ctx, const double *mean, const double *m
 /* mvc = {mean, M2, count}; returns = per (env, player) rolling returns [N*P] */
 bppo_status bppo_ret_norm_get(bppo_ctx *ctx, double *mvc, double *returns);
 bppo_status bppo_ret_norm_set(bppo_ctx *ctx, const double *mvc, const double *returns);
+/* PopArtNormalizer state {mean, M2, count, epsilon} (normalization.rs:275-284) */
+bppo_status bppo_popart_get(bppo_ctx *ctx, double *state4);
+bppo_status bppo_popart_set(bppo_ctx *ctx, const double *state4);
 
 /* ---- the hot path ------------------------------------------------------- */
 bppo_status bppo_collect_rollouts(bppo_ctx *ctx, bppo_rollout_info *info);

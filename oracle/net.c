@@ -62,6 +62,12 @@ static int net_layers(const or_net_desc *d, layer_t *L, int *n_actor_total) {
     return n;
 }
 
+void or_net_value_head(const or_net_desc *d, size_t *w, size_t *b, int *in) {
+    layer_t L[32]; int na;
+    int n = net_layers(d, L, &na);
+    *w = L[n - 1].w; *b = L[n - 1].b; *in = L[n - 1].in;
+}
+
 size_t or_net_num_params(const or_net_desc *d) {
     layer_t L[32]; int na;
     int n = net_layers(d, L, &na);

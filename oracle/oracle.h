@@ -191,6 +191,7 @@ typedef struct {
     int cnn, n_conv, conv_ch[4], ksize, H, W, C;
 } or_net_desc;
 size_t or_net_num_params(const or_net_desc *d);
+void or_net_value_head(const or_net_desc *d, size_t *w, size_t *b, int *in);   /* value head W offset, b offset, in */
 /* forward for B rows; logits [B*A], values [B] */
 void or_net_forward(const or_net_desc *d, const float *params, const float *obs,
                     const float *priv, size_t B, float *logits, float *values);
@@ -242,7 +243,16 @@ typedef struct {
     float avg_valid_actions, entropy_valid_pct;
     int32_t num_updates;
     int32_t epochs_run;
+    float value_norm_target_mean, value_norm_target_std, value_norm_rescale_mag;   /* NaN = None */
 } or_update_metrics;
+
+/* PopArtNormalizer (normalization.rs:262-366) */
+typedef struct { double mean, var, count, epsilon; } or_popart;
+void or_popart_init(or_popart *p);
+double or_popart_std(const or_popart *p);
+void or_popart_update(or_popart *p, const float *returns, size_t n, double *old_mean, double *old_std);
+void or_popart_normalize(const or_popart *p, const float *x, size_t n, float *out);
+void or_popart_denormalize(const or_popart *p, float *v, size_t n);
 
 /* per-minibatch loss/grad: grads [n_params]; returns loss. Used by the update and by tests */
 typedef struct {
@@ -277,6 +287,7 @@ typedef struct {
     uint64_t seed;
     int threads;             /* env-step threads (rayon equivalent); 0 = all */
     int cnn, num_conv, conv_ch[4], ksize;   /* network_type = "cnn" (Connect Four) */
+    int normalize_values;    /* PopArt (config.rs:827-832) */
 } or_train_cfg;
 or_trainer *or_trainer_new(const or_train_cfg *c, const float *init_params);
 void or_trainer_free(or_trainer *t);
@@ -287,6 +298,7 @@ uint64_t or_trainer_rng_pos(const or_trainer *t);
 void or_trainer_set_rng(or_trainer *t, const uint32_t key[8], uint64_t pos);
 void or_trainer_set_adam(or_trainer *t, const float *m1, const float *m2, const int32_t *steps, int n_tensors);
 void or_trainer_get_adam(const or_trainer *t, float *m1, float *m2, int32_t *steps, int n_tensors);
+void or_trainer_popart(or_trainer *t, double *get4, const double *set4);
 void or_trainer_set_norms(or_trainer *t, const double *mean, const double *m2, double count, const double *mvc,
                           const double *returns);
 /* phases of one update, so tests can compare buffers phase by phase */

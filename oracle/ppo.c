@@ -93,6 +93,7 @@ struct or_trainer {
     or_vecenv *env;
     or_obs_norm on;
     or_ret_norm rn;
+    or_popart pa;
     or_rng rng;
     int T, N, D, A, P, G;
     float *obs, *priv, *rewards, *dones, *values, *logp, *all_r, *masks, *adv, *ret, *raw, *lvpp;
@@ -140,6 +141,7 @@ or_trainer *or_trainer_new(const or_train_cfg *c, const float *init_params) {
     or_adam_init(&t->adam, &t->net);
     or_obs_norm_init(&t->on, t->D, 10.0f);
     or_ret_norm_init(&t->rn, t->N, t->P, c->gamma, c->return_clip);
+    or_popart_init(&t->pa);
     or_rng_seed_u64(&t->rng, c->seed);   /* main.rs:189 */
     size_t TN = (size_t)t->T * t->N;
     t->obs = malloc(sizeof(float) * TN * t->D);
@@ -254,6 +256,11 @@ void or_trainer_set_norms(or_trainer *t, const double *mean, const double *m2, d
     }
 }
 
+void or_trainer_popart(or_trainer *t, double *get4, const double *set4) {
+    if (get4) { get4[0] = t->pa.mean; get4[1] = t->pa.var; get4[2] = t->pa.count; get4[3] = t->pa.epsilon; }
+    if (set4) { t->pa.mean = set4[0]; t->pa.var = set4[1]; t->pa.count = set4[2]; t->pa.epsilon = set4[3]; }
+}
+
 size_t or_trainer_num_params(const or_trainer *t) { return t->net.n_params; }
 void or_trainer_get_params(const or_trainer *t, float *o) { memcpy(o, t->params, sizeof(float) * t->net.n_params); }
 void or_trainer_set_params(or_trainer *t, const float *i) { memcpy(t->params, i, sizeof(float) * t->net.n_params); }
@@ -319,6 +326,7 @@ static int collect_opp(or_trainer *t) {
             }
             if (t->c.normalize_obs) or_obs_norm_normalize_batch(&t->on, xo, n);
             forward_rows(t, xo, xp, n, logits, vals);
+            if (t->c.normalize_values) or_popart_denormalize(&t->pa, vals, (size_t)n);   /* :759-763 */
             if (hm) mask_rows(logits, mk, rows, n, A);
             or_sample_categorical(&t->rng, logits, n, A, sact);
             for (int j = 0; j < n; j++) {
@@ -407,6 +415,7 @@ int or_trainer_collect(or_trainer *t) {
         if (hm)
             for (size_t q = 0; q < (size_t)N * A; q++) t->masks[base * A + q] = mk[q] ? 1.0f : 0.0f;
         forward_rows(t, obs, G ? t->priv + base * G : NULL, N, logits, vals);  /* :322-333 */
+        if (t->c.normalize_values) or_popart_denormalize(&t->pa, vals, (size_t)N);   /* :355-359 */
         if (hm) {                                                /* :337 apply_action_mask */
             long bad = or_apply_action_mask(logits, mk, (size_t)N, A);
             if (bad >= 0) { fprintf(stderr, "Empty action mask: env %ld\n", bad); abort(); }
@@ -461,6 +470,7 @@ void or_trainer_gae(or_trainer *t) {
     if (t->c.normalize_obs) or_obs_norm_normalize_batch(&t->on, obs, N);
     if (G) or_vecenv_get_priv(t->env, priv);
     forward_rows(t, obs, priv, N, logits, lv);
+    if (t->c.normalize_values) or_popart_denormalize(&t->pa, lv, (size_t)N);   /* main.rs:898-907 */
     if (P > 1) {
         int32_t *cp = malloc(sizeof(int32_t) * N);
         or_vecenv_get_players(t->env, cp);
@@ -490,6 +500,24 @@ void or_trainer_update(or_trainer *t, or_update_metrics *m) {
     }
     const int D = t->D, A = t->A, G = t->G;
     const or_ppo_cfg *c = &t->c.ppo;
+    /* ppo.rs:1787-1808 PopArt: statistics over the (learner) returns, then rescale the value head */
+    float rescale_mag = NAN;
+    double tsum = 0.0, tsq = 0.0, tcnt = 0.0;
+    if (t->c.normalize_values) {
+        float *rr = malloc(sizeof(float) * (B ? B : 1));
+        for (size_t i = 0; i < B; i++) rr[i] = t->ret[vidx ? vidx[i] : i];
+        double om, os;
+        or_popart_update(&t->pa, rr, B, &om, &os);
+        free(rr);
+        if (t->pa.count >= 2.0) {
+            size_t vw, vb; int vin;
+            or_net_value_head(&t->net, &vw, &vb, &vin);    /* ppo.rs:1599-1653 */
+            const double nm = t->pa.mean, ns = or_popart_std(&t->pa), sc = os / ns;
+            for (int i = 0; i < vin; i++) t->params[vw + i] = (float)((double)t->params[vw + i] * sc);
+            t->params[vb] = (float)(((double)t->params[vb] * os + om - nm) / ns);
+            rescale_mag = (float)fabs(sc);
+        }
+    }
     uint32_t *idx = malloc(sizeof(uint32_t) * B);
     size_t np = t->net.n_params;
     float *grads = malloc(sizeof(float) * np);
@@ -519,6 +547,11 @@ void or_trainer_update(or_trainer *t, or_update_metrics *m) {
                 if (mm) memcpy(mm + q * A, t->masks + r * A, sizeof(float) * A);
                 ma[q] = t->actions[r]; mlp[q] = t->logp[r]; madv[q] = t->adv[r];
                 mret[q] = t->ret[r]; mov[q] = t->values[r];
+            }
+            if (t->c.normalize_values) {                        /* ppo.rs:1859-1897 */
+                or_popart_normalize(&t->pa, mret, sz, mret);
+                or_popart_normalize(&t->pa, mov, sz, mov);
+                for (size_t q = 0; q < sz; q++) { tsum += (double)mret[q]; tsq += (double)mret[q] * mret[q]; tcnt += 1.0; }
             }
             float am, as, amn, amx;
             or_normalize_advantages(madv, sz, madvn, &am, &as, &amn, &amx);
@@ -559,6 +592,13 @@ void or_trainer_update(or_trainer *t, or_update_metrics *m) {
         m->avg_valid_actions = t->has_masks ? tav / n : 0.0f;
         m->entropy_valid_pct = t->has_masks ? tevp / n : 0.0f;
         m->num_updates = nup; m->epochs_run = epochs_run;
+        m->value_norm_rescale_mag = rescale_mag;
+        m->value_norm_target_mean = m->value_norm_target_std = NAN;
+        if (tcnt > 0) {                                                /* ppo.rs:2061-2068 */
+            const double mean = tsum / tcnt, var = tsq / tcnt - mean * mean;
+            m->value_norm_target_mean = (float)mean;
+            m->value_norm_target_std = (float)sqrt(var > 0.0 ? var : 0.0);
+        }
     }
     free(vidx); free(idx); free(grads); free(mo); free(mp); free(mm); free(ma); free(mlp); free(madv);
     free(mret); free(mov); free(madvn);

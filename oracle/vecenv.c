@@ -232,3 +232,32 @@ void or_ret_norm_update_and_normalize_all(or_ret_norm *n, float *rewards, const 
         if (dones[e]) or_ret_norm_reset_player(n, e, 0);
     }
 }
+
+/* ======================================================== PopArtNormalizer */
+void or_popart_init(or_popart *p) { p->mean = 0.0; p->var = 0.0; p->count = 0.0; p->epsilon = 1e-4; }
+/* normalization.rs:299-305 */
+double or_popart_std(const or_popart *p) { return p->count < 2.0 ? 1.0 : sqrt(p->var / p->count + p->epsilon); }
+/* normalization.rs:316-332: sequential Welford; returns the stats before the batch */
+void or_popart_update(or_popart *p, const float *r, size_t n, double *old_mean, double *old_std) {
+    *old_mean = p->mean;
+    *old_std = or_popart_std(p);
+    for (size_t i = 0; i < n; i++) {
+        const double x = (double)r[i];
+        p->count += 1.0;
+        const double d = x - p->mean;
+        p->mean += d / p->count;
+        p->var += d * (x - p->mean);
+    }
+}
+/* normalization.rs:337-348 */
+void or_popart_normalize(const or_popart *p, const float *x, size_t n, float *out) {
+    if (p->count < 2.0) { memmove(out, x, sizeof(float) * n); return; }
+    const double sd = or_popart_std(p);
+    for (size_t i = 0; i < n; i++) out[i] = (float)(((double)x[i] - p->mean) / sd);
+}
+/* normalization.rs:351-360 */
+void or_popart_denormalize(const or_popart *p, float *v, size_t n) {
+    if (p->count < 2.0) return;
+    const double sd = or_popart_std(p);
+    for (size_t i = 0; i < n; i++) v[i] = (float)((double)v[i] * sd + p->mean);
+}

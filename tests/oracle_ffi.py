@@ -61,6 +61,10 @@ class RetNorm(C.Structure):
                 ("epsilon", C.c_double), ("clip", C.c_float)]
 
 
+class PopArt(C.Structure):
+    _fields_ = [("mean", C.c_double), ("var", C.c_double), ("count", C.c_double), ("epsilon", C.c_double)]
+
+
 class Adam(C.Structure):
     _fields_ = [("m1", C.POINTER(C.c_float)), ("m2", C.POINTER(C.c_float)), ("time", C.POINTER(C.c_int32)),
                 ("has_state", C.c_int)]
@@ -93,7 +97,8 @@ class TrainCfg(C.Structure):
                 ("return_clip", C.c_float), ("gamma", C.c_double), ("gae_lambda", C.c_double),
                 ("lr", C.c_double), ("ent_coef", C.c_double), ("reward_shaping", C.c_double),
                 ("ppo", PpoCfg), ("seed", C.c_uint64), ("threads", C.c_int),
-                ("cnn", C.c_int), ("num_conv", C.c_int), ("conv_ch", C.c_int * 4), ("ksize", C.c_int)]
+                ("cnn", C.c_int), ("num_conv", C.c_int), ("conv_ch", C.c_int * 4), ("ksize", C.c_int),
+                ("normalize_values", C.c_int)]
 
 
 class UpdateMetrics(C.Structure):
@@ -102,7 +107,8 @@ class UpdateMetrics(C.Structure):
         "explained_variance", "total_loss", "value_mean", "returns_mean", "adv_mean_raw",
         "adv_std_raw", "adv_min_raw", "adv_max_raw", "value_error_mean", "value_error_std",
         "value_error_max", "avg_valid_actions", "entropy_valid_pct")] + [
-        ("num_updates", C.c_int32), ("epochs_run", C.c_int32)]
+        ("num_updates", C.c_int32), ("epochs_run", C.c_int32)] + [
+        (n, C.c_float) for n in ("value_norm_target_mean", "value_norm_target_std", "value_norm_rescale_mag")]
 
 
 class MbStats(C.Structure):
@@ -218,6 +224,13 @@ def lib():
             "or_apply_action_mask": (C.c_long, [f32, u8, C.c_size_t, C.c_int]),
             "or_trainer_set_rng": (None, [C.c_void_p, u32, C.c_uint64]),
             "or_trainer_set_adam": (None, [C.c_void_p, f32, f32, i32, C.c_int]),
+            "or_trainer_popart": (None, [C.c_void_p, C.c_void_p, C.c_void_p]),
+            "or_popart_init": (None, [C.POINTER(PopArt)]),
+            "or_popart_std": (C.c_double, [C.POINTER(PopArt)]),
+            "or_popart_update": (None, [C.POINTER(PopArt), f32, C.c_size_t, C.POINTER(C.c_double),
+                                        C.POINTER(C.c_double)]),
+            "or_popart_normalize": (None, [C.POINTER(PopArt), f32, C.c_size_t, f32]),
+            "or_popart_denormalize": (None, [C.POINTER(PopArt), f32, C.c_size_t]),
             "or_trainer_get_adam": (None, [C.c_void_p, f32, f32, i32, C.c_int]),
             "or_trainer_set_norms": (None, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_double, C.c_void_p,
                                             C.c_void_p]),
@@ -339,7 +352,7 @@ def ppo_cfg(num_epochs=4, num_minibatches=4, clip=0.2, value_coef=0.5, max_grad_
 def train_cfg(env_kind=ENV_CARTPOLE, num_envs=8, num_steps=128, hidden=64, num_hidden=2, relu=True,
               ctde=False, critic_hidden=0, critic_num_hidden=0, normalize_obs=True,
               normalize_returns=True, return_clip=10.0, gamma=0.99, gae_lambda=0.95, lr=1e-3,
-              ent_coef=0.01, reward_shaping=0.0, seed=42, threads=0, cnn=None, **ppo):
+              ent_coef=0.01, reward_shaping=0.0, seed=42, threads=0, cnn=None, normalize_values=False, **ppo):
     """cnn: None, or (conv_channels per layer, kernel_size); hidden / num_hidden are
     then cnn_fc_hidden_size / cnn_num_fc_layers"""
     extra = {}
@@ -347,7 +360,7 @@ def train_cfg(env_kind=ENV_CARTPOLE, num_envs=8, num_steps=128, hidden=64, num_h
         ch, ks = cnn
         extra = dict(cnn=1, num_conv=len(ch), conv_ch=(C.c_int * 4)(*[ch[min(i, len(ch) - 1)] for i in range(4)]),
                      ksize=ks)
-    return TrainCfg(**extra, env_kind=env_kind, num_envs=num_envs, num_steps=num_steps, hidden=hidden,
+    return TrainCfg(**extra, normalize_values=int(normalize_values), env_kind=env_kind, num_envs=num_envs, num_steps=num_steps, hidden=hidden,
                     num_hidden=num_hidden, relu=int(relu), ctde=int(ctde), critic_hidden=critic_hidden,
                     critic_num_hidden=critic_num_hidden, normalize_obs=int(normalize_obs),
                     normalize_returns=int(normalize_returns), return_clip=return_clip, gamma=gamma,
@@ -432,6 +445,14 @@ class Trainer:
         lp = np.zeros(max(n_opp, 1), np.int32); po = np.zeros(max(n_opp, 1) * P, np.int32)
         lib().or_trainer_opponent_envs(self.h, lp.ctypes.data, po.ctypes.data)
         return lp[:n_opp], po[:n_opp * P]
+
+    def popart(self, set4=None):
+        g = np.zeros(4)
+        lib().or_trainer_popart(self.h, g.ctypes.data, None)
+        if set4 is not None:
+            s4 = np.ascontiguousarray(set4, np.float64)
+            lib().or_trainer_popart(self.h, None, s4.ctypes.data)
+        return g
 
     def phase_seconds(self, ph):
         return lib().or_trainer_last_phase_seconds(self.h, ph)

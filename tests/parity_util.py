@@ -102,6 +102,17 @@ def assert_metrics_close(m, om, values=None, returns=None, skip=(), rtol=RTOL):
         tol = rtol * max(abs(o), _floor(k, om))
         if not abs(d - o) <= tol:
             bad.append((k, d, o, abs(d - o) / max(abs(o), 1e-30)))
+    # PopArt (ppo.rs:2061-2068): NaN = None on both sides
+    for k in ("value_norm_target_mean", "value_norm_target_std", "value_norm_rescale_mag"):
+        if k in skip or k not in om:
+            continue
+        d, o = float(m[k]), float(om[k])
+        if np.isnan(o) or np.isnan(d):
+            if not (np.isnan(o) and np.isnan(d)):
+                bad.append((k, d, o))
+            continue
+        if not abs(d - o) <= rtol * max(abs(o), 1.0 if k == "value_norm_target_mean" else 0.0):
+            bad.append((k, d, o))
     assert not bad, bad
 
 

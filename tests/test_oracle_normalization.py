@@ -223,3 +223,86 @@ def test_apply_action_mask_empty_row_panics():       # utils.rs:246-254 (#[shoul
     m = np.array([1, 1, 0, 0, 0, 0], np.uint8)      # row 1 of 2 (A = 3) has no valid action
     assert O.lib().or_apply_action_mask(lg, m, 2, 3) == 1
     assert (lg == 0.0).all()                         # nothing applied: the reference panics first
+
+
+# --------------------------------------------------------------- PopArt ---
+class Pop:
+    def __init__(self):
+        self.p = O.PopArt()
+        O.lib().or_popart_init(C.byref(self.p))
+
+    def update(self, xs):
+        om, os_ = C.c_double(), C.c_double()
+        O.lib().or_popart_update(C.byref(self.p), np.asarray(xs, np.float32), len(xs), C.byref(om), C.byref(os_))
+        return om.value, os_.value
+
+    def std(self):
+        return O.lib().or_popart_std(C.byref(self.p))
+
+    def initialized(self):
+        return self.p.count >= 2.0
+
+    def normalize(self, xs):
+        x = np.asarray(xs, np.float32)
+        out = np.zeros_like(x)
+        O.lib().or_popart_normalize(C.byref(self.p), x, x.size, out)
+        return out
+
+    def denormalize(self, xs):
+        x = np.array(xs, np.float32)
+        O.lib().or_popart_denormalize(C.byref(self.p), x, x.size)
+        return x
+
+
+def test_popart_creation():                          # normalization.rs:713-718
+    n = Pop()
+    assert not n.initialized() and n.std() == 1.0
+
+
+def test_popart_update():                            # normalization.rs:721-736
+    n = Pop()
+    _, os_ = n.update([10.0])
+    assert not n.initialized() and os_ == 1.0
+    n.update([20.0])
+    assert n.initialized() and abs(n.p.mean - 15.0) < 0.01
+
+
+def test_popart_multi_sample_update():               # normalization.rs:739-749
+    n = Pop()
+    n.update([0.0, 10.0, 20.0, 30.0, 40.0])
+    assert abs(n.p.mean - 20.0) < 0.01 and 14.0 < n.std() < 15.0
+    assert n.std() == np.sqrt(200.0 + 1e-4)
+
+
+def test_popart_normalize():                         # normalization.rs:752-765
+    n = Pop()
+    n.update([0.0, 10.0, 20.0, 30.0, 40.0])
+    assert abs(n.normalize([20.0])[0]) < 0.1
+    assert 0.5 < n.normalize([34.14])[0] < 1.5
+
+
+def test_popart_returns_old_stats():                 # normalization.rs:768-785
+    n = Pop()
+    n.update([0.0, 10.0])
+    mb, sb = n.p.mean, n.std()
+    om, os_ = n.update([20.0])
+    assert abs(om - mb) < 1e-10 and abs(os_ - sb) < 1e-10 and n.p.mean != mb
+
+
+def test_popart_normalize_before_initialized():      # normalization.rs:800-810
+    n = Pop()
+    n.update([10.0])
+    assert not n.initialized() and n.normalize([5.0])[0] == 5.0
+
+
+def test_popart_denormalize_inverse_of_normalize():  # normalization.rs:813-827
+    n = Pop()
+    n.update([10.0, 20.0, 100.0, 200.0])
+    d = n.denormalize(n.normalize([15.0, 150.0]))
+    assert np.allclose(d, [15.0, 150.0], atol=1e-4)
+
+
+def test_popart_denormalize_before_initialized():    # normalization.rs:830-841
+    n = Pop()
+    n.update([10.0])
+    assert n.denormalize([5.0])[0] == 5.0
