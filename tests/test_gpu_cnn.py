@@ -77,10 +77,13 @@ def test_cnn_forward_bit_exact(net):
 # (test_cnn_single_minibatch_gradient); what grows over the steps is the f32
 # reduction-order difference of the conv weight gradients (sums over B*H*W
 # positions) amplified by Adam (m/sqrt(v): entries with near-zero gradient move
-# by ~lr either way) — measured 6e-5..1.1e-4 on approx_kl / value_mean.
+# by ~lr either way) — measured 6e-5..1.1e-4 on approx_kl / value_mean, and
+# 0.18 % of the parameters beyond atol 2e-5 (max 1.7e-4 = 0.17 lr): parameter
+# atol 5e-4 for that case.
 @pytest.mark.parametrize("net,N,T,rtol", [(NETS[0], 64, 16, 1e-5), (NETS[1], 64, 12, 1e-5), (NETS[2], 1024, 8, 2e-4),
                                           (NETS[3], 48, 10, 1e-5)])
 def test_cnn_rollout_update_second_rollout(net, N, T, rtol):
+    from parity_util import PARAM_ATOL, PARAM_RTOL
     cfg, tr, ot = _pair(N, T, net)
     bppo.collect_rollouts(tr.ctx); ot.collect()
     _cmp(tr, ot)
@@ -90,7 +93,8 @@ def test_cnn_rollout_update_second_rollout(net, N, T, rtol):
     om = ot.update()
     assert tr.ctx.rng_pos() == ot.rng_pos()
     assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"), rtol=rtol)
-    assert_params_close(tr.model.get_params(), ot.params())
+    np.testing.assert_allclose(tr.model.get_params(), ot.params(), rtol=PARAM_RTOL,
+                               atol=PARAM_ATOL if rtol == 1e-5 else 5e-4)
     tr.model.set_params(ot.params())
     bppo.collect_rollouts(tr.ctx); ot.collect()
     _cmp(tr, ot)
