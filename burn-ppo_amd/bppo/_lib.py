@@ -71,7 +71,7 @@ ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_size_t, C.c_void_p)
 EXPORTS = (
     "bppo_create", "bppo_destroy", "bppo_last_error", "bppo_version", "bppo_num_params",
     "bppo_params_set", "bppo_params_get", "bppo_forward", "bppo_rng_get", "bppo_rng_set",
-    "bppo_vecenv_reset", "bppo_vecenv_observe", "bppo_vecenv_step", "bppo_vecenv_set_step",
+    "bppo_vecenv_reset", "bppo_vecenv_observe", "bppo_vecenv_step", "bppo_vecenv_set_step", "bppo_set_reward_shaping_schedule",
     "bppo_obs_norm_get", "bppo_obs_norm_set", "bppo_ret_norm_get", "bppo_ret_norm_set",
     "bppo_collect_rollouts", "bppo_rollout_episodes", "bppo_compute_gae", "bppo_ppo_update",
     "bppo_set_allreduce", "bppo_set_allreduce_async", "bppo_get_stream", "bppo_opponents_set", "bppo_opponents_get_envs", "bppo_buffer_get", "bppo_buffer_set", "bppo_gae_device",
@@ -118,6 +118,7 @@ def lib():
         "bppo_vecenv_observe": (i32, [vp, vp, vp, vp, vp]),
         "bppo_vecenv_step": (i32, [vp, vp, vp, vp, vp, vp, i32, C.POINTER(i32)]),
         "bppo_vecenv_set_step": (i32, [vp, u64]),
+        "bppo_set_reward_shaping_schedule": (i32, [vp, vp, vp, i32]),
         "bppo_obs_norm_get": (i32, [vp, vp, vp, dp]),
         "bppo_obs_norm_set": (i32, [vp, vp, vp, C.c_double]),
         "bppo_ret_norm_get": (i32, [vp, vp, vp]),

@@ -14,6 +14,15 @@ def minibatch_sizes(batch_size, num_minibatches):
             if base + (1 if i < rem else 0) > 0]
 
 
+def shaping_schedule(c):
+    """reward_shaping_coef as (value, step) milestones: a number is Schedule::constant
+    (schedule.rs:44-46, 232-251), a list is sorted by step (schedule.rs:257-270)."""
+    v = c["reward_shaping_coef"]
+    if isinstance(v, (int, float)):
+        return [(float(v), 0)]
+    return sorted(((float(a), int(b)) for a, b in v), key=lambda p: p[1])
+
+
 def schedule_get(points, step):
     """schedule.rs:54-78 piecewise-linear [(value, step), ...]."""
     if not points:
@@ -88,8 +97,10 @@ def to_struct(c, rank=0, world=1, envs_per_rank=None):
     s.normalize_returns = int(nr)
     s.clip_value = int(c["clip_value"])
     for k in ("gamma", "gae_lambda", "clip_epsilon", "value_coef", "max_grad_norm", "adam_epsilon",
-              "return_clip", "reward_shaping_coef"):
+              "return_clip"):
         setattr(s, k, float(c[k]))
+    # a Schedule's initial value; the milestones follow via bppo_set_reward_shaping_schedule
+    s.reward_shaping_coef = schedule_get(shaping_schedule(c), 0)
     s.target_kl = -1.0 if c["target_kl"] is None else float(c["target_kl"])
     s.seed = c["seed"]
     s.normalize_values = int(bool(c.get("normalize_values", False)))

@@ -21,7 +21,7 @@ from collections import deque
 import numpy as np
 
 from . import _lib as L
-from .host import make_config, orthogonal_init, schedule_get, to_struct
+from .host import make_config, orthogonal_init, schedule_get, shaping_schedule, to_struct
 
 
 class Context:
@@ -41,6 +41,9 @@ class Context:
             raise L.BppoError(st, msg)
         self.N = self.struct.num_envs
         self.T = self.struct.num_steps
+        sched = shaping_schedule(cfg)
+        if len(sched) != 1 or sched[0][1] != 0:
+            self.set_reward_shaping_schedule(sched)
         self.n_params = L.lib().bppo_num_params(self.h)
         self.obs_dim = {"cartpole": 5, "connect_four": 86, "liars_dice": 270}[cfg["env"]]
         self.num_actions = {"cartpole": 2, "connect_four": 7, "liars_dice": 49}[cfg["env"]]
@@ -106,6 +109,12 @@ class Context:
         if r.size != self.N * self.num_players:
             raise ValueError(f"returns must hold num_envs * num_players = {self.N * self.num_players} values")
         self._chk(L.lib().bppo_ret_norm_set(self.h, mvc.ctypes.data, r.ctypes.data))
+
+    def set_reward_shaping_schedule(self, milestones):
+        """reward_shaping_coef: Schedule [(value, step), ...] (config.rs:761-762)."""
+        v = np.ascontiguousarray([float(a) for a, _ in milestones], np.float64)
+        st = np.ascontiguousarray([int(b) for _, b in milestones], np.uint64)
+        self._chk(L.lib().bppo_set_reward_shaping_schedule(self.h, v.ctypes.data, st.ctypes.data, len(v)))
 
     def popart(self):
         """PopArtNormalizer state [mean, M2, count, epsilon] (normalization.rs:275-284)"""

@@ -141,6 +141,7 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     }
     c->wide = cfg->env_kind != BPPO_ENV_CARTPOLE;
     if (c->wide && !cfg->ctde) c->G = 0;
+    if (!(cfg->reward_shaping_coef >= 0.0)) { c->err = "reward_shaping_coef must be >= 0"; return BPPO_ERR_ARG; }   // config.rs:1514-1519
     if (cfg->cnn) {
         // cnn.rs:73-74 "CNN requires OBSERVATION_SHAPE" (only Connect Four has one)
         if (cfg->env_kind != BPPO_ENV_CONNECT_FOUR || cfg->ctde) { c->err = "CNN requires OBSERVATION_SHAPE (Connect Four)"; return BPPO_ERR_ARG; }
@@ -218,6 +219,7 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     TRY(c->shuf.init(dev, c->rng_key, cfg->rng_stream, (uint32_t)TN, cfg->num_epochs, TN * (uint64_t)c->A, c->err));
     c->on_mean.assign(c->D, 0.0); c->on_m2.assign(c->D, 0.0); c->on_count = 0;
     c->u_ret = c->d_ret; c->u_val = c->d_val;
+    c->shaping_v.assign(1, cfg->reward_shaping_coef); c->shaping_s.assign(1, 0);   // Schedule::constant
     if (cfg->normalize_values) TRY(popart_alloc(c));
     if (c->wide) {
         TRY(wide_init(c));
@@ -423,7 +425,6 @@ extern "C" bppo_status bppo_vecenv_step(bppo_ctx *c, const int32_t *actions, flo
                 eps[i].step = recs[i].step; eps[i].pad = 0;
             }
         }
-        c->global_step += N;
         return BPPO_OK;
     }
     // persistent scratch (ctx_init): no allocator round-trip per step
@@ -449,13 +450,28 @@ extern "C" bppo_status bppo_vecenv_step(bppo_ctx *c, const int32_t *actions, flo
             eps[i].step = recs[i].step; eps[i].pad = 0;
         }
     }
-    c->global_step += N;
     return BPPO_OK;
 }
 
+// Environment::set_step (env.rs:329-333): the step every schedulable env parameter
+// (Liar's Dice reward shaping, liars_dice.rs:535, 635) is evaluated at
 extern "C" bppo_status bppo_vecenv_set_step(bppo_ctx *c, uint64_t s) {
     if (!c) return BPPO_ERR_ARG;
-    c->global_step = s;
+    c->env_step = s;
+    return BPPO_OK;
+}
+
+// reward_shaping_coef as a Schedule (config.rs:761-762; schedule.rs:29): milestones
+// (values[i], steps[i]) in the caller's order (the reference sorts at parse time,
+// schedule.rs:144, 268).  n = 0 is the empty schedule (get = 0.0).  Initial value
+// must be >= 0 (config.rs:1514-1519).
+extern "C" bppo_status bppo_set_reward_shaping_schedule(bppo_ctx *c, const double *values, const uint64_t *steps,
+                                                        int32_t n) {
+    if (!c || n < 0 || (n > 0 && (!values || !steps))) return BPPO_ERR_ARG;
+    std::vector<double> v(values, values + n);
+    std::vector<uint64_t> s(steps, steps + n);
+    if (bppo::schedule_get(v, s, 0) < 0.0) { c->err = "reward_shaping_coef must be >= 0"; return BPPO_ERR_ARG; }
+    c->shaping_v = std::move(v); c->shaping_s = std::move(s);
     return BPPO_OK;
 }
 
@@ -549,7 +565,6 @@ extern "C" bppo_status bppo_collect_rollouts(bppo_ctx *c, bppo_rollout_info *inf
     BPPO_HIP(c, sync_stream(c));
     tm_read(c, TM_ROLLOUT); tm_read(c, TM_RETNORM);
     c->collected = 1; c->gae_done = 0;
-    c->global_step += TN;
     // device error bits: 1 non-finite log-prob, 2 empty action mask, 4 opponent seat
     // table names a model outside [0, n_models)
     if (hv[1] & 2) { c->err = "Empty action mask: an env has no valid action"; return BPPO_ERR_EMPTY_MASK; }

@@ -194,7 +194,10 @@ struct bppo_ctx {
     uint64_t *d_env_pos = nullptr;
     float *d_ep_ret = nullptr;        // [N*P]
     int32_t *d_ep_len = nullptr;
-    uint64_t global_step = 0;
+    uint64_t env_step = 0;            // the envs' current_step (Environment::set_step, env.rs:329-333)
+    // reward_shaping_coef Schedule (schedule.rs:29) as (value, step) milestones
+    std::vector<double> shaping_v;
+    std::vector<uint64_t> shaping_s;
     // rollout buffer [T][N][...]
     float *d_obs = nullptr, *d_rew = nullptr, *d_rew_raw = nullptr, *d_done = nullptr;
     float *d_val = nullptr, *d_logp = nullptr, *d_adv = nullptr, *d_ret = nullptr;
@@ -379,6 +382,22 @@ bppo_status wide_forward_host(bppo_ctx *c, const float *obs, const float *priv, 
 bppo_status wide_buffer_get(bppo_ctx *c, const char *name, void *host, size_t bytes, bool *handled);
 // PopArt (popart.hip)
 double popart_std(const bppo_ctx *c);
+
+// Schedule::get (schedule.rs:54-78): piecewise-linear over (value, step) milestones,
+// first value before the first milestone, last value after the last, 0 when empty
+inline double schedule_get(const std::vector<double> &v, const std::vector<uint64_t> &s, uint64_t step) {
+    const size_t n = v.size();
+    if (n == 0) return 0.0;
+    if (n == 1 || step <= s[0]) return v[0];
+    for (size_t i = 0; i + 1 < n; i++)
+        if (step >= s[i] && step < s[i + 1]) {
+            const double t = (double)(step - s[i]) / (double)(s[i + 1] - s[i]);
+            return v[i] + (v[i + 1] - v[i]) * t;
+        }
+    return v[n - 1];
+}
+// the shaping bonus the envs add this step: reward_shaping_coef.get(current_step) as f32
+inline float shaping_coef(const bppo_ctx *c) { return (float)schedule_get(c->shaping_v, c->shaping_s, c->env_step); }
 bppo_status popart_alloc(bppo_ctx *c);
 void popart_free(bppo_ctx *c);
 bppo_status popart_denorm(bppo_ctx *c, float *v, size_t n);

@@ -220,7 +220,7 @@ bppo_status wide_collect(bppo_ctx *c, uint64_t base) {
         WHIP(c, wide_sample(A, c->stream, s));
         WideStepArgs w;
         w.N = N; w.t = t; w.state = c->d_wstate; w.env_pos = c->d_env_pos; w.seed_base = c->cfg.env_seed_base;
-        w.actions = c->d_act + r0; w.shaping = (float)c->cfg.reward_shaping_coef;
+        w.actions = c->d_act + r0; w.shaping = shaping_coef(c);
         w.all_r = c->d_allr + r0 * P; w.rew_act = (c->cfg.normalize_returns ? c->d_rew_raw : c->d_rew) + r0; w.done_f = c->d_done + r0; w.done_u8 = nullptr;
         w.ep_ret = c->d_ep_ret; w.ep_len = c->d_ep_len; w.eps = c->d_eps; w.ep_count = c->d_ep_count;
         w.eps_cap = c->eps_cap;
@@ -348,7 +348,7 @@ bppo_status wide_step_host(bppo_ctx *c, const int32_t *actions, float *obs, floa
     WHIP(c, hipMemcpyAsync(c->d_act_in, actions, 4 * (size_t)N, hipMemcpyHostToDevice, c->stream));
     WideStepArgs w;
     w.N = N; w.t = 0; w.state = c->d_wstate; w.env_pos = c->d_env_pos; w.seed_base = c->cfg.env_seed_base;
-    w.actions = c->d_act_in; w.shaping = (float)c->cfg.reward_shaping_coef;
+    w.actions = c->d_act_in; w.shaping = shaping_coef(c);
     w.all_r = c->d_scr_r; w.rew_act = nullptr; w.done_f = nullptr; w.done_u8 = c->d_scr_d;
     w.ep_ret = c->d_ep_ret; w.ep_len = c->d_ep_len; w.eps = c->d_eps; w.ep_count = c->d_ep_count;
     w.eps_cap = c->eps_cap;

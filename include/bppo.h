@@ -143,7 +143,15 @@ bppo_status bppo_vecenv_observe(bppo_ctx *ctx, float *obs, int32_t *players, uin
  * completed episodes in env order (up to cap), count in *n_eps */
 bppo_status bppo_vecenv_step(bppo_ctx *ctx, const int32_t *actions, float *obs, float *rewards,
                              uint8_t *dones, bppo_episode *eps, int32_t cap, int32_t *n_eps);
+/* VecEnv::set_step (env.rs:329-333, main.rs:727): the step schedulable env
+ * parameters are evaluated at (Liar's Dice shaping, liars_dice.rs:535, 635) */
 bppo_status bppo_vecenv_set_step(bppo_ctx *ctx, uint64_t global_step);
+/* reward_shaping_coef: Schedule (config.rs:761-762, schedule.rs:29-78) as n
+ * (value, step) milestones, sorted by step as Schedule::parse_cli / Deserialize
+ * leave them; replaces the constant config.reward_shaping_coef.  n = 0: empty
+ * schedule (0.0).  BPPO_ERR_ARG when the initial value is < 0 (config.rs:1514). */
+bppo_status bppo_set_reward_shaping_schedule(bppo_ctx *ctx, const double *values, const uint64_t *steps,
+                                             int32_t n);
 
 /* ---- normalizers (f64 state, normalization.rs) ------------------------ */
 bppo_status bppo_obs_norm_get(bppo_ctx *ctx, double *mean, double *m2, double *count);

@@ -131,6 +131,7 @@ int or_vecenv_act_dim(const or_vecenv *v);
 int or_vecenv_players(const or_vecenv *v);
 int or_vecenv_priv_dim(const or_vecenv *v);
 void or_vecenv_set_shaping(or_vecenv *v, float coef);
+double or_schedule_get(const double *values, const uint64_t *steps, int n, uint64_t step);
 void or_vecenv_get_obs(const or_vecenv *v, float *obs);
 void or_vecenv_get_players(const or_vecenv *v, int32_t *players);
 int or_vecenv_get_masks(const or_vecenv *v, uint8_t *masks);  /* returns 0 if env has no masks */
@@ -296,6 +297,8 @@ void or_trainer_get_params(const or_trainer *t, float *out);
 void or_trainer_set_params(or_trainer *t, const float *in);
 uint64_t or_trainer_rng_pos(const or_trainer *t);
 void or_trainer_set_rng(or_trainer *t, const uint32_t key[8], uint64_t pos);
+/* main.rs:720-727: reward_shaping_coef.get(global_step) for the next rollout */
+void or_trainer_set_shaping(or_trainer *t, float coef);
 void or_trainer_set_adam(or_trainer *t, const float *m1, const float *m2, const int32_t *steps, int n_tensors);
 void or_trainer_get_adam(const or_trainer *t, float *m1, float *m2, int32_t *steps, int n_tensors);
 void or_trainer_popart(or_trainer *t, double *get4, const double *set4);

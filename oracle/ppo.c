@@ -228,6 +228,8 @@ void or_trainer_opponent_envs(const or_trainer *t, int32_t *learner_pos, int32_t
 
 /* resume hooks (checkpoint.rs:405-465 load_*): main RNG = StdRng::from_seed(key
  * bytes) at word position pos, Adam moments + per-tensor steps, normalizer state */
+void or_trainer_set_shaping(or_trainer *t, float coef) { or_vecenv_set_shaping(t->env, coef); }
+
 void or_trainer_set_rng(or_trainer *t, const uint32_t key[8], uint64_t pos) {
     or_rng_from_key(&t->rng, key, 12);
     t->rng.word_pos = pos;

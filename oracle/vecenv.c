@@ -73,6 +73,19 @@ int or_vecenv_players(const or_vecenv *v) { return v->players; }
 int or_vecenv_priv_dim(const or_vecenv *v) { return v->priv_dim; }
 void or_vecenv_set_shaping(or_vecenv *v, float c) { v->shaping = c; }
 
+/* schedule.rs:54-78 Schedule::get over n (value, step) milestones */
+double or_schedule_get(const double *v, const uint64_t *s, int n, uint64_t step) {
+    if (n <= 0) return 0.0;
+    if (n == 1 || step <= s[0]) return v[0];
+    for (int i = 0; i < n - 1; i++) {
+        if (step >= s[i] && step < s[i + 1]) {
+            double t = (double)(step - s[i]) / (double)(s[i + 1] - s[i]);
+            return v[i] + (v[i + 1] - v[i]) * t;
+        }
+    }
+    return v[n - 1];
+}
+
 /* env.rs:336-376 */
 void or_vecenv_get_obs(const or_vecenv *v, float *obs) {
     memcpy(obs, v->obs, sizeof(float) * (size_t)v->n * v->obs_dim);

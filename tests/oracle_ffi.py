@@ -223,6 +223,8 @@ def lib():
             "or_ret_norm_update_and_normalize_all": (None, [C.POINTER(RetNorm), f32, u8]),
             "or_apply_action_mask": (C.c_long, [f32, u8, C.c_size_t, C.c_int]),
             "or_trainer_set_rng": (None, [C.c_void_p, u32, C.c_uint64]),
+            "or_trainer_set_shaping": (None, [C.c_void_p, C.c_float]),
+            "or_schedule_get": (C.c_double, [C.c_void_p, C.c_void_p, C.c_int, C.c_uint64]),
             "or_trainer_set_adam": (None, [C.c_void_p, f32, f32, i32, C.c_int]),
             "or_trainer_popart": (None, [C.c_void_p, C.c_void_p, C.c_void_p]),
             "or_popart_init": (None, [C.POINTER(PopArt)]),

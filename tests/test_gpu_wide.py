@@ -16,6 +16,7 @@ import bppo
 import bppo._lib as L
 import oracle_ffi as O
 from parity_util import assert_metrics_close, assert_params_close
+from bppo.host import shaping_schedule
 
 pytestmark = pytest.mark.gpu
 
@@ -91,7 +92,7 @@ def _pair(env, N, T, seed=42, ctde=None, **kw):
                        normalize_returns=bool(cfg["normalize_returns"]), gamma=cfg["gamma"], gae_lambda=cfg["gae_lambda"],
                        lr=bppo.schedule_get(cfg["learning_rate"], 0),
                        ent_coef=bppo.schedule_get(cfg["entropy_coef"], 0),
-                       reward_shaping=cfg["reward_shaping_coef"], num_epochs=cfg["num_epochs"],
+                       reward_shaping=bppo.schedule_get(shaping_schedule(cfg), 0), num_epochs=cfg["num_epochs"],
                        num_minibatches=cfg["num_minibatches"], clip=cfg["clip_epsilon"],
                        value_coef=cfg["value_coef"], target_kl=cfg["target_kl"])
     ot = O.Trainer(ocfg, params)
@@ -123,6 +124,40 @@ def _cmp_rollout(env, tr, ot, rew_rtol=0.0):
         assert np.array_equal(_bits(b.rewards.reshape(-1)), _bits(ot.buffer("rewards")))
         assert np.array_equal(_bits(b.all_rewards.reshape(-1)), _bits(ot.buffer("all_rewards")))
     assert tr.ctx.rng_pos() == ot.rng_pos()
+
+
+@pytest.mark.parametrize("ctde", [None, False])
+def test_liars_dice_shaping_schedule(ctde):
+    """reward_shaping_coef as a Schedule (liars_dice.rs:164, 535; main.rs:720-727):
+    each rollout uses coef.get(global_step) set through VecEnv::set_step; the
+    oracle gets the same value from its own Schedule::get restatement."""
+    N, T = 48, 16
+    sched = [(0.2, 0), (0.05, 2 * N * T), (0.0, 4 * N * T)]
+    cfg, tr, ot = _pair("liars_dice", N, T, ctde=ctde, reward_shaping_coef=sched)
+    v = np.array([a for a, _ in sched]); st = np.array([b for _, b in sched], np.uint64)
+    coefs = []
+    for k in range(4):
+        step = k * N * T + (N * T // 2 if k == 3 else 0)
+        tr.vec_env.set_step(step)
+        c = O.lib().or_schedule_get(v.ctypes.data, st.ctypes.data, len(v), step)
+        assert c == bppo.schedule_get(sched, step)
+        coefs.append(c)
+        O.lib().or_trainer_set_shaping(ot.h, c)
+        bppo.collect_rollouts(tr.ctx); ot.collect()
+        _cmp_rollout("liars_dice", tr, ot)
+    assert len(set(coefs)) == 4
+    tr.close(); ot.close()
+
+
+def test_shaping_schedule_rejects_negative_initial():
+    cfg = bppo.make_config("liars_dice_ctde", num_envs=8, num_steps=4)
+    tr = bppo.Trainer(cfg)
+    with pytest.raises(bppo.BppoError):
+        tr.ctx.set_reward_shaping_schedule([(-0.1, 0), (0.1, 100)])
+    tr.ctx.set_reward_shaping_schedule([(0.0, 0), (-0.1, 100)])    # only the initial value is validated
+    tr.close()
+    with pytest.raises(bppo.BppoError):
+        bppo.Trainer(bppo.make_config("liars_dice_ctde", num_envs=8, num_steps=4, reward_shaping_coef=-1.0))
 
 
 CASES = [("connect_four", 64, 16, None), ("liars_dice", 48, 16, None), ("liars_dice", 40, 12, False)]
