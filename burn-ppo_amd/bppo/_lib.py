@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libbppo.so")
+# BPPO_LIB_PATH: a diagnostic build of the same library (e.g. libbppo_stamps.so)
+LIB_PATH = os.environ.get("BPPO_LIB_PATH") or os.path.join(HERE, "libbppo.so")
 
 OK, ERR_ARG, ERR_NONFINITE, ERR_EMPTY_MASK, ERR_HIP, ERR_COMM, ERR_UNSUPPORTED = range(7)
 ENV_CARTPOLE, ENV_CONNECT_FOUR, ENV_LIARS_DICE = 0, 1, 2

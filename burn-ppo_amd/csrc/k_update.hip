@@ -31,7 +31,27 @@ struct MbArgs {
     float inv_mb, ent_coef, value_coef;
     int clip_value;
     const float4 *rows;    // packed rows [B][4 x float4] (k_pack_rows) or nullptr
+    unsigned long long *stamps;   // diagnostic build only (BPPO_MB_STAMPS): per-wave segment cycles
 };
+
+// diagnostic build (-DBPPO_MB_STAMPS): s_memtime segment sums per wave
+// (cdna_hip_programming.md §7 in-kernel stamps); read the shares, not the time
+#ifdef BPPO_MB_STAMPS
+constexpr int MB_NSEG = 11;
+#define MB_STAMP(k)                                                                              \
+    do {                                                                                         \
+        __builtin_amdgcn_sched_barrier(0);                                                       \
+        unsigned long long t_;                                                                   \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");               \
+        __builtin_amdgcn_sched_barrier(0);                                                       \
+        st_acc[k] += t_ - st_prev;                                                               \
+        st_prev = t_;                                                                            \
+    } while (0)
+#else
+#define MB_STAMP(k) \
+    do {            \
+    } while (0)
+#endif
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -350,6 +370,10 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
     WaveB &B = reinterpret_cast<WaveB *>(smem + sizeof(Params) / 4)[wv];
     load_params(S, g.params);
     __syncthreads();
+#ifdef BPPO_MB_STAMPS
+    unsigned long long st_acc[MB_NSEG] = {}, st_prev;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_prev)::"memory");
+#endif
 
     const int c = lane & 31, h = lane >> 5;
     const int gwave = blockIdx.x * WAVES + wv, nwaves = gridDim.x * WAVES;
@@ -406,6 +430,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
             for (int d = 0; d < 5; d++) B.X[c * 5 + d] = cur.x(d);
         }
         wave_sync();
+        MB_STAMP(0);
         // ---- layer 1 (K = 5 padded to 6: the pad operand is 0)
         f32x16_t acc[2];
 #pragma unroll
@@ -427,6 +452,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
                 B.T1[cd_row(q, h) * RS + c + 32 * ct] = v > 0.0f ? v : 0.0f;
             }
         wave_sync();
+        MB_STAMP(1);
         // ---- layer 2 (K = 64)
 #pragma unroll
         for (int ct = 0; ct < 2; ct++)
@@ -439,6 +465,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
             acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv0, acc[0], 0, 0, 0);
             acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv1, acc[1], 0, 0, 0);
         }
+        MB_STAMP(2);
 #pragma unroll
         for (int ct = 0; ct < 2; ct++)
 #pragma unroll
@@ -447,8 +474,11 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
                 B.T2[cd_row(q, h) * RS + c + 32 * ct] = v > 0.0f ? v : 0.0f;
             }
         wave_sync();
-        // ---- heads + loss, lane = row (rows 0..31 on the low half-wave)
-        if (h == 0) {
+        MB_STAMP(3);
+        // ---- heads + loss, lane = row c on both lane halves (the halves compute the
+        // same heads; the row's exp pairs -- softmax terms, probabilities -- run
+        // one per half; the rest of the loss, dl and the metrics on the low half)
+        {
             float l0 = 0.0f, l1 = 0.0f, vv = 0.0f;
             const float *hr = B.T2 + c * RS;
 #pragma unroll 16
@@ -458,15 +488,20 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
                 l1 = __builtin_fmaf(hk, S.Wp[2 * k + 1], l1);
                 vv = __builtin_fmaf(hk, S.Wv[k], vv);
             }
+            MB_STAMP(9);
             const float lg0 = __fadd_rn(l0, S.bp[0]), lg1 = __fadd_rn(l1, S.bp[1]), v = __fadd_rn(vv, S.bv[0]);
-            const float An = __fdiv_rn(__fsub_rn(A, mean), denom);   // utils.rs:88
             const float mx = lg0 > lg1 ? lg0 : lg1;
-            const float e0 = S.expf(__fsub_rn(lg0, mx));
-            const float e1 = S.expf(__fsub_rn(lg1, mx));
+            const float eh = S.expf(__fsub_rn(h ? lg1 : lg0, mx));
+            const float eo = __shfl_xor(eh, 32, 64);
+            const float e0 = h ? eo : eh, e1 = h ? eh : eo;
             const float lse = S.logf(__fadd_rn(e0, e1));
             const float ls0 = __fsub_rn(__fsub_rn(lg0, mx), lse);
             const float ls1 = __fsub_rn(__fsub_rn(lg1, mx), lse);
-            const float p0 = S.expf(ls0), p1 = S.expf(ls1);
+            const float ph = S.expf(h ? ls1 : ls0);
+            const float po = __shfl_xor(ph, 32, 64);
+            const float p0 = h ? po : ph, p1 = h ? ph : po;
+          if (h == 0) {
+            const float An = __fdiv_rn(__fsub_rn(A, mean), denom);   // utils.rs:88
             const float Hn = -__fadd_rn(__fmul_rn(p0, ls0), __fmul_rn(p1, ls1));
             const float newlp = a == 1 ? ls1 : ls0;
             const float log_ratio = __fsub_rn(newlp, olp);
@@ -506,8 +541,11 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
             }
             gbp0 += dl0; gbp1 += dl1; gbv += dv;
             B.dl[c * 4 + 0] = dl0; B.dl[c * 4 + 1] = dl1; B.dl[c * 4 + 2] = dv; B.dl[c * 4 + 3] = 0.0f;
+          }
         }
         wave_sync();
+        MB_STAMP(10);
+        MB_STAMP(4);
         // ---- head weight gradients dWp, dWv += H2^T [dl | dv] (lane = hidden unit)
 #pragma unroll 4
         for (int q = 0; q < 16; q++) {
@@ -550,6 +588,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
             if ((q & 3) == 3) __builtin_amdgcn_sched_barrier(0);   // bound the LDS read hoisting
         }
         wave_sync();
+        MB_STAMP(5);
         // ---- dZ1 = dZ2 W1^T (32 k-steps) interleaved with dW1 += H1^T dZ2 (16
         // k-steps over row pairs): both operands of every MFMA come from LDS
 #pragma unroll
@@ -574,6 +613,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
             dW1[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, z0, dW1[1][0], 0, 0, 0);
             dW1[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, z1, dW1[1][1], 0, 0, 0);
         }
+        MB_STAMP(6);
         // dZ1 masked by relu'(H1); dW0 and db0 on the VALU (lane = hidden unit)
 #pragma unroll
         for (int q = 0; q < 16; q++) {
@@ -591,6 +631,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
             if ((q & 3) == 3) __builtin_amdgcn_sched_barrier(0);   // bound the LDS read hoisting
         }
         wave_sync();
+        MB_STAMP(7);
     }
     // ---- this wave's partial gradient row (lane halves hold different rows: combine)
 #pragma unroll
@@ -649,6 +690,11 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
         }
         g.slab[(size_t)blockIdx.x * W_ + p] = acc;
     }
+#ifdef BPPO_MB_STAMPS
+    MB_STAMP(8);
+    if (lane == 0)
+        for (int k = 0; k < MB_NSEG; k++) g.stamps[(size_t)gwave * MB_NSEG + k] = st_acc[k];
+#endif
 }
 
 // fixed-order reduction of the wave partials: grad[p] = sum_w slab[w][p], in two
@@ -906,6 +952,13 @@ bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_
     g.inv_mb = (float)(1.0 / (double)n); g.ent_coef = ent_coef; g.value_coef = (float)c->cfg.value_coef;
     g.clip_value = c->cfg.clip_value;
     g.rows = c->d_mbrow;
+    g.stamps = nullptr;
+#ifdef BPPO_MB_STAMPS
+    static unsigned long long *d_st = nullptr;
+    if (!d_st) (void)hipMalloc((void **)&d_st, sizeof(unsigned long long) * 2048 * MB_NSEG);
+    (void)hipMemsetAsync(d_st, 0, sizeof(unsigned long long) * 2048 * MB_NSEG, c->stream);
+    g.stamps = d_st;
+#endif
     int blocks = 256;
     const size_t params_bytes = ((c->net.n_params + 3) & ~(size_t)3) * sizeof(float);
     if (h == 64 && nl == 2 && c->relu_mfma) {
@@ -915,6 +968,24 @@ bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_
         }
         c->slab_used = blocks;
         hipLaunchKernelGGL(k_minibatch_mfma, dim3(blocks), dim3(64 * mmb::WAVES), mmb::LDSB, c->stream, g);
+#ifdef BPPO_MB_STAMPS
+        {   // mean per-wave cycles per segment, accumulated over launches; printed every 16
+            static double acc_s[MB_NSEG] = {};
+            static int nl = 0;
+            std::vector<unsigned long long> h((size_t)blocks * mmb::WAVES * MB_NSEG);
+            (void)hipMemcpyAsync(h.data(), d_st, h.size() * 8, hipMemcpyDeviceToHost, c->stream);
+            (void)hipStreamSynchronize(c->stream);
+            for (size_t w = 0; w < (size_t)blocks * mmb::WAVES; w++)
+                for (int k = 0; k < MB_NSEG; k++) acc_s[k] += (double)h[w * MB_NSEG + k] / (blocks * mmb::WAVES);
+            if (++nl % 16 == 0) {
+                double tot = 0;
+                for (int k = 0; k < MB_NSEG; k++) tot += acc_s[k];
+                fprintf(stderr, "[mbstamp] launches=%d cycles/wave=%.0f shares:", nl, tot / nl);
+                for (int k = 0; k < MB_NSEG; k++) fprintf(stderr, " s%d=%.3f", k, acc_s[k] / tot);
+                fprintf(stderr, "\n");
+            }
+        }
+#endif
     } else
 #define L(H_, NL_)                                                                                 \
     if (h == H_ && nl == NL_) {                                                                     \
