@@ -16,8 +16,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "burn-ppo_amd"))
 
 WORKLOADS = {
-    # configs/connect_four.toml at num_envs=16384, T=128 (opponent pool off), 6 epochs x 4 minibatches
-    "cfgC": dict(preset="connect_four", num_envs=16384, num_steps=128),
+    # configs/connect_four.toml at num_envs=16384, T=64 (opponent pool off), 6 epochs x 4 minibatches
+    "cfgC": dict(preset="connect_four", num_envs=16384, num_steps=64),
     # configs/liars_dice_ctde.toml at num_envs=32768, T=128, 4 epochs x 8 minibatches
     "cfgD": dict(preset="liars_dice_ctde", num_envs=32768, num_steps=128),
 }
