@@ -15,7 +15,10 @@ LIB_PATH = os.environ.get("BPPO_LIB_PATH") or os.path.join(HERE, "libbppo.so")
 
 OK, ERR_ARG, ERR_NONFINITE, ERR_EMPTY_MASK, ERR_HIP, ERR_COMM, ERR_UNSUPPORTED = range(7)
 ENV_CARTPOLE, ENV_CONNECT_FOUR, ENV_LIARS_DICE = 0, 1, 2
-ENV_KINDS = {"cartpole": ENV_CARTPOLE, "connect_four": ENV_CONNECT_FOUR, "liars_dice": ENV_LIARS_DICE}
+ENV_SKULL = 3
+ENV_KINDS = {"cartpole": ENV_CARTPOLE, "connect_four": ENV_CONNECT_FOUR, "liars_dice": ENV_LIARS_DICE,
+             "skull": ENV_SKULL}
+MAX_PLAYERS = 6
 
 
 class BppoError(RuntimeError):
@@ -37,11 +40,11 @@ class Config(C.Structure):
                 ("rng_stream", C.c_uint64),
                 ("cnn", C.c_int32), ("num_conv_layers", C.c_int32), ("conv_channels", C.c_int32 * 4),
                 ("kernel_size", C.c_int32), ("cnn_fc_hidden_size", C.c_int32), ("cnn_num_fc_layers", C.c_int32),
-                ("normalize_values", C.c_int32)]
+                ("normalize_values", C.c_int32), ("player_count", C.c_int32)]
 
 
 class Episode(C.Structure):
-    _fields_ = [("total_reward", C.c_float * 4), ("length", C.c_int32), ("env_index", C.c_int32),
+    _fields_ = [("total_reward", C.c_float * MAX_PLAYERS), ("length", C.c_int32), ("env_index", C.c_int32),
                 ("step", C.c_int32), ("pad", C.c_int32)]
 
 

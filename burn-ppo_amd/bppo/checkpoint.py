@@ -166,9 +166,8 @@ class CheckpointMetadata:
     @classmethod
     def for_config(cls, cfg, step, avg_return, recent_returns=(), best_avg_return=None, forked_from=None):
         """the metadata run_training writes (main.rs:451-476, 1245-1271)"""
-        obs = {"cartpole": 5, "connect_four": 86, "liars_dice": 270}[cfg["env"]]
-        act = {"cartpole": 2, "connect_four": 7, "liars_dice": 49}[cfg["env"]]
-        P = {"cartpole": 1, "connect_four": 2, "liars_dice": 4}[cfg["env"]]
+        from .host import ENV_DIMS
+        obs, act, P, priv = ENV_DIMS[cfg["env"]]
         ctde = cfg["network_type"] == "ctde"
         cnn = {}
         if cfg["network_type"] == "cnn":
@@ -180,11 +179,10 @@ class CheckpointMetadata:
                    best_avg_return=best_avg_return, recent_returns=[float(x) for x in recent_returns],
                    forked_from=forked_from, obs_dim=obs, action_count=act, num_players=P,
                    hidden_size=cfg["hidden_size"], num_hidden=cfg["num_hidden"], activation=cfg["activation"],
-                   network_type=cfg["network_type"], privileged_obs_dim=120 if ctde else None,
+                   network_type=cfg["network_type"], privileged_obs_dim=priv if ctde else None,
                    critic_hidden_size=cfg["critic_hidden_size"] if ctde else cfg.get("critic_hidden_size"),
                    critic_num_hidden=cfg["critic_num_hidden"] if ctde else cfg.get("critic_num_hidden"),
-                   env_name={"cartpole": "cartpole", "connect_four": "connect_four",
-                             "liars_dice": "liars_dice"}[cfg["env"]])
+                   env_name=cfg["env"])
 
 
 def load_metadata(ckpt_dir):

@@ -35,13 +35,18 @@ def schedule_get(points, step):
     return float(points[-1][0])
 
 
+# Environment constants: OBSERVATION_DIM, ACTION_COUNT, NUM_PLAYERS, PRIVILEGED_OBS_DIM
+# (cartpole.rs, connect_four.rs, liars_dice.rs:455-460, skull.rs:1046-1060)
+ENV_DIMS = {"cartpole": (5, 2, 1, 0), "connect_four": (86, 7, 2, 0), "liars_dice": (270, 49, 4, 120),
+            "skull": (135, 33, 6, 200)}
+
 # config presets = the reference's configs + BASELINE.json sizes (SURVEY.md CfgA..CfgE)
 BASE = dict(env="cartpole", num_envs=32, num_steps=128, hidden_size=64, num_hidden=2, activation="relu",
             network_type="mlp", critic_hidden_size=None, critic_num_hidden=None, num_epochs=4,
             num_minibatches=4, normalize_obs=False, normalize_returns=None, clip_value=False, gamma=0.99,
             gae_lambda=0.95, clip_epsilon=0.2, value_coef=0.5, max_grad_norm=0.5, adam_epsilon=1e-5,
             target_kl=None, return_clip=10.0, reward_shaping_coef=0.0, learning_rate=[(2.5e-4, 0)],
-            entropy_coef=[(0.01, 0)], seed=42,
+            entropy_coef=[(0.01, 0)], seed=42, player_count=4,
             # network_type = "cnn" (config.rs:996-1010 defaults)
             num_conv_layers=2, conv_channels=[8, 8], kernel_size=3, cnn_fc_hidden_size=32, cnn_num_fc_layers=1)
 
@@ -62,6 +67,16 @@ PRESETS = {
                             learning_rate=[(3e-4, 0)], gamma=0.97, gae_lambda=0.90,
                             entropy_coef=[(0.05, 0)], value_coef=1.0, target_kl=0.025, num_epochs=4,
                             num_minibatches=8),
+    # configs/skull.toml / skull_ctde.toml ([player_count] Fixed 4)
+    "skull": dict(env="skull", num_envs=128, num_steps=128, hidden_size=256, num_hidden=3,
+                  learning_rate=[(1e-3, 0), (3e-4, 80_000_000), (0.0, 100_000_000)], gamma=0.99, gae_lambda=0.9,
+                  clip_epsilon=0.1, entropy_coef=[(0.05, 0)], value_coef=0.5, target_kl=0.02, num_epochs=4,
+                  num_minibatches=8),
+    "skull_ctde": dict(env="skull", num_envs=128, num_steps=128, network_type="ctde", hidden_size=256,
+                       num_hidden=3, critic_hidden_size=256, critic_num_hidden=3,
+                       learning_rate=[(1e-3, 0), (3e-4, 80_000_000), (0.0, 100_000_000)], gamma=0.99,
+                       gae_lambda=0.9, clip_epsilon=0.1, entropy_coef=[(0.05, 0)], value_coef=0.5, target_kl=0.02,
+                       num_epochs=4, num_minibatches=8),
 }
 
 
@@ -73,7 +88,7 @@ def make_config(preset="cartpole", **over):
 
 
 def num_players(env):
-    return {"cartpole": 1, "connect_four": 2, "liars_dice": 4}[env]
+    return ENV_DIMS[env][2]
 
 
 def to_struct(c, rank=0, world=1, envs_per_rank=None):
@@ -104,6 +119,7 @@ def to_struct(c, rank=0, world=1, envs_per_rank=None):
     s.target_kl = -1.0 if c["target_kl"] is None else float(c["target_kl"])
     s.seed = c["seed"]
     s.normalize_values = int(bool(c.get("normalize_values", False)))
+    s.player_count = int(c.get("player_count", 4)) if c["env"] == "skull" else 0
     s.cnn = int(c["network_type"] == "cnn")
     if s.cnn:
         s.num_conv_layers = c["num_conv_layers"]
@@ -130,8 +146,7 @@ def layer_shapes(c):
     """Burn record order: hidden..., policy head, value head (MLP) /
     actor hidden..., policy, critic hidden..., value (CTDE) /
     conv layers (as (Cin*k*k, Cout)), FC layers, policy, value (CNN)."""
-    obs = {"cartpole": 5, "connect_four": 86, "liars_dice": 270}[c["env"]]
-    act = {"cartpole": 2, "connect_four": 7, "liars_dice": 49}[c["env"]]
+    obs, act, _, priv = ENV_DIMS[c["env"]]
     shapes, gains = [], []
     hg = np.sqrt(2.0) if c["activation"] == "relu" else 1.0
     i = obs
@@ -152,7 +167,7 @@ def layer_shapes(c):
         shapes.append((i, c["hidden_size"])); gains.append(hg); i = c["hidden_size"]
     shapes.append((i, act)); gains.append(0.01)
     if c["network_type"] == "ctde":
-        ci = 120 + obs
+        ci = priv + obs
         for _ in range(c["critic_num_hidden"] or c["num_hidden"]):
             w = c["critic_hidden_size"] or c["hidden_size"]
             shapes.append((ci, w)); gains.append(hg); ci = w

@@ -21,7 +21,7 @@ from collections import deque
 import numpy as np
 
 from . import _lib as L
-from .host import make_config, orthogonal_init, schedule_get, shaping_schedule, to_struct
+from .host import ENV_DIMS, make_config, orthogonal_init, schedule_get, shaping_schedule, to_struct
 
 
 class Context:
@@ -45,11 +45,11 @@ class Context:
         if len(sched) != 1 or sched[0][1] != 0:
             self.set_reward_shaping_schedule(sched)
         self.n_params = L.lib().bppo_num_params(self.h)
-        self.obs_dim = {"cartpole": 5, "connect_four": 86, "liars_dice": 270}[cfg["env"]]
-        self.num_actions = {"cartpole": 2, "connect_four": 7, "liars_dice": 49}[cfg["env"]]
-        self.num_players = {"cartpole": 1, "connect_four": 2, "liars_dice": 4}[cfg["env"]]
-        # liars_dice.rs:459; the device keeps privileged rows only for CTDE nets
-        self.priv_dim = 120 if cfg["env"] == "liars_dice" and cfg["network_type"] == "ctde" else 0
+        self.obs_dim, self.num_actions, self.num_players, priv = ENV_DIMS[cfg["env"]]
+        # the device keeps privileged rows only for CTDE nets
+        self.priv_dim = priv if cfg["network_type"] == "ctde" else 0
+        # seated players (opponent-pool seat tables): Skull's player_count, else NUM_PLAYERS
+        self.seats = int(cfg.get("player_count", 4)) if cfg["env"] == "skull" else self.num_players
         self.has_masks = cfg["env"] != "cartpole"
         self._ar_keep = None
 
@@ -132,7 +132,7 @@ class Context:
         [0, num_opponent_envs) (EnvState, opponent_pool.rs:80-124), current_opp
         [P - 1] = OpponentPool::sample_all_slots."""
         params = np.ascontiguousarray(params, np.float32).reshape(-1, self.n_params)
-        K, D, P = params.shape[0], self.obs_dim, self.num_players
+        K, D, P = params.shape[0], self.obs_dim, self.seats
         mean = np.zeros((max(K, 1), D)); m2 = np.zeros((max(K, 1), D)); cnt = np.zeros(max(K, 1))
         for k, nm in enumerate(norms or []):
             if nm is not None:
@@ -148,9 +148,9 @@ class Context:
     def opponent_envs(self):
         """-> (learner_pos [n_opp], pos_to_opp [n_opp, P]) after the last rollout"""
         n = getattr(self, "_n_opp", 0)
-        lp = np.zeros(max(n, 1), np.int32); po = np.zeros(max(n, 1) * self.num_players, np.int32)
+        lp = np.zeros(max(n, 1), np.int32); po = np.zeros(max(n, 1) * self.seats, np.int32)
         self._chk(L.lib().bppo_opponents_get_envs(self.h, lp.ctypes.data, po.ctypes.data))
-        return lp[:n], po[:n * self.num_players].reshape(n, self.num_players)
+        return lp[:n], po[:n * self.seats].reshape(n, self.seats)
 
     def kernel_ms(self, name):
         f = C.c_float()
@@ -214,7 +214,7 @@ class VecEnv:
         return m.astype(bool)
 
     def get_privileged_obs(self):
-        """env.rs:365-376: [N*120] for Liar's Dice, None otherwise."""
+        """env.rs:365-376: [N*G] (Liar's Dice 120, Skull 200) for CTDE contexts, None otherwise."""
         if not self.ctx.priv_dim:
             return None
         g = np.zeros(self.ctx.N * self.ctx.priv_dim, np.float32)
@@ -262,7 +262,7 @@ class ActorCritic:
 
     def forward(self, obs, priv=None):
         """network/mod.rs:93-114 (MLP) / forward_actor + forward_critic (CTDE, ctde.rs:132-183)
-        -> (logits [B, A], values [B, 1]); priv [B, 120] is required for CTDE."""
+        -> (logits [B, A], values [B, 1]); priv [B, G] is required for CTDE."""
         obs = np.ascontiguousarray(obs, np.float32).reshape(-1, self.ctx.obs_dim)
         B = obs.shape[0]
         pr = None

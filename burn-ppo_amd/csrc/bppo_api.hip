@@ -137,7 +137,13 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     case BPPO_ENV_CARTPOLE: c->D = 5; c->A = 2; c->P = 1; c->G = 0; break;
     case BPPO_ENV_CONNECT_FOUR: c->D = 86; c->A = 7; c->P = 2; c->G = 0; break;
     case BPPO_ENV_LIARS_DICE: c->D = 270; c->A = 49; c->P = 4; c->G = cfg->ctde ? 120 : 0; break;
+    case BPPO_ENV_SKULL: c->D = 135; c->A = 33; c->P = 6; c->G = cfg->ctde ? 200 : 0; break;   // skull.rs:1046-1060
     default: c->err = "unknown env_kind"; return BPPO_ERR_ARG;
+    }
+    c->Pa = c->P;
+    if (cfg->env_kind == BPPO_ENV_SKULL) {
+        c->Pa = cfg->player_count ? cfg->player_count : 4;          // PlayerCountMode::default (config.rs:667-671)
+        if (c->Pa < 2 || c->Pa > 6) { c->err = "Skull supports 2-6 players"; return BPPO_ERR_ARG; }   // skull.rs:159-162
     }
     c->wide = cfg->env_kind != BPPO_ENV_CARTPOLE;
     if (c->wide && !cfg->ctde) c->G = 0;
@@ -420,7 +426,7 @@ extern "C" bppo_status bppo_vecenv_step(bppo_ctx *c, const int32_t *actions, flo
             std::sort(recs.begin(), recs.end(), [](const EpisodeRec &a, const EpisodeRec &b) {
                 return a.env_index < b.env_index; });
             for (int i = 0; i < (int)recs.size() && i < cap; i++) {
-                std::memcpy(eps[i].total_reward, recs[i].total_reward, sizeof(float) * 4);
+                std::memcpy(eps[i].total_reward, recs[i].total_reward, sizeof(float) * BPPO_MAX_PLAYERS);
                 eps[i].length = recs[i].length; eps[i].env_index = recs[i].env_index;
                 eps[i].step = recs[i].step; eps[i].pad = 0;
             }
@@ -445,7 +451,7 @@ extern "C" bppo_status bppo_vecenv_step(bppo_ctx *c, const int32_t *actions, flo
         std::sort(recs.begin(), recs.end(), [](const EpisodeRec &a, const EpisodeRec &b) {
             return a.env_index < b.env_index; });
         for (int i = 0; i < (int)recs.size() && i < cap; i++) {
-            std::memcpy(eps[i].total_reward, recs[i].total_reward, sizeof(float) * 4);
+            std::memcpy(eps[i].total_reward, recs[i].total_reward, sizeof(float) * BPPO_MAX_PLAYERS);
             eps[i].length = recs[i].length; eps[i].env_index = recs[i].env_index;
             eps[i].step = recs[i].step; eps[i].pad = 0;
         }
@@ -570,6 +576,7 @@ extern "C" bppo_status bppo_collect_rollouts(bppo_ctx *c, bppo_rollout_info *inf
     if (hv[1] & 2) { c->err = "Empty action mask: an env has no valid action"; return BPPO_ERR_EMPTY_MASK; }
     if (hv[1] & 1) { c->err = "NaN/Inf in log probs — model producing corrupt logits"; return BPPO_ERR_NONFINITE; }
     if (hv[1] & 4) { c->err = "opponent pool: pos_to_opp names a model index outside [0, n_models)"; return BPPO_ERR_ARG; }
+    if (hv[1] & 8) { c->err = "Invalid action: outside the env's action mask"; return BPPO_ERR_ARG; }   // skull.rs:1116-1128
     if (hv[1]) { c->err = "collect_rollouts: unknown device error flag"; return BPPO_ERR_HIP; }
     if (info) {
         info->episodes = hv[0];
@@ -602,7 +609,7 @@ extern "C" bppo_status bppo_rollout_episodes(bppo_ctx *c, bppo_episode *eps, int
     std::sort(recs.begin(), recs.end(), [](const EpisodeRec &a, const EpisodeRec &b) {
         return a.step != b.step ? a.step < b.step : a.env_index < b.env_index; });
     for (int i = 0; i < m && i < cap; i++) {
-        std::memcpy(eps[i].total_reward, recs[i].total_reward, sizeof(float) * 4);
+        std::memcpy(eps[i].total_reward, recs[i].total_reward, sizeof(float) * BPPO_MAX_PLAYERS);
         eps[i].length = recs[i].length; eps[i].env_index = recs[i].env_index;
         eps[i].step = recs[i].step; eps[i].pad = 0;
     }
@@ -903,7 +910,7 @@ extern "C" bppo_status bppo_gae_mp_device(const float *ar, const int32_t *pl, co
                                           const float *v, const float *lvpp, int32_t T, int32_t N,
                                           int32_t P, float gamma, float lambda, float *adv, float *ret,
                                           void *stream) {
-    if (!ar || !pl || !d || !v || !lvpp || !adv || !ret || T < 0 || N < 0 || P < 1 || P > 4)
+    if (!ar || !pl || !d || !v || !lvpp || !adv || !ret || T < 0 || N < 0 || P < 1 || P > BPPO_MAX_PLAYERS)
         return BPPO_ERR_ARG;
     return launch_gae_mp(ar, pl, d, v, lvpp, T, N, P, gamma, lambda, adv, ret, (hipStream_t)stream);
 }

@@ -36,7 +36,7 @@ NetLayout make_layout(const bppo_config &c, int obs_dim, int priv_dim, int act_d
 
 // episode record written by the rollout kernel
 struct EpisodeRec {
-    float total_reward[4];
+    float total_reward[BPPO_MAX_PLAYERS];
     int32_t length, env_index, step, pad;
 };
 
@@ -177,6 +177,7 @@ struct bppo_ctx {
     bool own_stream = false;
     std::string err;
     int N = 0, T = 0, D = 0, A = 0, P = 1, G = 0;
+    int Pa = 1;                       // players actually seated (Skull: player_count; else P)
     bppo::NetLayout net;
     // parameters + Adam
     float *d_params = nullptr, *d_m1 = nullptr, *d_m2 = nullptr;

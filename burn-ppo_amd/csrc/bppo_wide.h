@@ -25,6 +25,7 @@ struct WideStepArgs {
     EpisodeRec *eps;
     int32_t *ep_count;
     int eps_cap;
+    int32_t *err;        // bit 3: an action outside the env's mask (Skull panics, skull.rs:1113-1128)
 };
 
 struct SampleArgs {
@@ -65,8 +66,9 @@ struct LossArgs {
     int clip_value;
 };
 
-hipError_t wide_env_reset(int kind, hipStream_t st, int N, uint64_t seed_base, void *state, uint64_t *env_pos,
-                          float *ep_ret, int32_t *ep_len);
+// players: Skull's num_players (new_with_players, main.rs:2008-2014)
+hipError_t wide_env_reset(int kind, hipStream_t st, int N, uint64_t seed_base, int players, void *state,
+                          uint64_t *env_pos, float *ep_ret, int32_t *ep_len);
 // rows [priv | obs] when with_priv (CTDE), [obs] otherwise
 hipError_t wide_env_observe(int kind, int with_priv, hipStream_t st, int N, const void *state, float *xc,
                             uint8_t *mask, int32_t *players);

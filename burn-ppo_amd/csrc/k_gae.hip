@@ -209,6 +209,8 @@ bppo_status launch_gae_mp(const float *ar, const int32_t *pl, const float *d, co
     case 2: hipLaunchKernelGGL(k_gae_mp<2>, g, b, 0, s, ar, pl, d, v, lvpp, T, N, gamma, lambda, adv, ret); break;
     case 3: hipLaunchKernelGGL(k_gae_mp<3>, g, b, 0, s, ar, pl, d, v, lvpp, T, N, gamma, lambda, adv, ret); break;
     case 4: hipLaunchKernelGGL(k_gae_mp<4>, g, b, 0, s, ar, pl, d, v, lvpp, T, N, gamma, lambda, adv, ret); break;
+    case 5: hipLaunchKernelGGL(k_gae_mp<5>, g, b, 0, s, ar, pl, d, v, lvpp, T, N, gamma, lambda, adv, ret); break;
+    case 6: hipLaunchKernelGGL(k_gae_mp<6>, g, b, 0, s, ar, pl, d, v, lvpp, T, N, gamma, lambda, adv, ret); break;
     default: return BPPO_ERR_ARG;
     }
     return hipGetLastError() == hipSuccess ? BPPO_OK : BPPO_ERR_HIP;

@@ -182,8 +182,8 @@ __global__ void __launch_bounds__(256) k_cartpole_rollout(RolloutArgs a) {
             int32_t k = atomicAdd(a.ep_count, 1);
             if (k < a.eps_cap) {
                 EpisodeRec rec;
-                rec.total_reward[0] = ep_ret; rec.total_reward[1] = rec.total_reward[2] =
-                    rec.total_reward[3] = 0.0f;
+                rec.total_reward[0] = ep_ret;
+                for (int p = 1; p < BPPO_MAX_PLAYERS; p++) rec.total_reward[p] = 0.0f;
                 rec.length = ep_len; rec.env_index = e; rec.step = t; rec.pad = 0;
                 a.eps[k] = rec;
             }
@@ -346,8 +346,8 @@ __global__ void __launch_bounds__(512, 2) k_cartpole_rollout_mfma(RolloutArgs a,
                 const int32_t k = atomicAdd(a.ep_count, 1);
                 if (k < a.eps_cap) {
                     EpisodeRec rec;
-                    rec.total_reward[0] = ep_ret; rec.total_reward[1] = rec.total_reward[2] =
-                        rec.total_reward[3] = 0.0f;
+                    rec.total_reward[0] = ep_ret;
+                    for (int p = 1; p < BPPO_MAX_PLAYERS; p++) rec.total_reward[p] = 0.0f;
                     rec.length = ep_len; rec.env_index = e; rec.step = t; rec.pad = 0;
                     a.eps[k] = rec;
                 }
@@ -390,7 +390,8 @@ __global__ void k_cartpole_step(int N, uint64_t seed_base, float *cp, int32_t *s
         int32_t k = atomicAdd(ep_count, 1);
         if (k < cap) {
             EpisodeRec rec;
-            rec.total_reward[0] = er; rec.total_reward[1] = rec.total_reward[2] = rec.total_reward[3] = 0;
+            rec.total_reward[0] = er;
+            for (int p = 1; p < BPPO_MAX_PLAYERS; p++) rec.total_reward[p] = 0.0f;
             rec.length = el; rec.env_index = e; rec.step = 0; rec.pad = 0;
             eps[k] = rec;
         }

@@ -14,12 +14,12 @@ template <int ENV> struct EnvT;
 template <> struct EnvT<BPPO_ENV_CONNECT_FOUR> {
     using S = C4State;
     static constexpr int D = C4_OBS, A = C4_ACT, P = 2, G = 0;
-    __device__ static void reset_new(S &s, const Key8 &, uint64_t &) { c4_reset(s); }   // new() ignores the seed
+    __device__ static void reset_new(S &s, const Key8 &, uint64_t &, int) { c4_reset(s); }   // new() ignores the seed
     __device__ static void reset(S &s, const Key8 &, uint64_t &) { c4_reset(s); }
     __device__ static int player(const S &s) { return s.cur - 1; }
-    __device__ static void step(S &s, int a, float, float r[4], int &done, const Key8 &, uint64_t &) {
+    __device__ static void step(S &s, int a, float, float r[BPPO_MAX_PLAYERS], int &done, int &, const Key8 &,
+                                uint64_t &) {
         c4_step(s, a, r, done);
-        r[2] = r[3] = 0.0f;
     }
     __device__ static void obs(const S &s, float *row) { c4_obs(s, row); }
     __device__ static void priv(const S &, float *) {}
@@ -29,7 +29,7 @@ template <> struct EnvT<BPPO_ENV_LIARS_DICE> {
     using S = LDState;
     static constexpr int D = LD_OBS, A = LD_ACT, P = 4, G = LD_PRIV;
     // VecEnv::new: new_with_config rolls once, reset() rolls again (liars_dice.rs:186, 476)
-    __device__ static void reset_new(S &s, const Key8 &k, uint64_t &pos) {
+    __device__ static void reset_new(S &s, const Key8 &k, uint64_t &pos, int) {
         WordCursor c; c.init(k, 0, 0);
         ld_new(s, c);
         ld_reset(s, c);
@@ -41,7 +41,8 @@ template <> struct EnvT<BPPO_ENV_LIARS_DICE> {
         pos = c.pos;
     }
     __device__ static int player(const S &s) { return s.current; }
-    __device__ static void step(S &s, int a, float shaping, float r[4], int &done, const Key8 &k, uint64_t &pos) {
+    __device__ static void step(S &s, int a, float shaping, float r[BPPO_MAX_PLAYERS], int &done, int &,
+                                const Key8 &k, uint64_t &pos) {
         WordCursor c; c.init(k, 0, pos);
         ld_step(s, a, shaping, r, done, c);
         pos = c.pos;
@@ -49,6 +50,23 @@ template <> struct EnvT<BPPO_ENV_LIARS_DICE> {
     __device__ static void obs(const S &s, float *row) { ld_obs(s, row); }
     __device__ static void priv(const S &s, float *row) { ld_priv(s, row); }
     __device__ static void mask(const S &s, uint8_t *m) { ld_mask(s, m); }
+};
+template <> struct EnvT<BPPO_ENV_SKULL> {
+    using S = SKState;
+    static constexpr int D = SK_OBS, A = SK_ACT, P = SK_P, G = SK_PRIV;
+    // VecEnv::new: new_with_players(n, shaping, seed + i) then reset(); neither draws
+    __device__ static void reset_new(S &s, const Key8 &, uint64_t &pos, int players) { sk_reset(s, players); pos = 0; }
+    __device__ static void reset(S &s, const Key8 &, uint64_t &) { sk_reset(s, s.n); }
+    __device__ static int player(const S &s) { return s.current; }
+    __device__ static void step(S &s, int a, float shaping, float r[BPPO_MAX_PLAYERS], int &done, int &bad,
+                                const Key8 &k, uint64_t &pos) {
+        WordCursor c; c.init(k, 0, pos);
+        sk_step(s, a, shaping, r, done, bad, c);
+        pos = c.pos;
+    }
+    __device__ static void obs(const S &s, float *row) { sk_obs(s, row); }
+    __device__ static void priv(const S &s, float *row) { sk_priv(s, row); }
+    __device__ static void mask(const S &s, uint8_t *m) { sk_mask(s, m); }
 };
 
 template <int ENV>
@@ -58,7 +76,7 @@ __device__ __forceinline__ typename EnvT<ENV>::S *env_state(void *base) {
 
 // VecEnv::new (env.rs:281-302): factory(seed_base + i) then reset()
 template <int ENV>
-__global__ void k_wide_reset(int N, uint64_t seed_base, void *state, uint64_t *env_pos, float *ep_ret,
+__global__ void k_wide_reset(int N, uint64_t seed_base, int players, void *state, uint64_t *env_pos, float *ep_ret,
                              int32_t *ep_len) {
     using E = EnvT<ENV>;
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -66,7 +84,7 @@ __global__ void k_wide_reset(int N, uint64_t seed_base, void *state, uint64_t *e
     typename E::S s;
     uint64_t pos = 0;
     const Key8 k = seed_key(seed_base + (uint64_t)e);
-    E::reset_new(s, k, pos);
+    E::reset_new(s, k, pos, players);
     env_state<ENV>(state)[e] = s;
     env_pos[e] = pos;
     for (int p = 0; p < E::P; p++) ep_ret[(size_t)e * E::P + p] = 0.0f;
@@ -114,9 +132,10 @@ __global__ void k_wide_step(WideStepArgs a) {
     const int p_act = E::player(s);
     const Key8 k = seed_key(a.seed_base + (uint64_t)e);
     uint64_t pos = a.env_pos[e];
-    float r[4] = {0, 0, 0, 0};
-    int done = 0;
-    E::step(s, act, a.shaping, r, done, k, pos);
+    float r[BPPO_MAX_PLAYERS] = {0, 0, 0, 0, 0, 0};
+    int done = 0, bad = 0;
+    E::step(s, act, a.shaping, r, done, bad, k, pos);
+    if (bad && a.err) atomicOr(a.err, 8);
     float *er = a.ep_ret + (size_t)e * E::P;
     for (int p = 0; p < E::P; p++) {
         er[p] = __fadd_rn(er[p], r[p]);
@@ -130,7 +149,7 @@ __global__ void k_wide_step(WideStepArgs a) {
         const int slot = atomicAdd(a.ep_count, 1);
         if (slot < a.eps_cap) {
             EpisodeRec rec;
-            for (int p = 0; p < 4; p++) rec.total_reward[p] = p < E::P ? er[p] : 0.0f;
+            for (int p = 0; p < BPPO_MAX_PLAYERS; p++) rec.total_reward[p] = p < E::P ? er[p] : 0.0f;
             rec.length = len; rec.env_index = e; rec.step = a.t; rec.pad = 0;
             a.eps[slot] = rec;
         }
@@ -343,13 +362,16 @@ __global__ void __launch_bounds__(64) k_wide_metric_reduce(const double *part, i
     do {                                                                                    \
         if ((kind) == BPPO_ENV_CONNECT_FOUR)                                                \
             hipLaunchKernelGGL(KERNEL<BPPO_ENV_CONNECT_FOUR>, grid, block, 0, st, __VA_ARGS__); \
+        else if ((kind) == BPPO_ENV_SKULL)                                                  \
+            hipLaunchKernelGGL(KERNEL<BPPO_ENV_SKULL>, grid, block, 0, st, __VA_ARGS__);       \
         else                                                                                \
             hipLaunchKernelGGL(KERNEL<BPPO_ENV_LIARS_DICE>, grid, block, 0, st, __VA_ARGS__);  \
     } while (0)
 
-hipError_t wide_env_reset(int kind, hipStream_t st, int N, uint64_t seed_base, void *state, uint64_t *env_pos,
-                          float *ep_ret, int32_t *ep_len) {
-    ENV_DISPATCH(kind, k_wide_reset, dim3((N + 255) / 256), dim3(256), N, seed_base, state, env_pos, ep_ret, ep_len);
+hipError_t wide_env_reset(int kind, hipStream_t st, int N, uint64_t seed_base, int players, void *state,
+                          uint64_t *env_pos, float *ep_ret, int32_t *ep_len) {
+    ENV_DISPATCH(kind, k_wide_reset, dim3((N + 255) / 256), dim3(256), N, seed_base, players, state, env_pos, ep_ret,
+                 ep_len);
     return hipGetLastError();
 }
 
@@ -358,6 +380,10 @@ hipError_t wide_env_observe(int kind, int with_priv, hipStream_t st, int N, cons
     const dim3 grid((N + 63) / 64), block(64);
     if (kind == BPPO_ENV_CONNECT_FOUR)
         hipLaunchKernelGGL((k_wide_observe<BPPO_ENV_CONNECT_FOUR, false>), grid, block, 0, st, N, state, xc, mask, players);
+    else if (kind == BPPO_ENV_SKULL && with_priv)
+        hipLaunchKernelGGL((k_wide_observe<BPPO_ENV_SKULL, true>), grid, block, 0, st, N, state, xc, mask, players);
+    else if (kind == BPPO_ENV_SKULL)
+        hipLaunchKernelGGL((k_wide_observe<BPPO_ENV_SKULL, false>), grid, block, 0, st, N, state, xc, mask, players);
     else if (with_priv)
         hipLaunchKernelGGL((k_wide_observe<BPPO_ENV_LIARS_DICE, true>), grid, block, 0, st, N, state, xc, mask, players);
     else
@@ -375,6 +401,7 @@ hipError_t wide_sample(int A, hipStream_t st, const SampleArgs &g) {
     if (A == 2) hipLaunchKernelGGL(k_sample_masked<2>, grid, block, 0, st, g);   // CartPole (bppo_debug_sample)
     else if (A == C4_ACT) hipLaunchKernelGGL(k_sample_masked<C4_ACT>, grid, block, 0, st, g);
     else if (A == LD_ACT) hipLaunchKernelGGL(k_sample_masked<LD_ACT>, grid, block, 0, st, g);
+    else if (A == SK_ACT) hipLaunchKernelGGL(k_sample_masked<SK_ACT>, grid, block, 0, st, g);
     else return hipErrorInvalidValue;
     return hipGetLastError();
 }
@@ -402,6 +429,7 @@ hipError_t wide_pack_heads(hipStream_t st, const float *params, int K, int A, si
 hipError_t wide_loss(int A, hipStream_t st, const LossArgs &g, int blocks, float *metrics_out) {
     if (A == C4_ACT) hipLaunchKernelGGL(k_wide_loss<C4_ACT>, dim3(blocks), dim3(256), 0, st, g);
     else if (A == LD_ACT) hipLaunchKernelGGL(k_wide_loss<LD_ACT>, dim3(blocks), dim3(256), 0, st, g);
+    else if (A == SK_ACT) hipLaunchKernelGGL(k_wide_loss<SK_ACT>, dim3(blocks), dim3(256), 0, st, g);
     else return hipErrorInvalidValue;
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -413,6 +441,6 @@ hipError_t wide_loss(int A, hipStream_t st, const LossArgs &g, int blocks, float
 
 namespace bppo {
 size_t wide_state_bytes(int kind) {
-    return kind == BPPO_ENV_CONNECT_FOUR ? sizeof(C4State) : sizeof(LDState);
+    return kind == BPPO_ENV_CONNECT_FOUR ? sizeof(C4State) : kind == BPPO_ENV_SKULL ? sizeof(SKState) : sizeof(LDState);
 }
 }  // namespace bppo

@@ -189,7 +189,7 @@ __global__ void __launch_bounds__(SEAT_THREADS) k_opp_seats(int N, int n_opp, in
                 for (; q < nd && c.pos + SEAT_MARGIN <= c.end; q++) {
                     const int e = list[q];
                     const int lp = (int)dev_range_u64(c, (uint64_t)P);        // opponent_pool.rs:109
-                    int other[4], no = 0;
+                    int other[BPPO_MAX_PLAYERS], no = 0;
                     for (int p = 0; p < P; p++) if (p != lp) other[no++] = p;
                     for (int i = no - 1; i >= 1; i--) {                          // :114-115 SliceRandom::shuffle
                         const int j = (int)dev_range_u32(c, (uint32_t)(i + 1));
@@ -292,7 +292,7 @@ bppo_status opp_step_group(bppo_ctx *c, int t) {
     const size_t r0 = (size_t)t * c->N;
     BPPO_HIP(c, hipMemcpyAsync(c->d_oraw, c->d_xc + r0 * c->L, sizeof(float) * (size_t)c->N * c->L,
                                hipMemcpyDeviceToDevice, c->stream));
-    hipLaunchKernelGGL(k_opp_group, dim3(1), dim3(OG_THREADS), 0, c->stream, c->N, c->n_opp, c->P, c->opp_K + 1,
+    hipLaunchKernelGGL(k_opp_group, dim3(1), dim3(OG_THREADS), 0, c->stream, c->N, c->n_opp, c->Pa, c->opp_K + 1,
                        c->d_players + r0, c->d_lpos, c->d_p2o, c->d_group, c->d_gpos, c->d_gbase, c->d_err);
     BPPO_HIP(c, hipGetLastError());
     // the per-model row counts size the opponents' GEMMs: one small read per step
@@ -331,7 +331,7 @@ bppo_status opp_step_forwards(bppo_ctx *c) {
 
 bppo_status opp_step_seats(bppo_ctx *c, int t) {
     const size_t r0 = (size_t)t * c->N;
-    hipLaunchKernelGGL(k_opp_seats, dim3(1), dim3(SEAT_THREADS), 0, c->stream, c->N, c->n_opp, c->P, c->A, c->d_done + r0,
+    hipLaunchKernelGGL(k_opp_seats, dim3(1), dim3(SEAT_THREADS), 0, c->stream, c->N, c->n_opp, c->Pa, c->A, c->d_done + r0,
                        c->d_players + r0, c->rng_key, (uint64_t)c->cfg.rng_stream, c->d_curopp, c->d_rngpos,
                        c->d_lpos, c->d_p2o, c->d_valid + r0);
     BPPO_HIP(c, hipGetLastError());
@@ -380,7 +380,7 @@ extern "C" bppo_status bppo_opponents_set(bppo_ctx *c, int32_t n_models, const f
         c->err = "opponent pool: models and seat state required";
         return BPPO_ERR_ARG;
     }
-    const int P = c->P, D = c->D;
+    const int P = c->Pa, D = c->D;   // EnvState seats: the active player count (main.rs:552, 649)
     const size_t np = c->net.n_params;
     if (num_opponent_envs > 0) {
         for (int e = 0; e < num_opponent_envs; e++) {
@@ -437,7 +437,7 @@ extern "C" bppo_status bppo_opponents_get_envs(bppo_ctx *c, int32_t *learner_pos
     if (!c->n_opp) return BPPO_OK;
     if (learner_pos) BPPO_HIP(c, hipMemcpyAsync(learner_pos, c->d_lpos, sizeof(int32_t) * c->n_opp, hipMemcpyDeviceToHost, c->stream));
     if (pos_to_opp)
-        BPPO_HIP(c, hipMemcpyAsync(pos_to_opp, c->d_p2o, sizeof(int32_t) * (size_t)c->n_opp * c->P, hipMemcpyDeviceToHost, c->stream));
+        BPPO_HIP(c, hipMemcpyAsync(pos_to_opp, c->d_p2o, sizeof(int32_t) * (size_t)c->n_opp * c->Pa, hipMemcpyDeviceToHost, c->stream));
     BPPO_HIP(c, hipStreamSynchronize(c->stream));
     return BPPO_OK;
 }

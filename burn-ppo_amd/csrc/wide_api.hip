@@ -47,7 +47,10 @@ static bool is_hidden(const NetLayout &n, int l) {
 
 bppo_status wide_init(bppo_ctx *c) {
     const bppo_config &cfg = c->cfg;
-    if (cfg.ctde && cfg.env_kind != BPPO_ENV_LIARS_DICE) { c->err = "CTDE needs privileged obs"; return BPPO_ERR_ARG; }
+    if (cfg.ctde && cfg.env_kind != BPPO_ENV_LIARS_DICE && cfg.env_kind != BPPO_ENV_SKULL) {
+        c->err = "CTDE needs privileged obs";
+        return BPPO_ERR_ARG;
+    }
     if (!cfg.ctde) c->G = 0;
     c->L = c->G + c->D;
     const NetLayout &n = c->net;
@@ -116,7 +119,7 @@ void wide_free(bppo_ctx *c) {
 }
 
 bppo_status wide_reset(bppo_ctx *c) {
-    WHIP(c, wide_env_reset(c->cfg.env_kind, c->stream, c->N, c->cfg.env_seed_base, c->d_wstate, c->d_env_pos,
+    WHIP(c, wide_env_reset(c->cfg.env_kind, c->stream, c->N, c->cfg.env_seed_base, c->Pa, c->d_wstate, c->d_env_pos,
                            c->d_ep_ret, c->d_ep_len));
     return BPPO_OK;
 }
@@ -223,7 +226,7 @@ bppo_status wide_collect(bppo_ctx *c, uint64_t base) {
         w.actions = c->d_act + r0; w.shaping = shaping_coef(c);
         w.all_r = c->d_allr + r0 * P; w.rew_act = (c->cfg.normalize_returns ? c->d_rew_raw : c->d_rew) + r0; w.done_f = c->d_done + r0; w.done_u8 = nullptr;
         w.ep_ret = c->d_ep_ret; w.ep_len = c->d_ep_len; w.eps = c->d_eps; w.ep_count = c->d_ep_count;
-        w.eps_cap = c->eps_cap;
+        w.eps_cap = c->eps_cap; w.err = c->d_err;
         WHIP(c, wide_env_step(c->cfg.env_kind, c->stream, w));
         if (opp) WTRY(opp_step_seats(c, t));
     }
@@ -346,19 +349,22 @@ bppo_status wide_step_host(bppo_ctx *c, const int32_t *actions, float *obs, floa
                            int32_t *n_eps) {
     const int N = c->N, P = c->P;
     WHIP(c, hipMemcpyAsync(c->d_act_in, actions, 4 * (size_t)N, hipMemcpyHostToDevice, c->stream));
+    WHIP(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
     WideStepArgs w;
     w.N = N; w.t = 0; w.state = c->d_wstate; w.env_pos = c->d_env_pos; w.seed_base = c->cfg.env_seed_base;
     w.actions = c->d_act_in; w.shaping = shaping_coef(c);
     w.all_r = c->d_scr_r; w.rew_act = nullptr; w.done_f = nullptr; w.done_u8 = c->d_scr_d;
     w.ep_ret = c->d_ep_ret; w.ep_len = c->d_ep_len; w.eps = c->d_eps; w.ep_count = c->d_ep_count;
-    w.eps_cap = c->eps_cap;
+    w.eps_cap = c->eps_cap; w.err = c->d_err;
     WHIP(c, wide_env_step(c->cfg.env_kind, c->stream, w));
     if (rewards) WHIP(c, hipMemcpyAsync(rewards, c->d_scr_r, 4 * (size_t)N * P, hipMemcpyDeviceToHost, c->stream));
     if (dones) WHIP(c, hipMemcpyAsync(dones, c->d_scr_d, (size_t)N, hipMemcpyDeviceToHost, c->stream));
-    int32_t cnt = 0;
+    int32_t cnt = 0, err = 0;
     WHIP(c, hipMemcpyAsync(&cnt, c->d_ep_count, 4, hipMemcpyDeviceToHost, c->stream));
+    WHIP(c, hipMemcpyAsync(&err, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
     WHIP(c, hipStreamSynchronize(c->stream));
     if (n_eps) *n_eps = cnt;
+    if (err & 8) { c->err = "Invalid action: outside the env's action mask"; return BPPO_ERR_ARG; }   // skull.rs:1116-1128
     if (obs) WTRY(wide_observe_host(c, obs, nullptr, nullptr, nullptr));
     return BPPO_OK;
 }

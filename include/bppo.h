@@ -40,7 +40,9 @@ typedef enum {
     BPPO_ERR_UNSUPPORTED = 6   /* configuration not implemented on the device path */
 } bppo_status;
 
-typedef enum { BPPO_ENV_CARTPOLE = 0, BPPO_ENV_CONNECT_FOUR = 1, BPPO_ENV_LIARS_DICE = 2 } bppo_env_kind;
+typedef enum { BPPO_ENV_CARTPOLE = 0, BPPO_ENV_CONNECT_FOUR = 1, BPPO_ENV_LIARS_DICE = 2, BPPO_ENV_SKULL = 3 } bppo_env_kind;
+/* the widest player axis (Skull: MAX_PLAYERS = 6, envs/skull.rs:13) */
+#define BPPO_MAX_PLAYERS 6
 
 /* Mirrors the subset of config.rs:747-924 the hot path reads. */
 typedef struct {
@@ -54,7 +56,7 @@ typedef struct {
     double gamma, gae_lambda, clip_epsilon, value_coef, max_grad_norm, adam_epsilon;
     double target_kl;            /* < 0 : None */
     double return_clip;          /* ReturnNormalizer clip (config.rs:966-968) */
-    double reward_shaping_coef;  /* Liar's Dice per-round shaping (constant schedule) */
+    double reward_shaping_coef;  /* Liar's Dice / Skull shaping (constant schedule; see below) */
     uint64_t seed;               /* main StdRng seed (main.rs:189) */
     uint64_t env_seed_base;      /* env i is seeded env_seed_base + i (main.rs:1964) */
     uint64_t rng_stream;         /* ChaCha stream id of the main RNG: 0 = reference; rank for W>1 */
@@ -66,10 +68,13 @@ typedef struct {
     /* normalize_values (config.rs:827-832, default false): PopArt value normalization
      * with value-head rescaling (normalization.rs:262-366, ppo.rs:1599-1653) */
     int32_t normalize_values;
+    /* Skull: player_count (config.rs:767 PlayerCountMode, get_fixed_count, main.rs:1998);
+     * 2..6, 0 = the default 4.  The player axis of the buffers stays NUM_PLAYERS = 6. */
+    int32_t player_count;
 } bppo_config;
 
 typedef struct {
-    float total_reward[4];
+    float total_reward[BPPO_MAX_PLAYERS];   /* players >= the env's NUM_PLAYERS: 0 */
     int32_t length;
     int32_t env_index;
     int32_t step;                /* rollout step t at which it ended */
@@ -197,7 +202,8 @@ bppo_status bppo_get_stream(bppo_ctx *ctx, void **hip_stream);
  *   state learner_pos [num_opponent_envs] and pos_to_opp [num_opponent_envs][P]
  *   (model index per seat, -1 on the learner's seat) (EnvState, opponent_pool.rs:80-124);
  *   current_opp [P - 1]: OpponentPool::sample_all_slots, the models a finished game
- *   is given before its seats are reshuffled from the main RNG.
+ *   is given before its seats are reshuffled from the main RNG.  P here is the
+ *   seated player count (main.rs:552: Skull's player_count, else NUM_PLAYERS).
  * Opponent batches sample in ascending model index (the reference iterates a
  * HashMap, whose order is unspecified).  num_opponent_envs = 0 switches it off.
  * Buffer "valid" holds the learner-turn flags of the last rollout; ppo_update

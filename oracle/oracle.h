@@ -63,7 +63,7 @@ void or_rng_words_key(const uint32_t key[8], int rounds, uint64_t skip, uint32_t
 void or_rng_seed_key(uint64_t seed, uint32_t key_out[8]);
 
 /* ----------------------------------------------------------------- envs -- */
-enum { OR_ENV_CARTPOLE = 0, OR_ENV_CONNECT_FOUR = 1, OR_ENV_LIARS_DICE = 2 };
+enum { OR_ENV_CARTPOLE = 0, OR_ENV_CONNECT_FOUR = 1, OR_ENV_LIARS_DICE = 2, OR_ENV_SKULL = 3 };
 
 #define OR_CP_OBS 5
 #define OR_CP_ACT 2
@@ -122,9 +122,46 @@ void or_ld_mask(const or_liars_dice *e, uint8_t mask[49]);
 void or_ld_priv(const or_liars_dice *e, float *priv);
 int or_ld_current_player(const or_liars_dice *e);
 
+#define OR_SK_MAXP 6
+#define OR_SK_CARDS 4
+#define OR_SK_ROSES 3
+#define OR_SK_MAXBID 24
+#define OR_SK_WINS 2
+#define OR_SK_OBS 135
+#define OR_SK_ACT 33
+#define OR_SK_PRIV 200
+#define OR_SK_HIST 8
+typedef struct {
+    int32_t n;                                  /* num_players, 2..6 */
+    uint8_t has_trap[OR_SK_MAXP], rose_count[OR_SK_MAXP], wins[OR_SK_MAXP];
+    uint8_t stack_len[OR_SK_MAXP], stack[OR_SK_MAXP][OR_SK_CARDS];   /* 1 = skull, bottom first */
+    uint8_t passed[OR_SK_MAXP], revealed[OR_SK_MAXP];
+    int32_t phase, current, round_starter, current_bid, current_bidder;   /* bidder -1: None */
+    int32_t hist_len;
+    uint8_t hist_player[OR_SK_HIST], hist_bid[OR_SK_HIST];              /* bid 0 = pass */
+    int32_t roses_found, must_reveal_own, last_skull_owner;
+    int8_t elim_order[OR_SK_MAXP];
+    int32_t num_elim, game_over, winner;        /* winner -1: None */
+    or_rng rng;
+} or_skull;
+void or_skull_new(or_skull *e, int num_players, uint64_t seed);
+void or_skull_reset(or_skull *e, float *obs);
+void or_skull_step(or_skull *e, int32_t action, float shaping, float *obs, float rewards[6], int *done,
+                   int *invalid);
+void or_skull_get_obs(const or_skull *e, float *obs);
+void or_skull_mask(const or_skull *e, uint8_t mask[33]);
+void or_skull_priv(const or_skull *e, float *priv);
+int or_skull_current_player(const or_skull *e);
+void or_skull_outcome(const or_skull *e, int32_t out[6]);
+void or_skull_placements(const or_skull *e, int32_t out[6]);
+void or_skull_final_rewards(const or_skull *e, float r[6]);
+
 /* -------------------------------------------------------------- VecEnv --- */
 typedef struct or_vecenv or_vecenv;
 or_vecenv *or_vecenv_new(int env_kind, int num_envs, uint64_t seed_base);
+/* Skull: player_count (config.rs:767, Fixed count; 0 = the default 4) */
+or_vecenv *or_vecenv_new_np(int env_kind, int num_envs, uint64_t seed_base, int player_count);
+int or_vecenv_invalid(const or_vecenv *v);   /* an action outside the mask was stepped (panic) */
 void or_vecenv_free(or_vecenv *v);
 int or_vecenv_obs_dim(const or_vecenv *v);
 int or_vecenv_act_dim(const or_vecenv *v);
@@ -138,7 +175,7 @@ int or_vecenv_get_masks(const or_vecenv *v, uint8_t *masks);  /* returns 0 if en
 void or_vecenv_get_priv(const or_vecenv *v, float *priv);
 /* step: rewards [N*P]; dones [N]; episode stats appended (up to cap) */
 typedef struct {
-    float total_rewards[4];
+    float total_rewards[6];
     int32_t length;
     int32_t env_index;
 } or_episode;
@@ -289,6 +326,7 @@ typedef struct {
     int threads;             /* env-step threads (rayon equivalent); 0 = all */
     int cnn, num_conv, conv_ch[4], ksize;   /* network_type = "cnn" (Connect Four) */
     int normalize_values;    /* PopArt (config.rs:827-832) */
+    int player_count;        /* Skull (config.rs:767), 0 = 4 */
 } or_train_cfg;
 or_trainer *or_trainer_new(const or_train_cfg *c, const float *init_params);
 void or_trainer_free(or_trainer *t);

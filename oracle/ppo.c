@@ -109,6 +109,7 @@ struct or_trainer {
     or_obs_norm *opp_on;
     int *opp_has_norm;
     int32_t *lpos, *p2o, *curopp;
+    int Pa;                  /* seated players: EnvState's num_players (main.rs:552, 649) */
     float *valid;
 };
 
@@ -121,11 +122,12 @@ static double now_s(void) {
 or_trainer *or_trainer_new(const or_train_cfg *c, const float *init_params) {
     or_trainer *t = calloc(1, sizeof *t);
     t->c = *c;
-    t->env = or_vecenv_new(c->env_kind, c->num_envs, c->seed);
+    t->env = or_vecenv_new_np(c->env_kind, c->num_envs, c->seed, c->player_count);
     or_vecenv_set_shaping(t->env, (float)c->reward_shaping);
     t->T = c->num_steps; t->N = c->num_envs;
     t->D = or_vecenv_obs_dim(t->env); t->A = or_vecenv_act_dim(t->env);
     t->P = or_vecenv_players(t->env); t->G = c->ctde ? or_vecenv_priv_dim(t->env) : 0;
+    t->Pa = c->env_kind == OR_ENV_SKULL ? (c->player_count > 0 ? c->player_count : 4) : t->P;
     t->net.ctde = c->ctde; t->net.obs_dim = t->D; t->net.priv_dim = t->G; t->net.act_dim = t->A;
     t->net.relu = c->relu; t->net.n_actor = c->num_hidden; t->net.actor_width = c->hidden;
     t->net.n_critic = c->ctde ? c->critic_num_hidden : 0;
@@ -210,20 +212,20 @@ void or_trainer_set_opponents(or_trainer *t, int K, const float *params, const d
         }
     }
     t->lpos = malloc(sizeof(int32_t) * (n_opp > 0 ? n_opp : 1));
-    t->p2o = malloc(sizeof(int32_t) * (size_t)(n_opp > 0 ? n_opp : 1) * t->P);
-    t->curopp = malloc(sizeof(int32_t) * t->P);
+    t->p2o = malloc(sizeof(int32_t) * (size_t)(n_opp > 0 ? n_opp : 1) * t->Pa);
+    t->curopp = malloc(sizeof(int32_t) * t->Pa);
     if (n_opp) {
         memcpy(t->lpos, learner_pos, sizeof(int32_t) * n_opp);
-        memcpy(t->p2o, pos_to_opp, sizeof(int32_t) * (size_t)n_opp * t->P);
+        memcpy(t->p2o, pos_to_opp, sizeof(int32_t) * (size_t)n_opp * t->Pa);
     }
-    memcpy(t->curopp, current_opp, sizeof(int32_t) * (t->P - 1));
+    memcpy(t->curopp, current_opp, sizeof(int32_t) * (t->Pa - 1));
     if (!t->valid) t->valid = malloc(sizeof(float) * (size_t)t->T * t->N);
 }
 
 void or_trainer_opponent_envs(const or_trainer *t, int32_t *learner_pos, int32_t *pos_to_opp) {
     if (!t->n_opp) return;
     if (learner_pos) memcpy(learner_pos, t->lpos, sizeof(int32_t) * t->n_opp);
-    if (pos_to_opp) memcpy(pos_to_opp, t->p2o, sizeof(int32_t) * (size_t)t->n_opp * t->P);
+    if (pos_to_opp) memcpy(pos_to_opp, t->p2o, sizeof(int32_t) * (size_t)t->n_opp * t->Pa);
 }
 
 /* resume hooks (checkpoint.rs:405-465 load_*): main RNG = StdRng::from_seed(key
@@ -343,7 +345,7 @@ static int collect_opp(or_trainer *t) {
         for (int k = 0; k < t->K; k++) {
             n = 0;
             for (int e = 0; e < t->n_opp; e++)
-                if (cp[e] != t->lpos[e] && t->p2o[(size_t)e * P + cp[e]] == k) rows[n++] = e;
+                if (cp[e] != t->lpos[e] && t->p2o[(size_t)e * t->Pa + cp[e]] == k) rows[n++] = e;
             if (!n) continue;
             for (int j = 0; j < n; j++) {
                 memcpy(xo + (size_t)j * D, raw + (size_t)rows[j] * D, sizeof(float) * D);
@@ -360,7 +362,7 @@ static int collect_opp(or_trainer *t) {
         t->n_eps += ne < cap ? ne : cap;
         t->n_eps_total += ne;
         for (int e = 0; e < t->n_opp; e++)                                   /* :874-925 */
-            if (dn[e]) or_shuffle_positions(&t->rng, P, t->curopp, &t->lpos[e], &t->p2o[(size_t)e * P]);
+            if (dn[e]) or_shuffle_positions(&t->rng, t->Pa, t->curopp, &t->lpos[e], &t->p2o[(size_t)e * t->Pa]);
         for (int e = 0; e < N; e++) {                                        /* :928-1003 */
             const int cur = cp[e];
             const int valid = e >= t->n_opp || cur == t->lpos[e];

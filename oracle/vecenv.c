@@ -8,7 +8,7 @@
 #include "oracle.h"
 
 struct or_vecenv {
-    int kind, n, obs_dim, act_dim, players, priv_dim;
+    int kind, n, obs_dim, act_dim, players, priv_dim, invalid;
     float shaping;
     void *envs;
     size_t env_size;
@@ -24,13 +24,18 @@ static void env_reset(or_vecenv *v, int i, float *obs) {
     switch (v->kind) {
     case OR_ENV_CARTPOLE: or_cartpole_reset(env_at(v, i), obs); break;
     case OR_ENV_CONNECT_FOUR: or_c4_reset(env_at(v, i), obs); break;
+    case OR_ENV_SKULL: or_skull_reset(env_at(v, i), obs); break;
     default: or_ld_reset(env_at(v, i), obs); break;
     }
 }
 
 /* env.rs:281-302 — factory(i) (main.rs:1964 seed+i) then reset() AGAIN. */
-or_vecenv *or_vecenv_new(int kind, int n, uint64_t seed_base) {
+or_vecenv *or_vecenv_new(int kind, int n, uint64_t seed_base) { return or_vecenv_new_np(kind, n, seed_base, 0); }
+int or_vecenv_invalid(const or_vecenv *v) { return v->invalid; }
+
+or_vecenv *or_vecenv_new_np(int kind, int n, uint64_t seed_base, int np) {
     or_vecenv *v = calloc(1, sizeof *v);
+    if (np <= 0) np = 4;                               /* PlayerCountMode::default (config.rs:667-671) */
     v->kind = kind; v->n = n;
     switch (kind) {
     case OR_ENV_CARTPOLE:
@@ -40,6 +45,10 @@ or_vecenv *or_vecenv_new(int kind, int n, uint64_t seed_base) {
     case OR_ENV_CONNECT_FOUR:
         v->obs_dim = OR_C4_OBS; v->act_dim = OR_C4_ACT; v->players = 2; v->priv_dim = 0;
         v->env_size = sizeof(or_connect_four);
+        break;
+    case OR_ENV_SKULL:   /* Environment::NUM_PLAYERS = MAX_PLAYERS (skull.rs:1049) */
+        v->obs_dim = OR_SK_OBS; v->act_dim = OR_SK_ACT; v->players = OR_SK_MAXP; v->priv_dim = OR_SK_PRIV;
+        v->env_size = sizeof(or_skull);
         break;
     default:
         v->obs_dim = OR_LD_OBS; v->act_dim = OR_LD_ACT; v->players = 4; v->priv_dim = OR_LD_PRIV;
@@ -55,6 +64,7 @@ or_vecenv *or_vecenv_new(int kind, int n, uint64_t seed_base) {
         switch (kind) {
         case OR_ENV_CARTPOLE: or_cartpole_new(env_at(v, i), s); break;
         case OR_ENV_CONNECT_FOUR: or_c4_new(env_at(v, i)); break;
+        case OR_ENV_SKULL: or_skull_new(env_at(v, i), np, s); break;   /* main.rs:2008-2014 */
         default: or_ld_new(env_at(v, i), s); break;
         }
         env_reset(v, i, v->obs + (size_t)i * v->obs_dim);
@@ -95,6 +105,7 @@ void or_vecenv_get_players(const or_vecenv *v, int32_t *p) {
         switch (v->kind) {
         case OR_ENV_CARTPOLE: p[i] = 0; break;
         case OR_ENV_CONNECT_FOUR: p[i] = or_c4_current_player(env_at(v, i)); break;
+        case OR_ENV_SKULL: p[i] = or_skull_current_player(env_at(v, i)); break;
         default: p[i] = or_ld_current_player(env_at(v, i)); break;
         }
     }
@@ -103,11 +114,16 @@ int or_vecenv_get_masks(const or_vecenv *v, uint8_t *m) {
     if (v->kind == OR_ENV_CARTPOLE) return 0;
     for (int i = 0; i < v->n; i++) {
         if (v->kind == OR_ENV_CONNECT_FOUR) or_c4_mask(env_at(v, i), m + (size_t)i * 7);
+        else if (v->kind == OR_ENV_SKULL) or_skull_mask(env_at(v, i), m + (size_t)i * OR_SK_ACT);
         else or_ld_mask(env_at(v, i), m + (size_t)i * 49);
     }
     return 1;
 }
 void or_vecenv_get_priv(const or_vecenv *v, float *g) {
+    if (v->kind == OR_ENV_SKULL) {
+        for (int i = 0; i < v->n; i++) or_skull_priv(env_at(v, i), g + (size_t)i * OR_SK_PRIV);
+        return;
+    }
     if (v->kind != OR_ENV_LIARS_DICE) return;
     for (int i = 0; i < v->n; i++) or_ld_priv(env_at(v, i), g + (size_t)i * OR_LD_PRIV);
 }
@@ -119,12 +135,19 @@ int or_vecenv_step(or_vecenv *v, const int32_t *actions, float *obs_out, float *
     const int P = v->players, D = v->obs_dim;
 #pragma omp parallel for schedule(static)
     for (int i = 0; i < v->n; i++) {
-        float r[4] = {0, 0, 0, 0};
-        int done = 0;
+        float r[6] = {0, 0, 0, 0, 0, 0};
+        int done = 0, bad = 0;
         float *o = v->obs + (size_t)i * D;
         switch (v->kind) {
         case OR_ENV_CARTPOLE: or_cartpole_step(env_at(v, i), actions[i], o, &r[0], &done); break;
         case OR_ENV_CONNECT_FOUR: or_c4_step(env_at(v, i), actions[i], o, r, &done); break;
+        case OR_ENV_SKULL:
+            or_skull_step(env_at(v, i), actions[i], v->shaping, o, r, &done, &bad);
+            if (bad) {
+#pragma omp atomic write
+                v->invalid = 1;
+            }
+            break;
         default: or_ld_step(env_at(v, i), actions[i], v->shaping, o, r, &done); break;
         }
         for (int p = 0; p < P; p++) {

@@ -14,11 +14,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(ROOT, "oracle")
 LIB_PATH = os.path.join(ORACLE_DIR, "build", "liboracle.so")
 
-ENV_CARTPOLE, ENV_CONNECT_FOUR, ENV_LIARS_DICE = 0, 1, 2
+ENV_CARTPOLE, ENV_CONNECT_FOUR, ENV_LIARS_DICE, ENV_SKULL = 0, 1, 2, 3
 
 
 def _num_players(kind):
-    return {ENV_CARTPOLE: 1, ENV_CONNECT_FOUR: 2, ENV_LIARS_DICE: 4}[kind]
+    return {ENV_CARTPOLE: 1, ENV_CONNECT_FOUR: 2, ENV_LIARS_DICE: 4, ENV_SKULL: 6}[kind]
 
 
 def build():
@@ -50,6 +50,18 @@ class LiarsDice(C.Structure):
                 ("global_step", C.c_uint64), ("rng", Rng)]
 
 
+class Skull(C.Structure):
+    _fields_ = [("n", C.c_int32), ("has_trap", C.c_uint8 * 6), ("rose_count", C.c_uint8 * 6),
+                ("wins", C.c_uint8 * 6), ("stack_len", C.c_uint8 * 6), ("stack", (C.c_uint8 * 4) * 6),
+                ("passed", C.c_uint8 * 6), ("revealed", C.c_uint8 * 6),
+                ("phase", C.c_int32), ("current", C.c_int32), ("round_starter", C.c_int32),
+                ("current_bid", C.c_int32), ("current_bidder", C.c_int32), ("hist_len", C.c_int32),
+                ("hist_player", C.c_uint8 * 8), ("hist_bid", C.c_uint8 * 8),
+                ("roses_found", C.c_int32), ("must_reveal_own", C.c_int32), ("last_skull_owner", C.c_int32),
+                ("elim_order", C.c_int8 * 6), ("num_elim", C.c_int32), ("game_over", C.c_int32),
+                ("winner", C.c_int32), ("rng", Rng)]
+
+
 class ObsNorm(C.Structure):
     _fields_ = [("dim", C.c_int), ("mean", C.POINTER(C.c_double)), ("var", C.POINTER(C.c_double)),
                 ("count", C.c_double), ("clip", C.c_float)]
@@ -71,7 +83,7 @@ class Adam(C.Structure):
 
 
 class Episode(C.Structure):
-    _fields_ = [("total_rewards", C.c_float * 4), ("length", C.c_int32), ("env_index", C.c_int32)]
+    _fields_ = [("total_rewards", C.c_float * 6), ("length", C.c_int32), ("env_index", C.c_int32)]
 
 
 class NetDesc(C.Structure):
@@ -98,7 +110,7 @@ class TrainCfg(C.Structure):
                 ("lr", C.c_double), ("ent_coef", C.c_double), ("reward_shaping", C.c_double),
                 ("ppo", PpoCfg), ("seed", C.c_uint64), ("threads", C.c_int),
                 ("cnn", C.c_int), ("num_conv", C.c_int), ("conv_ch", C.c_int * 4), ("ksize", C.c_int),
-                ("normalize_values", C.c_int)]
+                ("normalize_values", C.c_int), ("player_count", C.c_int)]
 
 
 class UpdateMetrics(C.Structure):
@@ -163,7 +175,19 @@ def lib():
             "or_ld_mask": (None, [C.POINTER(LiarsDice), u8]),
             "or_ld_priv": (None, [C.POINTER(LiarsDice), f32]),
             "or_ld_get_obs": (None, [C.POINTER(LiarsDice), f32]),
+            "or_skull_new": (None, [C.POINTER(Skull), C.c_int, C.c_uint64]),
+            "or_skull_reset": (None, [C.POINTER(Skull), C.c_void_p]),
+            "or_skull_step": (None, [C.POINTER(Skull), C.c_int32, C.c_float, C.c_void_p, f32,
+                                     C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+            "or_skull_mask": (None, [C.POINTER(Skull), u8]),
+            "or_skull_get_obs": (None, [C.POINTER(Skull), f32]),
+            "or_skull_priv": (None, [C.POINTER(Skull), f32]),
+            "or_skull_placements": (None, [C.POINTER(Skull), i32]),
+            "or_skull_final_rewards": (None, [C.POINTER(Skull), f32]),
+            "or_skull_outcome": (None, [C.POINTER(Skull), i32]),
             "or_vecenv_new": (C.c_void_p, [C.c_int, C.c_int, C.c_uint64]),
+            "or_vecenv_new_np": (C.c_void_p, [C.c_int, C.c_int, C.c_uint64, C.c_int]),
+            "or_vecenv_invalid": (C.c_int, [C.c_void_p]),
             "or_vecenv_free": (None, [C.c_void_p]),
             "or_vecenv_get_obs": (None, [C.c_void_p, f32]),
             "or_vecenv_get_players": (None, [C.c_void_p, i32]),
@@ -354,7 +378,8 @@ def ppo_cfg(num_epochs=4, num_minibatches=4, clip=0.2, value_coef=0.5, max_grad_
 def train_cfg(env_kind=ENV_CARTPOLE, num_envs=8, num_steps=128, hidden=64, num_hidden=2, relu=True,
               ctde=False, critic_hidden=0, critic_num_hidden=0, normalize_obs=True,
               normalize_returns=True, return_clip=10.0, gamma=0.99, gae_lambda=0.95, lr=1e-3,
-              ent_coef=0.01, reward_shaping=0.0, seed=42, threads=0, cnn=None, normalize_values=False, **ppo):
+              ent_coef=0.01, reward_shaping=0.0, seed=42, threads=0, cnn=None, normalize_values=False,
+              player_count=0, **ppo):
     """cnn: None, or (conv_channels per layer, kernel_size); hidden / num_hidden are
     then cnn_fc_hidden_size / cnn_num_fc_layers"""
     extra = {}
@@ -362,7 +387,7 @@ def train_cfg(env_kind=ENV_CARTPOLE, num_envs=8, num_steps=128, hidden=64, num_h
         ch, ks = cnn
         extra = dict(cnn=1, num_conv=len(ch), conv_ch=(C.c_int * 4)(*[ch[min(i, len(ch) - 1)] for i in range(4)]),
                      ksize=ks)
-    return TrainCfg(**extra, normalize_values=int(normalize_values), env_kind=env_kind, num_envs=num_envs, num_steps=num_steps, hidden=hidden,
+    return TrainCfg(**extra, normalize_values=int(normalize_values), player_count=player_count, env_kind=env_kind, num_envs=num_envs, num_steps=num_steps, hidden=hidden,
                     num_hidden=num_hidden, relu=int(relu), ctde=int(ctde), critic_hidden=critic_hidden,
                     critic_num_hidden=critic_num_hidden, normalize_obs=int(normalize_obs),
                     normalize_returns=int(normalize_returns), return_clip=return_clip, gamma=gamma,
