@@ -127,7 +127,14 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     c->dev = dev;
     BPPO_HIP(c, hipSetDevice(dev));
     if (stream) { c->stream = (hipStream_t)stream; c->own_stream = false; }
-    else { BPPO_HIP(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)); c->own_stream = true; }
+    else {
+        // the hot path's stream at the highest priority: the shuffle engine's copy-stream
+        // kernels (J expansion) only take CUs the update kernels leave free
+        int lo = 0, hi = 0;
+        BPPO_HIP(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
+        BPPO_HIP(c, hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi));
+        c->own_stream = true;
+    }
     if (cfg->num_envs <= 0 || cfg->num_steps <= 0 || cfg->num_epochs <= 0 || cfg->num_minibatches <= 0) {
         c->err = "num_envs, num_steps, num_epochs, num_minibatches must be positive";
         return BPPO_ERR_ARG;

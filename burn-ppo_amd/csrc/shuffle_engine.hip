@@ -65,50 +65,81 @@ __global__ void k_chacha_words(Key8 key, uint64_t stream, uint64_t base, uint64_
     o[3] = make_uint4(blk[12], blk[13], blk[14], blk[15]);
 }
 
-// J from walk segments: thread i re-walks words [pos0, pos1) of segment i from
-// range r0 and writes J[r-1] = hi(w * r) for every ACCEPTED word (each r is
-// accepted exactly once, so segments never write the same slot).  Words come
-// from the jobs' device word buffers when a region holds the segment, else
-// from ChaCha12 here.
+// J from walk segments.  Segments are consecutive pieces of the epoch's chain
+// (segment i covers words [pos0, pos1) from range r0; segment i+1 starts where it
+// ends), so a block takes XJ_SEG consecutive segments: it stages their words in
+// LDS with coalesced loads (from the jobs' device word buffers when a region holds
+// them, else ChaCha12 here), one lane per segment re-walks its piece and writes
+// J[r-1] = hi(w * r) for every ACCEPTED word into an LDS copy of the block's J
+// range (each r is accepted exactly once), and the block stores that range with
+// coalesced writes.  Short-lived blocks: the copy stream's J expansion holds CUs
+// for microseconds, not for the whole epoch's walk.
 struct WordRegions {
     const uint32_t *ptr[4];
     uint64_t base[4], len[4];
     int n;
 };
-__global__ void __launch_bounds__(256) k_expand_J(Key8 key, uint64_t stream, const ShuffleEngine::Seg *segs, int ns,
-                                                  WordRegions wr, uint32_t *J) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0) J[0] = 0;
-    if (i >= ns) return;
-    const ShuffleEngine::Seg g = segs[i];
-    uint32_t r = g.r0;
-    const uint32_t *src = nullptr;
-    for (int k = 0; k < wr.n; k++)
-        if (g.pos0 >= wr.base[k] && g.pos1 <= wr.base[k] + wr.len[k]) src = wr.ptr[k] + (g.pos0 - wr.base[k]);
-    const uint64_t nw = g.pos1 - g.pos0;
-    auto step = [&](uint32_t w) {
-        const uint64_t m = (uint64_t)w * r;
-        const uint32_t z = (r << __clz(r)) - 1u;
-        if ((uint32_t)m <= z) { J[r - 1] = (uint32_t)(m >> 32); r--; }
-    };
-    if (!src) {
-        WordCursor c;
-        c.init(key, stream, g.pos0);
-        for (uint64_t p = 0; p < nw && r >= 2; p++) step(c.next());
-        return;
+constexpr int XJ_SEG = 16;                           // segments per block
+constexpr int XJ_THREADS = 64;
+constexpr size_t XJ_WORDS = XJ_SEG * SHUF_CK + 32;   // staged words (16-word aligned window)
+constexpr size_t XJ_LDS = sizeof(uint32_t) * (XJ_WORDS + XJ_SEG * SHUF_CK);
+__global__ void __launch_bounds__(XJ_THREADS) k_expand_J(Key8 key, uint64_t stream, const ShuffleEngine::Seg *segs,
+                                                         int ns, WordRegions wr, uint32_t *J) {
+    extern __shared__ uint32_t xj[];
+    uint32_t *words = xj, *jst = xj + XJ_WORDS;
+    const int tid = threadIdx.x;
+    const int s0 = blockIdx.x * XJ_SEG, s1 = min(ns, s0 + XJ_SEG);
+    if (blockIdx.x == 0 && tid == 0) J[0] = 0;
+    if (s0 >= ns) return;
+    const uint64_t p0 = segs[s0].pos0, p1 = segs[s1 - 1].pos1;
+    const uint32_t hi = segs[s0].r0, lo = s1 < ns ? segs[s1].r0 : 1u;   // J[lo .. hi) is this block's
+    const uint64_t wb = p0 >> 4 << 4;                                    // window base (block aligned)
+    const uint64_t nblk = (p1 - wb + 15) >> 4;
+    for (uint64_t b = tid; b < nblk; b += XJ_THREADS) {                 // 16 words per thread and turn
+        const uint64_t q = wb + b * 16;
+        const uint32_t *src = nullptr;
+        for (int k = 0; k < wr.n; k++)
+            if (q >= wr.base[k] && q + 16 <= wr.base[k] + wr.len[k]) src = wr.ptr[k] + (q - wr.base[k]);
+        uint4 *dst = reinterpret_cast<uint4 *>(words + b * 16);
+        if (src && (((uintptr_t)src & 15) == 0)) {
+            const uint4 *v = reinterpret_cast<const uint4 *>(src);
+            dst[0] = v[0]; dst[1] = v[1]; dst[2] = v[2]; dst[3] = v[3];
+        } else if (src) {
+            for (int i = 0; i < 16; i++) words[b * 16 + i] = src[i];
+        } else {
+            uint32_t blk[16];
+            chacha12_block(key, q >> 4, stream, blk);
+            dst[0] = make_uint4(blk[0], blk[1], blk[2], blk[3]);
+            dst[1] = make_uint4(blk[4], blk[5], blk[6], blk[7]);
+            dst[2] = make_uint4(blk[8], blk[9], blk[10], blk[11]);
+            dst[3] = make_uint4(blk[12], blk[13], blk[14], blk[15]);
+        }
     }
-    // head up to 16-byte alignment, then 16 words per iteration (4 x 16-byte loads)
-    uint64_t p = 0;
-    while (p < nw && (((uintptr_t)(src + p)) & 15) && r >= 2) step(src[p++]);
-    for (; p + 16 <= nw && r >= 2; p += 16) {
-        const uint4 *v = reinterpret_cast<const uint4 *>(src + p);
-        const uint4 a0 = v[0], a1 = v[1], a2 = v[2], a3 = v[3];
-        const uint32_t w[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
-                                a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+    __syncthreads();
+    if (s0 + tid < s1) {
+        const ShuffleEngine::Seg g = segs[s0 + tid];
+        uint32_t r = g.r0;
+        auto step = [&](uint32_t w) {
+            const uint64_t m = (uint64_t)w * r;
+            const uint32_t z = (r << __clz(r)) - 1u;
+            if ((uint32_t)m <= z) { jst[hi - r] = (uint32_t)(m >> 32); r--; }
+        };
+        // words 16 at a time (four 16-byte LDS reads ahead of the chain), head and
+        // tail one by one; absolute position p sits at words[p - wb] (wb 16-aligned)
+        uint64_t p = g.pos0;
+        while (p < g.pos1 && (p & 15) && r >= 2) step(words[p++ - wb]);
+        for (; p + 16 <= g.pos1 && r >= 2; p += 16) {
+            const uint4 *v = reinterpret_cast<const uint4 *>(words + (p - wb));
+            const uint4 a0 = v[0], a1 = v[1], a2 = v[2], a3 = v[3];
+            const uint32_t w16[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
+                                      a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
 #pragma unroll
-        for (int j = 0; j < 16; j++) if (r >= 2) step(w[j]);
+            for (int j = 0; j < 16; j++) if (r >= 2) step(w16[j]);
+        }
+        for (; p < g.pos1 && r >= 2; p++) step(words[p - wb]);
     }
-    for (; p < nw && r >= 2; p++) step(src[p]);
+    __syncthreads();
+    for (uint32_t k = tid; k < hi - lo; k += XJ_THREADS) J[hi - 1 - k] = jst[k];
 }
 
 // expected words per shuffle of n and its std dev: draw with range R accepts with
@@ -169,7 +200,9 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
             err = "shuffle events: creation failed";
             return BPPO_ERR_HIP;
         }
-    if (hipStreamCreateWithFlags(&copy, hipStreamNonBlocking) != hipSuccess) {
+    int prio_lo = 0, prio_hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    if (hipStreamCreateWithPriority(&copy, hipStreamNonBlocking, prio_lo) != hipSuccess) {   // lowest priority
         err = "shuffle copy stream: creation failed";
         return BPPO_ERR_HIP;
     }
@@ -330,8 +363,11 @@ void ShuffleEngine::worker(int i) {
     // scheduler otherwise shares them evenly and delays the walk needed first)
     {
         static const int nice_step = getenv("BPPO_SHUFFLE_NICE") ? atoi(getenv("BPPO_SHUFFLE_NICE")) : 3;
+        // every speculative walk below the true walk (the driver thread, nice 0)
+        static const int nice_base = getenv("BPPO_SHUFFLE_NICE_BASE") ? atoi(getenv("BPPO_SHUFFLE_NICE_BASE")) : 0;
         const int g = i < ncur ? i / std::max(K, 1) : std::max(epochs - C, 0);
-        if (nice_step > 0 && g > 0) (void)setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), std::min(19, nice_step * g));
+        const int nv = nice_base + nice_step * g;
+        if (nv > 0) (void)setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), std::min(19, nv));
     }
     std::vector<uint32_t> scratch;
     uint64_t seen = 0;
@@ -604,8 +640,9 @@ void ShuffleEngine::run() {
                     }
                 Seg *dS = d_seg[slot] + (size_t)e * maxseg;
                 (void)hipMemcpyAsync(dS, S, sizeof(Seg) * (size_t)std::max(ns, 1), hipMemcpyHostToDevice, copy);
-                hipLaunchKernelGGL(k_expand_J, dim3((unsigned)((std::max(ns, 1) + 255) / 256)), dim3(256), 0, copy, key,
-                                   stream, (const Seg *)dS, ns, wr, d_J[slot] + (size_t)e * n);
+                hipLaunchKernelGGL(k_expand_J, dim3((unsigned)((std::max(ns, 1) + XJ_SEG - 1) / XJ_SEG)),
+                                   dim3(XJ_THREADS), XJ_LDS, copy, key, stream, (const Seg *)dS, ns, wr,
+                                   d_J[slot] + (size_t)e * n);
             }
             end_pos[slot][e] = pos;
             (void)hipEventRecord(ev[slot][e], copy);
