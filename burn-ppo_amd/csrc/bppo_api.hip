@@ -210,6 +210,7 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     c->eps_cap = c->N * 4 + 4096;
     TRY(dalloc(c, &c->d_eps, (size_t)c->eps_cap));
     TRY(dalloc(c, &c->d_ep_count, 1));
+    TRY(dalloc(c, &c->d_ep_sum, 2 * EP_SUMMARY_BLOCKS));
     TRY(dalloc(c, &c->d_err, 1));
     TRY(dalloc(c, &c->d_perm, TN));
     TRY(dalloc(c, &c->d_fy, 4 * TN));
@@ -264,7 +265,7 @@ extern "C" void bppo_destroy(bppo_ctx *c) {
                     c->d_env_pos, c->d_ep_ret, c->d_ep_len, c->d_obs, c->d_rew, c->d_rew_raw,
                     c->d_done, c->d_val, c->d_logp, c->d_adv, c->d_ret, c->d_act, c->d_X, c->d_on,
                     c->d_obs_part, c->d_rn_returns, c->d_rn_stats, c->d_scan_agg, c->d_last_v,
-                    c->d_eps, c->d_ep_count, c->d_err, c->d_perm, c->d_fy, c->d_scan,
+                    c->d_eps, c->d_ep_count, c->d_ep_sum, c->d_err, c->d_perm, c->d_fy, c->d_scan,
                     c->d_red, c->d_mb_stats, c->d_gumbel, c->d_rows, c->d_mbrow};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     fy_ranges_free(c->fyr);
@@ -299,19 +300,21 @@ extern "C" bppo_status bppo_forward(bppo_ctx *c, const float *obs, const float *
                                     float *logits, float *values) {
     if (!c || !obs || B <= 0) return BPPO_ERR_ARG;
     if (c->wide) return wide_forward_host(c, obs, priv, B, logits, values);
-    float *d_o = nullptr, *d_l = nullptr, *d_v = nullptr;
-    BPPO_HIP(c, hipMalloc((void **)&d_o, sizeof(float) * (size_t)B * c->D));
-    BPPO_HIP(c, hipMalloc((void **)&d_l, sizeof(float) * (size_t)B * c->A));
-    BPPO_HIP(c, hipMalloc((void **)&d_v, sizeof(float) * (size_t)B));
+    // scratch freed on every return path (an inference call, not the rollout path)
+    struct Scratch { float *p[3] = {nullptr, nullptr, nullptr}; ~Scratch() { for (float *q : p) (void)hipFree(q); } } t;
+    BPPO_HIP(c, hipMalloc((void **)&t.p[0], sizeof(float) * (size_t)B * c->D));
+    BPPO_HIP(c, hipMalloc((void **)&t.p[1], sizeof(float) * (size_t)B * c->A));
+    BPPO_HIP(c, hipMalloc((void **)&t.p[2], sizeof(float) * (size_t)B));
+    float *d_o = t.p[0], *d_l = t.p[1], *d_v = t.p[2];
     BPPO_HIP(c, hipMemcpyAsync(d_o, obs, sizeof(float) * (size_t)B * c->D, hipMemcpyHostToDevice, c->stream));
     bppo_status s = launch_forward_rows(c, d_o, B, d_l, d_v);
     if (s == BPPO_OK) {
         if (logits) BPPO_HIP(c, hipMemcpyAsync(logits, d_l, sizeof(float) * (size_t)B * c->A, hipMemcpyDeviceToHost, c->stream));
         if (values) BPPO_HIP(c, hipMemcpyAsync(values, d_v, sizeof(float) * (size_t)B, hipMemcpyDeviceToHost, c->stream));
-        BPPO_HIP(c, sync_stream(c));
     }
-    (void)hipFree(d_o); (void)hipFree(d_l); (void)hipFree(d_v);
-    return s;
+    // drain before the scratch is freed, whatever happened above
+    const bppo_status ss = sync_stream(c) == hipSuccess ? BPPO_OK : BPPO_ERR_HIP;
+    return s != BPPO_OK ? s : ss;
 }
 
 extern "C" bppo_status bppo_rng_get(bppo_ctx *c, uint64_t *p) {
@@ -573,8 +576,11 @@ extern "C" bppo_status bppo_collect_rollouts(bppo_ctx *c, bppo_rollout_info *inf
     else if (!c->wide) BPPO_HIP(c, hipMemcpyAsync(c->d_rew, c->d_rew_raw, TN * 4, hipMemcpyDeviceToDevice, c->stream));
     tm_end(c, TM_RETNORM);
     int32_t hv[2] = {0, 0};
+    double part[2 * EP_SUMMARY_BLOCKS];
+    if (info) TRY(launch_episode_summary(c));
     BPPO_HIP(c, hipMemcpyAsync(&hv[0], c->d_ep_count, 4, hipMemcpyDeviceToHost, c->stream));
     BPPO_HIP(c, hipMemcpyAsync(&hv[1], c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
+    if (info) BPPO_HIP(c, hipMemcpyAsync(part, c->d_ep_sum, sizeof(part), hipMemcpyDeviceToHost, c->stream));
     BPPO_HIP(c, sync_stream(c));
     tm_read(c, TM_ROLLOUT); tm_read(c, TM_RETNORM);
     c->collected = 1; c->gae_done = 0;
@@ -589,12 +595,10 @@ extern "C" bppo_status bppo_collect_rollouts(bppo_ctx *c, bppo_rollout_info *inf
         info->episodes = hv[0];
         info->rng_word_pos = c->rng_pos;
         info->mean_return = 0; info->mean_length = 0;
-        int n = std::min(hv[0], c->eps_cap);
+        const int n = std::min(hv[0], c->eps_cap);
         if (n > 0) {
-            std::vector<EpisodeRec> recs(n);
-            BPPO_HIP(c, hipMemcpy(recs.data(), c->d_eps, sizeof(EpisodeRec) * n, hipMemcpyDeviceToHost));
             double sr = 0, sl = 0;
-            for (auto &r : recs) { sr += r.total_reward[0]; sl += r.length; }
+            for (int b = 0; b < EP_SUMMARY_BLOCKS; b++) { sr += part[2 * b]; sl += part[2 * b + 1]; }
             info->mean_return = (float)(sr / n); info->mean_length = (float)(sl / n);
         }
     }

@@ -35,6 +35,8 @@ struct NetLayout {
 NetLayout make_layout(const bppo_config &c, int obs_dim, int priv_dim, int act_dim);
 
 // episode record written by the rollout kernel
+constexpr int EP_SUMMARY_BLOCKS = 128;   // k_ep_summary grid (partial sums per block)
+
 struct EpisodeRec {
     float total_reward[BPPO_MAX_PLAYERS];
     int32_t length, env_index, step, pad;
@@ -88,6 +90,15 @@ struct FyRanges {
     uint32_t n = 0;
 };
 
+// one epoch's minibatch split (ppo.rs:1830-1836: minibatch m has base + (m < rem)
+// rows) and the block chunking of its per-minibatch advantage statistics: block b
+// owns shuffled positions [b C, (b + 1) C), C no larger than the smallest
+// minibatch, so a block touches at most two minibatches (k_update.hip)
+struct EpochSplit { uint32_t B, base, rem, M; };
+__device__ __forceinline__ uint32_t mb_of(uint32_t i, const EpochSplit &s) {
+    const uint32_t big = s.rem * (s.base + 1);
+    return i < big ? i / (s.base + 1) : s.rem + (i - big) / s.base;
+}
 struct ShuffleEngine {
     int dev = 0;
     uint32_t n = 0;
@@ -219,6 +230,7 @@ struct bppo_ctx {
     bppo::EpisodeRec *d_eps = nullptr;
     int32_t *d_ep_count = nullptr;
     int32_t eps_cap = 0;
+    double *d_ep_sum = nullptr;          // [EP_SUMMARY_BLOCKS][2] partial sums (return, length)
     int32_t *d_err = nullptr;
     // main RNG
     bppo::Key8 rng_key{};
@@ -321,6 +333,7 @@ bppo_status launch_cartpole_vecenv_step(bppo_ctx *c, const int32_t *d_actions, f
                                         uint8_t *d_done, float *d_obs_out);
 bppo_status launch_cartpole_observe(bppo_ctx *c, float *d_obs_out);
 bppo_status launch_obs_norm_merge(bppo_ctx *c);
+bppo_status launch_episode_summary(bppo_ctx *c);
 bppo_status launch_obs_norm_rows(bppo_ctx *c, int rows, float *x, int ld, float *raw);
 bppo_status launch_obs_norm_rows_on(bppo_ctx *c, int rows, float *x, int ld, float *raw, const double *on);
 bppo_status launch_bootstrap(bppo_ctx *c, const double *mean, const double *sd, int norm_on);

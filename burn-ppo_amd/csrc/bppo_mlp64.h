@@ -22,6 +22,7 @@ struct Params {
     float bp[2];
     float Wv[H];
     float bv[2];
+    float2 PV[2][H];      // {Wp[2k + h], Wv[k]}: the minibatch heads' (logit h, value) chain pair
     __device__ __forceinline__ float expf(float x) const { return bppo_math::expf_glibc_tab(x, exp2tab); }
     __device__ __forceinline__ float logf(float x) const { return bppo_math::logf_glibc_tab(x, linvc, llogc); }
 };
@@ -53,6 +54,8 @@ __device__ __forceinline__ void load_params(Params &S, const float *__restrict__
     for (int i = threadIdx.x; i < H; i += blockDim.x) {
         S.b0[i] = P[O.b0 + i]; S.b1[i] = P[O.b1 + i]; S.Wv[i] = P[O.wv + i];
         S.Wp[2 * i] = P[O.wp + 2 * i]; S.Wp[2 * i + 1] = P[O.wp + 2 * i + 1];
+        S.PV[0][i] = make_float2(P[O.wp + 2 * i], P[O.wv + i]);
+        S.PV[1][i] = make_float2(P[O.wp + 2 * i + 1], P[O.wv + i]);
     }
     if (threadIdx.x < 32) S.exp2tab[threadIdx.x] = bppo_math::kExp2fTab[threadIdx.x];
     if (threadIdx.x < 16) {

@@ -728,4 +728,33 @@ bppo_status launch_obs_norm_merge(bppo_ctx *c) {
     return BPPO_OK;
 }
 
+// the rollout's completed-episode summary (mean return of player 0, mean length)
+// for bppo_rollout_info: per-block f64 partial sums in a fixed order, combined on
+// the host — no episode records cross PCIe (there are ~N * T / 20 of them)
+__global__ void __launch_bounds__(256) k_ep_summary(const EpisodeRec *eps, const int32_t *count, int cap,
+                                                    double *part) {
+    const int n = min(*count, cap);
+    double sr = 0.0, sl = 0.0;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        sr += (double)eps[i].total_reward[0];
+        sl += (double)eps[i].length;
+    }
+    __shared__ double sh[2][4];
+    for (int o = 32; o > 0; o >>= 1) { sr += __shfl_down(sr, o, 64); sl += __shfl_down(sl, o, 64); }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { sh[0][w] = sr; sh[1][w] = sl; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        part[2 * blockIdx.x] = sh[0][0] + sh[0][1] + sh[0][2] + sh[0][3];
+        part[2 * blockIdx.x + 1] = sh[1][0] + sh[1][1] + sh[1][2] + sh[1][3];
+    }
+}
+
+bppo_status launch_episode_summary(bppo_ctx *c) {
+    hipLaunchKernelGGL(k_ep_summary, dim3(EP_SUMMARY_BLOCKS), dim3(256), 0, c->stream, c->d_eps, c->d_ep_count,
+                       c->eps_cap, c->d_ep_sum);
+    BPPO_HIP(c, hipGetLastError());
+    return BPPO_OK;
+}
+
 }  // namespace bppo

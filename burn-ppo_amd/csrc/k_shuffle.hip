@@ -169,7 +169,8 @@ __global__ void __launch_bounds__(256) k_fy_link(uint32_t n, const uint32_t *off
 }
 
 __global__ void __launch_bounds__(256) k_fy_final(const uint32_t *J, uint32_t n, const uint32_t *succ,
-                                                  const uint32_t *fw, uint32_t *perm) {
+                                                  const uint32_t *fw, uint32_t *perm, const uint32_t *skip) {
+    if (skip && *skip) return;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint32_t s = succ[i];
         uint32_t v;
@@ -291,6 +292,66 @@ __global__ void __launch_bounds__(FYB_LINK_THREADS) k_fyb_link(uint32_t n, FyTab
     }
 }
 
+// overflow fallback of the ranged path (a range held more steps than its LDS
+// capacity: J far from uniform): the direct bucketing of k_fy_zero .. k_fy_final
+// in ONE block, phase by phase (__syncthreads orders the block's global memory).
+// Slow, exact, and launched unconditionally behind the flag, so the common case
+// costs one empty launch instead of eight.
+__global__ void __launch_bounds__(SCAN_B) k_fy_direct_block(const uint32_t *J, uint32_t n, uint32_t *scratch,
+                                                            uint32_t *perm, const uint32_t *flag) {
+    if (*flag == 0u) return;
+    __shared__ uint32_t sh[SCAN_B / 64];
+    uint32_t *cnt = scratch, *bucket = scratch + (size_t)n, *succ = scratch + 2 * (size_t)n,
+             *fw = scratch + 3 * (size_t)n, *off = perm;
+    const uint32_t t = threadIdx.x, T = blockDim.x;
+    for (uint32_t i = t; i < n; i += T) cnt[i] = 0u;
+    __syncthreads();
+    for (uint32_t i = t; i < n; i += T) atomicAdd(&cnt[J[i]], 1u);
+    __syncthreads();
+    uint32_t carry = 0;
+    for (uint32_t b0 = 0; b0 < n; b0 += SCAN_TILE) {
+        const uint32_t base = b0 + t * SCAN_IPT;
+        uint32_t v[SCAN_IPT], sum = 0;
+#pragma unroll
+        for (int k = 0; k < SCAN_IPT; k++) { v[k] = base + k < n ? cnt[base + k] : 0u; sum += v[k]; }
+        uint32_t tot;
+        uint32_t run = carry + block_exclusive_u32(sum, sh, &tot);
+#pragma unroll
+        for (int k = 0; k < SCAN_IPT; k++) {
+            if (base + k < n) off[base + k] = run;
+            run += v[k];
+        }
+        carry += tot;
+    }
+    __syncthreads();
+    for (uint32_t i = t; i < n; i += T) {
+        const uint32_t j = J[i];
+        bucket[off[j] + atomicSub(&cnt[j], 1u) - 1u] = i;
+    }
+    __syncthreads();
+    for (uint32_t j = t; j < n; j += T) {
+        const uint32_t b = off[j], e = j + 1 < n ? off[j + 1] : n;
+        for (uint32_t a = b + 1; a < e; a++) {
+            const uint32_t x = bucket[a];
+            uint32_t q = a;
+            while (q > b && bucket[q - 1] > x) { bucket[q] = bucket[q - 1]; q--; }
+            bucket[q] = x;
+        }
+        for (uint32_t a = b; a < e; a++) succ[bucket[a]] = a + 1 < e ? bucket[a + 1] : FY_NONE;
+        uint32_t f = FY_NONE;
+        if (e > b) f = bucket[b] > j ? bucket[b] : (e > b + 1 ? bucket[b + 1] : FY_NONE);
+        fw[j] = f;
+    }
+    __syncthreads();
+    for (uint32_t i = t; i < n; i += T) {
+        const uint32_t s = succ[i];
+        uint32_t v = s;
+        if (s == FY_NONE) v = J[i];
+        else for (uint32_t f = fw[v]; f != FY_NONE; f = fw[v]) v = f;
+        perm[i] = v;
+    }
+}
+
 static size_t fyb_lds(int nb, int ncb) { return sizeof(uint32_t) * (size_t)(2 * nb + 1 + ncb); }
 
 // range boundaries: equal expected load FYB_LOAD, at most FYB_RMAX targets each
@@ -351,7 +412,6 @@ hipError_t fisher_yates_device(const uint32_t *d_J, uint32_t n, uint32_t *scratc
              *fw = scratch + 3 * (size_t)n;
     uint32_t *off = perm;                // the direct path's offsets live in perm until the final pass
     const int grid = 2048;
-    const uint32_t *gate = nullptr;
     if (rg && rg->nb > 0 && rg->n == n) {
         const FyTab t{rg->x, rg->cb, rg->nb, rg->ncb};
         uint32_t *H = perm, *flag = scan + n / 8192 + 1;
@@ -363,15 +423,21 @@ hipError_t fisher_yates_device(const uint32_t *d_J, uint32_t n, uint32_t *scratc
                            (const uint32_t *)H, reinterpret_cast<uint2 *>(scratch));
         hipLaunchKernelGGL(k_fyb_link, dim3(t.nb), dim3(FYB_LINK_THREADS), 0, st, n, t, (const uint32_t *)H,
                            FYB_BLOCKS, reinterpret_cast<const uint2 *>(scratch), succ, fw, flag);
-        gate = flag;
+        // pass 4 (k_fy_final) runs unless a range overflowed; then the one-block
+        // direct pass computes the permutation instead
+        hipLaunchKernelGGL(k_fy_final, dim3(grid), dim3(256), 0, st, d_J, n, (const uint32_t *)succ,
+                           (const uint32_t *)fw, perm, (const uint32_t *)flag);
+        hipLaunchKernelGGL(k_fy_direct_block, dim3(1), dim3(SCAN_B), 0, st, d_J, n, scratch, perm,
+                           (const uint32_t *)flag);
+        return hipGetLastError();
     }
-    // direct path: always, or only after a ranged pass that overflowed
-    hipLaunchKernelGGL(k_fy_zero, dim3(grid), dim3(256), 0, st, cnt, n, gate);
-    hipLaunchKernelGGL(k_fy_count, dim3(grid), dim3(256), 0, st, d_J, n, cnt, gate);
-    launch_scan(cnt, n, scan, off, gate, st);
-    hipLaunchKernelGGL(k_fy_scatter, dim3(grid), dim3(256), 0, st, d_J, n, (const uint32_t *)off, cnt, bucket, gate);
-    hipLaunchKernelGGL(k_fy_link, dim3(grid), dim3(256), 0, st, n, (const uint32_t *)off, bucket, succ, fw, gate);
-    hipLaunchKernelGGL(k_fy_final, dim3(grid), dim3(256), 0, st, d_J, n, succ, fw, perm);
+    // direct path
+    hipLaunchKernelGGL(k_fy_zero, dim3(grid), dim3(256), 0, st, cnt, n, nullptr);
+    hipLaunchKernelGGL(k_fy_count, dim3(grid), dim3(256), 0, st, d_J, n, cnt, nullptr);
+    launch_scan(cnt, n, scan, off, nullptr, st);
+    hipLaunchKernelGGL(k_fy_scatter, dim3(grid), dim3(256), 0, st, d_J, n, (const uint32_t *)off, cnt, bucket, nullptr);
+    hipLaunchKernelGGL(k_fy_link, dim3(grid), dim3(256), 0, st, n, (const uint32_t *)off, bucket, succ, fw, nullptr);
+    hipLaunchKernelGGL(k_fy_final, dim3(grid), dim3(256), 0, st, d_J, n, succ, fw, perm, nullptr);
     return hipGetLastError();
 }
 

@@ -475,19 +475,24 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
             }
         wave_sync();
         MB_STAMP(3);
-        // ---- heads + loss, lane = row c on both lane halves (the halves compute the
-        // same heads; the row's exp pairs -- softmax terms, probabilities -- run
-        // one per half; the rest of the loss, dl and the metrics on the low half)
+        // ---- heads + loss, lane = row c on both lane halves: half h runs the k-ordered
+        // chain of logit h and both run the value chain (two chains per lane instead
+        // of three; each chain is the same fma sequence as before, so bit-identical);
+        // the row's exp pairs -- softmax terms, probabilities -- run one per half;
+        // the rest of the loss, dl and the metrics on the low half
         {
-            float l0 = 0.0f, l1 = 0.0f, vv = 0.0f;
+            float lh = 0.0f, vv = 0.0f;
             const float *hr = B.T2 + c * RS;
+            const float2 *pv = S.PV[h];
 #pragma unroll 16
             for (int k = 0; k < H; k++) {
                 const float hk = hr[k];
-                l0 = __builtin_fmaf(hk, S.Wp[2 * k], l0);
-                l1 = __builtin_fmaf(hk, S.Wp[2 * k + 1], l1);
-                vv = __builtin_fmaf(hk, S.Wv[k], vv);
+                const float2 w = pv[k];
+                lh = __builtin_fmaf(hk, w.x, lh);
+                vv = __builtin_fmaf(hk, w.y, vv);
             }
+            const float lx = __shfl_xor(lh, 32, 64);
+            const float l0 = h ? lx : lh, l1 = h ? lh : lx;
             MB_STAMP(9);
             const float lg0 = __fadd_rn(l0, S.bp[0]), lg1 = __fadd_rn(l1, S.bp[1]), v = __fadd_rn(vv, S.bv[0]);
             const float mx = lg0 > lg1 ? lg0 : lg1;
@@ -854,47 +859,60 @@ __global__ void __launch_bounds__(256) k_ev(size_t n, const float *val, const fl
 // ------------------------------------------------------------- launchers ---
 // advantage stats of every minibatch of one epoch in one pass (ppo.rs:1905-1913,
 // utils.rs:80-89): f64 sum and sum of squares, min, max over each minibatch's
-// shuffled rows.  Block b owns positions [b C, (b + 1) C) with C no larger than
-// the smallest minibatch, so it touches at most two minibatches; the final pass
-// adds the block partials of each minibatch in block order (deterministic).
-struct EpochSplit { uint32_t B, base, rem, M; };   // minibatch m has base + (m < rem) rows
-__device__ __forceinline__ uint32_t mb_of(uint32_t i, const EpochSplit &s) {
-    const uint32_t big = s.rem * (s.base + 1);
-    return i < big ? i / (s.base + 1) : s.rem + (i - big) / s.base;
-}
-__global__ void __launch_bounds__(256) k_adv_epoch(const float *adv, const uint32_t *perm, EpochSplit sp, uint32_t C,
-                                                   double *part) {
-    __shared__ double ss[2][256], sq[2][256];
-    __shared__ float smn[2][256], smx[2][256];
+// shuffled rows.  Block b owns positions [b C, (b + 1) C) (EpochSplit in
+// bppo_internal.h); the final pass adds the block partials of each minibatch in
+// block order (deterministic).  On the ranged shuffle path the partials come
+// from the fused Fisher-Yates final pass (k_shuffle.hip k_fy_final_ranged).
+// 1024 threads per block, ADV_U positions per thread in flight (perm then adv are
+// two dependent random-ish loads; one pair at a time left the block latency bound)
+constexpr int ADV_THREADS = 1024, ADV_U = 4;
+__global__ void __launch_bounds__(ADV_THREADS) k_adv_epoch(const float *__restrict__ adv,
+                                                           const uint32_t *__restrict__ perm, EpochSplit sp,
+                                                           uint32_t C, double *part) {
+    __shared__ double red[ADV_THREADS / 64][2][4];
     const uint32_t i0 = blockIdx.x * C, i1 = min(sp.B, i0 + C);
     const uint32_t m0 = mb_of(i0, sp);
     double s[2] = {0.0, 0.0}, q[2] = {0.0, 0.0};
     float mn[2] = {INFINITY, INFINITY}, mx[2] = {-INFINITY, -INFINITY};
-    for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-        const float a = adv[perm[i]];
-        const double d = (double)a;
-        if (mb_of(i, sp) != m0) { s[1] += d; q[1] += d * d; mn[1] = fminf(mn[1], a); mx[1] = fmaxf(mx[1], a); }
-        else { s[0] += d; q[0] += d * d; mn[0] = fminf(mn[0], a); mx[0] = fmaxf(mx[0], a); }
+    for (uint32_t b = i0 + threadIdx.x; b < i1; b += ADV_THREADS * ADV_U) {
+        uint32_t pi[ADV_U];
+        float a[ADV_U];
+#pragma unroll
+        for (int k = 0; k < ADV_U; k++) pi[k] = perm[min(b + k * ADV_THREADS, i1 - 1)];
+#pragma unroll
+        for (int k = 0; k < ADV_U; k++) a[k] = adv[pi[k]];
+#pragma unroll
+        for (int k = 0; k < ADV_U; k++) {
+            const uint32_t i = b + k * ADV_THREADS;
+            if (i >= i1) continue;
+            const double d = (double)a[k];
+            if (mb_of(i, sp) != m0) { s[1] += d; q[1] += d * d; mn[1] = fminf(mn[1], a[k]); mx[1] = fmaxf(mx[1], a[k]); }
+            else { s[0] += d; q[0] += d * d; mn[0] = fminf(mn[0], a[k]); mx[0] = fmaxf(mx[0], a[k]); }
+        }
     }
+    // wave reduction, then the block's waves in order (deterministic)
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
     for (int k = 0; k < 2; k++) {
-        ss[k][threadIdx.x] = s[k]; sq[k][threadIdx.x] = q[k]; smn[k][threadIdx.x] = mn[k]; smx[k][threadIdx.x] = mx[k];
+        double x = s[k], y = q[k];
+        float u = mn[k], v = mx[k];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            x += __shfl_xor(x, o, 64); y += __shfl_xor(y, o, 64);
+            u = fminf(u, __shfl_xor(u, o, 64)); v = fmaxf(v, __shfl_xor(v, o, 64));
+        }
+        if (lane == 0) { red[w][k][0] = x; red[w][k][1] = y; red[w][k][2] = u; red[w][k][3] = v; }
     }
     __syncthreads();
-    for (int st = 128; st > 0; st >>= 1) {
-        if (threadIdx.x < st)
-            for (int k = 0; k < 2; k++) {
-                ss[k][threadIdx.x] += ss[k][threadIdx.x + st];
-                sq[k][threadIdx.x] += sq[k][threadIdx.x + st];
-                smn[k][threadIdx.x] = fminf(smn[k][threadIdx.x], smn[k][threadIdx.x + st]);
-                smx[k][threadIdx.x] = fmaxf(smx[k][threadIdx.x], smx[k][threadIdx.x + st]);
-            }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0)
-        for (int k = 0; k < 2; k++) {
-            double *o = part + ((size_t)blockIdx.x * 2 + k) * 4;
-            o[0] = ss[k][0]; o[1] = sq[k][0]; o[2] = smn[k][0]; o[3] = smx[k][0];
+    if (threadIdx.x < 2) {
+        const int k = threadIdx.x;
+        double x = 0.0, y = 0.0, u = INFINITY, v = -INFINITY;
+        for (int ww = 0; ww < ADV_THREADS / 64; ww++) {
+            x += red[ww][k][0]; y += red[ww][k][1]; u = fmin(u, red[ww][k][2]); v = fmax(v, red[ww][k][3]);
         }
+        double *o = part + ((size_t)blockIdx.x * 2 + k) * 4;
+        o[0] = x; o[1] = y; o[2] = u; o[3] = v;
+    }
 }
 // one block per minibatch: its rows' partials in block order -> [mean, std, min, max]
 __global__ void __launch_bounds__(256) k_adv_epoch_final(const double *part, int nblk, uint32_t C, EpochSplit sp,
@@ -928,13 +946,13 @@ __global__ void __launch_bounds__(256) k_adv_epoch_final(const double *part, int
 }
 
 bppo_status launch_epoch_adv_stats(bppo_ctx *c, uint32_t B, int M) {
-    EpochSplit sp{B, B / (uint32_t)M, B % (uint32_t)M, (uint32_t)M};
+    const EpochSplit sp{B, B / (uint32_t)M, B % (uint32_t)M, (uint32_t)M};
     uint32_t C = (B + 511) / 512;
     if (sp.base > 0 && C > sp.base) C = sp.base;
     if (sp.base == 0) C = 1;
     const uint32_t nblk = (B + C - 1) / C;
     if ((size_t)nblk * 8 > 4 * 1024 + 64) { c->err = "epoch advantage stats: too many minibatches"; return BPPO_ERR_UNSUPPORTED; }
-    hipLaunchKernelGGL(k_adv_epoch, dim3(nblk), dim3(256), 0, c->stream, c->d_adv, c->d_perm, sp, C, c->d_red);
+    hipLaunchKernelGGL(k_adv_epoch, dim3(nblk), dim3(ADV_THREADS), 0, c->stream, c->d_adv, c->d_perm, sp, C, c->d_red);
     hipLaunchKernelGGL(k_adv_epoch_final, dim3(M), dim3(256), 0, c->stream, c->d_red, (int)nblk, C, sp, c->d_mb_stats);
     BPPO_HIP(c, hipGetLastError());
     return BPPO_OK;

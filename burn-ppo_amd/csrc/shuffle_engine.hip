@@ -66,80 +66,90 @@ __global__ void k_chacha_words(Key8 key, uint64_t stream, uint64_t base, uint64_
 }
 
 // J from walk segments.  Segments are consecutive pieces of the epoch's chain
-// (segment i covers words [pos0, pos1) from range r0; segment i+1 starts where it
-// ends), so a block takes XJ_SEG consecutive segments: it stages their words in
-// LDS with coalesced loads (from the jobs' device word buffers when a region holds
-// them, else ChaCha12 here), one lane per segment re-walks its piece and writes
-// J[r-1] = hi(w * r) for every ACCEPTED word into an LDS copy of the block's J
-// range (each r is accepted exactly once), and the block stores that range with
-// coalesced writes.  Short-lived blocks: the copy stream's J expansion holds CUs
-// for microseconds, not for the whole epoch's walk.
+// (segment i covers words [pos0, pos1) from range r0), one lane per segment: the
+// lane streams its words 16 at a time (the next 16 prefetched while it walks the
+// current ones) from the jobs' device word buffers when a region holds them,
+// else ChaCha12 here, and writes J[r-1] = hi(w * r) for every ACCEPTED word (each
+// r is accepted exactly once in the epoch, so lanes never write the same J).  The
+// zone follows r by subtraction (z -= 2^lz per accept; lz re-derived only when r
+// crosses a power of two), so the per-word chain is mul -> compare -> subtract.
+// No LDS and a handful of VGPRs: the blocks fit beside the update kernels'
+// resident blocks instead of waiting for whole CUs.
 struct WordRegions {
     const uint32_t *ptr[4];
     uint64_t base[4], len[4];
     int n;
 };
-constexpr int XJ_SEG = 16;                           // segments per block
 constexpr int XJ_THREADS = 64;
-constexpr size_t XJ_WORDS = XJ_SEG * SHUF_CK + 32;   // staged words (16-word aligned window)
-constexpr size_t XJ_LDS = sizeof(uint32_t) * (XJ_WORDS + XJ_SEG * SHUF_CK);
+
+__device__ __forceinline__ void xj_fetch(const Key8 &key, uint64_t stream, const WordRegions &wr, uint64_t q,
+                                         uint32_t (&w)[16]) {
+    const uint32_t *src = nullptr;
+    for (int k = 0; k < wr.n; k++)
+        if (q >= wr.base[k] && q + 16 <= wr.base[k] + wr.len[k]) src = wr.ptr[k] + (q - wr.base[k]);
+    if (src && (((uintptr_t)src & 15) == 0)) {
+        const uint4 *v = reinterpret_cast<const uint4 *>(src);
+        const uint4 a0 = v[0], a1 = v[1], a2 = v[2], a3 = v[3];
+        w[0] = a0.x; w[1] = a0.y; w[2] = a0.z; w[3] = a0.w; w[4] = a1.x; w[5] = a1.y; w[6] = a1.z; w[7] = a1.w;
+        w[8] = a2.x; w[9] = a2.y; w[10] = a2.z; w[11] = a2.w; w[12] = a3.x; w[13] = a3.y; w[14] = a3.z; w[15] = a3.w;
+    } else if (src) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) w[i] = src[i];
+    } else {
+        chacha12_block(key, q >> 4, stream, w);
+    }
+}
+
+// 64 words (4 blocks) per turn, the next 64 loaded while this turn walks: the
+// J stores share the vmcnt counter with those loads (gfx9 counts both, in order),
+// so the wait for a turn's words covers only the stores of the turn before it,
+// issued ~64 walk steps earlier, not the stores just made
+constexpr int XJ_NB = 4;
 __global__ void __launch_bounds__(XJ_THREADS) k_expand_J(Key8 key, uint64_t stream, const ShuffleEngine::Seg *segs,
                                                          int ns, WordRegions wr, uint32_t *J) {
-    extern __shared__ uint32_t xj[];
-    uint32_t *words = xj, *jst = xj + XJ_WORDS;
-    const int tid = threadIdx.x;
-    const int s0 = blockIdx.x * XJ_SEG, s1 = min(ns, s0 + XJ_SEG);
-    if (blockIdx.x == 0 && tid == 0) J[0] = 0;
-    if (s0 >= ns) return;
-    const uint64_t p0 = segs[s0].pos0, p1 = segs[s1 - 1].pos1;
-    const uint32_t hi = segs[s0].r0, lo = s1 < ns ? segs[s1].r0 : 1u;   // J[lo .. hi) is this block's
-    const uint64_t wb = p0 >> 4 << 4;                                    // window base (block aligned)
-    const uint64_t nblk = (p1 - wb + 15) >> 4;
-    for (uint64_t b = tid; b < nblk; b += XJ_THREADS) {                 // 16 words per thread and turn
-        const uint64_t q = wb + b * 16;
-        const uint32_t *src = nullptr;
-        for (int k = 0; k < wr.n; k++)
-            if (q >= wr.base[k] && q + 16 <= wr.base[k] + wr.len[k]) src = wr.ptr[k] + (q - wr.base[k]);
-        uint4 *dst = reinterpret_cast<uint4 *>(words + b * 16);
-        if (src && (((uintptr_t)src & 15) == 0)) {
-            const uint4 *v = reinterpret_cast<const uint4 *>(src);
-            dst[0] = v[0]; dst[1] = v[1]; dst[2] = v[2]; dst[3] = v[3];
-        } else if (src) {
-            for (int i = 0; i < 16; i++) words[b * 16 + i] = src[i];
-        } else {
-            uint32_t blk[16];
-            chacha12_block(key, q >> 4, stream, blk);
-            dst[0] = make_uint4(blk[0], blk[1], blk[2], blk[3]);
-            dst[1] = make_uint4(blk[4], blk[5], blk[6], blk[7]);
-            dst[2] = make_uint4(blk[8], blk[9], blk[10], blk[11]);
-            dst[3] = make_uint4(blk[12], blk[13], blk[14], blk[15]);
-        }
-    }
-    __syncthreads();
-    if (s0 + tid < s1) {
-        const ShuffleEngine::Seg g = segs[s0 + tid];
-        uint32_t r = g.r0;
-        auto step = [&](uint32_t w) {
-            const uint64_t m = (uint64_t)w * r;
-            const uint32_t z = (r << __clz(r)) - 1u;
-            if ((uint32_t)m <= z) { jst[hi - r] = (uint32_t)(m >> 32); r--; }
-        };
-        // words 16 at a time (four 16-byte LDS reads ahead of the chain), head and
-        // tail one by one; absolute position p sits at words[p - wb] (wb 16-aligned)
-        uint64_t p = g.pos0;
-        while (p < g.pos1 && (p & 15) && r >= 2) step(words[p++ - wb]);
-        for (; p + 16 <= g.pos1 && r >= 2; p += 16) {
-            const uint4 *v = reinterpret_cast<const uint4 *>(words + (p - wb));
-            const uint4 a0 = v[0], a1 = v[1], a2 = v[2], a3 = v[3];
-            const uint32_t w16[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
-                                      a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+    const int si = blockIdx.x * XJ_THREADS + threadIdx.x;
+    if (si == 0) J[0] = 0;
+    if (si >= ns) return;
+    const ShuffleEngine::Seg g = segs[si];
+    uint32_t r = g.r0;
+    if (r < 2 || g.pos1 <= g.pos0) return;
+    int lz = __clz(r);
+    uint32_t lowr = 1u << (31 - lz), sh = 1u << lz, z = (r << lz) - 1u;
+    constexpr uint64_t TW = 16 * XJ_NB;
+    uint64_t q = g.pos0 & ~(uint64_t)15;
+    uint32_t cur[XJ_NB][16], nxt[XJ_NB][16];
 #pragma unroll
-            for (int j = 0; j < 16; j++) if (r >= 2) step(w16[j]);
-        }
-        for (; p < g.pos1 && r >= 2; p++) step(words[p - wb]);
+    for (int k = 0; k < XJ_NB; k++)
+        if (q + 16 * k < g.pos1) xj_fetch(key, stream, wr, q + 16 * k, cur[k]);
+    uint32_t j0 = (uint32_t)(g.pos0 - q);
+    while (q < g.pos1 && r >= 2) {
+        const uint64_t qn = q + TW;
+#pragma unroll
+        for (int k = 0; k < XJ_NB; k++)
+            if (qn + 16 * k < g.pos1) xj_fetch(key, stream, wr, qn + 16 * k, nxt[k]);
+        const uint32_t j1 = (uint32_t)min(TW, g.pos1 - q);
+#pragma unroll
+        for (int k = 0; k < XJ_NB; k++)
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                const uint32_t jj = (uint32_t)(16 * k + j);
+                if (jj >= j0 && jj < j1 && r >= 2) {
+                    const uint64_t m = (uint64_t)cur[k][j] * r;
+                    if ((uint32_t)m <= z) {
+                        J[r - 1] = (uint32_t)(m >> 32);
+                        r--;
+                        z -= sh;
+                        if (r < lowr) { lz = __clz(r); lowr = 1u << (31 - lz); sh = 1u << lz; z = (r << lz) - 1u; }
+                    }
+                }
+            }
+#pragma unroll
+        for (int k = 0; k < XJ_NB; k++)
+#pragma unroll
+            for (int j = 0; j < 16; j++) cur[k][j] = nxt[k][j];
+        j0 = 0;
+        q = qn;
     }
-    __syncthreads();
-    for (uint32_t k = tid; k < hi - lo; k += XJ_THREADS) J[hi - 1 - k] = jst[k];
 }
 
 // expected words per shuffle of n and its std dev: draw with range R accepts with
@@ -640,8 +650,8 @@ void ShuffleEngine::run() {
                     }
                 Seg *dS = d_seg[slot] + (size_t)e * maxseg;
                 (void)hipMemcpyAsync(dS, S, sizeof(Seg) * (size_t)std::max(ns, 1), hipMemcpyHostToDevice, copy);
-                hipLaunchKernelGGL(k_expand_J, dim3((unsigned)((std::max(ns, 1) + XJ_SEG - 1) / XJ_SEG)),
-                                   dim3(XJ_THREADS), XJ_LDS, copy, key, stream, (const Seg *)dS, ns, wr,
+                hipLaunchKernelGGL(k_expand_J, dim3((unsigned)((std::max(ns, 1) + XJ_THREADS - 1) / XJ_THREADS)),
+                                   dim3(XJ_THREADS), 0, copy, key, stream, (const Seg *)dS, ns, wr,
                                    d_J[slot] + (size_t)e * n);
             }
             end_pos[slot][e] = pos;
