@@ -63,6 +63,22 @@ __device__ __forceinline__ uint32_t chacha12_word(const Key8 &key, uint64_t stre
 }
 
 // sequential reader (BlockRng semantics) caching the current block in registers
+// slot of this lane's episode record: one atomicAdd per wave for all of its
+// lanes that finished an episode this step (a per-lane atomic on the one counter
+// serialises ~N/20 atomics per step early in training).  Call with every lane
+// that may be done active; returns -1 for lanes that are not done.  Record order
+// in the buffer is not part of the contract (bppo_rollout_episodes sorts).
+__device__ __forceinline__ int32_t wave_episode_slot(bool done, int32_t *count) {
+    const uint64_t m = (uint64_t)__ballot(done ? 1 : 0);
+    if (m == 0) return -1;
+    const int lane = (int)__lane_id();
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    int32_t base = 0;
+    if (lane == leader) base = atomicAdd(count, (int32_t)__popcll(m));
+    base = __shfl(base, leader, 64);
+    return done ? base + (int32_t)__popcll(m & ((1ull << lane) - 1ull)) : -1;
+}
+
 struct WordCursor {
     Key8 key;
     uint64_t stream, pos, cached;

@@ -178,8 +178,8 @@ __global__ void __launch_bounds__(256) k_cartpole_rollout(RolloutArgs a) {
         const bool done = cartpole_step(s, act, r);
         ep_ret = __fadd_rn(ep_ret, r);
         ep_len += 1;
+        const int32_t k = wave_episode_slot(done, a.ep_count);
         if (done) {
-            int32_t k = atomicAdd(a.ep_count, 1);
             if (k < a.eps_cap) {
                 EpisodeRec rec;
                 rec.total_reward[0] = ep_ret;
@@ -319,16 +319,24 @@ __global__ void __launch_bounds__(512, 2) k_cartpole_rollout_mfma(RolloutArgs a,
                 B.T[cd_row(q, h) * RS + c + 32 * ct] = v > 0.0f ? v : 0.0f;
             }
         wave_sync();
-        if (mine) {
-            float l0 = 0.0f, l1 = 0.0f, vv = 0.0f;
+        // heads: lane half h runs the k-ordered chain of logit h, both run the value
+        // chain (two chains per lane instead of three on the low half alone; each
+        // chain is the same fma sequence, so the values are bit-identical)
+        float lh = 0.0f, vv = 0.0f;
+        if (e < N) {
             const float *hr = B.T + c * RS;
+            const float2 *pv = S.PV[h];
 #pragma unroll 16
             for (int k = 0; k < H; k++) {
                 const float hk = hr[k];
-                l0 = __builtin_fmaf(hk, S.Wp[2 * k], l0);
-                l1 = __builtin_fmaf(hk, S.Wp[2 * k + 1], l1);
-                vv = __builtin_fmaf(hk, S.Wv[k], vv);
+                const float2 w = pv[k];
+                lh = __builtin_fmaf(hk, w.x, lh);
+                vv = __builtin_fmaf(hk, w.y, vv);
             }
+        }
+        const float lx = __shfl_xor(lh, 32, 64);
+        if (mine) {
+            const float l0 = lh, l1 = lx;
             float lg[2];
             lg[0] = __fadd_rn(l0, S.bp[0]);
             lg[1] = __fadd_rn(l1, S.bp[1]);
@@ -342,8 +350,8 @@ __global__ void __launch_bounds__(512, 2) k_cartpole_rollout_mfma(RolloutArgs a,
             const bool done = cartpole_step(s, act, r);
             ep_ret = __fadd_rn(ep_ret, r);
             ep_len += 1;
+            const int32_t k = wave_episode_slot(done, a.ep_count);
             if (done) {
-                const int32_t k = atomicAdd(a.ep_count, 1);
                 if (k < a.eps_cap) {
                     EpisodeRec rec;
                     rec.total_reward[0] = ep_ret;
@@ -386,8 +394,8 @@ __global__ void k_cartpole_step(int N, uint64_t seed_base, float *cp, int32_t *s
     bool done = cartpole_step(s, actions[e], r);
     float er = __fadd_rn(ep_ret[e], r);
     int32_t el = ep_len[e] + 1;
+    const int32_t k = wave_episode_slot(done, ep_count);
     if (done) {
-        int32_t k = atomicAdd(ep_count, 1);
         if (k < cap) {
             EpisodeRec rec;
             rec.total_reward[0] = er;

@@ -145,8 +145,8 @@ __global__ void k_wide_step(WideStepArgs a) {
     if (a.rew_act) a.rew_act[e] = r[p_act];
     if (a.done_f) a.done_f[e] = done ? 1.0f : 0.0f;
     if (a.done_u8) a.done_u8[e] = (uint8_t)done;
+    const int slot = wave_episode_slot(done != 0, a.ep_count);
     if (done) {
-        const int slot = atomicAdd(a.ep_count, 1);
         if (slot < a.eps_cap) {
             EpisodeRec rec;
             for (int p = 0; p < BPPO_MAX_PLAYERS; p++) rec.total_reward[p] = p < E::P ? er[p] : 0.0f;
