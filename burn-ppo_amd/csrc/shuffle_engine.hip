@@ -103,16 +103,27 @@ __device__ __forceinline__ void xj_fetch(const Key8 &key, uint64_t stream, const
 // 64 words (4 blocks) per turn, the next 64 loaded while this turn walks: the
 // J stores share the vmcnt counter with those loads (gfx9 counts both, in order),
 // so the wait for a turn's words covers only the stores of the turn before it,
-// issued ~64 walk steps earlier, not the stores just made
+// issued ~64 walk steps earlier, not the stores just made.
+// Word slices: one launch walks words [w0, w1) of every segment and leaves the
+// range r for the next slice in rst[] — blocks live ~1/8 of a segment walk, so
+// the copy stream never holds a CU for long against the update kernels (which
+// leave no room beside their own resident blocks).
 constexpr int XJ_NB = 4;
+constexpr int XJ_TRASH = 4096;                       // u32 slots rejected words store to
+constexpr uint32_t XJ_SLICE = 128;                   // words per segment per launch
 __global__ void __launch_bounds__(XJ_THREADS) k_expand_J(Key8 key, uint64_t stream, const ShuffleEngine::Seg *segs,
-                                                         int ns, WordRegions wr, uint32_t *J) {
+                                                         int ns, WordRegions wr, uint32_t *J, uint32_t *trash_buf,
+                                                         uint32_t w0, uint32_t w1, uint32_t *rst) {
     const int si = blockIdx.x * XJ_THREADS + threadIdx.x;
-    if (si == 0) J[0] = 0;
+    uint32_t *trash = trash_buf + (si & (XJ_TRASH - 1));
+    if (si == 0 && w0 == 0) J[0] = 0;
     if (si >= ns) return;
-    const ShuffleEngine::Seg g = segs[si];
-    uint32_t r = g.r0;
-    if (r < 2 || g.pos1 <= g.pos0) return;
+    ShuffleEngine::Seg g = segs[si];
+    uint32_t r = w0 == 0 ? g.r0 : rst[si];
+    const uint64_t e1 = min(g.pos1, g.pos0 + w1);
+    g.pos0 += w0;
+    g.pos1 = e1;
+    if (r < 2 || g.pos1 <= g.pos0) { rst[si] = r; return; }
     int lz = __clz(r);
     uint32_t lowr = 1u << (31 - lz), sh = 1u << lz, z = (r << lz) - 1u;
     constexpr uint64_t TW = 16 * XJ_NB;
@@ -128,6 +139,21 @@ __global__ void __launch_bounds__(XJ_THREADS) k_expand_J(Key8 key, uint64_t stre
         for (int k = 0; k < XJ_NB; k++)
             if (qn + 16 * k < g.pos1) xj_fetch(key, stream, wr, qn + 16 * k, nxt[k]);
         const uint32_t j1 = (uint32_t)min(TW, g.pos1 - q);
+        // interior turn (all TW words inside the segment, r stays in this lz band and
+        // >= 2): no per-word predicates or branches — every word stores, an accepted
+        // one to J[r-1], a rejected one to this lane's trash slot (address select)
+        if (j0 == 0 && j1 == (uint32_t)TW && r >= lowr + (uint32_t)TW && r >= (uint32_t)TW + 2u) {
+#pragma unroll
+            for (int k = 0; k < XJ_NB; k++)
+#pragma unroll
+                for (int j = 0; j < 16; j++) {
+                    const uint64_t m = (uint64_t)cur[k][j] * r;
+                    const bool acc = (uint32_t)m <= z;
+                    *(acc ? J + (r - 1) : trash) = (uint32_t)(m >> 32);
+                    r -= acc ? 1u : 0u;
+                    z -= acc ? sh : 0u;
+                }
+        } else {
 #pragma unroll
         for (int k = 0; k < XJ_NB; k++)
 #pragma unroll
@@ -143,6 +169,7 @@ __global__ void __launch_bounds__(XJ_THREADS) k_expand_J(Key8 key, uint64_t stre
                     }
                 }
             }
+        }
 #pragma unroll
         for (int k = 0; k < XJ_NB; k++)
 #pragma unroll
@@ -150,6 +177,7 @@ __global__ void __launch_bounds__(XJ_THREADS) k_expand_J(Key8 key, uint64_t stre
         j0 = 0;
         q = qn;
     }
+    rst[si] = r;
 }
 
 // expected words per shuffle of n and its std dev: draw with range R accepts with
@@ -210,6 +238,11 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
             err = "shuffle events: creation failed";
             return BPPO_ERR_HIP;
         }
+    if (hipMalloc((void **)&d_trash, sizeof(uint32_t) * XJ_TRASH) != hipSuccess ||
+        hipMalloc((void **)&d_xj_r, sizeof(uint32_t) * (size_t)maxseg) != hipSuccess) {
+        err = "shuffle trash buffer: allocation failed";
+        return BPPO_ERR_HIP;
+    }
     int prio_lo = 0, prio_hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
     if (hipStreamCreateWithPriority(&copy, hipStreamNonBlocking, prio_lo) != hipSuccess) {   // lowest priority
@@ -650,9 +683,11 @@ void ShuffleEngine::run() {
                     }
                 Seg *dS = d_seg[slot] + (size_t)e * maxseg;
                 (void)hipMemcpyAsync(dS, S, sizeof(Seg) * (size_t)std::max(ns, 1), hipMemcpyHostToDevice, copy);
-                hipLaunchKernelGGL(k_expand_J, dim3((unsigned)((std::max(ns, 1) + XJ_THREADS - 1) / XJ_THREADS)),
-                                   dim3(XJ_THREADS), 0, copy, key, stream, (const Seg *)dS, ns, wr,
-                                   d_J[slot] + (size_t)e * n);
+                static const uint32_t slice = getenv("BPPO_XJ_SLICE") ? (uint32_t)atoi(getenv("BPPO_XJ_SLICE")) : XJ_SLICE;
+                for (uint32_t w0 = 0; w0 < (uint32_t)SHUF_CK; w0 += slice)
+                    hipLaunchKernelGGL(k_expand_J, dim3((unsigned)((std::max(ns, 1) + XJ_THREADS - 1) / XJ_THREADS)),
+                                       dim3(XJ_THREADS), 0, copy, key, stream, (const Seg *)dS, ns, wr,
+                                       d_J[slot] + (size_t)e * n, d_trash, w0, w0 + slice, d_xj_r);
             }
             end_pos[slot][e] = pos;
             (void)hipEventRecord(ev[slot][e], copy);
@@ -706,6 +741,8 @@ void ShuffleEngine::shutdown() {
         gens.clear();
     }
     if (copy) { (void)hipStreamSynchronize(copy); (void)hipStreamDestroy(copy); copy = nullptr; }
+    if (d_trash) { (void)hipFree(d_trash); d_trash = nullptr; }
+    if (d_xj_r) { (void)hipFree(d_xj_r); d_xj_r = nullptr; }
     for (int s = 0; s < 2; s++) {
         if (consumed[s]) { (void)hipEventDestroy(consumed[s]); consumed[s] = nullptr; }
         for (int e = 0; e < epochs; e++) if (ev[s][e]) { (void)hipEventDestroy(ev[s][e]); ev[s][e] = nullptr; }
