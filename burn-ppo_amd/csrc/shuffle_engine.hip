@@ -328,8 +328,20 @@ void ShuffleEngine::release(int slot, hipStream_t st) {
 
 // words [pos, pos + len) of word buffer b (one checkpoint piece: never crosses a
 // chunk); outside its regions (not at the usual sizes) they are made here
+// BPPO_SHUFFLE_SELFGEN=1: every walk makes its own words piece by piece (no
+// producer threads, no pinned-buffer streaming: L1-resident words, more ChaCha work)
+static bool shuf_selfgen() {
+    static const int v = getenv("BPPO_SHUFFLE_SELFGEN") ? atoi(getenv("BPPO_SHUFFLE_SELFGEN")) : 0;
+    return v != 0;
+}
+
 const uint32_t *ShuffleEngine::words(int b, uint64_t pos, uint64_t len, std::vector<uint32_t> &scratch) {
     WordBuf &w = wb[b];
+    if (shuf_selfgen()) {
+        scratch.resize(len);
+        bppo_host::chacha12_words(key.k, stream, pos, scratch.data(), len);
+        return scratch.data();
+    }
     for (int g = 0; g < w.nreg; g++) {
         const WordBuf::Region &R = w.reg[g];
         if (pos >= R.base && pos + len <= R.base + R.len) {
@@ -564,7 +576,7 @@ void ShuffleEngine::run() {
                 const WordBuf::Region *R = nullptr;
                 for (int g = 0; g < W.nreg; g++)
                     if (c * SHUF_CHUNK >= W.reg[g].off && c * SHUF_CHUNK < W.reg[g].off + W.reg[g].len) R = &W.reg[g];
-                if (R) gen_order.push_back({R->base + (c * SHUF_CHUNK - R->off), c});
+                if (R && !shuf_selfgen()) gen_order.push_back({R->base + (c * SHUF_CHUNK - R->off), c});
             }
             gen_buf = &W;
             gen_next.store(0, std::memory_order_relaxed);
@@ -603,24 +615,48 @@ void ShuffleEngine::run() {
             else { s0 = cur0 + (e - C) * K; s1 = s0 + K; }
             tck.clear();
             tck.push_back({pos, r});
+            // The true walk never waits on a speculative walk: at each checkpoint it
+            // compares only with the candidates already past it (one that lags would
+            // gain nothing).  After a meet it keeps walking itself and leapfrogs to the
+            // met chain's recorded states whenever that chain is ahead, so the epoch
+            // closes at the earlier of its own walk and the chain's end.
+            int fin = -1;                              // chain walk whose end closes the epoch
+            uint64_t endp = 0;
             while (r >= 2) {
+                if (met >= 0) {
+                    if (cancel.load(std::memory_order_relaxed) || quit) { cancelled = true; break; }
+                    int f = met;                       // the chain's current last walk
+                    for (int mt; (mt = spec[f].merged_to.load(std::memory_order_acquire)) >= 0;) f = mt;
+                    const bool chain_done = spec[f].done.load(std::memory_order_acquire) != 0 &&
+                                            spec[f].merged_to.load(std::memory_order_acquire) < 0;
+                    uint32_t rr = 0;
+                    for (uint64_t q = (pos / SHUF_CK + 1) * SHUF_CK; r >= 2 && peek(met, q, &rr) == 1; q += SHUF_CK) {
+                        tck.push_back({q, rr});
+                        pos = q;
+                        r = rr;
+                    }
+                    if (r < 2) break;
+                    if (chain_done && spec[f].end > pos && spec[f].end - pos <= SHUF_CK) {
+                        fin = f;
+                        endp = spec[f].end;
+                        break;
+                    }
+                }
                 const uint64_t q = (pos / SHUF_CK + 1) * SHUF_CK;
                 pos = walk_piece(b, pos, &r, scratch);
                 if (cancel.load(std::memory_order_relaxed)) { cancelled = true; break; }
                 if (pos != q || r < 2) continue;
                 tck.push_back({q, r});
-                if (s0 == s1) continue;
+                if (met >= 0 || s0 == s1) continue;
                 walked++;
                 for (int i = s0; i < s1 && met < 0; i++) {
-                    // wait until that walk (or the one it coalesced with) has passed q
                     uint32_t rs = 0;
-                    int st;
-                    // (sleep, not spin: the process runs under a CPU quota that spinning eats)
-                    while ((st = peek(i, q, &rs)) == 0 && !cancel.load(std::memory_order_relaxed))
-                        std::this_thread::sleep_for(std::chrono::microseconds(20));
-                    if (st == 1 && rs == r) met = i;
+                    if (peek(i, q, &rs) == 1 && rs == r) met = i;
                 }
-                if (met >= 0) break;
+                // walks right of the met one can never carry its states (walks only
+                // coalesce leftwards): free their CPUs
+                if (met >= 0)
+                    for (int i = met + 1; i < s1; i++) spec[i].stop.store(true, std::memory_order_relaxed);
             }
             if (cancelled) break;
             Seg *S = seg_host[slot] + (size_t)e * maxseg;
@@ -632,40 +668,9 @@ void ShuffleEngine::run() {
                 S[ns++] = Seg{p0, p1, r0, 0};
             };
             for (size_t i = 0; i + 1 < tck.size(); i++) add(tck[i].first, tck[i + 1].first, tck[i].second);
-            if (met >= 0) {
-                // the other walks of this boundary cannot serve any more: free their CPUs
-                // for the met one (it still has to finish the epoch) and the later epochs
-                // (walks only coalesce leftwards, so the ones right of the met walk
-                // can never carry its states)
-                for (int i = met + 1; i < s1; i++) spec[i].stop.store(true, std::memory_order_relaxed);
-                // the walk that finishes the epoch: follow the links until one ends on its own
-                int fin = met;
-                for (;;) {
-                    SpecWalk &sp = spec[fin];
-                    {
-                        std::unique_lock<std::mutex> lk(mu);
-                        cv.wait(lk, [&] {
-                            return sp.done.load(std::memory_order_acquire) || cancel.load(std::memory_order_relaxed) || quit;
-                        });
-                    }
-                    const int mt = sp.merged_to.load(std::memory_order_acquire);
-                    if (mt < 0 || cancel.load(std::memory_order_relaxed)) break;
-                    fin = mt;
-                }
-                if (cancel.load(std::memory_order_relaxed)) { cancelled = true; break; }
-                // from the meeting checkpoint on, the speculative walks' states
-                const uint64_t endp = spec[fin].end;
-                for (uint64_t q0 = tck.back().first; q0 < endp; q0 += SHUF_CK) {
-                    uint32_t r0 = 0;
-                    if (peek(met, q0, &r0) != 1) { overflow = true; break; }   // cannot happen: all walks done
-                    add(q0, std::min(q0 + SHUF_CK, endp), r0);
-                }
-                pos = endp;
-                coalesced[slot][e] = walked;
-            } else {
-                add(tck.back().first, pos, tck.back().second);
-                coalesced[slot][e] = -1;
-            }
+            if (fin >= 0) pos = endp;                  // the chain's last piece closes the epoch
+            add(tck.back().first, pos, tck.back().second);
+            coalesced[slot][e] = met >= 0 ? walked : -1;
             if (overflow) {   // never at sane sizes: fall back to the sequential walk of the epoch
                 std::vector<uint32_t> Jh(n);
                 const uint64_t e0 = shuffle_walk_host(key, stream, tck.front().first, n, Jh.data());
