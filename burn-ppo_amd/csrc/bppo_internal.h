@@ -70,6 +70,7 @@ struct SpecWalk {
     std::atomic<int> merged_to{-1};               // left neighbour it coalesced with (then stopped)
     uint64_t merge_q = 0;                         // word position of that checkpoint (set before merged_to)
     uint64_t gen = 0;                             // assignment counter (the worker follows it)
+    uint64_t job = 0;                             // engine job (seq) that launched it
     bool running = false;                         // guarded by the engine mutex
 };
 
@@ -118,6 +119,14 @@ struct ShuffleEngine {
     SpecWalk spec[SHUF_MAX_SPEC];
     int nspec = 0, ncur = 0;
     int C = 1;                                    // leading epochs of the next job speculated during this one
+    // exact continuations: when a walk of this job's last epoch finishes that epoch
+    // at word x, a walk of the next job's first epoch starts at x + gap — exactly
+    // where the next job starts whenever the true walk met that chain.  Two sets of
+    // K slots (by job parity) after the carry groups.
+    int cont0 = 0;                                // first continuation slot (0: none)
+    bool cont_valid[2] = {false, false};
+    int cont_src0 = -1, cont_dst0 = -1, cont_wb = 0;   // this job's last-epoch group -> its set (mu)
+    uint64_t cont_seq = 0;
     std::vector<std::thread> workers;
     // host word producers: the job's ChaCha12 words into the pinned word buffer,
     // chunk by chunk in the order the walks need them (no device -> host copies)

@@ -214,9 +214,15 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
     // get a whole job of head start; later epochs' walks start with their job)
     C = std::min(2, std::max(epochs, 1));
     if (const char *e = getenv("BPPO_SHUFFLE_CARRY")) C = std::max(1, std::min(epochs, atoi(e)));
-    K = std::min(K, SHUF_MAX_SPEC / (std::max(epochs - C, 0) + 2 * C));
+    // exact continuations need the last epoch in the in-job groups (BPPO_SHUFFLE_CONT=0: off)
+    const bool cont_on = (getenv("BPPO_SHUFFLE_CONT") ? atoi(getenv("BPPO_SHUFFLE_CONT")) : 1) != 0 && epochs - 1 >= C;
+    K = std::min(K, SHUF_MAX_SPEC / (std::max(epochs - C, 0) + 2 * C + (cont_on ? 2 : 0)));
     ncur = K * std::max(epochs - C, 0);
     nspec = ncur + 2 * C * K;
+    if (cont_on && K > 0) {
+        cont0 = nspec;
+        nspec += 2 * K;
+    }
     const size_t bytes = sizeof(uint32_t) * (size_t)n * epochs;
     maxseg = (int)((Ew + 48.0 * sigma) / SHUF_CK) + 16;
     const size_t sbytes = sizeof(Seg) * (size_t)maxseg * epochs;
@@ -379,6 +385,7 @@ void ShuffleEngine::launch_walk(int i, uint64_t start, int wbuf) {
     s.merge_q = 0;
     s.done.store(0, std::memory_order_release);
     s.running = true;
+    s.job = seq;
     s.gen++;
 }
 
@@ -458,6 +465,12 @@ void ShuffleEngine::worker(int i) {
             std::lock_guard<std::mutex> lk(mu);
             s.done.store(1, std::memory_order_release);
             s.running = false;
+            // a walk of this job's last epoch that finished the epoch on its own: its
+            // exact continuation into the next job's first epoch
+            if (cont_dst0 >= 0 && s.job == cont_seq && i >= cont_src0 && i < cont_src0 + K && r < 2 &&
+                !s.stop.load(std::memory_order_relaxed) && s.merged_to.load(std::memory_order_relaxed) < 0 &&
+                !quit && !cancel.load(std::memory_order_relaxed))
+                launch_walk(cont_dst0 + (i - cont_src0), pos + gap, cont_wb);
         }
         cv.notify_all();
     }
@@ -529,6 +542,20 @@ void ShuffleEngine::run() {
                  slot, (int)carry_valid[cs]);
         // walks of two jobs ago still on this buffer / carry slots have stopped
         stop_walks(cn0, cn1);
+        const int ccn0 = cont0 ? cont0 + b * K : 0, ccp0 = cont0 ? cont0 + cs * K : 0;
+        if (cont0) {
+            stop_walks(ccn0, ccn0 + K);
+            std::lock_guard<std::mutex> lk(mu);
+            for (int i = ccn0; i < ccn0 + K; i++) {          // not launched yet: peek() says never
+                spec[i].start = ~0ull;
+                spec[i].merged_to.store(-1, std::memory_order_relaxed);
+            }
+            cont_src0 = cur0 + (epochs - 1 - C) * K;
+            cont_dst0 = ccn0;
+            cont_wb = b;
+            cont_seq = seq;
+            cont_valid[b] = K > 0;
+        }
         // ---- words: this job's epochs, then the region of the next job's first epoch
         WordBuf &W = wb[b];
         const double sE = sigma * std::sqrt((double)std::max(epochs, 1));
@@ -613,6 +640,8 @@ void ShuffleEngine::run() {
             int s0 = 0, s1 = 0;                        // candidate speculative walks for this epoch
             if (e < C) { if (carry_valid[cs]) { s0 = cp0 + e * K; s1 = s0 + K; } }
             else { s0 = cur0 + (e - C) * K; s1 = s0 + K; }
+            int c0 = 0, c1 = 0;                        // the previous job's exact continuations (epoch 0)
+            if (e == 0 && cont0 && cont_valid[cs]) { c0 = ccp0; c1 = ccp0 + K; }
             tck.clear();
             tck.push_back({pos, r});
             // The true walk never waits on a speculative walk: at each checkpoint it
@@ -647,16 +676,32 @@ void ShuffleEngine::run() {
                 if (cancel.load(std::memory_order_relaxed)) { cancelled = true; break; }
                 if (pos != q || r < 2) continue;
                 tck.push_back({q, r});
-                if (met >= 0 || s0 == s1) continue;
-                walked++;
-                for (int i = s0; i < s1 && met < 0; i++) {
-                    uint32_t rs = 0;
-                    if (peek(i, q, &rs) == 1 && rs == r) met = i;
+                if (s0 == s1 && c0 == c1) continue;
+                if (met < 0) walked++;
+                // candidates on our chain at q; keep (or switch to) the one furthest
+                // ahead — an exact continuation meets at once but started late, a
+                // guessed walk of the same chain may have a long head start
+                auto frontier = [&](int i) -> uint64_t {
+                    for (int mt; (mt = spec[i].merged_to.load(std::memory_order_acquire)) >= 0;) i = mt;
+                    const int64_t pr = spec[i].progress.load(std::memory_order_acquire);
+                    return pr < 0 ? 0 : spec[i].ck_base + (uint64_t)pr * SHUF_CK;
+                };
+                int best = met;
+                uint64_t bf = met >= 0 ? frontier(met) : 0;
+                for (int g = 0; g < 2; g++)
+                    for (int i = g ? s0 : c0; i < (g ? s1 : c1); i++) {
+                        uint32_t rs = 0;
+                        if (i == met || peek(i, q, &rs) != 1 || rs != r) continue;
+                        const uint64_t f = frontier(i);
+                        if (best < 0 || f > bf) { best = i; bf = f; }
+                    }
+                if (best != met) {
+                    met = best;
+                    // walks right of the met one in its group can never carry its
+                    // states (walks only coalesce leftwards): free their CPUs
+                    const int g1 = (met >= c0 && met < c1) ? c1 : s1;
+                    for (int i = met + 1; i < g1; i++) spec[i].stop.store(true, std::memory_order_relaxed);
                 }
-                // walks right of the met one can never carry its states (walks only
-                // coalesce leftwards): free their CPUs
-                if (met >= 0)
-                    for (int i = met + 1; i < s1; i++) spec[i].stop.store(true, std::memory_order_relaxed);
             }
             if (cancelled) break;
             Seg *S = seg_host[slot] + (size_t)e * maxseg;
@@ -706,6 +751,7 @@ void ShuffleEngine::run() {
             }
             cv.notify_all();
             if (K > 0) stop_walks(s0, s1);        // this epoch's walks have served
+            if (c1 > c0) { stop_walks(c0, c1); cont_valid[cs] = false; }
             if (e == C - 1) carry_valid[cs] = false;
         }
         SHUF_LOG("[shuf] job done cancelled=%d\n", (int)cancelled);
@@ -715,6 +761,7 @@ void ShuffleEngine::run() {
         if (cancelled) {
             stop_walks(0, nspec);
             carry_valid[0] = carry_valid[1] = false;
+            cont_valid[0] = cont_valid[1] = false;
         }
         {
             std::lock_guard<std::mutex> lk(mu);
