@@ -716,6 +716,42 @@ void ShuffleEngine::run() {
             if (fin >= 0) pos = endp;                  // the chain's last piece closes the epoch
             add(tck.back().first, pos, tck.back().second);
             coalesced[slot][e] = met >= 0 ? walked : -1;
+            // The next boundary is now known exactly (x).  Walks of one boundary never
+            // cross, so only the two started nearest x on either side can ever meet the
+            // true walk (any farther one meets it only through them); a walk started at
+            // x itself is the true chain.  Stop the rest and give their CPUs to those.
+            auto prune = [&](int g0, int g1, uint64_t x) {
+                int lo = -1, hi = -1, exact = -1;
+                for (int i = g0; i < g1; i++) {
+                    const uint64_t st = spec[i].start;
+                    if (st == ~0ull) continue;
+                    if (st == x) exact = i;
+                    if (st <= x && (lo < 0 || st > spec[lo].start)) lo = i;
+                    if (st > x && (hi < 0 || st < spec[hi].start)) hi = i;
+                }
+                // keep those walks and the walks their chains continue in (merge links)
+                bool keep[SHUF_MAX_SPEC] = {};
+                for (int k0 : {exact >= 0 ? exact : lo, exact >= 0 ? -1 : hi})
+                    for (int i = k0; i >= 0; i = spec[i].merged_to.load(std::memory_order_acquire)) keep[i] = true;
+                for (int i = g0; i < g1; i++)
+                    if (!keep[i]) spec[i].stop.store(true, std::memory_order_relaxed);
+                return exact;
+            };
+            static const bool prune_on = (getenv("BPPO_SHUFFLE_PRUNE") ? atoi(getenv("BPPO_SHUFFLE_PRUNE")) : 1) != 0;
+            if (prune_on && K > 0 && !cancelled) {
+                std::lock_guard<std::mutex> lk(mu);
+                if (e + 1 < epochs) {
+                    if (e + 1 < C) { if (carry_valid[cs]) prune(cp0 + (e + 1) * K, cp0 + (e + 2) * K, pos); }
+                    else prune(cur0 + (e + 1 - C) * K, cur0 + (e + 2 - C) * K, pos);
+                } else {
+                    // the next job's first epoch: an exact continuation makes the
+                    // guessed walks redundant
+                    const uint64_t x = pos + gap;
+                    const int ex = cont0 ? prune(ccn0, ccn0 + K, x) : -1;
+                    if (ex >= 0) for (int i = cn0; i < cn0 + K; i++) spec[i].stop.store(true, std::memory_order_relaxed);
+                    else prune(cn0, cn0 + K, x);
+                }
+            }
             if (overflow) {   // never at sane sizes: fall back to the sequential walk of the epoch
                 std::vector<uint32_t> Jh(n);
                 const uint64_t e0 = shuffle_walk_host(key, stream, tck.front().first, n, Jh.data());
