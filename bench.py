@@ -31,6 +31,7 @@ timing with gloo and no GPU work (the CPU test of the N>1 harness).
 import argparse
 import hashlib
 import json
+import resource
 import os
 import socket
 import subprocess
@@ -81,16 +82,37 @@ def launch_ranks(args):
     return subprocess.call(cmd, env=env)
 
 
+def cgroup_cpu_quota():
+    """CPUs the cgroup (v2 cpu.max) lets this process use, or None if unlimited/unknown."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        return None
+
+
+def thread_cpu_ms():
+    """CPU time (ms) of this process's threads summed by thread name (/proc task stat)."""
+    out = {}
+    tick = os.sysconf("SC_CLK_TCK")
+    for t in os.listdir("/proc/self/task"):
+        try:
+            st = open(f"/proc/self/task/{t}/stat").read()
+        except OSError:
+            continue
+        name = st[st.index("(") + 1:st.rindex(")")]
+        f = st[st.rindex(")") + 2:].split()
+        out[name] = out.get(name, 0.0) + (int(f[11]) + int(f[12])) * 1000.0 / tick
+    return out
+
+
 def host_cpu_budget(local_world):
     """CPUs this rank may use for the shuffle engine's host threads: the CPUs
     the process may run on (affinity, cgroup quota) / ranks on this node."""
     n = len(os.sched_getaffinity(0))
-    try:
-        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
-        if q != "max":
-            n = min(n, max(1, int(int(q) / int(per))))
-    except (OSError, ValueError):
-        pass
+    q = cgroup_cpu_quota()
+    if q is not None:
+        n = min(n, max(1, int(q)))
     return max(1, n // max(1, local_world))
 
 
@@ -233,8 +255,12 @@ def main():
     if dist:
         dist.barrier()
     t0 = time.perf_counter()
+    ru0 = resource.getrusage(resource.RUSAGE_SELF)
+    th0 = thread_cpu_ms()
     phase = {"rollout": 0.0, "return_norm": 0.0, "gae": 0.0, "minibatch": 0.0, "shuffle": 0.0, "update": 0.0,
-             "shuffle_walk": 0.0, "shuffle_wait": 0.0, "shuffle_met": 0.0}
+             "shuffle_walk": 0.0, "shuffle_wait": 0.0, "shuffle_met": 0.0,
+             "shuffle_spec_mwords": 0.0, "shuffle_true_mwords": 0.0,
+             "shuffle_walk_tsc_ms": 0.0, "shuffle_words_tsc_ms": 0.0}
     last = None
     for _ in range(args.steps):
         last = tr.train_update()
@@ -244,6 +270,11 @@ def main():
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
+    ru1 = resource.getrusage(resource.RUSAGE_SELF)
+    th1 = thread_cpu_ms()
+    host_cpu_threads = {k: round((v - th0.get(k, 0.0)) / args.steps, 1) for k, v in th1.items()
+                        if v - th0.get(k, 0.0) > 0.5 * args.steps}
+    host_cpu_ms = ((ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)) * 1e3 / args.steps
     if dist:
         t = torch.tensor([dt], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -284,7 +315,12 @@ def main():
                                      "stream-ordered" if world > 1 else None),
                       "w_gt_1_semantics": ("per-rank obs/return normalizers and per-rank minibatch advantage "
                                            "stats (SURVEY 8e); parity is defined at N=1" if world > 1 else None),
-                      "host_cpus_per_rank": int(os.environ["BPPO_HOST_THREADS"])},
+                      "host_cpus_per_rank": int(os.environ["BPPO_HOST_THREADS"]),
+                      "host_cpu_quota": cgroup_cpu_quota()},
+           # this process's CPU time per update over the timed region (all threads:
+           # shuffle engine walkers and word producers, the driver thread, HIP runtime)
+           "host_cpu_ms_per_step": round(host_cpu_ms, 2),
+           "host_cpu_ms_per_step_by_thread": host_cpu_threads,
            "roofline": roof, "gae_roofline": gae_roof,
            "phase_ms_per_update": {k: round(v / args.steps, 3) for k, v in phase.items()},
            "last_update": {k: (round(v, 5) if isinstance(v, float) else v) for k, v in last.items()

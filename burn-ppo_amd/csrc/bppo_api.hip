@@ -8,12 +8,28 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <thread>
+#include <x86intrin.h>
 #include "bppo_internal.h"
 #include "bppo_wide.h"
 
 using namespace bppo;
 
 namespace bppo {
+// TSC ticks per millisecond, measured once against steady_clock (shuffle engine
+// diagnostics)
+static double tsc_per_ms() {
+    static double v = 0.0;
+    if (v == 0.0) {
+        const auto t0 = std::chrono::steady_clock::now();
+        const uint64_t c0 = __rdtsc();
+        std::this_thread::sleep_for(std::chrono::milliseconds(20));
+        const uint64_t c1 = __rdtsc();
+        v = (double)(c1 - c0) / std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return v;
+}
+
 
 NetLayout make_layout(const bppo_config &c, int obs_dim, int priv_dim, int act_dim) {
     NetLayout L;
@@ -785,6 +801,10 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
             c->last_walk_ms += c->shuf.walk_ms[slot][e];
             c->last_met += c->shuf.coalesced[slot][e] >= 0 && e > 0;
         }
+        c->last_spec_mwords = (double)c->shuf.spec_words.exchange(0) * 1e-6;
+        c->last_true_mwords = (double)c->shuf.true_words.exchange(0) * 1e-6;
+        c->last_walk_cpu_ms = (double)c->shuf.tsc_walk.exchange(0) / tsc_per_ms();
+        c->last_words_cpu_ms = (double)c->shuf.tsc_words.exchange(0) / tsc_per_ms();
         c->shuf_slot = -1;
         // this update's reads of the J slot are enqueued; the next update's shuffles
         // begin after its rollout's T*N*A Gumbel words (usually chained already)
@@ -936,6 +956,10 @@ extern "C" bppo_status bppo_last_kernel_ms(bppo_ctx *c, const char *k, float *ms
     // time ppo_update blocked waiting for it
     if (!strcmp(k, "shuffle_walk")) { *ms = (float)c->last_walk_ms; return BPPO_OK; }
     if (!strcmp(k, "shuffle_wait")) { *ms = (float)c->last_wait_ms; return BPPO_OK; }
+    if (!strcmp(k, "shuffle_walk_tsc_ms")) { *ms = (float)c->last_walk_cpu_ms; return BPPO_OK; }    // all walks, in chain_walk
+    if (!strcmp(k, "shuffle_words_tsc_ms")) { *ms = (float)c->last_words_cpu_ms; return BPPO_OK; }  // all walks, getting words
+    if (!strcmp(k, "shuffle_spec_mwords")) { *ms = (float)c->last_spec_mwords; return BPPO_OK; }   // speculative walk words (M)
+    if (!strcmp(k, "shuffle_true_mwords")) { *ms = (float)c->last_true_mwords; return BPPO_OK; }   // true walk words (M)
     if (!strcmp(k, "shuffle_met")) { *ms = (float)c->last_met; return BPPO_OK; }   // epochs resolved by speculation
     return BPPO_ERR_ARG;
 }

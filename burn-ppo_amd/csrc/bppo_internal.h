@@ -119,6 +119,7 @@ struct ShuffleEngine {
     SpecWalk spec[SHUF_MAX_SPEC];
     int nspec = 0, ncur = 0;
     int C = 1;                                    // leading epochs of the next job speculated during this one
+    int fr_depth = 0;                             // frontier scheduling depth (0: all groups at job start)
     // exact continuations: when a walk of this job's last epoch finishes that epoch
     // at word x, a walk of the next job's first epoch starts at x + gap — exactly
     // where the next job starts whenever the true walk met that chain.  Two sets of
@@ -170,6 +171,8 @@ struct ShuffleEngine {
     hipStream_t copy = nullptr;
     double walk_ms[2][SHUF_MAX_EPOCHS] = {};
     int coalesced[2][SHUF_MAX_EPOCHS] = {};       // checkpoints walked before meeting a speculative walk (-1: none)
+    std::atomic<uint64_t> spec_words{0}, true_words{0};   // words walked since the caller last read them
+    std::atomic<uint64_t> tsc_walk{0}, tsc_words{0};      // TSC ticks walking / getting words (all walks)
     bppo_status init(int device, const Key8 &key, uint64_t stream, uint32_t n_, int epochs_, uint64_t gap_,
                      std::string &err);
     int ensure(uint64_t start);               // job for this start (reused if already running/done) -> slot
@@ -181,7 +184,9 @@ struct ShuffleEngine {
     void launch_walk(int i, uint64_t start, int wbuf);   // mu held
     void stop_walks(int lo, int hi);                     // stop and wait (mu not held)
     const uint32_t *words(int b, uint64_t pos, uint64_t len, std::vector<uint32_t> &scratch);
-    uint64_t walk_piece(int b, uint64_t pos, uint32_t *r, std::vector<uint32_t> &scratch);
+    struct WalkStats { uint64_t words = 0, tsc_walk = 0, tsc_words = 0; };
+    uint64_t walk_piece(int b, uint64_t pos, uint32_t *r, std::vector<uint32_t> &scratch, WalkStats &st);
+    void flush(WalkStats &st, std::atomic<uint64_t> &words_ctr);
     int peek(int i, uint64_t q, uint32_t *r);     // walk i's range at checkpoint q: 1 known, 0 not yet, -1 never
 };
 uint64_t shuffle_walk_host(const Key8 &key, uint64_t stream, uint64_t pos, uint32_t n, uint32_t *J);
@@ -327,6 +332,8 @@ struct bppo_ctx {
     hipEvent_t ev_block = nullptr;    // blocking-sync event for host waits on the stream
     float last_ms[8] = {0};
     double last_walk_ms = 0.0, last_wait_ms = 0.0;
+    double last_spec_mwords = 0.0, last_true_mwords = 0.0;   // host walk work since the previous update
+    double last_walk_cpu_ms = 0.0, last_words_cpu_ms = 0.0;   // thread time in chain_walk / in words()
     int last_met = 0;
     int collected = 0, gae_done = 0;
 };

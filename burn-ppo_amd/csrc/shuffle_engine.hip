@@ -34,6 +34,9 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <pthread.h>
+#include <x86intrin.h>
+#include <sys/mman.h>
 #include <sys/resource.h>
 #include <sys/syscall.h>
 #include <unistd.h>
@@ -193,6 +196,34 @@ static void shuffle_word_stats(uint32_t n, double &mean, double &sd) {
     sd = std::sqrt(v);
 }
 
+// The host copy of the words is read only by the host walkers (the GPU makes its
+// own), so it is plain memory on 2 MB pages, not pinned 4 KB pages: a walker
+// streams ~8 GB/s of words, and on 4 KB pages the hardware prefetcher restarts at
+// every page (= every 1024-word checkpoint piece).  Touched here so the producers
+// never fault.  BPPO_SHUFFLE_PINNED_WORDS=1: the old pinned buffer.
+static bool words_pinned() {
+    static const int v = getenv("BPPO_SHUFFLE_PINNED_WORDS") ? atoi(getenv("BPPO_SHUFFLE_PINNED_WORDS")) : 0;
+    return v != 0;
+}
+static uint32_t *host_words_alloc(uint64_t words) {
+    const size_t bytes = (size_t)words * 4;
+    if (words_pinned()) {
+        uint32_t *h = nullptr;
+        return hipHostMalloc((void **)&h, bytes, hipHostMallocDefault) == hipSuccess ? h : nullptr;
+    }
+    const size_t huge = (size_t)2 << 20, sz = (bytes + huge - 1) / huge * huge;
+    void *p = mmap(nullptr, sz, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (p == MAP_FAILED) return nullptr;
+    (void)madvise(p, sz, MADV_HUGEPAGE);
+    memset(p, 0, sz);
+    return static_cast<uint32_t *>(p);
+}
+static void host_words_free(uint32_t *h, uint64_t words) {
+    if (words_pinned()) { (void)hipHostFree(h); return; }
+    const size_t huge = (size_t)2 << 20, bytes = (size_t)words * 4;
+    (void)munmap(h, (bytes + huge - 1) / huge * huge);
+}
+
 bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32_t n_, int epochs_, uint64_t gap_,
                                 std::string &err) {
     dev = device; n = n_; epochs = epochs_; key = k; stream = strm; gap = gap_;
@@ -214,6 +245,23 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
     // get a whole job of head start; later epochs' walks start with their job)
     C = std::min(2, std::max(epochs, 1));
     if (const char *e = getenv("BPPO_SHUFFLE_CARRY")) C = std::max(1, std::min(epochs, atoi(e)));
+    // frontier scheduling (depth D): the walks of a boundary start only when the
+    // boundary D epochs before it is known exactly, so they guess around an exact
+    // position with one-sigma-times-sqrt(D) spread, and only ~2 groups walk at once
+    // (the job-start policy ran every boundary's group at once, sqrt(e) wide, and
+    // oversubscribed a 16-CPU share).  Needs the next job's first D + 1 epochs as
+    // carry groups.  BPPO_SHUFFLE_FRONTIER=0: the job-start policy.
+    fr_depth = getenv("BPPO_SHUFFLE_FRONTIER") ? atoi(getenv("BPPO_SHUFFLE_FRONTIER")) : 1;
+    if (fr_depth > 0 && epochs >= 3 && K > 0) {
+        C = std::min(fr_depth + 1, epochs - 1);
+        fr_depth = C - 1;
+        // one-sigma anchors: K = 5 over +-2 sigma misses ~1 in 40 boundaries and
+        // meets after ~2 M words (scripts/microbench/comb_sim.cpp); fewer walks
+        // leave the true walk and the met chains their CPUs
+        if (!getenv("BPPO_SHUFFLE_SPEC")) K = std::max(1, std::min(5, (5 * host_cpus + 8) / 16));
+    } else {
+        fr_depth = 0;
+    }
     // exact continuations need the last epoch in the in-job groups (BPPO_SHUFFLE_CONT=0: off)
     const bool cont_on = (getenv("BPPO_SHUFFLE_CONT") ? atoi(getenv("BPPO_SHUFFLE_CONT")) : 1) != 0 && epochs - 1 >= C;
     K = std::min(K, SHUF_MAX_SPEC / (std::max(epochs - C, 0) + 2 * C + (cont_on ? 2 : 0)));
@@ -265,7 +313,7 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
         WordBuf &w = wb[b];
         w.cap = cap0 + cap1;
         if (hipMalloc((void **)&w.d, w.cap * 4) != hipSuccess ||
-            hipHostMalloc((void **)&w.h, w.cap * 4, hipHostMallocDefault) != hipSuccess) {
+            !(w.h = host_words_alloc(w.cap))) {
             err = "shuffle word buffers: allocation failed";
             return BPPO_ERR_HIP;
         }
@@ -366,10 +414,25 @@ const uint32_t *ShuffleEngine::words(int b, uint64_t pos, uint64_t len, std::vec
 }
 
 // walk from pos up to the next checkpoint boundary (or the end of the shuffle)
-uint64_t ShuffleEngine::walk_piece(int b, uint64_t pos, uint32_t *r, std::vector<uint32_t> &scratch) {
+// (the diagnostic counters are per walk thread and folded into the engine's
+// atomics once per walk / epoch: shared counters per piece would ping-pong one
+// cache line between every walker's core)
+uint64_t ShuffleEngine::walk_piece(int b, uint64_t pos, uint32_t *r, std::vector<uint32_t> &scratch, WalkStats &st) {
     const uint64_t q = (pos / SHUF_CK + 1) * SHUF_CK;
+    const uint64_t t0 = __rdtsc();
     const uint32_t *w = words(b, pos, q - pos, scratch);
-    return pos + bppo_host::chain_walk_nj(w, (size_t)(q - pos), r);
+    const uint64_t t1 = __rdtsc();
+    const uint64_t used = bppo_host::chain_walk_nj(w, (size_t)(q - pos), r);
+    st.tsc_words += t1 - t0;
+    st.tsc_walk += __rdtsc() - t1;
+    st.words += used;
+    return pos + used;
+}
+void ShuffleEngine::flush(WalkStats &st, std::atomic<uint64_t> &words_ctr) {
+    words_ctr.fetch_add(st.words, std::memory_order_relaxed);
+    tsc_walk.fetch_add(st.tsc_walk, std::memory_order_relaxed);
+    tsc_words.fetch_add(st.tsc_words, std::memory_order_relaxed);
+    st = WalkStats{};
 }
 
 void ShuffleEngine::launch_walk(int i, uint64_t start, int wbuf) {
@@ -419,6 +482,7 @@ int ShuffleEngine::peek(int i, uint64_t q, uint32_t *r) {
 }
 
 void ShuffleEngine::worker(int i) {
+    (void)pthread_setname_np(pthread_self(), "bppo-spec");   // per-thread CPU accounting (bench.py)
     (void)hipSetDevice(dev);
     // CPU priority by when a walk is needed: epoch 1's walks first, then epoch
     // 2's, ..., the next job's carry set last (16 CPUs run ~K (E + 1) walks; the
@@ -428,10 +492,13 @@ void ShuffleEngine::worker(int i) {
         // every speculative walk below the true walk (the driver thread, nice 0)
         static const int nice_base = getenv("BPPO_SHUFFLE_NICE_BASE") ? atoi(getenv("BPPO_SHUFFLE_NICE_BASE")) : 0;
         const int g = i < ncur ? i / std::max(K, 1) : std::max(epochs - C, 0);
-        const int nv = nice_base + nice_step * g;
+        // frontier scheduling keeps few walks alive at once: one niceness for all
+        static const int fr_nice = getenv("BPPO_SHUFFLE_FNICE") ? atoi(getenv("BPPO_SHUFFLE_FNICE")) : 1;
+        const int nv = fr_depth > 0 ? fr_nice : nice_base + nice_step * g;
         if (nv > 0) (void)setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), std::min(19, nv));
     }
     std::vector<uint32_t> scratch;
+    WalkStats wst;
     uint64_t seen = 0;
     SpecWalk &s = spec[i];
     for (;;) {
@@ -445,7 +512,7 @@ void ShuffleEngine::worker(int i) {
         uint32_t r = n;
         while (r >= 2 && !s.stop.load(std::memory_order_relaxed)) {
             const uint64_t q = (pos / SHUF_CK + 1) * SHUF_CK;
-            pos = walk_piece(s.wbuf, pos, &r, scratch);
+            pos = walk_piece(s.wbuf, pos, &r, scratch, wst);
             if (pos == q) {
                 const int64_t c = (int64_t)((q - s.ck_base) / SHUF_CK);
                 if (c < (int64_t)s.ck.size()) {
@@ -461,6 +528,7 @@ void ShuffleEngine::worker(int i) {
             }
         }
         s.end = pos;
+        flush(wst, spec_words);
         {
             std::lock_guard<std::mutex> lk(mu);
             s.done.store(1, std::memory_order_release);
@@ -477,6 +545,7 @@ void ShuffleEngine::worker(int i) {
 }
 
 void ShuffleEngine::generator() {
+    (void)pthread_setname_np(pthread_self(), "bppo-words");
     uint64_t seen = 0;
     for (;;) {
         WordBuf *W;
@@ -504,6 +573,7 @@ void ShuffleEngine::generator() {
 }
 
 void ShuffleEngine::run() {
+    (void)pthread_setname_np(pthread_self(), "bppo-true");
     (void)hipSetDevice(dev);
     std::vector<uint32_t> scratch;
     for (;;) {
@@ -611,13 +681,20 @@ void ShuffleEngine::run() {
         }
         cv.notify_all();
         // ---- speculative walks: epochs 1 .. E-1 of this job, and the next job's first epoch
-        {
+        // K guesses evenly over centre +- spread*sd
+        static const double spread = getenv("BPPO_SHUFFLE_SPREAD") ? atof(getenv("BPPO_SHUFFLE_SPREAD")) : 2.0;
+        auto guess = [&](double centre, double sd, int k) {
+            return (uint64_t)std::max((double)start, std::floor(centre + ((k + 0.5) / K - 0.5) * 2.0 * spread * sd));
+        };
+        if (fr_depth > 0) {
+            // frontier: this job's in-job groups and the next job's carry groups are
+            // launched as boundaries resolve (below); until then peek() says never
             std::lock_guard<std::mutex> lk(mu);
-            // K guesses evenly over centre +- spread*sd
-            static const double spread = getenv("BPPO_SHUFFLE_SPREAD") ? atof(getenv("BPPO_SHUFFLE_SPREAD")) : 2.0;
-            auto guess = [&](double centre, double sd, int k) {
-                return (uint64_t)std::max((double)start, std::floor(centre + ((k + 0.5) / K - 0.5) * 2.0 * spread * sd));
-            };
+            for (int i = cur0; i < cur1; i++) { spec[i].start = ~0ull; spec[i].merged_to.store(-1, std::memory_order_relaxed); }
+            for (int i = cn0; i < cn1; i++) { spec[i].start = ~0ull; spec[i].merged_to.store(-1, std::memory_order_relaxed); }
+            carry_valid[b] = K > 0;
+        } else {
+            std::lock_guard<std::mutex> lk(mu);
             for (int e = C; e < epochs; e++)
                 for (int k = 0; k < K; k++)
                     launch_walk(cur0 + (e - C) * K + k, guess((double)start + e * Ew, sigma * std::sqrt((double)e), k), b);
@@ -631,6 +708,7 @@ void ShuffleEngine::run() {
         // ---- true walks (checkpoint states only; J is rebuilt on the GPU)
         uint64_t pos = start;
         bool cancelled = false;
+        WalkStats tst;
         std::vector<std::pair<uint64_t, uint32_t>> tck;
         for (int e = 0; e < epochs && !cancelled; e++) {
             auto t0 = std::chrono::steady_clock::now();
@@ -650,7 +728,7 @@ void ShuffleEngine::run() {
             // met chain's recorded states whenever that chain is ahead, so the epoch
             // closes at the earlier of its own walk and the chain's end.
             int fin = -1;                              // chain walk whose end closes the epoch
-            uint64_t endp = 0;
+            uint64_t endp = 0, chain_front = 0;
             while (r >= 2) {
                 if (met >= 0) {
                     if (cancel.load(std::memory_order_relaxed) || quit) { cancelled = true; break; }
@@ -670,9 +748,17 @@ void ShuffleEngine::run() {
                         endp = spec[f].end;
                         break;
                     }
+                    // frontier: the met chain's walker started a boundary earlier and is
+                    // ahead on this same chain; our own piece would only duplicate it, so
+                    // sleep while it advances and walk only if it stalls
+                    if (fr_depth > 0 && !chain_done && pos > chain_front) {
+                        chain_front = pos;
+                        std::this_thread::sleep_for(std::chrono::microseconds(20));
+                        continue;
+                    }
                 }
                 const uint64_t q = (pos / SHUF_CK + 1) * SHUF_CK;
-                pos = walk_piece(b, pos, &r, scratch);
+                pos = walk_piece(b, pos, &r, scratch, tst);
                 if (cancel.load(std::memory_order_relaxed)) { cancelled = true; break; }
                 if (pos != q || r < 2) continue;
                 tck.push_back({q, r});
@@ -703,6 +789,7 @@ void ShuffleEngine::run() {
                     for (int i = met + 1; i < g1; i++) spec[i].stop.store(true, std::memory_order_relaxed);
                 }
             }
+            flush(tst, true_words);
             if (cancelled) break;
             Seg *S = seg_host[slot] + (size_t)e * maxseg;
             int ns = 0;
@@ -751,6 +838,21 @@ void ShuffleEngine::run() {
                     if (ex >= 0) for (int i = cn0; i < cn0 + K; i++) spec[i].stop.store(true, std::memory_order_relaxed);
                     else prune(cn0, cn0 + K, x);
                 }
+            }
+            // frontier: the boundary fr_depth epochs past this one now has an exact
+            // anchor (this epoch's end, + gap across the job boundary)
+            if (fr_depth > 0 && !cancelled) {
+                std::lock_guard<std::mutex> lk(mu);
+                const int t = e + 1 + fr_depth;
+                int g0 = -1;
+                if (t < epochs) g0 = cur0 + (t - C) * K;
+                else if (t - epochs < C) g0 = cn0 + (t - epochs) * K;
+                if (g0 >= 0) {
+                    const double centre = (double)pos + fr_depth * Ew + (t >= epochs ? (double)gap : 0.0);
+                    const double sd = sigma * std::sqrt((double)fr_depth);
+                    for (int k = 0; k < K; k++) launch_walk(g0 + k, guess(centre, sd, k), b);
+                }
+                cv.notify_all();
             }
             if (overflow) {   // never at sane sizes: fall back to the sequential walk of the epoch
                 std::vector<uint32_t> Jh(n);
@@ -842,7 +944,7 @@ void ShuffleEngine::shutdown() {
         for (auto &e : wb[b].ev) if (e) (void)hipEventDestroy(e);
         wb[b].ev.clear();
         if (wb[b].d) { (void)hipFree(wb[b].d); wb[b].d = nullptr; }
-        if (wb[b].h) { (void)hipHostFree(wb[b].h); wb[b].h = nullptr; }
+        if (wb[b].h) { host_words_free(wb[b].h, wb[b].cap); wb[b].h = nullptr; }
     }
 }
 

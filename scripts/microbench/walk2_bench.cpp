@@ -5,9 +5,12 @@
 //   g++ -O3 -march=native -std=c++17 -I../../burn-ppo_amd/csrc walk2_bench.cpp \
 //       ../../burn-ppo_amd/csrc/shuffle_host.cpp -o walk2_bench
 #include <immintrin.h>
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <ctime>
 #include <cstdlib>
+#include <thread>
 #include <vector>
 #include "shuffle_host.h"
 
@@ -85,6 +88,56 @@ static void walk2(Ch &a, Ch &b) {
     }
 }
 
+// self-made words: ChaCha12 pieces of 1024 words into an L1-resident buffer,
+// (a) made then walked, (b) the next piece made in the same loop iteration as
+// the current piece is walked (out-of-order overlap of the two)
+static size_t walk_selfgen(const u32 key[8], u64 stream, u64 pos, u32 *r, bool overlap) {
+    alignas(64) static thread_local u32 buf[2][1024 + 32];
+    const u64 p0 = pos;
+    int cur = 0;
+    bppo_host::chacha12_words(key, stream, pos, buf[cur], 1024);
+    while (*r >= 2) {
+        if (overlap) bppo_host::chacha12_words(key, stream, pos + 1024, buf[cur ^ 1], 1024);
+        Ch c{buf[cur], 1024, 0, *r};
+        walk1(c);
+        *r = c.r;
+        if (c.p < 1024) { pos += c.p; break; }
+        pos += 1024;
+        cur ^= 1;
+        if (!overlap) bppo_host::chacha12_words(key, stream, pos, buf[cur], 1024);
+    }
+    return (size_t)(pos - p0);
+}
+
+// T threads each walking one chain at once over shared read-only words: does
+// the per-thread rate hold as the host's cores fill?
+static void scaling(const std::vector<u32> &wa, size_t pa) {
+    const char *tl = getenv("WALK_THREADS");
+    std::vector<int> Ts = tl ? std::vector<int>{atoi(tl)} : std::vector<int>{1, 2, 4, 8, 12, 16};
+    const int reps = getenv("WALK_REPS") ? atoi(getenv("WALK_REPS")) : 1;
+    for (int rep = 0; rep < reps; rep++)
+    for (int T : Ts) {
+        std::vector<std::thread> th;
+        std::vector<double> ns(T), cpu(T);
+        for (int t = 0; t < T; t++)
+            th.emplace_back([&, t]() {
+                Ch a{wa.data() + 64 * t, wa.size() - 64 * t, 0, 8388608u};
+                timespec c0, c1;
+                clock_gettime(CLOCK_THREAD_CPUTIME_ID, &c0);
+                auto t0 = std::chrono::steady_clock::now();
+                walk1(a);
+                ns[t] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / a.p * 1e9;
+                clock_gettime(CLOCK_THREAD_CPUTIME_ID, &c1);
+                cpu[t] = ((c1.tv_sec - c0.tv_sec) * 1e9 + (c1.tv_nsec - c0.tv_nsec)) / a.p;
+            });
+        for (auto &x : th) x.join();
+        double mx = 0, sm = 0, sc = 0;
+        for (int t = 0; t < T; t++) { mx = std::max(mx, ns[t]); sm += ns[t]; sc += cpu[t]; }
+        printf("threads %2d: wall mean %.3f max %.3f | cpu mean %.3f ns/word per thread\n", T, sm / T, mx, sc / T);
+    }
+    (void)pa;
+}
+
 int main() {
     const u32 n = 8388608;
     const size_t W = 12000000;
@@ -106,6 +159,18 @@ int main() {
         printf("one chain %.3f ns/word | two interleaved %.3f ns/word (per word of both) | ok %d %d %d\n",
                d1 / a.p * 1e9, d2 / (a2.p + b2.p) * 1e9, a.p == pa && a.r == ra, a2.p == pa && a2.r == ra,
                b2.p == pb && b2.r == rb);
+    }
+    scaling(wa, pa);
+    if (getenv("WALK_THREADS")) return 0;
+    for (int rep = 0; rep < 2; rep++) {
+        for (int ov = 0; ov < 2; ov++) {
+            u32 r = n;
+            auto t0 = std::chrono::steady_clock::now();
+            const size_t used = walk_selfgen(key, 3, 0, &r, ov != 0);
+            const double d = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            printf("self-made words (%s): %.3f ns/word | ok %d\n", ov ? "next piece made beside the walk" : "make then walk",
+                   d / used * 1e9, used == pa && r == ra);
+        }
     }
     return 0;
 }

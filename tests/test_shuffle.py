@@ -121,3 +121,32 @@ def test_shuffle_engine_equals_sequential_walks(seed, start, n, epochs, gap, job
         pos += gap
     if n == 1 << 23:
         assert (met[epochs:] >= 0).any(), met      # at CfgB size the speculation does meet
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("policy", ["0", "2"])
+@pytest.mark.parametrize("seed,start,n,epochs,gap,jobs", [
+    (5, 77, 1 << 23, 4, 16_777_216, 3),
+    (9, 3, 100_003, 6, 700_000, 3),
+])
+def test_shuffle_engine_policies_equal_sequential(monkeypatch, policy, seed, start, n, epochs, gap, jobs):
+    """The job-start speculation policy (BPPO_SHUFFLE_FRONTIER=0) and frontier depth 2
+    give the same J and word positions as the sequential walk (the default, depth 1,
+    is covered above)."""
+    monkeypatch.setenv("BPPO_SHUFFLE_FRONTIER", policy)
+    J = np.zeros(n * epochs * jobs, np.uint32)
+    ends = np.zeros(epochs * jobs, np.uint64)
+    met = np.zeros(epochs * jobs, np.int32)
+    assert L.lib().bppo_debug_shuffle_engine(seed, 0, start, n, epochs, gap, jobs, J.ctypes.data,
+                                             ends.ctypes.data, met.ctypes.data) == 0
+    pos = start
+    for j in range(jobs):
+        for e in range(epochs):
+            k = j * epochs + e
+            Je = np.zeros(n, np.uint32)
+            end = C.c_uint64()
+            assert L.lib().bppo_debug_shuffle_chain(seed, 0, pos, n, Je.ctypes.data, C.byref(end)) == 0
+            assert ends[k] == end.value, (j, e, met)
+            assert np.array_equal(J[k * n:(k + 1) * n], Je), (j, e, met)
+            pos = end.value
+        pos += gap
