@@ -228,7 +228,18 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     TRY(dalloc(c, &c->d_ep_count, 1));
     TRY(dalloc(c, &c->d_ep_sum, 2 * EP_SUMMARY_BLOCKS));
     TRY(dalloc(c, &c->d_err, 1));
-    TRY(dalloc(c, &c->d_perm, TN));
+    TRY(dalloc(c, &c->d_perm_base, TN));
+    c->d_perm = c->d_perm_base;
+    TRY(dalloc(c, &c->d_perm_ep, TN * (size_t)cfg->num_epochs));
+    TRY(dalloc(c, &c->d_inv_ep, TN * (size_t)cfg->num_epochs));
+    TRY(dalloc(c, &c->d_advpart, (size_t)ADV_STREAM_BLOCKS * ADV_STREAM_MAXM * 4));
+    {
+        int lo = 0, hi = 0;
+        BPPO_HIP(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
+        BPPO_HIP(c, hipStreamCreateWithPriority(&c->fy_stream, hipStreamNonBlocking, lo));
+        for (int e = 0; e < cfg->num_epochs && e < SHUF_MAX_EPOCHS; e++)
+            BPPO_HIP(c, hipEventCreateWithFlags(&c->fy_ev[e], hipEventDisableTiming));
+    }
     TRY(dalloc(c, &c->d_fy, 4 * TN));
     TRY(dalloc(c, &c->d_scan, TN / 8192 + 2));
     BPPO_HIP(c, fy_ranges_init(c->fyr, (uint32_t)TN));
@@ -273,6 +284,7 @@ extern "C" bppo_status bppo_create(const bppo_config *cfg, int hip_device, void 
 
 extern "C" void bppo_destroy(bppo_ctx *c) {
     if (!c) return;
+    if (c->fy_stream) (void)hipStreamSynchronize(c->fy_stream);   // reads the engine's J buffers
     c->shuf.shutdown();
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     wide_free(c);
@@ -281,7 +293,7 @@ extern "C" void bppo_destroy(bppo_ctx *c) {
                     c->d_env_pos, c->d_ep_ret, c->d_ep_len, c->d_obs, c->d_rew, c->d_rew_raw,
                     c->d_done, c->d_val, c->d_logp, c->d_adv, c->d_ret, c->d_act, c->d_X, c->d_on,
                     c->d_obs_part, c->d_rn_returns, c->d_rn_stats, c->d_scan_agg, c->d_last_v,
-                    c->d_eps, c->d_ep_count, c->d_ep_sum, c->d_err, c->d_perm, c->d_fy, c->d_scan,
+                    c->d_eps, c->d_ep_count, c->d_ep_sum, c->d_err, c->d_perm_base, c->d_perm_ep, c->d_inv_ep, c->d_advpart, c->d_fy, c->d_scan,
                     c->d_red, c->d_mb_stats, c->d_gumbel, c->d_rows, c->d_mbrow};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     fy_ranges_free(c->fyr);
@@ -291,6 +303,8 @@ extern "C" void bppo_destroy(bppo_ctx *c) {
         if (c->ev[i][0]) (void)hipEventDestroy(c->ev[i][0]);
         if (c->ev[i][1]) (void)hipEventDestroy(c->ev[i][1]);
     }
+    if (c->fy_stream) { (void)hipStreamSynchronize(c->fy_stream); (void)hipStreamDestroy(c->fy_stream); }
+    for (hipEvent_t e : c->fy_ev) if (e) (void)hipEventDestroy(e);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -341,6 +355,7 @@ extern "C" bppo_status bppo_rng_get(bppo_ctx *c, uint64_t *p) {
 extern "C" bppo_status bppo_rng_set(bppo_ctx *c, uint64_t p) {
     if (!c) return BPPO_ERR_ARG;
     c->shuf_slot = -1;
+    c->fy_slot = -1; c->fy_done = 0;     // permutations made ahead belong to the old start
     c->rng_pos = p;
     return BPPO_OK;
 }
@@ -360,6 +375,7 @@ extern "C" bppo_status bppo_rng_fill_bytes(bppo_ctx *c, uint8_t *dst, size_t n) 
     }
     c->rng_pos += nw;
     c->shuf_slot = -1;
+    c->fy_slot = -1; c->fy_done = 0;
     return BPPO_OK;
 }
 
@@ -373,6 +389,8 @@ extern "C" bppo_status bppo_rng_from_seed(bppo_ctx *c, const uint8_t *seed) {
         k.k[i] = (uint32_t)seed[4 * i] | ((uint32_t)seed[4 * i + 1] << 8) | ((uint32_t)seed[4 * i + 2] << 16) |
                  ((uint32_t)seed[4 * i + 3] << 24);
     BPPO_HIP(c, sync_stream(c));
+    BPPO_HIP(c, hipStreamSynchronize(c->fy_stream));   // its permutations read the engine's J
+    c->fy_slot = -1; c->fy_done = 0;
     c->shuf.shutdown();
     c->shuf.~ShuffleEngine();
     new (&c->shuf) ShuffleEngine();
@@ -564,6 +582,27 @@ static void tm_read(bppo_ctx *c, int slot) {
     if (hipEventElapsedTime(&ms, c->ev[slot][0], c->ev[slot][1]) == hipSuccess) c->last_ms[slot] = ms;
 }
 
+// Fisher-Yates of every epoch of the engine's job in `slot` whose J is already on
+// the device (the host engine has resolved it), in epoch order on fy_stream,
+// each into its own permutation buffer (ppo.rs:1816 indices.shuffle; the
+// permutation of epoch e depends only on that epoch's RNG words)
+static bppo_status fy_enqueue_ready(bppo_ctx *c, int slot) {
+    const size_t B = (size_t)c->T * c->N;
+    if (slot != c->fy_slot) { c->fy_slot = slot; c->fy_done = 0; }
+    while (c->fy_done < c->cfg.num_epochs && c->shuf.epoch_ready(slot, c->fy_done)) {
+        const int e = c->fy_done;
+        BPPO_HIP(c, hipStreamWaitEvent(c->fy_stream, c->shuf.ev[slot][e], 0));
+        (void)hipEventRecord(c->ev[TM_SHUFFLE][0], c->fy_stream);
+        BPPO_HIP(c, fisher_yates_device(c->shuf.d_J[slot] + (size_t)e * B, (uint32_t)B, c->d_fy, c->d_scan,
+                                        c->d_perm_ep + (size_t)e * B, c->fy_stream, &c->fyr,
+                                        c->d_inv_ep + (size_t)e * B));
+        (void)hipEventRecord(c->ev[TM_SHUFFLE][1], c->fy_stream);
+        BPPO_HIP(c, hipEventRecord(c->fy_ev[e], c->fy_stream));
+        c->fy_done++;
+    }
+    return BPPO_OK;
+}
+
 // collect_rollouts (ppo.rs:213-500)
 extern "C" bppo_status bppo_collect_rollouts(bppo_ctx *c, bppo_rollout_info *info) {
     if (!c) return BPPO_ERR_ARG;
@@ -578,6 +617,13 @@ extern "C" bppo_status bppo_collect_rollouts(bppo_ctx *c, bppo_rollout_info *inf
         TRY(popart_denorm(c, c->d_val, TN));            // ppo.rs:355-359 (multi-player: in the sampler)
     }
     tm_end(c, TM_ROLLOUT);
+    // self-play: the update's shuffles start right after this rollout's Gumbel words,
+    // so the epochs the engine has resolved are permuted now, beside the rollout
+    static const bool fy_ahead = getenv("BPPO_FY_AHEAD") ? atoi(getenv("BPPO_FY_AHEAD")) != 0 : true;
+    if (!opp_active(c) && fy_ahead) {
+        c->shuf_slot = c->shuf.ensure(base + TN * (uint64_t)c->A);
+        TRY(fy_enqueue_ready(c, c->shuf_slot));
+    }
     if (opp_active(c)) {
         // opponent pool: seat reshuffles drew a data-dependent number of words
         TRY(opp_rollout_end(c));
@@ -679,7 +725,14 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
     // varies per update, so each epoch's swap targets come from the sequential
     // host walk instead of the speculating shuffle engine
     const bool opp = opp_active(c);
-    if (opp) TRY(opp_compact_valid(c));
+    if (opp) {
+        // the opponent path permutes on this stream with the shared scratch, into the
+        // context's own buffer, after anything still queued on fy_stream
+        if (c->fy_done > 0) BPPO_HIP(c, hipStreamWaitEvent(c->stream, c->fy_ev[c->fy_done - 1], 0));
+        c->fy_slot = -1; c->fy_done = 0;
+        c->d_perm = c->d_perm_base;
+        TRY(opp_compact_valid(c));
+    }
     if (!opp && c->shuf_slot < 0) c->shuf_slot = c->shuf.ensure(c->rng_pos);
     const int slot = c->shuf_slot;
     const size_t B = opp ? (size_t)c->n_valid : (size_t)c->T * c->N;
@@ -717,20 +770,19 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
             if (B) TRY(opp_map_perm(c, (uint32_t)B));
             (void)hipEventRecord(s1, c->stream);
         } else {
-            {
+            if (slot != c->fy_slot || ep >= c->fy_done) {
                 auto w0 = std::chrono::steady_clock::now();
                 c->shuf.wait_epoch(slot, ep);
                 wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
             }
-            BPPO_HIP(c, hipStreamWaitEvent(c->stream, c->shuf.ev[slot][ep], 0));
-            (void)hipEventRecord(s0, c->stream);
-            TRY(launch_fisher_yates(c, c->shuf.d_J[slot] + (size_t)ep * B, (uint32_t)B));
-            (void)hipEventRecord(s1, c->stream);
+            TRY(fy_enqueue_ready(c, slot));          // this epoch and any other resolved since
+            BPPO_HIP(c, hipStreamWaitEvent(c->stream, c->fy_ev[ep], 0));
+            c->d_perm = c->d_perm_ep + (size_t)ep * B;
         }
         // no learner rows (opponent pool): the reference shuffles an empty index
         // list (no RNG words) and skips every minibatch (ppo.rs:1815-1831)
         if (B == 0) continue;
-        TRY(launch_epoch_adv_stats(c, (uint32_t)B, M));
+        TRY(launch_epoch_adv_stats(c, (uint32_t)B, M, opp ? nullptr : c->d_inv_ep + (size_t)ep * B));
         size_t start = 0;
         for (int mb = 0; mb < M; mb++) {
             const size_t sz = base_mb + ((size_t)mb < rem ? 1 : 0);
@@ -806,8 +858,13 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
         c->last_walk_cpu_ms = (double)c->shuf.tsc_walk.exchange(0) / tsc_per_ms();
         c->last_words_cpu_ms = (double)c->shuf.tsc_words.exchange(0) / tsc_per_ms();
         c->shuf_slot = -1;
-        // this update's reads of the J slot are enqueued; the next update's shuffles
-        // begin after its rollout's T*N*A Gumbel words (usually chained already)
+        // this update's reads of the J slot are enqueued (fy_stream's too: epochs
+        // permuted ahead but not run after a KL early stop); the next update's
+        // shuffles begin after its rollout's T*N*A Gumbel words (usually chained already)
+        if (c->fy_slot == slot && c->fy_done > 0)
+            BPPO_HIP(c, hipStreamWaitEvent(c->stream, c->fy_ev[c->fy_done - 1], 0));
+        c->fy_slot = -1;
+        c->fy_done = 0;
         c->shuf.release(slot, c->stream);
         c->shuf.ensure(c->rng_pos + (uint64_t)c->T * c->N * (uint64_t)c->A);
     }

@@ -36,6 +36,7 @@ NetLayout make_layout(const bppo_config &c, int obs_dim, int priv_dim, int act_d
 
 // episode record written by the rollout kernel
 constexpr int EP_SUMMARY_BLOCKS = 128;   // k_ep_summary grid (partial sums per block)
+constexpr int ADV_STREAM_BLOCKS = 512, ADV_STREAM_MAXM = 16;   // k_adv_stream grid, most minibatches
 
 struct EpisodeRec {
     float total_reward[BPPO_MAX_PLAYERS];
@@ -178,6 +179,7 @@ struct ShuffleEngine {
     int ensure(uint64_t start);               // job for this start (reused if already running/done) -> slot
     void release(int slot, hipStream_t st);   // the caller is done enqueuing reads of d_J[slot] on st
     void wait_epoch(int slot, int e);
+    bool epoch_ready(int slot, int e);        // non-blocking wait_epoch
     void shutdown();
     void run();
     void worker(int i);
@@ -253,7 +255,17 @@ struct bppo_ctx {
     uint64_t rng_pos = 0;
     // shuffle
     bppo::ShuffleEngine shuf;
-    uint32_t *d_perm = nullptr;       // shuffled indices of the current epoch
+    uint32_t *d_perm = nullptr;       // shuffled indices of the current epoch (may point into d_perm_ep)
+    uint32_t *d_perm_base = nullptr;  // allocation behind d_perm for the opponent-pool path
+    // the engine's epochs are permuted on fy_stream as soon as their J is on the
+    // device — from the rollout on, so the permutations run beside the rollout
+    // and the return-normaliser / GAE kernels instead of between minibatches
+    uint32_t *d_perm_ep = nullptr;    // [epochs][TN] one permutation per epoch
+    uint32_t *d_inv_ep = nullptr;     // [epochs][TN] their inverses (row -> shuffled position)
+    double *d_advpart = nullptr;      // k_adv_stream block partials
+    hipStream_t fy_stream = nullptr;
+    hipEvent_t fy_ev[bppo::SHUF_MAX_EPOCHS] = {};
+    int fy_slot = -1, fy_done = 0;    // engine slot whose epochs [0, fy_done) are enqueued on fy_stream
     uint32_t *d_fy = nullptr;         // Fisher-Yates scratch [4][TN]: count/offset, bucket, succ, fw
     uint32_t *d_scan = nullptr;       // scan block sums
     bppo::FyRanges fyr;               // target ranges of the ranged Fisher-Yates bucketing
@@ -367,10 +379,10 @@ bppo_status launch_return_norm(bppo_ctx *c);
 // (k_update.hip)
 bppo_status launch_fisher_yates(bppo_ctx *c, const uint32_t *d_J, uint32_t n);
 hipError_t fisher_yates_device(const uint32_t *d_J, uint32_t n, uint32_t *scratch, uint32_t *scan, uint32_t *perm,
-                               hipStream_t st, const FyRanges *rg);
+                               hipStream_t st, const FyRanges *rg, uint32_t *inv = nullptr);
 hipError_t fy_ranges_init(FyRanges &r, uint32_t n);
 void fy_ranges_free(FyRanges &r);
-bppo_status launch_epoch_adv_stats(bppo_ctx *c, uint32_t B, int M);
+bppo_status launch_epoch_adv_stats(bppo_ctx *c, uint32_t B, int M, const uint32_t *inv = nullptr);
 bppo_status launch_minibatch(bppo_ctx *c, uint32_t mb_start, uint32_t mb_size, float ent_coef,
                              double *h_stats_out);
 bppo_status launch_adam(bppo_ctx *c, float lr, const float *c1, const float *c2, float *metric_dst = nullptr,

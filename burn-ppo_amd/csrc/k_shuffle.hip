@@ -168,8 +168,12 @@ __global__ void __launch_bounds__(256) k_fy_link(uint32_t n, const uint32_t *off
     }
 }
 
+// perm[i] = v, and optionally the inverse inv[v] = i (where each index landed:
+// the epoch's per-minibatch advantage statistics then stream over the rows in
+// order instead of gathering them through perm, k_update.hip k_adv_stream)
 __global__ void __launch_bounds__(256) k_fy_final(const uint32_t *J, uint32_t n, const uint32_t *succ,
-                                                  const uint32_t *fw, uint32_t *perm, const uint32_t *skip) {
+                                                  const uint32_t *fw, uint32_t *perm, const uint32_t *skip,
+                                                  uint32_t *inv) {
     if (skip && *skip) return;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint32_t s = succ[i];
@@ -181,6 +185,7 @@ __global__ void __launch_bounds__(256) k_fy_final(const uint32_t *J, uint32_t n,
             for (uint32_t f = fw[v]; f != FY_NONE; f = fw[v]) v = f;   // strictly increasing: terminates
         }
         perm[i] = v;
+        if (inv) inv[v] = i;
     }
 }
 
@@ -298,7 +303,7 @@ __global__ void __launch_bounds__(FYB_LINK_THREADS) k_fyb_link(uint32_t n, FyTab
 // Slow, exact, and launched unconditionally behind the flag, so the common case
 // costs one empty launch instead of eight.
 __global__ void __launch_bounds__(SCAN_B) k_fy_direct_block(const uint32_t *J, uint32_t n, uint32_t *scratch,
-                                                            uint32_t *perm, const uint32_t *flag) {
+                                                            uint32_t *perm, const uint32_t *flag, uint32_t *inv) {
     if (*flag == 0u) return;
     __shared__ uint32_t sh[SCAN_B / 64];
     uint32_t *cnt = scratch, *bucket = scratch + (size_t)n, *succ = scratch + 2 * (size_t)n,
@@ -349,6 +354,7 @@ __global__ void __launch_bounds__(SCAN_B) k_fy_direct_block(const uint32_t *J, u
         if (s == FY_NONE) v = J[i];
         else for (uint32_t f = fw[v]; f != FY_NONE; f = fw[v]) v = f;
         perm[i] = v;
+        if (inv) inv[v] = i;
     }
 }
 
@@ -406,7 +412,7 @@ void fy_ranges_free(FyRanges &r) {
 
 // scratch: 4n u32 (counts/pairs, buckets/pairs, succ, fw); scan: n/8192 + 2 u32; perm: n u32
 hipError_t fisher_yates_device(const uint32_t *d_J, uint32_t n, uint32_t *scratch, uint32_t *scan, uint32_t *perm,
-                               hipStream_t st, const FyRanges *rg) {
+                               hipStream_t st, const FyRanges *rg, uint32_t *inv) {
     if (n == 0) return hipSuccess;
     uint32_t *cnt = scratch, *bucket = scratch + (size_t)n, *succ = scratch + 2 * (size_t)n,
              *fw = scratch + 3 * (size_t)n;
@@ -426,9 +432,9 @@ hipError_t fisher_yates_device(const uint32_t *d_J, uint32_t n, uint32_t *scratc
         // pass 4 (k_fy_final) runs unless a range overflowed; then the one-block
         // direct pass computes the permutation instead
         hipLaunchKernelGGL(k_fy_final, dim3(grid), dim3(256), 0, st, d_J, n, (const uint32_t *)succ,
-                           (const uint32_t *)fw, perm, (const uint32_t *)flag);
+                           (const uint32_t *)fw, perm, (const uint32_t *)flag, inv);
         hipLaunchKernelGGL(k_fy_direct_block, dim3(1), dim3(SCAN_B), 0, st, d_J, n, scratch, perm,
-                           (const uint32_t *)flag);
+                           (const uint32_t *)flag, inv);
         return hipGetLastError();
     }
     // direct path
@@ -437,12 +443,12 @@ hipError_t fisher_yates_device(const uint32_t *d_J, uint32_t n, uint32_t *scratc
     launch_scan(cnt, n, scan, off, nullptr, st);
     hipLaunchKernelGGL(k_fy_scatter, dim3(grid), dim3(256), 0, st, d_J, n, (const uint32_t *)off, cnt, bucket, nullptr);
     hipLaunchKernelGGL(k_fy_link, dim3(grid), dim3(256), 0, st, n, (const uint32_t *)off, bucket, succ, fw, nullptr);
-    hipLaunchKernelGGL(k_fy_final, dim3(grid), dim3(256), 0, st, d_J, n, succ, fw, perm, nullptr);
+    hipLaunchKernelGGL(k_fy_final, dim3(grid), dim3(256), 0, st, d_J, n, succ, fw, perm, nullptr, inv);
     return hipGetLastError();
 }
 
 bppo_status launch_fisher_yates(bppo_ctx *c, const uint32_t *d_J, uint32_t n) {
-    BPPO_HIP(c, fisher_yates_device(d_J, n, c->d_fy, c->d_scan, c->d_perm, c->stream, &c->fyr));
+    BPPO_HIP(c, fisher_yates_device(d_J, n, c->d_fy, c->d_scan, c->d_perm, c->stream, &c->fyr, nullptr));
     return BPPO_OK;
 }
 

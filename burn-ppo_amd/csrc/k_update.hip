@@ -945,8 +945,111 @@ __global__ void __launch_bounds__(256) k_adv_epoch_final(const double *part, int
     stats[m * 4 + 3] = (float)smx[0];
 }
 
-bppo_status launch_epoch_adv_stats(bppo_ctx *c, uint32_t B, int M) {
+// The same statistics from the inverse permutation (inv[r] = shuffled position of
+// row r, written by the Fisher-Yates final pass on the side stream): rows stream
+// in order, adv[r] and inv[r] coalesced, each added to the bins of its minibatch
+// mb_of(inv[r]) (MB >= M bins in registers).  Block b owns rows [b C, (b+1) C);
+// every block writes MB partials, summed per minibatch in block order.
+template <int MB>
+__global__ void __launch_bounds__(256) k_adv_stream(const float *__restrict__ adv, const uint32_t *__restrict__ inv,
+                                                    EpochSplit sp, uint32_t C, double *part) {
+    constexpr int U = 4;
+    __shared__ double red[4][MB][4];
+    double s[MB], q[MB];
+    float mn[MB], mx[MB];
+#pragma unroll
+    for (int k = 0; k < MB; k++) { s[k] = 0.0; q[k] = 0.0; mn[k] = INFINITY; mx[k] = -INFINITY; }
+    const uint32_t r0 = blockIdx.x * C, r1 = min(sp.B, r0 + C);
+    for (uint32_t b = r0 + threadIdx.x; b < r1; b += 256 * U) {
+        float a[U];
+        uint32_t p[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t r = min(b + u * 256, r1 - 1);
+            a[u] = adv[r];
+            p[u] = inv[r];
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (b + u * 256 >= r1) continue;
+            const uint32_t m = mb_of(p[u], sp);
+            const double d = (double)a[u];
+#pragma unroll
+            for (int k = 0; k < MB; k++) {
+                const bool hit = m == (uint32_t)k;
+                s[k] += hit ? d : 0.0;
+                q[k] += hit ? d * d : 0.0;
+                mn[k] = hit ? fminf(mn[k], a[u]) : mn[k];
+                mx[k] = hit ? fmaxf(mx[k], a[u]) : mx[k];
+            }
+        }
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < MB; k++) {
+        double x = s[k], y = q[k];
+        float u = mn[k], v = mx[k];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            x += __shfl_xor(x, o, 64); y += __shfl_xor(y, o, 64);
+            u = fminf(u, __shfl_xor(u, o, 64)); v = fmaxf(v, __shfl_xor(v, o, 64));
+        }
+        if (lane == 0) { red[w][k][0] = x; red[w][k][1] = y; red[w][k][2] = u; red[w][k][3] = v; }
+    }
+    __syncthreads();
+    if (threadIdx.x < MB) {
+        const int k = threadIdx.x;
+        double x = 0.0, y = 0.0, u = INFINITY, v = -INFINITY;
+        for (int ww = 0; ww < 4; ww++) {
+            x += red[ww][k][0]; y += red[ww][k][1]; u = fmin(u, red[ww][k][2]); v = fmax(v, red[ww][k][3]);
+        }
+        double *o = part + ((size_t)blockIdx.x * MB + k) * 4;
+        o[0] = x; o[1] = y; o[2] = u; o[3] = v;
+    }
+}
+// one block per minibatch: the block partials in block order -> [mean, std, min, max]
+__global__ void __launch_bounds__(256) k_adv_stream_final(const double *part, int nblk, int MB, EpochSplit sp,
+                                                          float *stats) {
+    __shared__ double ss[256], sq[256], smn[256], smx[256];
+    const uint32_t m = blockIdx.x;
+    double s = 0.0, q = 0.0, mn = INFINITY, mx = -INFINITY;
+    for (int b = threadIdx.x; b < nblk; b += blockDim.x) {
+        const double *o = part + ((size_t)b * MB + m) * 4;
+        s += o[0]; q += o[1]; mn = fmin(mn, o[2]); mx = fmax(mx, o[3]);
+    }
+    ss[threadIdx.x] = s; sq[threadIdx.x] = q; smn[threadIdx.x] = mn; smx[threadIdx.x] = mx;
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+        if (threadIdx.x < st) {
+            ss[threadIdx.x] += ss[threadIdx.x + st]; sq[threadIdx.x] += sq[threadIdx.x + st];
+            smn[threadIdx.x] = fmin(smn[threadIdx.x], smn[threadIdx.x + st]);
+            smx[threadIdx.x] = fmax(smx[threadIdx.x], smx[threadIdx.x + st]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x != 0) return;
+    const double n = (double)(sp.base + (m < sp.rem ? 1u : 0u));
+    const double mean = ss[0] / n;
+    stats[m * 4 + 0] = (float)mean;
+    stats[m * 4 + 1] = n > 1.0 ? sqrtf((float)(fmax(sq[0] - ss[0] * mean, 0.0) / (n - 1.0))) : NAN;
+    stats[m * 4 + 2] = (float)smn[0];
+    stats[m * 4 + 3] = (float)smx[0];
+}
+
+bppo_status launch_epoch_adv_stats(bppo_ctx *c, uint32_t B, int M, const uint32_t *inv) {
     const EpochSplit sp{B, B / (uint32_t)M, B % (uint32_t)M, (uint32_t)M};
+    static const bool stream_on = getenv("BPPO_ADV_STREAM") ? atoi(getenv("BPPO_ADV_STREAM")) != 0 : true;
+    if (inv && stream_on && M <= ADV_STREAM_MAXM && sp.base > 0) {
+        const uint32_t C = (B + ADV_STREAM_BLOCKS - 1) / ADV_STREAM_BLOCKS;
+        const int nblk = (int)((B + C - 1) / C);
+        const int MB = M <= 4 ? 4 : (M <= 8 ? 8 : 16);
+        if (MB == 4) hipLaunchKernelGGL(k_adv_stream<4>, dim3(nblk), dim3(256), 0, c->stream, c->d_adv, inv, sp, C, c->d_advpart);
+        else if (MB == 8) hipLaunchKernelGGL(k_adv_stream<8>, dim3(nblk), dim3(256), 0, c->stream, c->d_adv, inv, sp, C, c->d_advpart);
+        else hipLaunchKernelGGL(k_adv_stream<16>, dim3(nblk), dim3(256), 0, c->stream, c->d_adv, inv, sp, C, c->d_advpart);
+        hipLaunchKernelGGL(k_adv_stream_final, dim3(M), dim3(256), 0, c->stream, c->d_advpart, nblk, MB, sp, c->d_mb_stats);
+        BPPO_HIP(c, hipGetLastError());
+        return BPPO_OK;
+    }
     uint32_t C = (B + 511) / 512;
     if (sp.base > 0 && C > sp.base) C = sp.base;
     if (sp.base == 0) C = 1;

@@ -374,6 +374,11 @@ void ShuffleEngine::wait_epoch(int slot, int e) {
     cv.wait(lk, [&] { return ready[slot] > e || !slot_valid[slot]; });
 }
 
+bool ShuffleEngine::epoch_ready(int slot, int e) {
+    std::lock_guard<std::mutex> lk(mu);
+    return slot_valid[slot] && ready[slot] > e;
+}
+
 void ShuffleEngine::release(int slot, hipStream_t st) {
     (void)hipEventRecord(consumed[slot], st);
     std::lock_guard<std::mutex> lk(mu);
