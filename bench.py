@@ -169,6 +169,38 @@ def cpu_baseline(args):
                       f"single-threaded as in the reference; per-env-step cost is independent of N"}
 
 
+def gae_isolated_ms(N, T, gamma=0.99, lam=0.95, reps=20):
+    """k_gae_1p_seg at the workload's [T, N] shape on its own stream, nothing else on
+    the GPU (in the update loop it co-runs with the side-stream Fisher-Yates passes,
+    so its in-loop duration measures the sharing, not the kernel)."""
+    import torch
+    from bppo import _lib as L
+    g = torch.Generator(device="cuda").manual_seed(0)
+    r = torch.rand(T, N, device="cuda", generator=g)
+    d = (torch.rand(T, N, device="cuda", generator=g) < 0.01).float()
+    v = torch.rand(T, N, device="cuda", generator=g)
+    lv = torch.rand(N, device="cuda", generator=g)
+    adv, ret = torch.empty_like(r), torch.empty_like(r)
+    st = torch.cuda.Stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+
+    def once():
+        rc = L.lib().bppo_gae_device(r.data_ptr(), d.data_ptr(), v.data_ptr(), lv.data_ptr(), T, N, gamma, lam,
+                                     adv.data_ptr(), ret.data_ptr(), st.cuda_stream)
+        if rc != 0:
+            raise RuntimeError(f"bppo_gae_device status {rc}")
+    with torch.cuda.stream(st):
+        for _ in range(3):
+            once()
+        e0.record(st)
+        for _ in range(reps):
+            once()
+        e1.record(st)
+    st.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
 def steps_to_475(bppo, preset_over, max_steps, init_seed=0):
     """Train until the 100-episode rolling mean return (main.rs:842-853) reaches
     475; -> global_step after that rollout, or None within max_steps."""
@@ -296,12 +328,17 @@ def main():
             "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": mb_tr, "traffic_unit": "B/launch",
             "traffic_source": mb_src, "kernel": "k_minibatch_mfma", "launch_ms": round(mb_ms, 4),
             "algorithmic": f"{mb_rows} rows x {FLOP_PER_ROW_FWD_BWD} FLOP"}
-    gae_ms = phase["gae"] / args.steps
+    gae_loop_ms = phase["gae"] / args.steps
+    gae_ms = gae_isolated_ms(N, T)
     gae_gbs = N * T * GAE_BYTES_PER_ELEM / (gae_ms * 1e-3) / 1e9
     g_tr, g_src = traffic_for("k_gae_1p_seg", "k_gae.hip") if cfgB else (None, "not the profiled shape")
     gae_roof = {"bound": "hbm", "achieved": round(gae_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(gae_gbs / HBM_PEAK_GBS, 4), "traffic": g_tr, "traffic_unit": "B/launch",
                 "traffic_source": g_src, "kernel": "k_gae_1p_seg", "launch_ms": round(gae_ms, 4),
+                "measured": "isolated launches at the workload shape after the timed region (HIP events on "
+                            "the launch stream); in the update loop the kernel shares the GPU with the "
+                            "side-stream Fisher-Yates passes",
+                "launch_ms_in_loop": round(gae_loop_ms, 4),
                 "algorithmic": f"{N * T} x {GAE_BYTES_PER_ELEM} B"}
     out = {"metric": METRIC, "value": round(value, 1), "unit": "env-steps/sec", "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
