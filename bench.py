@@ -262,6 +262,7 @@ def main():
     if args.selftest:
         return selftest_main(args, world, rank)
     os.environ.setdefault("BPPO_HOST_THREADS", str(host_cpu_budget(local_world)))
+
     import torch
     import bppo
     dist = None
@@ -281,6 +282,12 @@ def main():
         fn = make_allreduce(dist, mode="device_async", max_elems=tr.ctx.n_params + 64, stream=tr.ctx.stream)
         tr.ctx.set_allreduce(fn, world, stream_ordered=True)
 
+    try:   # name the driving thread (after the runtime's threads exist: they inherit the name
+        # at creation) so host_cpu_ms_per_step_by_thread tells it from them
+        import ctypes
+        ctypes.CDLL(None).prctl(15, b"bench-main", 0, 0, 0)       # PR_SET_NAME
+    except (OSError, AttributeError):
+        pass
     for _ in range(args.warmup):
         tr.train_update()
     torch.cuda.synchronize()
@@ -292,7 +299,7 @@ def main():
     phase = {"rollout": 0.0, "return_norm": 0.0, "gae": 0.0, "minibatch": 0.0, "shuffle": 0.0, "update": 0.0,
              "shuffle_walk": 0.0, "shuffle_wait": 0.0, "shuffle_met": 0.0,
              "shuffle_spec_mwords": 0.0, "shuffle_true_mwords": 0.0,
-             "shuffle_walk_tsc_ms": 0.0, "shuffle_words_tsc_ms": 0.0}
+             "shuffle_walk_tsc_ms": 0.0, "shuffle_words_tsc_ms": 0.0, "host_enqueue": 0.0, "host_sync_wait": 0.0}
     last = None
     for _ in range(args.steps):
         last = tr.train_update()

@@ -329,14 +329,26 @@ def compute_gae(ctx):
     ctx._chk(L.lib().bppo_compute_gae(ctx.h))
 
 
-def ppo_update(ctx, learning_rate, entropy_coef):
-    """ppo.rs:1661-2112 -> UpdateMetrics dict."""
-    m = L.UpdateMetrics()
-    ctx._chk(L.lib().bppo_ppo_update(ctx.h, float(learning_rate), float(entropy_coef), C.byref(m)))
+def _metrics_dict(m):
     d = {k: getattr(m, k) for k in L.METRIC_NAMES + L.POPART_METRICS}
     d["num_updates"] = m.num_updates
     d["epochs_run"] = m.epochs_run
     return d
+
+
+def ppo_update(ctx, learning_rate, entropy_coef):
+    """ppo.rs:1661-2112 -> UpdateMetrics dict."""
+    m = L.UpdateMetrics()
+    ctx._chk(L.lib().bppo_ppo_update(ctx.h, float(learning_rate), float(entropy_coef), C.byref(m)))
+    return _metrics_dict(m)
+
+
+def train_step(ctx, learning_rate, entropy_coef):
+    """collect_rollouts + bootstrap/GAE + ppo_update in one call (bppo_train_step):
+    enqueued back to back, one host wait.  -> (rollout info, UpdateMetrics dict)."""
+    info, m = L.RolloutInfo(), L.UpdateMetrics()
+    ctx._chk(L.lib().bppo_train_step(ctx.h, float(learning_rate), float(entropy_coef), C.byref(info), C.byref(m)))
+    return info, _metrics_dict(m)
 
 
 class Trainer:
@@ -363,12 +375,14 @@ class Trainer:
         lr = schedule_get(self.cfg["learning_rate"], self.global_step)         # main.rs:706
         ent = schedule_get(self.cfg["entropy_coef"], self.global_step)         # main.rs:716
         self.vec_env.set_step(self.global_step)
-        info = collect_rollouts(self.ctx)
         if track_returns:
+            info = collect_rollouts(self.ctx)
             for ep in rollout_episodes(self.ctx):
                 self.recent_returns.append(ep["total_rewards"][0])
-        compute_gae(self.ctx)
-        metrics = ppo_update(self.ctx, lr, ent)
+            compute_gae(self.ctx)
+            metrics = ppo_update(self.ctx, lr, ent)
+        else:
+            info, metrics = train_step(self.ctx, lr, ent)        # the same three steps, one host wait
         self.global_step += self.ctx.T * self.ctx.N                           # main.rs:988
         metrics["episodes"] = info.episodes
         metrics["mean_return"] = info.mean_return

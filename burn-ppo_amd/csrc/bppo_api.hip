@@ -9,6 +9,7 @@
 #include <cstring>
 #include <new>
 #include <thread>
+#include <sys/prctl.h>
 #include <x86intrin.h>
 #include "bppo_internal.h"
 #include "bppo_wide.h"
@@ -132,10 +133,23 @@ extern "C" const char *bppo_last_error(const bppo_ctx *c) { return c ? c->err.c_
 
 // wait for the context stream on a blocking-sync event: the host thread sleeps
 // instead of polling (polling eats the CPU quota the shuffle walkers run on)
+// (hipEventSynchronize on a blocking-sync event still spun here: measured ~1 CPU per
+// process for the whole update; a sleeping poll at 20 us with 1 us timer slack frees it)
 static hipError_t sync_stream(bppo_ctx *c) {
-    if (!c->ev_block) return hipStreamSynchronize(c->stream);
-    hipError_t e = hipEventRecord(c->ev_block, c->stream);
-    return e == hipSuccess ? hipEventSynchronize(c->ev_block) : e;
+    const auto t0 = std::chrono::steady_clock::now();
+    hipError_t e;
+    if (!c->ev_block) e = hipStreamSynchronize(c->stream);
+    else {
+        static thread_local bool slack = false;
+        if (!slack) { (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0); slack = true; }
+        e = hipEventRecord(c->ev_block, c->stream);
+        while (e == hipSuccess && (e = hipEventQuery(c->ev_block)) == hipErrorNotReady) {
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+            e = hipSuccess;
+        }
+    }
+    c->sync_wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return e;
 }
 
 static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *stream) {
@@ -247,9 +261,13 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     TRY(dalloc(c, &c->d_mb_stats, (size_t)4 * std::max(cfg->num_minibatches, 2)));
     c->d_mb_cur = c->d_mb_stats;
     TRY(dalloc(c, &c->d_rows, (size_t)cfg->num_epochs * cfg->num_minibatches * (WM_COUNT + 4)));
+    BPPO_HIP(c, hipHostMalloc((void **)&c->h_rows,
+                              sizeof(float) * (size_t)cfg->num_epochs * cfg->num_minibatches * (WM_COUNT + 4),
+                              hipHostMallocDefault));
     if (!c->wide && cfg->hidden_size == 64 && cfg->num_hidden == 2 && cfg->relu && c->D == 5)
         BPPO_HIP(c, hipMalloc((void **)&c->d_mbrow, sizeof(float4) * 4 * TN));
-    BPPO_HIP(c, hipHostMalloc((void **)&c->h_red, sizeof(double) * (4 * 1024 + 64), hipHostMallocDefault));
+    BPPO_HIP(c, hipHostMalloc((void **)&c->h_red, sizeof(double) * (4 * 1024 + 64 + 2 + 2 * EP_SUMMARY_BLOCKS),
+                              hipHostMallocDefault));   // + the rollout's flags and episode partials
     BPPO_HIP(c, hipEventCreateWithFlags(&c->ev_block, hipEventDisableTiming | hipEventBlockingSync));
     for (int i = 0; i < 8; i++) {
         BPPO_HIP(c, hipEventCreate(&c->ev[i][0]));
@@ -298,6 +316,7 @@ extern "C" void bppo_destroy(bppo_ctx *c) {
     for (void *p : ptrs) if (p) (void)hipFree(p);
     fy_ranges_free(c->fyr);
     if (c->h_red) (void)hipHostFree(c->h_red);
+    if (c->h_rows) (void)hipHostFree(c->h_rows);
     if (c->ev_block) (void)hipEventDestroy(c->ev_block);
     for (int i = 0; i < 8; i++) {
         if (c->ev[i][0]) (void)hipEventDestroy(c->ev[i][0]);
@@ -603,9 +622,9 @@ static bppo_status fy_enqueue_ready(bppo_ctx *c, int slot) {
     return BPPO_OK;
 }
 
-// collect_rollouts (ppo.rs:213-500)
-extern "C" bppo_status bppo_collect_rollouts(bppo_ctx *c, bppo_rollout_info *info) {
-    if (!c) return BPPO_ERR_ARG;
+// collect_rollouts (ppo.rs:213-500), enqueue half: everything up to the episode
+// summary and the device flags' copies into pinned host words (no host wait)
+static bppo_status collect_enqueue(bppo_ctx *c, bool summary) {
     const size_t TN = (size_t)c->T * c->N;
     BPPO_HIP(c, hipMemsetAsync(c->d_ep_count, 0, 4, c->stream));
     BPPO_HIP(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
@@ -637,15 +656,24 @@ extern "C" bppo_status bppo_collect_rollouts(bppo_ctx *c, bppo_rollout_info *inf
     if (c->cfg.normalize_returns) TRY(launch_return_norm(c));      // ppo.rs:390-408
     else if (!c->wide) BPPO_HIP(c, hipMemcpyAsync(c->d_rew, c->d_rew_raw, TN * 4, hipMemcpyDeviceToDevice, c->stream));
     tm_end(c, TM_RETNORM);
-    int32_t hv[2] = {0, 0};
-    double part[2 * EP_SUMMARY_BLOCKS];
-    if (info) TRY(launch_episode_summary(c));
+    if (summary) TRY(launch_episode_summary(c));
+    int32_t *hv = reinterpret_cast<int32_t *>(c->h_red + 4 * 1024 + 64);     // pinned: truly async copies
+    double *part = c->h_red + 4 * 1024 + 64 + 2;
     BPPO_HIP(c, hipMemcpyAsync(&hv[0], c->d_ep_count, 4, hipMemcpyDeviceToHost, c->stream));
     BPPO_HIP(c, hipMemcpyAsync(&hv[1], c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
-    if (info) BPPO_HIP(c, hipMemcpyAsync(part, c->d_ep_sum, sizeof(part), hipMemcpyDeviceToHost, c->stream));
-    BPPO_HIP(c, sync_stream(c));
-    tm_read(c, TM_ROLLOUT); tm_read(c, TM_RETNORM);
+    if (summary) BPPO_HIP(c, hipMemcpyAsync(part, c->d_ep_sum, sizeof(double) * 2 * EP_SUMMARY_BLOCKS,
+                                            hipMemcpyDeviceToHost, c->stream));
     c->collected = 1; c->gae_done = 0;
+    c->rollout_rng_pos = c->rng_pos;     // RNG position after the rollout (info; the update moves it on)
+    return BPPO_OK;
+}
+
+// finish half, after the stream has drained past collect_enqueue: device error
+// flags -> status, episode summary -> info
+static bppo_status collect_finish(bppo_ctx *c, bppo_rollout_info *info) {
+    tm_read(c, TM_ROLLOUT); tm_read(c, TM_RETNORM);
+    const int32_t *hv = reinterpret_cast<const int32_t *>(c->h_red + 4 * 1024 + 64);
+    const double *part = c->h_red + 4 * 1024 + 64 + 2;
     // device error bits: 1 non-finite log-prob, 2 empty action mask, 4 opponent seat
     // table names a model outside [0, n_models)
     if (hv[1] & 2) { c->err = "Empty action mask: an env has no valid action"; return BPPO_ERR_EMPTY_MASK; }
@@ -655,7 +683,7 @@ extern "C" bppo_status bppo_collect_rollouts(bppo_ctx *c, bppo_rollout_info *inf
     if (hv[1]) { c->err = "collect_rollouts: unknown device error flag"; return BPPO_ERR_HIP; }
     if (info) {
         info->episodes = hv[0];
-        info->rng_word_pos = c->rng_pos;
+        info->rng_word_pos = c->rollout_rng_pos;
         info->mean_return = 0; info->mean_length = 0;
         const int n = std::min(hv[0], c->eps_cap);
         if (n > 0) {
@@ -665,6 +693,13 @@ extern "C" bppo_status bppo_collect_rollouts(bppo_ctx *c, bppo_rollout_info *inf
         }
     }
     return BPPO_OK;
+}
+
+extern "C" bppo_status bppo_collect_rollouts(bppo_ctx *c, bppo_rollout_info *info) {
+    if (!c) return BPPO_ERR_ARG;
+    TRY(collect_enqueue(c, info != nullptr));
+    BPPO_HIP(c, sync_stream(c));
+    return collect_finish(c, info);
 }
 
 extern "C" bppo_status bppo_rollout_episodes(bppo_ctx *c, bppo_episode *eps, int32_t cap, int32_t *n) {
@@ -691,14 +726,12 @@ extern "C" bppo_status bppo_rollout_episodes(bppo_ctx *c, bppo_episode *eps, int
 }
 
 // bootstrap + GAE (main.rs:877-947)
-extern "C" bppo_status bppo_compute_gae(bppo_ctx *c) {
-    if (!c || !c->collected) { if (c) c->err = "compute_gae before collect_rollouts"; return BPPO_ERR_ARG; }
+// enqueue half (the CartPole path has no host read in it)
+static bppo_status gae_enqueue(bppo_ctx *c) {
     if (c->wide) {
         tm_begin(c, TM_GAE);
         TRY(wide_bootstrap_gae(c));
         tm_end(c, TM_GAE);
-        BPPO_HIP(c, sync_stream(c));
-        tm_read(c, TM_GAE);
         c->gae_done = 1;
         return BPPO_OK;
     }
@@ -712,9 +745,16 @@ extern "C" bppo_status bppo_compute_gae(bppo_ctx *c) {
                                   c->stream);
     tm_end(c, TM_GAE);
     if (s != BPPO_OK) { c->err = "gae launch failed"; return s; }
-    BPPO_HIP(c, sync_stream(c));
-    tm_read(c, TM_BOOT); tm_read(c, TM_GAE);
     c->gae_done = 1;
+    return BPPO_OK;
+}
+
+extern "C" bppo_status bppo_compute_gae(bppo_ctx *c) {
+    if (!c || !c->collected) { if (c) c->err = "compute_gae before collect_rollouts"; return BPPO_ERR_ARG; }
+    TRY(gae_enqueue(c));
+    BPPO_HIP(c, sync_stream(c));
+    if (!c->wide) tm_read(c, TM_BOOT);
+    tm_read(c, TM_GAE);
     return BPPO_OK;
 }
 
@@ -833,8 +873,11 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
     }
     if (deferred && nrow > 0) {
         rows.resize((size_t)nrow * (NM + 4));
-        BPPO_HIP(c, hipMemcpyAsync(rows.data(), c->d_rows, sizeof(float) * rows.size(), hipMemcpyDeviceToHost, c->stream));
+        // into pinned memory: a pageable destination makes the copy synchronous and the
+        // host thread spins in it for the whole update (a CPU the shuffle walkers need)
+        BPPO_HIP(c, hipMemcpyAsync(c->h_rows, c->d_rows, sizeof(float) * rows.size(), hipMemcpyDeviceToHost, c->stream));
         BPPO_HIP(c, sync_stream(c));
+        std::memcpy(rows.data(), c->h_rows, sizeof(float) * rows.size());
         float ms = 0;
         if (hipEventElapsedTime(&ms, c->ev[TM_FWDBWD][0], c->ev[TM_FWDBWD][1]) == hipSuccess) fw_ms = ms;
         if (hipEventElapsedTime(&ms, c->ev[TM_SHUFFLE][0], c->ev[TM_SHUFFLE][1]) == hipSuccess) sh_ms = ms;
@@ -925,6 +968,29 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
     return BPPO_OK;
 }
 
+// One iteration of main.rs:860-947 + ppo_update in one call: the rollout, the
+// bootstrap/GAE and the update are enqueued back to back with no host wait
+// between them (bppo_collect_rollouts and bppo_compute_gae each drain the stream
+// for their results).  The rollout's device error flags are read after the update:
+// a non-finite log-prob or an empty mask returns its status then, with the update
+// already applied (the reference panics before updating; either way the run ends).
+extern "C" bppo_status bppo_train_step(bppo_ctx *c, double lr, double ent_coef, bppo_rollout_info *info,
+                                       bppo_update_metrics *m) {
+    if (!c) return BPPO_ERR_ARG;
+    const auto t0 = std::chrono::steady_clock::now();
+    c->sync_wait_ms = 0.0;
+    TRY(collect_enqueue(c, info != nullptr));
+    TRY(gae_enqueue(c));
+    const bppo_status us = bppo_ppo_update(c, lr, ent_coef, m);   // drains the stream at its end
+    if (us == BPPO_OK) { if (!c->wide) tm_read(c, TM_BOOT); tm_read(c, TM_GAE); }
+    const bppo_status cs = collect_finish(c, info);
+    // host time in the call outside stream waits: enqueue work + engine waits
+    c->last_host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() -
+                      c->sync_wait_ms;
+    c->last_sync_ms = c->sync_wait_ms;
+    return cs != BPPO_OK ? cs : us;
+}
+
 extern "C" bppo_status bppo_set_allreduce(bppo_ctx *c, bppo_allreduce_fn fn, void *user, int32_t world) {
     if (!c || world < 1) return BPPO_ERR_ARG;
     c->allreduce = fn; c->allreduce_user = user; c->world = world; c->allreduce_async = 0;
@@ -1013,6 +1079,8 @@ extern "C" bppo_status bppo_last_kernel_ms(bppo_ctx *c, const char *k, float *ms
     // time ppo_update blocked waiting for it
     if (!strcmp(k, "shuffle_walk")) { *ms = (float)c->last_walk_ms; return BPPO_OK; }
     if (!strcmp(k, "shuffle_wait")) { *ms = (float)c->last_wait_ms; return BPPO_OK; }
+    if (!strcmp(k, "host_enqueue")) { *ms = (float)c->last_host_ms; return BPPO_OK; }   // bppo_train_step outside stream waits
+    if (!strcmp(k, "host_sync_wait")) { *ms = (float)c->last_sync_ms; return BPPO_OK; }
     if (!strcmp(k, "shuffle_walk_tsc_ms")) { *ms = (float)c->last_walk_cpu_ms; return BPPO_OK; }    // all walks, in chain_walk
     if (!strcmp(k, "shuffle_words_tsc_ms")) { *ms = (float)c->last_words_cpu_ms; return BPPO_OK; }  // all walks, getting words
     if (!strcmp(k, "shuffle_spec_mwords")) { *ms = (float)c->last_spec_mwords; return BPPO_OK; }   // speculative walk words (M)

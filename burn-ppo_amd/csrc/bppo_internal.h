@@ -253,6 +253,7 @@ struct bppo_ctx {
     // main RNG
     bppo::Key8 rng_key{};
     uint64_t rng_pos = 0;
+    uint64_t rollout_rng_pos = 0;     // rng_pos right after the last rollout (bppo_rollout_info)
     // shuffle
     bppo::ShuffleEngine shuf;
     uint32_t *d_perm = nullptr;       // shuffled indices of the current epoch (may point into d_perm_ep)
@@ -273,6 +274,7 @@ struct bppo_ctx {
     // scratch
     double *d_red = nullptr;          // reduction scratch
     double *h_red = nullptr;          // pinned mirror
+    float *h_rows = nullptr;          // pinned: the update's metric rows
     float *d_mb_stats = nullptr;      // advantage [mean, std, min, max] of each minibatch of the epoch [M][4]
     float *d_mb_cur = nullptr;        // the current minibatch's row of d_mb_stats
     float *d_rows = nullptr;          // per-minibatch metric rows of one update [E*M][WM_COUNT + 4]
@@ -344,6 +346,7 @@ struct bppo_ctx {
     hipEvent_t ev_block = nullptr;    // blocking-sync event for host waits on the stream
     float last_ms[8] = {0};
     double last_walk_ms = 0.0, last_wait_ms = 0.0;
+    double sync_wait_ms = 0.0, last_host_ms = 0.0, last_sync_ms = 0.0;   // bppo_train_step host split
     double last_spec_mwords = 0.0, last_true_mwords = 0.0;   // host walk work since the previous update
     double last_walk_cpu_ms = 0.0, last_words_cpu_ms = 0.0;   // thread time in chain_walk / in words()
     int last_met = 0;

@@ -173,6 +173,11 @@ bppo_status bppo_collect_rollouts(bppo_ctx *ctx, bppo_rollout_info *info);
 bppo_status bppo_rollout_episodes(bppo_ctx *ctx, bppo_episode *eps, int32_t cap, int32_t *n);
 bppo_status bppo_compute_gae(bppo_ctx *ctx);
 bppo_status bppo_ppo_update(bppo_ctx *ctx, double lr, double ent_coef, bppo_update_metrics *m);
+/* the three calls above as one (main.rs:860-947 then ppo.rs:1661-2112): enqueued back to
+ * back with one host wait at the end; the rollout's error statuses are reported after
+ * the update (info may be NULL) */
+bppo_status bppo_train_step(bppo_ctx *ctx, double lr, double ent_coef, bppo_rollout_info *info,
+                            bppo_update_metrics *m);
 
 /* multi-GPU: called once per minibatch with the flat f32 gradient (+ metric
  * partials) in DEVICE memory, on the context's stream, before clip + Adam.

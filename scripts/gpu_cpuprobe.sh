@@ -1,6 +1,8 @@
-# frontier depth A/B with per-thread CPU time
+# shuffle engine parity, then the default bench repeated (per-thread CPU, walk/wait split)
 set -u
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-STEPS=20 bash scripts/bench_ab.sh ab_cpu 2 BPPO_SHUFFLE_FRONTIER=1 BPPO_SHUFFLE_FRONTIER=2 "BPPO_SHUFFLE_FRONTIER=2 BPPO_SHUFFLE_SPEC=4"
+timeout -k 10 300 python -u -m pytest tests/test_shuffle.py -m gpu -q -x --timeout 200 --timeout-method thread > gpurun_out/pytest_frontier.log 2>&1
+rc=$?; tail -2 gpurun_out/pytest_frontier.log; [ $rc -eq 0 ] || exit $rc
+STEPS=20 bash scripts/bench_ab.sh ab_cpu 3 BPPO_SHUFFLE_FRONTIER=1

@@ -293,3 +293,33 @@ def test_empty_mask_and_nonfinite_statuses():
             bppo.collect_rollouts(tr.ctx)
         assert ei.value.status == L.ERR_NONFINITE, (preset, N, ei.value)
         tr.close()
+
+
+@pytest.mark.parametrize("preset,N,T", [("cartpole", 4096, 64), ("connect_four", 256, 16)])
+def test_train_step_equals_three_calls(preset, N, T):
+    """bppo_train_step (rollout, bootstrap/GAE and update enqueued with one host wait)
+    gives bit-for-bit the parameters, metrics, rollout info and RNG position of
+    collect_rollouts + compute_gae + ppo_update; a NaN rollout still returns
+    BPPO_ERR_NONFINITE."""
+    cfg = bppo.make_config(preset, num_envs=N, num_steps=T, seed=11)
+    a, b = bppo.Trainer(cfg, init_seed=3), bppo.Trainer(cfg, init_seed=3)
+    try:
+        for _ in range(3):
+            ia = bppo.collect_rollouts(a.ctx)
+            bppo.compute_gae(a.ctx)
+            ma = bppo.ppo_update(a.ctx, 3e-4, 0.01)
+            ib, mb = bppo.train_step(b.ctx, 3e-4, 0.01)
+            assert (ia.episodes, ia.mean_return, ia.mean_length, ia.rng_word_pos) == \
+                   (ib.episodes, ib.mean_return, ib.mean_length, ib.rng_word_pos)
+            assert bits(a.model.get_params()).tolist() == bits(b.model.get_params()).tolist()
+            for k, v in ma.items():
+                assert bits(np.float32(v)) == bits(np.float32(mb[k])) or (np.isnan(v) and np.isnan(mb[k])), k
+        p = b.model.get_params()
+        p[:] = np.nan
+        b.model.set_params(p)
+        with pytest.raises(L.BppoError) as ei:
+            bppo.train_step(b.ctx, 3e-4, 0.01)
+        assert ei.value.status == L.ERR_NONFINITE
+    finally:
+        a.close()
+        b.close()
