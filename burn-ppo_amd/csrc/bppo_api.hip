@@ -874,13 +874,9 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
     if (deferred && nrow > 0) {
         rows.resize((size_t)nrow * (NM + 4));
         // into pinned memory: a pageable destination makes the copy synchronous and the
-        // host thread spins in it for the whole update (a CPU the shuffle walkers need)
+        // host thread spins in it for the whole update (a CPU the shuffle walkers need);
+        // read after the one stream wait below, behind the explained-variance pass
         BPPO_HIP(c, hipMemcpyAsync(c->h_rows, c->d_rows, sizeof(float) * rows.size(), hipMemcpyDeviceToHost, c->stream));
-        BPPO_HIP(c, sync_stream(c));
-        std::memcpy(rows.data(), c->h_rows, sizeof(float) * rows.size());
-        float ms = 0;
-        if (hipEventElapsedTime(&ms, c->ev[TM_FWDBWD][0], c->ev[TM_FWDBWD][1]) == hipSuccess) fw_ms = ms;
-        if (hipEventElapsedTime(&ms, c->ev[TM_SHUFFLE][0], c->ev[TM_SHUFFLE][1]) == hipSuccess) sh_ms = ms;
     }
     tm_end(c, TM_UPDATE);
     c->last_wait_ms = wait_ms;
@@ -912,8 +908,16 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
         c->shuf.ensure(c->rng_pos + (uint64_t)c->T * c->N * (uint64_t)c->A);
     }
     TRY(popart_target_stats(c, stop ? epochs_run - 1 : epochs_run, rows_done, opp ? c->d_valid : nullptr));
+    TRY(launch_explained_variance(c, opp ? c->d_valid : nullptr));
+    BPPO_HIP(c, sync_stream(c));
+    if (deferred && nrow > 0) {
+        std::memcpy(rows.data(), c->h_rows, sizeof(float) * rows.size());
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, c->ev[TM_FWDBWD][0], c->ev[TM_FWDBWD][1]) == hipSuccess) fw_ms = ms;
+        if (hipEventElapsedTime(&ms, c->ev[TM_SHUFFLE][0], c->ev[TM_SHUFFLE][1]) == hipSuccess) sh_ms = ms;
+    }
     double ev4[4];
-    TRY(launch_explained_variance(c, ev4, opp ? c->d_valid : nullptr));
+    explained_variance_sums(c, ev4);
     tm_read(c, TM_UPDATE);
     c->last_ms[TM_FWDBWD] = fw_ms;
     c->last_ms[TM_SHUFFLE] = sh_ms;

@@ -392,7 +392,8 @@ bppo_status launch_adam(bppo_ctx *c, float lr, const float *c1, const float *c2,
                         int nm = 0);
 bppo_status launch_metric_row(bppo_ctx *c, float *dst, int nm);
 bppo_status launch_pack_rows(bppo_ctx *c);
-bppo_status launch_explained_variance(bppo_ctx *c, double *out6, const float *valid = nullptr);
+bppo_status launch_explained_variance(bppo_ctx *c, const float *valid);
+void explained_variance_sums(bppo_ctx *c, double *out4);   // after the stream wait
 // (wide_api.hip) multi-player path
 bppo_status wide_init(bppo_ctx *c);
 void wide_free(bppo_ctx *c);

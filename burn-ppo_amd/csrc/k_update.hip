@@ -1172,16 +1172,19 @@ bppo_status launch_adam(bppo_ctx *c, float lr, const float *c1, const float *c2,
     return BPPO_OK;
 }
 
-bppo_status launch_explained_variance(bppo_ctx *c, double *out4, const float *valid) {
+// enqueue: block sums into pinned h_red; explained_variance_sums reads them once the
+// caller has waited for the stream
+bppo_status launch_explained_variance(bppo_ctx *c, const float *valid) {
     const size_t n = (size_t)c->T * c->N;
     hipLaunchKernelGGL(k_ev, dim3(STAT_BLOCKS), dim3(256), 0, c->stream, n, c->d_val, c->d_ret, valid, c->d_red);
     BPPO_HIP(c, hipMemcpyAsync(c->h_red, c->d_red, sizeof(double) * 4 * STAT_BLOCKS,
                                hipMemcpyDeviceToHost, c->stream));
-    BPPO_HIP(c, hipStreamSynchronize(c->stream));
+    return BPPO_OK;
+}
+void explained_variance_sums(bppo_ctx *c, double *out4) {
     for (int k = 0; k < 4; k++) out4[k] = 0.0;
     for (int b = 0; b < STAT_BLOCKS; b++)
         for (int k = 0; k < 4; k++) out4[k] += c->h_red[b * 4 + k];
-    return BPPO_OK;
 }
 
 }  // namespace bppo

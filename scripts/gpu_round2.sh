@@ -14,4 +14,6 @@ timeout -k 10 400 python bench.py > gpurun_out/bench_$TAG.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -2 gpurun_out/bench_$TAG.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/kt_$TAG -o kt -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-learning > gpurun_out/kt_$TAG.log 2>&1
 rc=$?; echo "kt rc=$rc"; [ $rc -eq 0 ] || exit $rc
+python3 scripts/rocpd_summary.py $(find gpurun_out/kt_$TAG -name "*.db" | head -1) > gpurun_out/kt_$TAG.txt
+python3 scripts/kt_timeline.py $(find gpurun_out/kt_$TAG -name "*.db" | head -1) > gpurun_out/kt_${TAG}_timeline.txt
 bash scripts/pmc_traffic.sh $TAG
