@@ -611,6 +611,9 @@ static bppo_status fy_enqueue_ready(bppo_ctx *c, int slot) {
     while (c->fy_done < c->cfg.num_epochs && c->shuf.epoch_ready(slot, c->fy_done)) {
         const int e = c->fy_done;
         BPPO_HIP(c, hipStreamWaitEvent(c->fy_stream, c->shuf.ev[slot][e], 0));
+        // the previous epoch may have been permuted on the update stream (late epochs,
+        // BPPO_FY_LATE_INLINE): the scratch is shared
+        if (e > 0) BPPO_HIP(c, hipStreamWaitEvent(c->fy_stream, c->fy_ev[e - 1], 0));
         (void)hipEventRecord(c->ev[TM_SHUFFLE][0], c->fy_stream);
         BPPO_HIP(c, fisher_yates_device(c->shuf.d_J[slot] + (size_t)e * B, (uint32_t)B, c->d_fy, c->d_scan,
                                         c->d_perm_ep + (size_t)e * B, c->fy_stream, &c->fyr,
@@ -810,10 +813,28 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
             if (B) TRY(opp_map_perm(c, (uint32_t)B));
             (void)hipEventRecord(s1, c->stream);
         } else {
+            static const bool late_inline = getenv("BPPO_FY_LATE_INLINE") ? atoi(getenv("BPPO_FY_LATE_INLINE")) != 0 : false;
             if (slot != c->fy_slot || ep >= c->fy_done) {
                 auto w0 = std::chrono::steady_clock::now();
                 c->shuf.wait_epoch(slot, ep);
                 wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
+                if (late_inline) {
+                    // an epoch not permuted ahead: on the update stream, between the previous
+                    // epoch's minibatches and this one's, instead of beside them
+                    if (slot != c->fy_slot) { c->fy_slot = slot; c->fy_done = 0; }
+                    while (c->fy_done <= ep) {
+                        const int e = c->fy_done;
+                        if (e > 0) BPPO_HIP(c, hipStreamWaitEvent(c->stream, c->fy_ev[e - 1], 0));
+                        BPPO_HIP(c, hipStreamWaitEvent(c->stream, c->shuf.ev[slot][e], 0));
+                        (void)hipEventRecord(c->ev[TM_SHUFFLE][0], c->stream);
+                        BPPO_HIP(c, fisher_yates_device(c->shuf.d_J[slot] + (size_t)e * B, (uint32_t)B, c->d_fy,
+                                                        c->d_scan, c->d_perm_ep + (size_t)e * B, c->stream, &c->fyr,
+                                                        c->d_inv_ep + (size_t)e * B));
+                        (void)hipEventRecord(c->ev[TM_SHUFFLE][1], c->stream);
+                        BPPO_HIP(c, hipEventRecord(c->fy_ev[e], c->stream));
+                        c->fy_done++;
+                    }
+                }
             }
             TRY(fy_enqueue_ready(c, slot));          // this epoch and any other resolved since
             BPPO_HIP(c, hipStreamWaitEvent(c->stream, c->fy_ev[ep], 0));
