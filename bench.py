@@ -288,8 +288,7 @@ def main():
         ctypes.CDLL(None).prctl(15, b"bench-main", 0, 0, 0)       # PR_SET_NAME
     except (OSError, AttributeError):
         pass
-    for _ in range(args.warmup):
-        tr.train_update()
+    tr.train_updates(args.warmup)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -300,11 +299,18 @@ def main():
              "shuffle_walk": 0.0, "shuffle_wait": 0.0, "shuffle_met": 0.0,
              "shuffle_spec_mwords": 0.0, "shuffle_true_mwords": 0.0,
              "shuffle_walk_tsc_ms": 0.0, "shuffle_words_tsc_ms": 0.0, "host_enqueue": 0.0, "host_sync_wait": 0.0}
-    last = None
-    for _ in range(args.steps):
-        last = tr.train_update()
-        for k in phase:
-            phase[k] += tr.ctx.kernel_ms(k)
+    # the K updates in one pipelined call (bppo_train_steps: each rollout enqueued behind
+    # the previous update, per-update phase times summed on the host side of the library)
+    if os.environ.get("BPPO_BENCH_SEQUENTIAL") == "1":     # A/B: one train_update call per step
+        last = None
+        for _ in range(args.steps):
+            last = tr.train_update()
+            for k in phase:
+                phase[k] += tr.ctx.kernel_ms(k)
+    else:
+        mets, sums = tr.train_updates(args.steps, tuple(phase))
+        phase.update(sums)
+        last = mets[-1]
     torch.cuda.synchronize()
     if dist:
         dist.barrier()

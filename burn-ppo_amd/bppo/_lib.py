@@ -77,7 +77,7 @@ EXPORTS = (
     "bppo_params_set", "bppo_params_get", "bppo_forward", "bppo_rng_get", "bppo_rng_set",
     "bppo_vecenv_reset", "bppo_vecenv_observe", "bppo_vecenv_step", "bppo_vecenv_set_step", "bppo_set_reward_shaping_schedule",
     "bppo_obs_norm_get", "bppo_obs_norm_set", "bppo_ret_norm_get", "bppo_ret_norm_set",
-    "bppo_collect_rollouts", "bppo_rollout_episodes", "bppo_compute_gae", "bppo_ppo_update", "bppo_train_step",
+    "bppo_collect_rollouts", "bppo_rollout_episodes", "bppo_compute_gae", "bppo_ppo_update", "bppo_train_step", "bppo_train_steps",
     "bppo_set_allreduce", "bppo_set_allreduce_async", "bppo_get_stream", "bppo_opponents_set", "bppo_opponents_get_envs", "bppo_buffer_get", "bppo_buffer_set", "bppo_gae_device",
     "bppo_gae_mp_device", "bppo_last_kernel_ms", "bppo_debug_libm", "bppo_debug_shuffle_chain",
     "bppo_debug_fisher_yates", "bppo_debug_gemm", "bppo_debug_shuffle_engine", "bppo_debug_sample",
@@ -132,6 +132,7 @@ def lib():
         "bppo_compute_gae": (i32, [vp]),
         "bppo_ppo_update": (i32, [vp, C.c_double, C.c_double, C.POINTER(UpdateMetrics)]),
         "bppo_train_step": (i32, [vp, C.c_double, C.c_double, C.POINTER(RolloutInfo), C.POINTER(UpdateMetrics)]),
+        "bppo_train_steps": (i32, [vp, i32, vp, vp, C.c_uint64, vp, vp, vp, i32, vp]),
         "bppo_set_allreduce": (i32, [vp, ALLREDUCE_FN, vp, i32]),
         "bppo_set_allreduce_async": (i32, [vp, ALLREDUCE_FN, vp, i32]),
         "bppo_get_stream": (i32, [vp, C.POINTER(vp)]),

@@ -388,5 +388,27 @@ class Trainer:
         metrics["mean_return"] = info.mean_return
         return metrics
 
+    def train_updates(self, n, phase_keys=()):
+        """n iterations of train_update in one pipelined call (bppo_train_steps): the
+        same results as n train_update(track_returns=False) calls, the GPU never idle
+        between them.  -> (list of metrics dicts, {key: sum of last_kernel_ms(key)})."""
+        lr = np.array([schedule_get(self.cfg["learning_rate"], self.global_step + k * self.ctx.T * self.ctx.N)
+                       for k in range(n)], np.float64)
+        ent = np.array([schedule_get(self.cfg["entropy_coef"], self.global_step + k * self.ctx.T * self.ctx.N)
+                        for k in range(n)], np.float64)
+        infos, ms = (L.RolloutInfo * max(n, 1))(), (L.UpdateMetrics * max(n, 1))()
+        keys = (C.c_char_p * max(len(phase_keys), 1))(*[k.encode() for k in phase_keys])
+        sums = np.zeros(max(len(phase_keys), 1), np.float32)
+        self.ctx._chk(L.lib().bppo_train_steps(self.ctx.h, n, lr.ctypes.data, ent.ctypes.data, self.global_step,
+                                                infos, ms, keys, len(phase_keys), sums.ctypes.data))
+        out = []
+        for k in range(n):
+            d = _metrics_dict(ms[k])
+            d["episodes"] = infos[k].episodes
+            d["mean_return"] = infos[k].mean_return
+            out.append(d)
+        self.global_step += n * self.ctx.T * self.ctx.N
+        return out, {k: float(sums[i]) for i, k in enumerate(phase_keys)}
+
     def close(self):
         self.ctx.close()

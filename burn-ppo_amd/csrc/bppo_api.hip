@@ -135,6 +135,14 @@ extern "C" const char *bppo_last_error(const bppo_ctx *c) { return c ? c->err.c_
 // instead of polling (polling eats the CPU quota the shuffle walkers run on)
 // (hipEventSynchronize on a blocking-sync event still spun here: measured ~1 CPU per
 // process for the whole update; a sleeping poll at 20 us with 1 us timer slack frees it)
+static hipError_t wait_event(bppo_ctx *c, hipEvent_t ev) {   // sleeping poll (see sync_stream)
+    const auto t0 = std::chrono::steady_clock::now();
+    hipError_t e;
+    while ((e = hipEventQuery(ev)) == hipErrorNotReady) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    c->sync_wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return e;
+}
+
 static hipError_t sync_stream(bppo_ctx *c) {
     const auto t0 = std::chrono::steady_clock::now();
     hipError_t e;
@@ -266,10 +274,12 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
                               hipHostMallocDefault));
     if (!c->wide && cfg->hidden_size == 64 && cfg->num_hidden == 2 && cfg->relu && c->D == 5)
         BPPO_HIP(c, hipMalloc((void **)&c->d_mbrow, sizeof(float4) * 4 * TN));
-    BPPO_HIP(c, hipHostMalloc((void **)&c->h_red, sizeof(double) * (4 * 1024 + 64 + 2 + 2 * EP_SUMMARY_BLOCKS),
-                              hipHostMallocDefault));   // + the rollout's flags and episode partials
+    BPPO_HIP(c, hipHostMalloc((void **)&c->h_red, sizeof(double) * (4 * 1024 + 64 + 2 * ROLL_HOST_WORDS),
+                              hipHostMallocDefault));   // + two slots of the rollout's flags and episode partials
+    BPPO_HIP(c, hipEventCreateWithFlags(&c->ev_upd, hipEventDisableTiming));
+    BPPO_HIP(c, hipEventRecord(c->ev_upd, c->stream));      // recorded once, so every wait on it is defined
     BPPO_HIP(c, hipEventCreateWithFlags(&c->ev_block, hipEventDisableTiming | hipEventBlockingSync));
-    for (int i = 0; i < 8; i++) {
+    for (int i = 0; i < TM_SLOTS; i++) {
         BPPO_HIP(c, hipEventCreate(&c->ev[i][0]));
         BPPO_HIP(c, hipEventCreate(&c->ev[i][1]));
     }
@@ -318,7 +328,8 @@ extern "C" void bppo_destroy(bppo_ctx *c) {
     if (c->h_red) (void)hipHostFree(c->h_red);
     if (c->h_rows) (void)hipHostFree(c->h_rows);
     if (c->ev_block) (void)hipEventDestroy(c->ev_block);
-    for (int i = 0; i < 8; i++) {
+    if (c->ev_upd) (void)hipEventDestroy(c->ev_upd);
+    for (int i = 0; i < TM_SLOTS; i++) {
         if (c->ev[i][0]) (void)hipEventDestroy(c->ev[i][0]);
         if (c->ev[i][1]) (void)hipEventDestroy(c->ev[i][1]);
     }
@@ -607,7 +618,13 @@ static void tm_read(bppo_ctx *c, int slot) {
 // permutation of epoch e depends only on that epoch's RNG words)
 static bppo_status fy_enqueue_ready(bppo_ctx *c, int slot) {
     const size_t B = (size_t)c->T * c->N;
-    if (slot != c->fy_slot) { c->fy_slot = slot; c->fy_done = 0; }
+    if (slot != c->fy_slot) {
+        // a new update's permutations overwrite perm/inv, which the previous update's
+        // minibatches may still be reading when its successor's rollout is enqueued
+        // behind it (bppo_train_steps): wait for the end of that update
+        c->fy_slot = slot; c->fy_done = 0;
+        BPPO_HIP(c, hipStreamWaitEvent(c->fy_stream, c->ev_upd, 0));
+    }
     while (c->fy_done < c->cfg.num_epochs && c->shuf.epoch_ready(slot, c->fy_done)) {
         const int e = c->fy_done;
         BPPO_HIP(c, hipStreamWaitEvent(c->fy_stream, c->shuf.ev[slot][e], 0));
@@ -627,18 +644,25 @@ static bppo_status fy_enqueue_ready(bppo_ctx *c, int slot) {
 
 // collect_rollouts (ppo.rs:213-500), enqueue half: everything up to the episode
 // summary and the device flags' copies into pinned host words (no host wait)
+// the rollout's device flags and episode partials land in one of two pinned slots, so
+// a rollout enqueued behind an update (bppo_train_steps) does not overwrite the
+// previous rollout's before they are read
+static double *roll_host(bppo_ctx *c, int slot) { return c->h_red + 4 * 1024 + 64 + (size_t)slot * ROLL_HOST_WORDS; }
+
 static bppo_status collect_enqueue(bppo_ctx *c, bool summary) {
     const size_t TN = (size_t)c->T * c->N;
+    c->coll_slot ^= 1;
+    const int tro = c->coll_slot ? TM_ROLLOUT_B : TM_ROLLOUT, trn = c->coll_slot ? TM_RETNORM_B : TM_RETNORM;
     BPPO_HIP(c, hipMemsetAsync(c->d_ep_count, 0, 4, c->stream));
     BPPO_HIP(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
     const uint64_t base = c->rng_pos;
-    tm_begin(c, TM_ROLLOUT);
+    tm_begin(c, tro);
     if (c->wide) TRY(wide_collect(c, base));
     else {
         TRY(launch_cartpole_rollout(c, base, nullptr, nullptr, c->cfg.normalize_obs));
         TRY(popart_denorm(c, c->d_val, TN));            // ppo.rs:355-359 (multi-player: in the sampler)
     }
-    tm_end(c, TM_ROLLOUT);
+    tm_end(c, tro);
     // self-play: the update's shuffles start right after this rollout's Gumbel words,
     // so the epochs the engine has resolved are permuted now, beside the rollout
     static const bool fy_ahead = getenv("BPPO_FY_AHEAD") ? atoi(getenv("BPPO_FY_AHEAD")) != 0 : true;
@@ -655,28 +679,31 @@ static bppo_status collect_enqueue(bppo_ctx *c, bool summary) {
         c->shuf_slot = c->shuf.ensure(c->rng_pos);
     }
     if (c->cfg.normalize_obs) TRY(launch_obs_norm_merge(c));       // ppo.rs:495-497
-    tm_begin(c, TM_RETNORM);
+    tm_begin(c, trn);
     if (c->cfg.normalize_returns) TRY(launch_return_norm(c));      // ppo.rs:390-408
     else if (!c->wide) BPPO_HIP(c, hipMemcpyAsync(c->d_rew, c->d_rew_raw, TN * 4, hipMemcpyDeviceToDevice, c->stream));
-    tm_end(c, TM_RETNORM);
+    tm_end(c, trn);
     if (summary) TRY(launch_episode_summary(c));
-    int32_t *hv = reinterpret_cast<int32_t *>(c->h_red + 4 * 1024 + 64);     // pinned: truly async copies
-    double *part = c->h_red + 4 * 1024 + 64 + 2;
+    int32_t *hv = reinterpret_cast<int32_t *>(roll_host(c, c->coll_slot));     // pinned: truly async copies
+    double *part = roll_host(c, c->coll_slot) + 2;
     BPPO_HIP(c, hipMemcpyAsync(&hv[0], c->d_ep_count, 4, hipMemcpyDeviceToHost, c->stream));
     BPPO_HIP(c, hipMemcpyAsync(&hv[1], c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
     if (summary) BPPO_HIP(c, hipMemcpyAsync(part, c->d_ep_sum, sizeof(double) * 2 * EP_SUMMARY_BLOCKS,
                                             hipMemcpyDeviceToHost, c->stream));
     c->collected = 1; c->gae_done = 0;
-    c->rollout_rng_pos = c->rng_pos;     // RNG position after the rollout (info; the update moves it on)
+    c->rollout_rng_pos[c->coll_slot] = c->rng_pos;   // RNG position after the rollout (info; the update moves it on)
     return BPPO_OK;
 }
 
 // finish half, after the stream has drained past collect_enqueue: device error
 // flags -> status, episode summary -> info
-static bppo_status collect_finish(bppo_ctx *c, bppo_rollout_info *info) {
-    tm_read(c, TM_ROLLOUT); tm_read(c, TM_RETNORM);
-    const int32_t *hv = reinterpret_cast<const int32_t *>(c->h_red + 4 * 1024 + 64);
-    const double *part = c->h_red + 4 * 1024 + 64 + 2;
+static bppo_status collect_finish(bppo_ctx *c, bppo_rollout_info *info, int slot) {
+    float ms = 0;
+    const int tro = slot ? TM_ROLLOUT_B : TM_ROLLOUT, trn = slot ? TM_RETNORM_B : TM_RETNORM;
+    if (hipEventElapsedTime(&ms, c->ev[tro][0], c->ev[tro][1]) == hipSuccess) c->last_ms[TM_ROLLOUT] = ms;
+    if (hipEventElapsedTime(&ms, c->ev[trn][0], c->ev[trn][1]) == hipSuccess) c->last_ms[TM_RETNORM] = ms;
+    const int32_t *hv = reinterpret_cast<const int32_t *>(roll_host(c, slot));
+    const double *part = roll_host(c, slot) + 2;
     // device error bits: 1 non-finite log-prob, 2 empty action mask, 4 opponent seat
     // table names a model outside [0, n_models)
     if (hv[1] & 2) { c->err = "Empty action mask: an env has no valid action"; return BPPO_ERR_EMPTY_MASK; }
@@ -686,7 +713,7 @@ static bppo_status collect_finish(bppo_ctx *c, bppo_rollout_info *info) {
     if (hv[1]) { c->err = "collect_rollouts: unknown device error flag"; return BPPO_ERR_HIP; }
     if (info) {
         info->episodes = hv[0];
-        info->rng_word_pos = c->rollout_rng_pos;
+        info->rng_word_pos = c->rollout_rng_pos[slot];
         info->mean_return = 0; info->mean_length = 0;
         const int n = std::min(hv[0], c->eps_cap);
         if (n > 0) {
@@ -702,7 +729,7 @@ extern "C" bppo_status bppo_collect_rollouts(bppo_ctx *c, bppo_rollout_info *inf
     if (!c) return BPPO_ERR_ARG;
     TRY(collect_enqueue(c, info != nullptr));
     BPPO_HIP(c, sync_stream(c));
-    return collect_finish(c, info);
+    return collect_finish(c, info, c->coll_slot);
 }
 
 extern "C" bppo_status bppo_rollout_episodes(bppo_ctx *c, bppo_episode *eps, int32_t cap, int32_t *n) {
@@ -930,7 +957,19 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
     }
     TRY(popart_target_stats(c, stop ? epochs_run - 1 : epochs_run, rows_done, opp ? c->d_valid : nullptr));
     TRY(launch_explained_variance(c, opp ? c->d_valid : nullptr));
-    BPPO_HIP(c, sync_stream(c));
+    BPPO_HIP(c, hipEventRecord(c->ev_upd, c->stream));      // end of this update's work
+    if (c->prefetch_next) {
+        // bppo_train_steps: the next rollout goes in behind this update (it needs only the
+        // updated parameters and the RNG position after this update's shuffles, both in
+        // stream / host order now); the host then waits for this update alone
+        c->prefetch_next = false;
+        c->env_step = c->prefetch_env_step;
+        TRY(collect_enqueue(c, true));
+        c->prefetched = true;
+        BPPO_HIP(c, wait_event(c, c->ev_upd));
+    } else {
+        BPPO_HIP(c, sync_stream(c));
+    }
     if (deferred && nrow > 0) {
         std::memcpy(rows.data(), c->h_rows, sizeof(float) * rows.size());
         float ms = 0;
@@ -1008,12 +1047,51 @@ extern "C" bppo_status bppo_train_step(bppo_ctx *c, double lr, double ent_coef, 
     TRY(gae_enqueue(c));
     const bppo_status us = bppo_ppo_update(c, lr, ent_coef, m);   // drains the stream at its end
     if (us == BPPO_OK) { if (!c->wide) tm_read(c, TM_BOOT); tm_read(c, TM_GAE); }
-    const bppo_status cs = collect_finish(c, info);
+    const bppo_status cs = collect_finish(c, info, c->coll_slot);
     // host time in the call outside stream waits: enqueue work + engine waits
     c->last_host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() -
                       c->sync_wait_ms;
     c->last_sync_ms = c->sync_wait_ms;
     return cs != BPPO_OK ? cs : us;
+}
+
+// n iterations of bppo_train_step in one call, software-pipelined: each update's
+// last stream wait covers that update only, with the next iteration's rollout
+// already enqueued behind it, so the GPU never idles between iterations (the
+// host tail of one update, the caller and the next enqueue ran in that gap).
+// Results are those of n sequential bppo_train_step calls with lr[k], ent[k] and
+// the env step global_step0 + k*T*N; nothing is left pending when it returns.
+// phase_keys/phase_sums (optional): bppo_last_kernel_ms of each key summed over the n.
+extern "C" bppo_status bppo_train_steps(bppo_ctx *c, int32_t n, const double *lr, const double *ent_coef,
+                                        uint64_t global_step0, bppo_rollout_info *infos, bppo_update_metrics *ms,
+                                        const char *const *phase_keys, int32_t nkeys, float *phase_sums) {
+    if (!c || n < 0 || !lr || !ent_coef || (nkeys > 0 && (!phase_keys || !phase_sums))) return BPPO_ERR_ARG;
+    for (int k = 0; k < nkeys; k++) phase_sums[k] = 0.0f;
+    const uint64_t TN = (uint64_t)c->T * c->N;
+    for (int32_t k = 0; k < n; k++) {
+        const auto t0 = std::chrono::steady_clock::now();
+        c->sync_wait_ms = 0.0;
+        if (!c->prefetched) { c->env_step = global_step0 + (uint64_t)k * TN; TRY(collect_enqueue(c, true)); }
+        c->prefetched = false;
+        const int slot = c->coll_slot;
+        TRY(gae_enqueue(c));
+        c->prefetch_next = k + 1 < n;
+        c->prefetch_env_step = global_step0 + (uint64_t)(k + 1) * TN;
+        const bppo_status us = bppo_ppo_update(c, lr[k], ent_coef[k], ms ? &ms[k] : nullptr);
+        c->prefetch_next = false;
+        if (us != BPPO_OK) { c->prefetched = false; return us; }
+        if (!c->wide) tm_read(c, TM_BOOT);
+        tm_read(c, TM_GAE);
+        TRY(collect_finish(c, infos ? &infos[k] : nullptr, slot));
+        c->last_host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() -
+                          c->sync_wait_ms;
+        c->last_sync_ms = c->sync_wait_ms;
+        for (int q = 0; q < nkeys; q++) {
+            float v = 0.0f;
+            if (bppo_last_kernel_ms(c, phase_keys[q], &v) == BPPO_OK) phase_sums[q] += v;
+        }
+    }
+    return BPPO_OK;
 }
 
 extern "C" bppo_status bppo_set_allreduce(bppo_ctx *c, bppo_allreduce_fn fn, void *user, int32_t world) {

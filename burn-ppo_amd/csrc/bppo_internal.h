@@ -36,6 +36,8 @@ NetLayout make_layout(const bppo_config &c, int obs_dim, int priv_dim, int act_d
 
 // episode record written by the rollout kernel
 constexpr int EP_SUMMARY_BLOCKS = 128;   // k_ep_summary grid (partial sums per block)
+constexpr int TM_SLOTS = 10;             // phase timer event pairs (enum TM_* below)
+constexpr int ROLL_HOST_WORDS = 2 + 2 * EP_SUMMARY_BLOCKS;     // pinned doubles per rollout slot
 constexpr int ADV_STREAM_BLOCKS = 512, ADV_STREAM_MAXM = 16;   // k_adv_stream grid, most minibatches
 
 struct EpisodeRec {
@@ -253,7 +255,6 @@ struct bppo_ctx {
     // main RNG
     bppo::Key8 rng_key{};
     uint64_t rng_pos = 0;
-    uint64_t rollout_rng_pos = 0;     // rng_pos right after the last rollout (bppo_rollout_info)
     // shuffle
     bppo::ShuffleEngine shuf;
     uint32_t *d_perm = nullptr;       // shuffled indices of the current epoch (may point into d_perm_ep)
@@ -342,7 +343,7 @@ struct bppo_ctx {
     float *d_scr_r = nullptr;         // VecEnv::step rewards [N][P]
     uint8_t *d_scr_d = nullptr;       // VecEnv::step dones [N]
     // timing
-    hipEvent_t ev[8][2] = {};
+    hipEvent_t ev[bppo::TM_SLOTS][2] = {};
     hipEvent_t ev_block = nullptr;    // blocking-sync event for host waits on the stream
     float last_ms[8] = {0};
     double last_walk_ms = 0.0, last_wait_ms = 0.0;
@@ -351,12 +352,21 @@ struct bppo_ctx {
     double last_walk_cpu_ms = 0.0, last_words_cpu_ms = 0.0;   // thread time in chain_walk / in words()
     int last_met = 0;
     int collected = 0, gae_done = 0;
+    // bppo_train_steps pipelining
+    hipEvent_t ev_upd = nullptr;      // end of an update's work (its host wait)
+    int coll_slot = 1;                // pinned / timer slot of the last enqueued rollout
+    uint64_t rollout_rng_pos[2] = {0, 0};
+    bool prefetch_next = false, prefetched = false;
+    uint64_t prefetch_env_step = 0;
 };
 
 namespace bppo {
 // kernel-phase timer slots
 enum { TM_ROLLOUT = 0, TM_GAE = 1, TM_UPDATE = 2, TM_FWDBWD = 3, TM_RETNORM = 4, TM_SHUFFLE = 5,
        TM_ADAM = 6, TM_BOOT = 7 };
+// the rollout / return-normaliser events of the other rollout slot (bppo_train_steps
+// enqueues a rollout while the previous one's events are still to be read)
+enum { TM_ROLLOUT_B = 8, TM_RETNORM_B = 9 };
 
 // launchers (k_rollout.hip)
 bppo_status launch_cartpole_reset(bppo_ctx *c);

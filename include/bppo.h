@@ -178,6 +178,15 @@ bppo_status bppo_ppo_update(bppo_ctx *ctx, double lr, double ent_coef, bppo_upda
  * the update (info may be NULL) */
 bppo_status bppo_train_step(bppo_ctx *ctx, double lr, double ent_coef, bppo_rollout_info *info,
                             bppo_update_metrics *m);
+/* n bppo_train_step iterations (main.rs:684-988 loop body, lr[k] / ent_coef[k], env step
+ * global_step0 + k*T*N), software-pipelined: each iteration's rollout is enqueued behind the
+ * previous update before the host waits for that update, so the GPU does not idle between
+ * iterations.  Same results as n bppo_train_step calls; nothing pending on return.
+ * infos / ms: n entries each (may be NULL); phase_keys (bppo_last_kernel_ms names, nkeys of
+ * them): per-key sums over the n iterations into phase_sums */
+bppo_status bppo_train_steps(bppo_ctx *ctx, int32_t n, const double *lr, const double *ent_coef,
+                             uint64_t global_step0, bppo_rollout_info *infos, bppo_update_metrics *ms,
+                             const char *const *phase_keys, int32_t nkeys, float *phase_sums);
 
 /* multi-GPU: called once per minibatch with the flat f32 gradient (+ metric
  * partials) in DEVICE memory, on the context's stream, before clip + Adam.

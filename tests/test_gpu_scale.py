@@ -323,3 +323,28 @@ def test_train_step_equals_three_calls(preset, N, T):
     finally:
         a.close()
         b.close()
+
+
+@pytest.mark.parametrize("preset,N,T", [("cartpole", 4096, 64), ("connect_four", 256, 16)])
+def test_train_steps_pipelined_equals_sequential(preset, N, T):
+    """bppo_train_steps (each rollout enqueued behind the previous update) returns, for
+    every iteration, the metrics and rollout info of sequential bppo_train_step calls,
+    and leaves the same parameters and RNG position."""
+    cfg = bppo.make_config(preset, num_envs=N, num_steps=T, seed=13)
+    a, b = bppo.Trainer(cfg, init_seed=4), bppo.Trainer(cfg, init_seed=4)
+    try:
+        seq = [a.train_update() for _ in range(4)]
+        pip, sums = b.train_updates(4, ("rollout", "update"))
+        assert sums["rollout"] > 0 and sums["update"] > 0
+        for ma, mb in zip(seq, pip):
+            for k, v in ma.items():
+                assert bits(np.float32(v)) == bits(np.float32(mb[k])) or (np.isnan(v) and np.isnan(mb[k])), k
+        assert bits(a.model.get_params()).tolist() == bits(b.model.get_params()).tolist()
+        pa, pb = C.c_uint64(), C.c_uint64()
+        assert L.lib().bppo_rng_get(a.ctx.h, C.byref(pa)) == 0 and L.lib().bppo_rng_get(b.ctx.h, C.byref(pb)) == 0
+        assert pa.value == pb.value
+        # and the pipelined context carries on like the sequential one
+        assert bits(np.float32(a.train_update()["policy_loss"])) == bits(np.float32(b.train_update()["policy_loss"]))
+    finally:
+        a.close()
+        b.close()
