@@ -319,6 +319,19 @@ def main():
     th1 = thread_cpu_ms()
     host_cpu_threads = {k: round((v - th0.get(k, 0.0)) / args.steps, 1) for k, v in th1.items()
                         if v - th0.get(k, 0.0) > 0.5 * args.steps}
+    if os.environ.get("BPPO_BENCH_THREADS") == "1":      # diagnostic: every thread's CPU and wait channel
+        tick = os.sysconf("SC_CLK_TCK")
+        for t in sorted(os.listdir("/proc/self/task"), key=int):
+            try:
+                st = open(f"/proc/self/task/{t}/stat").read()
+                wch = open(f"/proc/self/task/{t}/wchan").read()
+            except OSError:
+                continue
+            f = st[st.rindex(")") + 2:].split()
+            ms = (int(f[11]) + int(f[12])) * 1000.0 / tick
+            if ms > 0:
+                print(f"thread {t} {st[st.index('(') + 1:st.rindex(')')]:16s} cpu {ms:9.1f} ms wchan {wch}",
+                      file=sys.stderr)
     host_cpu_ms = ((ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)) * 1e3 / args.steps
     if dist:
         t = torch.tensor([dt], device="cuda", dtype=torch.float64)
