@@ -770,9 +770,11 @@ static bppo_status gae_enqueue(bppo_ctx *c) {
     TRY(popart_denorm(c, c->d_last_v, (size_t)c->N));   // main.rs:898-907
     tm_end(c, TM_BOOT);
     tm_begin(c, TM_GAE);
+    bool packed = false;
     bppo_status s = launch_gae_1p(c->d_rew, c->d_done, c->d_val, c->d_last_v, c->T, c->N,
                                   (float)c->cfg.gamma, (float)c->cfg.gae_lambda, c->d_adv, c->d_ret,
-                                  c->stream);
+                                  c->stream, c->rows_from_rollout ? (float4 *)c->d_mbrow : nullptr, &packed);
+    c->rows_packed = packed;
     tm_end(c, TM_GAE);
     if (s != BPPO_OK) { c->err = "gae launch failed"; return s; }
     c->gae_done = 1;
@@ -818,7 +820,8 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
     double wait_ms = 0.0;
     tm_begin(c, TM_UPDATE);
     TRY(popart_update_begin(c, opp ? c->d_valid : nullptr));   // ppo.rs:1787-1808
-    if (c->d_mbrow) TRY(launch_pack_rows(c));
+    if (c->d_mbrow && !c->rows_packed) TRY(launch_pack_rows(c));
+    c->rows_packed = false;
     float fw_ms = 0, sh_ms = 0;
     // without a KL early stop or a host all-reduce nothing in the loop needs the
     // metrics on the host: the minibatches are enqueued back to back and the rows
@@ -1153,6 +1156,7 @@ extern "C" bppo_status bppo_buffer_set(bppo_ctx *c, const char *name, const void
     BPPO_HIP(c, hipMemcpyAsync(b.ptr, host, b.bytes, hipMemcpyHostToDevice, c->stream));
     BPPO_HIP(c, sync_stream(c));
     if (!strcmp(name, "advantages") || !strcmp(name, "returns")) c->gae_done = c->collected = 1;
+    c->rows_packed = c->rows_from_rollout = false;   // the update re-packs its rows from the buffers
     return BPPO_OK;
 }
 

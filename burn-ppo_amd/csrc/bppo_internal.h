@@ -357,6 +357,9 @@ struct bppo_ctx {
     int coll_slot = 1;                // pinned / timer slot of the last enqueued rollout
     uint64_t rollout_rng_pos[2] = {0, 0};
     bool prefetch_next = false, prefetched = false;
+    // packed update rows written by the MFMA rollout (obs, action, log-prob, value) and
+    // the GAE pass (advantage, return): k_pack_rows is skipped when both did
+    bool rows_from_rollout = false, rows_packed = false;
     uint64_t prefetch_env_step = 0;
 };
 
@@ -384,7 +387,8 @@ bppo_status launch_forward_rows(bppo_ctx *c, const float *d_obs, int B, float *d
                                 float *d_values);
 // (k_gae.hip)
 bppo_status launch_gae_1p(const float *r, const float *d, const float *v, const float *lv, int T,
-                          int N, float gamma, float lambda, float *adv, float *ret, hipStream_t s);
+                          int N, float gamma, float lambda, float *adv, float *ret, hipStream_t s,
+                          float4 *rows = nullptr, bool *rows_done = nullptr);
 bppo_status launch_gae_mp(const float *ar, const int32_t *pl, const float *d, const float *v,
                           const float *lvpp, int T, int N, int P, float gamma, float lambda,
                           float *adv, float *ret, hipStream_t s);

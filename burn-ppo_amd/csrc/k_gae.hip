@@ -75,7 +75,8 @@ __global__ void __launch_bounds__(GSEG_WAVES * 64) k_gae_1p_seg(const float4 *__
                                                                  const float4 *__restrict__ v,
                                                                  const float4 *__restrict__ lv, int T, int N4,
                                                                  int L, float gamma, float lambda,
-                                                                 float4 *__restrict__ adv, float4 *__restrict__ ret) {
+                                                                 float4 *__restrict__ adv, float4 *__restrict__ ret,
+                                                                 float4 *__restrict__ rows) {
     __shared__ float4 carry[GSEG_WAVES][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int g = blockIdx.x * 64 + lane;
@@ -129,7 +130,13 @@ __global__ void __launch_bounds__(GSEG_WAVES * 64) k_gae_1p_seg(const float4 *__
         const size_t i = (size_t)(t0 + u) * N4 + g;
         const float4 A = x0[u], vu = vv[u];
         adv[i] = A;
-        ret[i] = make_float4(__fadd_rn(A.x, vu.x), __fadd_rn(A.y, vu.y), __fadd_rn(A.z, vu.z), __fadd_rn(A.w, vu.w));
+        const float4 R = make_float4(__fadd_rn(A.x, vu.x), __fadd_rn(A.y, vu.y), __fadd_rn(A.z, vu.z), __fadd_rn(A.w, vu.w));
+        ret[i] = R;
+        if (rows) {   // the packed update rows of these 4 envs (row 4i + j): [adv, ret] at float 8
+            float2 *o = reinterpret_cast<float2 *>(rows + 4 * (4 * i) + 2);
+            o[0] = make_float2(A.x, R.x); o[8] = make_float2(A.y, R.y);
+            o[16] = make_float2(A.z, R.z); o[24] = make_float2(A.w, R.w);
+        }
     }
 }
 
@@ -184,14 +191,17 @@ __global__ void __launch_bounds__(256) k_gae_mp(const float *__restrict__ ar,
 }
 
 bppo_status launch_gae_1p(const float *r, const float *d, const float *v, const float *lv, int T,
-                          int N, float gamma, float lambda, float *adv, float *ret, hipStream_t s) {
+                          int N, float gamma, float lambda, float *adv, float *ret, hipStream_t s,
+                          float4 *rows, bool *rows_done) {
+    if (rows_done) *rows_done = false;
     if (T <= 0 || N <= 0) return BPPO_OK;
     const bool al = ((uintptr_t)r | (uintptr_t)d | (uintptr_t)v | (uintptr_t)lv | (uintptr_t)adv | (uintptr_t)ret) % 16 == 0;
     if (N % 4 == 0 && T <= GSEG_WAVES * GSEG_L && al) {
         const int N4 = N / 4, L = (T + GSEG_WAVES - 1) / GSEG_WAVES;
         hipLaunchKernelGGL(k_gae_1p_seg, dim3((N4 + 63) / 64), dim3(GSEG_WAVES * 64), 0, s, (const float4 *)r,
                            (const float4 *)d, (const float4 *)v, (const float4 *)lv, T, N4, L, gamma, lambda,
-                           (float4 *)adv, (float4 *)ret);
+                           (float4 *)adv, (float4 *)ret, rows);
+        if (rows_done) *rows_done = rows != nullptr;
     } else {
         hipLaunchKernelGGL(k_gae_1p, dim3((N + 255) / 256), dim3(256), 0, s, r, d, v, lv, T, N, gamma,
                            lambda, adv, ret);

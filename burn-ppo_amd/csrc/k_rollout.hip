@@ -115,6 +115,7 @@ struct RolloutArgs {
     double *obs_part;
     EpisodeRec *eps; int32_t *ep_count; int eps_cap;
     int32_t *err;
+    float4 *rows;        // MFMA rollout: also the update's packed rows (k_update.hip load_row), or null
 };
 
 template <int H, int NL, int ACT>
@@ -264,6 +265,7 @@ __global__ void __launch_bounds__(512, 2) k_cartpole_rollout_mfma(RolloutArgs a,
 #pragma unroll 1
     for (int t = 0; t < a.T; t++) {
         const size_t row = (size_t)t * N + e;
+        float x4 = 0.0f;
         if (h == 0) {
             float x[5] = {0, 0, 0, 0, 0};
             if (mine) {
@@ -273,6 +275,8 @@ __global__ void __launch_bounds__(512, 2) k_cartpole_rollout_mfma(RolloutArgs a,
                 nz.apply(raw, x);
 #pragma unroll
                 for (int d = 0; d < 5; d++) a.obs[row * 5 + d] = x[d];
+                if (a.rows) a.rows[row * 4] = make_float4(x[0], x[1], x[2], x[3]);
+                x4 = x[4];
             }
 #pragma unroll
             for (int d = 0; d < 5; d++) B.X[c * 9 + d] = x[d];
@@ -368,6 +372,7 @@ __global__ void __launch_bounds__(512, 2) k_cartpole_rollout_mfma(RolloutArgs a,
             a.done[row] = done ? 1.0f : 0.0f;
             a.val[row] = v;
             a.logp[row] = lp;
+            if (a.rows) a.rows[row * 4 + 1] = make_float4(x4, __int_as_float(act), lp, v);
         }
         wave_sync();
     }
@@ -575,7 +580,16 @@ bppo_status launch_cartpole_rollout(bppo_ctx *c, uint64_t base_pos, const double
     a.obs = c->d_obs; a.rew_raw = c->d_rew_raw; a.done = c->d_done; a.val = c->d_val;
     a.logp = c->d_logp; a.act = c->d_act; a.obs_part = c->d_obs_part; a.eps = c->d_eps;
     a.ep_count = c->d_ep_count; a.eps_cap = c->eps_cap; a.err = c->d_err;
+    a.rows = nullptr;
+    c->rows_from_rollout = false;
     if (h == 64 && nl == 2 && c->cfg.relu && c->d_gumbel) {
+        // the update's packed rows (obs, action, log-prob, value) written by the rollout
+        // itself; GAE adds advantage and return, so k_pack_rows is not needed (PopArt
+        // trains on normalized values computed at update start: packed there instead)
+        if (c->d_mbrow && !c->cfg.normalize_values && !getenv("BPPO_NO_FUSED_PACK")) {
+            a.rows = c->d_mbrow;
+            c->rows_from_rollout = true;
+        }
         // Gumbel noise for every (t, env, action) first, then the MFMA rollout
         const uint64_t count = (uint64_t)c->T * c->N * 2;
         const uint64_t blocks = ((base_pos + count + 15) >> 4) - (base_pos >> 4);

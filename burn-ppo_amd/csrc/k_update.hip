@@ -308,14 +308,14 @@ __device__ __forceinline__ RowData load_row(const MbArgs &g, uint32_t idx) {
     const bool ok = idx != 0xFFFFFFFFu;
     const size_t i = ok ? idx : 0;
     RowData d;
-    if (g.rows) {                     // one 64-byte line per row
+    if (g.rows) {                     // one 64-byte line per row: [obs 0..3][obs 4, action, log-prob, value][adv, ret, -, -]
         const float4 a = g.rows[i * 4], b = g.rows[i * 4 + 1];
         const float2 c = *reinterpret_cast<const float2 *>(g.rows + i * 4 + 2);
         d.x0 = ok ? a.x : 0.0f; d.x1 = ok ? a.y : 0.0f; d.x2 = ok ? a.z : 0.0f; d.x3 = ok ? a.w : 0.0f;
         d.x4 = ok ? b.x : 0.0f;
         d.a = ok ? __float_as_int(b.y) : 0;
-        d.olp = ok ? b.z : 0.0f; d.A = ok ? b.w : 0.0f; d.R = ok ? c.x : 0.0f;
-        d.ov = (ok && g.clip_value) ? c.y : 0.0f;
+        d.olp = ok ? b.z : 0.0f; d.A = ok ? c.x : 0.0f; d.R = ok ? c.y : 0.0f;
+        d.ov = (ok && g.clip_value) ? b.w : 0.0f;
         return d;
     }
     const float *o = g.obs + i * 5;
@@ -328,7 +328,7 @@ __device__ __forceinline__ RowData load_row(const MbArgs &g, uint32_t idx) {
 }
 
 // the update's rows packed once per update into 64-byte records
-// [obs 0..4, action, log-prob, advantage, return, value, pad] so the shuffled
+// [obs 0..3][obs 4, action, log-prob, value][advantage, return, -, -] so the shuffled
 // minibatch gather touches one cache line per row instead of six
 __global__ void __launch_bounds__(256) k_pack_rows(size_t B, const float *obs, const int32_t *act, const float *logp,
                                                    const float *adv, const float *ret, const float *val,
@@ -336,9 +336,8 @@ __global__ void __launch_bounds__(256) k_pack_rows(size_t B, const float *obs, c
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < B; i += (size_t)gridDim.x * blockDim.x) {
         const float *o = obs + i * 5;
         rows[i * 4] = make_float4(o[0], o[1], o[2], o[3]);
-        rows[i * 4 + 1] = make_float4(o[4], __int_as_float(act[i]), logp[i], adv[i]);
-        rows[i * 4 + 2] = make_float4(ret[i], val[i], 0.0f, 0.0f);
-        rows[i * 4 + 3] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        rows[i * 4 + 1] = make_float4(o[4], __int_as_float(act[i]), logp[i], val[i]);
+        rows[i * 4 + 2] = make_float4(adv[i], ret[i], 0.0f, 0.0f);
     }
 }
 bppo_status launch_pack_rows(bppo_ctx *c) {
