@@ -256,9 +256,7 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     TRY(dalloc(c, &c->d_inv_ep, TN * (size_t)cfg->num_epochs));
     TRY(dalloc(c, &c->d_advpart, (size_t)ADV_STREAM_BLOCKS * ADV_STREAM_MAXM * 4));
     {
-        int lo = 0, hi = 0;
-        BPPO_HIP(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
-        BPPO_HIP(c, hipStreamCreateWithPriority(&c->fy_stream, hipStreamNonBlocking, lo));
+        BPPO_HIP(c, make_side_stream(dev, &c->fy_stream));
         for (int e = 0; e < cfg->num_epochs && e < SHUF_MAX_EPOCHS; e++)
             BPPO_HIP(c, hipEventCreateWithFlags(&c->fy_ev[e], hipEventDisableTiming));
     }

@@ -194,6 +194,9 @@ struct ShuffleEngine {
     int peek(int i, uint64_t q, uint32_t *r);     // walk i's range at checkpoint q: 1 known, 0 not yet, -1 never
 };
 uint64_t shuffle_walk_host(const Key8 &key, uint64_t stream, uint64_t pos, uint32_t n, uint32_t *J);
+// a low-priority side stream (shuffle copy stream, Fisher-Yates stream); with
+// BPPO_SIDE_CUS=n restricted to n CUs spread over the device instead (CU mask)
+hipError_t make_side_stream(int device, hipStream_t *st);
 
 struct Timers {
     hipEvent_t a = nullptr, b = nullptr;

@@ -298,9 +298,7 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
         err = "shuffle trash buffer: allocation failed";
         return BPPO_ERR_HIP;
     }
-    int prio_lo = 0, prio_hi = 0;
-    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-    if (hipStreamCreateWithPriority(&copy, hipStreamNonBlocking, prio_lo) != hipSuccess) {   // lowest priority
+    if (make_side_stream(dev, &copy) != hipSuccess) {   // lowest priority
         err = "shuffle copy stream: creation failed";
         return BPPO_ERR_HIP;
     }
@@ -952,6 +950,23 @@ void ShuffleEngine::shutdown() {
         if (wb[b].d) { (void)hipFree(wb[b].d); wb[b].d = nullptr; }
         if (wb[b].h) { host_words_free(wb[b].h, wb[b].cap); wb[b].h = nullptr; }
     }
+}
+
+hipError_t make_side_stream(int device, hipStream_t *st) {
+    const char *e = getenv("BPPO_SIDE_CUS");
+    hipDeviceProp_t pr{};
+    if (e && atoi(e) > 0 && hipGetDeviceProperties(&pr, device) == hipSuccess && atoi(e) < pr.multiProcessorCount) {
+        const int ncu = pr.multiProcessorCount, want = atoi(e);
+        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+        for (int k = 0; k < want; k++) {
+            const int cu = (int)((int64_t)k * ncu / want);
+            mask[cu / 32] |= 1u << (cu % 32);
+        }
+        return hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data());
+    }
+    int lo = 0, hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+    return hipStreamCreateWithPriority(st, hipStreamNonBlocking, lo);
 }
 
 // single-shot host walk (parity hook): J for one shuffle of n from word position pos
