@@ -245,7 +245,11 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     TRY(dalloc(c, &c->d_rn_stats, 4));
     TRY(dalloc(c, &c->d_scan_agg, (TN + 4095) / 4096 + 1));
     TRY(dalloc(c, &c->d_last_v, (size_t)c->N));
-    c->eps_cap = c->N * 4 + 4096;
+    // room for every episode a rollout can complete (one per env-step): the episode
+    // summary then sums all of them (a smaller cap kept whichever episodes claimed
+    // slots first); CartPole's integer returns sum exactly in f64, so its mean does not
+    // depend on the order the waves claimed their record slots
+    c->eps_cap = (int)std::min<size_t>((size_t)c->T * c->N + 4096, (size_t)INT32_MAX / 2);
     TRY(dalloc(c, &c->d_eps, (size_t)c->eps_cap));
     TRY(dalloc(c, &c->d_ep_count, 1));
     TRY(dalloc(c, &c->d_ep_sum, 2 * EP_SUMMARY_BLOCKS));

@@ -348,3 +348,24 @@ def test_train_steps_pipelined_equals_sequential(preset, N, T):
     finally:
         a.close()
         b.close()
+
+
+def test_fused_row_packing_equals_pack_pass(monkeypatch):
+    """The update rows written by the MFMA rollout and the segmented GAE give bit-for-bit
+    the parameters and metrics of the k_pack_rows pass (BPPO_NO_FUSED_PACK=1)."""
+    cfg = bppo.make_config("cartpole", num_envs=8192, num_steps=128, seed=21)
+    a = bppo.Trainer(cfg, init_seed=6)
+    monkeypatch.setenv("BPPO_NO_FUSED_PACK", "1")
+    b = bppo.Trainer(cfg, init_seed=6)
+    try:
+        for _ in range(2):
+            monkeypatch.delenv("BPPO_NO_FUSED_PACK", raising=False)
+            ma = a.train_update()
+            monkeypatch.setenv("BPPO_NO_FUSED_PACK", "1")
+            mb = b.train_update()
+            for k, v in ma.items():
+                assert bits(np.float32(v)) == bits(np.float32(mb[k])) or (np.isnan(v) and np.isnan(mb[k])), k
+        assert bits(a.model.get_params()).tolist() == bits(b.model.get_params()).tolist()
+    finally:
+        a.close()
+        b.close()
