@@ -70,14 +70,14 @@ def test_allreduce_callback_and_sharding_gloo():
     assert shard(bppo.make_config("cartpole"), 0, 1, 64) == (42, 0)
 
 
-def _gpu_worker(rank, world, port, q, updates):
+def _gpu_worker(rank, world, port, q, updates, pipelined=False):
     dist = _init(rank, world, port)
     try:
         cfg = bppo.make_config("cartpole", num_envs=256, num_steps=32)
         # identical shards on purpose: rank=0 seeding for both processes
         tr = bppo.Trainer(cfg, device=0, init_seed=3)
         tr.ctx.set_allreduce(make_allreduce(dist, mode="host_staged"), world)
-        ms = [tr.train_update() for _ in range(updates)]
+        ms = tr.train_updates(updates)[0] if pipelined else [tr.train_update() for _ in range(updates)]
         q.put((rank, tr.model.get_params(), ms[-1]["policy_loss"]))
         tr.close()
     finally:
@@ -85,7 +85,8 @@ def _gpu_worker(rank, world, port, q, updates):
 
 
 @pytest.mark.gpu
-def test_two_ranks_identical_shards_match_single_rank():
+@pytest.mark.parametrize("pipelined", [False, True])
+def test_two_ranks_identical_shards_match_single_rank(pipelined):
     updates = 3
     cfg = bppo.make_config("cartpole", num_envs=256, num_steps=32)
     solo = bppo.Trainer(cfg, device=0, init_seed=3)
@@ -95,7 +96,7 @@ def test_two_ranks_identical_shards_match_single_rank():
     world, port = 2, _port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_gpu_worker, args=(r, world, port, q, updates)) for r in range(world)]
+    procs = [ctx.Process(target=_gpu_worker, args=(r, world, port, q, updates, pipelined)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=300) for _ in range(world))
@@ -108,7 +109,8 @@ def test_two_ranks_identical_shards_match_single_rank():
 
 
 @pytest.mark.gpu
-def test_stream_ordered_allreduce_matches_single_rank():
+@pytest.mark.parametrize("pipelined", [False, True])
+def test_stream_ordered_allreduce_matches_single_rank(pipelined):
     """bppo_set_allreduce_async: the callback only ENQUEUES its reduction on the
     context's stream (staging copies + a torch op on an ExternalStream), with no
     host wait per minibatch.  An emulated 2-rank SUM of identical shards (x2,
@@ -126,8 +128,11 @@ def test_stream_ordered_allreduce_matches_single_rank():
     tr = bppo.Trainer(cfg, device=0, init_seed=3)
     fn = make_allreduce(None, mode="device_async", stream=tr.ctx.stream, reduce=lambda t: t.mul_(2.0))
     tr.ctx.set_allreduce(fn, 2, stream_ordered=True)
-    for _ in range(updates):
-        tr.train_update()
+    if pipelined:        # bench.py's form: bppo_train_steps, rollouts enqueued behind updates
+        tr.train_updates(updates)
+    else:
+        for _ in range(updates):
+            tr.train_update()
     p = tr.model.get_params()
     tr.close()
     assert np.array_equal(p, p_solo)
