@@ -361,9 +361,10 @@ def main():
     gae_roof = {"bound": "hbm", "achieved": round(gae_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(gae_gbs / HBM_PEAK_GBS, 4), "traffic": g_tr, "traffic_unit": "B/launch",
                 "traffic_source": g_src, "kernel": "k_gae_1p_seg", "launch_ms": round(gae_ms, 4),
-                "measured": "isolated launches at the workload shape after the timed region (HIP events on "
-                            "the launch stream); in the update loop the kernel also writes the advantage/return "
-                            "pair of each packed update row and shares the GPU with the side-stream "
+                "measured": "achieved: isolated launches at the workload shape after the timed region (HIP "
+                            "events on the launch stream); in the update loop the kernel also writes the "
+                            "advantage/return pair of each packed update row (8 B/row, in traffic, which is "
+                            "PMC of the in-loop launches) and shares the GPU with the side-stream "
                             "Fisher-Yates passes",
                 "launch_ms_in_loop": round(gae_loop_ms, 4),
                 "algorithmic": f"{N * T} x {GAE_BYTES_PER_ELEM} B"}
