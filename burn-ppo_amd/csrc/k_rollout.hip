@@ -265,6 +265,8 @@ __global__ void __launch_bounds__(512, 2) k_cartpole_rollout_mfma(RolloutArgs a,
 #pragma unroll 1
     for (int t = 0; t < a.T; t++) {
         const size_t row = (size_t)t * N + e;
+        // this step's Gumbel pair, loaded before the MLP so its HBM latency hides under it
+        const float2 gz = mine ? *reinterpret_cast<const float2 *>(gum + row * 2) : make_float2(0.0f, 0.0f);
         float x4 = 0.0f;
         if (h == 0) {
             float x[5] = {0, 0, 0, 0, 0};
@@ -345,8 +347,8 @@ __global__ void __launch_bounds__(512, 2) k_cartpole_rollout_mfma(RolloutArgs a,
             lg[0] = __fadd_rn(l0, S.bp[0]);
             lg[1] = __fadd_rn(l1, S.bp[1]);
             const float v = __fadd_rn(vv, S.bv[0]);
-            const float n0 = __fadd_rn(lg[0], gum[row * 2]);
-            const float n1 = __fadd_rn(lg[1], gum[row * 2 + 1]);
+            const float n0 = __fadd_rn(lg[0], gz.x);
+            const float n1 = __fadd_rn(lg[1], gz.y);
             const int act = n1 > n0 ? 1 : 0;               // argmax, first maximum
             const float lp = log_prob_row<2>(lg, act);
             bad |= !isfinite(lp);
