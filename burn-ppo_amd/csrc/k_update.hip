@@ -728,6 +728,36 @@ __global__ void k_slab_reduce(const double *part, int width, float *grad) {
     }
     grad[p] = (float)s;
 }
+// both passes in one launch, same association (bit-identical grad): a block owns 64
+// columns; its four waves take row groups g = q, q + 4, ... and leave the group sums
+// in LDS, then wave 0 adds the 32 groups in order.  One dependent launch fewer per
+// minibatch, and eight loads per thread in flight instead of a 32-row grid pass
+__global__ void __launch_bounds__(256) k_slab_reduce1(const float *__restrict__ slab, int rows, int width,
+                                                      float *__restrict__ grad) {
+    __shared__ double part[SLAB_GROUPS][64];
+    const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+    const int p = blockIdx.x * 64 + lane;
+    const bool live = p < width, is_max = p == width - NUM_M + M_VEMAX;
+    const int per = (rows + SLAB_GROUPS - 1) / SLAB_GROUPS;
+    if (live) {
+        for (int g = q; g < SLAB_GROUPS; g += 4) {
+            const int w0 = g * per, w1 = min(rows, w0 + per);
+            double s = is_max ? -INFINITY : 0.0;
+#pragma unroll 8
+            for (int w = w0; w < w1; w++) {
+                const double v = slab[(size_t)w * width + p];
+                s = is_max ? fmax(s, v) : s + v;
+            }
+            part[g][lane] = s;
+        }
+    }
+    __syncthreads();
+    if (q == 0 && live) {
+        double s = is_max ? -INFINITY : 0.0;
+        for (int g = 0; g < SLAB_GROUPS; g++) s = is_max ? fmax(s, part[g][lane]) : s + part[g][lane];
+        grad[p] = (float)s;
+    }
+}
 
 // per-tensor norm clip + Adam (burn-optim 0.20 restated).  Each tensor is cut
 // into ADAM_CHUNK-element blocks: pass 1 writes every block's sum of squares,
@@ -1123,10 +1153,16 @@ bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_
 #undef L
     BPPO_HIP(c, hipGetLastError());
     const int width = (int)c->net.n_params + NUM_M;
-    hipLaunchKernelGGL(k_slab_reduce_groups, dim3((width + 255) / 256, SLAB_GROUPS), dim3(256), 0, c->stream,
-                       c->d_slab, c->slab_used, width, c->d_slab_part);
-    hipLaunchKernelGGL(k_slab_reduce, dim3((width + 255) / 256), dim3(256), 0, c->stream, c->d_slab_part,
-                       width, c->d_grad);
+    static const bool two_pass = getenv("BPPO_SLAB_TWO_PASS") && atoi(getenv("BPPO_SLAB_TWO_PASS"));
+    if (two_pass) {
+        hipLaunchKernelGGL(k_slab_reduce_groups, dim3((width + 255) / 256, SLAB_GROUPS), dim3(256), 0, c->stream,
+                           c->d_slab, c->slab_used, width, c->d_slab_part);
+        hipLaunchKernelGGL(k_slab_reduce, dim3((width + 255) / 256), dim3(256), 0, c->stream, c->d_slab_part,
+                           width, c->d_grad);
+    } else {
+        hipLaunchKernelGGL(k_slab_reduce1, dim3((width + 63) / 64), dim3(256), 0, c->stream, c->d_slab,
+                           c->slab_used, width, c->d_grad);
+    }
     BPPO_HIP(c, hipGetLastError());
     return BPPO_OK;
 }
