@@ -729,10 +729,12 @@ __global__ void k_slab_reduce(const double *part, int width, float *grad) {
     grad[p] = (float)s;
 }
 // both passes in one launch, same association (bit-identical grad): a block owns 64
-// columns; its four waves take row groups g = q, q + 4, ... and leave the group sums
-// in LDS, then wave 0 adds the 32 groups in order.  One dependent launch fewer per
-// minibatch, and eight loads per thread in flight instead of a 32-row grid pass
-__global__ void __launch_bounds__(256) k_slab_reduce1(const float *__restrict__ slab, int rows, int width,
+// columns; its 16 waves take row groups g = q, q + 16 and leave the group sums in
+// LDS, then wave 0 adds the 32 groups in order.  One dependent launch fewer per
+// minibatch; 16 waves per block keep loads in flight while the side-stream
+// Fisher-Yates passes load HBM
+constexpr int SLAB1_WAVES = 16;
+__global__ void __launch_bounds__(64 * SLAB1_WAVES) k_slab_reduce1(const float *__restrict__ slab, int rows, int width,
                                                       float *__restrict__ grad) {
     __shared__ double part[SLAB_GROUPS][64];
     const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
@@ -740,7 +742,7 @@ __global__ void __launch_bounds__(256) k_slab_reduce1(const float *__restrict__ 
     const bool live = p < width, is_max = p == width - NUM_M + M_VEMAX;
     const int per = (rows + SLAB_GROUPS - 1) / SLAB_GROUPS;
     if (live) {
-        for (int g = q; g < SLAB_GROUPS; g += 4) {
+        for (int g = q; g < SLAB_GROUPS; g += SLAB1_WAVES) {
             const int w0 = g * per, w1 = min(rows, w0 + per);
             double s = is_max ? -INFINITY : 0.0;
 #pragma unroll 8
@@ -825,17 +827,24 @@ __global__ void __launch_bounds__(256) k_adam(AdamArgs a) {
 
 // every tensor within one ADAM_CHUNK (the CfgB net): one block per tensor does
 // pass 1 (the same per-thread sums and tree as k_adam_norm) and pass 2 (the
-// update) back to back; block 0 also copies the minibatch's metric row
-__global__ void __launch_bounds__(256) k_adam1(AdamArgs a, const float *gtail, const float *mb_stats, int nm,
-                                               float *metric_dst) {
+// update) back to back; block 0 also copies the minibatch's metric row.  The norm
+// uses the first 256 threads exactly as k_adam_norm does (bit-identical); the
+// elementwise update spreads over all ADAM1_THREADS (4 elements per thread for a
+// 64x64 weight instead of 16 in a serial chain)
+constexpr int ADAM1_THREADS = 1024;
+__global__ void __launch_bounds__(ADAM1_THREADS) k_adam1(AdamArgs a, const float *gtail, const float *mb_stats,
+                                                         int nm, float *metric_dst) {
     __shared__ double red[256];
     const AdamTensor T = a.t[blockIdx.x];
-    double ss = 0.0;
-    for (int i = threadIdx.x; i < T.len; i += blockDim.x) {
-        const float gi = a.grad[T.off + i] * a.inv_world;
-        ss += (double)gi * (double)gi;
+    if (threadIdx.x < 256) {
+        double ss = 0.0;
+#pragma unroll 4
+        for (int i = threadIdx.x; i < T.len; i += 256) {
+            const float gi = a.grad[T.off + i] * a.inv_world;
+            ss += (double)gi * (double)gi;
+        }
+        red[threadIdx.x] = ss;
     }
-    red[threadIdx.x] = ss;
     __syncthreads();
     for (int st = 128; st > 0; st >>= 1) {
         if (threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
@@ -846,7 +855,8 @@ __global__ void __launch_bounds__(256) k_adam1(AdamArgs a, const float *gtail, c
     const float scale = norm > a.max_norm ? __fdiv_rn(a.max_norm, norm) : 1.0f;
     const bool clip = norm > a.max_norm;
     const float b1 = 0.9f, b2 = 0.999f, f1 = 1.0f - 0.9f, f2 = 1.0f - 0.999f;
-    for (int i = threadIdx.x; i < T.len; i += blockDim.x) {
+#pragma unroll 2
+    for (int i = threadIdx.x; i < T.len; i += ADAM1_THREADS) {
         float gi = a.grad[T.off + i] * a.inv_world;
         if (clip) gi = __fmul_rn(gi, scale);
         const float m1 = __fadd_rn(__fmul_rn(a.m1[T.off + i], b1), __fmul_rn(gi, f1));
@@ -1160,7 +1170,7 @@ bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_
         hipLaunchKernelGGL(k_slab_reduce, dim3((width + 255) / 256), dim3(256), 0, c->stream, c->d_slab_part,
                            width, c->d_grad);
     } else {
-        hipLaunchKernelGGL(k_slab_reduce1, dim3((width + 63) / 64), dim3(256), 0, c->stream, c->d_slab,
+        hipLaunchKernelGGL(k_slab_reduce1, dim3((width + 63) / 64), dim3(64 * SLAB1_WAVES), 0, c->stream, c->d_slab,
                            c->slab_used, width, c->d_grad);
     }
     BPPO_HIP(c, hipGetLastError());
@@ -1195,8 +1205,8 @@ bppo_status launch_adam(bppo_ctx *c, float lr, const float *c1, const float *c2,
     for (int t = 0; t < a.nt; t++) { a.blk0[t] = nb; nb += (a.t[t].len + ADAM_CHUNK - 1) / ADAM_CHUNK; }
     a.blk0[a.nt] = nb;
     if (nb == a.nt && metric_dst) {       // one chunk per tensor: fused
-        hipLaunchKernelGGL(k_adam1, dim3(nb), dim3(256), 0, c->stream, a, c->d_grad + c->net.n_params, c->d_mb_cur, nm,
-                           metric_dst);
+        hipLaunchKernelGGL(k_adam1, dim3(nb), dim3(ADAM1_THREADS), 0, c->stream, a, c->d_grad + c->net.n_params,
+                           c->d_mb_cur, nm, metric_dst);
         BPPO_HIP(c, hipGetLastError());
         return BPPO_OK;
     }
