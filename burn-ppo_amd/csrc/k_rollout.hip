@@ -528,14 +528,26 @@ __global__ void k_obs_norm_final(int D, int nblk, const double *bp, double *on) 
     const int d = threadIdx.x;
     if (d >= D) return;
     double n = 0.0, mean = 0.0, m2 = 0.0;
-    for (int b = 0; b < nblk; b++) {
-        const double *o = bp + ((size_t)b * OBS_MAX_D + d) * 3;
-        const double nb = o[0];
-        if (nb <= 0) continue;
-        const double nn = n + nb, delta = o[1] - mean;
-        mean = n > 0 ? mean + delta * (nb / nn) : o[1];
-        m2 += o[2] + (n > 0 ? delta * delta * (n * nb / nn) : 0.0);
-        n = nn;
+    // the block partials of 16 blocks are loaded before the in-order merge consumes
+    // them: one load round trip per 16 blocks instead of one per block
+    constexpr int U = 16;
+    for (int b0 = 0; b0 < nblk; b0 += U) {
+        double pn[U], pm[U], p2[U];
+#pragma unroll
+        for (int k = 0; k < U; k++) {
+            const double *o = bp + ((size_t)min(b0 + k, nblk - 1) * OBS_MAX_D + d) * 3;
+            pn[k] = o[0]; pm[k] = o[1]; p2[k] = o[2];
+        }
+#pragma unroll
+        for (int k = 0; k < U; k++) {
+            if (b0 + k >= nblk) break;
+            const double nb = pn[k];
+            if (nb <= 0) continue;
+            const double nn = n + nb, delta = pm[k] - mean;
+            mean = n > 0 ? mean + delta * (nb / nn) : pm[k];
+            m2 += p2[k] + (n > 0 ? delta * delta * (n * nb / nn) : 0.0);
+            n = nn;
+        }
     }
     // old stats (count on[2D]) merged with the batch
     const double na = on[2 * D], nn = na + n, delta = mean - on[d];
