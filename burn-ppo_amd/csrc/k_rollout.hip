@@ -208,17 +208,31 @@ __global__ void __launch_bounds__(256) k_cartpole_rollout(RolloutArgs a) {
 
 // Gumbel noise of a whole rollout, ahead of it (utils.rs:10-31): g[i] for the
 // word at base + i, i < count (row-major [t][env][action], one word per draw).
-// One ChaCha12 block per thread; the rollout reads two floats per env-step.
-__global__ void k_gumbel_words(Key8 key, uint64_t stream, uint64_t base, uint64_t count, float *g) {
-    const uint64_t b = (base >> 4) + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    const uint64_t w0 = b * 16;
-    if (w0 >= base + count) return;
-    uint32_t blk[16];
-    chacha12_block(key, b, stream, blk);
+// One ChaCha12 block per thread; the rollout reads two floats per env-step.  The
+// block's 16 x 256 noise floats are transposed through LDS so every store
+// instruction writes 256 consecutive floats (a thread's own 16 words would be
+// a 64-B-strided store per word)
+constexpr int GUM_THREADS = 256;
+__global__ void __launch_bounds__(GUM_THREADS) k_gumbel_words(Key8 key, uint64_t stream, uint64_t base,
+                                                              uint64_t count, float *__restrict__ g) {
+    __shared__ float tile[16 * GUM_THREADS + GUM_THREADS / 2];
+    const uint64_t blk0 = (base >> 4) + blockIdx.x * (uint64_t)GUM_THREADS;
+    const uint64_t b = blk0 + threadIdx.x, wb = blk0 * 16;
+    if (b * 16 < base + count) {
+        uint32_t blk[16];
+        chacha12_block(key, b, stream, blk);
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const int k = threadIdx.x * 16 + j;
+            tile[k + (k >> 5)] = gumbel_from_word(blk[j]);   // one pad float per 32: conflict-free writes
+        }
+    }
+    __syncthreads();
 #pragma unroll
     for (int j = 0; j < 16; j++) {
-        const uint64_t w = w0 + j;
-        if (w >= base && w < base + count) g[w - base] = gumbel_from_word(blk[j]);
+        const int k = j * GUM_THREADS + threadIdx.x;
+        const uint64_t w = wb + k;
+        if (w >= base && w < base + count) g[w - base] = tile[k + (k >> 5)];
     }
 }
 
