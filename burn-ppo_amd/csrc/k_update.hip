@@ -992,7 +992,7 @@ __global__ void __launch_bounds__(256) k_adv_epoch_final(const double *part, int
 template <int MB>
 __global__ void __launch_bounds__(256) k_adv_stream(const float *__restrict__ adv, const uint32_t *__restrict__ inv,
                                                     EpochSplit sp, uint32_t C, double *part) {
-    constexpr int U = 4;
+    constexpr int U = 16;   // rows per thread per load round (a thread still adds its rows in order)
     __shared__ double red[4][MB][4];
     double s[MB], q[MB];
     float mn[MB], mx[MB];
