@@ -165,24 +165,23 @@ class CheckpointMetadata:
 
     @classmethod
     def for_config(cls, cfg, step, avg_return, recent_returns=(), best_avg_return=None, forked_from=None):
-        """the metadata run_training writes (main.rs:451-476, 1245-1271)"""
+        """the metadata run_training writes (main.rs:451-476, 1245-1271): every CNN field,
+        split_networks and the critic sizes straight from the config whatever the network
+        type, obs_shape = E::OBSERVATION_SHAPE (Connect Four only, connect_four.rs:217),
+        privileged_obs_dim for CTDE only (main.rs:215-230)"""
         from .host import ENV_DIMS
         obs, act, P, priv = ENV_DIMS[cfg["env"]]
         ctde = cfg["network_type"] == "ctde"
-        cnn = {}
-        if cfg["network_type"] == "cnn":
-            from .host import conv_channels
-            cnn = dict(num_conv_layers=cfg["num_conv_layers"], conv_channels=conv_channels(cfg),
-                       kernel_size=cfg["kernel_size"], cnn_fc_hidden_size=cfg["cnn_fc_hidden_size"],
-                       cnn_num_fc_layers=cfg["cnn_num_fc_layers"], obs_shape=(6, 7, 2))
-        return cls(**cnn, step=int(step), avg_return=float(avg_return), rng_seed=int(cfg["seed"]),
+        return cls(step=int(step), avg_return=float(avg_return), rng_seed=int(cfg["seed"]),
                    best_avg_return=best_avg_return, recent_returns=[float(x) for x in recent_returns],
                    forked_from=forked_from, obs_dim=obs, action_count=act, num_players=P,
                    hidden_size=cfg["hidden_size"], num_hidden=cfg["num_hidden"], activation=cfg["activation"],
-                   network_type=cfg["network_type"], privileged_obs_dim=priv if ctde else None,
-                   critic_hidden_size=cfg["critic_hidden_size"] if ctde else cfg.get("critic_hidden_size"),
-                   critic_num_hidden=cfg["critic_num_hidden"] if ctde else cfg.get("critic_num_hidden"),
-                   env_name=cfg["env"])
+                   split_networks=bool(cfg.get("split_networks", False)), network_type=cfg["network_type"],
+                   num_conv_layers=int(cfg["num_conv_layers"]), conv_channels=[int(c) for c in cfg["conv_channels"]],
+                   kernel_size=int(cfg["kernel_size"]), cnn_fc_hidden_size=int(cfg["cnn_fc_hidden_size"]),
+                   cnn_num_fc_layers=int(cfg["cnn_num_fc_layers"]), privileged_obs_dim=priv if ctde else None,
+                   critic_hidden_size=cfg.get("critic_hidden_size"), critic_num_hidden=cfg.get("critic_num_hidden"),
+                   obs_shape=(6, 7, 2) if cfg["env"] == "connect_four" else None, env_name=cfg["env"])
 
 
 def load_metadata(ckpt_dir):
@@ -323,6 +322,18 @@ def save_optimizer(ctx, path_dir):
         f.write(msgpack.packb(rec, use_bin_type=True))
 
 
+def model_param_ids(path_dir):
+    """ParamIds of model.mpk in record order (weight, bias of each layer), or None.
+    Burn keys the optimizer record by the model's ParamIds, which are random per
+    model, so an optimizer.mpk is read with the ids of the model saved beside it."""
+    p = os.path.join(path_dir, "model.mpk")
+    if not os.path.exists(p):
+        return None
+    with open(p, "rb") as f:
+        item = msgpack.unpackb(f.read(), raw=False)["item"]
+    return [lin[k]["id"] for lin in _linears_in_order(item) for k in ("weight", "bias")]
+
+
 def load_optimizer(ctx, path_dir):
     """checkpoint.rs:311-335: no optimizer.mpk -> optimizer unchanged (False)"""
     p = os.path.join(path_dir, "optimizer.mpk")
@@ -330,18 +341,28 @@ def load_optimizer(ctx, path_dir):
         return False
     with open(p, "rb") as f:
         rec = msgpack.unpackb(f.read(), raw=False)
-    _, ids = optimizer_record(ctx.cfg, np.zeros(ctx.n_params, np.float32), np.zeros(ctx.n_params, np.float32),
-                              np.zeros(len(layer_shapes(ctx.cfg)[0]) * 2, np.int32))
+    ids = model_param_ids(path_dir)
+    if ids is None:   # no model record beside it: the ids this module writes
+        _, ids = optimizer_record(ctx.cfg, np.zeros(ctx.n_params, np.float32), np.zeros(ctx.n_params, np.float32),
+                                  np.zeros(len(layer_shapes(ctx.cfg)[0]) * 2, np.int32))
+    m1, m2, steps = optimizer_arrays(rec, ids)
+    ctx._chk(L.lib().bppo_optimizer_set(ctx.h, m1.ctypes.data, m2.ctypes.data, steps.ctypes.data, ctx.n_params))
+    return True
+
+
+def optimizer_arrays(rec, ids):
+    """flat (moment_1, moment_2, per-tensor step) of an optimizer record, tensors in
+    the order of `ids` (the model's ParamIds in record order)"""
     m1, m2, steps = [], [], []
     for pid in ids:
+        if pid not in rec["item"]:
+            raise KeyError(f"optimizer record has no state for parameter id {pid}")
         st = rec["item"][pid]["momentum"]
         m1.append(np.frombuffer(st["moment_1"]["bytes"], np.float32))
         m2.append(np.frombuffer(st["moment_2"]["bytes"], np.float32))
         steps.append(st["time"])
-    m1 = np.ascontiguousarray(np.concatenate(m1)); m2 = np.ascontiguousarray(np.concatenate(m2))
-    steps = np.asarray(steps, np.int32)
-    ctx._chk(L.lib().bppo_optimizer_set(ctx.h, m1.ctypes.data, m2.ctypes.data, steps.ctypes.data, ctx.n_params))
-    return True
+    return (np.ascontiguousarray(np.concatenate(m1)), np.ascontiguousarray(np.concatenate(m2)),
+            np.asarray(steps, np.int32))
 
 
 # ------------------------------------------------------------ normalizers ---
@@ -472,9 +493,13 @@ class CheckpointManager:
         return load_model(os.path.join(ckpt_dir, "model.mpk")), meta
 
 
-def save_training_checkpoint(manager, ctx, params, metadata, update_best=True):
+def save_training_checkpoint(manager, ctx, params, metadata, update_best=None):
     """one periodic checkpoint of run_training (main.rs:1276-1310): model +
-    metadata, optimizer, normalizers (when on), then the RNG draw"""
+    metadata, optimizer, normalizers (when on), then the RNG draw.  update_best
+    defaults to use_avg_return_for_best = (num_players == 1) (main.rs:659, 1276):
+    multi-player runs move 'best' through pool evaluation, not avg_return."""
+    if update_best is None:
+        update_best = ctx.num_players == 1
     path = manager.save(ctx, params, metadata, update_best)
     save_optimizer(ctx, path)
     if ctx.cfg["normalize_obs"]:

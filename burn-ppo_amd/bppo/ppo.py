@@ -386,6 +386,7 @@ class Trainer:
         self.global_step += self.ctx.T * self.ctx.N                           # main.rs:988
         metrics["episodes"] = info.episodes
         metrics["mean_return"] = info.mean_return
+        metrics["rng_word_pos"] = info.rng_word_pos
         return metrics
 
     def train_updates(self, n, phase_keys=()):
@@ -406,6 +407,7 @@ class Trainer:
             d = _metrics_dict(ms[k])
             d["episodes"] = infos[k].episodes
             d["mean_return"] = infos[k].mean_return
+            d["rng_word_pos"] = infos[k].rng_word_pos
             out.append(d)
         self.global_step += n * self.ctx.T * self.ctx.N
         return out, {k: float(sums[i]) for i, k in enumerate(phase_keys)}

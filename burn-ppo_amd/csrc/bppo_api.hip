@@ -729,7 +729,10 @@ static bppo_status collect_finish(bppo_ctx *c, bppo_rollout_info *info, int slot
 
 extern "C" bppo_status bppo_collect_rollouts(bppo_ctx *c, bppo_rollout_info *info) {
     if (!c) return BPPO_ERR_ARG;
-    TRY(collect_enqueue(c, info != nullptr));
+    // a rollout bppo_train_steps enqueued ahead (it returned an error before using it)
+    // IS the next rollout: the RNG and the envs have moved past it already
+    if (c->prefetched) c->prefetched = false;
+    else TRY(collect_enqueue(c, info != nullptr));
     BPPO_HIP(c, sync_stream(c));
     return collect_finish(c, info, c->coll_slot);
 }
@@ -1048,7 +1051,8 @@ extern "C" bppo_status bppo_train_step(bppo_ctx *c, double lr, double ent_coef, 
     if (!c) return BPPO_ERR_ARG;
     const auto t0 = std::chrono::steady_clock::now();
     c->sync_wait_ms = 0.0;
-    TRY(collect_enqueue(c, info != nullptr));
+    if (c->prefetched) c->prefetched = false;     // enqueued ahead by bppo_train_steps (see bppo_collect_rollouts)
+    else TRY(collect_enqueue(c, info != nullptr));
     TRY(gae_enqueue(c));
     const bppo_status us = bppo_ppo_update(c, lr, ent_coef, m);   // drains the stream at its end
     if (us == BPPO_OK) { if (!c->wide) tm_read(c, TM_BOOT); tm_read(c, TM_GAE); }
@@ -1084,10 +1088,15 @@ extern "C" bppo_status bppo_train_steps(bppo_ctx *c, int32_t n, const double *lr
         c->prefetch_env_step = global_step0 + (uint64_t)(k + 1) * TN;
         const bppo_status us = bppo_ppo_update(c, lr[k], ent_coef[k], ms ? &ms[k] : nullptr);
         c->prefetch_next = false;
-        if (us != BPPO_OK) { c->prefetched = false; return us; }
+        // on an error the next iteration's rollout may already be enqueued (ppo_update
+        // enqueues it before its wait): drain the stream so nothing is pending on
+        // return; that rollout stays the context's next one (prefetched), which
+        // bppo_collect_rollouts / bppo_train_step(s) then use instead of drawing another
+        if (us != BPPO_OK) { (void)sync_stream(c); c->collected = c->prefetched ? 1 : 0; return us; }
         if (!c->wide) tm_read(c, TM_BOOT);
         tm_read(c, TM_GAE);
-        TRY(collect_finish(c, infos ? &infos[k] : nullptr, slot));
+        const bppo_status cs = collect_finish(c, infos ? &infos[k] : nullptr, slot);
+        if (cs != BPPO_OK) { (void)sync_stream(c); c->collected = c->prefetched ? 1 : 0; return cs; }
         c->last_host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() -
                           c->sync_wait_ms;
         c->last_sync_ms = c->sync_wait_ms;

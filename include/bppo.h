@@ -181,7 +181,10 @@ bppo_status bppo_train_step(bppo_ctx *ctx, double lr, double ent_coef, bppo_roll
 /* n bppo_train_step iterations (main.rs:684-988 loop body, lr[k] / ent_coef[k], env step
  * global_step0 + k*T*N), software-pipelined: each iteration's rollout is enqueued behind the
  * previous update before the host waits for that update, so the GPU does not idle between
- * iterations.  Same results as n bppo_train_step calls; nothing pending on return.
+ * iterations.  Same results as n bppo_train_step calls; the stream is drained on return.
+ * After an error status the next iteration's rollout may already have run (the RNG and
+ * the envs are past it): it stays the context's next rollout, which bppo_collect_rollouts,
+ * bppo_train_step and bppo_train_steps use instead of drawing another one.
  * infos / ms: n entries each (may be NULL); phase_keys (bppo_last_kernel_ms names, nkeys of
  * them): per-key sums over the n iterations into phase_sums */
 bppo_status bppo_train_steps(bppo_ctx *ctx, int32_t n, const double *lr, const double *ent_coef,

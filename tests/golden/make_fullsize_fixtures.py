@@ -1,0 +1,163 @@
+"""Full-size oracle fixtures for the paths the benches run.
+
+TEST INFRASTRUCTURE ONLY: runs the CPU oracle (oracle/, a restatement of the
+reference path) in the build container at the configs' real sizes -- sizes the
+oracle cannot finish inside a GPU test -- and writes compact fixtures that
+tests/test_gpu_fullsize.py compares the device against:
+
+  full_cfgB.npz  CartPole N=65,536 T=128 (configs/cartpole.toml at CfgB): rollout,
+                 both normalizers, bootstrap, GAE and one ppo_update (4 epochs x 4
+                 minibatches of 2,097,152 rows)            ppo.rs:213-500, 1069-1124, 1661-2112
+  full_cfgC.npz  Connect Four N=16,384 T=64 (configs/connect_four.toml, pool off):
+                 rollout, bootstrap, multi-player GAE, one update (6 x 4, target_kl 0.02)
+  full_cfgD.npz  Liar's Dice CTDE N=32,768 T=128 (configs/liars_dice_ctde.toml, pool
+                 off): the same (4 x 8, target_kl 0.025)
+
+What a fixture holds (data only, no reference source):
+  * sha256 of every buffer the device must reproduce bit for bit (actions, dones,
+    observations, values, log-probs; players, masks, privileged obs, all_rewards
+    and advantages/returns of the multi-player paths) and the main-RNG word
+    positions after the rollout and after the update;
+  * for buffers held to a tolerance (CartPole rewards after the return
+    normalizer's scan, and the advantages/returns that follow from them): a fixed
+    strided sample and the f64 sum of every step row;
+  * the 19 UpdateMetrics, num_updates / epochs_run, the exact f64 explained
+    variance of the buffers, the sha256 of the last epoch's permutation;
+  * the parameters after the update (all of them for CfgB; a fixed random sample
+    plus per-tensor f64 sums of |p - p0| for the larger nets);
+  * the sha256 of the initial parameters (bppo.orthogonal_init(cfg, init_seed)), so
+    a test fails loudly if the box regenerates different weights.
+
+Regenerate (about 10-40 min on 8 cores, mostly CfgD's update):
+    python tests/golden/make_fullsize_fixtures.py [cfgB cfgC cfgD]
+"""
+import ctypes as C
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "burn-ppo_amd"))
+
+import oracle_ffi as O  # noqa: E402
+from bppo.host import layer_shapes, make_config, orthogonal_init  # noqa: E402
+from parity_util import METRICS, ev_f64, oracle_train_cfg  # noqa: E402
+
+# the benched configurations (BASELINE.json configs[1..3]); init_seed picks the weights
+CASES = {
+    "cfgB": dict(preset="cartpole", num_envs=65536, num_steps=128, init_seed=1),
+    "cfgC": dict(preset="connect_four", num_envs=16384, num_steps=64, init_seed=5),
+    "cfgD": dict(preset="liars_dice_ctde", num_envs=32768, num_steps=128, init_seed=5),
+}
+SAMPLE_STRIDE = 251          # tolerance buffers: every 251st element (from element 7)
+PARAM_SAMPLE = 16384         # larger nets: this many parameters at fixed random indices
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).view(np.uint8)).hexdigest()
+
+
+def case_config(name):
+    c = dict(CASES[name])
+    preset, init_seed = c.pop("preset"), c.pop("init_seed")
+    return make_config(preset, **c), init_seed
+
+
+def exact_buffers(cfg):
+    """(name, dtype) of the buffers the device reproduces bit for bit"""
+    out = [("actions", np.int32), ("dones", np.float32), ("obs", np.float32), ("values", np.float32),
+           ("log_probs", np.float32)]
+    if cfg["env"] != "cartpole":
+        out += [("players", np.int32), ("masks", np.float32), ("rewards", np.float32),
+                ("all_rewards", np.float32), ("advantages", np.float32), ("returns", np.float32)]
+        if cfg["network_type"] == "ctde":
+            out.append(("priv", np.float32))
+    return out
+
+
+def tolerance_buffers(cfg):
+    return ("rewards", "advantages", "returns") if cfg["env"] == "cartpole" else ()
+
+
+def strided(a):
+    return np.ascontiguousarray(a[7::SAMPLE_STRIDE])
+
+
+def param_sample_idx(n):
+    if n <= 20000:
+        return np.arange(n, dtype=np.int64)
+    return np.sort(np.random.default_rng(12345).choice(n, PARAM_SAMPLE, replace=False)).astype(np.int64)
+
+
+def tensor_abs_delta(cfg, p, p0):
+    """per Burn record tensor (W then b of each Linear): f64 sum of |p - p0|"""
+    out, o = [], 0
+    for (i, n), _ in zip(*layer_shapes(cfg)):
+        for sz in (i * n, n):
+            out.append(np.abs(p[o:o + sz].astype(np.float64) - p0[o:o + sz].astype(np.float64)).sum())
+            o += sz
+    assert o == p.size
+    return np.array(out)
+
+
+def last_perm(seed, start, B, epochs):
+    r = O.new_rng(seed)
+    r.word_pos = start
+    p = np.arange(B, dtype=np.uint32)
+    for _ in range(epochs):
+        p = np.arange(B, dtype=np.uint32)
+        O.lib().or_shuffle_u32(C.byref(r), p, B)
+    return p
+
+
+def make(name):
+    cfg, init_seed = case_config(name)
+    params = orthogonal_init(cfg, seed=init_seed)
+    t0 = time.time()
+    ot = O.Trainer(oracle_train_cfg(cfg), params)
+    N, T = cfg["num_envs"], cfg["num_steps"]
+    episodes = ot.collect()
+    rng_rollout = ot.rng_pos()
+    t1 = time.time()
+    ot.gae()
+    out = dict(config=json.dumps({k: v for k, v in CASES[name].items()}), init_sha=sha(params),
+               episodes=episodes, rng_rollout=rng_rollout, sample_stride=SAMPLE_STRIDE)
+    for b, dt in exact_buffers(cfg):
+        out["sha_" + b] = sha(ot.buffer(b, dt))
+    for b in tolerance_buffers(cfg):
+        x = ot.buffer(b)
+        out["sample_" + b] = strided(x)
+        out["rowsum_" + b] = x.reshape(T, N).astype(np.float64).sum(axis=1)
+    if cfg["env"] == "cartpole":
+        m, v, c = ot.obs_norm_state(5)
+        out.update(obs_norm_mean=m, obs_norm_m2=v, obs_norm_count=c)
+        mvc, rets = ot.ret_norm_state(returns=True)
+        out.update(ret_norm=mvc, sha_ret_norm_returns=sha(rets))
+    else:
+        out["sha_last_v_pp"] = sha(ot.buffer("last_v_pp"))
+    vals, rets = ot.buffer("values"), ot.buffer("returns")
+    out["ev_exact"] = ev_f64(vals, rets)
+    start = ot.rng_pos()
+    om = ot.update()
+    t2 = time.time()
+    out["metrics"] = np.array([om[k] for k in METRICS], np.float32)
+    out["num_updates"], out["epochs_run"] = om["num_updates"], om["epochs_run"]
+    out["rng_update"] = ot.rng_pos()
+    out["sha_perm"] = sha(last_perm(cfg["seed"], start, N * T, om["epochs_run"]))
+    p = ot.params()
+    idx = param_sample_idx(p.size)
+    out.update(param_idx=idx, param_sample=p[idx], tensor_abs_delta=tensor_abs_delta(cfg, p, params))
+    ot.close()
+    print(f"{name}: rollout {t1 - t0:.1f} s, gae+update {t2 - t1:.1f} s, epochs_run {om['epochs_run']}", flush=True)
+    np.savez(os.path.join(HERE, f"full_{name}.npz"), **out)
+
+
+if __name__ == "__main__":
+    for n in (sys.argv[1:] or list(CASES)):
+        make(n)

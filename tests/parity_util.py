@@ -124,6 +124,23 @@ def bits(a):
     return np.ascontiguousarray(a, np.float32).view(np.uint32)
 
 
+def oracle_train_cfg(cfg, threads=0):
+    """the oracle's TrainCfg for a bppo config dict (CartPole, Connect Four, Liar's Dice; MLP / CTDE)"""
+    kind = {"cartpole": O.ENV_CARTPOLE, "connect_four": O.ENV_CONNECT_FOUR, "liars_dice": O.ENV_LIARS_DICE}[cfg["env"]]
+    nr = cfg["normalize_returns"]
+    if nr is None:
+        nr = cfg["env"] == "cartpole"                      # main.rs:243: single-player only
+    return O.train_cfg(env_kind=kind, num_envs=cfg["num_envs"], num_steps=cfg["num_steps"], seed=cfg["seed"],
+                       hidden=cfg["hidden_size"], num_hidden=cfg["num_hidden"], ctde=cfg["network_type"] == "ctde",
+                       relu=cfg["activation"] == "relu", critic_hidden=cfg["critic_hidden_size"] or 0,
+                       critic_num_hidden=cfg["critic_num_hidden"] or 0, normalize_obs=bool(cfg["normalize_obs"]),
+                       normalize_returns=bool(nr), gamma=cfg["gamma"], gae_lambda=cfg["gae_lambda"],
+                       lr=bppo.schedule_get(cfg["learning_rate"], 0), ent_coef=bppo.schedule_get(cfg["entropy_coef"], 0),
+                       reward_shaping=cfg["reward_shaping_coef"], num_epochs=cfg["num_epochs"],
+                       num_minibatches=cfg["num_minibatches"], clip=cfg["clip_epsilon"], value_coef=cfg["value_coef"],
+                       max_grad_norm=cfg["max_grad_norm"], target_kl=cfg["target_kl"], threads=threads)
+
+
 def cartpole_pair(N, T, preset="cartpole", seed=42, init_seed=1, **kw):
     """Device trainer + oracle trainer of one CartPole config (same params, seeds)."""
     cfg = bppo.make_config(preset, num_envs=N, num_steps=T, seed=seed, **kw)

@@ -88,6 +88,64 @@ def test_optimizer_record_round_trip():
     assert [rec["item"][i]["momentum"]["time"] for i in ids] == list(steps)
 
 
+def test_optimizer_read_with_the_model_record_ids(tmp_path):
+    """Burn keys optimizer.mpk by the model's random ParamIds: a record written
+    with ids unknown to this module loads through the ids of model.mpk beside it."""
+    import msgpack
+    cfg = bppo.make_config("cartpole")
+    p = bppo.orthogonal_init(cfg)
+    rec = K.model_record(cfg, p)
+    rng = np.random.default_rng(9)
+    fresh = [str(int(x)) for x in rng.integers(1, 2**48, 8)]
+    lins = K._linears_in_order(rec["item"])
+    for t, (lin, k) in enumerate((lin, k) for lin in lins for k in ("weight", "bias")):
+        lin[k]["id"] = fresh[t]
+    (tmp_path / "model.mpk").write_bytes(msgpack.packb(rec, use_bin_type=True))
+    assert K.model_param_ids(str(tmp_path)) == fresh
+    n = p.size
+    m1, m2 = rng.normal(size=n).astype(np.float32), rng.random(n).astype(np.float32)
+    steps = np.arange(8, dtype=np.int32) + 5
+    orec, hashed = K.optimizer_record(cfg, m1, m2, steps)
+    orec["item"] = {fresh[i]: orec["item"][h] for i, h in enumerate(hashed)}    # as the reference writes it
+    a1, a2, st = K.optimizer_arrays(orec, K.model_param_ids(str(tmp_path)))
+    assert np.array_equal(a1, m1) and np.array_equal(a2, m2) and list(st) == list(steps)
+    with pytest.raises(KeyError):
+        K.optimizer_arrays(orec, hashed)
+    assert K.model_param_ids(str(tmp_path / "missing")) is None
+
+
+def _ref_meta(obs_dim, action_count, num_players, env_name, **kw):
+    """what main.rs:451-476 writes: every config field as given (config.rs defaults
+    num_conv_layers 2, conv_channels [8, 8], kernel_size 3, cnn_fc_hidden_size 32,
+    cnn_num_fc_layers 1), obs_shape = E::OBSERVATION_SHAPE"""
+    d = dict(step=0, avg_return=0.0, rng_seed=42, best_avg_return=None, recent_returns=[], forked_from=None,
+             obs_dim=obs_dim, action_count=action_count, num_players=num_players, hidden_size=64, num_hidden=2,
+             activation="relu", split_networks=False, network_type="mlp", num_conv_layers=2, conv_channels=[8, 8],
+             kernel_size=3, cnn_fc_hidden_size=32, cnn_num_fc_layers=1, privileged_obs_dim=None,
+             critic_hidden_size=None, critic_num_hidden=None, obs_shape=None, env_name=env_name,
+             exploitability_vs_pool=None)
+    d.update(kw)
+    return d
+
+
+@pytest.mark.parametrize("preset,over,ref", [
+    ("cartpole", {}, _ref_meta(5, 2, 1, "cartpole")),
+    ("connect_four", {}, _ref_meta(86, 7, 2, "connect_four", hidden_size=512, obs_shape=[6, 7, 2])),
+    ("connect_four", {"network_type": "cnn", "conv_channels": [64]},
+     _ref_meta(86, 7, 2, "connect_four", hidden_size=512, network_type="cnn", conv_channels=[64], obs_shape=[6, 7, 2])),
+    ("liars_dice_ctde", {}, _ref_meta(270, 49, 4, "liars_dice", hidden_size=256, network_type="ctde",
+                                      privileged_obs_dim=120, critic_hidden_size=512, critic_num_hidden=3)),
+    ("liars_dice_ctde", {"network_type": "mlp", "split_networks": True},
+     _ref_meta(270, 49, 4, "liars_dice", hidden_size=256, split_networks=True, critic_hidden_size=512,
+               critic_num_hidden=3)),
+])
+def test_for_config_writes_the_reference_metadata(preset, over, ref):
+    """ADVICE r2: CheckpointMetadata::for_config vs the fields main.rs:451-476 writes"""
+    cfg = bppo.make_config(preset, **over)
+    got = json.loads(K.CheckpointMetadata.for_config(cfg, 0, 0.0).to_json())
+    assert got == ref
+
+
 class _FakeCtx:
     def __init__(self, cfg):
         self.cfg = cfg
