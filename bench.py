@@ -61,6 +61,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-learning", action="store_true", help="skip the steps-to-475 runs")
     p.add_argument("--selftest", action="store_true", help="N>1 harness check with gloo and no GPU work")
+    p.add_argument("--host-cpus", type=int, default=0,
+                   help="pin each rank to K host CPUs (its share of an 8-rank node) and size the shuffle "
+                        "engine's threads for K (BPPO_HOST_THREADS); default: affinity/quota / ranks per node")
     return p.parse_args()
 
 
@@ -261,6 +264,13 @@ def main():
         sys.exit(2)
     if args.selftest:
         return selftest_main(args, world, rank)
+    if args.host_cpus > 0:
+        # before any GPU call: the runtime's and the engine's threads inherit the mask
+        cpus = sorted(os.sched_getaffinity(0))
+        k = args.host_cpus
+        mine = cpus[local * k:(local + 1) * k] if len(cpus) >= (local + 1) * k else cpus[:k]
+        os.sched_setaffinity(0, mine)
+        os.environ["BPPO_HOST_THREADS"] = str(len(mine))
     os.environ.setdefault("BPPO_HOST_THREADS", str(host_cpu_budget(local_world)))
 
     import torch
@@ -381,6 +391,7 @@ def main():
                       "w_gt_1_semantics": ("per-rank obs/return normalizers and per-rank minibatch advantage "
                                            "stats (SURVEY 8e); parity is defined at N=1" if world > 1 else None),
                       "host_cpus_per_rank": int(os.environ["BPPO_HOST_THREADS"]),
+                      "host_cpu_affinity": len(os.sched_getaffinity(0)),
                       "host_cpu_quota": cgroup_cpu_quota()},
            # this process's CPU time per update over the timed region (all threads:
            # shuffle engine walkers and word producers, the driver thread, HIP runtime)

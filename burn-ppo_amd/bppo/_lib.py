@@ -40,7 +40,7 @@ class Config(C.Structure):
                 ("rng_stream", C.c_uint64),
                 ("cnn", C.c_int32), ("num_conv_layers", C.c_int32), ("conv_channels", C.c_int32 * 4),
                 ("kernel_size", C.c_int32), ("cnn_fc_hidden_size", C.c_int32), ("cnn_num_fc_layers", C.c_int32),
-                ("normalize_values", C.c_int32), ("player_count", C.c_int32)]
+                ("normalize_values", C.c_int32), ("player_count", C.c_int32), ("split_networks", C.c_int32)]
 
 
 class Episode(C.Structure):

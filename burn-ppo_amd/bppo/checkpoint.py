@@ -250,10 +250,12 @@ def model_record(cfg, params):
                                            for i, (W, b) in enumerate(lin[nh + 1:nh + 1 + nc])],
                          "value_head": _linear(*lin[nh + 1 + nc], "value_head")}}
     else:
+        nc = nh if cfg.get("split_networks") else 0                     # mlp.rs:47-62 critic_layers
         item = {"Mlp": {"layers": [_linear(W, b, f"layers.{i}") for i, (W, b) in enumerate(lin[:nh])],
-                        "critic_layers": [],
-                        "policy_head": _linear(*lin[nh], "policy_head"),
-                        "value_head": _linear(*lin[nh + 1], "value_head")}}
+                        "critic_layers": [_linear(W, b, f"critic_layers.{i}")
+                                          for i, (W, b) in enumerate(lin[nh:nh + nc])],
+                        "policy_head": _linear(*lin[nh + nc], "policy_head"),
+                        "value_head": _linear(*lin[nh + nc + 1], "value_head")}}
     return {"metadata": BURN_METADATA, "item": item}
 
 
@@ -265,10 +267,8 @@ def _linears_in_order(item):
         return rec["conv_layers"] + rec["fc_layers"] + [rec["policy_head"], rec["value_head"]]
     if kind == "Ctde":
         seq = rec["actor_layers"] + [rec["policy_head"]] + rec["critic_layers"] + [rec["value_head"]]
-    elif kind == "Mlp":
-        if rec["critic_layers"]:
-            raise ValueError("split_networks MLP checkpoints are not supported by the device path")
-        seq = rec["layers"] + [rec["policy_head"], rec["value_head"]]
+    elif kind == "Mlp":      # record order: layers, critic_layers (split_networks), policy, value
+        seq = rec["layers"] + rec["critic_layers"] + [rec["policy_head"], rec["value_head"]]
     else:
         raise ValueError(f"network type {kind} is not supported by the device path")
     return seq

@@ -34,11 +34,13 @@ static double tsc_per_ms() {
 
 NetLayout make_layout(const bppo_config &c, int obs_dim, int priv_dim, int act_dim) {
     NetLayout L;
-    L.ctde = c.ctde; L.relu = c.relu;
-    size_t off = 0;
+    // split_networks (mlp.rs:100-130): a second trunk of num_hidden x hidden_size on obs,
+    // i.e. the CTDE structure with no privileged input (ctde.rs ignores the flag)
+    const bool split = c.split_networks && !c.ctde && !c.cnn;
+    L.ctde = c.ctde || split; L.relu = c.relu;
     auto add = [&](int in, int out) {
         int i = L.n_layers++;
-        L.in[i] = in; L.out[i] = out; L.w[i] = off; off += (size_t)in * out; L.b[i] = off; off += out;
+        L.in[i] = in; L.out[i] = out;
         return i;
     };
     int in = obs_dim;
@@ -65,13 +67,27 @@ NetLayout make_layout(const bppo_config &c, int obs_dim, int priv_dim, int act_d
         L.n_actor_hidden = c.num_hidden;
     }
     L.policy = add(in, act_dim);
-    if (c.ctde) {
-        int cin = priv_dim + obs_dim;
+    if (L.ctde) {
+        int cin = split ? obs_dim : priv_dim + obs_dim;
+        const int nc = split ? c.num_hidden : c.critic_num_hidden, wc = split ? c.hidden_size : c.critic_hidden_size;
         L.critic_first = L.n_layers;
-        for (int l = 0; l < c.critic_num_hidden; l++) { add(cin, c.critic_hidden_size); cin = c.critic_hidden_size; }
+        for (int l = 0; l < nc; l++) { add(cin, wc); cin = wc; }
         L.value = add(cin, 1);
     } else {
         L.value = add(in, 1);
+    }
+    // offsets in Burn record order: the layer order above, except split_networks'
+    // record (mlp.rs:47-62) puts the critic layers before the policy head
+    int order[16], no = 0;
+    for (int l = 0; l < L.n_layers; l++)
+        if (!split || l < L.n_actor_hidden || (l >= L.critic_first && l < L.value)) order[no++] = l;
+    if (split) { order[no++] = L.policy; order[no++] = L.value; }
+    size_t off = 0;
+    for (int r = 0; r < L.n_layers; r++) {
+        const int l = order[r];
+        L.rec[l] = r;
+        L.w[l] = off; off += (size_t)L.in[l] * L.out[l];
+        L.b[l] = off; off += L.out[l];
     }
     L.n_params = off;
     return L;
@@ -160,6 +176,11 @@ static hipError_t sync_stream(bppo_ctx *c) {
     return e;
 }
 
+static bool cartpole_fused_net(const bppo_config &c) {
+    return !c.split_networks && !c.cnn && !c.ctde && (c.hidden_size == 16 || c.hidden_size == 32 || c.hidden_size == 64) &&
+           (c.num_hidden == 1 || c.num_hidden == 2);
+}
+
 static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *stream) {
     c->cfg = *cfg;
     c->dev = dev;
@@ -190,8 +211,22 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
         c->Pa = cfg->player_count ? cfg->player_count : 4;          // PlayerCountMode::default (config.rs:667-671)
         if (c->Pa < 2 || c->Pa > 6) { c->err = "Skull supports 2-6 players"; return BPPO_ERR_ARG; }   // skull.rs:159-162
     }
-    c->wide = cfg->env_kind != BPPO_ENV_CARTPOLE;
+    // the fused CartPole kernels (k_rollout.hip, k_update.hip) cover the shared-trunk
+    // MLPs of {16, 32, 64} x {1, 2}; every other CartPole net (mlp.rs:76-132 accepts any
+    // width and depth; split_networks) runs on the GEMM engine path like the other envs
+    c->wide = cfg->env_kind != BPPO_ENV_CARTPOLE || !cartpole_fused_net(*cfg);
     if (c->wide && !cfg->ctde) c->G = 0;
+    if (cfg->split_networks && cfg->cnn) {
+        c->err = "split_networks with network_type = \"cnn\" is not on the device path";
+        return BPPO_ERR_UNSUPPORTED;
+    }
+    // num_hidden = 0 would feed obs into heads of hidden_size inputs (mlp.rs:121-125), a
+    // shape panic in the reference unless obs_dim == hidden_size
+    if (!cfg->cnn && (cfg->hidden_size < 1 || cfg->num_hidden < 1 ||
+                      (cfg->ctde && (cfg->critic_hidden_size < 1 || cfg->critic_num_hidden < 1)))) {
+        c->err = "hidden_size / num_hidden (critic_*) must be positive";
+        return BPPO_ERR_ARG;
+    }
     if (!(cfg->reward_shaping_coef >= 0.0)) { c->err = "reward_shaping_coef must be >= 0"; return BPPO_ERR_ARG; }   // config.rs:1514-1519
     if (cfg->cnn) {
         // cnn.rs:73-74 "CNN requires OBSERVATION_SHAPE" (only Connect Four has one)
@@ -447,7 +482,10 @@ extern "C" bppo_status bppo_optimizer_get(bppo_ctx *c, float *m1, float *m2, int
     if (m1) BPPO_HIP(c, hipMemcpyAsync(m1, c->d_m1, n * 4, hipMemcpyDeviceToHost, c->stream));
     if (m2) BPPO_HIP(c, hipMemcpyAsync(m2, c->d_m2, n * 4, hipMemcpyDeviceToHost, c->stream));
     BPPO_HIP(c, sync_stream(c));
-    if (steps) for (size_t t = 0; t < c->adam_t.size(); t++) steps[t] = c->adam_t[t];
+    // adam_t is indexed by layer (2 l, 2 l + 1); steps[] is in record order
+    if (steps)
+        for (int l = 0; l < c->net.n_layers; l++)
+            for (int k = 0; k < 2; k++) steps[2 * c->net.rec[l] + k] = c->adam_t[2 * l + k];
     return BPPO_OK;
 }
 
@@ -460,7 +498,8 @@ extern "C" bppo_status bppo_optimizer_set(bppo_ctx *c, const float *m1, const fl
     BPPO_HIP(c, hipMemcpyAsync(c->d_m1, m1, n * 4, hipMemcpyHostToDevice, c->stream));
     BPPO_HIP(c, hipMemcpyAsync(c->d_m2, m2, n * 4, hipMemcpyHostToDevice, c->stream));
     BPPO_HIP(c, sync_stream(c));
-    for (size_t t = 0; t < c->adam_t.size(); t++) c->adam_t[t] = steps[t];
+    for (int l = 0; l < c->net.n_layers; l++)
+        for (int k = 0; k < 2; k++) c->adam_t[2 * l + k] = steps[2 * c->net.rec[l] + k];
     return BPPO_OK;
 }
 
@@ -1025,7 +1064,8 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
         const double mres = ev4[2] / Bn, vres = ev4[3] / Bn - mres * mres;
         // ppo.rs:1268-1294 (fewer than 2 rows or Var(R) < 1e-8 -> 0)
         m->explained_variance = (B < 2 || vr < 1e-8) ? 0.0f : (float)(1.0 - vres / vr);
-        if (c->wide) { m->avg_valid_actions = tav / n; m->entropy_valid_pct = tevp / n; }
+        // ppo.rs:1549-1565: only envs with action masks report these (None -> 0)
+        if (c->cfg.env_kind != BPPO_ENV_CARTPOLE) { m->avg_valid_actions = tav / n; m->entropy_valid_pct = tevp / n; }
         m->num_updates = nup; m->epochs_run = epochs_run;
         // PopArt metrics (ppo.rs:2061-2068): None -> NaN
         m->value_norm_target_mean = m->value_norm_target_std = NAN;

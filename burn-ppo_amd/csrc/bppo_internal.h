@@ -23,8 +23,9 @@ struct NetLayout {
     size_t w[16], b[16];
     int n_actor_hidden = 0;       // hidden layers of the actor / shared backbone
     int policy = 0, value = 0;    // layer indices of the heads
-    int critic_first = -1;        // CTDE critic hidden layers [critic_first, value)
-    int ctde = 0, relu = 1;
+    int critic_first = -1;        // critic hidden layers [critic_first, value) (CTDE, split_networks)
+    int ctde = 0, relu = 1;       // ctde: two trunks (CTDE, or split_networks with the critic on obs)
+    int rec[16];                  // Burn record position of layer l (split_networks: actor, critic, heads)
     size_t n_params = 0;
     // CNN (network/cnn.rs): layers [0, n_conv) are the conv layers (in = Cin k k,
     // out = Cout; weight [Cout][Cin][k][k] then bias in Burn record order), then the

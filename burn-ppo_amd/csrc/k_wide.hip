@@ -1,5 +1,7 @@
-// k_wide.hip — device kernels of the multi-player ("wide") path: Connect Four
-// and Liar's Dice VecEnv (env.rs:281-487) with action masks, masked Gumbel-max
+// k_wide.hip — device kernels of the GEMM-engine ("wide") path: Connect Four,
+// Liar's Dice and Skull VecEnv (env.rs:281-487) with action masks -- and CartPole
+// for the nets the fused CartPole kernels do not cover (other widths / depths,
+// split_networks) -- masked Gumbel-max
 // sampling (utils.rs:10-31, 96-135), the masked clipped-surrogate loss and its
 // logit/value gradients (ppo.rs:1385-1592), and the small helpers around the
 // GEMM engine (row gather, head packing, metric reduction).
@@ -11,6 +13,38 @@ namespace bppo {
 
 // ------------------------------------------------------------ env traits --
 template <int ENV> struct EnvT;
+// CartPole (cartpole.rs:50-106, 272-301): no action mask (all actions valid, so the
+// -inf / (mask - 1) * 1e9 masking adds exactly 0), one player
+template <> struct EnvT<BPPO_ENV_CARTPOLE> {
+    using S = CartPoleState;
+    static constexpr int D = 5, A = 2, P = 1, G = 0;
+    // CartPole::new(seed) resets (cartpole.rs:104), VecEnv::new resets again (env.rs:289-293)
+    __device__ static void reset_new(S &s, const Key8 &k, uint64_t &pos, int) {
+        WordCursor c; c.init(k, 0, 0);
+        cartpole_reset(s, c);
+        cartpole_reset(s, c);
+        pos = c.pos;
+    }
+    __device__ static void reset(S &s, const Key8 &k, uint64_t &pos) {
+        WordCursor c; c.init(k, 0, pos);
+        cartpole_reset(s, c);
+        pos = c.pos;
+    }
+    __device__ static int player(const S &) { return 0; }
+    __device__ static void step(S &s, int a, float, float r[BPPO_MAX_PLAYERS], int &done, int &, const Key8 &,
+                                uint64_t &) {
+        float rw = 0.0f;
+        done = cartpole_step(s, a, rw) ? 1 : 0;
+        r[0] = rw;
+    }
+    __device__ static void obs(const S &s, float *row) {
+        float o[5];
+        cartpole_obs(s, o);
+        for (int i = 0; i < 5; i++) row[i] = o[i];
+    }
+    __device__ static void priv(const S &, float *) {}
+    __device__ static void mask(const S &, uint8_t *m) { m[0] = 1; m[1] = 1; }
+};
 template <> struct EnvT<BPPO_ENV_CONNECT_FOUR> {
     using S = C4State;
     static constexpr int D = C4_OBS, A = C4_ACT, P = 2, G = 0;
@@ -362,6 +396,8 @@ __global__ void __launch_bounds__(64) k_wide_metric_reduce(const double *part, i
     do {                                                                                    \
         if ((kind) == BPPO_ENV_CONNECT_FOUR)                                                \
             hipLaunchKernelGGL(KERNEL<BPPO_ENV_CONNECT_FOUR>, grid, block, 0, st, __VA_ARGS__); \
+        else if ((kind) == BPPO_ENV_CARTPOLE)                                               \
+            hipLaunchKernelGGL(KERNEL<BPPO_ENV_CARTPOLE>, grid, block, 0, st, __VA_ARGS__);    \
         else if ((kind) == BPPO_ENV_SKULL)                                                  \
             hipLaunchKernelGGL(KERNEL<BPPO_ENV_SKULL>, grid, block, 0, st, __VA_ARGS__);       \
         else                                                                                \
@@ -380,6 +416,8 @@ hipError_t wide_env_observe(int kind, int with_priv, hipStream_t st, int N, cons
     const dim3 grid((N + 63) / 64), block(64);
     if (kind == BPPO_ENV_CONNECT_FOUR)
         hipLaunchKernelGGL((k_wide_observe<BPPO_ENV_CONNECT_FOUR, false>), grid, block, 0, st, N, state, xc, mask, players);
+    else if (kind == BPPO_ENV_CARTPOLE)
+        hipLaunchKernelGGL((k_wide_observe<BPPO_ENV_CARTPOLE, false>), grid, block, 0, st, N, state, xc, mask, players);
     else if (kind == BPPO_ENV_SKULL && with_priv)
         hipLaunchKernelGGL((k_wide_observe<BPPO_ENV_SKULL, true>), grid, block, 0, st, N, state, xc, mask, players);
     else if (kind == BPPO_ENV_SKULL)
@@ -398,7 +436,7 @@ hipError_t wide_env_step(int kind, hipStream_t st, const WideStepArgs &a) {
 
 hipError_t wide_sample(int A, hipStream_t st, const SampleArgs &g) {
     const dim3 grid((g.N + 127) / 128), block(128);
-    if (A == 2) hipLaunchKernelGGL(k_sample_masked<2>, grid, block, 0, st, g);   // CartPole (bppo_debug_sample)
+    if (A == 2) hipLaunchKernelGGL(k_sample_masked<2>, grid, block, 0, st, g);   // CartPole (GEMM path, bppo_debug_sample)
     else if (A == C4_ACT) hipLaunchKernelGGL(k_sample_masked<C4_ACT>, grid, block, 0, st, g);
     else if (A == LD_ACT) hipLaunchKernelGGL(k_sample_masked<LD_ACT>, grid, block, 0, st, g);
     else if (A == SK_ACT) hipLaunchKernelGGL(k_sample_masked<SK_ACT>, grid, block, 0, st, g);
@@ -427,7 +465,8 @@ hipError_t wide_pack_heads(hipStream_t st, const float *params, int K, int A, si
 }
 
 hipError_t wide_loss(int A, hipStream_t st, const LossArgs &g, int blocks, float *metrics_out) {
-    if (A == C4_ACT) hipLaunchKernelGGL(k_wide_loss<C4_ACT>, dim3(blocks), dim3(256), 0, st, g);
+    if (A == 2) hipLaunchKernelGGL(k_wide_loss<2>, dim3(blocks), dim3(256), 0, st, g);   // CartPole
+    else if (A == C4_ACT) hipLaunchKernelGGL(k_wide_loss<C4_ACT>, dim3(blocks), dim3(256), 0, st, g);
     else if (A == LD_ACT) hipLaunchKernelGGL(k_wide_loss<LD_ACT>, dim3(blocks), dim3(256), 0, st, g);
     else if (A == SK_ACT) hipLaunchKernelGGL(k_wide_loss<SK_ACT>, dim3(blocks), dim3(256), 0, st, g);
     else return hipErrorInvalidValue;
@@ -441,6 +480,7 @@ hipError_t wide_loss(int A, hipStream_t st, const LossArgs &g, int blocks, float
 
 namespace bppo {
 size_t wide_state_bytes(int kind) {
-    return kind == BPPO_ENV_CONNECT_FOUR ? sizeof(C4State) : kind == BPPO_ENV_SKULL ? sizeof(SKState) : sizeof(LDState);
+    return kind == BPPO_ENV_CONNECT_FOUR ? sizeof(C4State) : kind == BPPO_ENV_SKULL ? sizeof(SKState)
+         : kind == BPPO_ENV_CARTPOLE ? sizeof(CartPoleState) : sizeof(LDState);
 }
 }  // namespace bppo

@@ -71,6 +71,11 @@ typedef struct {
     /* Skull: player_count (config.rs:767 PlayerCountMode, get_fixed_count, main.rs:1998);
      * 2..6, 0 = the default 4.  The player axis of the buffers stays NUM_PLAYERS = 6. */
     int32_t player_count;
+    /* split_networks (config.rs:860, default false; mlp.rs:40-130, 139-206): separate actor
+     * and critic trunks of num_hidden x hidden_size on the observation (MLP; CNN: not on the
+     * device path, BPPO_ERR_UNSUPPORTED).  Flat parameters in Burn record order: layers
+     * (actor), critic_layers, policy_head, value_head.  CTDE nets ignore it (ctde.rs). */
+    int32_t split_networks;
 } bppo_config;
 
 typedef struct {

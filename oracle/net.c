@@ -27,37 +27,43 @@ void or_set_mlp_parallel(int on) { g_mlp_parallel = on; }
 
 typedef struct { int in, out; size_t w, b; } layer_t;
 
-/* parameter layout = Burn record order (mlp.rs:47-62, ctde.rs:26-44) */
+/* two trunks: CTDE, or split_networks (the critic on obs alone) */
+static int two_trunk(const or_net_desc *d) { return d->ctde || d->split; }
+
+/* parameter layout = Burn record order (mlp.rs:47-62, ctde.rs:26-44).  Layer
+ * indices: actor hidden, policy, [critic hidden, value | value]; the offsets follow
+ * the record, which for split_networks holds critic_layers before the heads. */
 static int net_layers(const or_net_desc *d, layer_t *L, int *n_actor_total) {
-    int n = 0; size_t off = 0; int in = d->obs_dim;
+    int n = 0; int in = d->obs_dim;
     if (d->cnn) {
         /* conv layers first (Burn record order: weight [Cout][Cin][k][k], bias),
          * as layers with in = Cin k k, out = Cout; the FC stack then reads the
          * flattened conv output + the extra features */
         int cin = d->C;
         for (int i = 0; i < d->n_conv; i++) {
-            L[n].in = cin * d->ksize * d->ksize; L[n].out = d->conv_ch[i]; L[n].w = off;
-            off += (size_t)L[n].in * L[n].out; L[n].b = off; off += L[n].out; cin = d->conv_ch[i]; n++;
+            L[n].in = cin * d->ksize * d->ksize; L[n].out = d->conv_ch[i]; cin = d->conv_ch[i]; n++;
         }
         in = d->H * d->W * cin + (d->obs_dim - d->H * d->W * d->C);
     }
-    for (int i = 0; i < d->n_actor; i++) {
-        L[n].in = in; L[n].out = d->actor_width; L[n].w = off; off += (size_t)in * L[n].out;
-        L[n].b = off; off += L[n].out; in = d->actor_width; n++;
-    }
-    /* policy head */
-    L[n].in = in; L[n].out = d->act_dim; L[n].w = off; off += (size_t)in * d->act_dim;
-    L[n].b = off; off += d->act_dim; n++;
+    for (int i = 0; i < d->n_actor; i++) { L[n].in = in; L[n].out = d->actor_width; in = d->actor_width; n++; }
+    L[n].in = in; L[n].out = d->act_dim; n++;                 /* policy head */
     *n_actor_total = n;
-    if (d->ctde) {
+    if (two_trunk(d)) {
         int cin = d->priv_dim + d->obs_dim;
-        for (int i = 0; i < d->n_critic; i++) {
-            L[n].in = cin; L[n].out = d->critic_width; L[n].w = off; off += (size_t)cin * L[n].out;
-            L[n].b = off; off += L[n].out; cin = d->critic_width; n++;
-        }
-        L[n].in = cin; L[n].out = 1; L[n].w = off; off += cin; L[n].b = off; off += 1; n++;
+        for (int i = 0; i < d->n_critic; i++) { L[n].in = cin; L[n].out = d->critic_width; cin = d->critic_width; n++; }
+        L[n].in = cin; L[n].out = 1; n++;
     } else {
-        L[n].in = in; L[n].out = 1; L[n].w = off; off += in; L[n].b = off; off += 1; n++;
+        L[n].in = in; L[n].out = 1; n++;
+    }
+    int order[32], no = 0;
+    for (int i = 0; i < n; i++)
+        if (!d->split || (i != *n_actor_total - 1 && i != n - 1)) order[no++] = i;
+    if (d->split) { order[no++] = *n_actor_total - 1; order[no++] = n - 1; }
+    size_t off = 0;
+    for (int r = 0; r < n; r++) {
+        layer_t *l = &L[order[r]];
+        l->w = off; off += (size_t)l->in * l->out;
+        l->b = off; off += l->out;
     }
     return n;
 }
@@ -71,7 +77,7 @@ void or_net_value_head(const or_net_desc *d, size_t *w, size_t *b, int *in) {
 size_t or_net_num_params(const or_net_desc *d) {
     layer_t L[32]; int na;
     int n = net_layers(d, L, &na);
-    return L[n - 1].b + 1;
+    return L[n - 1].b + 1;       /* the value head is last in every record */
 }
 
 static float act_fwd(float y, int relu) { return relu ? (y > 0.0f ? y : 0.0f) : tanhf(y); }
@@ -187,13 +193,13 @@ static void forward_cached(const or_net_desc *d, const float *p, const float *ob
         x = y;
     }
     or_linear(x, p + L[na - 1].w, p + L[na - 1].b, B, L[na - 1].in, L[na - 1].out, -1, logits);
-    if (!d->ctde) {
+    if (!two_trunk(d)) {
         or_linear(x, p + L[na].w, p + L[na].b, B, L[na].in, 1, -1, values);
     } else {
         int cin = d->priv_dim + d->obs_dim;
         float *xc = malloc(sizeof(float) * B * cin);
         for (size_t r = 0; r < B; r++) {
-            memcpy(xc + r * cin, priv + r * d->priv_dim, sizeof(float) * d->priv_dim);
+            if (d->priv_dim) memcpy(xc + r * cin, priv + r * d->priv_dim, sizeof(float) * d->priv_dim);
             memcpy(xc + r * cin + d->priv_dim, obs + r * d->obs_dim, sizeof(float) * d->obs_dim);
         }
         if (A) A->buf[31] = xc;
@@ -517,7 +523,7 @@ void or_minibatch_loss_grad(const or_net_desc *d, const float *p, size_t mb, con
             linear_bwd(xin, NULL, dcur, p + L[li].w, mb, L[li].in, L[li].out, -1, g + L[li].w,
                        g + L[li].b, dx);
             float *dh = dx;
-            if (!d->ctde) {
+            if (!two_trunk(d)) {
                 /* shared backbone: add value head gradient */
                 int vi = na;
                 float *dx2 = malloc(sizeof(float) * mb * L[vi].in);
@@ -538,7 +544,7 @@ void or_minibatch_loss_grad(const or_net_desc *d, const float *p, size_t mb, con
             if (d->cnn) cnn_bwd(d, L, p, obs, mb, &acts, dh, g);   /* dh = dL/dF */
             free(dh);
         }
-        if (d->ctde) {
+        if (two_trunk(d)) {
             int vi = n - 1;
             const float *xin = vi > na ? acts.buf[vi - 1] : acts.buf[31];
             float *dh = vi > na ? malloc(sizeof(float) * mb * L[vi].in) : NULL;

@@ -227,6 +227,10 @@ typedef struct {
      * n_conv conv layers of conv_ch[l] channels, odd kernel ksize, stride 1, same
      * padding, relu; then n_actor FC layers of actor_width, then the heads */
     int cnn, n_conv, conv_ch[4], ksize, H, W, C;
+    /* split_networks (mlp.rs:40-130, 139-206): a critic trunk of n_critic x critic_width on
+     * obs alone (priv_dim 0), structured like CTDE; record order: actor hidden, critic
+     * hidden, policy head, value head */
+    int split;
 } or_net_desc;
 size_t or_net_num_params(const or_net_desc *d);
 void or_net_value_head(const or_net_desc *d, size_t *w, size_t *b, int *in);   /* value head W offset, b offset, in */
@@ -327,6 +331,7 @@ typedef struct {
     int cnn, num_conv, conv_ch[4], ksize;   /* network_type = "cnn" (Connect Four) */
     int normalize_values;    /* PopArt (config.rs:827-832) */
     int player_count;        /* Skull (config.rs:767), 0 = 4 */
+    int split_networks;      /* config.rs:860 (MLP nets) */
 } or_train_cfg;
 or_trainer *or_trainer_new(const or_train_cfg *c, const float *init_params);
 void or_trainer_free(or_trainer *t);

@@ -91,7 +91,7 @@ class NetDesc(C.Structure):
                 ("relu", C.c_int), ("n_actor", C.c_int), ("actor_width", C.c_int),
                 ("n_critic", C.c_int), ("critic_width", C.c_int), ("n_params", C.c_size_t),
                 ("cnn", C.c_int), ("n_conv", C.c_int), ("conv_ch", C.c_int * 4), ("ksize", C.c_int),
-                ("H", C.c_int), ("W", C.c_int), ("C", C.c_int)]
+                ("H", C.c_int), ("W", C.c_int), ("C", C.c_int), ("split", C.c_int)]
 
 
 class PpoCfg(C.Structure):
@@ -110,7 +110,7 @@ class TrainCfg(C.Structure):
                 ("lr", C.c_double), ("ent_coef", C.c_double), ("reward_shaping", C.c_double),
                 ("ppo", PpoCfg), ("seed", C.c_uint64), ("threads", C.c_int),
                 ("cnn", C.c_int), ("num_conv", C.c_int), ("conv_ch", C.c_int * 4), ("ksize", C.c_int),
-                ("normalize_values", C.c_int), ("player_count", C.c_int)]
+                ("normalize_values", C.c_int), ("player_count", C.c_int), ("split_networks", C.c_int)]
 
 
 class UpdateMetrics(C.Structure):
@@ -298,9 +298,11 @@ def new_rng(seed):
     return r
 
 
-def mlp_desc(obs_dim, act_dim, hidden, num_hidden, relu=True):
+def mlp_desc(obs_dim, act_dim, hidden, num_hidden, relu=True, split=False):
+    """shared trunk, or split_networks (a critic trunk of the same shape on obs)"""
     d = NetDesc(ctde=0, obs_dim=obs_dim, priv_dim=0, act_dim=act_dim, relu=int(relu),
-                n_actor=num_hidden, actor_width=hidden, n_critic=0, critic_width=0)
+                n_actor=num_hidden, actor_width=hidden, n_critic=num_hidden if split else 0,
+                critic_width=hidden if split else 0, split=int(split))
     d.n_params = lib().or_net_num_params(C.byref(d))
     return d
 
@@ -379,7 +381,7 @@ def train_cfg(env_kind=ENV_CARTPOLE, num_envs=8, num_steps=128, hidden=64, num_h
               ctde=False, critic_hidden=0, critic_num_hidden=0, normalize_obs=True,
               normalize_returns=True, return_clip=10.0, gamma=0.99, gae_lambda=0.95, lr=1e-3,
               ent_coef=0.01, reward_shaping=0.0, seed=42, threads=0, cnn=None, normalize_values=False,
-              player_count=0, **ppo):
+              player_count=0, split=False, **ppo):
     """cnn: None, or (conv_channels per layer, kernel_size); hidden / num_hidden are
     then cnn_fc_hidden_size / cnn_num_fc_layers"""
     extra = {}
@@ -387,7 +389,8 @@ def train_cfg(env_kind=ENV_CARTPOLE, num_envs=8, num_steps=128, hidden=64, num_h
         ch, ks = cnn
         extra = dict(cnn=1, num_conv=len(ch), conv_ch=(C.c_int * 4)(*[ch[min(i, len(ch) - 1)] for i in range(4)]),
                      ksize=ks)
-    return TrainCfg(**extra, normalize_values=int(normalize_values), player_count=player_count, env_kind=env_kind, num_envs=num_envs, num_steps=num_steps, hidden=hidden,
+    return TrainCfg(**extra, normalize_values=int(normalize_values), player_count=player_count,
+                    split_networks=int(split), env_kind=env_kind, num_envs=num_envs, num_steps=num_steps, hidden=hidden,
                     num_hidden=num_hidden, relu=int(relu), ctde=int(ctde), critic_hidden=critic_hidden,
                     critic_num_hidden=critic_num_hidden, normalize_obs=int(normalize_obs),
                     normalize_returns=int(normalize_returns), return_clip=return_clip, gamma=gamma,

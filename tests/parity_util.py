@@ -138,7 +138,8 @@ def oracle_train_cfg(cfg, threads=0):
                        lr=bppo.schedule_get(cfg["learning_rate"], 0), ent_coef=bppo.schedule_get(cfg["entropy_coef"], 0),
                        reward_shaping=cfg["reward_shaping_coef"], num_epochs=cfg["num_epochs"],
                        num_minibatches=cfg["num_minibatches"], clip=cfg["clip_epsilon"], value_coef=cfg["value_coef"],
-                       max_grad_norm=cfg["max_grad_norm"], target_kl=cfg["target_kl"], threads=threads)
+                       max_grad_norm=cfg["max_grad_norm"], target_kl=cfg["target_kl"], threads=threads,
+                       split=bool(cfg.get("split_networks")))
 
 
 def cartpole_pair(N, T, preset="cartpole", seed=42, init_seed=1, **kw):

@@ -59,6 +59,7 @@ def test_metadata_required_fields_and_defaults():
 
 @pytest.mark.parametrize("preset,over", [("cartpole", {}), ("connect_four", {}), ("liars_dice_ctde", {}),
                                          ("connect_four", {"network_type": "cnn"}),
+                                         ("cartpole", {"split_networks": True, "hidden_size": 32, "num_hidden": 3}),
                                          ("liars_dice_ctde", {"network_type": "mlp", "hidden_size": 128})])
 def test_model_record_round_trip(tmp_path, preset, over):
     cfg = bppo.make_config(preset, **over)
@@ -73,6 +74,9 @@ def test_model_record_round_trip(tmp_path, preset, over):
     assert kind == {"ctde": "Ctde", "cnn": "Cnn", "mlp": "Mlp"}[cfg["network_type"]]
     lin = body["policy_head"]
     assert set(lin) == {"weight", "bias"} and lin["weight"]["param"]["dtype"] == "F32"
+    if cfg.get("split_networks"):   # mlp.rs:47-62: critic_layers on obs, same widths as the actor's
+        assert [c["weight"]["param"]["shape"] for c in body["critic_layers"]] == \
+            [[5, 32], [32, 32], [32, 32]]
 
 
 def test_optimizer_record_round_trip():

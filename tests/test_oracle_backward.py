@@ -20,6 +20,11 @@ def layer_shapes(desc):
         i = desc.H * desc.W * cin + desc.obs_dim - desc.H * desc.W * desc.C
     for _ in range(desc.n_actor):
         shapes.append((i, desc.actor_width)); i = desc.actor_width
+    if desc.split:   # mlp.rs:47-62 record: layers, critic_layers, policy_head, value_head
+        c = desc.obs_dim
+        for _ in range(desc.n_critic):
+            shapes.append((c, desc.critic_width)); c = desc.critic_width
+        return shapes + [(i, desc.act_dim), (c, 1)]
     shapes.append((i, desc.act_dim))
     if desc.ctde:
         c = desc.priv_dim + desc.obs_dim
@@ -57,6 +62,17 @@ def torch_loss(desc, params, obs, priv, actions, old_logp, adv_n, returns, old_v
             cin = co
         h = torch.cat([sp.reshape(sp.shape[0], -1), x[:, Hh * Ww * Cc:]], 1)
         Ws = Ws[desc.n_conv:]
+    if desc.split:   # mlp.rs:143-185: actor trunk -> policy, critic trunk on obs -> value
+        na, nc = desc.n_actor, desc.n_critic
+        for W, b in Ws[:na]:
+            h = act(h @ W + b)
+        hc = x
+        for W, b in Ws[na:na + nc]:
+            hc = act(hc @ W + b)
+        logits = h @ Ws[na + nc][0] + Ws[na + nc][1]
+        v = (hc @ Ws[-1][0] + Ws[-1][1])[:, 0]
+        return _loss_tail(logits, v, actions, old_logp, adv_n, returns, old_values, masks, clip, vcoef, ent,
+                          clip_value, p)
     for W, b in Ws[:desc.n_actor]:
         h = act(h @ W + b)
     logits = h @ Ws[desc.n_actor][0] + Ws[desc.n_actor][1]
@@ -67,6 +83,11 @@ def torch_loss(desc, params, obs, priv, actions, old_logp, adv_n, returns, old_v
         v = (hc @ Ws[-1][0] + Ws[-1][1])[:, 0]
     else:
         v = (h @ Ws[-1][0] + Ws[-1][1])[:, 0]
+    return _loss_tail(logits, v, actions, old_logp, adv_n, returns, old_values, masks, clip, vcoef, ent,
+                      clip_value, p)
+
+
+def _loss_tail(logits, v, actions, old_logp, adv_n, returns, old_values, masks, clip, vcoef, ent, clip_value, p):
     if masks is not None:
         logits = logits + (torch.tensor(masks, dtype=torch.float64) - 1.0) * 1e9
     ls = torch.log_softmax(logits, 1)
@@ -140,6 +161,15 @@ def test_tanh_activation():
 def test_cnn_connect_four_shape():
     """network/cnn.rs: 2 conv layers (8, 16 channels), 3x3 same, 1 FC layer of 24"""
     run_case(O.cnn_desc(7, [8, 16], 3, 24, 1), mb=33, masks=True, seed=5)
+
+
+def test_split_networks_cartpole_shape():
+    """mlp.rs split_networks: actor and critic trunks of 2 x 32 on obs"""
+    run_case(O.mlp_desc(5, 2, 32, 2, split=True), mb=150, seed=7)
+
+
+def test_split_networks_masked_tanh():
+    run_case(O.mlp_desc(86, 7, 24, 3, relu=False, split=True), mb=70, masks=True, seed=8)
 
 
 def test_cnn_one_conv_tanh_fc_kernel5():
