@@ -45,7 +45,8 @@ METRIC = "env-steps/sec (rollout+GAE+PPO update) at 1/2/4/8 MI355X; steps-to-475
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md: FP32 vector / matrix dense peak
 FLOP_PER_ROW_FWD_BWD = 27_008  # CfgB forward + backward per env-step (per minibatch row)
-GAE_BYTES_PER_ELEM = 20        # r, d, v in; adv, ret out (f32)
+GAE_BYTES_PER_ELEM = 28        # r, d, v in; adv, ret out (f32) = 20 B, plus the
+                               # [advantage, return] pair of the minibatch rows the bench path writes (8 B)
 TRAFFIC_JSON = os.path.join(ROOT, "pmc_traffic.json")   # copy of a scripts/pmc_traffic.sh summary
 CSRC = os.path.join(ROOT, "burn-ppo_amd", "csrc")
 
@@ -60,6 +61,8 @@ def parse():
     p.add_argument("--cpu-envs", type=int, default=8192, help="CPU baseline sample size (envs)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-learning", action="store_true", help="skip the steps-to-475 runs")
+    p.add_argument("--no-gae-isolated", action="store_true",
+                   help="skip the isolated GAE launches (kernel traces of the in-loop launches only)")
     p.add_argument("--selftest", action="store_true", help="N>1 harness check with gloo and no GPU work")
     p.add_argument("--host-cpus", type=int, default=0,
                    help="pin each rank to K host CPUs (its share of an 8-rank node) and size the shuffle "
@@ -165,17 +168,46 @@ def cpu_baseline(args):
     except OSError:
         pass
     return {"value": 2 * n * args.num_steps / dt, "unit": "env-steps/sec", "cores": threads, "kind": "port",
-            "cpu": model,
+            "cpu": model, "cfgA": cpu_baseline_cfgA(),
             "sample": f"CfgB config (cartpole.toml, 2x64 relu, 4x4 PPO) at num_envs={n}, T={args.num_steps}: "
                       f"1 warm-up + 2 timed full updates (rollout+GAE+update) = {2 * n * args.num_steps} env-steps "
                       f"in {dt:.1f}s; env stepping OpenMP x{threads}, MLP/GAE/normalizers/sampling/shuffle "
                       f"single-threaded as in the reference; per-env-step cost is independent of N"}
 
 
+def cpu_baseline_cfgA(seconds=5.0):
+    """BASELINE.json configs[0]: configs/test.toml at --num-envs 8 --num-steps 128 (1x16 relu,
+    1 epoch x 1 minibatch) on the oracle, from the committed weights tests/golden/w_cfgA.npz
+    (SURVEY 8(d)), single-threaded as the reference's ndarray path; full updates until
+    `seconds` have passed."""
+    import numpy as np
+    import oracle_ffi as O
+    import bppo
+    from parity_util import oracle_train_cfg
+    w = np.load(os.path.join(ROOT, "tests", "golden", "w_cfgA.npz"))
+    cfg = bppo.make_config("test", num_envs=int(w["num_envs"]), num_steps=int(w["num_steps"]))
+    O.lib().or_set_mlp_parallel(0)
+    ot = O.Trainer(oracle_train_cfg(cfg, threads=1), np.ascontiguousarray(w["params"]))
+    ot.collect(); ot.gae(); ot.update()                 # warm-up
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        ot.collect(); ot.gae(); ot.update()
+        n += 1
+    dt = time.perf_counter() - t0
+    ot.close()
+    O.lib().or_set_mlp_parallel(1)
+    steps = n * cfg["num_envs"] * cfg["num_steps"]
+    return {"value": steps / dt, "unit": "env-steps/sec", "cores": 1, "kind": "port",
+            "sample": f"CfgA (configs/test.toml, --num-envs 8 --num-steps 128, weights tests/golden/w_cfgA.npz): "
+                      f"{n} full updates = {steps} env-steps in {dt:.1f}s, one thread"}
+
+
 def gae_isolated_ms(N, T, gamma=0.99, lam=0.95, reps=20):
     """k_gae_1p_seg at the workload's [T, N] shape on its own stream, nothing else on
-    the GPU (in the update loop it co-runs with the side-stream Fisher-Yates passes,
-    so its in-loop duration measures the sharing, not the kernel)."""
+    the GPU, in the variant the update loop runs: it also stores the advantage /
+    return pair of every packed 64-byte update row (bppo_gae_rows_device).  In the
+    loop it co-runs with the side-stream Fisher-Yates passes, so its in-loop
+    duration measures the sharing, not the kernel."""
     import torch
     from bppo import _lib as L
     g = torch.Generator(device="cuda").manual_seed(0)
@@ -184,15 +216,16 @@ def gae_isolated_ms(N, T, gamma=0.99, lam=0.95, reps=20):
     v = torch.rand(T, N, device="cuda", generator=g)
     lv = torch.rand(N, device="cuda", generator=g)
     adv, ret = torch.empty_like(r), torch.empty_like(r)
+    rows = torch.zeros(T * N * 2, device="cuda")
     st = torch.cuda.Stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
 
     def once():
-        rc = L.lib().bppo_gae_device(r.data_ptr(), d.data_ptr(), v.data_ptr(), lv.data_ptr(), T, N, gamma, lam,
-                                     adv.data_ptr(), ret.data_ptr(), st.cuda_stream)
+        rc = L.lib().bppo_gae_rows_device(r.data_ptr(), d.data_ptr(), v.data_ptr(), lv.data_ptr(), T, N, gamma,
+                                          lam, adv.data_ptr(), ret.data_ptr(), rows.data_ptr(), st.cuda_stream)
         if rc != 0:
-            raise RuntimeError(f"bppo_gae_device status {rc}")
+            raise RuntimeError(f"bppo_gae_rows_device status {rc}")
     with torch.cuda.stream(st):
         for _ in range(3):
             once()
@@ -365,17 +398,16 @@ def main():
             "traffic_source": mb_src, "kernel": "k_minibatch_mfma", "launch_ms": round(mb_ms, 4),
             "algorithmic": f"{mb_rows} rows x {FLOP_PER_ROW_FWD_BWD} FLOP"}
     gae_loop_ms = phase["gae"] / args.steps
-    gae_ms = gae_isolated_ms(N, T)
+    gae_ms = gae_loop_ms if args.no_gae_isolated else gae_isolated_ms(N, T)
     gae_gbs = N * T * GAE_BYTES_PER_ELEM / (gae_ms * 1e-3) / 1e9
     g_tr, g_src = traffic_for("k_gae_1p_seg", "k_gae.hip") if cfgB else (None, "not the profiled shape")
     gae_roof = {"bound": "hbm", "achieved": round(gae_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(gae_gbs / HBM_PEAK_GBS, 4), "traffic": g_tr, "traffic_unit": "B/launch",
                 "traffic_source": g_src, "kernel": "k_gae_1p_seg", "launch_ms": round(gae_ms, 4),
-                "measured": "achieved: isolated launches at the workload shape after the timed region (HIP "
-                            "events on the launch stream); in the update loop the kernel also writes the "
-                            "advantage/return pair of each packed update row (8 B/row, in traffic, which is "
-                            "PMC of the in-loop launches) and shares the GPU with the side-stream "
-                            "Fisher-Yates passes",
+                "measured": "achieved: isolated launches of the in-loop variant ([advantage, return] "
+                            "pair of each minibatch row stored too) at the workload shape after the timed region "
+                            "(HIP events on the launch stream); launch_ms_in_loop: the same kernel inside the "
+                            "update loop, where it shares the GPU with the side-stream Fisher-Yates passes",
                 "launch_ms_in_loop": round(gae_loop_ms, 4),
                 "algorithmic": f"{N * T} x {GAE_BYTES_PER_ELEM} B"}
     out = {"metric": METRIC, "value": round(value, 1), "unit": "env-steps/sec", "n_gpus": world,

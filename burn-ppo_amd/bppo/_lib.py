@@ -78,7 +78,7 @@ EXPORTS = (
     "bppo_vecenv_reset", "bppo_vecenv_observe", "bppo_vecenv_step", "bppo_vecenv_set_step", "bppo_set_reward_shaping_schedule",
     "bppo_obs_norm_get", "bppo_obs_norm_set", "bppo_ret_norm_get", "bppo_ret_norm_set",
     "bppo_collect_rollouts", "bppo_rollout_episodes", "bppo_compute_gae", "bppo_ppo_update", "bppo_train_step", "bppo_train_steps",
-    "bppo_set_allreduce", "bppo_set_allreduce_async", "bppo_get_stream", "bppo_opponents_set", "bppo_opponents_get_envs", "bppo_buffer_get", "bppo_buffer_set", "bppo_gae_device",
+    "bppo_set_allreduce", "bppo_set_allreduce_async", "bppo_get_stream", "bppo_opponents_set", "bppo_opponents_get_envs", "bppo_buffer_get", "bppo_buffer_set", "bppo_gae_device", "bppo_gae_rows_device",
     "bppo_gae_mp_device", "bppo_last_kernel_ms", "bppo_debug_libm", "bppo_debug_shuffle_chain",
     "bppo_debug_fisher_yates", "bppo_debug_gemm", "bppo_debug_shuffle_engine", "bppo_debug_sample",
     "bppo_rng_fill_bytes", "bppo_rng_from_seed", "bppo_rng_key_get", "bppo_num_param_tensors",
@@ -141,6 +141,7 @@ def lib():
         "bppo_buffer_get": (i32, [vp, C.c_char_p, vp, sz]),
         "bppo_buffer_set": (i32, [vp, C.c_char_p, vp, sz]),
         "bppo_gae_device": (i32, [vp, vp, vp, vp, i32, i32, C.c_float, C.c_float, vp, vp, vp]),
+        "bppo_gae_rows_device": (i32, [vp, vp, vp, vp, i32, i32, C.c_float, C.c_float, vp, vp, vp, vp]),
         "bppo_gae_mp_device": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, C.c_float, C.c_float, vp, vp,
                                      vp]),
         "bppo_last_kernel_ms": (i32, [vp, C.c_char_p, fp]),

@@ -250,7 +250,6 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     c->slab_rows = 256 * 8;   // one 8-wave (MFMA) or 4-wave block per CU, persistent over the minibatch
     c->relu_mfma = cfg->relu ? 1 : 0;
     if (!c->wide) TRY(dalloc(c, &c->d_slab, c->slab_rows * (np + 64)));
-    if (!c->wide) TRY(dalloc(c, &c->d_slab_part, (size_t)32 * (np + 64)));
     TRY(dalloc(c, &c->d_cp, (size_t)4 * c->N));
     TRY(dalloc(c, &c->d_steps, (size_t)c->N));
     TRY(dalloc(c, &c->d_env_pos, (size_t)c->N));
@@ -310,7 +309,10 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
                               sizeof(float) * (size_t)cfg->num_epochs * cfg->num_minibatches * (WM_COUNT + 4),
                               hipHostMallocDefault));
     if (!c->wide && cfg->hidden_size == 64 && cfg->num_hidden == 2 && cfg->relu && c->D == 5)
-        BPPO_HIP(c, hipMalloc((void **)&c->d_mbrow, sizeof(float4) * 4 * TN));
+    {
+        BPPO_HIP(c, hipMalloc((void **)&c->d_rowA, sizeof(float4) * 2 * TN));
+        BPPO_HIP(c, hipMalloc((void **)&c->d_rowB, sizeof(float2) * TN));
+    }
     BPPO_HIP(c, hipHostMalloc((void **)&c->h_red, sizeof(double) * (4 * 1024 + 64 + 2 * ROLL_HOST_WORDS),
                               hipHostMallocDefault));   // + two slots of the rollout's flags and episode partials
     BPPO_HIP(c, hipEventCreateWithFlags(&c->ev_upd, hipEventDisableTiming));
@@ -354,12 +356,12 @@ extern "C" void bppo_destroy(bppo_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     wide_free(c);
     popart_free(c);
-    void *ptrs[] = {c->d_params, c->d_m1, c->d_m2, c->d_grad, c->d_slab, c->d_slab_part, c->d_cp, c->d_steps,
+    void *ptrs[] = {c->d_params, c->d_m1, c->d_m2, c->d_grad, c->d_slab, c->d_cp, c->d_steps,
                     c->d_env_pos, c->d_ep_ret, c->d_ep_len, c->d_obs, c->d_rew, c->d_rew_raw,
                     c->d_done, c->d_val, c->d_logp, c->d_adv, c->d_ret, c->d_act, c->d_X, c->d_on,
                     c->d_obs_part, c->d_rn_returns, c->d_rn_stats, c->d_scan_agg, c->d_last_v,
                     c->d_eps, c->d_ep_count, c->d_ep_sum, c->d_err, c->d_perm_base, c->d_perm_ep, c->d_inv_ep, c->d_advpart, c->d_fy, c->d_scan,
-                    c->d_red, c->d_mb_stats, c->d_gumbel, c->d_rows, c->d_mbrow};
+                    c->d_red, c->d_mb_stats, c->d_gumbel, c->d_rows, c->d_rowA, c->d_rowB};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     fy_ranges_free(c->fyr);
     if (c->h_red) (void)hipHostFree(c->h_red);
@@ -669,9 +671,7 @@ static bppo_status fy_enqueue_ready(bppo_ctx *c, int slot) {
     while (c->fy_done < c->cfg.num_epochs && c->shuf.epoch_ready(slot, c->fy_done)) {
         const int e = c->fy_done;
         BPPO_HIP(c, hipStreamWaitEvent(c->fy_stream, c->shuf.ev[slot][e], 0));
-        // the previous epoch may have been permuted on the update stream (late epochs,
-        // BPPO_FY_LATE_INLINE): the scratch is shared
-        if (e > 0) BPPO_HIP(c, hipStreamWaitEvent(c->fy_stream, c->fy_ev[e - 1], 0));
+        if (e > 0) BPPO_HIP(c, hipStreamWaitEvent(c->fy_stream, c->fy_ev[e - 1], 0));   // shared scratch
         (void)hipEventRecord(c->ev[TM_SHUFFLE][0], c->fy_stream);
         BPPO_HIP(c, fisher_yates_device(c->shuf.d_J[slot] + (size_t)e * B, (uint32_t)B, c->d_fy, c->d_scan,
                                         c->d_perm_ep + (size_t)e * B, c->fy_stream, &c->fyr,
@@ -817,7 +817,7 @@ static bppo_status gae_enqueue(bppo_ctx *c) {
     bool packed = false;
     bppo_status s = launch_gae_1p(c->d_rew, c->d_done, c->d_val, c->d_last_v, c->T, c->N,
                                   (float)c->cfg.gamma, (float)c->cfg.gae_lambda, c->d_adv, c->d_ret,
-                                  c->stream, c->rows_from_rollout ? (float4 *)c->d_mbrow : nullptr, &packed);
+                                  c->stream, c->rows_from_rollout ? c->d_rowB : nullptr, &packed);
     c->rows_packed = packed;
     tm_end(c, TM_GAE);
     if (s != BPPO_OK) { c->err = "gae launch failed"; return s; }
@@ -864,7 +864,7 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
     double wait_ms = 0.0;
     tm_begin(c, TM_UPDATE);
     TRY(popart_update_begin(c, opp ? c->d_valid : nullptr));   // ppo.rs:1787-1808
-    if (c->d_mbrow && !c->rows_packed) TRY(launch_pack_rows(c));
+    if (c->d_rowA && !c->rows_packed) TRY(launch_pack_rows(c));
     c->rows_packed = false;
     float fw_ms = 0, sh_ms = 0;
     // without a KL early stop or a host all-reduce nothing in the loop needs the
@@ -887,28 +887,10 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
             if (B) TRY(opp_map_perm(c, (uint32_t)B));
             (void)hipEventRecord(s1, c->stream);
         } else {
-            static const bool late_inline = getenv("BPPO_FY_LATE_INLINE") ? atoi(getenv("BPPO_FY_LATE_INLINE")) != 0 : false;
             if (slot != c->fy_slot || ep >= c->fy_done) {
                 auto w0 = std::chrono::steady_clock::now();
                 c->shuf.wait_epoch(slot, ep);
                 wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
-                if (late_inline) {
-                    // an epoch not permuted ahead: on the update stream, between the previous
-                    // epoch's minibatches and this one's, instead of beside them
-                    if (slot != c->fy_slot) { c->fy_slot = slot; c->fy_done = 0; }
-                    while (c->fy_done <= ep) {
-                        const int e = c->fy_done;
-                        if (e > 0) BPPO_HIP(c, hipStreamWaitEvent(c->stream, c->fy_ev[e - 1], 0));
-                        BPPO_HIP(c, hipStreamWaitEvent(c->stream, c->shuf.ev[slot][e], 0));
-                        (void)hipEventRecord(c->ev[TM_SHUFFLE][0], c->stream);
-                        BPPO_HIP(c, fisher_yates_device(c->shuf.d_J[slot] + (size_t)e * B, (uint32_t)B, c->d_fy,
-                                                        c->d_scan, c->d_perm_ep + (size_t)e * B, c->stream, &c->fyr,
-                                                        c->d_inv_ep + (size_t)e * B));
-                        (void)hipEventRecord(c->ev[TM_SHUFFLE][1], c->stream);
-                        BPPO_HIP(c, hipEventRecord(c->fy_ev[e], c->stream));
-                        c->fy_done++;
-                    }
-                }
             }
             TRY(fy_enqueue_ready(c, slot));          // this epoch and any other resolved since
             BPPO_HIP(c, hipStreamWaitEvent(c->stream, c->fy_ev[ep], 0));
@@ -1216,6 +1198,16 @@ extern "C" bppo_status bppo_gae_device(const float *r, const float *d, const flo
                                        float *ret, void *stream) {
     if (!r || !d || !v || !lv || !adv || !ret || T < 0 || N < 0) return BPPO_ERR_ARG;
     return launch_gae_1p(r, d, v, lv, T, N, gamma, lambda, adv, ret, (hipStream_t)stream);
+}
+
+extern "C" bppo_status bppo_gae_rows_device(const float *r, const float *d, const float *v, const float *lv,
+                                            int32_t T, int32_t N, float gamma, float lambda, float *adv,
+                                            float *ret, float *rows, void *stream) {
+    if (!r || !d || !v || !lv || !adv || !ret || !rows || T < 0 || N < 0) return BPPO_ERR_ARG;
+    bool packed = false;
+    const bppo_status s = launch_gae_1p(r, d, v, lv, T, N, gamma, lambda, adv, ret, (hipStream_t)stream,
+                                        reinterpret_cast<float2 *>(rows), &packed);
+    return s != BPPO_OK ? s : packed ? BPPO_OK : BPPO_ERR_UNSUPPORTED;
 }
 
 extern "C" bppo_status bppo_gae_mp_device(const float *ar, const int32_t *pl, const float *d,

@@ -195,8 +195,7 @@ struct ShuffleEngine {
     int peek(int i, uint64_t q, uint32_t *r);     // walk i's range at checkpoint q: 1 known, 0 not yet, -1 never
 };
 uint64_t shuffle_walk_host(const Key8 &key, uint64_t stream, uint64_t pos, uint32_t n, uint32_t *J);
-// a low-priority side stream (shuffle copy stream, Fisher-Yates stream); with
-// BPPO_SIDE_CUS=n restricted to n CUs spread over the device instead (CU mask)
+// a low-priority side stream (shuffle copy stream, Fisher-Yates stream)
 hipError_t make_side_stream(int device, hipStream_t *st);
 
 struct Timers {
@@ -220,7 +219,6 @@ struct bppo_ctx {
     float *d_grad = nullptr;          // [n_params + metric slots]
     double *d_grad64 = nullptr;
     float *d_slab = nullptr;          // per-wave partial gradients
-    double *d_slab_part = nullptr;    // row-group partials of the slab reduction [32][np + 64]
     size_t slab_rows = 0;
     int slab_used = 0;                // waves that wrote a row in the last minibatch launch
     int relu_mfma = 1;                // CfgB net (64x2 relu): the MFMA minibatch kernel
@@ -283,7 +281,12 @@ struct bppo_ctx {
     float *d_mb_stats = nullptr;      // advantage [mean, std, min, max] of each minibatch of the epoch [M][4]
     float *d_mb_cur = nullptr;        // the current minibatch's row of d_mb_stats
     float *d_rows = nullptr;          // per-minibatch metric rows of one update [E*M][WM_COUNT + 4]
-    float4 *d_mbrow = nullptr;        // CfgB net: the update's rows packed 64 B each [B][4] (k_pack_rows)
+    // CfgB net: the update's minibatch rows packed in two arrays, so every store of the
+    // rollout and of GAE covers whole 32-byte sectors of consecutive rows: d_rowA [B][2]
+    // float4 = [obs 0..3][obs 4, action, log-prob, value] (32 B, the rollout writes it),
+    // d_rowB [B] float2 = [advantage, return] (8 B, GAE writes it); k_pack_rows otherwise
+    float4 *d_rowA = nullptr;
+    float2 *d_rowB = nullptr;
     // all-reduce hook
     bppo_allreduce_fn allreduce = nullptr;
     void *allreduce_user = nullptr;
@@ -392,7 +395,7 @@ bppo_status launch_forward_rows(bppo_ctx *c, const float *d_obs, int B, float *d
 // (k_gae.hip)
 bppo_status launch_gae_1p(const float *r, const float *d, const float *v, const float *lv, int T,
                           int N, float gamma, float lambda, float *adv, float *ret, hipStream_t s,
-                          float4 *rows = nullptr, bool *rows_done = nullptr);
+                          float2 *pairs = nullptr, bool *pairs_done = nullptr);
 bppo_status launch_gae_mp(const float *ar, const int32_t *pl, const float *d, const float *v,
                           const float *lvpp, int T, int N, int P, float gamma, float lambda,
                           float *adv, float *ret, hipStream_t s);

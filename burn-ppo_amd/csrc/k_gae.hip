@@ -76,7 +76,7 @@ __global__ void __launch_bounds__(GSEG_WAVES * 64) k_gae_1p_seg(const float4 *__
                                                                  const float4 *__restrict__ lv, int T, int N4,
                                                                  int L, float gamma, float lambda,
                                                                  float4 *__restrict__ adv, float4 *__restrict__ ret,
-                                                                 float4 *__restrict__ rows) {
+                                                                 float2 *__restrict__ pairs) {
     __shared__ float4 carry[GSEG_WAVES][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int g = blockIdx.x * 64 + lane;
@@ -132,10 +132,15 @@ __global__ void __launch_bounds__(GSEG_WAVES * 64) k_gae_1p_seg(const float4 *__
         adv[i] = A;
         const float4 R = make_float4(__fadd_rn(A.x, vu.x), __fadd_rn(A.y, vu.y), __fadd_rn(A.z, vu.z), __fadd_rn(A.w, vu.w));
         ret[i] = R;
-        if (rows) {   // the packed update rows of these 4 envs (row 4i + j): [adv, ret] at float 8
-            float2 *o = reinterpret_cast<float2 *>(rows + 4 * (4 * i) + 2);
-            o[0] = make_float2(A.x, R.x); o[8] = make_float2(A.y, R.y);
-            o[16] = make_float2(A.z, R.z); o[24] = make_float2(A.w, R.w);
+        if (pairs) {
+            // the update rows' [advantage, return] pairs of these 4 envs: 32 contiguous
+            // bytes per lane, adjacent lanes adjacent (2 KB per wave store pair).  The
+            // same pairs stored into 64-byte interleaved rows, 8 B per row per lane, cost
+            // 241 us of stores at CfgB against 13.5 us for this pattern
+            // (scripts/probes/row_store_probe.hip, profiles/r03_row_store_probe.txt)
+            float4 *o = reinterpret_cast<float4 *>(pairs + 4 * i);
+            o[0] = make_float4(A.x, R.x, A.y, R.y);
+            o[1] = make_float4(A.z, R.z, A.w, R.w);
         }
     }
 }
@@ -190,18 +195,103 @@ __global__ void __launch_bounds__(256) k_gae_mp(const float *__restrict__ ar,
     }
 }
 
+// k_gae_mp with T split over GSEG_WAVES waves of a block (lane = env, 64 envs per
+// block): each wave loads its segment's players, dones, values and rewards at once,
+// then the per-env state of the two reverse passes (carry[P], gc[P], nv[P]) walks the
+// segments from the last to the first through LDS, one wave at a time, with the op
+// sequence of k_gae_mp per element (bit-identical).  At CfgD (N = 32768) the one-lane-
+// per-env kernel had 2 waves per CU; this one has 32, and every load is issued up front.
+template <int P>
+__global__ void __launch_bounds__(GSEG_WAVES * 64) k_gae_mp_seg(const float *__restrict__ ar,
+                                                               const int32_t *__restrict__ pl,
+                                                               const float *__restrict__ d,
+                                                               const float *__restrict__ v,
+                                                               const float *__restrict__ lvpp, int T, int N, int L,
+                                                               float gamma, float lambda, float *__restrict__ adv,
+                                                               float *__restrict__ ret) {
+    __shared__ float st[3 * P][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int e = blockIdx.x * 64 + lane;
+    const bool ok = e < N;
+    const int t0 = w * L, n = max(0, min(T, t0 + L) - t0);
+    const float gl = gamma * lambda;
+    int a_[GSEG_L];
+    float dn_[GSEG_L], v_[GSEG_L], rw_[GSEG_L][P];
+    if (ok) {
+#pragma unroll
+        for (int u = 0; u < GSEG_L; u++)
+            if (u < n) {
+                const size_t i = (size_t)(t0 + u) * N + e;
+                a_[u] = pl[i]; dn_[u] = d[i]; v_[u] = v[i];
+#pragma unroll
+                for (int p = 0; p < P; p++) rw_[u][p] = ar[i * P + p];
+            }
+    }
+    float out_a[GSEG_L];
+    for (int k = GSEG_WAVES - 1; k >= 0; k--) {
+        if (w == k && ok) {
+            float carry[P], gc[P], nv[P];
+#pragma unroll
+            for (int p = 0; p < P; p++) {
+                if (k == GSEG_WAVES - 1) { carry[p] = 0.0f; gc[p] = 0.0f; nv[p] = lvpp[(size_t)e * P + p]; }
+                else { carry[p] = st[p][lane]; gc[p] = st[P + p][lane]; nv[p] = st[2 * P + p][lane]; }
+            }
+#pragma unroll
+            for (int u = GSEG_L - 1; u >= 0; u--) {
+                if (u >= n) continue;
+                const int a = a_[u];
+                const float dn = dn_[u], vv = v_[u];
+                if (dn > 0.5f) {
+#pragma unroll
+                    for (int p = 0; p < P; p++) carry[p] = 0.0f;
+                }
+                float ca = 0.0f, ra = 0.0f;
+#pragma unroll
+                for (int p = 0; p < P; p++) if (p == a) { ca = carry[p]; ra = rw_[u][p]; }
+                const float attributed = __fadd_rn(ra, ca);
+#pragma unroll
+                for (int p = 0; p < P; p++) carry[p] = p == a ? 0.0f : __fadd_rn(carry[p], rw_[u][p]);
+                if (dn > 0.5f) {
+#pragma unroll
+                    for (int p = 0; p < P; p++) { gc[p] = 0.0f; if (p != a) nv[p] = 0.0f; }
+                }
+                float nva = 0.0f, gca = 0.0f;
+#pragma unroll
+                for (int p = 0; p < P; p++) if (p == a) { nva = nv[p]; gca = gc[p]; }
+                const float om = 1.0f - dn;
+                const float delta = __fsub_rn(__builtin_fmaf(gamma * nva, om, attributed), vv);
+                const float A = __builtin_fmaf(gl * om, gca, delta);
+                out_a[u] = A;
+#pragma unroll
+                for (int p = 0; p < P; p++) if (p == a) { gc[p] = A; nv[p] = vv; }
+            }
+#pragma unroll
+            for (int p = 0; p < P; p++) { st[p][lane] = carry[p]; st[P + p][lane] = gc[p]; st[2 * P + p][lane] = nv[p]; }
+        }
+        __syncthreads();
+    }
+    if (!ok) return;
+#pragma unroll
+    for (int u = 0; u < GSEG_L; u++) {
+        if (u >= n) continue;
+        const size_t i = (size_t)(t0 + u) * N + e;
+        adv[i] = out_a[u];
+        ret[i] = __fadd_rn(out_a[u], v_[u]);
+    }
+}
+
 bppo_status launch_gae_1p(const float *r, const float *d, const float *v, const float *lv, int T,
                           int N, float gamma, float lambda, float *adv, float *ret, hipStream_t s,
-                          float4 *rows, bool *rows_done) {
-    if (rows_done) *rows_done = false;
+                          float2 *pairs, bool *pairs_done) {
+    if (pairs_done) *pairs_done = false;
     if (T <= 0 || N <= 0) return BPPO_OK;
     const bool al = ((uintptr_t)r | (uintptr_t)d | (uintptr_t)v | (uintptr_t)lv | (uintptr_t)adv | (uintptr_t)ret) % 16 == 0;
     if (N % 4 == 0 && T <= GSEG_WAVES * GSEG_L && al) {
         const int N4 = N / 4, L = (T + GSEG_WAVES - 1) / GSEG_WAVES;
         hipLaunchKernelGGL(k_gae_1p_seg, dim3((N4 + 63) / 64), dim3(GSEG_WAVES * 64), 0, s, (const float4 *)r,
                            (const float4 *)d, (const float4 *)v, (const float4 *)lv, T, N4, L, gamma, lambda,
-                           (float4 *)adv, (float4 *)ret, rows);
-        if (rows_done) *rows_done = rows != nullptr;
+                           (float4 *)adv, (float4 *)ret, pairs);
+        if (pairs_done) *pairs_done = pairs != nullptr;
     } else {
         hipLaunchKernelGGL(k_gae_1p, dim3((N + 255) / 256), dim3(256), 0, s, r, d, v, lv, T, N, gamma,
                            lambda, adv, ret);
@@ -213,6 +303,21 @@ bppo_status launch_gae_mp(const float *ar, const int32_t *pl, const float *d, co
                           const float *lvpp, int T, int N, int P, float gamma, float lambda,
                           float *adv, float *ret, hipStream_t s) {
     if (T <= 0 || N <= 0) return BPPO_OK;
+    if (T <= GSEG_WAVES * GSEG_L && P >= 1 && P <= 6) {
+        const int L = (T + GSEG_WAVES - 1) / GSEG_WAVES;
+        const dim3 gs((N + 63) / 64), bs(GSEG_WAVES * 64);
+#define MPSEG(P_) hipLaunchKernelGGL(k_gae_mp_seg<P_>, gs, bs, 0, s, ar, pl, d, v, lvpp, T, N, L, gamma, lambda, adv, ret)
+        switch (P) {
+        case 1: MPSEG(1); break;
+        case 2: MPSEG(2); break;
+        case 3: MPSEG(3); break;
+        case 4: MPSEG(4); break;
+        case 5: MPSEG(5); break;
+        default: MPSEG(6); break;
+        }
+#undef MPSEG
+        return hipGetLastError() == hipSuccess ? BPPO_OK : BPPO_ERR_HIP;
+    }
     dim3 g((N + 255) / 256), b(256);
     switch (P) {
     case 1: hipLaunchKernelGGL(k_gae_mp<1>, g, b, 0, s, ar, pl, d, v, lvpp, T, N, gamma, lambda, adv, ret); break;

@@ -115,7 +115,7 @@ struct RolloutArgs {
     double *obs_part;
     EpisodeRec *eps; int32_t *ep_count; int eps_cap;
     int32_t *err;
-    float4 *rows;        // MFMA rollout: also the update's packed rows (k_update.hip load_row), or null
+    float4 *rows;        // MFMA rollout: also the update's rows A [B][2] float4 (k_update.hip load_row), or null
 };
 
 template <int H, int NL, int ACT>
@@ -281,6 +281,7 @@ __global__ void __launch_bounds__(512, 2) k_cartpole_rollout_mfma(RolloutArgs a,
         const size_t row = (size_t)t * N + e;
         // this step's Gumbel pair, loaded before the MLP so its HBM latency hides under it
         const float2 gz = mine ? *reinterpret_cast<const float2 *>(gum + row * 2) : make_float2(0.0f, 0.0f);
+        float4 xa = make_float4(0.f, 0.f, 0.f, 0.f);
         float x4 = 0.0f;
         if (h == 0) {
             float x[5] = {0, 0, 0, 0, 0};
@@ -291,7 +292,7 @@ __global__ void __launch_bounds__(512, 2) k_cartpole_rollout_mfma(RolloutArgs a,
                 nz.apply(raw, x);
 #pragma unroll
                 for (int d = 0; d < 5; d++) a.obs[row * 5 + d] = x[d];
-                if (a.rows) a.rows[row * 4] = make_float4(x[0], x[1], x[2], x[3]);
+                xa = make_float4(x[0], x[1], x[2], x[3]);
                 x4 = x[4];
             }
 #pragma unroll
@@ -388,7 +389,8 @@ __global__ void __launch_bounds__(512, 2) k_cartpole_rollout_mfma(RolloutArgs a,
             a.done[row] = done ? 1.0f : 0.0f;
             a.val[row] = v;
             a.logp[row] = lp;
-            if (a.rows) a.rows[row * 4 + 1] = make_float4(x4, __int_as_float(act), lp, v);
+            // the row's 32 bytes in one pair of stores (adjacent lanes: adjacent rows)
+            if (a.rows) { a.rows[row * 2] = xa; a.rows[row * 2 + 1] = make_float4(x4, __int_as_float(act), lp, v); }
         }
         wave_sync();
     }
@@ -614,8 +616,8 @@ bppo_status launch_cartpole_rollout(bppo_ctx *c, uint64_t base_pos, const double
         // the update's packed rows (obs, action, log-prob, value) written by the rollout
         // itself; GAE adds advantage and return, so k_pack_rows is not needed (PopArt
         // trains on normalized values computed at update start: packed there instead)
-        if (c->d_mbrow && !c->cfg.normalize_values && !getenv("BPPO_NO_FUSED_PACK")) {
-            a.rows = c->d_mbrow;
+        if (c->d_rowA && !c->cfg.normalize_values && !getenv("BPPO_NO_FUSED_PACK")) {
+            a.rows = c->d_rowA;
             c->rows_from_rollout = true;
         }
         // Gumbel noise for every (t, env, action) first, then the MFMA rollout

@@ -30,7 +30,8 @@ struct MbArgs {
     float lo, hi, ceps;    // clip bounds
     float inv_mb, ent_coef, value_coef;
     int clip_value;
-    const float4 *rows;    // packed rows [B][4 x float4] (k_pack_rows) or nullptr
+    const float4 *rowA;    // packed rows A [B][2] float4 and B [B] float2 (bppo_internal.h d_rowA / d_rowB) or nullptr
+    const float2 *rowB;
     unsigned long long *stamps;   // diagnostic build only (BPPO_MB_STAMPS): per-wave segment cycles
 };
 
@@ -308,9 +309,9 @@ __device__ __forceinline__ RowData load_row(const MbArgs &g, uint32_t idx) {
     const bool ok = idx != 0xFFFFFFFFu;
     const size_t i = ok ? idx : 0;
     RowData d;
-    if (g.rows) {                     // one 64-byte line per row: [obs 0..3][obs 4, action, log-prob, value][adv, ret, -, -]
-        const float4 a = g.rows[i * 4], b = g.rows[i * 4 + 1];
-        const float2 c = *reinterpret_cast<const float2 *>(g.rows + i * 4 + 2);
+    if (g.rowA) {                     // one 32-byte sector [obs 0..3][obs 4, action, log-prob, value] + [adv, ret]
+        const float4 a = g.rowA[i * 2], b = g.rowA[i * 2 + 1];
+        const float2 c = g.rowB[i];
         d.x0 = ok ? a.x : 0.0f; d.x1 = ok ? a.y : 0.0f; d.x2 = ok ? a.z : 0.0f; d.x3 = ok ? a.w : 0.0f;
         d.x4 = ok ? b.x : 0.0f;
         d.a = ok ? __float_as_int(b.y) : 0;
@@ -327,23 +328,24 @@ __device__ __forceinline__ RowData load_row(const MbArgs &g, uint32_t idx) {
     return d;
 }
 
-// the update's rows packed once per update into 64-byte records
-// [obs 0..3][obs 4, action, log-prob, value][advantage, return, -, -] so the shuffled
-// minibatch gather touches one cache line per row instead of six
+// the update's rows packed once per update: [obs 0..3][obs 4, action, log-prob, value]
+// (rows A, 32 B) and [advantage, return] (rows B, 8 B), so the shuffled minibatch
+// gather touches two sectors per row instead of six buffers (when the rollout and GAE
+// did not write them already)
 __global__ void __launch_bounds__(256) k_pack_rows(size_t B, const float *obs, const int32_t *act, const float *logp,
                                                    const float *adv, const float *ret, const float *val,
-                                                   float4 *rows) {
+                                                   float4 *rowA, float2 *rowB) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < B; i += (size_t)gridDim.x * blockDim.x) {
         const float *o = obs + i * 5;
-        rows[i * 4] = make_float4(o[0], o[1], o[2], o[3]);
-        rows[i * 4 + 1] = make_float4(o[4], __int_as_float(act[i]), logp[i], val[i]);
-        rows[i * 4 + 2] = make_float4(adv[i], ret[i], 0.0f, 0.0f);
+        rowA[i * 2] = make_float4(o[0], o[1], o[2], o[3]);
+        rowA[i * 2 + 1] = make_float4(o[4], __int_as_float(act[i]), logp[i], val[i]);
+        rowB[i] = make_float2(adv[i], ret[i]);
     }
 }
 bppo_status launch_pack_rows(bppo_ctx *c) {
     const size_t B = (size_t)c->T * c->N;
     hipLaunchKernelGGL(k_pack_rows, dim3(2048), dim3(256), 0, c->stream, B, c->d_obs, c->d_act, c->d_logp, c->d_adv,
-                       c->u_ret, c->u_val, c->d_mbrow);
+                       c->u_ret, c->u_val, c->d_rowA, c->d_rowB);
     BPPO_HIP(c, hipGetLastError());
     return BPPO_OK;
 }
@@ -701,33 +703,9 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
 #endif
 }
 
-// fixed-order reduction of the wave partials: grad[p] = sum_w slab[w][p], in two
-// passes (SLAB_GROUPS row groups in parallel, then the groups in order)
+// fixed-order reduction of the wave partials, grad[p] = sum_w slab[w][p]: SLAB_GROUPS
+// row groups each summed in f64 in row order, then the groups in order.
 constexpr int SLAB_GROUPS = 32;
-__global__ void k_slab_reduce_groups(const float *slab, int rows, int width, double *part) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= width) return;
-    const int per = (rows + SLAB_GROUPS - 1) / SLAB_GROUPS, g = blockIdx.y;
-    const int w0 = g * per, w1 = min(rows, w0 + per);
-    const bool is_max = p == width - NUM_M + M_VEMAX;
-    double s = is_max ? -INFINITY : 0.0;
-    for (int w = w0; w < w1; w++) {
-        const double v = slab[(size_t)w * width + p];
-        s = is_max ? fmax(s, v) : s + v;
-    }
-    part[(size_t)g * width + p] = s;
-}
-__global__ void k_slab_reduce(const double *part, int width, float *grad) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= width) return;
-    const bool is_max = p == width - NUM_M + M_VEMAX;
-    double s = is_max ? -INFINITY : 0.0;
-    for (int g = 0; g < SLAB_GROUPS; g++) {
-        const double v = part[(size_t)g * width + p];
-        s = is_max ? fmax(s, v) : s + v;
-    }
-    grad[p] = (float)s;
-}
 // both passes in one launch, same association (bit-identical grad): a block owns 64
 // columns; its 16 waves take row groups g = q, q + 16 and leave the group sums in
 // LDS, then wave 0 adds the 32 groups in order.  One dependent launch fewer per
@@ -1077,8 +1055,7 @@ __global__ void __launch_bounds__(256) k_adv_stream_final(const double *part, in
 
 bppo_status launch_epoch_adv_stats(bppo_ctx *c, uint32_t B, int M, const uint32_t *inv) {
     const EpochSplit sp{B, B / (uint32_t)M, B % (uint32_t)M, (uint32_t)M};
-    static const bool stream_on = getenv("BPPO_ADV_STREAM") ? atoi(getenv("BPPO_ADV_STREAM")) != 0 : true;
-    if (inv && stream_on && M <= ADV_STREAM_MAXM && sp.base > 0) {
+    if (inv && M <= ADV_STREAM_MAXM && sp.base > 0) {
         const uint32_t C = (B + ADV_STREAM_BLOCKS - 1) / ADV_STREAM_BLOCKS;
         const int nblk = (int)((B + C - 1) / C);
         const int MB = M <= 4 ? 4 : (M <= 8 ? 8 : 16);
@@ -1111,7 +1088,7 @@ bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_
     g.ceps = (float)c->cfg.clip_epsilon;
     g.inv_mb = (float)(1.0 / (double)n); g.ent_coef = ent_coef; g.value_coef = (float)c->cfg.value_coef;
     g.clip_value = c->cfg.clip_value;
-    g.rows = c->d_mbrow;
+    g.rowA = c->d_rowA; g.rowB = c->d_rowB;
     g.stamps = nullptr;
 #ifdef BPPO_MB_STAMPS
     static unsigned long long *d_st = nullptr;
@@ -1163,16 +1140,8 @@ bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_
 #undef L
     BPPO_HIP(c, hipGetLastError());
     const int width = (int)c->net.n_params + NUM_M;
-    static const bool two_pass = getenv("BPPO_SLAB_TWO_PASS") && atoi(getenv("BPPO_SLAB_TWO_PASS"));
-    if (two_pass) {
-        hipLaunchKernelGGL(k_slab_reduce_groups, dim3((width + 255) / 256, SLAB_GROUPS), dim3(256), 0, c->stream,
-                           c->d_slab, c->slab_used, width, c->d_slab_part);
-        hipLaunchKernelGGL(k_slab_reduce, dim3((width + 255) / 256), dim3(256), 0, c->stream, c->d_slab_part,
-                           width, c->d_grad);
-    } else {
-        hipLaunchKernelGGL(k_slab_reduce1, dim3((width + 63) / 64), dim3(64 * SLAB1_WAVES), 0, c->stream, c->d_slab,
-                           c->slab_used, width, c->d_grad);
-    }
+    hipLaunchKernelGGL(k_slab_reduce1, dim3((width + 63) / 64), dim3(64 * SLAB1_WAVES), 0, c->stream, c->d_slab,
+                       c->slab_used, width, c->d_grad);
     BPPO_HIP(c, hipGetLastError());
     return BPPO_OK;
 }

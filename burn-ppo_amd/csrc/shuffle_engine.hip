@@ -201,17 +201,9 @@ static void shuffle_word_stats(uint32_t n, double &mean, double &sd) {
 // own), so it is plain memory on 2 MB pages, not pinned 4 KB pages: a walker
 // streams ~8 GB/s of words, and on 4 KB pages the hardware prefetcher restarts at
 // every page (= every 1024-word checkpoint piece).  Touched here so the producers
-// never fault.  BPPO_SHUFFLE_PINNED_WORDS=1: the old pinned buffer.
-static bool words_pinned() {
-    static const int v = getenv("BPPO_SHUFFLE_PINNED_WORDS") ? atoi(getenv("BPPO_SHUFFLE_PINNED_WORDS")) : 0;
-    return v != 0;
-}
+// never fault.
 static uint32_t *host_words_alloc(uint64_t words) {
     const size_t bytes = (size_t)words * 4;
-    if (words_pinned()) {
-        uint32_t *h = nullptr;
-        return hipHostMalloc((void **)&h, bytes, hipHostMallocDefault) == hipSuccess ? h : nullptr;
-    }
     const size_t huge = (size_t)2 << 20, sz = (bytes + huge - 1) / huge * huge;
     void *p = mmap(nullptr, sz, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
     if (p == MAP_FAILED) return nullptr;
@@ -220,7 +212,6 @@ static uint32_t *host_words_alloc(uint64_t words) {
     return static_cast<uint32_t *>(p);
 }
 static void host_words_free(uint32_t *h, uint64_t words) {
-    if (words_pinned()) { (void)hipHostFree(h); return; }
     const size_t huge = (size_t)2 << 20, bytes = (size_t)words * 4;
     (void)munmap(h, (bytes + huge - 1) / huge * huge);
 }
@@ -245,7 +236,6 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
     // C leading epochs of the next job are speculated during this job (their walks
     // get a whole job of head start; later epochs' walks start with their job)
     C = std::min(2, std::max(epochs, 1));
-    if (const char *e = getenv("BPPO_SHUFFLE_CARRY")) C = std::max(1, std::min(epochs, atoi(e)));
     // frontier scheduling (depth D): the walks of a boundary start only when the
     // boundary D epochs before it is known exactly, so they guess around an exact
     // position with one-sigma-times-sqrt(D) spread, and only ~2 groups walk at once
@@ -263,8 +253,8 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
     } else {
         fr_depth = 0;
     }
-    // exact continuations need the last epoch in the in-job groups (BPPO_SHUFFLE_CONT=0: off)
-    const bool cont_on = (getenv("BPPO_SHUFFLE_CONT") ? atoi(getenv("BPPO_SHUFFLE_CONT")) : 1) != 0 && epochs - 1 >= C;
+    // exact continuations need the last epoch in the in-job groups
+    const bool cont_on = epochs - 1 >= C;
     K = std::min(K, SHUF_MAX_SPEC / (std::max(epochs - C, 0) + 2 * C + (cont_on ? 2 : 0)));
     ncur = K * std::max(epochs - C, 0);
     nspec = ncur + 2 * C * K;
@@ -330,8 +320,7 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
     const uint64_t nck = (uint64_t)((Ew + 24.0 * sigma) / SHUF_CK) + 4;
     for (int i = 0; i < nspec; i++) spec[i].ck.assign(nck, 0xFFFFFFFFu);
     for (int i = 0; i < nspec; i++) workers.emplace_back([this, i]() { worker(i); });
-    int ngen = std::max(1, std::min(4, host_cpus / 4));
-    if (const char *e = getenv("BPPO_SHUFFLE_GEN")) ngen = std::max(1, atoi(e));
+    const int ngen = std::max(1, std::min(4, host_cpus / 4));
     for (int i = 0; i < ngen; i++) gens.emplace_back([this]() { generator(); });
     th = std::thread([this]() { run(); });
     return BPPO_OK;
@@ -386,20 +375,9 @@ void ShuffleEngine::release(int slot, hipStream_t st) {
 
 // words [pos, pos + len) of word buffer b (one checkpoint piece: never crosses a
 // chunk); outside its regions (not at the usual sizes) they are made here
-// BPPO_SHUFFLE_SELFGEN=1: every walk makes its own words piece by piece (no
-// producer threads, no pinned-buffer streaming: L1-resident words, more ChaCha work)
-static bool shuf_selfgen() {
-    static const int v = getenv("BPPO_SHUFFLE_SELFGEN") ? atoi(getenv("BPPO_SHUFFLE_SELFGEN")) : 0;
-    return v != 0;
-}
 
 const uint32_t *ShuffleEngine::words(int b, uint64_t pos, uint64_t len, std::vector<uint32_t> &scratch) {
     WordBuf &w = wb[b];
-    if (shuf_selfgen()) {
-        scratch.resize(len);
-        bppo_host::chacha12_words(key.k, stream, pos, scratch.data(), len);
-        return scratch.data();
-    }
     for (int g = 0; g < w.nreg; g++) {
         const WordBuf::Region &R = w.reg[g];
         if (pos >= R.base && pos + len <= R.base + R.len) {
@@ -491,13 +469,9 @@ void ShuffleEngine::worker(int i) {
     // 2's, ..., the next job's carry set last (16 CPUs run ~K (E + 1) walks; the
     // scheduler otherwise shares them evenly and delays the walk needed first)
     {
-        static const int nice_step = getenv("BPPO_SHUFFLE_NICE") ? atoi(getenv("BPPO_SHUFFLE_NICE")) : 3;
-        // every speculative walk below the true walk (the driver thread, nice 0)
-        static const int nice_base = getenv("BPPO_SHUFFLE_NICE_BASE") ? atoi(getenv("BPPO_SHUFFLE_NICE_BASE")) : 0;
+        // frontier scheduling keeps few walks alive at once: one niceness (1) for all
         const int g = i < ncur ? i / std::max(K, 1) : std::max(epochs - C, 0);
-        // frontier scheduling keeps few walks alive at once: one niceness for all
-        static const int fr_nice = getenv("BPPO_SHUFFLE_FNICE") ? atoi(getenv("BPPO_SHUFFLE_FNICE")) : 1;
-        const int nv = fr_depth > 0 ? fr_nice : nice_base + nice_step * g;
+        const int nv = fr_depth > 0 ? 1 : 3 * g;
         if (nv > 0) (void)setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), std::min(19, nv));
     }
     std::vector<uint32_t> scratch;
@@ -677,7 +651,7 @@ void ShuffleEngine::run() {
                 const WordBuf::Region *R = nullptr;
                 for (int g = 0; g < W.nreg; g++)
                     if (c * SHUF_CHUNK >= W.reg[g].off && c * SHUF_CHUNK < W.reg[g].off + W.reg[g].len) R = &W.reg[g];
-                if (R && !shuf_selfgen()) gen_order.push_back({R->base + (c * SHUF_CHUNK - R->off), c});
+                if (R) gen_order.push_back({R->base + (c * SHUF_CHUNK - R->off), c});
             }
             gen_buf = &W;
             gen_next.store(0, std::memory_order_relaxed);
@@ -686,7 +660,7 @@ void ShuffleEngine::run() {
         cv.notify_all();
         // ---- speculative walks: epochs 1 .. E-1 of this job, and the next job's first epoch
         // K guesses evenly over centre +- spread*sd
-        static const double spread = getenv("BPPO_SHUFFLE_SPREAD") ? atof(getenv("BPPO_SHUFFLE_SPREAD")) : 2.0;
+        const double spread = 2.0;
         auto guess = [&](double centre, double sd, int k) {
             return (uint64_t)std::max((double)start, std::floor(centre + ((k + 0.5) / K - 0.5) * 2.0 * spread * sd));
         };
@@ -828,8 +802,7 @@ void ShuffleEngine::run() {
                     if (!keep[i]) spec[i].stop.store(true, std::memory_order_relaxed);
                 return exact;
             };
-            static const bool prune_on = (getenv("BPPO_SHUFFLE_PRUNE") ? atoi(getenv("BPPO_SHUFFLE_PRUNE")) : 1) != 0;
-            if (prune_on && K > 0 && !cancelled) {
+            if (K > 0 && !cancelled) {
                 std::lock_guard<std::mutex> lk(mu);
                 if (e + 1 < epochs) {
                     if (e + 1 < C) { if (carry_valid[cs]) prune(cp0 + (e + 1) * K, cp0 + (e + 2) * K, pos); }
@@ -875,7 +848,7 @@ void ShuffleEngine::run() {
                     }
                 Seg *dS = d_seg[slot] + (size_t)e * maxseg;
                 (void)hipMemcpyAsync(dS, S, sizeof(Seg) * (size_t)std::max(ns, 1), hipMemcpyHostToDevice, copy);
-                static const uint32_t slice = getenv("BPPO_XJ_SLICE") ? (uint32_t)atoi(getenv("BPPO_XJ_SLICE")) : XJ_SLICE;
+                const uint32_t slice = XJ_SLICE;
                 for (uint32_t w0 = 0; w0 < (uint32_t)SHUF_CK; w0 += slice)
                     hipLaunchKernelGGL(k_expand_J, dim3((unsigned)((std::max(ns, 1) + XJ_THREADS - 1) / XJ_THREADS)),
                                        dim3(XJ_THREADS), 0, copy, key, stream, (const Seg *)dS, ns, wr,
@@ -953,17 +926,7 @@ void ShuffleEngine::shutdown() {
 }
 
 hipError_t make_side_stream(int device, hipStream_t *st) {
-    const char *e = getenv("BPPO_SIDE_CUS");
-    hipDeviceProp_t pr{};
-    if (e && atoi(e) > 0 && hipGetDeviceProperties(&pr, device) == hipSuccess && atoi(e) < pr.multiProcessorCount) {
-        const int ncu = pr.multiProcessorCount, want = atoi(e);
-        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-        for (int k = 0; k < want; k++) {
-            const int cu = (int)((int64_t)k * ncu / want);
-            mask[cu / 32] |= 1u << (cu % 32);
-        }
-        return hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data());
-    }
+    (void)device;
     int lo = 0, hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
     return hipStreamCreateWithPriority(st, hipStreamNonBlocking, lo);

@@ -302,16 +302,7 @@ static size_t walk_avx512_nj_t(const u32 *w, size_t nw, u32 *rp) {
     *rp = r;
     return p;
 }
-static size_t walk_avx512_nj(const u32 *w, size_t nw, u32 *rp) {
-    static const int nh = getenv("BPPO_WALK_NH") ? atoi(getenv("BPPO_WALK_NH")) : 10;
-    switch (nh) {
-    case 8: return walk_avx512_nj_t<8>(w, nw, rp);
-    case 10: return walk_avx512_nj_t<10>(w, nw, rp);
-    case 14: return walk_avx512_nj_t<14>(w, nw, rp);
-    case 16: return walk_avx512_nj_t<16>(w, nw, rp);
-    default: return walk_avx512_nj_t<12>(w, nw, rp);
-    }
-}
+static size_t walk_avx512_nj(const u32 *w, size_t nw, u32 *rp) { return walk_avx512_nj_t<10>(w, nw, rp); }
 
 static int isa_level() {
     static int v = -1;

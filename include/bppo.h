@@ -248,6 +248,13 @@ bppo_status bppo_buffer_set(bppo_ctx *ctx, const char *name, const void *host, s
 bppo_status bppo_gae_device(const float *rewards, const float *dones, const float *values,
                             const float *last_values, int32_t T, int32_t N, float gamma,
                             float lambda, float *advantages, float *returns, void *hip_stream);
+/* the same, plus the [advantage, return] pair of every row, pairs [T*N][2] floats (row
+ * t*N+e), as the update path writes them for its minibatch gathers;
+ * BPPO_ERR_UNSUPPORTED unless N % 4 == 0, T <= 128 and the arrays are 16-byte aligned */
+bppo_status bppo_gae_rows_device(const float *rewards, const float *dones, const float *values,
+                                 const float *last_values, int32_t T, int32_t N, float gamma,
+                                 float lambda, float *advantages, float *returns, float *pairs,
+                                 void *hip_stream);
 /* compute_gae_multiplayer (ppo.rs:1140-1264): all_rewards [T,N,P], players [T,N] i32,
  * last_v_pp [N,P] */
 bppo_status bppo_gae_mp_device(const float *all_rewards, const int32_t *players,

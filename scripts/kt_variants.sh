@@ -10,7 +10,7 @@ i=0
 for v in "$@"; do
   d=gpurun_out/kv_${TAG}_$i
   export $v
-  timeout -k 10 240 rocprofv3 --kernel-trace -d $d -o kt -- python3 bench.py --steps 6 --warmup 1 --no-cpu-baseline --no-learning > $d.log 2>&1
+  timeout -k 10 240 rocprofv3 --kernel-trace -d $d -o kt -- python3 bench.py --steps 6 --warmup 1 --no-cpu-baseline --no-learning --no-gae-isolated > $d.log 2>&1
   rc=$?; [ $rc -eq 0 ] || { echo "[$v] rc=$rc"; exit $rc; }
   python3 - "$v" "$RE" $d <<'PY'
 import glob, re, sqlite3, statistics, sys

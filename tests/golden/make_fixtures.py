@@ -7,6 +7,11 @@ from the CPU oracle (oracle/, a restatement of the reference path):
   c4_scripted.npz           Connect Four VecEnv driven by a scripted action matrix
   ld_scripted.npz           Liar's Dice VecEnv (with privileged obs) the same way
                             (env.rs:400-487, connect_four.rs, liars_dice.rs)
+  w_cfgA.npz                CfgA (configs/test.toml at --num-envs 8 --num-steps 128): the
+                            initial weights the CPU baseline and the parity runs load
+                            ("weights from fixture w_cfgA.bin"), and the
+                            oracle's first two updates from them (metrics, RNG positions,
+                            parameters after each)
   minibatch_cfgB.npz        one minibatch (512 rows, CfgB net) through
                             compute_minibatch_loss + backward + Adam with per-tensor
                             clip (ppo.rs:1385-1592, main.rs:264-268): metrics, the
@@ -120,11 +125,30 @@ def minibatch():
                 adv_mean=st[0].value, adv_std=st[1].value, lr=1e-3, ent_coef=0.01, max_grad_norm=0.5)
 
 
+def cfgA():
+    from parity_util import METRICS, oracle_train_cfg
+    cfg = make_config("test", num_envs=8, num_steps=128)
+    params = orthogonal_init(cfg, seed=0)
+    ot = O.Trainer(oracle_train_cfg(cfg), params)
+    out = dict(params=params, num_envs=8, num_steps=128, seed=cfg["seed"])
+    for u in range(2):
+        out[f"episodes_{u}"] = ot.collect()
+        out[f"rng_rollout_{u}"] = ot.rng_pos()
+        ot.gae()
+        m = ot.update()
+        out[f"metrics_{u}"] = np.array([m[k] for k in METRICS], np.float32)
+        out[f"rng_update_{u}"] = ot.rng_pos()
+        out[f"params_{u}"] = ot.params()
+    ot.close()
+    return out
+
+
 def main():
     np.savez_compressed(os.path.join(HERE, "cartpole_traj_16x32.npz"), **cartpole_traj())
     np.savez_compressed(os.path.join(HERE, "c4_scripted.npz"), **scripted(O.ENV_CONNECT_FOUR, 6, 60, 86, 7, 2, 0, 0.0))
     np.savez_compressed(os.path.join(HERE, "ld_scripted.npz"), **scripted(O.ENV_LIARS_DICE, 4, 80, 270, 49, 4, 120, 0.05))
     np.savez_compressed(os.path.join(HERE, "minibatch_cfgB.npz"), **minibatch())
+    np.savez_compressed(os.path.join(HERE, "w_cfgA.npz"), **cfgA())
 
 
 if __name__ == "__main__":

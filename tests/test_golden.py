@@ -15,7 +15,8 @@ import make_fixtures as MF  # noqa: E402
 FIX = {"cartpole_traj_16x32": MF.cartpole_traj,
        "c4_scripted": lambda: MF.scripted(1, 6, 60, 86, 7, 2, 0, 0.0),
        "ld_scripted": lambda: MF.scripted(2, 4, 80, 270, 49, 4, 120, 0.05),
-       "minibatch_cfgB": MF.minibatch}
+       "minibatch_cfgB": MF.minibatch,
+       "w_cfgA": MF.cfgA}
 
 
 @pytest.mark.parametrize("name", sorted(FIX))

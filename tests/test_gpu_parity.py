@@ -69,10 +69,39 @@ def test_gae_device_bit_exact(T, N):
     assert np.array_equal(ret.cpu().numpy().view(np.uint32), ret_o.view(np.uint32))
 
 
-@pytest.mark.parametrize("P", [2, 3, 4])
-def test_gae_multiplayer_device_bit_exact(P):
+@pytest.mark.parametrize("T,N", [(128, 4096), (37, 1000), (16, 1002)])
+def test_gae_rows_device_bit_exact(T, N):
+    """bppo_gae_rows_device (the bench path's GAE: the [advantage, return] pair of every
+    minibatch row too) = the oracle"""
     torch = _torch()
-    T, N = 64, 2048
+    rng = np.random.default_rng(T + N)
+    r = (rng.random((T, N)) < 0.98).astype(np.float32)
+    d = (rng.random((T, N)) < 0.01).astype(np.float32)
+    v = rng.normal(50, 20, (T, N)).astype(np.float32)
+    lv = rng.normal(50, 20, N).astype(np.float32)
+    adv_o, ret_o = O.compute_gae(r, d, v, lv, 0.99, 0.95)
+    dev = [torch.from_numpy(a).cuda() for a in (r, d, v, lv)]
+    adv = torch.empty((T, N), device="cuda")
+    ret = torch.empty((T, N), device="cuda")
+    pairs = torch.full((T * N, 2), 7.0, device="cuda")
+    st = L.lib().bppo_gae_rows_device(*[t.data_ptr() for t in dev], T, N, 0.99, 0.95, adv.data_ptr(),
+                                      ret.data_ptr(), pairs.data_ptr(), None)
+    if N % 4:
+        assert st == L.ERR_UNSUPPORTED
+        return
+    assert st == 0
+    torch.cuda.synchronize()
+    pw = pairs.cpu().numpy()
+    assert np.array_equal(adv.cpu().numpy().view(np.uint32), adv_o.view(np.uint32))
+    assert np.array_equal(pw[:, 0].view(np.uint32), adv_o.reshape(-1).view(np.uint32))
+    assert np.array_equal(pw[:, 1].view(np.uint32), ret_o.reshape(-1).view(np.uint32))
+
+
+@pytest.mark.parametrize("P,T,N", [(2, 64, 2048), (3, 64, 2048), (4, 64, 2048), (4, 128, 32768), (6, 37, 1000),
+                                   (2, 129, 300), (1, 16, 64)])
+def test_gae_multiplayer_device_bit_exact(P, T, N):
+    """k_gae_mp_seg (T <= 128: T split over the waves of a block) and k_gae_mp (longer T)"""
+    torch = _torch()
     rng = np.random.default_rng(P)
     pl = rng.integers(0, P, (T, N)).astype(np.int32)
     d = (rng.random((T, N)) < 0.05).astype(np.float32)
