@@ -703,357 +703,6 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
 #endif
 }
 
-// ======================================= MFMA minibatch, 16-row tiles (H=64, NL=2) ==
-// The same network and arithmetic as k_minibatch_mfma, re-tiled for occupancy: a
-// wave owns 16 rows on v_mfma_f32_16x16x4_f32 (an exact k-ordered fma chain, like the
-// 32x32x2 form), so its activation tiles are 4 KB each and the accumulators of a
-// layer 16 VGPRs.  12 waves per block (3 per SIMD, <= 168 VGPRs, ~126 KB LDS): while
-// two waves of a SIMD sit in latency-bound VALU/LDS segments (heads, loss, gradient
-// loops), the third keeps the matrix pipe fed.
-//   forward   H1 = relu(X W0 + b0) (K 5 padded to 8), H2 = relu(H1 W1 + b1): k-ordered
-//             chains, bit-identical to the rollout's forward;
-//   heads     lane (row li, chain lg < 3) runs one k-ordered chain: logit 0, logit 1,
-//             value; the loss on lane li;
-//   backward  lane = hidden unit k for the head gradients, dZ2 (the VALU form of the
-//             two-step MFMA chain d0 wp0 -> + d1 wp1 -> + dv wv) with its relu mask, and
-//             dW0 / db0; dZ1 = dZ2 W1^T and dW1 += H1^T dZ2 on the MFMA (16 + 64).
-// LDS images are row-padded, so every address is one lane base + an immediate: the
-// activation tiles at stride 68 (the MFMA A reads -- 16 rows x 4 consecutive
-// columns -- and the C/D epilogue stores are conflict-free; the weight-gradient
-// reads -- 4 rows x 16 columns -- 4-way), W1 at stride 72 (2-way both as the layer-2
-// B operand W1[k][n] and as the dZ1 B operand W1[n][k]).
-namespace m16 {
-constexpr int H = 64, TR = 16, WAVES = 12, RT = 68, RW = 72;
-__device__ __forceinline__ int at(int r, int c) { return r * RT + c; }
-__device__ __forceinline__ int aw(int r, int c) { return r * RW + c; }
-struct Params {
-    uint64_t exp2tab[32];
-    double linvc[16], llogc[16];
-    float W1[H * RW];    // [k][o], row stride 72
-    float W0[8 * H];     // [d][k], d = 5..7 zero pad rows
-    float b0[H], b1[H];
-    float HW[4][H];      // head chains: Wp[2k], Wp[2k + 1], Wv[k], 0
-    float bp[2], bv[2];
-    __device__ __forceinline__ float expf(float x) const { return bppo_math::expf_glibc_tab(x, exp2tab); }
-    __device__ __forceinline__ float logf(float x) const { return bppo_math::logf_glibc_tab(x, linvc, llogc); }
-};
-// a tile's 16 gathered rows, written straight from HBM by LDS-DMA loads (lane-linear)
-struct Rows {
-    float A0[TR * 4];    // obs 0..3
-    float A1[TR * 4];    // obs 4, action (int bits), old log-prob, old value
-    float adv[TR], ret[TR];
-};
-struct Wave {
-    float T1[TR * RT];   // H1 [row][k]
-    float T2[TR * RT];   // H2 -> dZ2 -> dZ1 [row][k]
-    Rows rb[2];          // this tile's rows and the next tile's (in flight)
-    float dl[TR * 4];    // dL/d(logit0, logit1, value), 0
-    float MET[TR * 16];  // per-row-lane sums: the 11 metrics, then the head-bias gradients
-};
-constexpr size_t LDS = sizeof(Params) + WAVES * sizeof(Wave);
-static_assert(LDS <= 160 * 1024, "16-row minibatch kernel LDS over the gfx950 limit");
-static_assert(sizeof(Params) % 16 == 0 && sizeof(Wave) % 16 == 0, "float4 alignment of the LDS images");
-
-__device__ __forceinline__ void load_params(Params &S, const float *__restrict__ P) {
-    constexpr CpOffsets O = cp_offsets<64, 2>();
-    for (int i = threadIdx.x; i < H * H; i += blockDim.x) S.W1[aw(i / H, i % H)] = P[O.w1 + i];
-    for (int i = threadIdx.x; i < 8 * H; i += blockDim.x) S.W0[i] = i < 5 * H ? P[O.w0 + i] : 0.0f;
-    for (int i = threadIdx.x; i < H; i += blockDim.x) {
-        S.b0[i] = P[O.b0 + i]; S.b1[i] = P[O.b1 + i];
-        S.HW[0][i] = P[O.wp + 2 * i]; S.HW[1][i] = P[O.wp + 2 * i + 1]; S.HW[2][i] = P[O.wv + i]; S.HW[3][i] = 0.0f;
-    }
-    if (threadIdx.x < 32) S.exp2tab[threadIdx.x] = bppo_math::kExp2fTab[threadIdx.x];
-    if (threadIdx.x < 16) {
-        S.linvc[threadIdx.x] = bppo_math::kLogfInvc[threadIdx.x];
-        S.llogc[threadIdx.x] = bppo_math::kLogfLogc[threadIdx.x];
-    }
-    if (threadIdx.x < 2) S.bp[threadIdx.x] = P[O.bp + threadIdx.x];
-    if (threadIdx.x == 0) { S.bv[0] = P[O.bv]; S.bv[1] = 0.0f; }
-}
-}  // namespace m16
-
-typedef float f32x4_t __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) void lds_void_t;
-typedef __attribute__((address_space(1))) void gbl_void_t;
-
-__global__ void __launch_bounds__(64 * m16::WAVES, 1) k_minibatch_mfma16(MbArgs g) {
-    using namespace m16;
-    constexpr CpOffsets O = cp_offsets<64, 2>();
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    Params &S = *reinterpret_cast<Params *>(smem);
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    Wave &B = reinterpret_cast<Wave *>(smem + sizeof(Params) / 4)[wv];
-    load_params(S, g.params);
-    for (int i = lane; i < TR * 16; i += 64) B.MET[i] = i % 16 == M_VEMAX ? -INFINITY : 0.0f;
-    __syncthreads();
-
-    const int gwave = blockIdx.x * WAVES + wv, nwaves = gridDim.x * WAVES;
-    const float mean = g.mb_stats[0], denom = g.mb_stats[1] + 1e-8f;
-    f32x4_t dW1[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-#pragma unroll
-        for (int j = 0; j < 4; j++) dW1[i][j] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
-    float gW0[5] = {0, 0, 0, 0, 0}, gb0 = 0, gb1 = 0, gP0 = 0, gP1 = 0, gV = 0;
-
-    // gather (ppo.rs:1833-1857): shuffled index two tiles ahead; the rows of the next
-    // tile DMA'd into the other row buffer while this tile computes (no VGPRs held)
-    const uint32_t stride = (uint32_t)nwaves * TR;
-    auto idx_of = [&](uint32_t b) -> uint32_t {
-        const uint32_t rr = b + (lane & 15);
-        return (lane < TR && rr < g.n) ? g.perm[g.start + rr] : 0xFFFFFFFFu;
-    };
-    auto issue_rows = [&](Rows &dst, uint32_t idx) {
-        if (lane < TR) {
-            const size_t i = idx != 0xFFFFFFFFu ? idx : 0;   // an absent row reads row 0; its dl is zeroed
-            __builtin_amdgcn_global_load_lds((gbl_void_t *)(g.rowA + i * 2), (lds_void_t *)dst.A0, 16, 0, 0);
-            __builtin_amdgcn_global_load_lds((gbl_void_t *)(g.rowA + i * 2 + 1), (lds_void_t *)dst.A1, 16, 0, 0);
-            __builtin_amdgcn_global_load_lds((gbl_void_t *)(&g.rowB[i].x), (lds_void_t *)dst.adv, 4, 0, 0);
-            __builtin_amdgcn_global_load_lds((gbl_void_t *)(&g.rowB[i].y), (lds_void_t *)dst.ret, 4, 0, 0);
-        }
-    };
-    uint32_t idx_next = idx_of((uint32_t)gwave * TR + stride);
-    issue_rows(B.rb[0], idx_of((uint32_t)gwave * TR));
-    int buf = 0;
-    for (uint32_t base = (uint32_t)gwave * TR; base < g.n; base += stride) {
-        // this tile's rows (DMA'd one tile ago) and idx_next have landed
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        issue_rows(B.rb[buf ^ 1], idx_next);
-        idx_next = idx_of(base + 2 * stride);
-        const Rows &R = B.rb[buf];
-        buf ^= 1;
-        // lane coordinates from an opaque copy each iteration (addresses = one base
-        // VGPR + immediates, not dozens of hoisted loop-invariant registers)
-        int ln_ = lane;
-        asm volatile("" : "+v"(ln_));
-        const int li = ln_ & 15, lg = ln_ >> 4;
-        const bool valid = lg == 0 && base + li < g.n;
-        // ---- layer 1 (K = 5 padded to 8: two k-steps, pad operands 0)
-        f32x4_t acc[4];
-#pragma unroll
-        for (int nb = 0; nb < 4; nb++) acc[nb] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-        for (int s = 0; s < 2; s++) {
-            const float av = s == 0 ? R.A0[li * 4 + lg] : (lg == 0 ? R.A1[li * 4] : 0.0f);
-#pragma unroll
-            for (int nb = 0; nb < 4; nb++)
-                acc[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, S.W0[(4 * s + lg) * H + 16 * nb + li], acc[nb], 0, 0, 0);
-        }
-#pragma unroll
-        for (int nb = 0; nb < 4; nb++) {
-            const float bb = S.b0[16 * nb + li];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const float v = __fadd_rn(acc[nb][j], bb);
-                B.T1[at(4 * lg + j, 16 * nb + li)] = v > 0.0f ? v : 0.0f;
-            }
-        }
-        wave_sync();
-        // ---- layer 2 (K = 64: 16 k-steps)
-#pragma unroll
-        for (int nb = 0; nb < 4; nb++) acc[nb] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll 4
-        for (int s = 0; s < 16; s++) {
-            const float av = B.T1[at(li, 4 * s + lg)];
-#pragma unroll
-            for (int nb = 0; nb < 4; nb++)
-                acc[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, S.W1[aw(4 * s + lg, 16 * nb + li)], acc[nb], 0, 0, 0);
-        }
-#pragma unroll
-        for (int nb = 0; nb < 4; nb++) {
-            const float bb = S.b1[16 * nb + li];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const float v = __fadd_rn(acc[nb][j], bb);
-                B.T2[at(4 * lg + j, 16 * nb + li)] = v > 0.0f ? v : 0.0f;
-            }
-        }
-        wave_sync();
-        // ---- heads: lane (li, lg) runs chain lg of row li (lg = 3: a zero chain)
-        {
-            float ch = 0.0f;
-            const float *hw = S.HW[lg];
-#pragma unroll 4
-            for (int q = 0; q < 16; q++) {
-                const float4 h4 = *reinterpret_cast<const float4 *>(&B.T2[at(li, 4 * q)]);
-                const float4 w4 = *reinterpret_cast<const float4 *>(&hw[4 * q]);
-                ch = __builtin_fmaf(h4.x, w4.x, ch);
-                ch = __builtin_fmaf(h4.y, w4.y, ch);
-                ch = __builtin_fmaf(h4.z, w4.z, ch);
-                ch = __builtin_fmaf(h4.w, w4.w, ch);
-            }
-            const float l0 = __shfl(ch, li, 64), l1 = __shfl(ch, li + 16, 64), vv = __shfl(ch, li + 32, 64);
-            if (lg == 0) {
-                const float4 rd = *reinterpret_cast<const float4 *>(&R.A1[li * 4]);
-                const int a = __float_as_int(rd.y);
-                const float olp = rd.z, A = R.adv[li], Rt = R.ret[li], ov = g.clip_value ? rd.w : 0.0f;
-                const float lg0 = __fadd_rn(l0, S.bp[0]), lg1 = __fadd_rn(l1, S.bp[1]), v = __fadd_rn(vv, S.bv[0]);
-                const float mx = lg0 > lg1 ? lg0 : lg1;
-                const float e0 = S.expf(__fsub_rn(lg0, mx)), e1 = S.expf(__fsub_rn(lg1, mx));
-                const float lse = S.logf(__fadd_rn(e0, e1));
-                const float ls0 = __fsub_rn(__fsub_rn(lg0, mx), lse);
-                const float ls1 = __fsub_rn(__fsub_rn(lg1, mx), lse);
-                const float p0 = S.expf(ls0), p1 = S.expf(ls1);
-                const float An = __fdiv_rn(__fsub_rn(A, mean), denom);   // utils.rs:88
-                const float Hn = -__fadd_rn(__fmul_rn(p0, ls0), __fmul_rn(p1, ls1));
-                const float newlp = a == 1 ? ls1 : ls0;
-                const float log_ratio = __fsub_rn(newlp, olp);
-                const float ratio = S.expf(log_ratio);
-                const float na = -An;
-                const float pl1 = __fmul_rn(na, ratio);
-                const float rc = ratio < g.lo ? g.lo : (ratio > g.hi ? g.hi : ratio);
-                const float pl2 = __fmul_rn(na, rc);
-                const bool rhs = pl1 < pl2;
-                const float pl = rhs ? pl2 : pl1;
-                float vl, dvl;
-                if (g.clip_value) {
-                    const float dlt = __fsub_rn(v, ov);
-                    const float dc = dlt < -g.ceps ? -g.ceps : (dlt > g.ceps ? g.ceps : dlt);
-                    const float vc = __fadd_rn(ov, dc);
-                    const float q1 = __fmul_rn(__fsub_rn(v, Rt), __fsub_rn(v, Rt));
-                    const float q2 = __fmul_rn(__fsub_rn(vc, Rt), __fsub_rn(vc, Rt));
-                    if (q1 < q2) { vl = q2; dvl = (dlt >= -g.ceps && dlt <= g.ceps) ? 2.0f * __fsub_rn(vc, Rt) : 0.0f; }
-                    else { vl = q1; dvl = 2.0f * __fsub_rn(v, Rt); }
-                } else {
-                    vl = __fmul_rn(__fsub_rn(v, Rt), __fsub_rn(v, Rt));
-                    dvl = 2.0f * __fsub_rn(v, Rt);
-                }
-                const float g_ratio = (!rhs || (ratio >= g.lo && ratio <= g.hi)) ? -An * g.inv_mb : 0.0f;
-                const float g_lr = g_ratio * ratio;
-                const float ec = g.ent_coef * g.inv_mb;
-                float dl0 = g_lr * ((a == 0 ? 1.0f : 0.0f) - p0) + ec * p0 * (ls0 + Hn);
-                float dl1 = g_lr * ((a == 1 ? 1.0f : 0.0f) - p1) + ec * p1 * (ls1 + Hn);
-                float dv = g.value_coef * 0.5f * g.inv_mb * dvl;
-                float *mt = B.MET + li * 16;
-                float4 m0 = *reinterpret_cast<const float4 *>(mt), m1 = *reinterpret_cast<const float4 *>(mt + 4);
-                float4 m2 = *reinterpret_cast<const float4 *>(mt + 8), m3 = *reinterpret_cast<const float4 *>(mt + 12);
-                if (!valid) { dl0 = dl1 = dv = 0.0f; }
-                else {
-                    const float ve = fabsf(__fsub_rn(v, Rt));
-                    m0.x += pl; m0.y += vl; m0.z += Hn; m0.w += (ratio - 1.0f) - log_ratio;
-                    m1.x += fabsf(ratio - 1.0f) > g.ceps ? 1.0f : 0.0f;
-                    m1.y += v; m1.z += Rt; m1.w += ve; m2.x += ve * ve; m2.y = fmaxf(m2.y, ve);
-                    m2.z += 1.0f;
-                }
-                m2.w += dl0; m3.x += dl1; m3.y += dv;
-                *reinterpret_cast<float4 *>(mt) = m0; *reinterpret_cast<float4 *>(mt + 4) = m1;
-                *reinterpret_cast<float4 *>(mt + 8) = m2; *reinterpret_cast<float4 *>(mt + 12) = m3;
-                *reinterpret_cast<float4 *>(&B.dl[li * 4]) = make_float4(dl0, dl1, dv, 0.0f);
-            }
-        }
-        wave_sync();
-        // ---- lane = hidden unit k: head weight gradients, dZ2 = [dl0 dl1 dv] [Wp0; Wp1; Wv]
-        // masked by relu'(H2) (over H2 in place), db1
-        const float wp0k = S.HW[0][ln_], wp1k = S.HW[1][ln_], wvk = S.HW[2][ln_];
-#pragma unroll 4
-        for (int r = 0; r < TR; r++) {
-            const int ad = at(r, ln_);
-            const float hv = B.T2[ad];
-            const float4 d = *reinterpret_cast<const float4 *>(&B.dl[r * 4]);
-            gP0 = __builtin_fmaf(hv, d.x, gP0);
-            gP1 = __builtin_fmaf(hv, d.y, gP1);
-            gV = __builtin_fmaf(hv, d.z, gV);
-            float t = __fmul_rn(d.x, wp0k);
-            t = __builtin_fmaf(d.y, wp1k, t);
-            t = __builtin_fmaf(d.z, wvk, t);
-            const float dz = hv > 0.0f ? t : 0.0f;
-            gb1 += dz;
-            B.T2[ad] = dz;
-        }
-        wave_sync();
-        // ---- dZ1 = dZ2 W1^T (16 k-steps) with dW1 += H1^T dZ2 (4 k-steps over the 16
-        // rows) spread one (ib) row of dW1 blocks per dZ1 step
-#pragma unroll
-        for (int nb = 0; nb < 4; nb++) acc[nb] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll 1
-        for (int ks = 0; ks < 4; ks++) {
-#pragma unroll
-            for (int ib = 0; ib < 4; ib++) {
-                const int s = 4 * ks + ib;
-                const float av = B.T2[at(li, 4 * s + lg)];
-#pragma unroll
-                for (int nb = 0; nb < 4; nb++)
-                    acc[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, S.W1[aw(16 * nb + li, 4 * s + lg)], acc[nb], 0, 0, 0);
-                const float a1 = B.T1[at(4 * ks + lg, 16 * ib + li)];
-#pragma unroll
-                for (int jb = 0; jb < 4; jb++)
-                    dW1[ib][jb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, B.T2[at(4 * ks + lg, 16 * jb + li)],
-                                                                       dW1[ib][jb], 0, 0, 0);
-            }
-        }
-#pragma unroll
-        for (int nb = 0; nb < 4; nb++)
-#pragma unroll
-            for (int j = 0; j < 4; j++) B.T2[at(4 * lg + j, 16 * nb + li)] = acc[nb][j];
-        wave_sync();
-        // ---- lane = hidden unit k: dZ1 masked by relu'(H1), db0, dW0 += X^T dZ1
-#pragma unroll 4
-        for (int r = 0; r < TR; r++) {
-            const int ad = at(r, ln_);
-            const float dz = B.T1[ad] > 0.0f ? B.T2[ad] : 0.0f;
-            gb0 += dz;
-            const float4 x = *reinterpret_cast<const float4 *>(&R.A0[r * 4]);
-            const float x4 = R.A1[r * 4];
-            gW0[0] = __builtin_fmaf(x.x, dz, gW0[0]);
-            gW0[1] = __builtin_fmaf(x.y, dz, gW0[1]);
-            gW0[2] = __builtin_fmaf(x.z, dz, gW0[2]);
-            gW0[3] = __builtin_fmaf(x.w, dz, gW0[3]);
-            gW0[4] = __builtin_fmaf(x4, dz, gW0[4]);
-        }
-        wave_sync();
-    }
-    // ---- the block's 12 wave rows summed in wave order in LDS (the tiles' space),
-    // then one slab row per block
-    // lane = metric slot: the row lanes' partial sums in lane order (max for VEMAX)
-    float msum = 0.0f;
-    if (lane < 14) {
-        msum = lane == M_VEMAX ? -INFINITY : 0.0f;
-        for (int r = 0; r < TR; r++) {
-            const float x = B.MET[r * 16 + lane];
-            msum = lane == M_VEMAX ? fmaxf(msum, x) : msum + x;
-        }
-    }
-    const float s_pl = __shfl(msum, M_PL, 64), s_vl = __shfl(msum, M_VL, 64), s_h = __shfl(msum, M_H, 64);
-    const float s_kl = __shfl(msum, M_KL, 64), s_cf = __shfl(msum, M_CF, 64), s_v = __shfl(msum, M_V, 64);
-    const float s_r = __shfl(msum, M_R, 64), s_ve = __shfl(msum, M_VE, 64), s_ve2 = __shfl(msum, M_VE2, 64);
-    const float s_mx = __shfl(msum, M_VEMAX, 64), s_n = __shfl(msum, M_N, 64);
-    const float s_bp0 = __shfl(msum, 11, 64), s_bp1 = __shfl(msum, 12, 64), s_bv = __shfl(msum, 13, 64);
-    const int W_ = g.np + NUM_M;
-    const int li = lane & 15, lg = lane >> 4;
-    float *row = smem + sizeof(Params) / 4;
-    __syncthreads();
-    for (int w = 0; w < WAVES; w++) {
-        if (wv == w) {
-            const bool first = w == 0;
-            auto put = [&](int p, float v) { row[p] = first ? v : row[p] + v; };
-#pragma unroll
-            for (int d = 0; d < 5; d++) put(O.w0 + d * H + lane, gW0[d]);
-            put(O.b0 + lane, gb0);
-            put(O.b1 + lane, gb1);
-            put(O.wp + 2 * lane, gP0);
-            put(O.wp + 2 * lane + 1, gP1);
-            put(O.wv + lane, gV);
-            // dW1[k][o]: block (ib, jb) register j of lane (lg, li) = D[4 lg + j][li]
-#pragma unroll
-            for (int ib = 0; ib < 4; ib++)
-#pragma unroll
-                for (int jb = 0; jb < 4; jb++)
-#pragma unroll
-                    for (int j = 0; j < 4; j++) put(O.w1 + (16 * ib + 4 * lg + j) * H + 16 * jb + li, dW1[ib][jb][j]);
-            if (lane == 0) {
-                put(O.bp, s_bp0); put(O.bp + 1, s_bp1); put(O.bv, s_bv);
-                float *mm = row + g.np;
-                put(g.np + M_PL, s_pl); put(g.np + M_VL, s_vl); put(g.np + M_H, s_h); put(g.np + M_KL, s_kl);
-                put(g.np + M_CF, s_cf); put(g.np + M_V, s_v); put(g.np + M_R, s_r); put(g.np + M_VE, s_ve);
-                put(g.np + M_VE2, s_ve2); put(g.np + M_N, s_n);
-                mm[M_VEMAX] = first ? s_mx : fmaxf(mm[M_VEMAX], s_mx);
-            }
-        }
-        __syncthreads();
-    }
-    for (int p = tid; p < W_; p += blockDim.x) g.slab[(size_t)blockIdx.x * W_ + p] = row[p];
-}
-
 // fixed-order reduction of the wave partials, grad[p] = sum_w slab[w][p]: SLAB_GROUPS
 // row groups each summed in f64 in row order, then the groups in order.
 constexpr int SLAB_GROUPS = 32;
@@ -1455,11 +1104,6 @@ bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_
             return BPPO_ERR_UNSUPPORTED;
         }
         c->slab_used = blocks;
-        static int mb16 = -1;
-        if (mb16 < 0) mb16 = getenv("BPPO_MB16") ? atoi(getenv("BPPO_MB16")) : 0;
-        if (mb16)
-            hipLaunchKernelGGL(k_minibatch_mfma16, dim3(blocks), dim3(64 * m16::WAVES), m16::LDS, c->stream, g);
-        else
         hipLaunchKernelGGL(k_minibatch_mfma, dim3(blocks), dim3(64 * mmb::WAVES), mmb::LDSB, c->stream, g);
 #ifdef BPPO_MB_STAMPS
         {   // mean per-wave cycles per segment, accumulated over launches; printed every 16
