@@ -230,17 +230,24 @@ def model_record(cfg, params):
         from .host import conv_channels
         ch, ks = conv_channels(cfg), cfg["kernel_size"]
         nc, nf = len(ch), cfg["cnn_num_fc_layers"]
-        conv = []
-        for i, (W, b) in enumerate(lin[:nc]):
-            cin = W.shape[0] // (ks * ks)
-            conv.append({"weight": {"id": _param_id(f"conv_layers.{i}.weight"),
-                                    "param": _tensor(W.reshape(-1).reshape(ch[i], cin, ks, ks))},
-                         "bias": {"id": _param_id(f"conv_layers.{i}.bias"), "param": _tensor(b)}})
-        item = {"Cnn": {"conv_layers": conv,
+
+        def convs(lins, name):
+            out = []
+            for i, (W, b) in enumerate(lins):
+                cin = W.shape[0] // (ks * ks)
+                out.append({"weight": {"id": _param_id(f"{name}.{i}.weight"),
+                                       "param": _tensor(W.reshape(-1).reshape(ch[i], cin, ks, ks))},
+                            "bias": {"id": _param_id(f"{name}.{i}.bias"), "param": _tensor(b)}})
+            return out
+        # record order (cnn.rs:24-50): conv, fc, critic conv, critic fc (split_networks), heads
+        t = nc + nf if cfg.get("split_networks") else 0
+        item = {"Cnn": {"conv_layers": convs(lin[:nc], "conv_layers"),
                         "fc_layers": [_linear(W, b, f"fc_layers.{i}") for i, (W, b) in enumerate(lin[nc:nc + nf])],
-                        "critic_conv_layers": [], "critic_fc_layers": [],
-                        "policy_head": _linear(*lin[nc + nf], "policy_head"),
-                        "value_head": _linear(*lin[nc + nf + 1], "value_head")}}
+                        "critic_conv_layers": convs(lin[nc + nf:nc + nf + nc], "critic_conv_layers") if t else [],
+                        "critic_fc_layers": [_linear(W, b, f"critic_fc_layers.{i}")
+                                             for i, (W, b) in enumerate(lin[2 * nc + nf:nc + nf + t])] if t else [],
+                        "policy_head": _linear(*lin[nc + nf + t], "policy_head"),
+                        "value_head": _linear(*lin[nc + nf + t + 1], "value_head")}}
         return {"metadata": BURN_METADATA, "item": item}
     if cfg["network_type"] == "ctde":
         nc = cfg["critic_num_hidden"] or nh
@@ -261,10 +268,9 @@ def model_record(cfg, params):
 
 def _linears_in_order(item):
     (kind, rec), = item.items()
-    if kind == "Cnn":
-        if rec["critic_conv_layers"] or rec["critic_fc_layers"]:
-            raise ValueError("split_networks CNN checkpoints are not supported by the device path")
-        return rec["conv_layers"] + rec["fc_layers"] + [rec["policy_head"], rec["value_head"]]
+    if kind == "Cnn":      # record order: conv, fc, critic conv, critic fc (split_networks), heads
+        return (rec["conv_layers"] + rec["fc_layers"] + rec["critic_conv_layers"] + rec["critic_fc_layers"] +
+                [rec["policy_head"], rec["value_head"]])
     if kind == "Ctde":
         seq = rec["actor_layers"] + [rec["policy_head"]] + rec["critic_layers"] + [rec["value_head"]]
     elif kind == "Mlp":      # record order: layers, critic_layers (split_networks), policy, value

@@ -162,6 +162,9 @@ def layer_shapes(c):
         i = H * W * cin + (obs - H * W * C0)
         for _ in range(c["cnn_num_fc_layers"]):
             shapes.append((i, c["cnn_fc_hidden_size"])); gains.append(hg); i = c["cnn_fc_hidden_size"]
+        if c.get("split_networks"):        # cnn.rs:116-135: the critic's own conv stack and FC layers
+            n_trunk = len(shapes)
+            shapes += shapes[:n_trunk]; gains += gains[:n_trunk]
         shapes.append((i, act)); gains.append(0.01)
         shapes.append((i, 1)); gains.append(1.0)
         return shapes, gains

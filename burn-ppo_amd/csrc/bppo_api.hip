@@ -36,7 +36,7 @@ NetLayout make_layout(const bppo_config &c, int obs_dim, int priv_dim, int act_d
     NetLayout L;
     // split_networks (mlp.rs:100-130): a second trunk of num_hidden x hidden_size on obs,
     // i.e. the CTDE structure with no privileged input (ctde.rs ignores the flag)
-    const bool split = c.split_networks && !c.ctde && !c.cnn;
+    const bool split = c.split_networks && !c.ctde;
     L.ctde = c.ctde || split; L.relu = c.relu;
     auto add = [&](int in, int out) {
         int i = L.n_layers++;
@@ -67,10 +67,18 @@ NetLayout make_layout(const bppo_config &c, int obs_dim, int priv_dim, int act_d
         L.n_actor_hidden = c.num_hidden;
     }
     L.policy = add(in, act_dim);
-    if (L.ctde) {
+    if (L.ctde && c.cnn) {
+        // split CNN (cnn.rs:116-135): the critic's own conv stack (same shapes) and FC layers
+        L.critic_first = L.n_layers;
+        for (int l = 0; l < L.n_conv; l++) add(L.in[l], L.out[l]);
+        L.critic_fc0 = L.n_layers;
+        int cin = L.fdim;
+        for (int l = 0; l < c.cnn_num_fc_layers; l++) { add(cin, c.cnn_fc_hidden_size); cin = c.cnn_fc_hidden_size; }
+        L.value = add(cin, 1);
+    } else if (L.ctde) {
         int cin = split ? obs_dim : priv_dim + obs_dim;
         const int nc = split ? c.num_hidden : c.critic_num_hidden, wc = split ? c.hidden_size : c.critic_hidden_size;
-        L.critic_first = L.n_layers;
+        L.critic_first = L.critic_fc0 = L.n_layers;
         for (int l = 0; l < nc; l++) { add(cin, wc); cin = wc; }
         L.value = add(cin, 1);
     } else {
@@ -216,10 +224,6 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     // width and depth; split_networks) runs on the GEMM engine path like the other envs
     c->wide = cfg->env_kind != BPPO_ENV_CARTPOLE || !cartpole_fused_net(*cfg);
     if (c->wide && !cfg->ctde) c->G = 0;
-    if (cfg->split_networks && cfg->cnn) {
-        c->err = "split_networks with network_type = \"cnn\" is not on the device path";
-        return BPPO_ERR_UNSUPPORTED;
-    }
     // num_hidden = 0 would feed obs into heads of hidden_size inputs (mlp.rs:121-125), a
     // shape panic in the reference unless obs_dim == hidden_size
     if (!cfg->cnn && (cfg->hidden_size < 1 || cfg->num_hidden < 1 ||
@@ -238,6 +242,8 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
         }
         for (int l = 0; l < cfg->num_conv_layers; l++)
             if (cfg->conv_channels[l < 4 ? l : 3] < 1) { c->err = "conv_channels must be positive"; return BPPO_ERR_ARG; }
+        const int layers = (cfg->split_networks ? 2 : 1) * (cfg->num_conv_layers + cfg->cnn_num_fc_layers) + 2;
+        if (layers > 16) { c->err = "CNN: at most 16 layers in all (conv + FC + heads)"; return BPPO_ERR_UNSUPPORTED; }
     }
     c->net = make_layout(*cfg, c->D, c->G, c->A);
     const size_t np = c->net.n_params;

@@ -23,15 +23,22 @@ struct NetLayout {
     size_t w[16], b[16];
     int n_actor_hidden = 0;       // hidden layers of the actor / shared backbone
     int policy = 0, value = 0;    // layer indices of the heads
-    int critic_first = -1;        // critic hidden layers [critic_first, value) (CTDE, split_networks)
+    int critic_first = -1;        // critic layers [critic_first, value) (CTDE, split_networks)
+    int critic_fc0 = -1;          // its first FC layer (split CNN: after the critic's own conv stack)
     int ctde = 0, relu = 1;       // ctde: two trunks (CTDE, or split_networks with the critic on obs)
     int rec[16];                  // Burn record position of layer l (split_networks: actor, critic, heads)
     size_t n_params = 0;
     // CNN (network/cnn.rs): layers [0, n_conv) are the conv layers (in = Cin k k,
     // out = Cout; weight [Cout][Cin][k][k] then bias in Burn record order), then the
-    // FC layers [n_conv, n_actor_hidden), policy, value
+    // FC layers [n_conv, n_actor_hidden), policy, value; split_networks (cnn.rs:116-135)
+    // adds the critic's conv stack [critic_first, critic_fc0) and FC layers [critic_fc0, value)
     int n_conv = 0, ksize = 3, H = 0, W = 0, C = 0, E = 0, fdim = 0;
     int conv_cin[4] = {0, 0, 0, 0};
+    // first layer of conv stack s (0: actor / shared, 1: the split critic's)
+    int conv_base(int s) const { return s ? critic_first : 0; }
+    bool is_conv(int l) const {
+        return n_conv && (l < n_conv || (critic_fc0 > critic_first && l >= critic_first && l < critic_fc0));
+    }
 };
 NetLayout make_layout(const bppo_config &c, int obs_dim, int priv_dim, int act_dim);
 
@@ -331,10 +338,13 @@ struct bppo_ctx {
     // CNN actor-critic (cnn.hip): conv outputs (post-relu, NHWC rows) per conv layer,
     // im2col scratch, the flattened NCHW features + extra [rows][fdim], backward
     // scratch, conv weights packed [k k Cin][Cout] (GEMM operand) and their gradient
-    float *d_cnn_y[4] = {nullptr, nullptr, nullptr, nullptr};
-    float *d_cnn_a = nullptr, *d_cnn_f = nullptr, *d_cnn_dy[2] = {nullptr, nullptr};
+    // -- per conv stack s (0: actor / shared, 1: the split_networks critic)
+    float *d_cnn_y[2][4] = {};
+    float *d_cnn_f[2] = {nullptr, nullptr};
+    float *d_cnn_a = nullptr, *d_cnn_dy[2] = {nullptr, nullptr};
     float *d_cnn_wt = nullptr, *d_cnn_owt = nullptr, *d_cnn_dwt = nullptr;
-    size_t cnn_wt_off[4] = {0, 0, 0, 0};
+    size_t cnn_wt_off[2][4] = {};
+    int cnn_stacks = 1;
     // PopArt value normalization (popart.hip, normalization.rs:262-366): running
     // statistics on the host, normalized update buffers, the update's views
     double pa_mean = 0.0, pa_m2 = 0.0, pa_count = 0.0, pa_eps = 1e-4;
@@ -427,8 +437,8 @@ bppo_status wide_forward_actor(bppo_ctx *c, int rows, const float *xc, int ldxc,
 bppo_status cnn_alloc(bppo_ctx *c);
 void cnn_free(bppo_ctx *c);
 bppo_status cnn_pack(bppo_ctx *c, const float *params, float *wt);
-bppo_status cnn_features(bppo_ctx *c, int rows, const float *x, int ldx, const float *params, const float *wt);
-bppo_status cnn_backward(bppo_ctx *c, int rows, const float *x, int ldx, float *dF, float *grad);
+bppo_status cnn_features(bppo_ctx *c, int s, int rows, const float *x, int ldx, const float *params, const float *wt);
+bppo_status cnn_backward(bppo_ctx *c, int s, int rows, const float *x, int ldx, float *dF, float *grad);
 // opponent pool (opponents.hip)
 bool opp_active(const bppo_ctx *c);
 bppo_status opp_alloc(bppo_ctx *c);

@@ -19,6 +19,9 @@
 //             atomics) times relu'(input).
 // Activations are NHWC rows ([b*HW + hw][channel]), so each conv is a plain
 // row-major GEMM and its output feeds the next im2col directly.
+// split_networks (cnn.rs:116-135, 264-302): a second conv stack (s = 1, layers
+// [critic_first, critic_fc0)) on the same spatial input feeds the critic's FC layers;
+// every function below takes the stack index s.
 #include "bppo_internal.h"
 #include "bppo_gemm.h"
 #include <algorithm>
@@ -122,16 +125,19 @@ bppo_status cnn_alloc(bppo_ctx *c) {
     const NetLayout &n = c->net;
     const size_t HW = (size_t)n.H * n.W, R = (size_t)c->rows_max * HW;
     size_t kmax = 0, cmax = 0, wt = 0;
-    for (int l = 0; l < n.n_conv; l++) {
-        kmax = std::max(kmax, (size_t)n.in[l]);
-        cmax = std::max(cmax, (size_t)std::max(n.out[l], n.conv_cin[l]));
-        c->cnn_wt_off[l] = wt;
-        wt += (size_t)n.in[l] * n.out[l];
-        CHIP(c, hipMalloc((void **)&c->d_cnn_y[l], R * n.out[l] * 4));
+    c->cnn_stacks = n.critic_fc0 > n.critic_first ? 2 : 1;
+    for (int s = 0; s < c->cnn_stacks; s++) {
+        for (int l = 0; l < n.n_conv; l++) {
+            kmax = std::max(kmax, (size_t)n.in[l]);
+            cmax = std::max(cmax, (size_t)std::max(n.out[l], n.conv_cin[l]));
+            c->cnn_wt_off[s][l] = wt;
+            wt += (size_t)n.in[l] * n.out[l];
+            CHIP(c, hipMalloc((void **)&c->d_cnn_y[s][l], R * n.out[l] * 4));
+        }
+        CHIP(c, hipMalloc((void **)&c->d_cnn_f[s], (size_t)c->rows_max * n.fdim * 4));
     }
     const size_t dy = std::max(R * cmax, (size_t)c->rows_max * n.fdim);
     CHIP(c, hipMalloc((void **)&c->d_cnn_a, R * kmax * 4));
-    CHIP(c, hipMalloc((void **)&c->d_cnn_f, (size_t)c->rows_max * n.fdim * 4));
     CHIP(c, hipMalloc((void **)&c->d_cnn_dy[0], dy * 4));
     CHIP(c, hipMalloc((void **)&c->d_cnn_dy[1], dy * 4));
     CHIP(c, hipMalloc((void **)&c->d_cnn_wt, wt * 4));
@@ -141,50 +147,54 @@ bppo_status cnn_alloc(bppo_ctx *c) {
 }
 
 void cnn_free(bppo_ctx *c) {
-    void *p[] = {c->d_cnn_y[0], c->d_cnn_y[1], c->d_cnn_y[2], c->d_cnn_y[3], c->d_cnn_a, c->d_cnn_f,
-                 c->d_cnn_dy[0], c->d_cnn_dy[1], c->d_cnn_wt, c->d_cnn_owt, c->d_cnn_dwt};
+    for (int s = 0; s < 2; s++) {
+        for (float *q : c->d_cnn_y[s]) if (q) (void)hipFree(q);
+        if (c->d_cnn_f[s]) (void)hipFree(c->d_cnn_f[s]);
+    }
+    void *p[] = {c->d_cnn_a, c->d_cnn_dy[0], c->d_cnn_dy[1], c->d_cnn_wt, c->d_cnn_owt, c->d_cnn_dwt};
     for (void *q : p) if (q) (void)hipFree(q);
 }
 
 // the conv weights of `params` as GEMM operands [K][Cout] (after every params change)
 bppo_status cnn_pack(bppo_ctx *c, const float *params, float *wt) {
     const NetLayout &n = c->net;
-    for (int l = 0; l < n.n_conv; l++) {
-        const int R = n.out[l], Cc = n.in[l];   // [Cout][K] -> [K][Cout]
-        hipLaunchKernelGGL(k_cnn_transpose, dim3((R * Cc + 255) / 256), dim3(256), 0, c->stream, R, Cc,
-                           params + n.w[l], wt + c->cnn_wt_off[l]);
-    }
+    for (int s = 0; s < c->cnn_stacks; s++)
+        for (int l = 0; l < n.n_conv; l++) {
+            const int R = n.out[l], Cc = n.in[l], lg = n.conv_base(s) + l;   // [Cout][K] -> [K][Cout]
+            hipLaunchKernelGGL(k_cnn_transpose, dim3((R * Cc + 255) / 256), dim3(256), 0, c->stream, R, Cc,
+                               params + n.w[lg], wt + c->cnn_wt_off[s][l]);
+        }
     CHIP(c, hipGetLastError());
     return BPPO_OK;
 }
 
-// conv stack + flatten of `rows` observation rows (x, ld ldx) -> d_cnn_f [rows][fdim]
-bppo_status cnn_features(bppo_ctx *c, int rows, const float *x, int ldx, const float *params, const float *wt) {
+// conv stack s + flatten of `rows` observation rows (x, ld ldx) -> d_cnn_f[s] [rows][fdim]
+bppo_status cnn_features(bppo_ctx *c, int s, int rows, const float *x, int ldx, const float *params, const float *wt) {
     const NetLayout &n = c->net;
-    const int HW = n.H * n.W;
+    const int HW = n.H * n.W, l0 = n.conv_base(s);
     for (int l = 0; l < n.n_conv; l++) {
         const ConvGeo g = geo(n, l, rows);
         const size_t tot = (size_t)rows * HW * n.in[l];
         if (l == 0) hipLaunchKernelGGL(k_cnn_im2col<true>, grid_for(tot), dim3(256), 0, c->stream, g, x, ldx, c->d_cnn_a);
         else hipLaunchKernelGGL(k_cnn_im2col<false>, grid_for(tot), dim3(256), 0, c->stream, g,
-                                (const float *)c->d_cnn_y[l - 1], 0, c->d_cnn_a);
+                                (const float *)c->d_cnn_y[s][l - 1], 0, c->d_cnn_a);
         CHIP(c, hipGetLastError());
-        CHIP(c, gemm_fwd(c->stream, rows * HW, n.out[l], n.in[l], c->d_cnn_a, n.in[l], wt + c->cnn_wt_off[l], n.out[l],
-                         params + n.b[l], 1, c->d_cnn_y[l], n.out[l], n.out[l], nullptr, 0));
+        CHIP(c, gemm_fwd(c->stream, rows * HW, n.out[l], n.in[l], c->d_cnn_a, n.in[l], wt + c->cnn_wt_off[s][l],
+                         n.out[l], params + n.b[l0 + l], 1, c->d_cnn_y[s][l], n.out[l], n.out[l], nullptr, 0));
     }
     const int Cl = n.out[n.n_conv - 1];
     hipLaunchKernelGGL(k_cnn_flatten, grid_for((size_t)rows * n.fdim), dim3(256), 0, c->stream, rows, HW, Cl, n.C, n.E,
-                       (const float *)c->d_cnn_y[n.n_conv - 1], x, ldx, c->d_cnn_f);
+                       (const float *)c->d_cnn_y[s][n.n_conv - 1], x, ldx, c->d_cnn_f[s]);
     CHIP(c, hipGetLastError());
     return BPPO_OK;
 }
 
 // dF = dL/dF [rows][fdim] (relu' of the last conv already applied) -> conv weight
-// and bias gradients into grad (Burn layout); the activations of the last
-// cnn_features call on the same rows are reused
-bppo_status cnn_backward(bppo_ctx *c, int rows, const float *x, int ldx, float *dF, float *grad) {
+// and bias gradients of stack s into grad (Burn layout); the activations of the last
+// cnn_features call of that stack on the same rows are reused
+bppo_status cnn_backward(bppo_ctx *c, int s, int rows, const float *x, int ldx, float *dF, float *grad) {
     const NetLayout &n = c->net;
-    const int HW = n.H * n.W, M = rows * HW, last = n.n_conv - 1;
+    const int HW = n.H * n.W, M = rows * HW, last = n.n_conv - 1, l0 = n.conv_base(s);
     float *dy = c->d_cnn_dy[0], *dy2 = c->d_cnn_dy[1];
     if (dF == dy) std::swap(dy, dy2);
     hipLaunchKernelGGL(k_cnn_unflatten, grid_for((size_t)M * n.out[last]), dim3(256), 0, c->stream, rows, HW,
@@ -196,19 +206,20 @@ bppo_status cnn_backward(bppo_ctx *c, int rows, const float *x, int ldx, float *
         const size_t tot = (size_t)M * K;
         if (l == 0) hipLaunchKernelGGL(k_cnn_im2col<true>, grid_for(tot), dim3(256), 0, c->stream, g, x, ldx, c->d_cnn_a);
         else hipLaunchKernelGGL(k_cnn_im2col<false>, grid_for(tot), dim3(256), 0, c->stream, g,
-                                (const float *)c->d_cnn_y[l - 1], 0, c->d_cnn_a);
+                                (const float *)c->d_cnn_y[s][l - 1], 0, c->d_cnn_a);
         CHIP(c, hipGetLastError());
         const int sp = gemm_wg_splits(K, Co, M);
         CHIP(c, gemm_wgrad(c->stream, K, Co, M, c->d_cnn_a, K, dy, Co, c->d_part, c->d_colsum, c->d_cnn_dwt, Co, Co,
-                           nullptr, 0, grad + n.b[l], nullptr, sp));
+                           nullptr, 0, grad + n.b[l0 + l], nullptr, sp));
         hipLaunchKernelGGL(k_cnn_transpose, dim3((K * Co + 255) / 256), dim3(256), 0, c->stream, K, Co,
-                           (const float *)c->d_cnn_dwt, grad + n.w[l]);
+                           (const float *)c->d_cnn_dwt, grad + n.w[l0 + l]);
         CHIP(c, hipGetLastError());
         if (l == 0) break;
         // dA = dY Wt^T (im2col layout), then col2im into the previous layer's output
-        CHIP(c, gemm_dx(c->stream, M, K, Co, dy, Co, c->d_cnn_wt + c->cnn_wt_off[l], Co, nullptr, 0, 0, c->d_cnn_a, K));
+        CHIP(c, gemm_dx(c->stream, M, K, Co, dy, Co, c->d_cnn_wt + c->cnn_wt_off[s][l], Co, nullptr, 0, 0, c->d_cnn_a,
+                        K));
         hipLaunchKernelGGL(k_cnn_col2im, grid_for((size_t)M * n.conv_cin[l]), dim3(256), 0, c->stream, g,
-                           (const float *)c->d_cnn_a, (const float *)c->d_cnn_y[l - 1], dy2);
+                           (const float *)c->d_cnn_a, (const float *)c->d_cnn_y[s][l - 1], dy2);
         CHIP(c, hipGetLastError());
         std::swap(dy, dy2);
     }

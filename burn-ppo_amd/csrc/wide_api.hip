@@ -42,7 +42,7 @@ static bppo_status walloc(bppo_ctx *c, T **p, size_t n) {
 // fully connected hidden layers (their activations live in d_hbuf); CNN conv
 // layers [0, n_conv) keep theirs in d_cnn_y (cnn.hip)
 static bool is_hidden(const NetLayout &n, int l) {
-    return (l >= n.n_conv && l < n.n_actor_hidden) || (n.ctde && l >= n.critic_first && l < n.value);
+    return (l >= n.n_conv && l < n.n_actor_hidden) || (n.ctde && l >= n.critic_fc0 && l < n.value);
 }
 
 bppo_status wide_init(bppo_ctx *c) {
@@ -85,7 +85,7 @@ bppo_status wide_init(bppo_ctx *c) {
         if (!n.ctde && l == n.policy) N = c->A + 1;
         if (!n.ctde && l == n.value) continue;
         const int Kin = (!n.ctde && l == n.policy) ? n.in[l] : n.in[l];
-        const int rows_l = l < n.n_conv ? mb_max * n.H * n.W : mb_max;   // conv GEMMs: one row per position
+        const int rows_l = n.is_conv(l) ? mb_max * n.H * n.W : mb_max;   // conv GEMMs: one row per position
         const int s = gemm_wg_splits(Kin, N, rows_l);
         part = std::max(part, (size_t)s * Kin * N);
         cs = std::max(cs, (size_t)s * N);
@@ -142,8 +142,8 @@ bppo_status wide_forward(bppo_ctx *c, int rows, const float *xc, int ldxc, float
     const float *x = xc + c->G;
     int ldx = ldxc;
     if (n.n_conv) {                                  // CNN trunk (cnn.rs:241-330) -> features [rows][fdim]
-        WTRY(cnn_features(c, rows, x, ldx, P, c->d_cnn_wt));
-        x = c->d_cnn_f; ldx = n.fdim;
+        WTRY(cnn_features(c, 0, rows, x, ldx, P, c->d_cnn_wt));
+        x = c->d_cnn_f[0]; ldx = n.fdim;
     }
     for (int l = n.n_conv; l < n.n_actor_hidden; l++) {
         float *h = c->d_hbuf + c->hoff[l];
@@ -161,7 +161,11 @@ bppo_status wide_forward(bppo_ctx *c, int rows, const float *xc, int ldxc, float
                      c->A, c->A, nullptr, 0));
     const float *xq = xc;
     int ldq = ldxc;
-    for (int l = n.critic_first; l < n.value; l++) {
+    if (n.n_conv) {                                  // split CNN critic: its own conv stack (cnn.rs:284-296)
+        WTRY(cnn_features(c, 1, rows, xc + c->G, ldxc, P, c->d_cnn_wt));
+        xq = c->d_cnn_f[1]; ldq = n.fdim;
+    }
+    for (int l = n.critic_fc0; l < n.value; l++) {
         float *h = c->d_hbuf + c->hoff[l];
         WHIP(c, gemm_fwd(c->stream, rows, n.out[l], n.in[l], xq, ldq, P + n.w[l], n.out[l], P + n.b[l], c->cfg.relu ? 1 : 2, h,
                          n.out[l], n.out[l], nullptr, 0));
@@ -180,8 +184,8 @@ bppo_status wide_forward_actor(bppo_ctx *c, int rows, const float *xc, int ldxc,
     int ldx = ldxc;
     if (n.n_conv) {
         WTRY(cnn_pack(c, P, c->d_cnn_owt));
-        WTRY(cnn_features(c, rows, x, ldx, P, c->d_cnn_owt));
-        x = c->d_cnn_f; ldx = n.fdim;
+        WTRY(cnn_features(c, 0, rows, x, ldx, P, c->d_cnn_owt));
+        x = c->d_cnn_f[0]; ldx = n.fdim;
     }
     for (int l = n.n_conv; l < n.n_actor_hidden; l++) {
         float *h = c->d_hbuf + c->hoff[l];
@@ -283,6 +287,7 @@ bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, float ent_c
         return BPPO_OK;
     };
     // walk hidden layers [first, last] down, dz holds dL/dz of layer `last`
+
     auto hidden_chain = [&](int first, int last, const float *x0, int ldx0) -> bppo_status {
         for (int l = last; l >= first; l--) {
             const float *X = l > first ? c->d_hbuf + c->hoff[l - 1] : x0;
@@ -296,6 +301,15 @@ bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, float ent_c
             }
         }
         return BPPO_OK;
+    };
+    // CNN stack s: FC layers [f0, last] down to the features, dF = dz W^T * [F > 0] (the
+    // conv part of F is relu output), then the conv stack
+    auto cnn_trunk_backward = [&](int s, int f0, int last) -> bppo_status {
+        WTRY(hidden_chain(f0, last, c->d_cnn_f[s], n.fdim));
+        float *dF = c->d_cnn_dy[0];
+        WHIP(c, gemm_dx(c->stream, rows, n.fdim, n.out[f0], dz, n.out[f0], P + n.w[f0], n.out[f0], c->d_cnn_f[s],
+                        n.fdim, 1, dF, n.fdim));
+        return cnn_backward(c, s, rows, c->d_xcg + c->G, L, dF, G);
     };
     const int la = n.n_actor_hidden - 1;
     const float *Ha = c->d_hbuf + c->hoff[la];
@@ -311,18 +325,14 @@ bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, float ent_c
         }
         // CNN: FC layers down to the features, dF = dz W^T * [F > 0] (the conv
         // part of F is relu output), then the conv stack
-        const int f0 = n.n_conv;
-        WTRY(hidden_chain(f0, la, c->d_cnn_f, n.fdim));
-        float *dF = c->d_cnn_dy[0];
-        WHIP(c, gemm_dx(c->stream, rows, n.fdim, n.out[f0], dz, n.out[f0], P + n.w[f0], n.out[f0], c->d_cnn_f, n.fdim, 1,
-                        dF, n.fdim));
-        WTRY(cnn_backward(c, rows, c->d_xcg + c->G, L, dF, G));
+        WTRY(cnn_trunk_backward(0, n.n_conv, la));
         return BPPO_OK;
     }
     // CTDE actor
     WTRY(wgrad(Wa, A, Ha, Wa, c->d_dout, A + 1, G + n.w[n.policy], A, A, nullptr, 0, G + n.b[n.policy], nullptr));
     WHIP(c, gemm_dx(c->stream, rows, Wa, A, c->d_dout, A + 1, P + n.w[n.policy], A, Ha, Wa, hact, dz, Wa));
-    WTRY(hidden_chain(0, la, c->d_xcg + c->G, L));
+    if (n.n_conv) WTRY(cnn_trunk_backward(0, n.n_conv, la));   // split CNN actor
+    else WTRY(hidden_chain(0, la, c->d_xcg + c->G, L));
     // CTDE critic
     const int lc = n.value - 1;
     const float *Hc = c->d_hbuf + c->hoff[lc];
@@ -330,6 +340,7 @@ bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, float ent_c
     dz = c->d_dz[0]; dz2 = c->d_dz[1];
     WTRY(wgrad(Wc, 1, Hc, Wc, c->d_dout + A, A + 1, G + n.w[n.value], 1, 1, nullptr, 0, G + n.b[n.value], nullptr));
     WHIP(c, gemm_dx(c->stream, rows, Wc, 1, c->d_dout + A, A + 1, P + n.w[n.value], 1, Hc, Wc, hact, dz, Wc));
+    if (n.n_conv) return cnn_trunk_backward(1, n.critic_fc0, lc);   // split CNN critic
     WTRY(hidden_chain(n.critic_first, lc, c->d_xcg, L));
     return BPPO_OK;
 }

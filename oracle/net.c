@@ -48,7 +48,16 @@ static int net_layers(const or_net_desc *d, layer_t *L, int *n_actor_total) {
     for (int i = 0; i < d->n_actor; i++) { L[n].in = in; L[n].out = d->actor_width; in = d->actor_width; n++; }
     L[n].in = in; L[n].out = d->act_dim; n++;                 /* policy head */
     *n_actor_total = n;
-    if (two_trunk(d)) {
+    if (two_trunk(d) && d->cnn) {
+        /* split CNN (cnn.rs:116-135): the critic's own conv stack and FC layers */
+        int cin = d->C;
+        for (int i = 0; i < d->n_conv; i++) {
+            L[n].in = cin * d->ksize * d->ksize; L[n].out = d->conv_ch[i]; cin = d->conv_ch[i]; n++;
+        }
+        int fin = d->H * d->W * cin + (d->obs_dim - d->H * d->W * d->C);
+        for (int i = 0; i < d->n_critic; i++) { L[n].in = fin; L[n].out = d->critic_width; fin = d->critic_width; n++; }
+        L[n].in = fin; L[n].out = 1; n++;
+    } else if (two_trunk(d)) {
         int cin = d->priv_dim + d->obs_dim;
         for (int i = 0; i < d->n_critic; i++) { L[n].in = cin; L[n].out = d->critic_width; cin = d->critic_width; n++; }
         L[n].in = cin; L[n].out = 1; n++;
@@ -115,9 +124,12 @@ void or_linear(const float *x, const float *W, const float *b, size_t B, int in,
     }
 }
 
-/* activations cache for backward */
+/* activations cache for backward: buf[l] = output of FC layer l (l < 32), buf[31] =
+ * the CTDE critic input, buf[ACT_CONV + 8 s + l] = conv layer l of stack s (0 actor /
+ * shared, 1 the split critic), buf[ACT_F + s] = the features F of stack s */
+enum { ACT_CONV = 40, ACT_F = 56, ACT_N = 64 };
 typedef struct {
-    float *buf[32];
+    float *buf[ACT_N];
 } acts_t;
 
 /* ------------------------------------------------------------------ CNN --
@@ -149,8 +161,10 @@ static float *conv_wt(const float *w, int cout, int K) {   /* [Cout][K] -> [K][C
     return t;
 }
 
-/* conv stack + flatten: A->buf[16 + l] = conv outputs, A->buf[30] = features F */
-static void cnn_trunk(const or_net_desc *d, const layer_t *L, const float *p, const float *obs, size_t B, acts_t *A) {
+/* conv stack s (its conv layers are L[0 .. n_conv)) + flatten:
+ * A->buf[ACT_CONV + 8 s + l] = conv outputs, A->buf[ACT_F + s] = features F */
+static void cnn_trunk(const or_net_desc *d, const layer_t *L, const float *p, const float *obs, size_t B, acts_t *A,
+                      int s) {
     const int HW = d->H * d->W;
     const float *src = obs;
     int cin = d->C;
@@ -162,7 +176,7 @@ static void cnn_trunk(const or_net_desc *d, const layer_t *L, const float *p, co
         float *y = malloc(sizeof(float) * B * HW * co);
         or_linear(a, wt, p + L[l].b, B * HW, K, co, 1, y);
         free(a); free(wt);
-        A->buf[16 + l] = y;
+        A->buf[ACT_CONV + 8 * s + l] = y;
         src = y; cin = co;
     }
     const int E = d->obs_dim - HW * d->C, fd = HW * cin + E;
@@ -172,7 +186,7 @@ static void cnn_trunk(const or_net_desc *d, const layer_t *L, const float *p, co
             for (int hw = 0; hw < HW; hw++) F[b * fd + (size_t)c * HW + hw] = src[(b * HW + hw) * cin + c];
         for (int j = 0; j < E; j++) F[b * fd + (size_t)HW * cin + j] = obs[b * d->obs_dim + (size_t)HW * d->C + j];
     }
-    A->buf[30] = F;
+    A->buf[ACT_F + s] = F;
 }
 
 static void forward_cached(const or_net_desc *d, const float *p, const float *obs,
@@ -183,8 +197,8 @@ static void forward_cached(const or_net_desc *d, const float *p, const float *ob
     const float *x = obs;
     const int l0 = d->cnn ? d->n_conv : 0;
     if (d->cnn) {
-        cnn_trunk(d, L, p, obs, B, A);
-        x = A->buf[30];
+        cnn_trunk(d, L, p, obs, B, A, 0);
+        x = A->buf[ACT_F];
     }
     for (int i = l0; i < na - 1; i++) {
         float *y = malloc(sizeof(float) * B * L[i].out);
@@ -195,6 +209,17 @@ static void forward_cached(const or_net_desc *d, const float *p, const float *ob
     or_linear(x, p + L[na - 1].w, p + L[na - 1].b, B, L[na - 1].in, L[na - 1].out, -1, logits);
     if (!two_trunk(d)) {
         or_linear(x, p + L[na].w, p + L[na].b, B, L[na].in, 1, -1, values);
+    } else if (d->cnn) {
+        /* split CNN critic: its conv stack on the same spatial input, its FC layers */
+        cnn_trunk(d, L + na, p, obs, B, A, 1);
+        const float *xx = A->buf[ACT_F + 1];
+        for (int i = na + d->n_conv; i < n - 1; i++) {
+            float *y = malloc(sizeof(float) * B * L[i].out);
+            or_linear(xx, p + L[i].w, p + L[i].b, B, L[i].in, L[i].out, d->relu, y);
+            A->buf[i] = y;
+            xx = y;
+        }
+        or_linear(xx, p + L[n - 1].w, p + L[n - 1].b, B, L[n - 1].in, 1, -1, values);
     } else {
         int cin = d->priv_dim + d->obs_dim;
         float *xc = malloc(sizeof(float) * B * cin);
@@ -219,7 +244,7 @@ static void forward_cached(const or_net_desc *d, const float *p, const float *ob
 }
 
 static void free_acts(acts_t *A) {
-    for (int i = 0; i < 32; i++) { free(A->buf[i]); A->buf[i] = NULL; }
+    for (int i = 0; i < ACT_N; i++) { free(A->buf[i]); A->buf[i] = NULL; }
 }
 
 void or_net_forward(const or_net_desc *d, const float *params, const float *obs,
@@ -284,11 +309,12 @@ static void linear_bwd(const float *x, const float *y, const float *dy, const fl
  * un-flatten, then per layer dWt = A^T dY (f64), db = sum dY, dA = dY Wt^T and the
  * col2im gather (taps in (kh, kw) order, f32 adds) times relu' of the input */
 static void cnn_bwd(const or_net_desc *d, const layer_t *L, const float *p, const float *obs, size_t B,
-                    const acts_t *A, const float *dF, double *g) {
+                    const acts_t *A, int s, const float *dF, double *g) {
+    float *const *Y = A->buf + ACT_CONV + 8 * s;   /* this stack's conv outputs */
     const int HW = d->H * d->W, last = d->n_conv - 1, ks = d->ksize, pad = ks / 2;
     const int cl = L[last].out, E = d->obs_dim - HW * d->C, fd = HW * cl + E;
     float *dy = malloc(sizeof(float) * B * HW * cl);
-    const float *yl = A->buf[16 + last];
+    const float *yl = Y[last];
     for (size_t b = 0; b < B; b++)
         for (int hw = 0; hw < HW; hw++)
             for (int c = 0; c < cl; c++) {
@@ -298,7 +324,7 @@ static void cnn_bwd(const or_net_desc *d, const layer_t *L, const float *p, cons
     for (int l = last; l >= 0; l--) {
         const int K = L[l].in, co = L[l].out, cin = l ? L[l - 1].out : d->C;
         float *a = malloc(sizeof(float) * B * HW * K);
-        im2col(d, l, l ? A->buf[16 + l - 1] : obs, d->obs_dim, B, cin, a);
+        im2col(d, l, l ? Y[l - 1] : obs, d->obs_dim, B, cin, a);
         float *wt = conv_wt(p + L[l].w, co, K);
         double *gwt = calloc((size_t)K * co, sizeof(double));
         float *da = l ? malloc(sizeof(float) * B * HW * K) : NULL;
@@ -308,7 +334,7 @@ static void cnn_bwd(const or_net_desc *d, const layer_t *L, const float *p, cons
         free(a); free(wt); free(gwt); free(dy);
         dy = NULL;
         if (!l) break;
-        const float *yp = A->buf[16 + l - 1];
+        const float *yp = Y[l - 1];
         dy = malloc(sizeof(float) * B * HW * cin);
         for (size_t b = 0; b < B; b++)
             for (int hw = 0; hw < HW; hw++)
@@ -534,29 +560,34 @@ void or_minibatch_loss_grad(const or_net_desc *d, const float *p, size_t mb, con
             }
             const int l0 = d->cnn ? d->n_conv : 0;     /* first FC layer */
             for (int l = li - 1; l >= l0; l--) {
-                const float *xl = l > l0 ? acts.buf[l - 1] : (d->cnn ? acts.buf[30] : obs);
+                const float *xl = l > l0 ? acts.buf[l - 1] : (d->cnn ? acts.buf[ACT_F] : obs);
                 float *dxl = (l > l0 || d->cnn) ? malloc(sizeof(float) * mb * L[l].in) : NULL;
                 linear_bwd(xl, acts.buf[l], dh, p + L[l].w, mb, L[l].in, L[l].out, d->relu,
                            g + L[l].w, g + L[l].b, dxl);
                 free(dh);
                 dh = dxl;
             }
-            if (d->cnn) cnn_bwd(d, L, p, obs, mb, &acts, dh, g);   /* dh = dL/dF */
+            if (d->cnn) cnn_bwd(d, L, p, obs, mb, &acts, 0, dh, g);   /* dh = dL/dF */
             free(dh);
         }
         if (two_trunk(d)) {
+            /* critic trunk: FC layers [c0, vi) on its input x0 (CTDE / split MLP: the
+             * critic rows; split CNN: the critic stack's features, then that stack) */
             int vi = n - 1;
-            const float *xin = vi > na ? acts.buf[vi - 1] : acts.buf[31];
-            float *dh = vi > na ? malloc(sizeof(float) * mb * L[vi].in) : NULL;
+            const int c0 = d->cnn ? na + d->n_conv : na;
+            const float *x0 = d->cnn ? acts.buf[ACT_F + 1] : acts.buf[31];
+            const float *xin = vi > c0 ? acts.buf[vi - 1] : x0;
+            float *dh = (vi > c0 || d->cnn) ? malloc(sizeof(float) * mb * L[vi].in) : NULL;
             linear_bwd(xin, NULL, dv, p + L[vi].w, mb, L[vi].in, 1, -1, g + L[vi].w, g + L[vi].b, dh);
-            for (int l = vi - 1; l >= na; l--) {
-                const float *xl = l > na ? acts.buf[l - 1] : acts.buf[31];
-                float *dxl = l > na ? malloc(sizeof(float) * mb * L[l].in) : NULL;
+            for (int l = vi - 1; l >= c0; l--) {
+                const float *xl = l > c0 ? acts.buf[l - 1] : x0;
+                float *dxl = (l > c0 || d->cnn) ? malloc(sizeof(float) * mb * L[l].in) : NULL;
                 linear_bwd(xl, acts.buf[l], dh, p + L[l].w, mb, L[l].in, L[l].out, d->relu,
                            g + L[l].w, g + L[l].b, dxl);
                 free(dh);
                 dh = dxl;
             }
+            if (d->cnn) cnn_bwd(d, L + na, p, obs, mb, &acts, 1, dh, g);
             free(dh);
         }
         for (size_t q = 0; q < np; q++) grads[q] = (float)g[q];

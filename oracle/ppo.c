@@ -130,7 +130,7 @@ or_trainer *or_trainer_new(const or_train_cfg *c, const float *init_params) {
     t->Pa = c->env_kind == OR_ENV_SKULL ? (c->player_count > 0 ? c->player_count : 4) : t->P;
     t->net.ctde = c->ctde; t->net.obs_dim = t->D; t->net.priv_dim = t->G; t->net.act_dim = t->A;
     t->net.relu = c->relu; t->net.n_actor = c->num_hidden; t->net.actor_width = c->hidden;
-    t->net.split = c->split_networks && !c->ctde && !c->cnn;   /* mlp.rs:100-130 */
+    t->net.split = c->split_networks && !c->ctde;   /* mlp.rs:100-130, cnn.rs:116-135 */
     t->net.n_critic = c->ctde ? c->critic_num_hidden : t->net.split ? c->num_hidden : 0;
     t->net.critic_width = c->ctde ? c->critic_hidden : t->net.split ? c->hidden : 0;
     if (c->cnn) {   /* cnn.rs:66-150 */

@@ -20,6 +20,13 @@ WORKLOADS = {
     "cfgC": dict(preset="connect_four", num_envs=16384, num_steps=64),
     # configs/liars_dice_ctde.toml at num_envs=32768, T=128, 4 epochs x 8 minibatches
     "cfgD": dict(preset="liars_dice_ctde", num_envs=32768, num_steps=128),
+    # CfgC with network_type = "cnn": the config.rs:996-1010 defaults (2 conv x 8 channels,
+    # 3x3, FC 32), and a wide variant (64 / 64 channels, FC 128 x 2)
+    "cfgC_cnn": dict(preset="connect_four", num_envs=16384, num_steps=64,
+                     over=dict(network_type="cnn")),
+    "cfgC_cnn64": dict(preset="connect_four", num_envs=16384, num_steps=64,
+                       over=dict(network_type="cnn", conv_channels=[64, 64], cnn_fc_hidden_size=128,
+                                 cnn_num_fc_layers=2)),
 }
 
 
@@ -40,7 +47,9 @@ def main():
     w = dict(WORKLOADS[a.workload])
     if a.num_envs:
         w["num_envs"] = a.num_envs
-    over = {"target_kl": None} if a.no_kl_stop else {}
+    over = dict(w.get("over", {}))
+    if a.no_kl_stop:
+        over["target_kl"] = None
     cfg = bppo.make_config(w["preset"], num_envs=w["num_envs"], num_steps=w["num_steps"], **over)
     torch.cuda.set_device(0)
     tr = bppo.Trainer(cfg, init_seed=0)

@@ -307,12 +307,13 @@ def mlp_desc(obs_dim, act_dim, hidden, num_hidden, relu=True, split=False):
     return d
 
 
-def cnn_desc(act_dim, conv_ch, ksize, fc_hidden, n_fc, relu=True):
-    """Connect Four CNN (obs 86, shape (6, 7, 2))"""
+def cnn_desc(act_dim, conv_ch, ksize, fc_hidden, n_fc, relu=True, split=False):
+    """Connect Four CNN (obs 86, shape (6, 7, 2)); split: the critic's own conv + FC trunk"""
     d = NetDesc(ctde=0, obs_dim=86, priv_dim=0, act_dim=act_dim, relu=int(relu), n_actor=n_fc,
-                actor_width=fc_hidden, n_critic=0, critic_width=0, cnn=1, n_conv=len(conv_ch),
+                actor_width=fc_hidden, n_critic=n_fc if split else 0, critic_width=fc_hidden if split else 0,
+                cnn=1, n_conv=len(conv_ch),
                 conv_ch=(C.c_int * 4)(*[conv_ch[min(i, len(conv_ch) - 1)] for i in range(4)]), ksize=ksize,
-                H=6, W=7, C=2)
+                H=6, W=7, C=2, split=int(split))
     d.n_params = lib().or_net_num_params(C.byref(d))
     return d
 

@@ -60,7 +60,8 @@ def test_metadata_required_fields_and_defaults():
 @pytest.mark.parametrize("preset,over", [("cartpole", {}), ("connect_four", {}), ("liars_dice_ctde", {}),
                                          ("connect_four", {"network_type": "cnn"}),
                                          ("cartpole", {"split_networks": True, "hidden_size": 32, "num_hidden": 3}),
-                                         ("liars_dice_ctde", {"network_type": "mlp", "hidden_size": 128})])
+                                         ("liars_dice_ctde", {"network_type": "mlp", "hidden_size": 128}),
+                                         ("connect_four", {"network_type": "cnn", "split_networks": True})])
 def test_model_record_round_trip(tmp_path, preset, over):
     cfg = bppo.make_config(preset, **over)
     p = bppo.orthogonal_init(cfg, seed=3)
@@ -74,9 +75,15 @@ def test_model_record_round_trip(tmp_path, preset, over):
     assert kind == {"ctde": "Ctde", "cnn": "Cnn", "mlp": "Mlp"}[cfg["network_type"]]
     lin = body["policy_head"]
     assert set(lin) == {"weight", "bias"} and lin["weight"]["param"]["dtype"] == "F32"
-    if cfg.get("split_networks"):   # mlp.rs:47-62: critic_layers on obs, same widths as the actor's
+    if cfg.get("split_networks") and kind == "Mlp":   # mlp.rs:47-62: critic_layers on obs, same widths
         assert [c["weight"]["param"]["shape"] for c in body["critic_layers"]] == \
             [[5, 32], [32, 32], [32, 32]]
+    if kind == "Cnn":   # cnn.rs:24-50: critic stacks only with split_networks, same shapes as the actor's
+        shapes = lambda layers: [c["weight"]["param"]["shape"] for c in layers]
+        assert shapes(body["conv_layers"]) == [[8, 2, 3, 3], [8, 8, 3, 3]]
+        split = bool(cfg.get("split_networks"))
+        assert shapes(body["critic_conv_layers"]) == (shapes(body["conv_layers"]) if split else [])
+        assert shapes(body["critic_fc_layers"]) == (shapes(body["fc_layers"]) if split else [])
 
 
 def test_optimizer_record_round_trip():

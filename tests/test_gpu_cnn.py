@@ -27,6 +27,7 @@ def _cfg(N, T, net, **kw):
 
 def _pair(N, T, net, **kw):
     cfg = _cfg(N, T, net, **kw)
+    split = bool(cfg.get("split_networks"))
     params = bppo.orthogonal_init(cfg, seed=7)
     tr = bppo.Trainer(cfg, params=params)
     ch = [net["conv_channels"][min(i, len(net["conv_channels"]) - 1)] for i in range(net["num_conv_layers"])]
@@ -36,7 +37,8 @@ def _pair(N, T, net, **kw):
                        gamma=cfg["gamma"], gae_lambda=cfg["gae_lambda"],
                        lr=bppo.schedule_get(cfg["learning_rate"], 0), ent_coef=bppo.schedule_get(cfg["entropy_coef"], 0),
                        num_epochs=cfg["num_epochs"], num_minibatches=cfg["num_minibatches"], clip=cfg["clip_epsilon"],
-                       value_coef=cfg["value_coef"], target_kl=cfg["target_kl"], cnn=(ch, net["kernel_size"]))
+                       value_coef=cfg["value_coef"], target_kl=cfg["target_kl"], cnn=(ch, net["kernel_size"]),
+                       split=split)
     ot = O.Trainer(ocfg, params)
     return cfg, tr, ot
 
@@ -99,6 +101,51 @@ def test_cnn_rollout_update_second_rollout(net, N, T, rtol):
     bppo.collect_rollouts(tr.ctx); ot.collect()
     _cmp(tr, ot)
     tr.close(); ot.close()
+
+
+@pytest.mark.parametrize("net", [NETS[0], NETS[3]])
+def test_cnn_split_networks(net):
+    """split_networks (cnn.rs:116-135, 264-302): the critic's own conv stack and FC
+    layers, parameters in the record order conv, fc, critic conv, critic fc, heads.
+    Forward bit-exact, then rollout / GAE / update / second rollout as above."""
+    from parity_util import PARAM_ATOL, PARAM_RTOL
+    cfg = _cfg(16, 2, net, split_networks=True)
+    params = bppo.orthogonal_init(cfg, seed=3)
+    tr = bppo.Trainer(cfg, params=params)
+    ch = [net["conv_channels"][min(i, len(net["conv_channels"]) - 1)] for i in range(net["num_conv_layers"])]
+    d = O.cnn_desc(7, ch, net["kernel_size"], net["cnn_fc_hidden_size"], net["cnn_num_fc_layers"],
+                   relu=cfg["activation"] == "relu", split=True)
+    assert tr.ctx.n_params == d.n_params == params.size
+    rng = np.random.default_rng(1)
+    obs = (rng.random((200, 86)) < 0.3).astype(np.float32)
+    lg, v = tr.model.forward(obs)
+    lo, vo = O.net_forward(d, params, obs)
+    assert np.array_equal(bits(lg), bits(lo)) and np.array_equal(bits(v.reshape(-1)), bits(vo))
+    # the critic's conv weights move only the values
+    nt = sum(i * o + o for i, o in bppo.host.layer_shapes(cfg)[0][:len(ch) + net["cnn_num_fc_layers"]])
+    q = params.copy()
+    q[nt:nt + 100] *= 1.5
+    tr.model.set_params(q)
+    lg2, v2 = tr.model.forward(obs)
+    assert np.array_equal(bits(lg2), bits(lg)) and not np.array_equal(bits(v2), bits(v))
+    tr.close()
+    cfg, tr, ot = _pair(48, 10, net, split_networks=True)
+    try:
+        bppo.collect_rollouts(tr.ctx); ot.collect()
+        _cmp(tr, ot)
+        bppo.compute_gae(tr.ctx); ot.gae()
+        assert np.array_equal(bits(tr.buffer.advantages.reshape(-1)), bits(ot.buffer("advantages")))
+        m = bppo.ppo_update(tr.ctx, bppo.schedule_get(cfg["learning_rate"], 0),
+                            bppo.schedule_get(cfg["entropy_coef"], 0))
+        om = ot.update()
+        assert tr.ctx.rng_pos() == ot.rng_pos()
+        assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"))
+        np.testing.assert_allclose(tr.model.get_params(), ot.params(), rtol=PARAM_RTOL, atol=PARAM_ATOL)
+        tr.model.set_params(ot.params())
+        bppo.collect_rollouts(tr.ctx); ot.collect()
+        _cmp(tr, ot)
+    finally:
+        tr.close(); ot.close()
 
 
 def test_cnn_requires_observation_shape():

@@ -20,6 +20,8 @@ def layer_shapes(desc):
         i = desc.H * desc.W * cin + desc.obs_dim - desc.H * desc.W * desc.C
     for _ in range(desc.n_actor):
         shapes.append((i, desc.actor_width)); i = desc.actor_width
+    if desc.split and desc.cnn:   # cnn.rs:24-50 record: conv, fc, critic conv, critic fc, heads
+        return shapes + shapes + [(i, desc.act_dim), (i, 1)]
     if desc.split:   # mlp.rs:47-62 record: layers, critic_layers, policy_head, value_head
         c = desc.obs_dim
         for _ in range(desc.n_critic):
@@ -48,19 +50,32 @@ def torch_loss(desc, params, obs, priv, actions, old_logp, adv_n, returns, old_v
     act = torch.relu if desc.relu else torch.tanh
     x = torch.tensor(obs, dtype=torch.float64)
     h = x
-    if desc.cnn:
+
+    def conv_stack(convs):
         # cnn.rs:241-330: obs[:, :HWC] reshaped [B, H, W, C] and permuted to NCHW,
         # conv (weight [Cout][Cin][k][k], same padding) + relu, flatten NCHW, cat extra
         Hh, Ww, Cc = desc.H, desc.W, desc.C
         sp = x[:, :Hh * Ww * Cc].reshape(-1, Hh, Ww, Cc).permute(0, 3, 1, 2)
         cin = Cc
-        for l in range(desc.n_conv):
-            W, b = Ws[l]
+        for l, (W, b) in enumerate(convs):
             co = desc.conv_ch[l]
             sp = torch.relu(torch.nn.functional.conv2d(sp, W.reshape(co, cin, desc.ksize, desc.ksize), b,
                                                        padding=desc.ksize // 2))
             cin = co
-        h = torch.cat([sp.reshape(sp.shape[0], -1), x[:, Hh * Ww * Cc:]], 1)
+        return torch.cat([sp.reshape(sp.shape[0], -1), x[:, Hh * Ww * Cc:]], 1)
+    if desc.cnn and desc.split:   # cnn.rs:264-302: two conv+FC trunks on the same input
+        nt = desc.n_conv + desc.n_actor
+        h, hc = conv_stack(Ws[:desc.n_conv]), conv_stack(Ws[nt:nt + desc.n_conv])
+        for W, b in Ws[desc.n_conv:nt]:
+            h = act(h @ W + b)
+        for W, b in Ws[nt + desc.n_conv:2 * nt]:
+            hc = act(hc @ W + b)
+        logits = h @ Ws[2 * nt][0] + Ws[2 * nt][1]
+        v = (hc @ Ws[-1][0] + Ws[-1][1])[:, 0]
+        return _loss_tail(logits, v, actions, old_logp, adv_n, returns, old_values, masks, clip, vcoef, ent,
+                          clip_value, p)
+    if desc.cnn:
+        h = conv_stack(Ws[:desc.n_conv])
         Ws = Ws[desc.n_conv:]
     if desc.split:   # mlp.rs:143-185: actor trunk -> policy, critic trunk on obs -> value
         na, nc = desc.n_actor, desc.n_critic
@@ -170,6 +185,11 @@ def test_split_networks_cartpole_shape():
 
 def test_split_networks_masked_tanh():
     run_case(O.mlp_desc(86, 7, 24, 3, relu=False, split=True), mb=70, masks=True, seed=8)
+
+
+def test_cnn_split_networks_shape():
+    """cnn.rs:116-135 split_networks: the critic's own conv stack and FC layers"""
+    run_case(O.cnn_desc(7, [8, 16], 3, 24, 1, split=True), mb=29, masks=True, seed=8)
 
 
 def test_cnn_one_conv_tanh_fc_kernel5():
