@@ -407,7 +407,9 @@ def main():
                 "measured": "achieved: isolated launches of the in-loop variant ([advantage, return] "
                             "pair of each minibatch row stored too) at the workload shape after the timed region "
                             "(HIP events on the launch stream); launch_ms_in_loop: the same kernel inside the "
-                            "update loop, where it shares the GPU with the side-stream Fisher-Yates passes",
+                            "update loop, where every launch overlaps the side-stream Fisher-Yates passes "
+                            "(k_fyb_link / k_fy_final, random-access HBM) of the update's first epoch: "
+                            "scripts/kt_overlap.py on the kernel trace, profiles/r03_gae_overlap.txt",
                 "launch_ms_in_loop": round(gae_loop_ms, 4),
                 "algorithmic": f"{N * T} x {GAE_BYTES_PER_ELEM} B"}
     out = {"metric": METRIC, "value": round(value, 1), "unit": "env-steps/sec", "n_gpus": world,

@@ -159,11 +159,22 @@ extern "C" const char *bppo_last_error(const bppo_ctx *c) { return c ? c->err.c_
 // instead of polling (polling eats the CPU quota the shuffle walkers run on)
 // (hipEventSynchronize on a blocking-sync event still spun here: measured ~1 CPU per
 // process for the whole update; a sleeping poll at 20 us with 1 us timer slack frees it)
+// The per-update wait of bppo_train_steps (~12 ms on CfgB) repeats from one update to
+// the next, so it starts with ONE coarse sleep of 70 % of the recent waits and only
+// then polls at 20 us: every poll is a wake-up plus an event query, and polling the
+// whole wait cost the driving thread ~1 CPU per rank (14 ms of CPU per 13.9 ms update
+// in r03h), CPU the shuffle walkers of an 8-rank node need.
 static hipError_t wait_event(bppo_ctx *c, hipEvent_t ev) {   // sleeping poll (see sync_stream)
     const auto t0 = std::chrono::steady_clock::now();
-    hipError_t e;
-    while ((e = hipEventQuery(ev)) == hipErrorNotReady) std::this_thread::sleep_for(std::chrono::microseconds(20));
-    c->sync_wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    hipError_t e = hipEventQuery(ev);
+    if (e == hipErrorNotReady) {
+        if (c->wait_est_us > 200.0)
+            std::this_thread::sleep_for(std::chrono::microseconds((long)(0.7 * c->wait_est_us)));
+        while ((e = hipEventQuery(ev)) == hipErrorNotReady) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    c->wait_est_us = c->wait_est_us > 0.0 ? 0.5 * c->wait_est_us + 500.0 * ms : 1000.0 * ms;
+    c->sync_wait_ms += ms;
     return e;
 }
 

@@ -4,7 +4,7 @@
 
 namespace bppo {
 
-constexpr int GEMM_MAX_SPLITS = 256;
+constexpr int GEMM_MAX_SPLITS = 1024;   // narrow conv weight gradients (Kin x Co = 72 x 8) need ~4 blocks per CU
 
 // Y = act(X W + b): X [M][K] (ldx), W [K][N] (ldw), bias [N]; columns [0, n0)
 // go to out0 (ld0), [n0, N) to out1 (ld1) when out1 != nullptr.  Bit-exact
@@ -25,5 +25,19 @@ hipError_t gemm_wgrad(hipStream_t st, int Kin, int N, int rows, const float *X, 
                       int ldz, float *part, float *colsum, float *dW0, int ldw0, int n0, float *dW1, int ldw1,
                       float *db0, float *db1, int splits);
 int gemm_wg_splits(int Kin, int N, int rows);
+
+// Implicit-GEMM convolutions on Connect Four's 6 x 7 board (k_gemm.hip ConvA): NHWC
+// activation rows [rows*42][C]; layer 0 reads the observation rows (obs_ld > 0: row
+// stride, channels-last (h*7 + w)*Cin + ci, cnn.rs:252-262).
+//   fwd   Y = relu(im2col(src) Wt + bias), Wt [Cin*ks*ks][Co] -- bit-identical to the
+//         materialised im2col GEMM (same k order and KC blocks)
+//   wgrad dWt = im2col(src)^T dY, db = column sums of dY (split-K, fixed-order reduce)
+//   dx    dX = (taps(dY) Wd^T) * [H > 0], Wd [Cin][ks*ks*Co]
+hipError_t gemm_conv_fwd(hipStream_t st, int rows, int Co, int Cin, int ks, const float *src, int obs_ld,
+                         const float *Wt, const float *bias, float *out);
+hipError_t gemm_conv_wgrad(hipStream_t st, int rows, int Co, int Cin, int ks, const float *src, int obs_ld,
+                           const float *dY, float *part, float *colsum, float *dWt, float *db, int splits);
+hipError_t gemm_conv_dx(hipStream_t st, int rows, int Cin, int Co, int ks, const float *dY, const float *Wd,
+                        const float *H, float *out);
 
 }  // namespace bppo

@@ -341,8 +341,8 @@ struct bppo_ctx {
     // -- per conv stack s (0: actor / shared, 1: the split_networks critic)
     float *d_cnn_y[2][4] = {};
     float *d_cnn_f[2] = {nullptr, nullptr};
-    float *d_cnn_a = nullptr, *d_cnn_dy[2] = {nullptr, nullptr};
-    float *d_cnn_wt = nullptr, *d_cnn_owt = nullptr, *d_cnn_dwt = nullptr;
+    float *d_cnn_dy[2] = {nullptr, nullptr};
+    float *d_cnn_wt = nullptr, *d_cnn_wd = nullptr, *d_cnn_owt = nullptr, *d_cnn_dwt = nullptr;
     size_t cnn_wt_off[2][4] = {};
     int cnn_stacks = 1;
     // PopArt value normalization (popart.hip, normalization.rs:262-366): running
@@ -365,6 +365,7 @@ struct bppo_ctx {
     float last_ms[8] = {0};
     double last_walk_ms = 0.0, last_wait_ms = 0.0;
     double sync_wait_ms = 0.0, last_host_ms = 0.0, last_sync_ms = 0.0;   // bppo_train_step host split
+    double wait_est_us = 0.0;         // recent per-update waits (wait_event: one coarse sleep first)
     double last_spec_mwords = 0.0, last_true_mwords = 0.0;   // host walk work since the previous update
     double last_walk_cpu_ms = 0.0, last_words_cpu_ms = 0.0;   // thread time in chain_walk / in words()
     int last_met = 0;
@@ -436,7 +437,7 @@ bppo_status wide_forward_actor(bppo_ctx *c, int rows, const float *xc, int ldxc,
 // of the conv stack from dF (dL/d features, [rows][fdim]) into the gradient
 bppo_status cnn_alloc(bppo_ctx *c);
 void cnn_free(bppo_ctx *c);
-bppo_status cnn_pack(bppo_ctx *c, const float *params, float *wt);
+bppo_status cnn_pack(bppo_ctx *c, const float *params, float *wt, float *wd);
 bppo_status cnn_features(bppo_ctx *c, int s, int rows, const float *x, int ldx, const float *params, const float *wt);
 bppo_status cnn_backward(bppo_ctx *c, int s, int rows, const float *x, int ldx, float *dF, float *grad);
 // opponent pool (opponents.hip)

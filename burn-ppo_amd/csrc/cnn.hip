@@ -1,7 +1,8 @@
 // cnn.hip — the CNN actor-critic trunk (network/cnn.rs:24-330) for Connect Four
-// on the f32 MFMA GEMM engine, as implicit-GEMM convolutions staged through an
-// im2col buffer in HBM (288 GB per GPU: the whole minibatch's im2col fits, so a
-// conv layer is ONE engine GEMM, not a loop of small ones).
+// as implicit-GEMM convolutions on the f32 MFMA engine (k_gemm.hip ConvA): the
+// patches are gathered from the NHWC activations while the GEMM's LDS stages are
+// filled, so no im2col matrix exists in HBM (a 64-channel layer's would be
+// rows*42 x 576 floats: 25 GB for a 262,144-row minibatch).
 //
 //   spatial   obs[:, :H*W*C] read as [B, H, W, C] then permuted to NCHW
 //             (cnn.rs:252-262) — the observation itself is plane-major
@@ -9,19 +10,14 @@
 //             obs[(h*W + w)*C + c], exactly as the reference's reshape sees it;
 //   conv      stride 1, same padding (k/2), bias, relu (cnn.rs:204-215):
 //             Y[b*HW + hw][co] = relu(sum_k A[b*HW + hw][k] Wt[k][co] + bias[co]),
-//             k = (ci, kh, kw) in Burn's weight order [Cout][Cin][kh][kw], through
-//             gemm_fwd (matrixmultiply's KC = 256 fma chains, like every Linear);
+//             k = (ci, kh, kw) in Burn's weight order [Cout][Cin][kh][kw], the
+//             KC = 256 fma chains of every Linear (bit-identical to the oracle's
+//             materialised im2col GEMM: same elements, same order);
 //   flatten   [B, C, H, W] -> [B, C*H*W] (NCHW, cnn.rs:216-218), then cat extra
 //             features (cnn.rs:307-311) -> F [B][fdim], the first FC layer's input;
-//   backward  dWt = im2col^T dY (gemm_wgrad, fixed-order split-K), db = column
-//             sums, dA = dY Wt^T (gemm_dx), then col2im as a GATHER (each input
-//             element sums its <= k*k taps in (kh, kw) order: deterministic, no
-//             atomics) times relu'(input).
-// Activations are NHWC rows ([b*HW + hw][channel]), so each conv is a plain
-// row-major GEMM and its output feeds the next im2col directly.
-// split_networks (cnn.rs:116-135, 264-302): a second conv stack (s = 1, layers
-// [critic_first, critic_fc0)) on the same spatial input feeds the critic's FC layers;
-// every function below takes the stack index s.
+//   backward  dWt = A^T dY (implicit A, fixed-order split-K), db = column sums; the
+//             input gradient as ONE transposed-conv GEMM dX = taps(dY) Wd^T times
+//             relu'(input), Wd [Cin][(kh, kw, co)] (no dA matrix, no col2im pass).
 #include "bppo_internal.h"
 #include "bppo_gemm.h"
 #include <algorithm>
@@ -33,32 +29,6 @@ namespace bppo {
         hipError_t _e = (expr);                                             \
         if (_e != hipSuccess) return hip_fail((c), _e, #expr);              \
     } while (0)
-
-struct ConvGeo { int B, H, W, Cin, ks, pad; };
-
-// im2col: A[b*HW + hw][(ci*ks + kh)*ks + kw].  src(b, hw', ci): from the raw
-// observation rows (layer 0, the reference's channels-last reshape) or from the
-// previous layer's NHWC output
-template <bool FROM_OBS>
-__global__ void __launch_bounds__(256) k_cnn_im2col(ConvGeo g, const float *__restrict__ src, int ld,
-                                                     float *__restrict__ A) {
-    const int K = g.Cin * g.ks * g.ks, HW = g.H * g.W;
-    const size_t total = (size_t)g.B * HW * K;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-        const int k = (int)(i % K);
-        const size_t row = i / K;
-        const int hw = (int)(row % HW);
-        const size_t b = row / HW;
-        const int ci = k / (g.ks * g.ks), kk = k % (g.ks * g.ks), kh = kk / g.ks, kw = kk % g.ks;
-        const int h = hw / g.W + kh - g.pad, w = hw % g.W + kw - g.pad;
-        float v = 0.0f;
-        if (h >= 0 && h < g.H && w >= 0 && w < g.W) {
-            const int hw2 = h * g.W + w;
-            v = FROM_OBS ? src[b * ld + (size_t)hw2 * g.Cin + ci] : src[(b * HW + hw2) * g.Cin + ci];
-        }
-        A[i] = v;
-    }
-}
 
 // F[b][c*HW + hw] = Y[b*HW + hw][c];  F[b][HW*Cl + j] = x[b*ldx + HW*C0 + j]
 __global__ void __launch_bounds__(256) k_cnn_flatten(int B, int HW, int Cl, int C0, int E,
@@ -84,29 +54,6 @@ __global__ void __launch_bounds__(256) k_cnn_unflatten(int B, int HW, int Cl, in
     }
 }
 
-// col2im gather: dX[b*HW + hw][ci] = [Y > 0] * sum over (kh, kw) ascending of
-// dA[b*HW + hw_out][(ci*ks + kh)*ks + kw], hw_out = (h - kh + pad, w - kw + pad)
-__global__ void __launch_bounds__(256) k_cnn_col2im(ConvGeo g, const float *__restrict__ dA,
-                                                     const float *__restrict__ Y, float *__restrict__ dX) {
-    const int K = g.Cin * g.ks * g.ks, HW = g.H * g.W;
-    const size_t total = (size_t)g.B * HW * g.Cin;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-        const int ci = (int)(i % g.Cin);
-        const size_t row = i / g.Cin;
-        const int hw = (int)(row % HW);
-        const size_t b = row / HW;
-        const int h = hw / g.W, w = hw % g.W;
-        float s = 0.0f;
-        for (int kh = 0; kh < g.ks; kh++)
-            for (int kw = 0; kw < g.ks; kw++) {
-                const int ho = h - kh + g.pad, wo = w - kw + g.pad;
-                if (ho < 0 || ho >= g.H || wo < 0 || wo >= g.W) continue;
-                s = __fadd_rn(s, dA[(b * HW + ho * g.W + wo) * K + (ci * g.ks + kh) * g.ks + kw]);
-            }
-        dX[i] = Y[i] > 0.0f ? s : 0.0f;
-    }
-}
-
 // Burn conv weight [Cout][K] <-> GEMM operand [K][Cout]
 __global__ void k_cnn_transpose(int R, int Cc, const float *__restrict__ src, float *__restrict__ dst) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -115,11 +62,15 @@ __global__ void k_cnn_transpose(int R, int Cc, const float *__restrict__ src, fl
     dst[(size_t)cc * R + r] = src[i];
 }
 
-static dim3 grid_for(size_t n) { return dim3((unsigned)std::min<size_t>((n + 255) / 256, 65536)); }
-
-static ConvGeo geo(const NetLayout &n, int l, int B) {
-    return ConvGeo{B, n.H, n.W, n.conv_cin[l], n.ksize, n.ksize / 2};
+// Burn conv weight [Co][Cin][kk] -> the transposed-conv operand Wd[ci][t*Co + co]
+__global__ void k_cnn_pack_dx(int Co, int Cin, int kk, const float *__restrict__ w, float *__restrict__ wd) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= Co * Cin * kk) return;
+    const int co = i / (Cin * kk), r = i % (Cin * kk), ci = r / kk, t = r % kk;
+    wd[(size_t)ci * kk * Co + t * Co + co] = w[i];
 }
+
+static dim3 grid_for(size_t n) { return dim3((unsigned)std::min<size_t>((n + 255) / 256, 65536)); }
 
 bppo_status cnn_alloc(bppo_ctx *c) {
     const NetLayout &n = c->net;
@@ -137,10 +88,10 @@ bppo_status cnn_alloc(bppo_ctx *c) {
         CHIP(c, hipMalloc((void **)&c->d_cnn_f[s], (size_t)c->rows_max * n.fdim * 4));
     }
     const size_t dy = std::max(R * cmax, (size_t)c->rows_max * n.fdim);
-    CHIP(c, hipMalloc((void **)&c->d_cnn_a, R * kmax * 4));
     CHIP(c, hipMalloc((void **)&c->d_cnn_dy[0], dy * 4));
     CHIP(c, hipMalloc((void **)&c->d_cnn_dy[1], dy * 4));
     CHIP(c, hipMalloc((void **)&c->d_cnn_wt, wt * 4));
+    CHIP(c, hipMalloc((void **)&c->d_cnn_wd, wt * 4));
     CHIP(c, hipMalloc((void **)&c->d_cnn_owt, wt * 4));
     CHIP(c, hipMalloc((void **)&c->d_cnn_dwt, kmax * cmax * 4));
     return BPPO_OK;
@@ -151,18 +102,24 @@ void cnn_free(bppo_ctx *c) {
         for (float *q : c->d_cnn_y[s]) if (q) (void)hipFree(q);
         if (c->d_cnn_f[s]) (void)hipFree(c->d_cnn_f[s]);
     }
-    void *p[] = {c->d_cnn_a, c->d_cnn_dy[0], c->d_cnn_dy[1], c->d_cnn_wt, c->d_cnn_owt, c->d_cnn_dwt};
+    void *p[] = {c->d_cnn_dy[0], c->d_cnn_dy[1], c->d_cnn_wt, c->d_cnn_wd, c->d_cnn_owt, c->d_cnn_dwt};
     for (void *q : p) if (q) (void)hipFree(q);
 }
 
-// the conv weights of `params` as GEMM operands [K][Cout] (after every params change)
-bppo_status cnn_pack(bppo_ctx *c, const float *params, float *wt) {
+// the conv weights of `params` as GEMM operands (after every params change): Wt
+// [K][Cout] for the forward, and (wd != nullptr) Wd [Cin][kk*Cout] for the input
+// gradient of layers >= 1
+bppo_status cnn_pack(bppo_ctx *c, const float *params, float *wt, float *wd) {
     const NetLayout &n = c->net;
+    const int kk = n.ksize * n.ksize;
     for (int s = 0; s < c->cnn_stacks; s++)
         for (int l = 0; l < n.n_conv; l++) {
             const int R = n.out[l], Cc = n.in[l], lg = n.conv_base(s) + l;   // [Cout][K] -> [K][Cout]
             hipLaunchKernelGGL(k_cnn_transpose, dim3((R * Cc + 255) / 256), dim3(256), 0, c->stream, R, Cc,
                                params + n.w[lg], wt + c->cnn_wt_off[s][l]);
+            if (wd && l > 0)
+                hipLaunchKernelGGL(k_cnn_pack_dx, dim3((R * Cc + 255) / 256), dim3(256), 0, c->stream, R,
+                                   n.conv_cin[l], kk, params + n.w[lg], wd + c->cnn_wt_off[s][l]);
         }
     CHIP(c, hipGetLastError());
     return BPPO_OK;
@@ -172,16 +129,9 @@ bppo_status cnn_pack(bppo_ctx *c, const float *params, float *wt) {
 bppo_status cnn_features(bppo_ctx *c, int s, int rows, const float *x, int ldx, const float *params, const float *wt) {
     const NetLayout &n = c->net;
     const int HW = n.H * n.W, l0 = n.conv_base(s);
-    for (int l = 0; l < n.n_conv; l++) {
-        const ConvGeo g = geo(n, l, rows);
-        const size_t tot = (size_t)rows * HW * n.in[l];
-        if (l == 0) hipLaunchKernelGGL(k_cnn_im2col<true>, grid_for(tot), dim3(256), 0, c->stream, g, x, ldx, c->d_cnn_a);
-        else hipLaunchKernelGGL(k_cnn_im2col<false>, grid_for(tot), dim3(256), 0, c->stream, g,
-                                (const float *)c->d_cnn_y[s][l - 1], 0, c->d_cnn_a);
-        CHIP(c, hipGetLastError());
-        CHIP(c, gemm_fwd(c->stream, rows * HW, n.out[l], n.in[l], c->d_cnn_a, n.in[l], wt + c->cnn_wt_off[s][l],
-                         n.out[l], params + n.b[l0 + l], 1, c->d_cnn_y[s][l], n.out[l], n.out[l], nullptr, 0));
-    }
+    for (int l = 0; l < n.n_conv; l++)
+        CHIP(c, gemm_conv_fwd(c->stream, rows, n.out[l], n.conv_cin[l], n.ksize, l ? c->d_cnn_y[s][l - 1] : x,
+                              l ? 0 : ldx, wt + c->cnn_wt_off[s][l], params + n.b[l0 + l], c->d_cnn_y[s][l]));
     const int Cl = n.out[n.n_conv - 1];
     hipLaunchKernelGGL(k_cnn_flatten, grid_for((size_t)rows * n.fdim), dim3(256), 0, c->stream, rows, HW, Cl, n.C, n.E,
                        (const float *)c->d_cnn_y[s][n.n_conv - 1], x, ldx, c->d_cnn_f[s]);
@@ -201,26 +151,18 @@ bppo_status cnn_backward(bppo_ctx *c, int s, int rows, const float *x, int ldx, 
                        n.out[last], n.fdim, (const float *)dF, dy);
     CHIP(c, hipGetLastError());
     for (int l = last; l >= 0; l--) {
-        const ConvGeo g = geo(n, l, rows);
         const int K = n.in[l], Co = n.out[l];
-        const size_t tot = (size_t)M * K;
-        if (l == 0) hipLaunchKernelGGL(k_cnn_im2col<true>, grid_for(tot), dim3(256), 0, c->stream, g, x, ldx, c->d_cnn_a);
-        else hipLaunchKernelGGL(k_cnn_im2col<false>, grid_for(tot), dim3(256), 0, c->stream, g,
-                                (const float *)c->d_cnn_y[s][l - 1], 0, c->d_cnn_a);
-        CHIP(c, hipGetLastError());
+        const float *src = l ? c->d_cnn_y[s][l - 1] : x;
         const int sp = gemm_wg_splits(K, Co, M);
-        CHIP(c, gemm_wgrad(c->stream, K, Co, M, c->d_cnn_a, K, dy, Co, c->d_part, c->d_colsum, c->d_cnn_dwt, Co, Co,
-                           nullptr, 0, grad + n.b[l0 + l], nullptr, sp));
+        CHIP(c, gemm_conv_wgrad(c->stream, rows, Co, n.conv_cin[l], n.ksize, src, l ? 0 : ldx, dy, c->d_part,
+                                c->d_colsum, c->d_cnn_dwt, grad + n.b[l0 + l], sp));
         hipLaunchKernelGGL(k_cnn_transpose, dim3((K * Co + 255) / 256), dim3(256), 0, c->stream, K, Co,
                            (const float *)c->d_cnn_dwt, grad + n.w[l0 + l]);
         CHIP(c, hipGetLastError());
         if (l == 0) break;
-        // dA = dY Wt^T (im2col layout), then col2im into the previous layer's output
-        CHIP(c, gemm_dx(c->stream, M, K, Co, dy, Co, c->d_cnn_wt + c->cnn_wt_off[s][l], Co, nullptr, 0, 0, c->d_cnn_a,
-                        K));
-        hipLaunchKernelGGL(k_cnn_col2im, grid_for((size_t)M * n.conv_cin[l]), dim3(256), 0, c->stream, g,
-                           (const float *)c->d_cnn_a, (const float *)c->d_cnn_y[s][l - 1], dy2);
-        CHIP(c, hipGetLastError());
+        // the input gradient straight into the previous layer's NHWC rows, relu' applied
+        CHIP(c, gemm_conv_dx(c->stream, rows, n.conv_cin[l], Co, n.ksize, dy, c->d_cnn_wd + c->cnn_wt_off[s][l],
+                             c->d_cnn_y[s][l - 1], dy2));
         std::swap(dy, dy2);
     }
     return BPPO_OK;

@@ -21,6 +21,7 @@
 #include "bppo_internal.h"
 #include "bppo_gemm.h"
 #include <algorithm>
+#include <type_traits>
 
 namespace bppo {
 
@@ -70,7 +71,74 @@ struct TileLoader {
     }
 };
 
+// Implicit-GEMM convolution operands on Connect Four's 6 x 7 board (cnn.rs:204-215,
+// connect_four.rs:217 OBSERVATION_SHAPE): the A operand is never materialised, each
+// element is gathered from the NHWC activation rows (or the raw observation rows of
+// layer 0) when its LDS stage is filled.
+//   kind 1  im2col rows: element (row = b*42 + hw, k = (ci*ks + kh)*ks + kw) =
+//           src(b, h + kh - pad, w + kw - pad, ci) or 0 -- the FWD A operand and the
+//           WG X operand (X^T dY = dW), in the reference's patch order, so the FWD
+//           chains are bit-identical to the im2col form;
+//   kind 2  transposed taps: element (row, k = (kh*ks + kw)*C + c) =
+//           dY(b, h - kh + pad, w - kw + pad, c) or 0 -- the DX A operand, so
+//           dX = A W_d^T is the input gradient directly (no dA matrix, no col2im).
+struct ConvA {
+    int kind = 0;
+    int cin = 0, ks = 1, pad = 0;   // channels of the gathered planes; kernel size; same padding
+    int obs = 0, ld = 0;            // kind 1 layer 0: src = observation rows, row stride ld
+};
+constexpr int CV_H = 6, CV_W = 7, CV_HW = CV_H * CV_W;
+
+// per thread: one fixed patch / tap index, a run of rows step apart
+template <int R, bool KCONTIG>
+struct ConvLoader {
+    static constexpr int E = GBK * R / 256;
+    float v[E];
+    __device__ __forceinline__ void load(const float *__restrict__ src, const ConvA &cv, int r0, int rmax, int k0,
+                                         int kmax, int tid) {
+        int fixed, row, step;
+        if constexpr (KCONTIG) { fixed = k0 + (tid & 31); row = r0 + (tid >> 5); step = 8; }
+        else { fixed = r0 + tid % R; row = k0 + tid / R; step = 256 / R; }
+        const bool fok = fixed < (KCONTIG ? kmax : rmax);
+        const int rowmax = KCONTIG ? rmax : kmax;
+        int ci, dh, dw;
+        if (cv.kind == 1) {
+            const int kk2 = cv.ks * cv.ks;
+            ci = fixed / kk2;
+            const int t = fixed - ci * kk2, kh = t / cv.ks;
+            dh = kh - cv.pad; dw = t - kh * cv.ks - cv.pad;
+        } else {
+            const int tap = fixed / cv.cin, kh = tap / cv.ks;
+            ci = fixed - tap * cv.cin;
+            dh = cv.pad - kh; dw = cv.pad - (tap - kh * cv.ks);
+        }
+        int b = row / CV_HW, hw = row - b * CV_HW;
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            const int h = hw / CV_W + dh, w = hw % CV_W + dw;
+            float x = 0.0f;
+            if (fok && row < rowmax && h >= 0 && h < CV_H && w >= 0 && w < CV_W) {
+                const int hw2 = h * CV_W + w;
+                x = cv.obs ? src[(size_t)b * cv.ld + hw2 * cv.cin + ci] : src[((size_t)b * CV_HW + hw2) * cv.cin + ci];
+            }
+            v[e] = x;
+            row += step; hw += step;
+            if (hw >= CV_HW) { hw -= CV_HW; b++; }
+        }
+    }
+    __device__ __forceinline__ void store(float *__restrict__ s, int tid) const {
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            int r, k;
+            if constexpr (KCONTIG) { k = tid & 31; r = (tid >> 5) + e * 8; }
+            else { r = tid % R; k = tid / R + e * (256 / R); }
+            s[k * (R + 1) + r] = v[e];
+        }
+    }
+};
+
 struct GemmArgs {
+    ConvA cv;                    // A operand: implicit convolution form (kind != 0)
     const float *A; int lda;
     const float *B; int ldb;
     int M, N, K;                 // C is M x N, reduction K
@@ -88,7 +156,7 @@ struct GemmArgs {
 
 enum { GEMM_FWD = 0, GEMM_DX = 1, GEMM_WG = 2 };
 
-template <int MODE, int BM, int BN, int WM, int WN>
+template <int MODE, int BM, int BN, int WM, int WN, int AK>
 __global__ void __launch_bounds__(256, 2) k_gemm(GemmArgs g) {
     using S = GemmShape<BM, BN, WM, WN>;
     constexpr bool A_KC = MODE != GEMM_WG;        // FWD/DX: A row-major [M][K]; WG: A = X^T, X [K][M]
@@ -103,8 +171,13 @@ __global__ void __launch_bounds__(256, 2) k_gemm(GemmArgs g) {
         kbeg = blockIdx.z * g.k_per_split;
         kend = min(g.K, kbeg + g.k_per_split);
     }
-    TileLoader<BM, A_KC> la;
+    // A: a plain operand, or (AK) the implicit convolution form g.cv
+    typename std::conditional<AK != 0, ConvLoader<BM, A_KC>, TileLoader<BM, A_KC>>::type la;
     TileLoader<BN, B_KC> lb;
+    auto load_a = [&](int k) {
+        if constexpr (AK != 0) la.load(g.A, g.cv, m0, g.M, k, kend, tid);
+        else la.load(g.A, g.lda, m0, g.M, k, kend, tid);
+    };
     f32x16 acc[S::TM][S::TN], tot[S::TM][S::TN];
 #pragma unroll
     for (int i = 0; i < S::TM; i++)
@@ -116,7 +189,7 @@ __global__ void __launch_bounds__(256, 2) k_gemm(GemmArgs g) {
     float csum = 0.0f;
     const bool do_colsum = MODE == GEMM_WG && g.colsum != nullptr && blockIdx.y == 0;
 
-    la.load(g.A, g.lda, m0, g.M, kbeg, kend, tid);
+    load_a(kbeg);
     lb.load(g.B, g.ldb, n0, g.N, kbeg, kend, tid);
     la.store(sA[0], tid);
     lb.store(sB[0], tid);
@@ -125,7 +198,7 @@ __global__ void __launch_bounds__(256, 2) k_gemm(GemmArgs g) {
     for (int k0 = kbeg; k0 < kend; k0 += GBK) {
         const bool more = k0 + GBK < kend;
         if (more) {
-            la.load(g.A, g.lda, m0, g.M, k0 + GBK, kend, tid);
+            load_a(k0 + GBK);
             lb.load(g.B, g.ldb, n0, g.N, k0 + GBK, kend, tid);
         }
         if (do_colsum) {
@@ -256,18 +329,18 @@ static hipError_t tanh_inplace(hipStream_t st, float *y, int M, int cols, int ld
 }
 
 // -------------------------------------------------------------- launchers --
-template <int MODE, int BM, int BN, int WM, int WN>
+template <int MODE, int BM, int BN, int WM, int WN, int AK>
 static hipError_t launch(const GemmArgs &g, int splits, hipStream_t st) {
     dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, splits);
-    hipLaunchKernelGGL((k_gemm<MODE, BM, BN, WM, WN>), grid, dim3(256), 0, st, g);
+    hipLaunchKernelGGL((k_gemm<MODE, BM, BN, WM, WN, AK>), grid, dim3(256), 0, st, g);
     return hipGetLastError();
 }
 
-template <int MODE>
+template <int MODE, int AK = 0>
 static hipError_t launch_by_width(const GemmArgs &g, int splits, hipStream_t st) {
-    if (g.N <= 32) return launch<MODE, 128, 32, 4, 1>(g, splits, st);
-    if (g.N <= 64) return launch<MODE, 128, 64, 4, 1>(g, splits, st);
-    return launch<MODE, 128, 128, 2, 2>(g, splits, st);
+    if (g.N <= 32) return launch<MODE, 128, 32, 4, 1, AK>(g, splits, st);
+    if (g.N <= 64) return launch<MODE, 128, 64, 4, 1, AK>(g, splits, st);
+    return launch<MODE, 128, 128, 2, 2, AK>(g, splits, st);
 }
 
 hipError_t gemm_fwd(hipStream_t st, int M, int N, int K, const float *X, int ldx, const float *W,
@@ -282,6 +355,30 @@ hipError_t gemm_fwd(hipStream_t st, int M, int N, int K, const float *X, int ldx
     if (e != hipSuccess || act != 2) return e;
     if ((e = tanh_inplace(st, out0, M, g.n0, ld0)) != hipSuccess) return e;
     return out1 ? tanh_inplace(st, out1, M, N - g.n0, ld1) : hipSuccess;
+}
+
+// conv layer forward (implicit im2col): Y [rows*42][Co] = relu(A(src) Wt + bias)
+hipError_t gemm_conv_fwd(hipStream_t st, int rows, int Co, int Cin, int ks, const float *src, int obs_ld,
+                         const float *Wt, const float *bias, float *out) {
+    if (rows <= 0 || Co <= 0) return hipSuccess;
+    GemmArgs g{};
+    g.cv.kind = 1; g.cv.cin = Cin; g.cv.ks = ks; g.cv.pad = ks / 2; g.cv.obs = obs_ld > 0; g.cv.ld = obs_ld;
+    g.A = src; g.B = Wt; g.ldb = Co; g.M = rows * CV_HW; g.N = Co; g.K = Cin * ks * ks;
+    g.bias = bias; g.act = 1;
+    g.out0 = out; g.ld0 = Co; g.n0 = Co;
+    return launch_by_width<GEMM_FWD, 1>(g, 1, st);
+}
+
+// conv input gradient (transposed taps): dX [rows*42][Cin] = (A_t(dY) Wd^T) * [H > 0],
+// Wd [Cin][ks*ks*Co] with Wd[ci][(kh*ks + kw)*Co + co] = weight[co][ci][kh][kw]
+hipError_t gemm_conv_dx(hipStream_t st, int rows, int Cin, int Co, int ks, const float *dY, const float *Wd,
+                        const float *H, float *out) {
+    if (rows <= 0 || Cin <= 0) return hipSuccess;
+    GemmArgs g{};
+    g.cv.kind = 2; g.cv.cin = Co; g.cv.ks = ks; g.cv.pad = ks / 2;
+    g.A = dY; g.B = Wd; g.ldb = ks * ks * Co; g.M = rows * CV_HW; g.N = Cin; g.K = ks * ks * Co;
+    g.H = H; g.ldh = Cin; g.dact = 1; g.out0 = out; g.ld0 = Cin; g.n0 = Cin;
+    return launch_by_width<GEMM_DX, 2>(g, 1, st);
 }
 
 hipError_t gemm_dx(hipStream_t st, int M, int N, int K, const float *dZ, int ldz, const float *W,
@@ -303,16 +400,36 @@ int gemm_wg_splits(int Kin, int N, int rows) {
     return s;
 }
 
+static hipError_t wgrad(hipStream_t st, const ConvA &cv, int Kin, int N, int rows, const float *X, int ldx,
+                        const float *dZ, int ldz, float *part, float *colsum, float *dW0, int ldw0, int n0,
+                        float *dW1, int ldw1, float *db0, float *db1, int splits);
+
 hipError_t gemm_wgrad(hipStream_t st, int Kin, int N, int rows, const float *X, int ldx, const float *dZ,
                       int ldz, float *part, float *colsum, float *dW0, int ldw0, int n0, float *dW1, int ldw1,
                       float *db0, float *db1, int splits) {
+    return wgrad(st, ConvA{}, Kin, N, rows, X, ldx, dZ, ldz, part, colsum, dW0, ldw0, n0, dW1, ldw1, db0, db1, splits);
+}
+
+// conv weight gradient (implicit im2col X): dWt [Cin*ks*ks][Co] = X(src)^T dY over rows*42 positions
+hipError_t gemm_conv_wgrad(hipStream_t st, int rows, int Co, int Cin, int ks, const float *src, int obs_ld,
+                           const float *dY, float *part, float *colsum, float *dWt, float *db, int splits) {
+    ConvA cv;
+    cv.kind = 1; cv.cin = Cin; cv.ks = ks; cv.pad = ks / 2; cv.obs = obs_ld > 0; cv.ld = obs_ld;
+    return wgrad(st, cv, Cin * ks * ks, Co, rows * CV_HW, src, 0, dY, Co, part, colsum, dWt, Co, Co, nullptr, 0, db,
+                 nullptr, splits);
+}
+
+static hipError_t wgrad(hipStream_t st, const ConvA &cv, int Kin, int N, int rows, const float *X, int ldx,
+                        const float *dZ, int ldz, float *part, float *colsum, float *dW0, int ldw0, int n0,
+                        float *dW1, int ldw1, float *db0, float *db1, int splits) {
     if (Kin <= 0 || N <= 0) return hipSuccess;
     GemmArgs g{};
+    g.cv = cv;
     g.A = X; g.lda = ldx; g.B = dZ; g.ldb = ldz; g.M = Kin; g.N = N; g.K = rows;
     g.part = part; g.colsum = (db0 || db1) ? colsum : nullptr;
     g.k_per_split = ((rows + splits - 1) / splits + GBK - 1) / GBK * GBK;
     const int sp = (rows + g.k_per_split - 1) / g.k_per_split;
-    hipError_t e = launch_by_width<GEMM_WG>(g, sp, st);
+    hipError_t e = cv.kind ? launch_by_width<GEMM_WG, 1>(g, sp, st) : launch_by_width<GEMM_WG>(g, sp, st);
     if (e != hipSuccess) return e;
     const size_t MN = (size_t)Kin * N;
     const int nn0 = dW1 ? n0 : N;

@@ -761,10 +761,17 @@ void ShuffleEngine::run() {
                     }
                 if (best != met) {
                     met = best;
-                    // walks right of the met one in its group can never carry its
-                    // states (walks only coalesce leftwards): free their CPUs
-                    const int g1 = (met >= c0 && met < c1) ? c1 : s1;
-                    for (int i = met + 1; i < g1; i++) spec[i].stop.store(true, std::memory_order_relaxed);
+                    // from here on the epoch's chain lives only in the met walk and the
+                    // walks it has merged into (merges go leftwards): every other walk of
+                    // this boundary, in both candidate groups, is stopped and frees its
+                    // CPU.  (Should the chain's head later merge into a neighbour stopped
+                    // here, that neighbour's recorded states stay valid and the true walk
+                    // walks on from its end -- slower, never wrong.)
+                    bool keep[SHUF_MAX_SPEC] = {};
+                    for (int i = met; i >= 0; i = spec[i].merged_to.load(std::memory_order_acquire)) keep[i] = true;
+                    for (int g = 0; g < 2; g++)
+                        for (int i = g ? s0 : c0; i < (g ? s1 : c1); i++)
+                            if (!keep[i]) spec[i].stop.store(true, std::memory_order_relaxed);
                 }
             }
             flush(tst, true_words);

@@ -127,7 +127,7 @@ bppo_status wide_reset(bppo_ctx *c) {
 // shared-trunk heads packed as one [W][A+1] GEMM operand (after every params change)
 bppo_status wide_pack(bppo_ctx *c) {
     const NetLayout &n = c->net;
-    if (n.n_conv) WTRY(cnn_pack(c, c->d_params, c->d_cnn_wt));
+    if (n.n_conv) WTRY(cnn_pack(c, c->d_params, c->d_cnn_wt, c->d_cnn_wd));
     if (n.ctde) return BPPO_OK;
     WHIP(c, wide_pack_heads(c->stream, c->d_params, n.in[n.policy], c->A, n.w[n.policy], n.b[n.policy],
                             n.w[n.value], n.b[n.value], c->d_heads, c->d_heads_b));
@@ -183,7 +183,7 @@ bppo_status wide_forward_actor(bppo_ctx *c, int rows, const float *xc, int ldxc,
     const float *x = xc + c->G;
     int ldx = ldxc;
     if (n.n_conv) {
-        WTRY(cnn_pack(c, P, c->d_cnn_owt));
+        WTRY(cnn_pack(c, P, c->d_cnn_owt, nullptr));
         WTRY(cnn_features(c, 0, rows, x, ldx, P, c->d_cnn_owt));
         x = c->d_cnn_f[0]; ldx = n.fdim;
     }
