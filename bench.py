@@ -112,6 +112,26 @@ def thread_cpu_ms():
     return out
 
 
+def idle_cpus_sample(cpus, secs):
+    """busy fraction of each CPU over `secs` (/proc/stat deltas)"""
+    def snap():
+        out = {}
+        for line in open("/proc/stat"):
+            if line.startswith("cpu") and line[3].isdigit():
+                f = line.split()
+                v = [int(x) for x in f[1:]]
+                out[int(f[0][3:])] = (sum(v), v[3] + v[4])     # total, idle + iowait
+        return out
+    a = snap()
+    time.sleep(secs)
+    b = snap()
+    busy = {}
+    for c in cpus:
+        if c in a and c in b and b[c][0] > a[c][0]:
+            busy[c] = 1.0 - (b[c][1] - a[c][1]) / (b[c][0] - a[c][0])
+    return busy
+
+
 def host_cpu_budget(local_world):
     """CPUs this rank may use for the shuffle engine's host threads: the CPUs
     the process may run on (affinity, cgroup quota) / ranks on this node."""
@@ -298,12 +318,18 @@ def main():
     if args.selftest:
         return selftest_main(args, world, rank)
     if args.host_cpus > 0:
-        # before any GPU call: the runtime's and the engine's threads inherit the mask
-        cpus = sorted(os.sched_getaffinity(0))
+        # before any GPU call: the runtime's and the engine's threads inherit the mask.
+        # The K CPUs are the idlest ones over a 0.5 s sample (the box's other tenants
+        # run on some of its CPUs: pinning to busy ones measures their load, not a
+        # K-CPU budget -- r03b's first-K pinning ran 31.8 ms/step at K = 16)
         k = args.host_cpus
-        mine = cpus[local * k:(local + 1) * k] if len(cpus) >= (local + 1) * k else cpus[:k]
+        cpus = sorted(os.sched_getaffinity(0))
+        busy = idle_cpus_sample(cpus, 0.5)
+        ranked = sorted(cpus, key=lambda c: busy.get(c, 1.0))
+        mine = ranked[local * k:(local + 1) * k] if len(ranked) >= (local + 1) * k else ranked[:k]
         os.sched_setaffinity(0, mine)
         os.environ["BPPO_HOST_THREADS"] = str(len(mine))
+        os.environ["BPPO_BENCH_PINNED_BUSY"] = f"{sum(busy.get(c, 1.0) for c in mine) / len(mine):.3f}"
     os.environ.setdefault("BPPO_HOST_THREADS", str(host_cpu_budget(local_world)))
 
     import torch
@@ -341,7 +367,8 @@ def main():
     phase = {"rollout": 0.0, "return_norm": 0.0, "gae": 0.0, "minibatch": 0.0, "shuffle": 0.0, "update": 0.0,
              "shuffle_walk": 0.0, "shuffle_wait": 0.0, "shuffle_met": 0.0,
              "shuffle_spec_mwords": 0.0, "shuffle_true_mwords": 0.0,
-             "shuffle_walk_tsc_ms": 0.0, "shuffle_words_tsc_ms": 0.0, "host_enqueue": 0.0, "host_sync_wait": 0.0}
+             "shuffle_walk_tsc_ms": 0.0, "shuffle_words_tsc_ms": 0.0, "host_enqueue": 0.0, "host_sync_wait": 0.0,
+             "minibatch_kernel": 0.0, "minibatch_kernel_min": 0.0, "minibatch_kernel_max": 0.0}
     # the K updates in one pipelined call (bppo_train_steps: each rollout enqueued behind
     # the previous update, per-update phase times summed on the host side of the library)
     if os.environ.get("BPPO_BENCH_SEQUENTIAL") == "1":     # A/B: one train_update call per step
@@ -389,13 +416,19 @@ def main():
     ms_step = dt / args.steps * 1000.0
     # dominant kernel: the fused minibatch forward/loss/backward (16 launches per update)
     mb_rows = N * T // cfg["num_minibatches"]
-    mb_ms = phase["minibatch"] / args.steps          # last minibatch launch of each update
+    # the kernel alone (HIP events around EVERY launch, on its stream), mean over all 16
+    # launches of each update: the side-stream shuffle passes share the GPU with some of
+    # them (min / max reported beside the mean)
+    mb_ms = phase["minibatch_kernel"] / args.steps
+    mb_min, mb_max = phase["minibatch_kernel_min"] / args.steps, phase["minibatch_kernel_max"] / args.steps
     achieved = mb_rows * FLOP_PER_ROW_FWD_BWD / (mb_ms * 1e-3) / 1e12
     cfgB = (N == 65536 and T == 128)
     mb_tr, mb_src = traffic_for("k_minibatch_mfma", "k_update.hip") if cfgB else (None, "not the profiled shape")
     roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": mb_tr, "traffic_unit": "B/launch",
             "traffic_source": mb_src, "kernel": "k_minibatch_mfma", "launch_ms": round(mb_ms, 4),
+            "launch_ms_min_max": [round(mb_min, 4), round(mb_max, 4)],
+            "measured": "mean over all minibatch launches of the timed updates (HIP events around each launch)",
             "algorithmic": f"{mb_rows} rows x {FLOP_PER_ROW_FWD_BWD} FLOP"}
     gae_loop_ms = phase["gae"] / args.steps
     gae_ms = gae_loop_ms if args.no_gae_isolated else gae_isolated_ms(N, T)
@@ -426,7 +459,9 @@ def main():
                                            "stats (SURVEY 8e); parity is defined at N=1" if world > 1 else None),
                       "host_cpus_per_rank": int(os.environ["BPPO_HOST_THREADS"]),
                       "host_cpu_affinity": len(os.sched_getaffinity(0)),
-                      "host_cpu_quota": cgroup_cpu_quota()},
+                      "host_cpu_quota": cgroup_cpu_quota(),
+                      "host_cpus_pinned_busy_before": (float(os.environ["BPPO_BENCH_PINNED_BUSY"])
+                                                       if "BPPO_BENCH_PINNED_BUSY" in os.environ else None)},
            # this process's CPU time per update over the timed region (all threads:
            # shuffle engine walkers and word producers, the driver thread, HIP runtime)
            "host_cpu_ms_per_step": round(host_cpu_ms, 2),

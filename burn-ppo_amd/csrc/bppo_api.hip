@@ -339,6 +339,10 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
         BPPO_HIP(c, hipEventCreate(&c->ev[i][0]));
         BPPO_HIP(c, hipEventCreate(&c->ev[i][1]));
     }
+    for (int i = 0; i < bppo_ctx::MB_EV; i++) {
+        BPPO_HIP(c, hipEventCreate(&c->mb_ev[i][0]));
+        BPPO_HIP(c, hipEventCreate(&c->mb_ev[i][1]));
+    }
     c->rng_key = seed_key(cfg->seed);
     c->rng_pos = 0;
     TRY(c->shuf.init(dev, c->rng_key, cfg->rng_stream, (uint32_t)TN, cfg->num_epochs, TN * (uint64_t)c->A, c->err));
@@ -389,6 +393,8 @@ extern "C" void bppo_destroy(bppo_ctx *c) {
         if (c->ev[i][0]) (void)hipEventDestroy(c->ev[i][0]);
         if (c->ev[i][1]) (void)hipEventDestroy(c->ev[i][1]);
     }
+    for (auto &pr : c->mb_ev)
+        for (hipEvent_t e : pr) if (e) (void)hipEventDestroy(e);
     if (c->fy_stream) { (void)hipStreamSynchronize(c->fy_stream); (void)hipStreamDestroy(c->fy_stream); }
     for (hipEvent_t e : c->fy_ev) if (e) (void)hipEventDestroy(e);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
@@ -1025,6 +1031,18 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
     double ev4[4];
     explained_variance_sums(c, ev4);
     tm_read(c, TM_UPDATE);
+    if (c->mb_ev_n > 0) {                     // every minibatch kernel launch of this update
+        double sum = 0.0;
+        float lo = INFINITY, hi = 0.0f;
+        int n = 0;
+        for (int i = 0; i < c->mb_ev_n; i++) {
+            float ms = 0.0f;
+            if (hipEventElapsedTime(&ms, c->mb_ev[i][0], c->mb_ev[i][1]) != hipSuccess) continue;
+            sum += ms; lo = std::min(lo, ms); hi = std::max(hi, ms); n++;
+        }
+        if (n) { c->mb_k_mean = (float)(sum / n); c->mb_k_min = lo; c->mb_k_max = hi; }
+        c->mb_ev_n = 0;
+    }
     c->last_ms[TM_FWDBWD] = fw_ms;
     c->last_ms[TM_SHUFFLE] = sh_ms;
     if (m) {
@@ -1245,6 +1263,9 @@ extern "C" bppo_status bppo_last_kernel_ms(bppo_ctx *c, const char *k, float *ms
     // host side of the shuffle: draw-chain walk of the last update's epochs, and the
     // time ppo_update blocked waiting for it
     if (!strcmp(k, "shuffle_walk")) { *ms = (float)c->last_walk_ms; return BPPO_OK; }
+    if (!strcmp(k, "minibatch_kernel")) { *ms = c->mb_k_mean; return BPPO_OK; }   // all launches of the last update
+    if (!strcmp(k, "minibatch_kernel_min")) { *ms = c->mb_k_min; return BPPO_OK; }
+    if (!strcmp(k, "minibatch_kernel_max")) { *ms = c->mb_k_max; return BPPO_OK; }
     if (!strcmp(k, "shuffle_wait")) { *ms = (float)c->last_wait_ms; return BPPO_OK; }
     if (!strcmp(k, "host_enqueue")) { *ms = (float)c->last_host_ms; return BPPO_OK; }   // bppo_train_step outside stream waits
     if (!strcmp(k, "host_sync_wait")) { *ms = (float)c->last_sync_ms; return BPPO_OK; }

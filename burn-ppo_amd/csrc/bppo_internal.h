@@ -366,6 +366,12 @@ struct bppo_ctx {
     double last_walk_ms = 0.0, last_wait_ms = 0.0;
     double sync_wait_ms = 0.0, last_host_ms = 0.0, last_sync_ms = 0.0;   // bppo_train_step host split
     double wait_est_us = 0.0;         // recent per-update waits (wait_event: one coarse sleep first)
+    // the fused CartPole minibatch kernel alone (no slab reduction), every launch of the
+    // last update: bppo_last_kernel_ms "minibatch_kernel" (mean), "_min", "_max"
+    static constexpr int MB_EV = 64;
+    hipEvent_t mb_ev[MB_EV][2] = {};
+    int mb_ev_n = 0;
+    float mb_k_mean = 0.0f, mb_k_min = 0.0f, mb_k_max = 0.0f;
     double last_spec_mwords = 0.0, last_true_mwords = 0.0;   // host walk work since the previous update
     double last_walk_cpu_ms = 0.0, last_words_cpu_ms = 0.0;   // thread time in chain_walk / in words()
     int last_met = 0;

@@ -1104,7 +1104,10 @@ bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_
             return BPPO_ERR_UNSUPPORTED;
         }
         c->slab_used = blocks;
+        const int ei = c->mb_ev_n < bppo_ctx::MB_EV ? c->mb_ev_n++ : -1;
+        if (ei >= 0) (void)hipEventRecord(c->mb_ev[ei][0], c->stream);
         hipLaunchKernelGGL(k_minibatch_mfma, dim3(blocks), dim3(64 * mmb::WAVES), mmb::LDSB, c->stream, g);
+        if (ei >= 0) (void)hipEventRecord(c->mb_ev[ei][1], c->stream);
 #ifdef BPPO_MB_STAMPS
         {   // mean per-wave cycles per segment, accumulated over launches; printed every 16
             static double acc_s[MB_NSEG] = {};

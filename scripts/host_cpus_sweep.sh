@@ -1,6 +1,7 @@
 # 1-GPU CfgB bench at K host CPUs per rank (bench.py --host-cpus K: the process is
-# pinned to K CPUs, the shuffle engine sized for K) -- the share each rank of an
-# 8-GPU node gets.  usage: scripts/host_cpus_sweep.sh TAG [K ...]
+# pinned to the K idlest CPUs of the box, the shuffle engine sized for K) -- the share
+# each rank of an 8-GPU node gets when the node's CPU budget is split 8 ways.
+#   usage: scripts/host_cpus_sweep.sh TAG [K ...]
 set -u
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
@@ -15,6 +16,7 @@ d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
 ph = d["phase_ms_per_update"]
 print(f"  {d['ms_per_step']} ms/step  {d['value']/1e6:.1f} M/s  cpu {d['host_cpu_ms_per_step']} ms/step "
       f"{d['host_cpu_ms_per_step_by_thread']}  walk {ph['shuffle_walk']} wait {ph['shuffle_wait']} "
-      f"spec {ph['shuffle_spec_mwords']}M true {ph['shuffle_true_mwords']}M met {ph['shuffle_met']}")
+      f"spec {ph['shuffle_spec_mwords']}M true {ph['shuffle_true_mwords']}M met {ph['shuffle_met']} "
+      f"pinned-busy-before {d['config'].get('host_cpus_pinned_busy_before')}")
 PY
 done
