@@ -470,7 +470,9 @@ def main():
            "phase_ms_per_update": {k: round(v / args.steps, 3) for k, v in phase.items()},
            "last_update": {k: (round(v, 5) if isinstance(v, float) else v) for k, v in last.items()
                            if k in ("policy_loss", "value_loss", "entropy", "approx_kl", "mean_return",
-                                    "episodes", "explained_variance")}}
+                                    "episodes", "explained_variance")},
+           "explained_variance_note": "from f64 sums (the reference sums sequentially in f32, ~1e-3 off "
+                                      "at 1e6 rows; INTEGRATION.md section 7)"}
     if world == 1 and not args.no_learning:
         out["steps_to_475"] = {
             "window": "100 episodes (main.rs:842-853), checked after each rollout",

@@ -729,8 +729,9 @@ static bppo_status collect_enqueue(bppo_ctx *c, bool summary) {
     tm_end(c, tro);
     // self-play: the update's shuffles start right after this rollout's Gumbel words,
     // so the epochs the engine has resolved are permuted now, beside the rollout
-    static const bool fy_ahead = getenv("BPPO_FY_AHEAD") ? atoi(getenv("BPPO_FY_AHEAD")) != 0 : true;
-    if (!opp_active(c) && fy_ahead) {
+    // (beside the rollout is where they cost least: it leaves VGPRs and LDS free on every
+    // CU, while the minibatch kernels fill them -- profiles/r03j_mb_overlap.txt)
+    if (!opp_active(c)) {
         c->shuf_slot = c->shuf.ensure(base + TN * (uint64_t)c->A);
         TRY(fy_enqueue_ready(c, c->shuf_slot));
     }

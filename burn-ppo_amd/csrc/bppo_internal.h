@@ -113,8 +113,6 @@ __device__ __forceinline__ uint32_t mb_of(uint32_t i, const EpochSplit &s) {
 }
 struct ShuffleEngine {
     int dev = 0;
-    uint32_t *d_trash = nullptr;                  // k_expand_J: rejected words' store slots
-    uint32_t *d_xj_r = nullptr;                   // k_expand_J: range r per segment between word slices
     uint32_t n = 0;
     int epochs = 0;
     Key8 key{};

@@ -70,118 +70,112 @@ __global__ void k_chacha_words(Key8 key, uint64_t stream, uint64_t base, uint64_
 }
 
 // J from walk segments.  Segments are consecutive pieces of the epoch's chain
-// (segment i covers words [pos0, pos1) from range r0), one lane per segment: the
-// lane streams its words 16 at a time (the next 16 prefetched while it walks the
-// current ones) from the jobs' device word buffers when a region holds them,
-// else ChaCha12 here, and writes J[r-1] = hi(w * r) for every ACCEPTED word (each
-// r is accepted exactly once in the epoch, so lanes never write the same J).  The
-// zone follows r by subtraction (z -= 2^lz per accept; lz re-derived only when r
-// crosses a power of two), so the per-word chain is mul -> compare -> subtract.
-// No LDS and a handful of VGPRs: the blocks fit beside the update kernels'
-// resident blocks instead of waiting for whole CUs.
+// (segment i covers words [pos0, pos1) from range r0, <= SHUF_CK words), ONE WAVE per
+// segment, 64 words per step: lane j holds word j of the step and tests it under
+// hypotheses h = 0 .. XJ_H-1 ("h rejections among the words before it": range
+// r - j + h), each test a compare whose lane mask is the hypothesis' rejection ballot
+// (lo(w (r - j + h)) and the zone advance by w and 2^lz per hypothesis: one mul per
+// word, then adds).  The step's true rejections are then a scalar find-first chain over
+// the ballots: the first rejection under h = 0, the next one under h = 1 past it, ...;
+// a step with XJ_H rejections ends at the last one.  Every accepted lane j then knows
+// its range r_j = r - j + (rejections below j) and stores J[r_j - 1] = hi(w r_j) --
+// consecutive lanes, consecutive (descending) J entries.  A step whose ranges would
+// leave the lz band (a power of two crossed, or the epoch's last words) walks on lane
+// 0 word by word.  Each range is accepted exactly once in the epoch, so segments never
+// write the same J.  (r01-r03h: one LANE per segment walking sequentially -- few
+// long-lived waves that held CUs against the update kernels: 5.7 ms of side-stream
+// busy time per CfgB update, overlapping 71 of 112 minibatch launches.)
 struct WordRegions {
     const uint32_t *ptr[4];
     uint64_t base[4], len[4];
     int n;
 };
-constexpr int XJ_THREADS = 64;
+constexpr int XJ_WAVES = 4;           // waves (segments) per block
+constexpr int XJ_H = 16;              // rejection hypotheses per 64-word step
 
-__device__ __forceinline__ void xj_fetch(const Key8 &key, uint64_t stream, const WordRegions &wr, uint64_t q,
-                                         uint32_t (&w)[16]) {
-    const uint32_t *src = nullptr;
+// word q (absolute stream position) of the job's device word regions, else ChaCha12
+__device__ __forceinline__ uint32_t xj_word(const Key8 &key, uint64_t stream, const WordRegions &wr, uint64_t q) {
     for (int k = 0; k < wr.n; k++)
-        if (q >= wr.base[k] && q + 16 <= wr.base[k] + wr.len[k]) src = wr.ptr[k] + (q - wr.base[k]);
-    if (src && (((uintptr_t)src & 15) == 0)) {
-        const uint4 *v = reinterpret_cast<const uint4 *>(src);
-        const uint4 a0 = v[0], a1 = v[1], a2 = v[2], a3 = v[3];
-        w[0] = a0.x; w[1] = a0.y; w[2] = a0.z; w[3] = a0.w; w[4] = a1.x; w[5] = a1.y; w[6] = a1.z; w[7] = a1.w;
-        w[8] = a2.x; w[9] = a2.y; w[10] = a2.z; w[11] = a2.w; w[12] = a3.x; w[13] = a3.y; w[14] = a3.z; w[15] = a3.w;
-    } else if (src) {
+        if (q >= wr.base[k] && q < wr.base[k] + wr.len[k]) return wr.ptr[k][q - wr.base[k]];
+    uint32_t blk[16];
+    chacha12_block(key, q >> 4, stream, blk);
+    uint32_t v = blk[0];
 #pragma unroll
-        for (int i = 0; i < 16; i++) w[i] = src[i];
-    } else {
-        chacha12_block(key, q >> 4, stream, w);
-    }
+    for (int i = 1; i < 16; i++) v = (int)(q & 15) == i ? blk[i] : v;
+    return v;
 }
 
-// 64 words (4 blocks) per turn, the next 64 loaded while this turn walks: the
-// J stores share the vmcnt counter with those loads (gfx9 counts both, in order),
-// so the wait for a turn's words covers only the stores of the turn before it,
-// issued ~64 walk steps earlier, not the stores just made.
-// Word slices: one launch walks words [w0, w1) of every segment and leaves the
-// range r for the next slice in rst[] — blocks live ~1/8 of a segment walk, so
-// the copy stream never holds a CU for long against the update kernels (which
-// leave no room beside their own resident blocks).
-constexpr int XJ_NB = 4;
-constexpr int XJ_TRASH = 4096;                       // u32 slots rejected words store to
-constexpr uint32_t XJ_SLICE = 128;                   // words per segment per launch
-__global__ void __launch_bounds__(XJ_THREADS) k_expand_J(Key8 key, uint64_t stream, const ShuffleEngine::Seg *segs,
-                                                         int ns, WordRegions wr, uint32_t *J, uint32_t *trash_buf,
-                                                         uint32_t w0, uint32_t w1, uint32_t *rst) {
-    const int si = blockIdx.x * XJ_THREADS + threadIdx.x;
-    uint32_t *trash = trash_buf + (si & (XJ_TRASH - 1));
-    if (si == 0 && w0 == 0) J[0] = 0;
+__global__ void __launch_bounds__(64 * XJ_WAVES) k_expand_J(Key8 key, uint64_t stream, const ShuffleEngine::Seg *segs,
+                                                          int ns, WordRegions wr, uint32_t *J) {
+    const int lane = threadIdx.x & 63;
+    const int si = blockIdx.x * XJ_WAVES + (threadIdx.x >> 6);
+    if (si == 0 && lane == 0) J[0] = 0;
     if (si >= ns) return;
-    ShuffleEngine::Seg g = segs[si];
-    uint32_t r = w0 == 0 ? g.r0 : rst[si];
-    const uint64_t e1 = min(g.pos1, g.pos0 + w1);
-    g.pos0 += w0;
-    g.pos1 = e1;
-    if (r < 2 || g.pos1 <= g.pos0) { rst[si] = r; return; }
-    int lz = __clz(r);
-    uint32_t lowr = 1u << (31 - lz), sh = 1u << lz, z = (r << lz) - 1u;
-    constexpr uint64_t TW = 16 * XJ_NB;
-    uint64_t q = g.pos0 & ~(uint64_t)15;
-    uint32_t cur[XJ_NB][16], nxt[XJ_NB][16];
-#pragma unroll
-    for (int k = 0; k < XJ_NB; k++)
-        if (q + 16 * k < g.pos1) xj_fetch(key, stream, wr, q + 16 * k, cur[k]);
-    uint32_t j0 = (uint32_t)(g.pos0 - q);
+    const ShuffleEngine::Seg g = segs[si];
+    uint32_t r = g.r0;
+    uint64_t q = g.pos0;
     while (q < g.pos1 && r >= 2) {
-        const uint64_t qn = q + TW;
+        const uint32_t avail = (uint32_t)min((uint64_t)64, g.pos1 - q);
+        const uint32_t w = lane < (int)avail ? xj_word(key, stream, wr, q + lane) : 0u;
+        const int lz = __clz(r);
+        const uint32_t lowr = 1u << (31 - lz);
+        if (r >= lowr + 64 && r >= 66) {
+            // ---- hypothesis ballots: lane j, hypothesis h tests range r - j + h
+            const uint32_t s = 1u << lz;
+            const uint32_t rj = r - (uint32_t)lane;
+            uint32_t lo = w * rj, z = (rj << lz) - 1u;
+            const uint64_t valid = avail >= 64 ? ~0ull : ((1ull << avail) - 1ull);
+            uint64_t rejm = 0;                 // the step's true rejections
+            uint32_t b = avail;                // words the step consumes
+            uint32_t nrej = 0;
+            uint64_t from = 0;                 // bits below `from` are resolved
+            bool open = true;
 #pragma unroll
-        for (int k = 0; k < XJ_NB; k++)
-            if (qn + 16 * k < g.pos1) xj_fetch(key, stream, wr, qn + 16 * k, nxt[k]);
-        const uint32_t j1 = (uint32_t)min(TW, g.pos1 - q);
-        // interior turn (all TW words inside the segment, r stays in this lz band and
-        // >= 2): no per-word predicates or branches — every word stores, an accepted
-        // one to J[r-1], a rejected one to this lane's trash slot (address select)
-        if (j0 == 0 && j1 == (uint32_t)TW && r >= lowr + (uint32_t)TW && r >= (uint32_t)TW + 2u) {
-#pragma unroll
-            for (int k = 0; k < XJ_NB; k++)
-#pragma unroll
-                for (int j = 0; j < 16; j++) {
-                    const uint64_t m = (uint64_t)cur[k][j] * r;
-                    const bool acc = (uint32_t)m <= z;
-                    *(acc ? J + (r - 1) : trash) = (uint32_t)(m >> 32);
-                    r -= acc ? 1u : 0u;
-                    z -= acc ? sh : 0u;
+            for (int h = 0; h < XJ_H; h++) {
+                const uint64_t acc = __ballot(lo <= z);
+                lo += w;
+                z += s;
+                if (open) {
+                    const uint64_t rem = ~acc & valid & ~from;
+                    if (rem == 0) { open = false; continue; }   // every remaining word accepted
+                    const int jh = __builtin_ctzll(rem);
+                    rejm |= 1ull << jh;
+                    nrej++;
+                    from = jh == 63 ? ~0ull : ((2ull << jh) - 1ull);
+                    if (h == XJ_H - 1) b = (uint32_t)jh + 1;        // XJ_H rejections: the step ends there
                 }
+            }
+            // ---- accepted lanes below b store their draw
+            const uint32_t below = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(rejm >> 32),
+                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)rejm, 0u));
+            if ((uint32_t)lane < b && !((rejm >> lane) & 1ull)) {
+                const uint32_t rr = r - (uint32_t)lane + below;
+                J[rr - 1] = __umulhi(w, rr);
+            }
+            r -= b - nrej;
+            q += b;
         } else {
-#pragma unroll
-        for (int k = 0; k < XJ_NB; k++)
-#pragma unroll
-            for (int j = 0; j < 16; j++) {
-                const uint32_t jj = (uint32_t)(16 * k + j);
-                if (jj >= j0 && jj < j1 && r >= 2) {
-                    const uint64_t m = (uint64_t)cur[k][j] * r;
+            // ---- band edge or the epoch's last words: lane 0 walks word by word
+            uint32_t rr = r, used = 0;
+            if (lane == 0) {
+                int lz1 = __clz(rr);
+                uint32_t lowr1 = 1u << (31 - lz1), sh = 1u << lz1, z = (rr << lz1) - 1u;
+                for (uint32_t j = 0; j < avail && rr >= 2; j++) {
+                    const uint32_t wj = xj_word(key, stream, wr, q + j);
+                    const uint64_t m = (uint64_t)wj * rr;
+                    used = j + 1;
                     if ((uint32_t)m <= z) {
-                        J[r - 1] = (uint32_t)(m >> 32);
-                        r--;
+                        J[rr - 1] = (uint32_t)(m >> 32);
+                        rr--;
                         z -= sh;
-                        if (r < lowr) { lz = __clz(r); lowr = 1u << (31 - lz); sh = 1u << lz; z = (r << lz) - 1u; }
+                        if (rr < lowr1 && rr >= 1) { lz1 = __clz(rr); lowr1 = 1u << (31 - lz1); sh = 1u << lz1; z = (rr << lz1) - 1u; }
                     }
                 }
             }
+            r = __shfl(rr, 0, 64);
+            q += __shfl(used, 0, 64);
         }
-#pragma unroll
-        for (int k = 0; k < XJ_NB; k++)
-#pragma unroll
-            for (int j = 0; j < 16; j++) cur[k][j] = nxt[k][j];
-        j0 = 0;
-        q = qn;
     }
-    rst[si] = r;
 }
 
 // expected words per shuffle of n and its std dev: draw with range R accepts with
@@ -283,11 +277,6 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
             err = "shuffle events: creation failed";
             return BPPO_ERR_HIP;
         }
-    if (hipMalloc((void **)&d_trash, sizeof(uint32_t) * XJ_TRASH) != hipSuccess ||
-        hipMalloc((void **)&d_xj_r, sizeof(uint32_t) * (size_t)maxseg) != hipSuccess) {
-        err = "shuffle trash buffer: allocation failed";
-        return BPPO_ERR_HIP;
-    }
     if (make_side_stream(dev, &copy) != hipSuccess) {   // lowest priority
         err = "shuffle copy stream: creation failed";
         return BPPO_ERR_HIP;
@@ -855,11 +844,9 @@ void ShuffleEngine::run() {
                     }
                 Seg *dS = d_seg[slot] + (size_t)e * maxseg;
                 (void)hipMemcpyAsync(dS, S, sizeof(Seg) * (size_t)std::max(ns, 1), hipMemcpyHostToDevice, copy);
-                const uint32_t slice = XJ_SLICE;
-                for (uint32_t w0 = 0; w0 < (uint32_t)SHUF_CK; w0 += slice)
-                    hipLaunchKernelGGL(k_expand_J, dim3((unsigned)((std::max(ns, 1) + XJ_THREADS - 1) / XJ_THREADS)),
-                                       dim3(XJ_THREADS), 0, copy, key, stream, (const Seg *)dS, ns, wr,
-                                       d_J[slot] + (size_t)e * n, d_trash, w0, w0 + slice, d_xj_r);
+                hipLaunchKernelGGL(k_expand_J, dim3((unsigned)((std::max(ns, 1) + XJ_WAVES - 1) / XJ_WAVES)),
+                                   dim3(64 * XJ_WAVES), 0, copy, key, stream, (const Seg *)dS, ns, wr,
+                                   d_J[slot] + (size_t)e * n);
             }
             end_pos[slot][e] = pos;
             (void)hipEventRecord(ev[slot][e], copy);
@@ -915,8 +902,6 @@ void ShuffleEngine::shutdown() {
         gens.clear();
     }
     if (copy) { (void)hipStreamSynchronize(copy); (void)hipStreamDestroy(copy); copy = nullptr; }
-    if (d_trash) { (void)hipFree(d_trash); d_trash = nullptr; }
-    if (d_xj_r) { (void)hipFree(d_xj_r); d_xj_r = nullptr; }
     for (int s = 0; s < 2; s++) {
         if (consumed[s]) { (void)hipEventDestroy(consumed[s]); consumed[s] = nullptr; }
         for (int e = 0; e < epochs; e++) if (ev[s][e]) { (void)hipEventDestroy(ev[s][e]); ev[s][e] = nullptr; }

@@ -31,4 +31,5 @@ DB=$(find gpurun_out/kt_${TAG} -name "*.db" | head -1)
 python3 scripts/rocpd_summary.py $DB > gpurun_out/${TAG}_kernels.txt
 python3 scripts/kt_timeline.py $DB > gpurun_out/${TAG}_timeline.txt
 python3 scripts/kt_overlap.py $DB k_gae_1p_seg > gpurun_out/${TAG}_gae_overlap.txt
-head -8 gpurun_out/${TAG}_kernels.txt; head -5 gpurun_out/${TAG}_timeline.txt; cat gpurun_out/${TAG}_gae_overlap.txt
+python3 scripts/kt_overlap.py $DB k_minibatch_mfma > gpurun_out/${TAG}_mb_overlap.txt
+head -8 gpurun_out/${TAG}_kernels.txt; head -5 gpurun_out/${TAG}_timeline.txt; cat gpurun_out/${TAG}_gae_overlap.txt gpurun_out/${TAG}_mb_overlap.txt
