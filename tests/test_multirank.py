@@ -154,3 +154,62 @@ def test_bench_launcher_starts_world_size_ranks_gloo():
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["selftest"] and d["config"]["parallelism"] == "dp2"
+
+
+def _rccl_worker(port, q, updates):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        cfg = bppo.make_config("cartpole", num_envs=256, num_steps=32)
+        tr = bppo.Trainer(cfg, device=0, init_seed=3)
+        # bench.py's N > 1 wiring: the RCCL all-reduce enqueued on the context's
+        # stream through an ExternalStream (bppo_set_allreduce_async); a one-rank
+        # group stands in for two ranks with identical shards (RCCL SUM, then x2,
+        # then libbppo's 1/world), since the box has one GPU
+        def reduce(t):
+            dist.all_reduce(t)
+            t.mul_(2.0)
+        fn = make_allreduce(dist, mode="device_async", max_elems=tr.ctx.n_params + 64, stream=tr.ctx.stream,
+                            reduce=reduce)
+        calls = [0]
+
+        def counted(ptr, n):
+            calls[0] += 1
+            fn(ptr, n)
+        tr.ctx.set_allreduce(counted, 2, stream_ordered=True)
+        tr.train_updates(updates)
+        q.put((tr.model.get_params(), calls[0], dist.get_backend()))
+        tr.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_rccl_collective_on_the_context_stream_world1():
+    """The RCCL leg of SURVEY 8(e) executed on hardware: a one-rank "nccl" (= RCCL)
+    process group, the all-reduce wired as bench.py wires it for N > 1 (device_async
+    on the context's stream, stream_ordered), through the pipelined
+    bppo_train_steps.  The RCCL SUM over one rank then x2 emulates two ranks with
+    identical shards (x+x then /2 is exact in f32), so the parameters must equal the
+    run without a collective bit for bit, and the callback must have run once per
+    minibatch (ppo.rs:1661-2112: epochs x minibatches per update)."""
+    updates = 3
+    cfg = bppo.make_config("cartpole", num_envs=256, num_steps=32)
+    solo = bppo.Trainer(cfg, device=0, init_seed=3)
+    solo.train_updates(updates)
+    p_solo = solo.model.get_params()
+    solo.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_port(), q, updates))
+    p.start()
+    params, calls, backend = q.get(timeout=300)
+    p.join(60)
+    assert p.exitcode == 0
+    assert backend == "nccl"
+    assert calls == updates * cfg["num_epochs"] * cfg["num_minibatches"]
+    assert np.array_equal(params, p_solo)
