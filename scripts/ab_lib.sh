@@ -13,7 +13,7 @@ import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
 ph = d["phase_ms_per_update"]; r = d["roofline"]
 print(f"{sys.argv[2]} {d['ms_per_step']:7.3f} ms/step  mb {r['launch_ms']:.4f} {r['launch_ms_min_max']}  rollout {ph['rollout']:.3f} "
-      f"gae {ph['gae']:.3f} wait {ph['shuffle_wait']:.2f} cpu {d['host_cpu_ms_per_step']}")
+      f"gae {ph['gae']:.3f} rn {ph.get('return_norm', 0):.3f} wait {ph['shuffle_wait']:.2f} cpu {d['host_cpu_ms_per_step']}")
 PY
   done
 done
