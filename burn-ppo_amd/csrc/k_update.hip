@@ -459,6 +459,10 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
         for (int ct = 0; ct < 2; ct++)
 #pragma unroll
             for (int q = 0; q < 16; q++) acc[ct][q] = 0.0f;
+        // the two matrix segments (layer 2, dZ1/dW1) run at wave priority 3: when both
+        // waves of a SIMD are ready, the one feeding the matrix pipe issues first
+        // (A/B: launch minimum 0.553 -> 0.548 ms, mean -1 %, profiles/r03_mb_setprio_ab.txt)
+        __builtin_amdgcn_s_setprio(3);
 #pragma unroll 8
         for (int s = 0; s < 32; s++) {
             const float av = B.T1[c * RS + 2 * s + h];
@@ -466,6 +470,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
             acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv0, acc[0], 0, 0, 0);
             acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv1, acc[1], 0, 0, 0);
         }
+        __builtin_amdgcn_s_setprio(0);
         MB_STAMP(2);
 #pragma unroll
         for (int ct = 0; ct < 2; ct++)
@@ -601,6 +606,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
         for (int jt = 0; jt < 2; jt++)
 #pragma unroll
             for (int q = 0; q < 16; q++) acc[jt][q] = 0.0f;
+        __builtin_amdgcn_s_setprio(3);
 #pragma unroll 4
         for (int s2 = 0; s2 < 16; s2++) {
 #pragma unroll
@@ -619,6 +625,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
             dW1[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, z0, dW1[1][0], 0, 0, 0);
             dW1[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, z1, dW1[1][1], 0, 0, 0);
         }
+        __builtin_amdgcn_s_setprio(0);
         MB_STAMP(6);
         // dZ1 masked by relu'(H1); dW0 and db0 on the VALU (lane = hidden unit)
 #pragma unroll
