@@ -432,6 +432,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
         }
         wave_sync();
         MB_STAMP(0);
+        __builtin_amdgcn_s_setprio(3);   // matrix segment (see layer 2)
         // ---- layer 1 (K = 5 padded to 6: the pad operand is 0)
         f32x16_t acc[2];
 #pragma unroll
@@ -453,6 +454,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
                 B.T1[cd_row(q, h) * RS + c + 32 * ct] = v > 0.0f ? v : 0.0f;
             }
         wave_sync();
+        __builtin_amdgcn_s_setprio(0);
         MB_STAMP(1);
         // ---- layer 2 (K = 64)
 #pragma unroll
@@ -461,7 +463,8 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
             for (int q = 0; q < 16; q++) acc[ct][q] = 0.0f;
         // the two matrix segments (layer 2, dZ1/dW1) run at wave priority 3: when both
         // waves of a SIMD are ready, the one feeding the matrix pipe issues first
-        // (A/B: launch minimum 0.553 -> 0.548 ms, mean -1 %, profiles/r03_mb_setprio_ab.txt)
+        // (A/B: launch minimum 0.553 -> 0.548 ms, mean -1 %; with layer 1 too, a further
+        // -0.5 % / -0.7 %: profiles/r03_mb_setprio_ab.txt)
         __builtin_amdgcn_s_setprio(3);
 #pragma unroll 8
         for (int s = 0; s < 32; s++) {
