@@ -83,7 +83,12 @@ EXPORTS = (
     "bppo_debug_fisher_yates", "bppo_debug_gemm", "bppo_debug_shuffle_engine", "bppo_debug_sample",
     "bppo_rng_fill_bytes", "bppo_rng_from_seed", "bppo_rng_key_get", "bppo_num_param_tensors",
     "bppo_optimizer_get", "bppo_optimizer_set", "bppo_popart_get", "bppo_popart_set",
+    "bppo_config_size", "bppo_update_metrics_size", "bppo_episode_size", "bppo_rollout_info_size",
 )
+
+# ABI struct -> the library's sizeof export (checked when the library loads)
+STRUCT_SIZES = {"bppo_config_size": Config, "bppo_update_metrics_size": UpdateMetrics,
+                "bppo_episode_size": Episode, "bppo_rollout_info_size": RolloutInfo}
 
 _lib = None
 
@@ -160,10 +165,16 @@ def lib():
         "bppo_popart_get": (i32, [vp, vp]),
         "bppo_popart_set": (i32, [vp, vp]),
     }
+    for name in STRUCT_SIZES:
+        sig[name] = (sz, [])
     for name, (res, args) in sig.items():
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
+    for name, struct in STRUCT_SIZES.items():
+        if getattr(L, name)() != C.sizeof(struct):
+            raise RuntimeError(f"{LIB_PATH}: {name}() = {getattr(L, name)()} but ctypes {struct.__name__} is "
+                               f"{C.sizeof(struct)} bytes (binding out of date with include/bppo.h)")
     _lib = L
     return L
 

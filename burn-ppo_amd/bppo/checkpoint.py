@@ -304,15 +304,19 @@ def optimizer_record(cfg, m1, m2, steps):
     """OptimizerAdaptor<Adam> record: per parameter id an AdamState
     {momentum: {time, moment_1, moment_2}} (burn-optim, restated)"""
     rec = model_record(cfg, np.zeros_like(m1))["item"]
-    ids = [lin[k]["id"] for lin in _linears_in_order(rec) for k in ("weight", "bias")]
-    shapes, _ = layer_shapes(cfg)
-    item, off, t = {}, 0, 0
-    for (i, o) in shapes:
-        for n, shp in ((i * o, [i, o]), (o, [o])):
-            item[ids[t]] = {"momentum": {"time": int(steps[t]),
-                                         "moment_1": _tensor(m1[off:off + n].reshape(shp)),
-                                         "moment_2": _tensor(m2[off:off + n].reshape(shp))}}
-            off += n; t += 1
+    params = [lin[k] for lin in _linears_in_order(rec) for k in ("weight", "bias")]
+    ids = [p["id"] for p in params]
+    # each moment has its parameter's record shape (Linear [in, out] / [out]; Conv2d
+    # [Cout, Cin, k, k] / [Cout]): Burn's Adam state mirrors the gradient's shape
+    item, off = {}, 0
+    for t, p in enumerate(params):
+        shp = p["param"]["shape"]
+        n = int(np.prod(shp))
+        item[ids[t]] = {"momentum": {"time": int(steps[t]),
+                                     "moment_1": _tensor(m1[off:off + n].reshape(shp)),
+                                     "moment_2": _tensor(m2[off:off + n].reshape(shp))}}
+        off += n
+    assert off == m1.size, (off, m1.size)
     return {"metadata": BURN_METADATA, "item": item}, ids
 
 

@@ -29,6 +29,7 @@ class Context:
 
     def __init__(self, cfg, device=0, stream=None, rank=0, world=1, envs_per_rank=None):
         self.cfg = cfg
+        self.rank, self.world = rank, world
         self.struct = to_struct(cfg, rank, world, envs_per_rank)
         h = C.c_void_p()
         st = L.lib().bppo_create(C.byref(self.struct), device, stream, C.byref(h))
@@ -363,6 +364,9 @@ class Trainer:
         self.buffer = RolloutBuffer(self.ctx)
         self.model.set_params(orthogonal_init(self.cfg, init_seed) if params is None else params)
         self.global_step = 0
+        # main.rs:988 global_step += num_steps * num_envs, num_envs of the whole job (every
+        # rank's shard) so the lr / entropy / shaping schedules see the job's env steps
+        self.steps_per_update = self.ctx.T * self.ctx.N * self.ctx.world
         # main.rs:850-853: the last 100 completed episodes' returns (player 0)
         self.recent_returns = deque(maxlen=100)
 
@@ -383,7 +387,7 @@ class Trainer:
             metrics = ppo_update(self.ctx, lr, ent)
         else:
             info, metrics = train_step(self.ctx, lr, ent)        # the same three steps, one host wait
-        self.global_step += self.ctx.T * self.ctx.N                           # main.rs:988
+        self.global_step += self.steps_per_update                             # main.rs:988
         metrics["episodes"] = info.episodes
         metrics["mean_return"] = info.mean_return
         metrics["rng_word_pos"] = info.rng_word_pos
@@ -393,9 +397,9 @@ class Trainer:
         """n iterations of train_update in one pipelined call (bppo_train_steps): the
         same results as n train_update(track_returns=False) calls, the GPU never idle
         between them.  -> (list of metrics dicts, {key: sum of last_kernel_ms(key)})."""
-        lr = np.array([schedule_get(self.cfg["learning_rate"], self.global_step + k * self.ctx.T * self.ctx.N)
+        lr = np.array([schedule_get(self.cfg["learning_rate"], self.global_step + k * self.steps_per_update)
                        for k in range(n)], np.float64)
-        ent = np.array([schedule_get(self.cfg["entropy_coef"], self.global_step + k * self.ctx.T * self.ctx.N)
+        ent = np.array([schedule_get(self.cfg["entropy_coef"], self.global_step + k * self.steps_per_update)
                         for k in range(n)], np.float64)
         infos, ms = (L.RolloutInfo * max(n, 1))(), (L.UpdateMetrics * max(n, 1))()
         keys = (C.c_char_p * max(len(phase_keys), 1))(*[k.encode() for k in phase_keys])
@@ -409,7 +413,7 @@ class Trainer:
             d["mean_return"] = infos[k].mean_return
             d["rng_word_pos"] = infos[k].rng_word_pos
             out.append(d)
-        self.global_step += n * self.ctx.T * self.ctx.N
+        self.global_step += n * self.steps_per_update
         return out, {k: float(sums[i]) for i, k in enumerate(phase_keys)}
 
     def close(self):

@@ -151,6 +151,11 @@ static bppo_status dalloc(bppo_ctx *c, T **p, size_t n) {
         if (_s != BPPO_OK) return _s;          \
     } while (0)
 
+extern "C" size_t bppo_config_size(void) { return sizeof(bppo_config); }
+extern "C" size_t bppo_update_metrics_size(void) { return sizeof(bppo_update_metrics); }
+extern "C" size_t bppo_episode_size(void) { return sizeof(bppo_episode); }
+extern "C" size_t bppo_rollout_info_size(void) { return sizeof(bppo_rollout_info); }
+
 extern "C" const char *bppo_version(void) { return "bppo-mi355x 0.1 (gfx950)"; }
 
 extern "C" const char *bppo_last_error(const bppo_ctx *c) { return c ? c->err.c_str() : "null ctx"; }
@@ -203,16 +208,7 @@ static bool cartpole_fused_net(const bppo_config &c) {
 static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *stream) {
     c->cfg = *cfg;
     c->dev = dev;
-    BPPO_HIP(c, hipSetDevice(dev));
-    if (stream) { c->stream = (hipStream_t)stream; c->own_stream = false; }
-    else {
-        // the hot path's stream at the highest priority: the shuffle engine's copy-stream
-        // kernels (J expansion) only take CUs the update kernels leave free
-        int lo = 0, hi = 0;
-        BPPO_HIP(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
-        BPPO_HIP(c, hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi));
-        c->own_stream = true;
-    }
+    // the configuration is validated before the first HIP call
     if (cfg->num_envs <= 0 || cfg->num_steps <= 0 || cfg->num_epochs <= 0 || cfg->num_minibatches <= 0) {
         c->err = "num_envs, num_steps, num_epochs, num_minibatches must be positive";
         return BPPO_ERR_ARG;
@@ -253,8 +249,28 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
         }
         for (int l = 0; l < cfg->num_conv_layers; l++)
             if (cfg->conv_channels[l < 4 ? l : 3] < 1) { c->err = "conv_channels must be positive"; return BPPO_ERR_ARG; }
-        const int layers = (cfg->split_networks ? 2 : 1) * (cfg->num_conv_layers + cfg->cnn_num_fc_layers) + 2;
-        if (layers > 16) { c->err = "CNN: at most 16 layers in all (conv + FC + heads)"; return BPPO_ERR_UNSUPPORTED; }
+    }
+    // NetLayout holds at most 16 layers (its per-layer tables, Adam's 32 tensors):
+    // MLP (split_networks doubles the trunk), CTDE actor + critic, CNN conv + FC stacks
+    {
+        const int split = cfg->split_networks && !cfg->ctde ? 2 : 1;
+        const int layers = cfg->cnn ? split * (cfg->num_conv_layers + cfg->cnn_num_fc_layers) + 2
+                         : cfg->ctde ? cfg->num_hidden + cfg->critic_num_hidden + 2
+                                     : split * cfg->num_hidden + 2;
+        if (layers > NetLayout::MAX_LAYERS) {
+            c->err = "network: at most 16 layers in all (hidden / conv / FC layers + heads)";
+            return BPPO_ERR_UNSUPPORTED;
+        }
+    }
+    BPPO_HIP(c, hipSetDevice(dev));
+    if (stream) { c->stream = (hipStream_t)stream; c->own_stream = false; }
+    else {
+        // the hot path's stream at the highest priority: the shuffle engine's copy-stream
+        // kernels (J expansion) only take CUs the update kernels leave free
+        int lo = 0, hi = 0;
+        BPPO_HIP(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
+        BPPO_HIP(c, hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi));
+        c->own_stream = true;
     }
     c->net = make_layout(*cfg, c->D, c->G, c->A);
     const size_t np = c->net.n_params;
@@ -403,8 +419,19 @@ extern "C" void bppo_destroy(bppo_ctx *c) {
 
 extern "C" size_t bppo_num_params(const bppo_ctx *c) { return c ? c->net.n_params : 0; }
 
+// a rollout bppo_train_steps enqueued ahead (and left pending by an error) was drawn
+// with the state these setters replace: drop it (the envs and the RNG stay where it
+// left them; the next bppo_collect_rollouts draws a new one)
+static void drop_prefetch(bppo_ctx *c) {
+    if (!c->prefetched) return;
+    c->prefetched = false;
+    c->collected = 0;
+    c->gae_done = 0;
+}
+
 extern "C" bppo_status bppo_params_set(bppo_ctx *c, const float *h, size_t n) {
     if (!c || !h || n != c->net.n_params) { if (c) c->err = "params_set: size mismatch"; return BPPO_ERR_ARG; }
+    drop_prefetch(c);
     BPPO_HIP(c, hipMemcpyAsync(c->d_params, h, n * 4, hipMemcpyHostToDevice, c->stream));
     if (c->wide) TRY(wide_pack(c));
     BPPO_HIP(c, sync_stream(c));
@@ -446,6 +473,7 @@ extern "C" bppo_status bppo_rng_get(bppo_ctx *c, uint64_t *p) {
 }
 extern "C" bppo_status bppo_rng_set(bppo_ctx *c, uint64_t p) {
     if (!c) return BPPO_ERR_ARG;
+    drop_prefetch(c);
     c->shuf_slot = -1;
     c->fy_slot = -1; c->fy_done = 0;     // permutations made ahead belong to the old start
     c->rng_pos = p;
@@ -476,6 +504,7 @@ extern "C" bppo_status bppo_rng_fill_bytes(bppo_ctx *c, uint8_t *dst, size_t n) 
 // engine precomputes words of the old key, so it is restarted on the new one.
 extern "C" bppo_status bppo_rng_from_seed(bppo_ctx *c, const uint8_t *seed) {
     if (!c || !seed) return BPPO_ERR_ARG;
+    drop_prefetch(c);
     Key8 k;
     for (int i = 0; i < 8; i++)
         k.k[i] = (uint32_t)seed[4 * i] | ((uint32_t)seed[4 * i + 1] << 8) | ((uint32_t)seed[4 * i + 2] << 16) |
@@ -517,6 +546,7 @@ extern "C" bppo_status bppo_optimizer_get(bppo_ctx *c, float *m1, float *m2, int
 extern "C" bppo_status bppo_optimizer_set(bppo_ctx *c, const float *m1, const float *m2, const int32_t *steps,
                                           size_t n) {
     if (!c || !m1 || !m2 || !steps || n != c->net.n_params) {
+    drop_prefetch(c);
         if (c) c->err = "optimizer_set: size mismatch";
         return BPPO_ERR_ARG;
     }
@@ -532,6 +562,7 @@ extern "C" size_t bppo_num_param_tensors(const bppo_ctx *c) { return c ? c->adam
 
 extern "C" bppo_status bppo_vecenv_reset(bppo_ctx *c) {
     if (!c) return BPPO_ERR_ARG;
+    drop_prefetch(c);
     TRY(c->wide ? wide_reset(c) : launch_cartpole_reset(c));
     BPPO_HIP(c, sync_stream(c));
     return BPPO_OK;
@@ -634,6 +665,7 @@ extern "C" bppo_status bppo_obs_norm_get(bppo_ctx *c, double *mean, double *m2, 
 
 extern "C" bppo_status bppo_obs_norm_set(bppo_ctx *c, const double *mean, const double *m2, double count) {
     if (!c || !mean || !m2) return BPPO_ERR_ARG;
+    drop_prefetch(c);
     std::vector<double> h(2 * c->D + 1);
     std::memcpy(h.data(), mean, sizeof(double) * c->D);
     std::memcpy(h.data() + c->D, m2, sizeof(double) * c->D);
@@ -653,6 +685,7 @@ extern "C" bppo_status bppo_ret_norm_get(bppo_ctx *c, double *mvc, double *retur
 
 extern "C" bppo_status bppo_ret_norm_set(bppo_ctx *c, const double *mvc, const double *returns) {
     if (!c) return BPPO_ERR_ARG;
+    drop_prefetch(c);
     if (mvc) BPPO_HIP(c, hipMemcpyAsync(c->d_rn_stats, mvc, sizeof(double) * 3, hipMemcpyHostToDevice, c->stream));
     if (returns) BPPO_HIP(c, hipMemcpyAsync(c->d_rn_returns, returns, sizeof(double) * (size_t)c->N * c->P, hipMemcpyHostToDevice, c->stream));
     BPPO_HIP(c, sync_stream(c));
@@ -667,6 +700,7 @@ extern "C" bppo_status bppo_popart_get(bppo_ctx *c, double *st) {
 
 extern "C" bppo_status bppo_popart_set(bppo_ctx *c, const double *st) {
     if (!c || !st) return BPPO_ERR_ARG;
+    drop_prefetch(c);
     c->pa_mean = st[0]; c->pa_m2 = st[1]; c->pa_count = st[2]; c->pa_eps = st[3];
     return BPPO_OK;
 }
@@ -826,6 +860,7 @@ extern "C" bppo_status bppo_rollout_episodes(bppo_ctx *c, bppo_episode *eps, int
 // bootstrap + GAE (main.rs:877-947)
 // enqueue half (the CartPole path has no host read in it)
 static bppo_status gae_enqueue(bppo_ctx *c) {
+    c->prefetched = false;        // a pending rollout is consumed here (e.g. after a bppo_train_steps error)
     if (c->wide) {
         tm_begin(c, TM_GAE);
         TRY(wide_bootstrap_gae(c));
@@ -1134,7 +1169,7 @@ extern "C" bppo_status bppo_train_steps(bppo_ctx *c, int32_t n, const double *lr
                                         const char *const *phase_keys, int32_t nkeys, float *phase_sums) {
     if (!c || n < 0 || !lr || !ent_coef || (nkeys > 0 && (!phase_keys || !phase_sums))) return BPPO_ERR_ARG;
     for (int k = 0; k < nkeys; k++) phase_sums[k] = 0.0f;
-    const uint64_t TN = (uint64_t)c->T * c->N;
+    const uint64_t TN = (uint64_t)c->T * c->N * (uint64_t)c->world;   // the job's env steps per iteration
     for (int32_t k = 0; k < n; k++) {
         const auto t0 = std::chrono::steady_clock::now();
         c->sync_wait_ms = 0.0;
@@ -1166,14 +1201,25 @@ extern "C" bppo_status bppo_train_steps(bppo_ctx *c, int32_t n, const double *lr
     return BPPO_OK;
 }
 
+// W > 1: PopArt's running return statistics and value-head rescale
+// are per rank, so the ranks' parameters would drift apart; an opponent pool trains a
+// per-rank number of learner rows, so the ranks' minibatches would not line up
+static bppo_status check_world(bppo_ctx *c, int32_t world) {
+    if (world > 1 && c->cfg.normalize_values) { c->err = "normalize_values (PopArt): single-rank only"; return BPPO_ERR_UNSUPPORTED; }
+    if (world > 1 && opp_active(c)) { c->err = "opponent pool: single-rank only"; return BPPO_ERR_UNSUPPORTED; }
+    return BPPO_OK;
+}
+
 extern "C" bppo_status bppo_set_allreduce(bppo_ctx *c, bppo_allreduce_fn fn, void *user, int32_t world) {
     if (!c || world < 1) return BPPO_ERR_ARG;
+    TRY(check_world(c, world));
     c->allreduce = fn; c->allreduce_user = user; c->world = world; c->allreduce_async = 0;
     return BPPO_OK;
 }
 
 extern "C" bppo_status bppo_set_allreduce_async(bppo_ctx *c, bppo_allreduce_fn fn, void *user, int32_t world) {
     if (!c || world < 1) return BPPO_ERR_ARG;
+    TRY(check_world(c, world));
     c->allreduce = fn; c->allreduce_user = user; c->world = world; c->allreduce_async = 1;
     return BPPO_OK;
 }
@@ -1240,6 +1286,10 @@ extern "C" bppo_status bppo_gae_rows_device(const float *r, const float *d, cons
                                             int32_t T, int32_t N, float gamma, float lambda, float *adv,
                                             float *ret, float *rows, void *stream) {
     if (!r || !d || !v || !lv || !adv || !ret || !rows || T < 0 || N < 0) return BPPO_ERR_ARG;
+    // only the segmented kernel writes the pairs: refuse other shapes before launching anything
+    if (N % 4 != 0 || T > 128 ||
+        ((uintptr_t)r | (uintptr_t)d | (uintptr_t)v | (uintptr_t)lv | (uintptr_t)adv | (uintptr_t)ret | (uintptr_t)rows) % 16)
+        return BPPO_ERR_UNSUPPORTED;
     bool packed = false;
     const bppo_status s = launch_gae_1p(r, d, v, lv, T, N, gamma, lambda, adv, ret, (hipStream_t)stream,
                                         reinterpret_cast<float2 *>(rows), &packed);

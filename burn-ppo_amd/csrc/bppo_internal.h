@@ -18,15 +18,16 @@ namespace bppo {
 
 // ---------------------------------------------------------------- layout ----
 struct NetLayout {
+    static constexpr int MAX_LAYERS = 16;   // checked by ctx_init before make_layout
     int n_layers = 0;             // linear layers in record order
-    int in[16], out[16];
-    size_t w[16], b[16];
+    int in[MAX_LAYERS], out[MAX_LAYERS];
+    size_t w[MAX_LAYERS], b[MAX_LAYERS];
     int n_actor_hidden = 0;       // hidden layers of the actor / shared backbone
     int policy = 0, value = 0;    // layer indices of the heads
     int critic_first = -1;        // critic layers [critic_first, value) (CTDE, split_networks)
     int critic_fc0 = -1;          // its first FC layer (split CNN: after the critic's own conv stack)
     int ctde = 0, relu = 1;       // ctde: two trunks (CTDE, or split_networks with the critic on obs)
-    int rec[16];                  // Burn record position of layer l (split_networks: actor, critic, heads)
+    int rec[MAX_LAYERS];          // Burn record position of layer l (split_networks: actor, critic, heads)
     size_t n_params = 0;
     // CNN (network/cnn.rs): layers [0, n_conv) are the conv layers (in = Cin k k,
     // out = Cout; weight [Cout][Cin][k][k] then bias in Burn record order), then the
@@ -47,6 +48,11 @@ constexpr int EP_SUMMARY_BLOCKS = 128;   // k_ep_summary grid (partial sums per 
 constexpr int TM_SLOTS = 10;             // phase timer event pairs (enum TM_* below)
 constexpr int ROLL_HOST_WORDS = 2 + 2 * EP_SUMMARY_BLOCKS;     // pinned doubles per rollout slot
 constexpr int ADV_STREAM_BLOCKS = 512, ADV_STREAM_MAXM = 16;   // k_adv_stream grid, most minibatches
+// metric slots after the gradient, d_grad[np + k]: GRAD_METRIC_SLOTS (= WM_COUNT, bppo_wide.h)
+// travel with the gradient through the W > 1 SUM all-reduce; value_error_max (slot
+// GRAD_VEMAX) cannot be summed, so its reduction also writes a rank-local copy to slot
+// GRAD_VEMAX_LOCAL, past the all-reduced range, and the metric row reads that copy
+constexpr int GRAD_METRIC_SLOTS = 14, GRAD_VEMAX = 9, GRAD_VEMAX_LOCAL = GRAD_METRIC_SLOTS;
 
 struct EpisodeRec {
     float total_reward[BPPO_MAX_PLAYERS];

@@ -8,7 +8,12 @@
 //   utils.rs:25         gumbel = -ln(-ln(u))
 //   cartpole.rs:51-52   theta.cos(), theta.sin()
 // The constant tables below are the data that glibc's libm.so.6 carries
-// (__logf_data, __sincosf_table, __inv_pio4).  tests/test_libm_restatement.py
+// (__logf_data, __sincosf_table, __inv_pio4).  Origin and licence: these tables
+// (and the tanhf/expm1f constants further down, from fdlibm via glibc) are third-
+// party data from the GNU C Library 2.35, licensed LGPL-2.1-or-later (the logf /
+// sincosf tables originate in ARM's optimized-routines, MIT / Apache-2.0 with LLVM
+// exception); they are reproduced as data, needed for bit-exact transcendentals.
+// tests/test_libm_restatement.py
 // checks every Gumbel input and every float |x| < 1 against the real glibc on
 // the host, and the GPU tests check device == host on the same inputs, so the
 // device kernels reproduce the reference bit for bit.

@@ -285,7 +285,8 @@ bppo_status launch_gae_1p(const float *r, const float *d, const float *v, const 
                           float2 *pairs, bool *pairs_done) {
     if (pairs_done) *pairs_done = false;
     if (T <= 0 || N <= 0) return BPPO_OK;
-    const bool al = ((uintptr_t)r | (uintptr_t)d | (uintptr_t)v | (uintptr_t)lv | (uintptr_t)adv | (uintptr_t)ret) % 16 == 0;
+    const bool al = ((uintptr_t)r | (uintptr_t)d | (uintptr_t)v | (uintptr_t)lv | (uintptr_t)adv | (uintptr_t)ret |
+                     (uintptr_t)pairs) % 16 == 0;   // k_gae_1p_seg stores the pairs as float4
     if (N % 4 == 0 && T <= GSEG_WAVES * GSEG_L && al) {
         const int N4 = N / 4, L = (T + GSEG_WAVES - 1) / GSEG_WAVES;
         hipLaunchKernelGGL(k_gae_1p_seg, dim3((N4 + 63) / 64), dim3(GSEG_WAVES * 64), 0, s, (const float4 *)r,

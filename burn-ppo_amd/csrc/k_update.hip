@@ -723,7 +723,7 @@ constexpr int SLAB_GROUPS = 32;
 // Fisher-Yates passes load HBM
 constexpr int SLAB1_WAVES = 16;
 __global__ void __launch_bounds__(64 * SLAB1_WAVES) k_slab_reduce1(const float *__restrict__ slab, int rows, int width,
-                                                      float *__restrict__ grad) {
+                                                      float *__restrict__ grad, float *__restrict__ vemax_local) {
     __shared__ double part[SLAB_GROUPS][64];
     const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
     const int p = blockIdx.x * 64 + lane;
@@ -746,6 +746,7 @@ __global__ void __launch_bounds__(64 * SLAB1_WAVES) k_slab_reduce1(const float *
         double s = is_max ? -INFINITY : 0.0;
         for (int g = 0; g < SLAB_GROUPS; g++) s = is_max ? fmax(s, part[g][lane]) : s + part[g][lane];
         grad[p] = (float)s;
+        if (is_max) *vemax_local = (float)s;     // kept out of the W > 1 SUM all-reduce
     }
 }
 
@@ -857,7 +858,7 @@ __global__ void __launch_bounds__(ADAM1_THREADS) k_adam1(AdamArgs a, const float
     }
     if (blockIdx.x == 0 && metric_dst) {
         const int i = threadIdx.x;
-        if (i < nm) metric_dst[i] = gtail[i];
+        if (i < nm) metric_dst[i] = gtail[i == GRAD_VEMAX ? GRAD_VEMAX_LOCAL : i];
         else if (i < nm + 4) metric_dst[i] = mb_stats[i - nm];
     }
 }
@@ -1153,8 +1154,9 @@ bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_
 #undef L
     BPPO_HIP(c, hipGetLastError());
     const int width = (int)c->net.n_params + NUM_M;
+    static_assert(M_VEMAX == GRAD_VEMAX && NUM_M <= GRAD_METRIC_SLOTS, "metric slot layout");
     hipLaunchKernelGGL(k_slab_reduce1, dim3((width + 63) / 64), dim3(64 * SLAB1_WAVES), 0, c->stream, c->d_slab,
-                       c->slab_used, width, c->d_grad);
+                       c->slab_used, width, c->d_grad, c->d_grad + c->net.n_params + GRAD_VEMAX_LOCAL);
     BPPO_HIP(c, hipGetLastError());
     return BPPO_OK;
 }
@@ -1162,7 +1164,7 @@ bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_
 // one minibatch's metric sums (grad tail) and advantage stats into the update's rows
 __global__ void k_metric_row(const float *gtail, const float *mb_stats, int nm, float *dst) {
     const int i = threadIdx.x;
-    if (i < nm) dst[i] = gtail[i];
+    if (i < nm) dst[i] = gtail[i == GRAD_VEMAX ? GRAD_VEMAX_LOCAL : i];
     else if (i < nm + 4) dst[i] = mb_stats[i - nm];
 }
 bppo_status launch_metric_row(bppo_ctx *c, float *dst, int nm) {

@@ -376,6 +376,7 @@ __global__ void __launch_bounds__(256) k_wide_loss(LossArgs g) {
 // fixed-order reduction of the loss partials into the metric slots after the
 // gradient (d_grad[np + k]), where the all-reduce callback picks them up: one
 // wave per metric, lane-strided sums then a fixed shuffle tree
+static_assert(WM_COUNT == GRAD_METRIC_SLOTS && WM_VEMAX == GRAD_VEMAX, "metric slot layout");
 __global__ void __launch_bounds__(64) k_wide_metric_reduce(const double *part, int nblk, float *out) {
     const int k = blockIdx.x, lane = threadIdx.x;
     const bool is_max = k == WM_VEMAX;
@@ -388,7 +389,10 @@ __global__ void __launch_bounds__(64) k_wide_metric_reduce(const double *part, i
         const double o = __shfl_xor(v, off, 64);
         v = is_max ? fmax(v, o) : v + o;
     }
-    if (lane == 0) out[k] = (float)v;
+    if (lane == 0) {
+        out[k] = (float)v;
+        if (is_max) out[GRAD_VEMAX_LOCAL] = (float)v;   // kept out of the W > 1 SUM all-reduce
+    }
 }
 
 // ------------------------------------------------------------- launchers --

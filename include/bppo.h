@@ -71,10 +71,13 @@ typedef struct {
     /* Skull: player_count (config.rs:767 PlayerCountMode, get_fixed_count, main.rs:1998);
      * 2..6, 0 = the default 4.  The player axis of the buffers stays NUM_PLAYERS = 6. */
     int32_t player_count;
-    /* split_networks (config.rs:860, default false; mlp.rs:40-130, 139-206): separate actor
-     * and critic trunks of num_hidden x hidden_size on the observation (MLP; CNN: not on the
-     * device path, BPPO_ERR_UNSUPPORTED).  Flat parameters in Burn record order: layers
-     * (actor), critic_layers, policy_head, value_head.  CTDE nets ignore it (ctde.rs). */
+    /* split_networks (config.rs:860, default false): separate actor and critic trunks.
+     * MLP (mlp.rs:40-130, 139-206): a critic trunk of num_hidden x hidden_size on the
+     * observation; flat parameters in Burn record order: layers (actor), critic_layers,
+     * policy_head, value_head.  CNN (cnn.rs:116-135, 264-302): the critic's own conv stack
+     * and FC layers; record order conv, fc, critic conv, critic fc, heads.  CTDE nets ignore
+     * it (ctde.rs).  Any net: at most 16 layers in all (hidden / conv / FC layers + the two
+     * heads), else bppo_create returns BPPO_ERR_UNSUPPORTED. */
     int32_t split_networks;
 } bppo_config;
 
@@ -115,6 +118,12 @@ bppo_status bppo_create(const bppo_config *cfg, int hip_device, void *hip_stream
 void bppo_destroy(bppo_ctx *ctx);
 const char *bppo_last_error(const bppo_ctx *ctx);
 const char *bppo_version(void);
+/* sizeof the ABI structs as this library was built: a binding (Rust #[repr(C)], ctypes)
+ * asserts its own struct sizes against these before the first bppo_create */
+size_t bppo_config_size(void);
+size_t bppo_update_metrics_size(void);
+size_t bppo_episode_size(void);
+size_t bppo_rollout_info_size(void);
 
 /* ---- ActorCritic -------------------------------------------------------- */
 /* flat parameters in Burn record order: per Linear W[in][out] then b[out];
@@ -184,12 +193,15 @@ bppo_status bppo_ppo_update(bppo_ctx *ctx, double lr, double ent_coef, bppo_upda
 bppo_status bppo_train_step(bppo_ctx *ctx, double lr, double ent_coef, bppo_rollout_info *info,
                             bppo_update_metrics *m);
 /* n bppo_train_step iterations (main.rs:684-988 loop body, lr[k] / ent_coef[k], env step
- * global_step0 + k*T*N), software-pipelined: each iteration's rollout is enqueued behind the
+ * global_step0 + k*T*N*world_size), software-pipelined: each iteration's rollout is enqueued behind the
  * previous update before the host waits for that update, so the GPU does not idle between
  * iterations.  Same results as n bppo_train_step calls; the stream is drained on return.
  * After an error status the next iteration's rollout may already have run (the RNG and
  * the envs are past it): it stays the context's next rollout, which bppo_collect_rollouts,
- * bppo_train_step and bppo_train_steps use instead of drawing another one.
+ * bppo_train_step and bppo_train_steps use instead of drawing another one (bppo_compute_gae
+ * consumes it too).  A setter of the state it was drawn with (bppo_params_set,
+ * bppo_optimizer_set, bppo_rng_set / _from_seed, bppo_obs_norm_set, bppo_ret_norm_set,
+ * bppo_popart_set, bppo_vecenv_reset) discards it; the next rollout is then drawn anew.
  * infos / ms: n entries each (may be NULL); phase_keys (bppo_last_kernel_ms names, nkeys of
  * them): per-key sums over the n iterations into phase_sums */
 bppo_status bppo_train_steps(bppo_ctx *ctx, int32_t n, const double *lr, const double *ent_coef,
@@ -201,6 +213,13 @@ bppo_status bppo_train_steps(bppo_ctx *ctx, int32_t n, const double *lr, const d
  * The callback must leave the SUM over ranks in place; the context divides
  * by world_size.  (RCCL all-reduce over xGMI, one per minibatch.) */
 typedef int (*bppo_allreduce_fn)(float *device_buf, size_t n, void *user);
+/* W = world_size > 1 semantics (the reference is single-process; DESIGN.md section 7,
+ * pinned by tests/test_gpu_multirank.py against the oracle's W-rank update): each rank's
+ * gradient is the mean over its own minibatch rows with its own advantage normalization;
+ * the SUM over ranks is scaled by 1/W before clip + Adam, so all ranks take the same step.
+ * The metric partials ride along, so the UpdateMetrics are those of all ranks' rows
+ * together, except value_error_max, adv_*_raw and explained_variance, which stay per rank.
+ * normalize_values (PopArt) and opponent pools are single-rank: BPPO_ERR_UNSUPPORTED. */
 bppo_status bppo_set_allreduce(bppo_ctx *ctx, bppo_allreduce_fn fn, void *user, int32_t world_size);
 
 /* stream-ordered variant: fn is called WITHOUT draining the stream, right after

@@ -332,6 +332,11 @@ typedef struct {
     int normalize_values;    /* PopArt (config.rs:827-832) */
     int player_count;        /* Skull (config.rs:767), 0 = 4 */
     int split_networks;      /* config.rs:860 (MLP nets) */
+    /* data-parallel rank r of W (libbppo's W > 1 semantics): envs are
+     * seeded seed + env_seed_offset + i (offset = r * num_envs) and the main RNG is
+     * StdRng::seed_from_u64(seed) on ChaCha stream rng_stream (= r).  Zero: the reference. */
+    uint64_t env_seed_offset;
+    uint64_t rng_stream;
 } or_train_cfg;
 or_trainer *or_trainer_new(const or_train_cfg *c, const float *init_params);
 void or_trainer_free(or_trainer *t);
@@ -351,9 +356,13 @@ void or_trainer_set_norms(or_trainer *t, const double *mean, const double *m2, d
 int or_trainer_collect(or_trainer *t);                     /* returns episodes completed (all, not only those stored) */
 void or_trainer_gae(or_trainer *t);
 void or_trainer_update(or_trainer *t, or_update_metrics *m);
+/* the same update for W data-parallel ranks in lockstep (gradients summed over the
+ * ranks then scaled by 1/W before clip + Adam; ms[W]); W = 1 is or_trainer_update */
+void or_trainers_update(or_trainer **ts, int W, or_update_metrics *ms);
 /* buffer export: name in {"obs","actions","rewards","dones","values","log_probs",
    "advantages","returns","players","all_rewards","masks","priv","last_v_pp"} */
 size_t or_trainer_buffer(const or_trainer *t, const char *name, void *out, size_t bytes);
+int or_trainer_set_buffer(or_trainer *t, const char *name, const void *src, size_t bytes);  /* values, advantages, returns, rewards, log_probs */
 void or_trainer_obs_norm_state(const or_trainer *t, double *mean, double *var, double *count);
 void or_trainer_ret_norm_state(const or_trainer *t, double *mean_var_count3, double *returns);
 int or_trainer_episodes(const or_trainer *t, or_episode *out, int cap);  /* last collect */

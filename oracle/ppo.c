@@ -122,7 +122,7 @@ static double now_s(void) {
 or_trainer *or_trainer_new(const or_train_cfg *c, const float *init_params) {
     or_trainer *t = calloc(1, sizeof *t);
     t->c = *c;
-    t->env = or_vecenv_new_np(c->env_kind, c->num_envs, c->seed, c->player_count);
+    t->env = or_vecenv_new_np(c->env_kind, c->num_envs, c->seed + c->env_seed_offset, c->player_count);
     or_vecenv_set_shaping(t->env, (float)c->reward_shaping);
     t->T = c->num_steps; t->N = c->num_envs;
     t->D = or_vecenv_obs_dim(t->env); t->A = or_vecenv_act_dim(t->env);
@@ -146,6 +146,7 @@ or_trainer *or_trainer_new(const or_train_cfg *c, const float *init_params) {
     or_ret_norm_init(&t->rn, t->N, t->P, c->gamma, c->return_clip);
     or_popart_init(&t->pa);
     or_rng_seed_u64(&t->rng, c->seed);   /* main.rs:189 */
+    t->rng.stream = c->rng_stream;       /* rank r of a data-parallel job: stream r */
     size_t TN = (size_t)t->T * t->N;
     t->obs = malloc(sizeof(float) * TN * t->D);
     t->raw = malloc(sizeof(float) * TN * t->D);
@@ -491,124 +492,227 @@ void or_trainer_gae(or_trainer *t) {
     t->phase_s[1] = now_s() - t0;
 }
 
-/* ppo.rs:1661-2112 ppo_update (no pool, no PopArt). */
-void or_trainer_update(or_trainer *t, or_update_metrics *m) {
+/* ppo.rs:1661-2112 ppo_update, for W ranks stepped in lockstep (W = 1: the
+ * reference's single-process update).  W > 1 restates libbppo's data-parallel
+ * semantics (the reference has no multi-GPU
+ * path): each rank shuffles its own rows with its own main-RNG stream, gathers
+ * its minibatch and normalizes the advantages over its own rows, and computes
+ * its loss gradient (mean over its rows).  The gradients are then SUMMED over
+ * the ranks in f32, in rank order, and scaled by 1/W (the all-reduce between
+ * loss.backward() and optimizer.step, ppo.rs:1953-1988), so every rank takes
+ * the same clip + Adam step.  The minibatch metrics are the ones of the W
+ * minibatches together (sums over all ranks' rows, as the device's metric
+ * partials travel with the gradient), except value_error_max and the raw
+ * advantage statistics, which stay per rank; the KL early stop reads the
+ * combined approx_kl, so all ranks stop together.  PopArt and opponent pools
+ * are single-rank only (libbppo returns BPPO_ERR_UNSUPPORTED for them at W > 1). */
+typedef struct {
+    uint32_t *vidx, *idx;
+    size_t B, sz, start;
+    float *grads, *mo, *mp, *mm, *mlp, *madv, *mret, *mov, *madvn;
+    int32_t *ma;
+    float am, as, amn, amx;
+    or_mb_stats st;
+    float tam, tas, tamin, tamax, tvemax;
+    float rescale_mag;
+    double tsum, tsq, tcnt;
+} rank_ws;
+
+void or_trainers_update(or_trainer **ts, int W, or_update_metrics *ms) {
     double t0 = now_s();
-    size_t B = (size_t)t->T * t->N;
-    /* opponent-pool training: only the learner rows, in (t, e) order (ppo.rs:1696-1720) */
-    uint32_t *vidx = NULL;
-    if (t->n_opp > 0) {
-        vidx = malloc(sizeof(uint32_t) * B);
-        size_t nv = 0;
-        for (size_t i = 0; i < B; i++) if (t->valid[i] > 0.5f) vidx[nv++] = (uint32_t)i;
-        B = nv;
-    }
-    const int D = t->D, A = t->A, G = t->G;
-    const or_ppo_cfg *c = &t->c.ppo;
-    /* ppo.rs:1787-1808 PopArt: statistics over the (learner) returns, then rescale the value head */
-    float rescale_mag = NAN;
-    double tsum = 0.0, tsq = 0.0, tcnt = 0.0;
-    if (t->c.normalize_values) {
-        float *rr = malloc(sizeof(float) * (B ? B : 1));
-        for (size_t i = 0; i < B; i++) rr[i] = t->ret[vidx ? vidx[i] : i];
-        double om, os;
-        or_popart_update(&t->pa, rr, B, &om, &os);
-        free(rr);
-        if (t->pa.count >= 2.0) {
-            size_t vw, vb; int vin;
-            or_net_value_head(&t->net, &vw, &vb, &vin);    /* ppo.rs:1599-1653 */
-            const double nm = t->pa.mean, ns = or_popart_std(&t->pa), sc = os / ns;
-            for (int i = 0; i < vin; i++) t->params[vw + i] = (float)((double)t->params[vw + i] * sc);
-            t->params[vb] = (float)(((double)t->params[vb] * os + om - nm) / ns);
-            rescale_mag = (float)fabs(sc);
+    if (W < 1) return;
+    if (W > 1)
+        for (int r = 0; r < W; r++)
+            if (ts[r]->n_opp > 0 || ts[r]->c.normalize_values) {
+                fprintf(stderr, "or_trainers_update: opponent pools / PopArt are single-rank only\n");
+                abort();
+            }
+    or_trainer *t0r = ts[0];
+    const int D = t0r->D, A = t0r->A, G = t0r->G;
+    const or_ppo_cfg *c = &t0r->c.ppo;
+    const size_t np = t0r->net.n_params;
+    rank_ws *ws = calloc((size_t)W, sizeof *ws);
+    size_t mbmax = 0;
+    for (int r = 0; r < W; r++) {
+        or_trainer *t = ts[r];
+        rank_ws *w = &ws[r];
+        w->B = (size_t)t->T * t->N;
+        /* opponent-pool training: only the learner rows, in (t, e) order (ppo.rs:1696-1720) */
+        if (t->n_opp > 0) {
+            w->vidx = malloc(sizeof(uint32_t) * w->B);
+            size_t nv = 0;
+            for (size_t i = 0; i < w->B; i++) if (t->valid[i] > 0.5f) w->vidx[nv++] = (uint32_t)i;
+            w->B = nv;
         }
+        /* ppo.rs:1787-1808 PopArt: statistics over the (learner) returns, then rescale the value head */
+        w->rescale_mag = NAN;
+        if (t->c.normalize_values) {
+            float *rr = malloc(sizeof(float) * (w->B ? w->B : 1));
+            for (size_t i = 0; i < w->B; i++) rr[i] = t->ret[w->vidx ? w->vidx[i] : i];
+            double om, os;
+            or_popart_update(&t->pa, rr, w->B, &om, &os);
+            free(rr);
+            if (t->pa.count >= 2.0) {
+                size_t vw, vb; int vin;
+                or_net_value_head(&t->net, &vw, &vb, &vin);    /* ppo.rs:1599-1653 */
+                const double nm = t->pa.mean, ns = or_popart_std(&t->pa), sc = os / ns;
+                for (int i = 0; i < vin; i++) t->params[vw + i] = (float)((double)t->params[vw + i] * sc);
+                t->params[vb] = (float)(((double)t->params[vb] * os + om - nm) / ns);
+                w->rescale_mag = (float)fabs(sc);
+            }
+        }
+        if (W > 1 && w->B != ws[0].B) { fprintf(stderr, "or_trainers_update: ranks differ in rows\n"); abort(); }
+        size_t mbm = w->B / c->num_minibatches + 1;
+        if (mbm > mbmax) mbmax = mbm;
     }
-    uint32_t *idx = malloc(sizeof(uint32_t) * B);
-    size_t np = t->net.n_params;
-    float *grads = malloc(sizeof(float) * np);
-    size_t mbmax = B / c->num_minibatches + 1;
-    float *mo = malloc(sizeof(float) * mbmax * D), *mp = G ? malloc(sizeof(float) * mbmax * G) : NULL;
-    float *mm = t->has_masks ? malloc(sizeof(float) * mbmax * A) : NULL;
-    int32_t *ma = malloc(sizeof(int32_t) * mbmax);
-    float *mlp = malloc(sizeof(float) * mbmax), *madv = malloc(sizeof(float) * mbmax);
-    float *mret = malloc(sizeof(float) * mbmax), *mov = malloc(sizeof(float) * mbmax);
-    float *madvn = malloc(sizeof(float) * mbmax);
-    float tp = 0, tv = 0, th = 0, tk = 0, tc = 0, tl = 0, tvm = 0, trm = 0, tam = 0, tas = 0;
-    float tamin = INFINITY, tamax = -INFINITY, tvem = 0, tves = 0, tvemax = -INFINITY;
-    float tav = 0, tevp = 0;
+    for (int r = 0; r < W; r++) {
+        rank_ws *w = &ws[r];
+        w->idx = malloc(sizeof(uint32_t) * (w->B ? w->B : 1));
+        w->grads = malloc(sizeof(float) * np);
+        w->mo = malloc(sizeof(float) * mbmax * D);
+        w->mp = G ? malloc(sizeof(float) * mbmax * G) : NULL;
+        w->mm = ts[r]->has_masks ? malloc(sizeof(float) * mbmax * A) : NULL;
+        w->ma = malloc(sizeof(int32_t) * mbmax);
+        w->mlp = malloc(sizeof(float) * mbmax); w->madv = malloc(sizeof(float) * mbmax);
+        w->mret = malloc(sizeof(float) * mbmax); w->mov = malloc(sizeof(float) * mbmax);
+        w->madvn = malloc(sizeof(float) * mbmax);
+        w->tamin = INFINITY; w->tamax = -INFINITY; w->tvemax = -INFINITY;
+    }
+    /* W > 1: the combined minibatch (stats only) and the summed gradient */
+    const size_t cmax = W > 1 ? (size_t)W * mbmax : 1;
+    float *co = W > 1 ? malloc(sizeof(float) * cmax * D) : NULL;
+    float *cp = W > 1 && G ? malloc(sizeof(float) * cmax * G) : NULL;
+    float *cm = W > 1 && t0r->has_masks ? malloc(sizeof(float) * cmax * A) : NULL;
+    int32_t *ca = W > 1 ? malloc(sizeof(int32_t) * cmax) : NULL;
+    float *clp = W > 1 ? malloc(sizeof(float) * cmax) : NULL, *cadv = W > 1 ? malloc(sizeof(float) * cmax) : NULL;
+    float *cret = W > 1 ? malloc(sizeof(float) * cmax) : NULL, *cov = W > 1 ? malloc(sizeof(float) * cmax) : NULL;
+    float *gsum = malloc(sizeof(float) * np), *gstep = malloc(sizeof(float) * np);
+    float tp = 0, tv = 0, th = 0, tk = 0, tc = 0, tl = 0, tvm = 0, trm = 0;
+    float tvem = 0, tves = 0, tav = 0, tevp = 0;
     int nup = 0, epochs_run = 0, stop = 0;
     for (int ep = 0; ep < c->num_epochs && !stop; ep++) {
         epochs_run++;
-        for (size_t i = 0; i < B; i++) idx[i] = (uint32_t)i;  /* :1815 */
-        or_shuffle_u32(&t->rng, idx, B);                         /* :1816 */
-        size_t base = B / c->num_minibatches, rem = B % c->num_minibatches, start = 0;
+        for (int r = 0; r < W; r++) {
+            rank_ws *w = &ws[r];
+            for (size_t i = 0; i < w->B; i++) w->idx[i] = (uint32_t)i;  /* :1815 */
+            or_shuffle_u32(&ts[r]->rng, w->idx, w->B);                    /* :1816 */
+            w->start = 0;
+        }
+        const size_t B = ws[0].B;
+        size_t base = B / c->num_minibatches, rem = B % c->num_minibatches;
         for (int mbi = 0; mbi < c->num_minibatches; mbi++) {
             size_t sz = base + ((size_t)mbi < rem ? 1 : 0);
             if (sz == 0) continue;
-            for (size_t q = 0; q < sz; q++) {                    /* :1833-1857 gather */
-                size_t r = vidx ? vidx[idx[start + q]] : idx[start + q];
-                memcpy(mo + q * D, t->obs + r * D, sizeof(float) * D);
-                if (G) memcpy(mp + q * G, t->priv + r * G, sizeof(float) * G);
-                if (mm) memcpy(mm + q * A, t->masks + r * A, sizeof(float) * A);
-                ma[q] = t->actions[r]; mlp[q] = t->logp[r]; madv[q] = t->adv[r];
-                mret[q] = t->ret[r]; mov[q] = t->values[r];
+            for (int r = 0; r < W; r++) {
+                or_trainer *t = ts[r];
+                rank_ws *w = &ws[r];
+                w->sz = sz;
+                for (size_t q = 0; q < sz; q++) {                    /* :1833-1857 gather */
+                    size_t i = w->vidx ? w->vidx[w->idx[w->start + q]] : w->idx[w->start + q];
+                    memcpy(w->mo + q * D, t->obs + i * D, sizeof(float) * D);
+                    if (G) memcpy(w->mp + q * G, t->priv + i * G, sizeof(float) * G);
+                    if (w->mm) memcpy(w->mm + q * A, t->masks + i * A, sizeof(float) * A);
+                    w->ma[q] = t->actions[i]; w->mlp[q] = t->logp[i]; w->madv[q] = t->adv[i];
+                    w->mret[q] = t->ret[i]; w->mov[q] = t->values[i];
+                }
+                if (t->c.normalize_values) {                        /* ppo.rs:1859-1897 */
+                    or_popart_normalize(&t->pa, w->mret, sz, w->mret);
+                    or_popart_normalize(&t->pa, w->mov, sz, w->mov);
+                    for (size_t q = 0; q < sz; q++) {
+                        w->tsum += (double)w->mret[q]; w->tsq += (double)w->mret[q] * w->mret[q]; w->tcnt += 1.0;
+                    }
+                }
+                or_normalize_advantages(w->madv, sz, w->madvn, &w->am, &w->as, &w->amn, &w->amx);
+                or_minibatch_loss_grad(&t->net, t->params, sz, w->mo, w->mp, w->ma, w->mlp, w->madvn, w->mret,
+                                       w->mov, w->mm, c, t->c.ent_coef, w->grads, &w->st);
             }
-            if (t->c.normalize_values) {                        /* ppo.rs:1859-1897 */
-                or_popart_normalize(&t->pa, mret, sz, mret);
-                or_popart_normalize(&t->pa, mov, sz, mov);
-                for (size_t q = 0; q < sz; q++) { tsum += (double)mret[q]; tsq += (double)mret[q] * mret[q]; tcnt += 1.0; }
+            or_mb_stats stg = ws[0].st;
+            if (W == 1) {
+                memcpy(gstep, ws[0].grads, sizeof(float) * np);
+            } else {
+                /* the SUM all-reduce in rank order, then 1/W before clip + Adam */
+                memcpy(gsum, ws[0].grads, sizeof(float) * np);
+                for (int r = 1; r < W; r++)
+                    for (size_t k = 0; k < np; k++) gsum[k] += ws[r].grads[k];
+                const float inv_world = 1.0f / (float)W;
+                for (size_t k = 0; k < np; k++) gstep[k] = gsum[k] * inv_world;
+                /* the metrics of all ranks' rows together */
+                size_t o = 0;
+                for (int r = 0; r < W; r++, o += sz) {
+                    rank_ws *w = &ws[r];
+                    memcpy(co + o * D, w->mo, sizeof(float) * sz * D);
+                    if (G) memcpy(cp + o * G, w->mp, sizeof(float) * sz * G);
+                    if (cm) memcpy(cm + o * A, w->mm, sizeof(float) * sz * A);
+                    memcpy(ca + o, w->ma, sizeof(int32_t) * sz); memcpy(clp + o, w->mlp, sizeof(float) * sz);
+                    memcpy(cadv + o, w->madvn, sizeof(float) * sz); memcpy(cret + o, w->mret, sizeof(float) * sz);
+                    memcpy(cov + o, w->mov, sizeof(float) * sz);
+                }
+                or_minibatch_loss_grad(&t0r->net, t0r->params, o, co, cp, ca, clp, cadv, cret, cov, cm, c,
+                                       t0r->c.ent_coef, NULL, &stg);
             }
-            float am, as, amn, amx;
-            or_normalize_advantages(madv, sz, madvn, &am, &as, &amn, &amx);
-            or_mb_stats st;
-            or_minibatch_loss_grad(&t->net, t->params, sz, mo, mp, ma, mlp, madvn, mret, mov, mm, c,
-                                   t->c.ent_coef, grads, &st);
-            or_adam_step(&t->net, &t->adam, t->params, grads, t->c.lr, (float)c->max_grad_norm,
-                         c->adam_epsilon);
-            tp += st.policy_loss; tv += st.value_loss; th += st.entropy; tk += st.approx_kl;
-            tc += st.clip_fraction; tl += st.loss; tvm += st.value_mean; trm += st.returns_mean;
-            tam += am; tas += as;
-            tamin = fminf(tamin, amn); tamax = fmaxf(tamax, amx);
-            tvem += st.value_error_mean; tves += st.value_error_std;
-            tvemax = fmaxf(tvemax, st.value_error_max);
-            tav += st.avg_valid_actions; tevp += st.entropy_valid_pct;
+            for (int r = 0; r < W; r++) {
+                or_trainer *t = ts[r];
+                float *g = gstep;
+                if (r + 1 < W) { memcpy(gsum, gstep, sizeof(float) * np); g = gsum; }   /* the step clips in place */
+                or_adam_step(&t->net, &t->adam, t->params, g, t->c.lr, (float)c->max_grad_norm, c->adam_epsilon);
+                rank_ws *w = &ws[r];
+                w->tam += w->am; w->tas += w->as;
+                w->tamin = fminf(w->tamin, w->amn); w->tamax = fmaxf(w->tamax, w->amx);
+                w->tvemax = fmaxf(w->tvemax, w->st.value_error_max);
+                w->start += sz;
+            }
+            tp += stg.policy_loss; tv += stg.value_loss; th += stg.entropy; tk += stg.approx_kl;
+            tc += stg.clip_fraction; tl += stg.loss; tvm += stg.value_mean; trm += stg.returns_mean;
+            tvem += stg.value_error_mean; tves += stg.value_error_std;
+            tav += stg.avg_valid_actions; tevp += stg.entropy_valid_pct;
             nup++;
-            if (c->target_kl >= 0 && st.approx_kl > (float)c->target_kl) { stop = 1; break; } /* :2019-2023 */
-            start += sz;
+            if (c->target_kl >= 0 && stg.approx_kl > (float)c->target_kl) { stop = 1; break; } /* :2019-2023 */
         }
     }
-    if (m) {
+    for (int r = 0; r < W; r++) {
+        or_trainer *t = ts[r];
+        rank_ws *w = &ws[r];
+        or_update_metrics *m = ms ? &ms[r] : NULL;
+        if (!m) continue;
+        const size_t B = w->B;
         float n = (float)nup;
         memset(m, 0, sizeof *m);
         m->policy_loss = tp / n; m->value_loss = tv / n; m->entropy = th / n;
         m->entropy_scaled = m->entropy / logf((float)A);
         m->approx_kl = tk / n; m->clip_fraction = tc / n;
-        if (vidx) {                                                   /* ppo.rs:2047-2056 */
+        if (w->vidx) {                                                /* ppo.rs:2047-2056 */
             float *fv = malloc(sizeof(float) * (B ? B : 1)), *fr = malloc(sizeof(float) * (B ? B : 1));
-            for (size_t i = 0; i < B; i++) { fv[i] = t->values[vidx[i]]; fr[i] = t->ret[vidx[i]]; }
+            for (size_t i = 0; i < B; i++) { fv[i] = t->values[w->vidx[i]]; fr[i] = t->ret[w->vidx[i]]; }
             m->explained_variance = or_explained_variance(fv, fr, B);
             free(fv); free(fr);
         } else {
             m->explained_variance = or_explained_variance(t->values, t->ret, B);
         }
         m->total_loss = tl / n; m->value_mean = tvm / n; m->returns_mean = trm / n;
-        m->adv_mean_raw = tam / n; m->adv_std_raw = tas / n; m->adv_min_raw = tamin; m->adv_max_raw = tamax;
-        m->value_error_mean = tvem / n; m->value_error_std = tves / n; m->value_error_max = tvemax;
+        m->adv_mean_raw = w->tam / n; m->adv_std_raw = w->tas / n; m->adv_min_raw = w->tamin; m->adv_max_raw = w->tamax;
+        m->value_error_mean = tvem / n; m->value_error_std = tves / n; m->value_error_max = w->tvemax;
         m->avg_valid_actions = t->has_masks ? tav / n : 0.0f;
         m->entropy_valid_pct = t->has_masks ? tevp / n : 0.0f;
         m->num_updates = nup; m->epochs_run = epochs_run;
-        m->value_norm_rescale_mag = rescale_mag;
+        m->value_norm_rescale_mag = w->rescale_mag;
         m->value_norm_target_mean = m->value_norm_target_std = NAN;
-        if (tcnt > 0) {                                                /* ppo.rs:2061-2068 */
-            const double mean = tsum / tcnt, var = tsq / tcnt - mean * mean;
+        if (w->tcnt > 0) {                                             /* ppo.rs:2061-2068 */
+            const double mean = w->tsum / w->tcnt, var = w->tsq / w->tcnt - mean * mean;
             m->value_norm_target_mean = (float)mean;
             m->value_norm_target_std = (float)sqrt(var > 0.0 ? var : 0.0);
         }
     }
-    free(vidx); free(idx); free(grads); free(mo); free(mp); free(mm); free(ma); free(mlp); free(madv);
-    free(mret); free(mov); free(madvn);
-    t->phase_s[2] = now_s() - t0;
+    for (int r = 0; r < W; r++) {
+        rank_ws *w = &ws[r];
+        free(w->vidx); free(w->idx); free(w->grads); free(w->mo); free(w->mp); free(w->mm); free(w->ma);
+        free(w->mlp); free(w->madv); free(w->mret); free(w->mov); free(w->madvn);
+    }
+    free(ws); free(co); free(cp); free(cm); free(ca); free(clp); free(cadv); free(cret); free(cov);
+    free(gsum); free(gstep);
+    for (int r = 0; r < W; r++) ts[r]->phase_s[2] = now_s() - t0;
 }
+
+void or_trainer_update(or_trainer *t, or_update_metrics *m) { or_trainers_update(&t, 1, m); }
 
 size_t or_trainer_buffer(const or_trainer *t, const char *name, void *out, size_t bytes) {
     size_t TN = (size_t)t->T * t->N;
@@ -631,6 +735,21 @@ size_t or_trainer_buffer(const or_trainer *t, const char *name, void *out, size_
     if (!src) return 0;
     if (out && bytes >= n) memcpy(out, src, n);
     return n;
+}
+
+/* parity hook: overwrite a RolloutBuffer field (names as or_trainer_buffer) */
+int or_trainer_set_buffer(or_trainer *t, const char *name, const void *src, size_t bytes) {
+    size_t n = or_trainer_buffer(t, name, NULL, 0);
+    if (!n || n != bytes) return -1;
+    void *dst = NULL;
+    if (!strcmp(name, "values")) dst = t->values;
+    else if (!strcmp(name, "advantages")) dst = t->adv;
+    else if (!strcmp(name, "returns")) dst = t->ret;
+    else if (!strcmp(name, "rewards")) dst = t->rewards;
+    else if (!strcmp(name, "log_probs")) dst = t->logp;
+    if (!dst) return -1;
+    memcpy(dst, src, bytes);
+    return 0;
 }
 
 void or_trainer_obs_norm_state(const or_trainer *t, double *mean, double *var, double *count) {

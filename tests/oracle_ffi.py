@@ -110,7 +110,8 @@ class TrainCfg(C.Structure):
                 ("lr", C.c_double), ("ent_coef", C.c_double), ("reward_shaping", C.c_double),
                 ("ppo", PpoCfg), ("seed", C.c_uint64), ("threads", C.c_int),
                 ("cnn", C.c_int), ("num_conv", C.c_int), ("conv_ch", C.c_int * 4), ("ksize", C.c_int),
-                ("normalize_values", C.c_int), ("player_count", C.c_int), ("split_networks", C.c_int)]
+                ("normalize_values", C.c_int), ("player_count", C.c_int), ("split_networks", C.c_int),
+                ("env_seed_offset", C.c_uint64), ("rng_stream", C.c_uint64)]
 
 
 class UpdateMetrics(C.Structure):
@@ -222,6 +223,8 @@ def lib():
             "or_trainer_collect": (C.c_int, [C.c_void_p]),
             "or_trainer_gae": (None, [C.c_void_p]),
             "or_trainer_update": (None, [C.c_void_p, C.POINTER(UpdateMetrics)]),
+            "or_trainers_update": (None, [C.c_void_p, C.c_int, C.c_void_p]),
+            "or_trainer_set_buffer": (C.c_int, [C.c_void_p, C.c_char_p, C.c_void_p, C.c_size_t]),
             "or_trainer_buffer": (C.c_size_t, [C.c_void_p, C.c_char_p, C.c_void_p, C.c_size_t]),
             "or_trainer_obs_norm_state": (None, [C.c_void_p, f64, f64, C.POINTER(C.c_double)]),
             "or_trainer_ret_norm_state": (None, [C.c_void_p, f64, C.c_void_p]),
@@ -382,7 +385,7 @@ def train_cfg(env_kind=ENV_CARTPOLE, num_envs=8, num_steps=128, hidden=64, num_h
               ctde=False, critic_hidden=0, critic_num_hidden=0, normalize_obs=True,
               normalize_returns=True, return_clip=10.0, gamma=0.99, gae_lambda=0.95, lr=1e-3,
               ent_coef=0.01, reward_shaping=0.0, seed=42, threads=0, cnn=None, normalize_values=False,
-              player_count=0, split=False, **ppo):
+              player_count=0, split=False, env_seed_offset=0, rng_stream=0, **ppo):
     """cnn: None, or (conv_channels per layer, kernel_size); hidden / num_hidden are
     then cnn_fc_hidden_size / cnn_num_fc_layers"""
     extra = {}
@@ -391,6 +394,7 @@ def train_cfg(env_kind=ENV_CARTPOLE, num_envs=8, num_steps=128, hidden=64, num_h
         extra = dict(cnn=1, num_conv=len(ch), conv_ch=(C.c_int * 4)(*[ch[min(i, len(ch) - 1)] for i in range(4)]),
                      ksize=ks)
     return TrainCfg(**extra, normalize_values=int(normalize_values), player_count=player_count,
+                    env_seed_offset=env_seed_offset, rng_stream=rng_stream,
                     split_networks=int(split), env_kind=env_kind, num_envs=num_envs, num_steps=num_steps, hidden=hidden,
                     num_hidden=num_hidden, relu=int(relu), ctde=int(ctde), critic_hidden=critic_hidden,
                     critic_num_hidden=critic_num_hidden, normalize_obs=int(normalize_obs),
@@ -425,6 +429,17 @@ class Trainer:
         lib().or_trainer_update(self.h, C.byref(m))
         return {k: getattr(m, k) for k, _ in UpdateMetrics._fields_}
 
+    @staticmethod
+    def update_ranks(trainers):
+        """or_trainers_update: one data-parallel update of W rank trainers in lockstep
+        (per-rank shuffles and advantage statistics, gradients summed over the ranks
+        and scaled by 1/W before clip + Adam) -> W metric dicts"""
+        W = len(trainers)
+        hs = (C.c_void_p * W)(*[t.h for t in trainers])
+        ms = (UpdateMetrics * W)()
+        lib().or_trainers_update(hs, W, ms)
+        return [{k: getattr(m, k) for k, _ in UpdateMetrics._fields_} for m in ms]
+
     def params(self):
         out = np.zeros(self.n_params, np.float32)
         lib().or_trainer_get_params(self.h, out)
@@ -438,6 +453,10 @@ class Trainer:
         out = np.zeros(n // 4, dtype)
         lib().or_trainer_buffer(self.h, name.encode(), out.ctypes.data, n)
         return out
+
+    def set_buffer(self, name, arr):
+        a = np.ascontiguousarray(arr)
+        assert lib().or_trainer_set_buffer(self.h, name.encode(), a.ctypes.data, a.nbytes) == 0, name
 
     def obs_norm_state(self, dim):
         mean = np.zeros(dim, np.float64)

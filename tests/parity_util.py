@@ -5,7 +5,8 @@ Tolerances (north_star: "fp32 returns/advantages/loss within 1e-5 relative"):
   * every UpdateMetrics field (ppo.rs:1342-1369) within 1e-5 relative to
     max(|oracle|, floor): the floor is the magnitude of the summands for the
     signed means that cancel to ~0 — policy_loss / total_loss are means of
-    -A_n * ratio with E|A_n| ~ 0.8 (floor 1.0); adv_mean_raw is a mean of raw
+    -A_n * ratio, floor mean|A_n| of the update's normalized advantages
+    (summand_magnitude, ~0.8; its bound 1.0 where a test passes no advantages); adv_mean_raw is a mean of raw
     advantages (floor adv_std_raw); value_mean / returns_mean (floor
     value_error_mean + |returns_mean|).  Both sides accumulate in f64 per
     minibatch, so what is left is per-row f32 rounding of the later minibatches,
@@ -35,9 +36,20 @@ RTOL = 1e-5
 PARAM_RTOL, PARAM_ATOL = 1e-4, 2e-5
 
 
-def _floor(k, om):
-    if k in ("policy_loss", "total_loss"):
+def summand_magnitude(advantages):
+    """mean |A_n| of the normalized advantages (utils.rs:80-89 over the update's rows): the
+    size of the policy-loss summands -A_n * ratio (ratio ~ 1), against which the means
+    policy_loss / total_loss, which cancel to ~0, are compared"""
+    a = np.asarray(advantages, np.float64)
+    if a.size < 2:
         return 1.0
+    sd = a.std(ddof=1)
+    return float(np.abs(a - a.mean()).mean() / sd) if sd > 0 else 1.0
+
+
+def _floor(k, om, pl_mag):
+    if k in ("policy_loss", "total_loss"):
+        return pl_mag
     if k == "adv_mean_raw":
         return abs(om["adv_std_raw"])
     if k in ("value_mean", "returns_mean"):
@@ -80,10 +92,14 @@ def ev_f32_sequential(values, returns):
     return np.float32(np.float32(1) - np.float32(vres / vr))
 
 
-def assert_metrics_close(m, om, values=None, returns=None, skip=(), rtol=RTOL):
+def assert_metrics_close(m, om, values=None, returns=None, skip=(), rtol=RTOL, advantages=None):
     """All 19 UpdateMetrics fields plus num_updates / epochs_run.  values /
-    returns: the buffers the explained variance is taken over (learner rows
-    only under an opponent pool)."""
+    returns / advantages: the buffers the update trained on (learner rows only
+    under an opponent pool): the explained variance is taken over the first two,
+    the policy-loss summand magnitude (the floor of policy_loss / total_loss) over
+    the advantages; without them the floor is its bound, E|A_n| <= 1 for
+    unit-variance normalized advantages."""
+    pl_mag = 1.0 if advantages is None else summand_magnitude(advantages)
     assert m["num_updates"] == om["num_updates"], (m["num_updates"], om["num_updates"])
     assert m["epochs_run"] == om["epochs_run"], (m["epochs_run"], om["epochs_run"])
     bad = []
@@ -99,7 +115,7 @@ def assert_metrics_close(m, om, values=None, returns=None, skip=(), rtol=RTOL):
             continue
         if np.isnan(o) and np.isnan(d):
             continue
-        tol = rtol * max(abs(o), _floor(k, om))
+        tol = rtol * max(abs(o), _floor(k, om, pl_mag))
         if not abs(d - o) <= tol:
             bad.append((k, d, o, abs(d - o) / max(abs(o), 1e-30)))
     # PopArt (ppo.rs:2061-2068): NaN = None on both sides
@@ -124,8 +140,9 @@ def bits(a):
     return np.ascontiguousarray(a, np.float32).view(np.uint32)
 
 
-def oracle_train_cfg(cfg, threads=0):
-    """the oracle's TrainCfg for a bppo config dict (CartPole, Connect Four, Liar's Dice; MLP / CTDE)"""
+def oracle_train_cfg(cfg, threads=0, rank=0, world=1):
+    """the oracle's TrainCfg for a bppo config dict (CartPole, Connect Four, Liar's Dice; MLP / CTDE);
+    rank / world: that rank's shard of a data-parallel job (bppo.dist.shard)"""
     kind = {"cartpole": O.ENV_CARTPOLE, "connect_four": O.ENV_CONNECT_FOUR, "liars_dice": O.ENV_LIARS_DICE}[cfg["env"]]
     nr = cfg["normalize_returns"]
     if nr is None:
@@ -139,7 +156,9 @@ def oracle_train_cfg(cfg, threads=0):
                        reward_shaping=cfg["reward_shaping_coef"], num_epochs=cfg["num_epochs"],
                        num_minibatches=cfg["num_minibatches"], clip=cfg["clip_epsilon"], value_coef=cfg["value_coef"],
                        max_grad_norm=cfg["max_grad_norm"], target_kl=cfg["target_kl"], threads=threads,
-                       split=bool(cfg.get("split_networks")))
+                       split=bool(cfg.get("split_networks")), clip_value=bool(cfg.get("clip_value")),
+                       env_seed_offset=rank * cfg["num_envs"] if world > 1 else 0,
+                       rng_stream=rank if world > 1 else 0)
 
 
 def cartpole_pair(N, T, preset="cartpole", seed=42, init_seed=1, **kw):

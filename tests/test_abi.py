@@ -55,3 +55,91 @@ def test_host_libm_path_without_gpu():
     y = np.zeros_like(x)
     assert L.lib().bppo_debug_libm(0, 0, x.ctypes.data, y.ctypes.data, x.size) == 0
     assert np.allclose(y, np.log(x), rtol=1e-6, atol=1e-7)
+
+
+# ------------------------------------------------------------ struct layouts ---
+_C_TYPES = {"int32_t": ("i32", C.c_int32), "float": ("f32", C.c_float), "double": ("f64", C.c_double),
+            "uint64_t": ("u64", C.c_uint64)}
+_CONSTS = {"BPPO_MAX_PLAYERS": 6}
+
+
+def _header_struct(name):
+    """[(field, type, array_len or 0)] of `typedef struct { ... } name;` in include/bppo.h"""
+    txt = open(os.path.join(ROOT, "include", "bppo.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    body = re.search(r"typedef struct \{([^}]*)\}\s*%s;" % name, txt).group(1)
+    out = []
+    for decl in body.split(";"):
+        decl = decl.strip()
+        if not decl:
+            continue
+        ty, rest = decl.split(None, 1)
+        for f in rest.split(","):
+            m = re.fullmatch(r"\s*(\w+)\s*(?:\[(\w+)\])?\s*", f)
+            n = 0 if m.group(2) is None else int(_CONSTS.get(m.group(2), m.group(2)))
+            out.append((m.group(1), _C_TYPES[ty][0], n))
+    return out
+
+
+def _ctypes_struct(cls):
+    inv = {v[1]: v[0] for v in _C_TYPES.values()}
+    out = []
+    for f, t in cls._fields_:
+        if hasattr(t, "_length_"):
+            out.append((f, inv[t._type_], t._length_))
+        else:
+            out.append((f, inv[t], 0))
+    return out
+
+
+def _rust_struct(name):
+    txt = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    i = txt.index("pub struct %s {" % name) + len("pub struct %s {" % name)
+    body = re.sub(r"//[^\n]*", "", txt[i:txt.index("}", i)])
+    out = []
+    for m in re.finditer(r"pub (\w+):\s*(\[\s*(\w+)\s*;\s*(\d+)\s*\]|\w+)", body):
+        if m.group(3):
+            out.append((m.group(1), m.group(3), int(m.group(4))))
+        else:
+            out.append((m.group(1), m.group(2), 0))
+    return out
+
+
+@pytest.mark.parametrize("c_name,rust_name,attr", [
+    ("bppo_config", "BppoConfig", "Config"), ("bppo_update_metrics", "BppoUpdateMetrics", "UpdateMetrics"),
+    ("bppo_episode", "BppoEpisode", "Episode"), ("bppo_rollout_info", "BppoRolloutInfo", "RolloutInfo")])
+def test_struct_layouts_match_header(so, c_name, rust_name, attr):
+    """include/bppo.h, the ctypes binding (bppo/_lib.py) and the Rust binding in
+    INTEGRATION.md list the same fields, in the same order, with the same types; and the
+    library's sizeof exports equal the ctypes sizes."""
+    import bppo._lib as L
+    hdr = _header_struct(c_name)
+    assert _ctypes_struct(getattr(L, attr)) == hdr
+    assert _rust_struct(rust_name) == hdr
+    size_fn = {"bppo_config": "bppo_config_size", "bppo_update_metrics": "bppo_update_metrics_size",
+               "bppo_episode": "bppo_episode_size", "bppo_rollout_info": "bppo_rollout_info_size"}[c_name]
+    assert getattr(L.lib(), size_fn)() == C.sizeof(getattr(L, attr))
+
+
+@pytest.mark.parametrize("preset,over", [
+    ("cartpole", dict(split_networks=True, num_hidden=8)),                         # 2 * 8 + 2 = 18 layers
+    ("connect_four", dict(hidden_size=32, num_hidden=15)),                         # 17
+    ("liars_dice_ctde", dict(num_hidden=8, critic_num_hidden=7)),                  # 17
+    ("connect_four", dict(network_type="cnn", split_networks=True, num_conv_layers=4,
+                          conv_channels=[4], cnn_num_fc_layers=4))])               # 2 * 8 + 2 = 18
+def test_create_rejects_nets_over_16_layers_before_any_hip_call(so, preset, over):
+    """NetLayout holds 16 layers; deeper nets (any net type) are refused with
+    BPPO_ERR_UNSUPPORTED by bppo_create's configuration check, which runs before the
+    first HIP call (so this runs without a GPU)."""
+    import bppo
+    import bppo._lib as L
+    from bppo.host import to_struct
+    cfg = bppo.make_config(preset, num_envs=8, num_steps=4, **over)
+    s = to_struct(cfg)
+    h = C.c_void_p()
+    st = L.lib().bppo_create(C.byref(s), 0, None, C.byref(h))
+    try:
+        assert st == L.ERR_UNSUPPORTED, (st, L.lib().bppo_last_error(h))
+        assert b"16 layers" in L.lib().bppo_last_error(h)
+    finally:
+        L.lib().bppo_destroy(h)

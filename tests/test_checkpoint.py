@@ -99,6 +99,29 @@ def test_optimizer_record_round_trip():
     assert [rec["item"][i]["momentum"]["time"] for i in ids] == list(steps)
 
 
+@pytest.mark.parametrize("preset,over", [("cartpole", {}), ("liars_dice_ctde", {}),
+                                         ("connect_four", {"network_type": "cnn"}),
+                                         ("connect_four", {"network_type": "cnn", "split_networks": True})])
+def test_optimizer_moment_shapes_match_model_record(preset, over):
+    """each Adam moment has the shape of its parameter in the model record
+    (Conv2d weights [Cout, Cin, k, k], critic conv stacks included), as Burn's state
+    mirrors the gradient; the flat moments round-trip through the record."""
+    cfg = bppo.make_config(preset, **over)
+    p = bppo.orthogonal_init(cfg, seed=1)
+    rng = np.random.default_rng(1)
+    m1, m2 = rng.normal(size=p.size).astype(np.float32), rng.random(p.size).astype(np.float32)
+    steps = np.arange(2 * len(bppo.host.layer_shapes(cfg)[0]), dtype=np.int32)
+    rec, ids = K.optimizer_record(cfg, m1, m2, steps)
+    model = K.model_record(cfg, p)["item"]
+    params = [lin[k] for lin in K._linears_in_order(model) for k in ("weight", "bias")]
+    assert ids == [q["id"] for q in params]
+    for q in params:
+        st = rec["item"][q["id"]]["momentum"]
+        assert st["moment_1"]["shape"] == q["param"]["shape"] == st["moment_2"]["shape"]
+    a1, a2, st = K.optimizer_arrays(rec, ids)
+    assert np.array_equal(a1, m1) and np.array_equal(a2, m2) and np.array_equal(st, steps)
+
+
 def test_optimizer_read_with_the_model_record_ids(tmp_path):
     """Burn keys optimizer.mpk by the model's random ParamIds: a record written
     with ids unknown to this module loads through the ids of model.mpk beside it."""

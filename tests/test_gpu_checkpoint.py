@@ -86,7 +86,7 @@ def test_save_resume_continues_like_the_oracle(tmp_path):
     md = bppo.ppo_update(tr2.ctx, 1e-3, 0.01)
     mo = ot2.update()
     assert tr2.ctx.rng_pos() == ot2.rng_pos()
-    assert_metrics_close(md, mo, values=ot2.buffer("values"), returns=ot2.buffer("returns"))
+    assert_metrics_close(md, mo, values=ot2.buffer("values"), returns=ot2.buffer("returns"), advantages=ot2.buffer("advantages"))
     assert_params_close(tr2.model.get_params(), ot2.params())
     tr2.close(); ot2.close()
 

@@ -94,7 +94,7 @@ def test_cnn_rollout_update_second_rollout(net, N, T, rtol):
     m = bppo.ppo_update(tr.ctx, bppo.schedule_get(cfg["learning_rate"], 0), bppo.schedule_get(cfg["entropy_coef"], 0))
     om = ot.update()
     assert tr.ctx.rng_pos() == ot.rng_pos()
-    assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"), rtol=rtol)
+    assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"), rtol=rtol, advantages=ot.buffer("advantages"))
     np.testing.assert_allclose(tr.model.get_params(), ot.params(), rtol=PARAM_RTOL,
                                atol=PARAM_ATOL if rtol == 1e-5 else 5e-4)
     tr.model.set_params(ot.params())
@@ -139,7 +139,7 @@ def test_cnn_split_networks(net):
                             bppo.schedule_get(cfg["entropy_coef"], 0))
         om = ot.update()
         assert tr.ctx.rng_pos() == ot.rng_pos()
-        assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"))
+        assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"), advantages=ot.buffer("advantages"))
         np.testing.assert_allclose(tr.model.get_params(), ot.params(), rtol=PARAM_RTOL, atol=PARAM_ATOL)
         tr.model.set_params(ot.params())
         bppo.collect_rollouts(tr.ctx); ot.collect()

@@ -33,7 +33,7 @@ import pytest
 
 import bppo
 import oracle_ffi as O
-from parity_util import METRICS, PARAM_ATOL, PARAM_RTOL, RTOL, _floor, oracle_train_cfg
+from parity_util import METRICS, PARAM_ATOL, PARAM_RTOL, RTOL, _floor, oracle_train_cfg, summand_magnitude
 
 pytestmark = pytest.mark.gpu
 
@@ -106,6 +106,7 @@ def test_bench_path_matches_fullsize_oracle(case):
         assert m["num_updates"] == int(fx["num_updates"]) and m["epochs_run"] == int(fx["epochs_run"])
         assert sha(ctx.buffer("perm", np.uint32)) == str(fx["sha_perm"])
         om = dict(zip(METRICS, (float(v) for v in fx["metrics"])))
+        pl_mag = summand_magnitude(ctx.buffer("advantages"))
         bad = []
         for k in METRICS:
             d, o = float(m[k]), om[k]
@@ -113,7 +114,7 @@ def test_bench_path_matches_fullsize_oracle(case):
                 if abs(d - float(fx["ev_exact"])) > 1e-6:
                     bad.append((k, d, float(fx["ev_exact"])))
                 continue
-            tol = RTOL * max(abs(o), _floor(k, om))
+            tol = RTOL * max(abs(o), _floor(k, om, pl_mag))
             if k == "clip_fraction":
                 # a count: rows whose ratio sits within rounding of 1 +- eps flip when the
                 # later minibatches' parameters differ in the last bits; allow 4 per minibatch
@@ -169,7 +170,8 @@ def test_updates_without_injection_action_agreement():
             if first_diff is None and not np.array_equal(da, oa):
                 first_diff = k
             om = ot.update()
-            rel = max(abs(float(m[q]) - om[q]) / max(abs(om[q]), _floor(q, om), 1e-6)
+            mag = summand_magnitude(ot.buffer("advantages"))
+            rel = max(abs(float(m[q]) - om[q]) / max(abs(om[q]), _floor(q, om, mag), 1e-6)
                       for q in METRICS if q != "explained_variance")
             worst.append(rel)
         print(f"\naction agreement per update: {agree}\nfirst differing rollout: {first_diff}\n"

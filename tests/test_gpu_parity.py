@@ -223,7 +223,7 @@ def test_update_matches_oracle_and_rng_chain_exact():
     perm = tr.ctx.buffer("perm", np.uint32)
     p_words = ot.rng_pos()
     assert sorted(perm.tolist()) == list(range(N * T))
-    assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"))
+    assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"), advantages=ot.buffer("advantages"))
     assert_params_close(tr.model.get_params(), ot.params())
     tr.close(); ot.close()
 
@@ -301,7 +301,7 @@ def test_tanh_update_matches_oracle(H, NL):
     m = bppo.ppo_update(tr.ctx, 1e-3, 0.01)
     om = ot.update()
     assert tr.ctx.rng_pos() == ot.rng_pos()
-    assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"))
+    assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"), advantages=ot.buffer("advantages"))
     assert_params_close(tr.model.get_params(), ot.params())
     tr.close(); ot.close()
 

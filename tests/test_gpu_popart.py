@@ -71,7 +71,7 @@ def _rounds(cfg, tr, ot, cmp, rounds=3):
         assert dp[2] == op[2] and dp[3] == op[3]
         np.testing.assert_allclose(dp[:2], op[:2], rtol=1e-12)
         assert not np.isnan(m["value_norm_rescale_mag"])
-        assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"))
+        assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"), advantages=ot.buffer("advantages"))
         assert_params_close(tr.model.get_params(), ot.params())
 
 

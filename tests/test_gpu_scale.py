@@ -64,7 +64,7 @@ def test_cfgA_test_preset_two_updates():
         cmp_cartpole_rollout(tr, ot)
         bppo.compute_gae(tr.ctx); ot.gae()
         m, om, _ = _update_pair(cfg, tr, ot)
-        assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"))
+        assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"), advantages=ot.buffer("advantages"))
         assert_params_close(tr.model.get_params(), ot.params())
     tr.close(); ot.close()
 
@@ -76,7 +76,7 @@ def test_relu_valu_shapes(H, NL):
     cmp_cartpole_rollout(tr, ot)
     bppo.compute_gae(tr.ctx); ot.gae()
     m, om, _ = _update_pair(cfg, tr, ot)
-    assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"))
+    assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"), advantages=ot.buffer("advantages"))
     assert_params_close(tr.model.get_params(), ot.params())
     tr.close(); ot.close()
 
@@ -119,7 +119,7 @@ def test_cfgB_update_at_262k_row_minibatches():
     perm, end = _last_perm(cfg["seed"], start, N * T, cfg["num_epochs"])
     assert end == tr.ctx.rng_pos()
     assert np.array_equal(tr.ctx.buffer("perm", np.uint32), perm)
-    assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"))
+    assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"), advantages=ot.buffer("advantages"))
     assert_params_close(tr.model.get_params(), ot.params())
     tr.close(); ot.close()
 
@@ -179,7 +179,7 @@ def test_wide_at_full_gemm_tiles(env, N, T, ctde):
     bppo.compute_gae(tr.ctx); ot.gae()
     assert np.array_equal(bits(tr.buffer.advantages.reshape(-1)), bits(ot.buffer("advantages")))
     m, om, _ = _update_pair(cfg, tr, ot, inject=False)
-    assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"))
+    assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"), advantages=ot.buffer("advantages"))
     assert_params_close(tr.model.get_params(), ot.params())
     tr.model.set_params(ot.params())
     bppo.collect_rollouts(tr.ctx); ot.collect()
@@ -221,7 +221,7 @@ def test_opponent_pool_at_scale():
     assert np.array_equal(bits(tr.buffer.advantages.reshape(-1)), bits(ot.buffer("advantages")))
     m, om, _ = _update_pair(cfg, tr, ot, inject=False)
     v = ot.buffer("valid") > 0.5
-    assert_metrics_close(m, om, values=ot.buffer("values")[v], returns=ot.buffer("returns")[v])
+    assert_metrics_close(m, om, values=ot.buffer("values")[v], returns=ot.buffer("returns")[v], advantages=ot.buffer("advantages")[v])
     assert_params_close(tr.model.get_params(), ot.params())
     tr.close(); ot.close()
 

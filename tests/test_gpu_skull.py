@@ -126,7 +126,7 @@ def test_rollout_gae_update_second_rollout(N, T, ctde, players):
     m = bppo.ppo_update(tr.ctx, bppo.schedule_get(cfg["learning_rate"], 0), bppo.schedule_get(cfg["entropy_coef"], 0))
     om = ot.update()
     assert tr.ctx.rng_pos() == ot.rng_pos()
-    assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"))
+    assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"), advantages=ot.buffer("advantages"))
     assert_params_close(tr.model.get_params(), ot.params())
     tr.model.set_params(ot.params())
     bppo.collect_rollouts(tr.ctx); ot.collect()
@@ -166,7 +166,7 @@ def test_opponent_pool_rollout_update(players, ctde):
         om = ot.update()
         assert tr.ctx.rng_pos() == ot.rng_pos()
         vm = ot.buffer("valid") > 0.5
-        assert_metrics_close(m, om, values=ot.buffer("values")[vm], returns=ot.buffer("returns")[vm])
+        assert_metrics_close(m, om, values=ot.buffer("values")[vm], returns=ot.buffer("returns")[vm], advantages=ot.buffer("advantages")[vm])
         assert_params_close(tr.model.get_params(), ot.params())
         tr.model.set_params(ot.params())
     tr.close(); ot.close()

@@ -42,7 +42,7 @@ def _update(cfg, tr, ot, inject):
     m = bppo.ppo_update(tr.ctx, bppo.schedule_get(cfg["learning_rate"], 0), bppo.schedule_get(cfg["entropy_coef"], 0))
     om = ot.update()
     assert tr.ctx.rng_pos() == ot.rng_pos()
-    assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"))
+    assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"), advantages=ot.buffer("advantages"))
     assert_params_close(tr.model.get_params(), ot.params())
 
 

@@ -188,7 +188,7 @@ def test_update_then_second_rollout(env, N, T, ctde):
     m = bppo.ppo_update(tr.ctx, lr, ent)
     om = ot.update()
     assert tr.ctx.rng_pos() == ot.rng_pos()
-    assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"))
+    assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"), advantages=ot.buffer("advantages"))
     assert_params_close(tr.model.get_params(), ot.params())
     # the next rollout from the oracle's parameters is bit-identical again
     tr.model.set_params(ot.params())
@@ -226,7 +226,7 @@ def test_tanh_rollout_update_second_rollout(env, N, T, ctde):
     assert np.array_equal(_bits(tr.buffer.advantages.reshape(-1)), _bits(ot.buffer("advantages")))
     m = bppo.ppo_update(tr.ctx, bppo.schedule_get(cfg["learning_rate"], 0), bppo.schedule_get(cfg["entropy_coef"], 0))
     om = ot.update()
-    assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"))
+    assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"), advantages=ot.buffer("advantages"))
     assert_params_close(tr.model.get_params(), ot.params())
     tr.model.set_params(ot.params())
     bppo.collect_rollouts(tr.ctx); ot.collect()
@@ -261,7 +261,7 @@ def test_normalizers_rollout_update_second_rollout(env, N, T, ctde):
     np.testing.assert_allclose(tr.buffer.advantages.reshape(-1), ot.buffer("advantages"), rtol=1e-5, atol=1e-6)
     m_ = bppo.ppo_update(tr.ctx, bppo.schedule_get(cfg["learning_rate"], 0), bppo.schedule_get(cfg["entropy_coef"], 0))
     om = ot.update()
-    assert_metrics_close(m_, om, values=ot.buffer("values"), returns=ot.buffer("returns"))
+    assert_metrics_close(m_, om, values=ot.buffer("values"), returns=ot.buffer("returns"), advantages=ot.buffer("advantages"))
     # second rollout from the oracle's params and normalizer state: normalized
     # observations (now count >= 2) and rewards bit-exact again
     tr.model.set_params(ot.params())
@@ -329,7 +329,7 @@ def test_opponent_pool_rollout_update_bit_exact(env, N, T, ctde, n_opp, K, norm)
         om = ot.update()
         assert tr.ctx.rng_pos() == ot.rng_pos()     # shuffles over the learner rows only
         vm = ot.buffer("valid") > 0.5
-        assert_metrics_close(m, om, values=ot.buffer("values")[vm], returns=ot.buffer("returns")[vm])
+        assert_metrics_close(m, om, values=ot.buffer("values")[vm], returns=ot.buffer("returns")[vm], advantages=ot.buffer("advantages")[vm])
         assert_params_close(tr.model.get_params(), ot.params())
         tr.model.set_params(ot.params())
     tr.close(); ot.close()

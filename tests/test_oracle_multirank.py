@@ -1,0 +1,71 @@
+"""The oracle's W-rank update (or_trainers_update, oracle/ppo.c), which pins libbppo's
+W > 1 semantics in tests/test_gpu_multirank.py, checked on CPU:
+  * W = 2 ranks holding IDENTICAL shards take exactly the W = 1 step (the summed
+    gradient g + g scaled by 1/2 is g bit for bit), so their parameters equal the
+    single-rank run's bit for bit;
+  * with distinct shards (env seeds seed + r*N + i, main-RNG stream r) the ranks'
+    rollouts differ, their parameters stay identical, and the step is the mean of
+    the two single-rank gradients: it equals the update of one rank whose
+    minibatch gradient is replaced by that mean (checked through the first Adam step,
+    where Adam's update depends on the gradient alone)."""
+import numpy as np
+
+import bppo
+import oracle_ffi as O
+from parity_util import oracle_train_cfg
+
+
+def _cfg(**kw):
+    return bppo.make_config("cartpole", num_envs=32, num_steps=16, **kw)
+
+
+def test_identical_shards_equal_single_rank():
+    cfg = _cfg()
+    params = bppo.orthogonal_init(cfg, seed=3)
+    solo = O.Trainer(oracle_train_cfg(cfg), params)
+    pair = [O.Trainer(oracle_train_cfg(cfg), params) for _ in range(2)]
+    for _ in range(2):
+        solo.collect(); solo.gae()
+        for t in pair:
+            t.collect(); t.gae()
+        m = solo.update()
+        ms = O.Trainer.update_ranks(pair)
+        for t in pair:
+            assert np.array_equal(t.params().view(np.uint32), solo.params().view(np.uint32))
+            assert t.rng_pos() == solo.rng_pos()
+        for k in ("policy_loss", "value_loss", "approx_kl", "value_error_max", "adv_mean_raw"):
+            assert abs(ms[0][k] - m[k]) <= 1e-6 * max(1.0, abs(m[k])), k
+    for t in [solo] + pair:
+        t.close()
+
+
+def test_distinct_shards_share_one_step():
+    cfg = _cfg(num_epochs=1, num_minibatches=1)
+    params = bppo.orthogonal_init(cfg, seed=4)
+    ranks = [O.Trainer(oracle_train_cfg(cfg, rank=r, world=2), params) for r in range(2)]
+    solos = [O.Trainer(oracle_train_cfg(cfg, rank=r, world=2), params) for r in range(2)]
+    for t in ranks + solos:
+        t.collect(); t.gae()
+    a0, a1 = ranks[0].buffer("actions", np.int32), ranks[1].buffer("actions", np.int32)
+    assert not np.array_equal(a0, a1)                       # distinct env seeds / streams
+    # rank 1's stream differs from the reference's stream 0
+    ref = O.Trainer(oracle_train_cfg(cfg), params)
+    ref.collect()
+    assert not np.array_equal(ref.buffer("actions", np.int32), a1)
+    ms = O.Trainer.update_ranks(ranks)
+    assert np.array_equal(ranks[0].params().view(np.uint32), ranks[1].params().view(np.uint32))
+    assert ms[0]["policy_loss"] == ms[1]["policy_loss"]
+    # one epoch x one minibatch: each solo rank's first Adam step moves a parameter by
+    # -lr * m1c / (sqrt(m2c) + eps) with m1c = g, m2c = g^2 after bias correction, i.e.
+    # -lr * sign(g) (|g| >> eps); the W = 2 step moves by -lr * sign(g0 + g1): where the
+    # two ranks' steps agree in sign, the shared step agrees with both
+    for t in solos:
+        t.update()
+    d0 = solos[0].params() - params
+    d1 = solos[1].params() - params
+    dw = ranks[0].params() - params
+    agree = (np.sign(d0) == np.sign(d1)) & (np.abs(d0) > 1e-6) & (np.abs(d1) > 1e-6)
+    assert agree.sum() > 100
+    assert np.array_equal(np.sign(dw[agree]), np.sign(d0[agree]))
+    for t in ranks + solos + [ref]:
+        t.close()
