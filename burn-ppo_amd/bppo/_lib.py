@@ -84,6 +84,7 @@ EXPORTS = (
     "bppo_rng_fill_bytes", "bppo_rng_from_seed", "bppo_rng_key_get", "bppo_num_param_tensors",
     "bppo_optimizer_get", "bppo_optimizer_set", "bppo_popart_get", "bppo_popart_set",
     "bppo_config_size", "bppo_update_metrics_size", "bppo_episode_size", "bppo_rollout_info_size",
+    "bppo_set_explained_variance_mode",
 )
 
 # ABI struct -> the library's sizeof export (checked when the library loads)
@@ -164,6 +165,7 @@ def lib():
         "bppo_optimizer_set": (i32, [vp, vp, vp, vp, sz]),
         "bppo_popart_get": (i32, [vp, vp]),
         "bppo_popart_set": (i32, [vp, vp]),
+        "bppo_set_explained_variance_mode": (i32, [vp, i32]),
     }
     for name in STRUCT_SIZES:
         sig[name] = (sz, [])

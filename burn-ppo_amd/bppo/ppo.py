@@ -158,6 +158,11 @@ class Context:
         self._chk(L.lib().bppo_last_kernel_ms(self.h, name.encode(), C.byref(f)))
         return f.value
 
+    def set_explained_variance_mode(self, mode):
+        """0: f64 sums on the device (default); 1: the reference's f32 sequential sums,
+        bit for bit (ppo.rs:1268-1294), on a host thread beside the update"""
+        self._chk(L.lib().bppo_set_explained_variance_mode(self.h, int(mode)))
+
     def set_allreduce(self, fn, world, stream_ordered=False):
         """fn(device_ptr:int, n:int) -> None must leave the SUM over ranks in place.
         stream_ordered: fn only enqueues the reduction on `self.stream` (no host

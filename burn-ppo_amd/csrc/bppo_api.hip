@@ -2,6 +2,7 @@
 // host-side orchestration of one update (collect_rollouts -> bootstrap + GAE ->
 // ppo_update, main.rs:724-963), the rand-0.8 shuffle chain thread, parity hooks.
 #include <algorithm>
+#include <pthread.h>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -388,6 +389,11 @@ extern "C" bppo_status bppo_create(const bppo_config *cfg, int hip_device, void 
 
 extern "C" void bppo_destroy(bppo_ctx *c) {
     if (!c) return;
+    if (c->ev_thread.joinable()) c->ev_thread.join();
+    if (c->ev_stream) { (void)hipStreamSynchronize(c->ev_stream); (void)hipStreamDestroy(c->ev_stream); }
+    if (c->ev_gae) (void)hipEventDestroy(c->ev_gae);
+    if (c->ev_copied) (void)hipEventDestroy(c->ev_copied);
+    for (float *h : {c->h_ev_v, c->h_ev_r, c->h_ev_valid}) if (h) (void)hipHostFree(h);
     if (c->fy_stream) (void)hipStreamSynchronize(c->fy_stream);   // reads the engine's J buffers
     c->shuf.shutdown();
     if (c->stream) (void)hipStreamSynchronize(c->stream);
@@ -893,6 +899,71 @@ extern "C" bppo_status bppo_compute_gae(bppo_ctx *c) {
     return BPPO_OK;
 }
 
+// ppo.rs:1268-1294 compute_explained_variance as the reference computes it: f32
+// iterator sums in order (each chain sequential; the two independent chains of a
+// round are interleaved only for instruction-level parallelism), population
+// variances, no fma contraction ((r - mean).powi(2) is a multiply, then the add)
+static float ev_reference_f32(const float *v, const float *r, const float *valid, size_t n_all) {
+#pragma clang fp contract(off)
+    size_t n_ = 0;
+    float s_r = 0.0f, s_res = 0.0f;
+    for (size_t i = 0; i < n_all; i++) {
+        if (valid && !(valid[i] > 0.5f)) continue;     // opponent pool: learner rows (ppo.rs:2047-2056)
+        s_r += r[i];
+        s_res += r[i] - v[i];
+        n_++;
+    }
+    const float n = (float)n_;
+    if (n < 2.0f) return 0.0f;
+    const float mr = s_r / n, mres = s_res / n;
+    float q_r = 0.0f, q_res = 0.0f;
+    for (size_t i = 0; i < n_all; i++) {
+        if (valid && !(valid[i] > 0.5f)) continue;
+        const float d = r[i] - mr;
+        q_r += d * d;
+        const float e = (r[i] - v[i]) - mres;
+        q_res += e * e;
+    }
+    const float vr = q_r / n;
+    if (vr < 1e-8f) return 0.0f;
+    return 1.0f - (q_res / n) / vr;
+}
+
+extern "C" bppo_status bppo_set_explained_variance_mode(bppo_ctx *c, int32_t mode) {
+    if (!c || mode < 0 || mode > 1) return BPPO_ERR_ARG;
+    if (mode == 1 && !c->h_ev_v) {
+        const size_t TN = (size_t)c->T * c->N;
+        BPPO_HIP(c, hipStreamCreateWithFlags(&c->ev_stream, hipStreamNonBlocking));
+        BPPO_HIP(c, hipEventCreateWithFlags(&c->ev_gae, hipEventDisableTiming));
+        BPPO_HIP(c, hipEventCreateWithFlags(&c->ev_copied, hipEventDisableTiming | hipEventBlockingSync));
+        BPPO_HIP(c, hipHostMalloc((void **)&c->h_ev_v, TN * 4, hipHostMallocDefault));
+        BPPO_HIP(c, hipHostMalloc((void **)&c->h_ev_r, TN * 4, hipHostMallocDefault));
+        BPPO_HIP(c, hipHostMalloc((void **)&c->h_ev_valid, TN * 4, hipHostMallocDefault));
+    }
+    c->ev_mode = mode;
+    return BPPO_OK;
+}
+
+// mode 1: copy the buffers the metric reads (stream order: after GAE, before anything
+// later rewrites them) and sum them on a host thread while the update runs
+static bppo_status ev_reference_begin(bppo_ctx *c, const float *d_valid) {
+    const size_t TN = (size_t)c->T * c->N;
+    BPPO_HIP(c, hipEventRecord(c->ev_gae, c->stream));
+    BPPO_HIP(c, hipStreamWaitEvent(c->ev_stream, c->ev_gae, 0));
+    BPPO_HIP(c, hipMemcpyAsync(c->h_ev_v, c->d_val, TN * 4, hipMemcpyDeviceToHost, c->ev_stream));
+    BPPO_HIP(c, hipMemcpyAsync(c->h_ev_r, c->d_ret, TN * 4, hipMemcpyDeviceToHost, c->ev_stream));
+    if (d_valid) BPPO_HIP(c, hipMemcpyAsync(c->h_ev_valid, d_valid, TN * 4, hipMemcpyDeviceToHost, c->ev_stream));
+    BPPO_HIP(c, hipEventRecord(c->ev_copied, c->ev_stream));
+    const bool vf = d_valid != nullptr;
+    if (c->ev_thread.joinable()) c->ev_thread.join();      // an update that returned early
+    c->ev_thread = std::thread([c, TN, vf]() {
+        (void)pthread_setname_np(pthread_self(), "bppo-ev");
+        (void)hipEventSynchronize(c->ev_copied);
+        c->ev_ref = ev_reference_f32(c->h_ev_v, c->h_ev_r, vf ? c->h_ev_valid : nullptr, TN);
+    });
+    return BPPO_OK;
+}
+
 // ppo_update (ppo.rs:1661-2112)
 extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, bppo_update_metrics *m) {
     if (!c || !c->gae_done) { if (c) c->err = "ppo_update before compute_gae"; return BPPO_ERR_ARG; }
@@ -922,6 +993,7 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
     bool stop = false;
     double wait_ms = 0.0;
     tm_begin(c, TM_UPDATE);
+    if (c->ev_mode == 1) TRY(ev_reference_begin(c, opp ? c->d_valid : nullptr));
     TRY(popart_update_begin(c, opp ? c->d_valid : nullptr));   // ppo.rs:1787-1808
     if (c->d_rowA && !c->rows_packed) TRY(launch_pack_rows(c));
     c->rows_packed = false;
@@ -1045,6 +1117,8 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
     }
     TRY(popart_target_stats(c, stop ? epochs_run - 1 : epochs_run, rows_done, opp ? c->d_valid : nullptr));
     TRY(launch_explained_variance(c, opp ? c->d_valid : nullptr));
+    // mode 1: nothing after this update (the next rollout) overwrites the copied buffers early
+    if (c->ev_mode == 1) BPPO_HIP(c, hipStreamWaitEvent(c->stream, c->ev_copied, 0));
     BPPO_HIP(c, hipEventRecord(c->ev_upd, c->stream));      // end of this update's work
     if (c->prefetch_next) {
         // bppo_train_steps: the next rollout goes in behind this update (it needs only the
@@ -1066,6 +1140,7 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
     }
     double ev4[4];
     explained_variance_sums(c, ev4);
+    if (c->ev_thread.joinable()) c->ev_thread.join();     // mode 1: the reference's f32 sums
     tm_read(c, TM_UPDATE);
     if (c->mb_ev_n > 0) {                     // every minibatch kernel launch of this update
         double sum = 0.0;
@@ -1117,6 +1192,7 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
         const double mres = ev4[2] / Bn, vres = ev4[3] / Bn - mres * mres;
         // ppo.rs:1268-1294 (fewer than 2 rows or Var(R) < 1e-8 -> 0)
         m->explained_variance = (B < 2 || vr < 1e-8) ? 0.0f : (float)(1.0 - vres / vr);
+        if (c->ev_mode == 1) m->explained_variance = c->ev_ref;
         // ppo.rs:1549-1565: only envs with action masks report these (None -> 0)
         if (c->cfg.env_kind != BPPO_ENV_CARTPOLE) { m->avg_valid_actions = tav / n; m->entropy_valid_pct = tevp / n; }
         m->num_updates = nup; m->epochs_run = epochs_run;

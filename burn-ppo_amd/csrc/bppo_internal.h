@@ -389,6 +389,15 @@ struct bppo_ctx {
     // the GAE pass (advantage, return): k_pack_rows is skipped when both did
     bool rows_from_rollout = false, rows_packed = false;
     uint64_t prefetch_env_step = 0;
+    // explained variance (bppo_set_explained_variance_mode): 0 = f64 sums on the device
+    // (k_ev); 1 = the reference's f32 sequential sums (ppo.rs:1268-1294) on a host thread,
+    // from D2H copies of the buffers made on ev_stream beside the update
+    int ev_mode = 0;
+    hipStream_t ev_stream = nullptr;
+    hipEvent_t ev_gae = nullptr, ev_copied = nullptr;
+    float *h_ev_v = nullptr, *h_ev_r = nullptr, *h_ev_valid = nullptr;
+    std::thread ev_thread;
+    float ev_ref = 0.0f;
 };
 
 namespace bppo {

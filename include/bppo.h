@@ -281,6 +281,13 @@ bppo_status bppo_gae_mp_device(const float *all_rewards, const int32_t *players,
                                int32_t T, int32_t N, int32_t P, float gamma, float lambda,
                                float *advantages, float *returns, void *hip_stream);
 
+/* UpdateMetrics.explained_variance (ppo.rs:1268-1294): mode 0 (default) = f64 sums on the
+ * device (within 1e-6 of the exact value; the reference's f32 sums drift ~1e-3 at 10^6
+ * rows); mode 1 = the reference's own arithmetic, bit for bit: four sequential f32 sums
+ * over the buffer, on a host thread from device->host copies made beside the update
+ * (it waits for them at the update's end: ~10 ms of one CPU per 8.4 M rows) */
+bppo_status bppo_set_explained_variance_mode(bppo_ctx *ctx, int32_t mode);
+
 /* device timing of the last call of each phase kernel (ms), for bench.py's roofline */
 bppo_status bppo_last_kernel_ms(bppo_ctx *ctx, const char *kernel, float *ms);
 
