@@ -1003,6 +1003,7 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
     // are read once after the last one (no per-minibatch stream drain)
     const bool deferred = c->cfg.target_kl < 0 && !(c->allreduce && c->world > 1 && !c->allreduce_async);
     int nrow = 0;
+    bool first_mb = true;                 // the update's first minibatch: the rollout's parameters
     size_t rows_done = 0;                 // rows of the KL-stopped epoch's minibatches that ran
     for (int ep = 0; ep < c->cfg.num_epochs && !stop; ep++) {
         epochs_run++;
@@ -1040,9 +1041,10 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
             if (c->wide) {
                 TRY(wide_minibatch(c, (uint32_t)start, (uint32_t)sz, (float)ent_coef));
             } else {
-                TRY(launch_minibatch(c, (uint32_t)start, (uint32_t)sz, (float)ent_coef, nullptr));
+                TRY(launch_minibatch(c, (uint32_t)start, (uint32_t)sz, (float)ent_coef, first_mb));
             }
             (void)hipEventRecord(c->ev[TM_FWDBWD][1], c->stream);
+            first_mb = false;
             if (c->allreduce && c->world > 1) {
                 if (!c->allreduce_async) BPPO_HIP(c, sync_stream(c));
                 if (c->allreduce(c->d_grad, (size_t)np + NM, c->allreduce_user) != 0) {

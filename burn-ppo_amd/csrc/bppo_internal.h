@@ -437,8 +437,7 @@ hipError_t fisher_yates_device(const uint32_t *d_J, uint32_t n, uint32_t *scratc
 hipError_t fy_ranges_init(FyRanges &r, uint32_t n);
 void fy_ranges_free(FyRanges &r);
 bppo_status launch_epoch_adv_stats(bppo_ctx *c, uint32_t B, int M, const uint32_t *inv = nullptr);
-bppo_status launch_minibatch(bppo_ctx *c, uint32_t mb_start, uint32_t mb_size, float ent_coef,
-                             double *h_stats_out);
+bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_coef, bool exact);
 bppo_status launch_adam(bppo_ctx *c, float lr, const float *c1, const float *c2, float *metric_dst = nullptr,
                         int nm = 0);
 bppo_status launch_metric_row(bppo_ctx *c, float *dst, int nm);

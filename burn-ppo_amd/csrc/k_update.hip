@@ -7,6 +7,8 @@
 //    weight-gradient reductions staged through LDS per wave, per-wave partial
 //    gradients reduced in fixed order (deterministic), per-tensor norm clip +
 //    Adam (main.rs:264-268).
+#include <algorithm>
+#include <cstdlib>
 #include "bppo_internal.h"
 #include "bppo_mlp64.h"
 
@@ -713,6 +715,458 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
 #endif
 }
 
+// ============================================ split-bf16 minibatch (H=64, NL=2) ==
+// Every minibatch but the update's first.  The first minibatch runs with the rollout's
+// parameters, where the forward must reproduce the rollout's values bit for bit (ratio
+// exactly 1: k_minibatch_mfma, k-ordered f32 MFMA chains).  After the first Adam step the
+// parameters already differ from the reference's in the last bits (gradient summation
+// order), so the later minibatches only need f32 ACCURACY, not the reference's rounding.
+// Here the three 64x64 contractions -- layer 2, dZ1 = dZ2 W1^T, dW1 = H1^T dZ2 -- run on
+// v_mfma_f32_32x32x16_bf16 (1/16 the cycles of the f32 MFMA per FLOP) with every f32
+// operand split exactly into three bf16 pieces x = x0 + x1 + x2 (8 significand bits each)
+// and the six products of order <= 2 accumulated in f32 (x0y0, x0y1, x1y0, x0y2, x1y1,
+// x2y0; the dropped terms are < 2^-26 relative): 48 bf16 MFMAs of 32 cycles per
+// contraction per 32-row tile instead of 64 f32 MFMAs of 64 cycles.
+//   layer 1 twice on the f32 MFMA (K = 6, b0 folded into the pad row): transposed
+//     (H1^T: units in registers, rows on lanes = layer 2's A fragments, no LDS) and in
+//     the C/D orientation (rows in registers = dW1's A fragments and the relu mask);
+//   heads on the VALU with ILP (lane = row, each lane half over 32 units);
+//   W1 split once per block into two bf16 images: [j1][j2] (dZ1's B fragments) and
+//   [j2][j1] with j1 bits 2 and 3 swapped (layer 2's B fragments, whose k order is the
+//   accumulator's permuted row order), row stride 72 (conflict-free ds_read_b128).
+namespace mmf {
+constexpr int H = 64, TR = 32, WS = 68, WPS = 72;
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+struct Params {
+    uint64_t exp2tab[32];
+    double linvc[16], llogc[16];
+    float W0[6 * H];              // [d][j1]; row 5 = b0 (the K pad multiplies a 1)
+    float b1[H];
+    float4 Wh[H];                 // {wp0, wp1, wv, 0} per hidden unit
+    float bp[2], bv[2];
+    __bf16 W1n[3][H * WPS];       // W1 pieces [j1][j2]
+    __bf16 W1t[3][H * WPS];       // W1 pieces [j2][perm(j1)]
+    __device__ __forceinline__ float expf(float x) const { return bppo_math::expf_glibc_tab(x, exp2tab); }
+    __device__ __forceinline__ float logf(float x) const { return bppo_math::logf_glibc_tab(x, linvc, llogc); }
+};
+struct Wave {
+    float X[TR * 5];
+    float T[TR * WS];             // H2, then dZ2 [row][j2]
+    float dl[TR * 4];
+    float met[TR * 16];           // per row lane: the metric sums and head-bias gradients (MT_*)
+};
+enum { MT_PL = 0, MT_VL, MT_H, MT_KL, MT_CF, MT_V, MT_R, MT_VE, MT_VE2, MT_VEMAX, MT_N, MT_BP0, MT_BP1, MT_BV };
+constexpr int WAVES = 8;
+constexpr size_t LDS_TILES = sizeof(Params) + WAVES * sizeof(Wave);
+static_assert(LDS_TILES <= 160 * 1024, "split minibatch kernel LDS over the gfx950 limit");
+__device__ __forceinline__ int perm_j1(int j) { return (j & ~12) | ((j & 4) << 1) | ((j & 8) >> 1); }
+struct Split8 { bf16x8_t p[3]; };
+// exact three-piece split of 8 f32 values
+__device__ __forceinline__ Split8 split8(const float (&x)[8]) {
+    Split8 s;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const __bf16 a = (__bf16)x[j];
+        const float r = x[j] - (float)a;
+        const __bf16 b = (__bf16)r;
+        const __bf16 c = (__bf16)(r - (float)b);
+        s.p[0][j] = a; s.p[1][j] = b; s.p[2][j] = c;
+    }
+    return s;
+}
+__device__ __forceinline__ void mfma6(f32x16_t &acc, const Split8 &a, const Split8 &b) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[2], b.p[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[1], b.p[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[1], b.p[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[0], acc, 0, 0, 0);
+}
+__device__ __forceinline__ Split8 load_pieces(const __bf16 (*img)[H * WPS], int off) {
+    Split8 s;
+#pragma unroll
+    for (int p = 0; p < 3; p++) s.p[p] = *reinterpret_cast<const bf16x8_t *>(img[p] + off);
+    return s;
+}
+__device__ __forceinline__ void load_params_split(Params &S, const float *__restrict__ P) {
+    constexpr CpOffsets O = cp_offsets<64, 2>();
+    for (int i = threadIdx.x; i < 6 * H; i += blockDim.x) S.W0[i] = i < 5 * H ? P[O.w0 + i] : P[O.b0 + i - 5 * H];
+    for (int i = threadIdx.x; i < H * H; i += blockDim.x) {
+        const int j1 = i / H, j2 = i % H;
+        const float w = P[O.w1 + i];                 // W1 [in = j1][out = j2]
+        const __bf16 a = (__bf16)w;
+        const float r = w - (float)a;
+        const __bf16 b = (__bf16)r;
+        const __bf16 c = (__bf16)(r - (float)b);
+        S.W1n[0][j1 * WPS + j2] = a; S.W1n[1][j1 * WPS + j2] = b; S.W1n[2][j1 * WPS + j2] = c;
+        const int t = j2 * WPS + perm_j1(j1);
+        S.W1t[0][t] = a; S.W1t[1][t] = b; S.W1t[2][t] = c;
+    }
+    for (int i = threadIdx.x; i < H; i += blockDim.x) {
+        S.b1[i] = P[O.b1 + i];
+        S.Wh[i] = make_float4(P[O.wp + 2 * i], P[O.wp + 2 * i + 1], P[O.wv + i], 0.0f);
+    }
+    if (threadIdx.x < 32) S.exp2tab[threadIdx.x] = bppo_math::kExp2fTab[threadIdx.x];
+    if (threadIdx.x < 16) {
+        S.linvc[threadIdx.x] = bppo_math::kLogfInvc[threadIdx.x];
+        S.llogc[threadIdx.x] = bppo_math::kLogfLogc[threadIdx.x];
+    }
+    if (threadIdx.x < 2) S.bp[threadIdx.x] = P[O.bp + threadIdx.x];
+    if (threadIdx.x == 0) S.bv[0] = P[O.bv];
+}
+}  // namespace mmf
+
+__global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
+    using namespace mmf;
+    using mmb::cd_row;
+    constexpr CpOffsets O = cp_offsets<64, 2>();
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    Params &S = *reinterpret_cast<Params *>(smem);
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    Wave &B = reinterpret_cast<Wave *>(smem + sizeof(Params) / 4)[wv];
+    load_params_split(S, g.params);
+    __syncthreads();
+
+    const int c = lane & 31, h = lane >> 5;
+    const int gwave = blockIdx.x * WAVES + wv, nwaves = gridDim.x * WAVES;
+    const float mean = g.mb_stats[0], denom = g.mb_stats[1] + 1e-8f;
+    f32x16_t dW1[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+#pragma unroll
+            for (int q = 0; q < 16; q++) dW1[i][j][q] = 0.0f;
+    float gW0[5][2], gb0[2] = {0, 0}, gb1[2] = {0, 0}, gP0[2] = {0, 0}, gP1[2] = {0, 0}, gV[2] = {0, 0};
+#pragma unroll
+    for (int d = 0; d < 5; d++) gW0[d][0] = gW0[d][1] = 0.0f;
+    // the per-row metric sums live in LDS (lane c of the low half owns row slot c), not
+    // in 14 loop-carried registers per lane
+    if (h == 0) {
+        float4 *mp = reinterpret_cast<float4 *>(B.met + c * 16);
+        mp[0] = make_float4(0, 0, 0, 0); mp[1] = make_float4(0, 0, 0, 0);
+        mp[2] = make_float4(0, -INFINITY, 0, 0); mp[3] = make_float4(0, 0, 0, 0);
+    }
+
+    const uint32_t stride = (uint32_t)nwaves * TR;
+    auto idx_of = [&](uint32_t b) -> uint32_t {
+        const uint32_t rr = b + c;
+        return (h == 0 && rr < g.n) ? g.perm[g.start + rr] : 0xFFFFFFFFu;
+    };
+    RowData nxt;
+    uint32_t idx_next = idx_of((uint32_t)gwave * TR + stride);
+    nxt = load_row(g, idx_of((uint32_t)gwave * TR));
+    for (uint32_t base = (uint32_t)gwave * TR; base < g.n; base += stride) {
+        const uint32_t r = base + c;
+        const bool valid = h == 0 && r < g.n;
+        const RowData cur = nxt;
+        int ln_ = lane;
+        asm volatile("" : "+v"(ln_));
+        const int c = ln_ & 31, h = ln_ >> 5;
+        const uint32_t idx_after = idx_of(base + 2 * stride);
+        nxt = load_row(g, idx_next);
+        idx_next = idx_after;
+        const int a = cur.a;
+        const float olp = cur.olp, A = cur.A, R = cur.R, ov = cur.ov;
+        if (h == 0) {
+#pragma unroll
+            for (int d = 0; d < 5; d++) B.X[c * 5 + d] = cur.x(d);
+        }
+        wave_sync();
+        // ---- layer 1, transposed: H1^T[j1][row c] (j1 = cd_row(q, h) + 32 it)
+        float xs[3];
+#pragma unroll
+        for (int s = 0; s < 3; s++) xs[s] = (s == 2 && h == 1) ? 1.0f : B.X[c * 5 + 2 * s + h];
+        // ---- layer 2 (C/D orientation): A = H1 from the layer-1 registers (one 32-unit
+        // tile of layer 1 at a time), B = W1 pieces
+        f32x16_t h2[2];
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++)
+#pragma unroll
+            for (int q = 0; q < 16; q++) h2[ct][q] = 0.0f;
+#pragma unroll
+        for (int it = 0; it < 2; it++) {
+            f32x16_t a1;
+#pragma unroll
+            for (int q = 0; q < 16; q++) a1[q] = 0.0f;
+#pragma unroll
+            for (int s = 0; s < 3; s++)
+                a1 = __builtin_amdgcn_mfma_f32_32x32x2f32(S.W0[(2 * s + h) * H + c + 32 * it], xs[s], a1, 0, 0, 0);
+#pragma unroll
+            for (int s2 = 0; s2 < 2; s2++) {
+                float v8[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) { const float v = a1[8 * s2 + j]; v8[j] = v > 0.0f ? v : 0.0f; }
+                const Split8 Af = split8(v8);
+#pragma unroll
+                for (int ct = 0; ct < 2; ct++)
+                    mfma6(h2[ct], Af, load_pieces(S.W1t, (c + 32 * ct) * WPS + 32 * it + 16 * s2 + 8 * h));
+                __builtin_amdgcn_sched_barrier(0);   // bound the piece-load hoisting (registers)
+            }
+        }
+        // H2 = relu(. + b1) -> the row-major tile for the heads
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++)
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const float v = h2[ct][q] + S.b1[c + 32 * ct];
+                B.T[cd_row(q, h) * WS + c + 32 * ct] = v > 0.0f ? v : 0.0f;
+            }
+        wave_sync();
+        // ---- heads: lane = row c, lane half h over units [32 h, 32 h + 32), 2 chains each
+        float l0, l1, vv;
+        {
+            float pa[3] = {0, 0, 0}, pb[3] = {0, 0, 0};
+            const float *hr = B.T + c * WS + 32 * h;
+#pragma unroll
+            for (int k = 0; k < 32; k += 4) {
+                const float4 x = *reinterpret_cast<const float4 *>(hr + k);
+                const float4 w0 = S.Wh[32 * h + k], w1 = S.Wh[32 * h + k + 1];
+                const float4 w2 = S.Wh[32 * h + k + 2], w3 = S.Wh[32 * h + k + 3];
+                pa[0] = __builtin_fmaf(x.x, w0.x, pa[0]); pa[1] = __builtin_fmaf(x.x, w0.y, pa[1]); pa[2] = __builtin_fmaf(x.x, w0.z, pa[2]);
+                pb[0] = __builtin_fmaf(x.y, w1.x, pb[0]); pb[1] = __builtin_fmaf(x.y, w1.y, pb[1]); pb[2] = __builtin_fmaf(x.y, w1.z, pb[2]);
+                pa[0] = __builtin_fmaf(x.z, w2.x, pa[0]); pa[1] = __builtin_fmaf(x.z, w2.y, pa[1]); pa[2] = __builtin_fmaf(x.z, w2.z, pa[2]);
+                pb[0] = __builtin_fmaf(x.w, w3.x, pb[0]); pb[1] = __builtin_fmaf(x.w, w3.y, pb[1]); pb[2] = __builtin_fmaf(x.w, w3.z, pb[2]);
+            }
+            float t0 = pa[0] + pb[0], t1 = pa[1] + pb[1], t2 = pa[2] + pb[2];
+            t0 += __shfl_xor(t0, 32, 64); t1 += __shfl_xor(t1, 32, 64); t2 += __shfl_xor(t2, 32, 64);
+            l0 = t0; l1 = t1; vv = t2;
+        }
+        // ---- loss (as k_minibatch_mfma), dl per row
+        {
+            const float lg0 = __fadd_rn(l0, S.bp[0]), lg1 = __fadd_rn(l1, S.bp[1]), v = __fadd_rn(vv, S.bv[0]);
+            const float mx = lg0 > lg1 ? lg0 : lg1;
+            const float eh = S.expf(__fsub_rn(h ? lg1 : lg0, mx));
+            const float eo = __shfl_xor(eh, 32, 64);
+            const float e0 = h ? eo : eh, e1 = h ? eh : eo;
+            const float lse = S.logf(__fadd_rn(e0, e1));
+            const float ls0 = __fsub_rn(__fsub_rn(lg0, mx), lse);
+            const float ls1 = __fsub_rn(__fsub_rn(lg1, mx), lse);
+            const float ph = S.expf(h ? ls1 : ls0);
+            const float po = __shfl_xor(ph, 32, 64);
+            const float p0 = h ? po : ph, p1 = h ? ph : po;
+          if (h == 0) {
+            const float An = __fdiv_rn(__fsub_rn(A, mean), denom);   // utils.rs:88
+            const float Hn = -__fadd_rn(__fmul_rn(p0, ls0), __fmul_rn(p1, ls1));
+            const float newlp = a == 1 ? ls1 : ls0;
+            const float log_ratio = __fsub_rn(newlp, olp);
+            const float ratio = S.expf(log_ratio);
+            const float na = -An;
+            const float pl1 = __fmul_rn(na, ratio);
+            const float rc = ratio < g.lo ? g.lo : (ratio > g.hi ? g.hi : ratio);
+            const float pl2 = __fmul_rn(na, rc);
+            const bool rhs = pl1 < pl2;
+            const float pl = rhs ? pl2 : pl1;
+            float vl, dvl;
+            if (g.clip_value) {
+                const float dlt = __fsub_rn(v, ov);
+                const float dc = dlt < -g.ceps ? -g.ceps : (dlt > g.ceps ? g.ceps : dlt);
+                const float vc = __fadd_rn(ov, dc);
+                const float q1 = __fmul_rn(__fsub_rn(v, R), __fsub_rn(v, R));
+                const float q2 = __fmul_rn(__fsub_rn(vc, R), __fsub_rn(vc, R));
+                if (q1 < q2) { vl = q2; dvl = (dlt >= -g.ceps && dlt <= g.ceps) ? 2.0f * __fsub_rn(vc, R) : 0.0f; }
+                else { vl = q1; dvl = 2.0f * __fsub_rn(v, R); }
+            } else {
+                vl = __fmul_rn(__fsub_rn(v, R), __fsub_rn(v, R));
+                dvl = 2.0f * __fsub_rn(v, R);
+            }
+            const float g_ratio = (!rhs || (ratio >= g.lo && ratio <= g.hi)) ? -An * g.inv_mb : 0.0f;
+            const float g_lr = g_ratio * ratio;
+            const float ec = g.ent_coef * g.inv_mb;
+            float dl0 = g_lr * ((a == 0 ? 1.0f : 0.0f) - p0) + ec * p0 * (ls0 + Hn);
+            float dl1 = g_lr * ((a == 1 ? 1.0f : 0.0f) - p1) + ec * p1 * (ls1 + Hn);
+            float dv = g.value_coef * 0.5f * g.inv_mb * dvl;
+            if (!valid) { dl0 = dl1 = dv = 0.0f; }
+            else {
+                const float ve = fabsf(__fsub_rn(v, R));
+                float4 *mp = reinterpret_cast<float4 *>(B.met + c * 16);
+                float4 m0 = mp[0], m1 = mp[1], m2 = mp[2], m3 = mp[3];
+                m0.x += pl; m0.y += vl; m0.z += Hn; m0.w += (ratio - 1.0f) - log_ratio;
+                m1.x += fabsf(ratio - 1.0f) > g.ceps ? 1.0f : 0.0f;
+                m1.y += v; m1.z += R; m1.w += ve; m2.x += ve * ve; m2.y = fmaxf(m2.y, ve);
+                m2.z += 1.0f; m2.w += dl0; m3.x += dl1; m3.y += dv;
+                mp[0] = m0; mp[1] = m1; mp[2] = m2; mp[3] = m3;
+            }
+            *reinterpret_cast<float4 *>(B.dl + c * 4) = make_float4(dl0, dl1, dv, 0.0f);
+          }
+        }
+        wave_sync();
+        // ---- head weight gradients (lane = hidden unit), dZ2 before the mask on the f32 MFMA
+#pragma unroll 4
+        for (int q = 0; q < 16; q++) {
+            const int row = cd_row(q, h);
+            const float4 d = *reinterpret_cast<const float4 *>(B.dl + row * 4);
+#pragma unroll
+            for (int ct = 0; ct < 2; ct++) {
+                const float hv = B.T[row * WS + c + 32 * ct];
+                gP0[ct] = __builtin_fmaf(hv, d.x, gP0[ct]);
+                gP1[ct] = __builtin_fmaf(hv, d.y, gP1[ct]);
+                gV[ct] = __builtin_fmaf(hv, d.z, gV[ct]);
+            }
+        }
+        f32x16_t acc[2];
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++)
+#pragma unroll
+            for (int q = 0; q < 16; q++) acc[ct][q] = 0.0f;
+        {
+            const float a0 = B.dl[c * 4 + h], a1 = B.dl[c * 4 + 2 + h];
+#pragma unroll
+            for (int ct = 0; ct < 2; ct++) {
+                const float4 w = S.Wh[c + 32 * ct];
+                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, h ? w.y : w.x, acc[ct], 0, 0, 0);
+                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, h ? 0.0f : w.z, acc[ct], 0, 0, 0);
+            }
+        }
+        // dZ2 = that * [H2 > 0]: kept in registers (dW1's B fragments) and written over H2
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+#pragma unroll
+            for (int ct = 0; ct < 2; ct++) {
+                const int ad = cd_row(q, h) * WS + c + 32 * ct;
+                const float dz = B.T[ad] > 0.0f ? acc[ct][q] : 0.0f;
+                gb1[ct] += dz;
+                B.T[ad] = dz;
+            }
+            if ((q & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+        }
+        // ---- layer 1 again, C/D orientation: H1[row][j1] (rows in registers)
+        f32x16_t h1[2];
+#pragma unroll
+        for (int jt = 0; jt < 2; jt++)
+#pragma unroll
+            for (int q = 0; q < 16; q++) h1[jt][q] = 0.0f;
+#pragma unroll
+        for (int s = 0; s < 3; s++) {
+            const float xv = (s == 2 && h == 1) ? 1.0f : B.X[c * 5 + 2 * s + h];
+#pragma unroll
+            for (int jt = 0; jt < 2; jt++)
+                h1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(xv, S.W0[(2 * s + h) * H + c + 32 * jt], h1[jt], 0, 0, 0);
+        }
+        uint32_t m1 = 0;                         // relu mask of H1, bit q + 16 jt
+#pragma unroll
+        for (int jt = 0; jt < 2; jt++)
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const bool on = h1[jt][q] > 0.0f;
+                m1 |= on ? (1u << (q + 16 * jt)) : 0u;
+                h1[jt][q] = on ? h1[jt][q] : 0.0f;
+            }
+        // ---- dW1 += H1^T dZ2: both operands straight from the C/D registers (k = rows)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; s2++) {
+            Split8 Bz[2];
+#pragma unroll
+            for (int t = 0; t < 2; t++) {
+                float z[8];      // this lane's own dZ2 elements, back from the tile
+#pragma unroll
+                for (int j = 0; j < 8; j++) z[j] = B.T[cd_row(8 * s2 + j, h) * WS + c + 32 * t];
+                Bz[t] = split8(z);
+            }
+#pragma unroll
+            for (int it = 0; it < 2; it++) {
+                float u[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) u[j] = h1[it][8 * s2 + j];
+                const Split8 Ah = split8(u);
+#pragma unroll
+                for (int jt = 0; jt < 2; jt++) mfma6(dW1[it][jt], Ah, Bz[jt]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        wave_sync();
+        // ---- dZ1 = dZ2 W1^T: A = dZ2 rows (natural k = j2) from the tile, B = W1 pieces
+        f32x16_t dz1[2];
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++)
+#pragma unroll
+            for (int q = 0; q < 16; q++) dz1[ct][q] = 0.0f;
+#pragma unroll
+        for (int ks = 0; ks < 4; ks++) {
+            const float *zr = B.T + c * WS + 16 * ks + 8 * h;
+            const float4 z0 = *reinterpret_cast<const float4 *>(zr), z1 = *reinterpret_cast<const float4 *>(zr + 4);
+            const float zz[8] = {z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w};
+            const Split8 Az = split8(zz);
+#pragma unroll
+            for (int ct = 0; ct < 2; ct++)
+                mfma6(dz1[ct], Az, load_pieces(S.W1n, (c + 32 * ct) * WPS + 16 * ks + 8 * h));
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // dZ1 masked by relu'(H1); dW0 and db0 on the VALU (lane = hidden unit)
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            const int row = cd_row(q, h);
+            float xr[5];
+#pragma unroll
+            for (int d = 0; d < 5; d++) xr[d] = B.X[row * 5 + d];
+#pragma unroll
+            for (int jt = 0; jt < 2; jt++) {
+                const float dzv = (m1 >> (q + 16 * jt)) & 1u ? dz1[jt][q] : 0.0f;
+                gb0[jt] += dzv;
+#pragma unroll
+                for (int d = 0; d < 5; d++) gW0[d][jt] = __builtin_fmaf(xr[d], dzv, gW0[d][jt]);
+            }
+            if ((q & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+        }
+        wave_sync();
+    }
+    // ---- this wave's partial gradient row (as k_minibatch_mfma)
+#pragma unroll
+    for (int ct = 0; ct < 2; ct++) {
+        gb0[ct] += __shfl_xor(gb0[ct], 32, 64); gb1[ct] += __shfl_xor(gb1[ct], 32, 64);
+        gP0[ct] += __shfl_xor(gP0[ct], 32, 64); gP1[ct] += __shfl_xor(gP1[ct], 32, 64);
+        gV[ct] += __shfl_xor(gV[ct], 32, 64);
+#pragma unroll
+        for (int d = 0; d < 5; d++) gW0[d][ct] += __shfl_xor(gW0[d][ct], 32, 64);
+    }
+    float mt[14];
+#pragma unroll
+    for (int k = 0; k < 14; k++) mt[k] = h == 0 ? B.met[c * 16 + k] : (k == MT_VEMAX ? -INFINITY : 0.0f);
+    const int W_ = g.np + NUM_M;
+    __syncthreads();
+    float *row = smem + (size_t)wv * W_;
+    if (h == 0) {
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++) {
+            const int k = c + 32 * ct;
+#pragma unroll
+            for (int d = 0; d < 5; d++) row[O.w0 + d * H + k] = gW0[d][ct];
+            row[O.b0 + k] = gb0[ct];
+            row[O.b1 + k] = gb1[ct];
+            row[O.wp + 2 * k] = gP0[ct];
+            row[O.wp + 2 * k + 1] = gP1[ct];
+            row[O.wv + k] = gV[ct];
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < 2; it++)
+#pragma unroll
+        for (int jt = 0; jt < 2; jt++)
+#pragma unroll
+            for (int q = 0; q < 16; q++)
+                row[O.w1 + ((q & 3) + 8 * (q >> 2) + 4 * h + 32 * it) * H + c + 32 * jt] = dW1[it][jt][q];
+    float st[14];
+#pragma unroll
+    for (int k = 0; k < 14; k++) st[k] = k == MT_VEMAX ? wave_max(mt[k]) : wave_sum(mt[k]);
+    if (lane == 0) {
+        row[O.bp] = st[MT_BP0]; row[O.bp + 1] = st[MT_BP1]; row[O.bv] = st[MT_BV];
+        float *mm = row + g.np;
+        static_assert(MT_PL == M_PL && MT_VEMAX == M_VEMAX && MT_N == M_N, "metric slots");
+#pragma unroll
+        for (int k = 0; k <= MT_N; k++) mm[k] = st[k];
+    }
+    __syncthreads();
+    for (int p = tid; p < W_; p += blockDim.x) {
+        float a2 = smem[p];
+        if (p == g.np + M_VEMAX) {
+            for (int w = 1; w < WAVES; w++) a2 = fmaxf(a2, smem[(size_t)w * W_ + p]);
+        } else {
+            for (int w = 1; w < WAVES; w++) a2 += smem[(size_t)w * W_ + p];
+        }
+        g.slab[(size_t)blockIdx.x * W_ + p] = a2;
+    }
+}
+
 // fixed-order reduction of the wave partials, grad[p] = sum_w slab[w][p]: SLAB_GROUPS
 // row groups each summed in f64 in row order, then the groups in order.
 constexpr int SLAB_GROUPS = 32;
@@ -1088,8 +1542,7 @@ bppo_status launch_epoch_adv_stats(bppo_ctx *c, uint32_t B, int M, const uint32_
     return BPPO_OK;
 }
 
-bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_coef,
-                             double *) {
+bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_coef, bool exact) {
     const int h = c->cfg.hidden_size, nl = c->cfg.num_hidden;
     MbArgs g;
     g.obs = c->d_obs; g.logp = c->d_logp; g.adv = c->d_adv; g.ret = c->u_ret; g.val = c->u_val;
@@ -1115,9 +1568,18 @@ bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_
             return BPPO_ERR_UNSUPPORTED;
         }
         c->slab_used = blocks;
+        // the update's first minibatch runs with the rollout's parameters: the exact
+        // f32 kernel, so the ratio is exactly 1; the others on the split-bf16 kernel
+        // (BPPO_MB_EXACT_ALL=1: the exact kernel for every minibatch, for A/B runs)
+        static const bool exact_all = getenv("BPPO_MB_EXACT_ALL") != nullptr;
+        const bool use_exact = exact || exact_all;
+        const size_t lds_split = std::max(mmf::LDS_TILES, (size_t)mmf::WAVES * (c->net.n_params + NUM_M) * sizeof(float));
         const int ei = c->mb_ev_n < bppo_ctx::MB_EV ? c->mb_ev_n++ : -1;
         if (ei >= 0) (void)hipEventRecord(c->mb_ev[ei][0], c->stream);
-        hipLaunchKernelGGL(k_minibatch_mfma, dim3(blocks), dim3(64 * mmb::WAVES), mmb::LDSB, c->stream, g);
+        if (use_exact)
+            hipLaunchKernelGGL(k_minibatch_mfma, dim3(blocks), dim3(64 * mmb::WAVES), mmb::LDSB, c->stream, g);
+        else
+            hipLaunchKernelGGL(k_minibatch_split, dim3(blocks), dim3(64 * mmf::WAVES), lds_split, c->stream, g);
         if (ei >= 0) (void)hipEventRecord(c->mb_ev[ei][1], c->stream);
 #ifdef BPPO_MB_STAMPS
         {   // mean per-wave cycles per segment, accumulated over launches; printed every 16
