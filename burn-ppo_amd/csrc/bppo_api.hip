@@ -1145,15 +1145,18 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
     if (c->ev_thread.joinable()) c->ev_thread.join();     // mode 1: the reference's f32 sums
     tm_read(c, TM_UPDATE);
     if (c->mb_ev_n > 0) {                     // every minibatch kernel launch of this update
-        double sum = 0.0;
+        double sum = 0.0, ks[2] = {0.0, 0.0};
         float lo = INFINITY, hi = 0.0f;
-        int n = 0;
+        int n = 0, kn[2] = {0, 0};
         for (int i = 0; i < c->mb_ev_n; i++) {
             float ms = 0.0f;
             if (hipEventElapsedTime(&ms, c->mb_ev[i][0], c->mb_ev[i][1]) != hipSuccess) continue;
             sum += ms; lo = std::min(lo, ms); hi = std::max(hi, ms); n++;
+            ks[c->mb_ev_split[i]] += ms; kn[c->mb_ev_split[i]]++;
         }
         if (n) { c->mb_k_mean = (float)(sum / n); c->mb_k_min = lo; c->mb_k_max = hi; }
+        c->mb_k_exact = kn[0] ? (float)(ks[0] / kn[0]) : 0.0f;
+        c->mb_k_split = kn[1] ? (float)(ks[1] / kn[1]) : 0.0f;
         c->mb_ev_n = 0;
     }
     c->last_ms[TM_FWDBWD] = fw_ms;
@@ -1395,6 +1398,8 @@ extern "C" bppo_status bppo_last_kernel_ms(bppo_ctx *c, const char *k, float *ms
     if (!strcmp(k, "minibatch_kernel")) { *ms = c->mb_k_mean; return BPPO_OK; }   // all launches of the last update
     if (!strcmp(k, "minibatch_kernel_min")) { *ms = c->mb_k_min; return BPPO_OK; }
     if (!strcmp(k, "minibatch_kernel_max")) { *ms = c->mb_k_max; return BPPO_OK; }
+    if (!strcmp(k, "minibatch_kernel_split")) { *ms = c->mb_k_split; return BPPO_OK; }   // k_minibatch_split launches
+    if (!strcmp(k, "minibatch_kernel_exact")) { *ms = c->mb_k_exact; return BPPO_OK; }   // k_minibatch_mfma launches
     if (!strcmp(k, "shuffle_wait")) { *ms = (float)c->last_wait_ms; return BPPO_OK; }
     if (!strcmp(k, "host_enqueue")) { *ms = (float)c->last_host_ms; return BPPO_OK; }   // bppo_train_step outside stream waits
     if (!strcmp(k, "host_sync_wait")) { *ms = (float)c->last_sync_ms; return BPPO_OK; }

@@ -376,6 +376,8 @@ struct bppo_ctx {
     hipEvent_t mb_ev[MB_EV][2] = {};
     int mb_ev_n = 0;
     float mb_k_mean = 0.0f, mb_k_min = 0.0f, mb_k_max = 0.0f;
+    bool mb_ev_split[MB_EV] = {};     // launch i ran k_minibatch_split (else the exact k_minibatch_mfma)
+    float mb_k_split = 0.0f, mb_k_exact = 0.0f;   // mean of each kind's launches (0: none)
     double last_spec_mwords = 0.0, last_true_mwords = 0.0;   // host walk work since the previous update
     double last_walk_cpu_ms = 0.0, last_words_cpu_ms = 0.0;   // thread time in chain_walk / in words()
     int last_met = 0;

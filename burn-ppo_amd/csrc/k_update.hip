@@ -1575,7 +1575,7 @@ bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_
         const bool use_exact = exact || exact_all;
         const size_t lds_split = std::max(mmf::LDS_TILES, (size_t)mmf::WAVES * (c->net.n_params + NUM_M) * sizeof(float));
         const int ei = c->mb_ev_n < bppo_ctx::MB_EV ? c->mb_ev_n++ : -1;
-        if (ei >= 0) (void)hipEventRecord(c->mb_ev[ei][0], c->stream);
+        if (ei >= 0) { c->mb_ev_split[ei] = !use_exact; (void)hipEventRecord(c->mb_ev[ei][0], c->stream); }
         if (use_exact)
             hipLaunchKernelGGL(k_minibatch_mfma, dim3(blocks), dim3(64 * mmb::WAVES), mmb::LDSB, c->stream, g);
         else

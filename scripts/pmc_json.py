@@ -36,6 +36,7 @@ KERNELS = {
     "k_gae_1p_seg": ("k_gae.hip", 2.0),
     "k_gae_1p": ("k_gae.hip", 1.0),
     "k_minibatch_mfma": ("k_update.hip", 1.0),
+    "k_minibatch_split": ("k_update.hip", 1.0),
     "k_cartpole_rollout_mfma": ("k_rollout.hip", 1.0),
     "k_pack_rows": ("k_update.hip", 1.0),
 }

@@ -8,7 +8,7 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-traffic}
-RE="k_minibatch_mfma|k_gae_1p|k_cartpole_rollout_mfma|k_pack_rows"
+RE="k_minibatch_mfma|k_minibatch_split|k_gae_1p|k_cartpole_rollout_mfma|k_pack_rows"
 timeout -s KILL 60 rocprofv3 -L > gpurun_out/rocprof_counters.txt 2>&1 || true
 have() { grep -qw "$1" gpurun_out/rocprof_counters.txt; }
 pick() { local out=""; for c in "$@"; do if have $c; then out="$out $c"; fi; done; echo $out; }

@@ -6,7 +6,9 @@ Tolerances (north_star: "fp32 returns/advantages/loss within 1e-5 relative"):
     max(|oracle|, floor): the floor is the magnitude of the summands for the
     signed means that cancel to ~0 — policy_loss / total_loss are means of
     -A_n * ratio, floor mean|A_n| of the update's normalized advantages
-    (summand_magnitude, ~0.8; its bound 1.0 where a test passes no advantages); adv_mean_raw is a mean of raw
+    (summand_magnitude, ~0.8; its bound 1.0 where a test passes no advantages);
+    approx_kl additionally to its f32 resolution 2^-24 / sqrt(B) (a mean of
+    (ratio - 1) - log(ratio) per row, evaluated from ratios near 1); adv_mean_raw is a mean of raw
     advantages (floor adv_std_raw); value_mean / returns_mean (floor
     value_error_mean + |returns_mean|).  Both sides accumulate in f64 per
     minibatch, so what is left is per-row f32 rounding of the later minibatches,
@@ -100,6 +102,10 @@ def assert_metrics_close(m, om, values=None, returns=None, skip=(), rtol=RTOL, a
     the advantages; without them the floor is its bound, E|A_n| <= 1 for
     unit-variance normalized advantages."""
     pl_mag = 1.0 if advantages is None else summand_magnitude(advantages)
+    # approx_kl: each row's (ratio - 1) - log(ratio) is evaluated in f32 from a ratio near 1
+    # (resolution 2^-24, half an ulp of 1.0), so a mean over the update's B rows resolves
+    # approx_kl only to ~2^-24 / sqrt(B) absolute, whatever its (small) size
+    kl_abs = 0.0 if advantages is None else 2.0 ** -24 / np.sqrt(max(np.asarray(advantages).size, 1))
     assert m["num_updates"] == om["num_updates"], (m["num_updates"], om["num_updates"])
     assert m["epochs_run"] == om["epochs_run"], (m["epochs_run"], om["epochs_run"])
     bad = []
@@ -116,6 +122,8 @@ def assert_metrics_close(m, om, values=None, returns=None, skip=(), rtol=RTOL, a
         if np.isnan(o) and np.isnan(d):
             continue
         tol = rtol * max(abs(o), _floor(k, om, pl_mag))
+        if k == "approx_kl":
+            tol = max(tol, kl_abs)
         if not abs(d - o) <= tol:
             bad.append((k, d, o, abs(d - o) / max(abs(o), 1e-30)))
     # PopArt (ppo.rs:2061-2068): NaN = None on both sides
