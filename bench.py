@@ -67,6 +67,10 @@ def parse():
     p.add_argument("--host-cpus", type=int, default=0,
                    help="pin each rank to K host CPUs (its share of an 8-rank node) and size the shuffle "
                         "engine's threads for K (BPPO_HOST_THREADS); default: affinity/quota / ranks per node")
+    p.add_argument("--shuffle-windows", choices=("auto", "on", "off"), default="auto",
+                   help="the shuffle_windows mode (epoch e of an update shuffles from a fixed window of the "
+                        "rank's RNG stream, so the host walks all epochs at once: bppo.h): auto = on for N>1 "
+                        "(per-rank streams already depart from the reference's), off at N=1 (reference-exact)")
     return p.parse_args()
 
 
@@ -342,7 +346,8 @@ def main():
     else:
         torch.cuda.set_device(0)
     N, T = args.num_envs, args.num_steps
-    cfg = bppo.make_config("cartpole", num_envs=N * world, num_steps=T)
+    windows = args.shuffle_windows == "on" or (args.shuffle_windows == "auto" and world > 1)
+    cfg = bppo.make_config("cartpole", num_envs=N * world, num_steps=T, shuffle_windows=windows)
     tr = bppo.Trainer(cfg, device=local, init_seed=0, rank=rank, world=world, envs_per_rank=N)
     if world > 1:
         # RCCL all-reduce of the gradient enqueued on the context's stream: no
@@ -472,6 +477,8 @@ def main():
                                      "stream-ordered" if world > 1 else None),
                       "w_gt_1_semantics": ("per-rank obs/return normalizers and per-rank minibatch advantage "
                                            "stats (SURVEY 8e); parity is defined at N=1" if world > 1 else None),
+                      "shuffle": ("shuffle_windows: epoch e shuffles from S + e*(2B + 2^20), all epochs "
+                                  "walked at once" if windows else "sequential (the reference's word positions)"),
                       "host_cpus_per_rank": int(os.environ["BPPO_HOST_THREADS"]),
                       "host_cpu_affinity": len(os.sched_getaffinity(0)),
                       "host_cpu_quota": cgroup_cpu_quota(),

@@ -40,7 +40,8 @@ class Config(C.Structure):
                 ("rng_stream", C.c_uint64),
                 ("cnn", C.c_int32), ("num_conv_layers", C.c_int32), ("conv_channels", C.c_int32 * 4),
                 ("kernel_size", C.c_int32), ("cnn_fc_hidden_size", C.c_int32), ("cnn_num_fc_layers", C.c_int32),
-                ("normalize_values", C.c_int32), ("player_count", C.c_int32), ("split_networks", C.c_int32)]
+                ("normalize_values", C.c_int32), ("player_count", C.c_int32), ("split_networks", C.c_int32),
+                ("shuffle_windows", C.c_int32)]
 
 
 class Episode(C.Structure):
@@ -155,7 +156,7 @@ def lib():
         "bppo_debug_shuffle_chain": (i32, [u64, u64, u64, C.c_uint32, vp, C.POINTER(u64)]),
         "bppo_debug_fisher_yates": (i32, [i32, vp, C.c_uint32, vp]),
         "bppo_debug_gemm": (i32, [i32, i32, i32, i32, vp, vp, vp, i32, vp, vp]),
-        "bppo_debug_shuffle_engine": (i32, [u64, u64, u64, C.c_uint32, i32, u64, i32, vp, vp, vp]),
+        "bppo_debug_shuffle_engine": (i32, [u64, u64, u64, C.c_uint32, i32, u64, i32, i32, vp, vp, vp]),
         "bppo_debug_sample": (i32, [i32, i32, vp, vp, u64, u64, u64, vp, vp]),
         "bppo_rng_fill_bytes": (i32, [vp, vp, sz]),
         "bppo_rng_from_seed": (i32, [vp, vp]),

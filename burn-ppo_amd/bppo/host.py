@@ -46,7 +46,7 @@ BASE = dict(env="cartpole", num_envs=32, num_steps=128, hidden_size=64, num_hidd
             num_minibatches=4, normalize_obs=False, normalize_returns=None, clip_value=False, gamma=0.99,
             gae_lambda=0.95, clip_epsilon=0.2, value_coef=0.5, max_grad_norm=0.5, adam_epsilon=1e-5,
             target_kl=None, return_clip=10.0, reward_shaping_coef=0.0, learning_rate=[(2.5e-4, 0)],
-            entropy_coef=[(0.01, 0)], seed=42, player_count=4, split_networks=False,
+            entropy_coef=[(0.01, 0)], seed=42, player_count=4, split_networks=False, shuffle_windows=False,
             # network_type = "cnn" (config.rs:996-1010 defaults)
             num_conv_layers=2, conv_channels=[8, 8], kernel_size=3, cnn_fc_hidden_size=32, cnn_num_fc_layers=1)
 
@@ -121,6 +121,7 @@ def to_struct(c, rank=0, world=1, envs_per_rank=None):
     s.normalize_values = int(bool(c.get("normalize_values", False)))
     s.player_count = int(c.get("player_count", 4)) if c["env"] == "skull" else 0
     s.split_networks = int(bool(c.get("split_networks", False)))
+    s.shuffle_windows = int(bool(c.get("shuffle_windows", False)))
     s.cnn = int(c["network_type"] == "cnn")
     if s.cnn:
         s.num_conv_layers = c["num_conv_layers"]

@@ -362,7 +362,8 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     }
     c->rng_key = seed_key(cfg->seed);
     c->rng_pos = 0;
-    TRY(c->shuf.init(dev, c->rng_key, cfg->rng_stream, (uint32_t)TN, cfg->num_epochs, TN * (uint64_t)c->A, c->err));
+    TRY(c->shuf.init(dev, c->rng_key, cfg->rng_stream, (uint32_t)TN, cfg->num_epochs, TN * (uint64_t)c->A, c->err,
+                     cfg->shuffle_windows != 0));
     c->on_mean.assign(c->D, 0.0); c->on_m2.assign(c->D, 0.0); c->on_count = 0;
     c->u_ret = c->d_ret; c->u_val = c->d_val;
     c->shaping_v.assign(1, cfg->reward_shaping_coef); c->shaping_s.assign(1, 0);   // Schedule::constant
@@ -525,7 +526,8 @@ extern "C" bppo_status bppo_rng_from_seed(bppo_ctx *c, const uint8_t *seed) {
     c->rng_pos = 0;
     c->shuf_slot = -1;
     const size_t TN = (size_t)c->T * c->N;
-    TRY(c->shuf.init(c->dev, c->rng_key, c->cfg.rng_stream, (uint32_t)TN, c->cfg.num_epochs, TN * (uint64_t)c->A, c->err));
+    TRY(c->shuf.init(c->dev, c->rng_key, c->cfg.rng_stream, (uint32_t)TN, c->cfg.num_epochs, TN * (uint64_t)c->A, c->err,
+                     c->cfg.shuffle_windows != 0));
     return BPPO_OK;
 }
 
@@ -1097,7 +1099,8 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
         c->last_walk_ms = wait_ms;
         BPPO_HIP(c, hipStreamSynchronize(c->stream));      // Jh's copies done
     } else {
-        c->rng_pos = c->shuf.end_pos[slot][epochs_run - 1];   // only started epochs consumed words
+        // only started epochs consumed words (reference); windowed: the update's fixed span
+        c->rng_pos = c->shuf.win ? c->shuf.job_end(slot) : c->shuf.end_pos[slot][epochs_run - 1];
         for (int e = 0; e < epochs_run; e++) {
             c->last_walk_ms += c->shuf.walk_ms[slot][e];
             c->last_met += c->shuf.coalesced[slot][e] >= 0 && e > 0;
@@ -1456,12 +1459,12 @@ extern "C" bppo_status bppo_debug_shuffle_chain(uint64_t seed, uint64_t stream, 
 // positions [jobs][epochs], and per epoch the checkpoints the true walk needed
 // before it met a speculative walk (-1: walked the whole epoch)
 extern "C" bppo_status bppo_debug_shuffle_engine(uint64_t seed, uint64_t stream, uint64_t start, uint32_t n,
-                                                 int32_t epochs, uint64_t gap, int32_t jobs, uint32_t *J,
-                                                 uint64_t *ends, int32_t *met) {
+                                                 int32_t epochs, uint64_t gap, int32_t jobs, int32_t windows,
+                                                 uint32_t *J, uint64_t *ends, int32_t *met) {
     if (!J || !ends || n < 2 || epochs < 1 || epochs > SHUF_MAX_EPOCHS || jobs < 1) return BPPO_ERR_ARG;
     ShuffleEngine *e = new ShuffleEngine();
     std::string err;
-    bppo_status s = e->init(0, seed_key(seed), stream, n, epochs, gap, err);
+    bppo_status s = e->init(0, seed_key(seed), stream, n, epochs, gap, err, windows != 0);
     uint64_t pos = start;
     for (int j = 0; j < jobs && s == BPPO_OK; j++) {
         const int slot = e->ensure(pos);
@@ -1474,7 +1477,7 @@ extern "C" bppo_status bppo_debug_shuffle_engine(uint64_t seed, uint64_t stream,
             ends[o + k] = e->end_pos[slot][k];
             if (met) met[o + k] = e->coalesced[slot][k];
         }
-        pos = e->end_pos[slot][epochs - 1] + gap;
+        pos = e->job_end(slot) + gap;
     }
     e->shutdown();
     delete e;

@@ -76,6 +76,11 @@ constexpr int SHUF_MAX_EPOCHS = 32;
 constexpr int SHUF_MAX_SPEC = 64;
 constexpr uint64_t SHUF_CK = 1024;               // checkpoint spacing (words) = GPU J segment length
 constexpr uint64_t SHUF_CHUNK = (uint64_t)1 << 20; // words per GPU->host copy
+// shuffle_windows (bppo_config): epoch e of an update draws from word position
+// S + e * shuffle_window(n) of the main stream, S the update's first shuffle word, and
+// the next rollout starts at S + epochs * shuffle_window(n).  A shuffle of n uses ~1.39 n
+// words (2 n at most but for a ~2^-(10^5) tail), so the window is 2 n + 2^20.
+__host__ __device__ constexpr uint64_t shuffle_window(uint64_t n) { return 2 * n + ((uint64_t)1 << 20); }
 
 struct SpecWalk {
     uint64_t start = 0, end = 0, ck_base = 0;     // checkpoint c is word position ck_base + c*CK
@@ -94,7 +99,7 @@ struct SpecWalk {
 struct WordBuf {                                  // ChaCha12 words made on the GPU for one job
     uint32_t *d = nullptr, *h = nullptr;
     uint64_t cap = 0;                             // words
-    struct Region { uint64_t base = 0, len = 0, off = 0; } reg[2];
+    struct Region { uint64_t base = 0, len = 0, off = 0; } reg[SHUF_MAX_EPOCHS];
     int nreg = 0;
     std::vector<hipEvent_t> ev;                   // per SHUF_CHUNK chunk of h
     std::unique_ptr<std::atomic<int>[]> ok;
@@ -124,6 +129,7 @@ struct ShuffleEngine {
     Key8 key{};
     uint64_t stream = 0;
     uint64_t gap = 0;                             // words between an update's last shuffle and the next update's first
+    uint64_t win = 0;                             // shuffle_windows: epoch e starts at job start + e * win (0: chained)
     double Ew = 0.0, sigma = 0.0;                 // expected words per shuffle, its std dev
     int K = 0;                                    // speculative walks per epoch boundary
     int host_cpus = 16;                           // CPU budget of this rank (BPPO_HOST_THREADS)
@@ -189,7 +195,9 @@ struct ShuffleEngine {
     std::atomic<uint64_t> spec_words{0}, true_words{0};   // words walked since the caller last read them
     std::atomic<uint64_t> tsc_walk{0}, tsc_words{0};      // TSC ticks walking / getting words (all walks)
     bppo_status init(int device, const Key8 &key, uint64_t stream, uint32_t n_, int epochs_, uint64_t gap_,
-                     std::string &err);
+                     std::string &err, bool windows = false);
+    bool run_windowed(int slot, uint64_t start);   // one job of independent epoch walks (false: cancelled)
+    uint64_t job_end(int slot) const { return win ? slot_start[slot] + (uint64_t)epochs * win : end_pos[slot][epochs - 1]; }
     int ensure(uint64_t start);               // job for this start (reused if already running/done) -> slot
     void release(int slot, hipStream_t st);   // the caller is done enqueuing reads of d_J[slot] on st
     void wait_epoch(int slot, int e);

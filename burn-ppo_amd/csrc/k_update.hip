@@ -749,11 +749,15 @@ struct Params {
     __device__ __forceinline__ float expf(float x) const { return bppo_math::expf_glibc_tab(x, exp2tab); }
     __device__ __forceinline__ float logf(float x) const { return bppo_math::logf_glibc_tab(x, linvc, llogc); }
 };
+constexpr int MET_STRIDE = 20;
 struct Wave {
     float X[TR * 5];
     float T[TR * WS];             // H2, then dZ2 [row][j2]
     float dl[TR * 4];
-    float met[TR * 16];           // per row lane: the metric sums and head-bias gradients (MT_*)
+    // per row lane: the metric sums and head-bias gradients (MT_*); row stride 20 floats,
+    // not 16: lanes c and c+4 of a b128 access then fall in different bank groups
+    // (stride 16 put 4 lanes on the same banks: r04g counted 6.5M conflict cycles/launch)
+    float met[TR * MET_STRIDE];
 };
 enum { MT_PL = 0, MT_VL, MT_H, MT_KL, MT_CF, MT_V, MT_R, MT_VE, MT_VE2, MT_VEMAX, MT_N, MT_BP0, MT_BP1, MT_BV };
 constexpr int WAVES = 8;
@@ -843,7 +847,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
     // the per-row metric sums live in LDS (lane c of the low half owns row slot c), not
     // in 14 loop-carried registers per lane
     if (h == 0) {
-        float4 *mp = reinterpret_cast<float4 *>(B.met + c * 16);
+        float4 *mp = reinterpret_cast<float4 *>(B.met + c * MET_STRIDE);
         mp[0] = make_float4(0, 0, 0, 0); mp[1] = make_float4(0, 0, 0, 0);
         mp[2] = make_float4(0, -INFINITY, 0, 0); mp[3] = make_float4(0, 0, 0, 0);
     }
@@ -979,7 +983,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
             if (!valid) { dl0 = dl1 = dv = 0.0f; }
             else {
                 const float ve = fabsf(__fsub_rn(v, R));
-                float4 *mp = reinterpret_cast<float4 *>(B.met + c * 16);
+                float4 *mp = reinterpret_cast<float4 *>(B.met + c * MET_STRIDE);
                 float4 m0 = mp[0], m1 = mp[1], m2 = mp[2], m3 = mp[3];
                 m0.x += pl; m0.y += vl; m0.z += Hn; m0.w += (ratio - 1.0f) - log_ratio;
                 m1.x += fabsf(ratio - 1.0f) > g.ceps ? 1.0f : 0.0f;
@@ -1121,7 +1125,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
     }
     float mt[14];
 #pragma unroll
-    for (int k = 0; k < 14; k++) mt[k] = h == 0 ? B.met[c * 16 + k] : (k == MT_VEMAX ? -INFINITY : 0.0f);
+    for (int k = 0; k < 14; k++) mt[k] = h == 0 ? B.met[c * MET_STRIDE + k] : (k == MT_VEMAX ? -INFINITY : 0.0f);
     const int W_ = g.np + NUM_M;
     __syncthreads();
     float *row = smem + (size_t)wv * W_;

@@ -211,10 +211,11 @@ static void host_words_free(uint32_t *h, uint64_t words) {
 }
 
 bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32_t n_, int epochs_, uint64_t gap_,
-                                std::string &err) {
+                                std::string &err, bool windows) {
     dev = device; n = n_; epochs = epochs_; key = k; stream = strm; gap = gap_;
     if (epochs > SHUF_MAX_EPOCHS) { err = "num_epochs > 32 not supported by the shuffle engine"; return BPPO_ERR_UNSUPPORTED; }
     shuffle_word_stats(n, Ew, sigma);
+    win = windows ? shuffle_window(n) : 0;
     // K walkers per epoch boundary: epochs 1..E-1 of a job plus the next job's
     // first epoch (two alternating carry sets).  K = 6 measured best for CfgB on a
     // 16-CPU share (K = 2/4/5/6: 281/284/311/316 M env-steps/s): more starting
@@ -247,8 +248,11 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
     } else {
         fr_depth = 0;
     }
+    // shuffle_windows: every epoch's start is known when the job starts, so each epoch is
+    // one exact walk (slot e), all walked at once; nothing to speculate or carry
+    if (win) { K = 1; C = 0; fr_depth = 0; }
     // exact continuations need the last epoch in the in-job groups
-    const bool cont_on = epochs - 1 >= C;
+    const bool cont_on = !win && epochs - 1 >= C;
     K = std::min(K, SHUF_MAX_SPEC / (std::max(epochs - C, 0) + 2 * C + (cont_on ? 2 : 0)));
     ncur = K * std::max(epochs - C, 0);
     nspec = ncur + 2 * C * K;
@@ -286,10 +290,13 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
     const double sE = sigma * std::sqrt((double)std::max(epochs, 1));
     const uint64_t cap0 = chunks(epochs * Ew + 12.0 * sE + 4.0 * SHUF_CK) + SHUF_CHUNK;
     const double sC = sigma * std::sqrt((double)(epochs + C));
-    const uint64_t cap1 = K ? chunks(C * Ew + 8.0 * sC + 12.0 * sigma + 8.0 * SHUF_CK) + SHUF_CHUNK : 0;
+    const uint64_t cap1 = K && !win ? chunks(C * Ew + 8.0 * sC + 12.0 * sigma + 8.0 * SHUF_CK) + SHUF_CHUNK : 0;
+    // windowed: one region per epoch of its expected words + 10 sigma (a longer walk makes
+    // the rest of its words itself)
+    const uint64_t capw = (uint64_t)epochs * chunks(Ew + 10.0 * sigma + 4.0 * SHUF_CK);
     for (int b = 0; b < 2; b++) {
         WordBuf &w = wb[b];
-        w.cap = cap0 + cap1;
+        w.cap = win ? capw : cap0 + cap1;
         if (hipMalloc((void **)&w.d, w.cap * 4) != hipSuccess ||
             !(w.h = host_words_alloc(w.cap))) {
             err = "shuffle word buffers: allocation failed";
@@ -570,6 +577,22 @@ void ShuffleEngine::run() {
         }
         if (wait_consumed) (void)hipStreamWaitEvent(copy, consumed[slot], 0);
         seq++;
+        if (win) {
+            const bool ok = run_windowed(slot, start);
+            if (!ok) stop_walks(0, nspec);
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                running = -1;
+                if (!ok) {
+                    slot_valid[slot] = false;
+                } else {
+                    chain_from = slot;                     // the next job: known since this one started
+                    chain_start = job_end(slot) + gap;
+                }
+            }
+            cv.notify_all();
+            continue;
+        }
         const int b = (int)(seq & 1);                 // word buffer and carry set of this job
         const int cs = 1 - b;                         // carry set the previous job launched for us
         const int cur0 = 0, cur1 = ncur;
@@ -884,6 +907,99 @@ void ShuffleEngine::run() {
         }
         cv.notify_all();
     }
+}
+
+// shuffle_windows: the job's epochs start at start + e * win, all known now, so each is
+// walked exactly and completely by its own walker (slot e), all at once; the epochs
+// resolve in order as their walks finish.  J is rebuilt on the GPU from the walk's
+// checkpoint states, as for the chained walks.
+bool ShuffleEngine::run_windowed(int slot, uint64_t start) {
+    const int b = (int)(seq & 1);
+    WordBuf &W = wb[b];
+    auto chunks = [](double w) { return ((uint64_t)std::max(w, 1.0) + SHUF_CHUNK - 1) / SHUF_CHUNK * SHUF_CHUNK; };
+    const uint64_t rlen = std::min(W.cap / (uint64_t)epochs, chunks(Ew + 10.0 * sigma + 4.0 * SHUF_CK));
+    W.nreg = epochs;
+    std::vector<std::pair<double, size_t>> order;
+    for (int e = 0; e < epochs; e++) {
+        WordBuf::Region &R = W.reg[e];
+        R.base = (start + (uint64_t)e * win) / SHUF_CK * SHUF_CK;
+        R.off = (uint64_t)e * rlen;
+        R.len = rlen;
+        hipLaunchKernelGGL(k_chacha_words, dim3((unsigned)((R.len / 16 + 255) / 256)), dim3(256), 0, copy, key,
+                           stream, R.base, R.len, W.d + R.off);
+        for (uint64_t o = 0; o < R.len; o += SHUF_CHUNK) {
+            const size_t c = (size_t)((R.off + o) / SHUF_CHUNK);
+            W.ok[c] = 0;
+            order.push_back({(double)o + 0.25 * e, c});     // every epoch's words in walk order, interleaved
+        }
+    }
+    std::sort(order.begin(), order.end());
+    {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return gen_active == 0 || quit; });
+        gen_order.clear();
+        for (auto &oc : order) {
+            const WordBuf::Region &R = W.reg[oc.second * SHUF_CHUNK / rlen];
+            gen_order.push_back({R.base + (oc.second * SHUF_CHUNK - R.off), oc.second});
+        }
+        gen_buf = &W;
+        gen_next.store(0, std::memory_order_relaxed);
+        gen_job++;
+        for (int e = 0; e < epochs; e++) launch_walk(e, start + (uint64_t)e * win, b);
+    }
+    cv.notify_all();
+    for (int e = 0; e < epochs; e++) {
+        const auto t0 = std::chrono::steady_clock::now();
+        if (ev_used[slot][e]) (void)hipEventSynchronize(ev[slot][e]);   // previous upload of this buffer
+        SpecWalk &w = spec[e];
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return quit || cancel.load(std::memory_order_relaxed) ||
+                                     (!w.running && w.done.load(std::memory_order_acquire)); });
+            if (quit || cancel.load(std::memory_order_relaxed)) return false;
+        }
+        const uint64_t p0 = start + (uint64_t)e * win, pend = w.end;   // (its words count as spec_words)
+        Seg *S = seg_host[slot] + (size_t)e * maxseg;
+        int ns = 0;
+        bool overflow = false;
+        auto add = [&](uint64_t a, uint64_t z, uint32_t r0) {
+            if (z <= a || r0 < 2) return;
+            if (ns >= maxseg) { overflow = true; return; }
+            S[ns++] = Seg{a, z, r0, 0};
+        };
+        // [p0, first checkpoint) from the full range, then one segment per checkpoint
+        uint64_t q = w.ck_base + SHUF_CK;
+        add(p0, std::min(q, pend), n);
+        for (size_t c = 1; q < pend; c++, q += SHUF_CK) {
+            if (c >= w.ck.size()) { overflow = true; break; }   // longer than any recorded walk
+            add(q, std::min(q + SHUF_CK, pend), w.ck[c]);
+        }
+        if (overflow) {   // never at sane sizes: the sequential walk of the epoch
+            std::vector<uint32_t> Jh(n);
+            (void)shuffle_walk_host(key, stream, p0, n, Jh.data());
+            (void)hipMemcpyAsync(d_J[slot] + (size_t)e * n, Jh.data(), 4ull * n, hipMemcpyHostToDevice, copy);
+            (void)hipStreamSynchronize(copy);
+        } else {
+            WordRegions wr{};
+            wr.ptr[0] = W.d + W.reg[e].off; wr.base[0] = W.reg[e].base; wr.len[0] = W.reg[e].len; wr.n = 1;
+            Seg *dS = d_seg[slot] + (size_t)e * maxseg;
+            (void)hipMemcpyAsync(dS, S, sizeof(Seg) * (size_t)std::max(ns, 1), hipMemcpyHostToDevice, copy);
+            hipLaunchKernelGGL(k_expand_J, dim3((unsigned)((std::max(ns, 1) + XJ_WAVES - 1) / XJ_WAVES)),
+                               dim3(64 * XJ_WAVES), 0, copy, key, stream, (const Seg *)dS, ns, wr,
+                               d_J[slot] + (size_t)e * n);
+        }
+        end_pos[slot][e] = pend;
+        coalesced[slot][e] = -1;
+        (void)hipEventRecord(ev[slot][e], copy);
+        ev_used[slot][e] = true;
+        walk_ms[slot][e] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            ready[slot] = e + 1;
+        }
+        cv.notify_all();
+    }
+    return true;
 }
 
 void ShuffleEngine::shutdown() {

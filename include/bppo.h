@@ -79,6 +79,14 @@ typedef struct {
      * it (ctde.rs).  Any net: at most 16 layers in all (hidden / conv / FC layers + the two
      * heads), else bppo_create returns BPPO_ERR_UNSUPPORTED. */
     int32_t split_networks;
+    /* shuffle_windows (not in the reference; for data-parallel ranks):
+     * 0 = the reference: each epoch's shuffle (ppo.rs:1816) continues the main RNG where
+     * the previous one ended.  1 = epoch e of an update draws from word S + e * (2 B + 2^20)
+     * of the main stream (S = the update's first shuffle word, B = rows shuffled) and the
+     * next rollout starts at S + epochs * (2 B + 2^20): every shuffle's start is known in
+     * advance, so the host walks the epochs at once instead of speculating (a fraction of
+     * the host CPU: what an 8-rank node can give each rank).  Self-play only. */
+    int32_t shuffle_windows;
 } bppo_config;
 
 typedef struct {
@@ -307,9 +315,12 @@ bppo_status bppo_debug_fisher_yates(int32_t device, const uint32_t *J, uint32_t 
  * position start, each next update `gap` words after the previous one's last
  * shuffle.  J [jobs][epochs][n], end word positions [jobs][epochs], met = checkpoints
  * walked before meeting a speculative walk (-1 = none; may be NULL).  Must equal
- * chained shuffle_chain calls. */
+ * chained shuffle_chain calls.  windows = 1: the shuffle_windows layout (epoch e of
+ * an update from its start + e * (2 n + 2^20), the next update gap words after its
+ * start + epochs * (2 n + 2^20)): must equal shuffle_chain calls from those starts. */
 bppo_status bppo_debug_shuffle_engine(uint64_t seed, uint64_t stream, uint64_t start, uint32_t n, int32_t epochs,
-                                      uint64_t gap, int32_t jobs, uint32_t *J, uint64_t *ends, int32_t *met);
+                                      uint64_t gap, int32_t jobs, int32_t windows, uint32_t *J, uint64_t *ends,
+                                      int32_t *met);
 
 /* sampling parity hook: apply_action_mask + sample_categorical + log_prob_categorical
  * (utils.rs:10-45, 96-135) for B host rows of A logits (A in {2, 7, 49}) on the device

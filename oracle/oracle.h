@@ -337,7 +337,12 @@ typedef struct {
      * StdRng::seed_from_u64(seed) on ChaCha stream rng_stream (= r).  Zero: the reference. */
     uint64_t env_seed_offset;
     uint64_t rng_stream;
+    /* shuffle_windows (libbppo's bppo_config field, not the reference): epoch e of an
+     * update shuffles from word S + e * OR_SHUFFLE_WINDOW(B) (S = the update's first
+     * shuffle word) and the update leaves the RNG at S + epochs * OR_SHUFFLE_WINDOW(B) */
+    int shuffle_windows;
 } or_train_cfg;
+#define OR_SHUFFLE_WINDOW(B) (2 * (uint64_t)(B) + ((uint64_t)1 << 20))
 or_trainer *or_trainer_new(const or_train_cfg *c, const float *init_params);
 void or_trainer_free(or_trainer *t);
 size_t or_trainer_num_params(const or_trainer *t);

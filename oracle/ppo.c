@@ -590,11 +590,16 @@ void or_trainers_update(or_trainer **ts, int W, or_update_metrics *ms) {
     float tp = 0, tv = 0, th = 0, tk = 0, tc = 0, tl = 0, tvm = 0, trm = 0;
     float tvem = 0, tves = 0, tav = 0, tevp = 0;
     int nup = 0, epochs_run = 0, stop = 0;
+    uint64_t S[64];                      /* each rank's first shuffle word (shuffle_windows) */
+    for (int r = 0; r < W && r < 64; r++) S[r] = ts[r]->rng.word_pos;
+    const int windows = t0r->c.shuffle_windows;
+    if (windows && (W > 64 || ws[0].vidx)) { fprintf(stderr, "or_trainers_update: shuffle_windows: self-play only\n"); abort(); }
     for (int ep = 0; ep < c->num_epochs && !stop; ep++) {
         epochs_run++;
         for (int r = 0; r < W; r++) {
             rank_ws *w = &ws[r];
             for (size_t i = 0; i < w->B; i++) w->idx[i] = (uint32_t)i;  /* :1815 */
+            if (windows) ts[r]->rng.word_pos = S[r] + (uint64_t)ep * OR_SHUFFLE_WINDOW(w->B);
             or_shuffle_u32(&ts[r]->rng, w->idx, w->B);                    /* :1816 */
             w->start = 0;
         }
@@ -669,6 +674,8 @@ void or_trainers_update(or_trainer **ts, int W, or_update_metrics *ms) {
             if (c->target_kl >= 0 && stg.approx_kl > (float)c->target_kl) { stop = 1; break; } /* :2019-2023 */
         }
     }
+    if (windows)
+        for (int r = 0; r < W; r++) ts[r]->rng.word_pos = S[r] + (uint64_t)c->num_epochs * OR_SHUFFLE_WINDOW(ws[r].B);
     for (int r = 0; r < W; r++) {
         or_trainer *t = ts[r];
         rank_ws *w = &ws[r];

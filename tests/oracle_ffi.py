@@ -111,7 +111,7 @@ class TrainCfg(C.Structure):
                 ("ppo", PpoCfg), ("seed", C.c_uint64), ("threads", C.c_int),
                 ("cnn", C.c_int), ("num_conv", C.c_int), ("conv_ch", C.c_int * 4), ("ksize", C.c_int),
                 ("normalize_values", C.c_int), ("player_count", C.c_int), ("split_networks", C.c_int),
-                ("env_seed_offset", C.c_uint64), ("rng_stream", C.c_uint64)]
+                ("env_seed_offset", C.c_uint64), ("rng_stream", C.c_uint64), ("shuffle_windows", C.c_int)]
 
 
 class UpdateMetrics(C.Structure):
@@ -385,7 +385,7 @@ def train_cfg(env_kind=ENV_CARTPOLE, num_envs=8, num_steps=128, hidden=64, num_h
               ctde=False, critic_hidden=0, critic_num_hidden=0, normalize_obs=True,
               normalize_returns=True, return_clip=10.0, gamma=0.99, gae_lambda=0.95, lr=1e-3,
               ent_coef=0.01, reward_shaping=0.0, seed=42, threads=0, cnn=None, normalize_values=False,
-              player_count=0, split=False, env_seed_offset=0, rng_stream=0, **ppo):
+              player_count=0, split=False, env_seed_offset=0, rng_stream=0, shuffle_windows=False, **ppo):
     """cnn: None, or (conv_channels per layer, kernel_size); hidden / num_hidden are
     then cnn_fc_hidden_size / cnn_num_fc_layers"""
     extra = {}
@@ -394,7 +394,7 @@ def train_cfg(env_kind=ENV_CARTPOLE, num_envs=8, num_steps=128, hidden=64, num_h
         extra = dict(cnn=1, num_conv=len(ch), conv_ch=(C.c_int * 4)(*[ch[min(i, len(ch) - 1)] for i in range(4)]),
                      ksize=ks)
     return TrainCfg(**extra, normalize_values=int(normalize_values), player_count=player_count,
-                    env_seed_offset=env_seed_offset, rng_stream=rng_stream,
+                    env_seed_offset=env_seed_offset, rng_stream=rng_stream, shuffle_windows=int(shuffle_windows),
                     split_networks=int(split), env_kind=env_kind, num_envs=num_envs, num_steps=num_steps, hidden=hidden,
                     num_hidden=num_hidden, relu=int(relu), ctde=int(ctde), critic_hidden=critic_hidden,
                     critic_num_hidden=critic_num_hidden, normalize_obs=int(normalize_obs),

@@ -34,6 +34,10 @@ CASES = {
     # CTDE (actor on obs, critic on cat[priv, obs]), 4 epochs x 8 minibatches
     "liars_dice_ctde": dict(preset="liars_dice_ctde", N=256, T=8,
                             over=dict(hidden_size=64, critic_hidden_size=64, critic_num_hidden=2)),
+    # shuffle_windows (bench.py's W > 1 mode): epoch e shuffles from S + e * (2B + 2^20)
+    "cartpole_windows": dict(preset="cartpole", N=1024, T=32, over=dict(shuffle_windows=True)),
+    "connect_four_windows": dict(preset="connect_four", N=256, T=16,
+                                 over=dict(hidden_size=64, shuffle_windows=True)),
 }
 
 
@@ -51,15 +55,18 @@ def _oracle_ranks(cfg, params, world):
     return [O.Trainer(oracle_train_cfg(cfg, rank=r, world=world), params) for r in range(world)]
 
 
-def _last_perm(seed, stream, start, B, epochs):
+def _last_perm(seed, stream, start, B, epochs, windows=False, num_epochs=0):
     import oracle_ffi as O
     r = O.new_rng(seed)
     r.stream = stream
     r.word_pos = start
-    for _ in range(epochs):
+    win = 2 * B + (1 << 20)
+    for e in range(epochs):
+        if windows:
+            r.word_pos = start + e * win
         p = np.arange(B, dtype=np.uint32)
         O.lib().or_shuffle_u32(C.byref(r), p, B)
-    return p, r.word_pos
+    return p, (start + num_epochs * win if windows else r.word_pos)
 
 
 def _worker(rank, world, port, q, case, mode):
@@ -113,7 +120,8 @@ def _worker(rank, world, port, q, case, mode):
         oms = O.Trainer.update_ranks(ots)
         assert tr.ctx.rng_pos() == ot.rng_pos()
         B = c["N"] * c["T"]
-        perm, end = _last_perm(cfg["seed"], rank, start, B, m["epochs_run"])
+        perm, end = _last_perm(cfg["seed"], rank, start, B, m["epochs_run"],
+                               bool(cfg.get("shuffle_windows")), cfg["num_epochs"])
         assert end == tr.ctx.rng_pos()
         assert np.array_equal(tr.ctx.buffer("perm", np.uint32)[:B], perm)
         assert_metrics_close(m, oms[rank], values=ot.buffer("values"), returns=ot.buffer("returns"), advantages=ot.buffer("advantages"))

@@ -69,3 +69,33 @@ def test_distinct_shards_share_one_step():
     assert np.array_equal(np.sign(dw[agree]), np.sign(d0[agree]))
     for t in ranks + solos + [ref]:
         t.close()
+
+
+def test_shuffle_windows_positions():
+    """shuffle_windows: epoch e shuffles from S + e * (2B + 2^20) and the update ends at
+    S + epochs * (2B + 2^20); epoch 0 is the reference's shuffle, so with one epoch the
+    parameters equal the sequential run's, only the RNG position after the update moves"""
+    cfg = _cfg(num_epochs=1)
+    params = bppo.orthogonal_init(cfg, seed=5)
+    seq = O.Trainer(oracle_train_cfg(cfg), params)
+    win = O.Trainer(oracle_train_cfg(dict(cfg, shuffle_windows=True)), params)
+    B = cfg["num_envs"] * cfg["num_steps"]
+    for t in (seq, win):
+        t.collect(); t.gae()
+    S = win.rng_pos()
+    assert seq.rng_pos() == S
+    seq.update(); win.update()
+    assert np.array_equal(seq.params().view(np.uint32), win.params().view(np.uint32))
+    assert win.rng_pos() == S + (2 * B + (1 << 20))
+    assert seq.rng_pos() < win.rng_pos()
+    # four epochs: epochs 1..3 shuffle from their windows, so the run departs from the
+    # sequential one
+    cfg4 = _cfg(num_epochs=4)
+    a = O.Trainer(oracle_train_cfg(cfg4), params)
+    b = O.Trainer(oracle_train_cfg(dict(cfg4, shuffle_windows=True)), params)
+    for t in (a, b):
+        t.collect(); t.gae(); t.update()
+    assert b.rng_pos() == S + 4 * (2 * B + (1 << 20))
+    assert not np.array_equal(a.params().view(np.uint32), b.params().view(np.uint32))
+    for t in (seq, win, a, b):
+        t.close()

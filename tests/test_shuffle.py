@@ -106,7 +106,7 @@ def test_shuffle_engine_equals_sequential_walks(seed, start, n, epochs, gap, job
     J = np.zeros(n * epochs * jobs, np.uint32)
     ends = np.zeros(epochs * jobs, np.uint64)
     met = np.zeros(epochs * jobs, np.int32)
-    assert L.lib().bppo_debug_shuffle_engine(seed, 0, start, n, epochs, gap, jobs, J.ctypes.data,
+    assert L.lib().bppo_debug_shuffle_engine(seed, 0, start, n, epochs, gap, jobs, 0, J.ctypes.data,
                                              ends.ctypes.data, met.ctypes.data) == 0
     pos = start
     for j in range(jobs):
@@ -137,7 +137,7 @@ def test_shuffle_engine_policies_equal_sequential(monkeypatch, policy, seed, sta
     J = np.zeros(n * epochs * jobs, np.uint32)
     ends = np.zeros(epochs * jobs, np.uint64)
     met = np.zeros(epochs * jobs, np.int32)
-    assert L.lib().bppo_debug_shuffle_engine(seed, 0, start, n, epochs, gap, jobs, J.ctypes.data,
+    assert L.lib().bppo_debug_shuffle_engine(seed, 0, start, n, epochs, gap, jobs, 0, J.ctypes.data,
                                              ends.ctypes.data, met.ctypes.data) == 0
     pos = start
     for j in range(jobs):
@@ -150,3 +150,36 @@ def test_shuffle_engine_policies_equal_sequential(monkeypatch, policy, seed, sta
             assert np.array_equal(J[k * n:(k + 1) * n], Je), (j, e, met)
             pos = end.value
         pos += gap
+
+
+def _window(n):
+    return 2 * n + (1 << 20)      # shuffle_window (bppo_internal.h)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("threads", ["16", "2"])
+@pytest.mark.parametrize("seed,start,n,epochs,gap,jobs", [
+    (5, 77, 1 << 23, 4, 16_777_216, 3),
+    (9, 3, 100_003, 6, 700_000, 3),
+])
+def test_shuffle_engine_windows_equal_sequential(monkeypatch, threads, seed, start, n, epochs, gap, jobs):
+    """shuffle_windows: epoch e of an update starts at S + e * (2 n + 2^20), the next
+    update gap words after S + epochs * (2 n + 2^20).  The engine walks the epochs at
+    once, exactly (no speculation), with 16 or 2 host CPUs; J and the end positions must
+    equal the single-thread walks from those starts."""
+    monkeypatch.setenv("BPPO_HOST_THREADS", threads)
+    J = np.zeros(n * epochs * jobs, np.uint32)
+    ends = np.zeros(epochs * jobs, np.uint64)
+    assert L.lib().bppo_debug_shuffle_engine(seed, 0, start, n, epochs, gap, jobs, 1, J.ctypes.data,
+                                             ends.ctypes.data, None) == 0
+    S = start
+    for j in range(jobs):
+        for e in range(epochs):
+            k = j * epochs + e
+            Je = np.zeros(n, np.uint32)
+            end = C.c_uint64()
+            assert L.lib().bppo_debug_shuffle_chain(seed, 0, S + e * _window(n), n, Je.ctypes.data, C.byref(end)) == 0
+            assert ends[k] == end.value, (j, e)
+            assert end.value - (S + e * _window(n)) < _window(n)      # the walk stays inside its window
+            assert np.array_equal(J[k * n:(k + 1) * n], Je), (j, e)
+        S = S + epochs * _window(n) + gap
