@@ -13,6 +13,7 @@
 #include <sys/prctl.h>
 #include <x86intrin.h>
 #include "bppo_internal.h"
+#include "shuffle_host.h"
 #include "bppo_wide.h"
 
 using namespace bppo;
@@ -1449,6 +1450,39 @@ extern "C" bppo_status bppo_debug_shuffle_chain(uint64_t seed, uint64_t stream, 
     const Key8 key = seed_key(seed);
     const uint64_t e = shuffle_walk_host(key, stream, word_pos, n, J);
     if (end_pos) *end_pos = e;
+    return BPPO_OK;
+}
+
+extern "C" bppo_status bppo_debug_chain_walk2(uint64_t seed, uint64_t stream, uint64_t pos_a, uint64_t pos_b,
+                                              uint32_t n, uint32_t piece, uint64_t *end_a, uint64_t *end_b) {
+    if (!end_a || !end_b || piece < 1) return BPPO_ERR_ARG;
+    const Key8 key = seed_key(seed);
+    struct Ch { uint64_t pos; uint32_t r; std::vector<uint32_t> w; size_t off, left; } ch[2];
+    ch[0].pos = pos_a; ch[1].pos = pos_b;
+    auto refill = [&](Ch &c) {
+        const uint64_t q = (c.pos / piece + 1) * piece;
+        c.w.resize(q - c.pos);
+        bppo_host::chacha12_words(key.k, stream, c.pos, c.w.data(), c.w.size());
+        c.off = 0;
+        c.left = c.w.size();
+    };
+    for (Ch &c : ch) { c.r = n; refill(c); }
+    auto live = [](const Ch &c) { return c.r >= 2; };
+    auto advance = [&](Ch &c, size_t u) {
+        c.off += u; c.left -= u; c.pos += u;
+        if (live(c) && c.left == 0) refill(c);
+    };
+    while (live(ch[0]) && live(ch[1])) {
+        size_t u0 = 0, u1 = 0;
+        bppo_host::chain_walk2_nj(ch[0].w.data() + ch[0].off, ch[0].left, &ch[0].r, &u0,
+                                  ch[1].w.data() + ch[1].off, ch[1].left, &ch[1].r, &u1);
+        advance(ch[0], u0);
+        advance(ch[1], u1);
+    }
+    for (Ch &c : ch)
+        while (live(c)) advance(c, bppo_host::chain_walk_nj(c.w.data() + c.off, c.left, &c.r));
+    *end_a = ch[0].pos;
+    *end_b = ch[1].pos;
     return BPPO_OK;
 }
 

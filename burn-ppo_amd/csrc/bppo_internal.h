@@ -130,6 +130,7 @@ struct ShuffleEngine {
     uint64_t stream = 0;
     uint64_t gap = 0;                             // words between an update's last shuffle and the next update's first
     uint64_t win = 0;                             // shuffle_windows: epoch e starts at job start + e * win (0: chained)
+    bool pair = false;                            // windowed: worker 2m walks epochs 2m and 2m+1 interleaved
     double Ew = 0.0, sigma = 0.0;                 // expected words per shuffle, its std dev
     int K = 0;                                    // speculative walks per epoch boundary
     int host_cpus = 16;                           // CPU budget of this rank (BPPO_HOST_THREADS)
@@ -209,6 +210,7 @@ struct ShuffleEngine {
     void stop_walks(int lo, int hi);                     // stop and wait (mu not held)
     const uint32_t *words(int b, uint64_t pos, uint64_t len, std::vector<uint32_t> &scratch);
     struct WalkStats { uint64_t words = 0, tsc_walk = 0, tsc_words = 0; };
+    void walk_pair(int i, WalkStats &st);
     uint64_t walk_piece(int b, uint64_t pos, uint32_t *r, std::vector<uint32_t> &scratch, WalkStats &st);
     void flush(WalkStats &st, std::atomic<uint64_t> &words_ctr);
     int peek(int i, uint64_t q, uint32_t *r);     // walk i's range at checkpoint q: 1 known, 0 not yet, -1 never

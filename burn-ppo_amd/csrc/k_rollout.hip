@@ -404,6 +404,253 @@ __global__ void __launch_bounds__(512, 2) k_cartpole_rollout_mfma(RolloutArgs a,
     }
 }
 
+// The CfgB rollout with every lane owning an env: a wave
+// holds 64 envs as two 32-env MFMA tiles (lane l = env l; tile A = lanes 0-31,
+// tile B = lanes 32-63 of the wave's 64 envs) and runs both layers TRANSPOSED
+// (H^T = W^T X^T on v_mfma_f32_32x32x2_f32, units on the MFMA rows, envs on
+// its columns), with no LDS round trip:
+//  * layer 1's K pairs (x0,x1) (x2,x3) (x4,1) come from the env lanes through one
+//    v_permlane32_swap per pair; b0 rides in the K pad (fma(1, b0, acc) is the
+//    reference's separate + b0, rounded once);
+//  * layer 1's output rows are hidden units permuted so that accumulator
+//    register m of lane half h holds unit 2m + h: register m is then directly the
+//    B operand of layer 2's K step m (k = 2m on half 0, 2m + 1 on half 1), in
+//    natural k order (same fma chain as the reference's matmul);
+//  * layer 2's output rows are permuted so register m holds unit 32h + m; one
+//    v_permlane32_swap per register pair (tile A, tile B) leaves lane l with all
+//    64 units of env l (register m: unit m, its partner: unit 32 + m) for the
+//    heads' k-ordered chains (+ b1, relu, three fma chains per lane);
+//  * W0 (+b0) and W1 live in VGPRs for the whole rollout (70 per lane), the
+//    heads' {wp0, wp1, wv, b1} rows are LDS broadcasts, expf/logf tables in LDS.
+// One wave per SIMD (CfgB: 65,536 envs = 1,024 waves): ~300 VGPRs incl. AGPRs.
+namespace mmr {
+constexpr int H = 64, WAVES = 4;
+struct Params {
+    uint64_t exp2tab[32];
+    double linvc[16], llogc[16];
+    float4 hw[H];                 // {Wp[2k], Wp[2k+1], Wv[k], b1[k]}
+    float bp[2], bv[2];
+    __device__ __forceinline__ float expf(float x) const { return bppo_math::expf_glibc_tab(x, exp2tab); }
+    __device__ __forceinline__ float logf(float x) const { return bppo_math::logf_glibc_tab(x, linvc, llogc); }
+};
+// MFMA output row r (0..63) -> hidden unit, layer 1 / layer 2
+__device__ __forceinline__ int unit1(int r) {
+    const int rr = r & 31, ct = r >> 5, q = (rr & 3) + 4 * (rr >> 3), hh = (rr >> 2) & 1;
+    return 2 * (q + 16 * ct) + hh;
+}
+__device__ __forceinline__ int unit2(int r) {
+    const int rr = r & 31, ct = r >> 5, q = (rr & 3) + 4 * (rr >> 3), hh = (rr >> 2) & 1;
+    return 32 * hh + q + 16 * ct;
+}
+__device__ __forceinline__ void swap_halves(float &lo, float &hi) {
+    // lanes 32-63 of `lo` <-> lanes 0-31 of `hi`
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(lo), __float_as_uint(hi), false, false);
+    lo = __uint_as_float(r[0]);
+    hi = __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float log_prob2(const Params &S, const float (&x)[2], int a) {
+    const float m = x[1] > x[0] ? x[1] : x[0];
+    float s = 0.0f;
+    s = __fadd_rn(s, S.expf(__fsub_rn(x[0], m)));
+    s = __fadd_rn(s, S.expf(__fsub_rn(x[1], m)));
+    const float lse = S.logf(s);
+    return __fsub_rn(__fsub_rn(a ? x[1] : x[0], m), lse);
+}
+}  // namespace mmr
+
+__global__ void __launch_bounds__(256, 1) k_cartpole_rollout_mfma64(RolloutArgs a, const float *__restrict__ gum) {
+    using namespace mmr;
+    constexpr CpOffsets O = cp_offsets<64, 2>();
+    __shared__ Params S;
+    const float *__restrict__ P = a.params;
+    for (int i = threadIdx.x; i < H; i += blockDim.x)
+        S.hw[i] = make_float4(P[O.wp + 2 * i], P[O.wp + 2 * i + 1], P[O.wv + i], P[O.b1 + i]);
+    if (threadIdx.x < 32) S.exp2tab[threadIdx.x] = bppo_math::kExp2fTab[threadIdx.x];
+    if (threadIdx.x < 16) {
+        S.linvc[threadIdx.x] = bppo_math::kLogfInvc[threadIdx.x];
+        S.llogc[threadIdx.x] = bppo_math::kLogfLogc[threadIdx.x];
+    }
+    if (threadIdx.x < 2) S.bp[threadIdx.x] = P[O.bp + threadIdx.x];
+    if (threadIdx.x == 0) S.bv[0] = P[O.bv];
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
+    const int N = a.N;
+    const int e = (blockIdx.x * WAVES + (threadIdx.x >> 6)) * 64 + lane;
+    const bool mine = e < N;
+    // the weights this lane feeds the MFMAs for the whole rollout
+    float w0r[3][2], w1r[32][2];
+#pragma unroll
+    for (int st = 0; st < 3; st++)
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++) {
+            const int d = 2 * st + h, u = unit1(c + 32 * ct);
+            w0r[st][ct] = d < 5 ? P[O.w0 + d * H + u] : P[O.b0 + u];
+        }
+#pragma unroll
+    for (int st = 0; st < 32; st++)
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++) w1r[st][ct] = P[O.w1 + (2 * st + h) * H + unit2(c + 32 * ct)];
+
+    CartPoleState s{};
+    uint64_t env_pos = 0;
+    float ep_ret = 0.0f;
+    int32_t ep_len = 0;
+    if (mine) {
+        load_state(a.cp, a.steps, N, e, s);
+        env_pos = a.env_pos[e];
+        ep_ret = a.ep_ret[e];
+        ep_len = a.ep_len[e];
+    }
+    ObsNorm5 nz;
+    nz.load(a.on, a.norm_on);
+    ObsAcc5 oa;
+    {
+        float raw0[5];
+        cartpole_obs(s, raw0);
+        oa.init(raw0);
+    }
+    int32_t bad = 0;
+    float2 gz = make_float2(0.0f, 0.0f);
+    if (mine && a.T > 0) gz = *reinterpret_cast<const float2 *>(gum + (size_t)e * 2);
+#pragma unroll 1
+    for (int t = 0; t < a.T; t++) {
+        const size_t row = (size_t)t * N + e;
+        // the next step's Gumbel pair, in flight under this step's MFMAs
+        float2 gz_next = make_float2(0.0f, 0.0f);
+        if (mine && t + 1 < a.T) gz_next = *reinterpret_cast<const float2 *>(gum + (row + N) * 2);
+        float x[6] = {0, 0, 0, 0, 0, 1.0f};
+        if (mine) {
+            float raw[5], z[5];
+            cartpole_obs(s, raw);
+            oa.push(raw);
+            nz.apply(raw, z);
+#pragma unroll
+            for (int d = 0; d < 5; d++) x[d] = z[d];
+        }
+        // ---- layer 1 (transposed): H1^T = [W0; b0]^T [x, 1]^T, two env tiles
+        f32x16_t h1[2][2];
+#pragma unroll
+        for (int tl = 0; tl < 2; tl++)
+#pragma unroll
+            for (int ct = 0; ct < 2; ct++)
+#pragma unroll
+                for (int q = 0; q < 16; q++) h1[tl][ct][q] = 0.0f;
+#pragma unroll
+        for (int st = 0; st < 3; st++) {
+            float pa = x[2 * st], pb = x[2 * st + 1];
+            swap_halves(pa, pb);         // pa: tile A's (k = 2st, 2st + 1), pb: tile B's
+#pragma unroll
+            for (int ct = 0; ct < 2; ct++) {
+                h1[0][ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(w0r[st][ct], pa, h1[0][ct], 0, 0, 0);
+                h1[1][ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(w0r[st][ct], pb, h1[1][ct], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int tl = 0; tl < 2; tl++)
+#pragma unroll
+            for (int ct = 0; ct < 2; ct++)
+#pragma unroll
+                for (int q = 0; q < 16; q++) {
+                    const float v = h1[tl][ct][q];
+                    h1[tl][ct][q] = v > 0.0f ? v : 0.0f;
+                }
+        // ---- layer 2 (transposed): register m of h1 is K step m
+        f32x16_t h2[2][2];
+#pragma unroll
+        for (int tl = 0; tl < 2; tl++)
+#pragma unroll
+            for (int ct = 0; ct < 2; ct++)
+#pragma unroll
+                for (int q = 0; q < 16; q++) h2[tl][ct][q] = 0.0f;
+#pragma unroll
+        for (int st = 0; st < 32; st++)
+#pragma unroll
+            for (int ct = 0; ct < 2; ct++)
+#pragma unroll
+                for (int tl = 0; tl < 2; tl++)
+                    h2[tl][ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(w1r[st][ct], h1[tl][st >> 4][st & 15],
+                                                                      h2[tl][ct], 0, 0, 0);
+        // lane l <- all 64 units of env l: hA[m] = unit m, hB[m] = unit 32 + m
+        float hA[32], hB[32];
+#pragma unroll
+        for (int m = 0; m < 32; m++) {
+            hA[m] = h2[0][m >> 4][m & 15];
+            hB[m] = h2[1][m >> 4][m & 15];
+            swap_halves(hA[m], hB[m]);
+        }
+        // ---- heads: + b1, relu, the k-ordered chains of logit 0, logit 1, value
+        // (the row reads stay in the step loop: hoisted, they would pin 256 VGPRs)
+        int zero = 0;
+        asm volatile("" : "+v"(zero));
+        const float4 *hw = S.hw + zero;
+        float l0 = 0.0f, l1 = 0.0f, vv = 0.0f;
+#pragma unroll
+        for (int k = 0; k < H; k++) {
+            const float4 w = hw[k];
+            float z = __fadd_rn(k < 32 ? hA[k] : hB[k - 32], w.w);
+            z = z > 0.0f ? z : 0.0f;
+            l0 = __builtin_fmaf(z, w.x, l0);
+            l1 = __builtin_fmaf(z, w.y, l1);
+            vv = __builtin_fmaf(z, w.z, vv);
+        }
+        float lg[2];
+        lg[0] = __fadd_rn(l0, S.bp[0]);
+        lg[1] = __fadd_rn(l1, S.bp[1]);
+        const float v = __fadd_rn(vv, S.bv[0]);
+        const float n0 = __fadd_rn(lg[0], gz.x);
+        const float n1 = __fadd_rn(lg[1], gz.y);
+        const int act = n1 > n0 ? 1 : 0;               // argmax, first maximum
+        const float lp = log_prob2(S, lg, act);
+        bool done = false;
+        float r = 0.0f;
+        if (mine) {
+            bad |= !isfinite(lp);
+            done = cartpole_step(s, act, r);
+            ep_ret = __fadd_rn(ep_ret, r);
+            ep_len += 1;
+        }
+        const int32_t k = wave_episode_slot(done, a.ep_count);
+        if (done) {
+            if (k < a.eps_cap) {
+                EpisodeRec rec;
+                rec.total_reward[0] = ep_ret;
+                for (int p = 1; p < BPPO_MAX_PLAYERS; p++) rec.total_reward[p] = 0.0f;
+                rec.length = ep_len; rec.env_index = e; rec.step = t; rec.pad = 0;
+                a.eps[k] = rec;
+            }
+            WordCursor ec;
+            ec.init(seed_key(a.seed_base + (uint64_t)e), 0, env_pos);
+            cartpole_reset(s, ec);
+            env_pos = ec.pos;
+            ep_ret = 0.0f;
+            ep_len = 0;
+        }
+        if (mine) {
+#pragma unroll
+            for (int d = 0; d < 5; d++) a.obs[row * 5 + d] = x[d];
+            a.act[row] = act;
+            a.rew_raw[row] = r;
+            a.done[row] = done ? 1.0f : 0.0f;
+            a.val[row] = v;
+            a.logp[row] = lp;
+            if (a.rows) {
+                a.rows[row * 2] = make_float4(x[0], x[1], x[2], x[3]);
+                a.rows[row * 2 + 1] = make_float4(x[4], __int_as_float(act), lp, v);
+            }
+        }
+        gz = gz_next;
+    }
+    if (mine) {
+        store_state(a.cp, a.steps, N, e, s);
+        a.env_pos[e] = env_pos;
+        a.ep_ret[e] = ep_ret;
+        a.ep_len[e] = ep_len;
+        oa.store((double)a.T, a.obs_part + (size_t)e * 10);
+        if (bad) atomicOr(a.err, 1);
+    }
+}
+
 // VecEnv::step surface (env.rs:400-487) for host-driven stepping.
 __global__ void k_cartpole_step(int N, uint64_t seed_base, float *cp, int32_t *steps,
                                 uint64_t *env_pos, float *ep_ret, int32_t *ep_len,
@@ -625,9 +872,16 @@ bppo_status launch_cartpole_rollout(bppo_ctx *c, uint64_t base_pos, const double
         const uint64_t blocks = ((base_pos + count + 15) >> 4) - (base_pos >> 4);
         hipLaunchKernelGGL(k_gumbel_words, dim3((unsigned)((blocks + 255) / 256)), dim3(256), 0, c->stream, c->rng_key,
                            (uint64_t)c->cfg.rng_stream, base_pos, count, c->d_gumbel);
-        const int waves = (c->N + mmb::TR - 1) / mmb::TR;
-        hipLaunchKernelGGL(k_cartpole_rollout_mfma, dim3((waves + mmb::WAVES - 1) / mmb::WAVES), dim3(64 * mmb::WAVES),
-                           mmb::LDS, c->stream, a, (const float *)c->d_gumbel);
+        static const bool tiles32 = getenv("BPPO_ROLLOUT_TILES32") != nullptr;   // A/B: r03's half-wave kernel
+        if (tiles32) {
+            const int waves = (c->N + mmb::TR - 1) / mmb::TR;
+            hipLaunchKernelGGL(k_cartpole_rollout_mfma, dim3((waves + mmb::WAVES - 1) / mmb::WAVES), dim3(64 * mmb::WAVES),
+                               mmb::LDS, c->stream, a, (const float *)c->d_gumbel);
+        } else {
+            const int waves = (c->N + 63) / 64;
+            hipLaunchKernelGGL(k_cartpole_rollout_mfma64, dim3((waves + mmr::WAVES - 1) / mmr::WAVES),
+                               dim3(64 * mmr::WAVES), 0, c->stream, a, (const float *)c->d_gumbel);
+        }
         BPPO_HIP(c, hipGetLastError());
         return BPPO_OK;
     }

@@ -251,6 +251,9 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
     // shuffle_windows: every epoch's start is known when the job starts, so each epoch is
     // one exact walk (slot e), all walked at once; nothing to speculate or carry
     if (win) { K = 1; C = 0; fr_depth = 0; }
+    // and the epochs' walks go in pairs, two chains interleaved per thread (half the
+    // walking CPU of one chain per thread: the walker is latency-bound)
+    pair = win && !(getenv("BPPO_SHUFFLE_PAIR") && atoi(getenv("BPPO_SHUFFLE_PAIR")) == 0);
     // exact continuations need the last epoch in the in-job groups
     const bool cont_on = !win && epochs - 1 >= C;
     K = std::min(K, SHUF_MAX_SPEC / (std::max(epochs - C, 0) + 2 * C + (cont_on ? 2 : 0)));
@@ -481,6 +484,11 @@ void ShuffleEngine::worker(int i) {
             if (quit) { s.running = false; cv.notify_all(); return; }
             seen = s.gen;
         }
+        if (pair && i < nspec - (nspec & 1)) {
+            if (i & 1) continue;        // walked by worker i - 1, interleaved with its own
+            walk_pair(i, wst);
+            continue;
+        }
         uint64_t pos = s.start;
         uint32_t r = n;
         while (r >= 2 && !s.stop.load(std::memory_order_relaxed)) {
@@ -515,6 +523,83 @@ void ShuffleEngine::worker(int i) {
         }
         cv.notify_all();
     }
+}
+
+// windowed jobs: walks i and i + 1 (two epochs, known starts, nothing to merge with)
+// in one thread, their 32-word blocks interleaved (chain_walk2_nj); checkpoints as
+// in worker().  A walk that ends is marked done at once, the other goes on alone.
+void ShuffleEngine::walk_pair(int i, WalkStats &st) {
+    struct Chain {
+        SpecWalk *s;
+        uint64_t pos;
+        uint32_t r;
+        const uint32_t *w;
+        size_t left;
+        std::vector<uint32_t> scratch;
+        bool live;
+    } ch[2];
+    {
+        std::unique_lock<std::mutex> lk(mu);   // the partner's launch is under the same lock
+        cv.wait(lk, [&] { return quit || spec[i + 1].running; });
+        if (quit) return;
+    }
+    auto refill = [&](Chain &c) {
+        const uint64_t q = (c.pos / SHUF_CK + 1) * SHUF_CK;
+        const uint64_t t0 = __rdtsc();
+        c.w = words(c.s->wbuf, c.pos, q - c.pos, c.scratch);
+        st.tsc_words += __rdtsc() - t0;
+        c.left = (size_t)(q - c.pos);
+    };
+    auto finish = [&](Chain &c) {
+        c.live = false;
+        c.s->end = c.pos;
+        std::lock_guard<std::mutex> lk(mu);
+        c.s->done.store(1, std::memory_order_release);
+        c.s->running = false;
+    };
+    auto advance = [&](Chain &c, size_t used) {
+        c.w += used;
+        c.left -= used;
+        c.pos += used;
+        st.words += used;
+        if (c.r < 2 || c.s->stop.load(std::memory_order_relaxed)) { finish(c); cv.notify_all(); return; }
+        if (c.left == 0) {                       // at a checkpoint
+            const int64_t k = (int64_t)((c.pos - c.s->ck_base) / SHUF_CK);
+            if (k < (int64_t)c.s->ck.size()) {
+                c.s->ck[k] = c.r;
+                c.s->progress.store(k, std::memory_order_release);
+            }
+            refill(c);
+        }
+    };
+    for (int k = 0; k < 2; k++) {
+        Chain &c = ch[k];
+        c.s = &spec[i + k];
+        c.pos = c.s->start;
+        c.r = n;
+        c.live = n >= 2;
+        if (c.live) refill(c);
+        else finish(c);
+    }
+    while (ch[0].live && ch[1].live) {
+        size_t u0 = 0, u1 = 0;
+        const uint64_t t0 = __rdtsc();
+        bppo_host::chain_walk2_nj(ch[0].w, ch[0].left, &ch[0].r, &u0, ch[1].w, ch[1].left, &ch[1].r, &u1);
+        st.tsc_walk += __rdtsc() - t0;
+        advance(ch[0], u0);
+        advance(ch[1], u1);
+    }
+    for (int k = 0; k < 2; k++) {
+        Chain &c = ch[k];
+        while (c.live) {
+            const uint64_t t0 = __rdtsc();
+            const size_t u = bppo_host::chain_walk_nj(c.w, c.left, &c.r);
+            st.tsc_walk += __rdtsc() - t0;
+            advance(c, u);
+        }
+    }
+    flush(st, spec_words);
+    cv.notify_all();
 }
 
 void ShuffleEngine::generator() {

@@ -304,6 +304,74 @@ static size_t walk_avx512_nj_t(const u32 *w, size_t nw, u32 *rp) {
 }
 static size_t walk_avx512_nj(const u32 *w, size_t nw, u32 *rp) { return walk_avx512_nj_t<10>(w, nw, rp); }
 
+// one 32-word block of walk_avx512_nj_t (the caller checked r >= lowr + 48 and
+// 32 words left): returns the words consumed, advances r
+template <int NH>
+__attribute__((target("avx512f,avx512bw,avx512vl,avx512dq,bmi,bmi2,popcnt"), always_inline))
+static inline u32 block32(const u32 *w, u32 &r) {
+    const int lz = __builtin_clz(r);
+    const u32 z = (r << lz) - 1u;
+    const __m512i kidx = _mm512_setr_epi32(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+    const __m512i kidx16 = _mm512_add_epi32(kidx, _mm512_set1_epi32(16));
+    const __m512i sv = _mm512_set1_epi32((int)(1u << lz));
+    const __m512i w0 = _mm512_loadu_si512((const void *)w);
+    const __m512i w1 = _mm512_loadu_si512((const void *)(w + 16));
+    const __m512i rv = _mm512_set1_epi32((int)r), zv = _mm512_set1_epi32((int)z);
+    __m512i lo0 = _mm512_mullo_epi32(w0, _mm512_sub_epi32(rv, kidx));
+    __m512i lo1 = _mm512_mullo_epi32(w1, _mm512_sub_epi32(rv, kidx16));
+    __m512i zz0 = _mm512_sub_epi32(zv, _mm512_slli_epi32(kidx, lz));
+    __m512i zz1 = _mm512_sub_epi32(zv, _mm512_slli_epi32(kidx16, lz));
+    u64 Z[NH];
+    for (int j = 0; j < NH; j++) {
+        const __mmask32 m = _mm512_kunpackw(_mm512_cmple_epu32_mask(lo1, zz1), _mm512_cmple_epu32_mask(lo0, zz0));
+        Z[j] = (u64)(u32)~_cvtmask32_u32(m) | 0xFFFFFFFF00000000ull;
+        lo0 = _mm512_add_epi32(lo0, w0); lo1 = _mm512_add_epi32(lo1, w1);
+        zz0 = _mm512_add_epi32(zz0, sv); zz1 = _mm512_add_epi32(zz1, sv);
+    }
+    u64 L = 0;
+    for (int j = 0; j < NH; j++) L = _blsmsk_u64(Z[j] & ~L);
+    const u32 P = (u32)__builtin_popcountll(L);
+    r -= P - NH;
+    return P < 32 ? P : 32;
+}
+
+static inline bool block_ok(u32 r, size_t p, size_t nw) {
+    const u32 lowr = 1u << (31 - __builtin_clz(r));
+    return r >= lowr + 48 && p + 32 <= nw;
+}
+
+// single draws until a full in-band block fits again (or the words / the chain end)
+static inline void steps_until_block(const u32 *w, size_t nw, size_t &p, u32 &r) {
+    while (r >= 2 && p < nw) {
+        if (r >= 2 && block_ok(r, p, nw)) return;
+        const int lz = __builtin_clz(r);
+        const u32 lo = w[p++] * r;
+        r -= lo <= (r << lz) - 1u;
+    }
+}
+
+// two independent chains, one block of each per iteration: the out-of-order core
+// overlaps their dependency chains (0.24-0.30 ns per word per chain measured on the
+// box with scripts/microbench/walk2_bench.cpp, vs 0.42-0.44 for one chain)
+__attribute__((target("avx512f,avx512bw,avx512vl,avx512dq,bmi,bmi2,popcnt")))
+static void walk2_avx512_nj(const u32 *wa, size_t na, u32 *rap, size_t *ua, const u32 *wb, size_t nb, u32 *rbp,
+                            size_t *ub) {
+    u32 ra = *rap, rb = *rbp;
+    size_t pa = 0, pb = 0;
+    for (;;) {
+        while (block_ok(ra, pa, na) && block_ok(rb, pb, nb)) {
+            pa += block32<10>(wa + pa, ra);
+            pb += block32<10>(wb + pb, rb);
+        }
+        steps_until_block(wa, na, pa, ra);
+        steps_until_block(wb, nb, pb, rb);
+        const bool da = ra < 2 || pa >= na || !block_ok(ra, pa, na);
+        const bool db = rb < 2 || pb >= nb || !block_ok(rb, pb, nb);
+        if (da || db) break;        // one chain has reached its end or the end of its words
+    }
+    *rap = ra; *rbp = rb; *ua = pa; *ub = pb;
+}
+
 static int isa_level() {
     static int v = -1;
     if (v < 0) {
@@ -319,6 +387,12 @@ int chain_walk_isa() { return isa_level(); }
 size_t chain_walk_nj(const u32 *w, size_t nw, u32 *r) {
     if (isa_level() == 2) return walk_avx512_nj(w, nw, r);
     return walk_scalar_nj(w, nw, r);
+}
+
+void chain_walk2_nj(const u32 *wa, size_t na, u32 *ra, size_t *ua, const u32 *wb, size_t nb, u32 *rb, size_t *ub) {
+    if (isa_level() == 2) return walk2_avx512_nj(wa, na, ra, ua, wb, nb, rb, ub);
+    *ua = walk_scalar_nj(wa, na, ra);
+    *ub = walk_scalar_nj(wb, nb, rb);
 }
 
 size_t chain_walk(const u32 *w, size_t nw, u32 *r, u32 *J) {

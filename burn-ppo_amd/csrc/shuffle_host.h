@@ -24,6 +24,13 @@ size_t chain_walk(const uint32_t *w, size_t nw, uint32_t *r, uint32_t *J);
 // chain_walk without writing J (the range r advances exactly the same way)
 size_t chain_walk_nj(const uint32_t *w, size_t nw, uint32_t *r);
 
+// two independent chains at once (their blocks interleaved in one loop): walks both
+// until EITHER has used all its words or reached r < 2; *ua / *ub = the words each
+// consumed (the other chain stops at a block boundary, its state exact).  Same
+// chains as chain_walk_nj over the same words.
+void chain_walk2_nj(const uint32_t *wa, size_t na, uint32_t *ra, size_t *ua,
+                    const uint32_t *wb, size_t nb, uint32_t *rb, size_t *ub);
+
 // 2 = AVX-512 walker, 1 = scalar
 int chain_walk_isa();
 

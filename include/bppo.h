@@ -310,6 +310,12 @@ bppo_status bppo_debug_libm(int32_t which, int32_t device, const float *x, float
 bppo_status bppo_debug_shuffle_chain(uint64_t seed, uint64_t stream, uint64_t word_pos, uint32_t n,
                                      uint32_t *J, uint64_t *end_pos);
 bppo_status bppo_debug_fisher_yates(int32_t device, const uint32_t *J, uint32_t n, uint32_t *perm);
+/* host only: two draw chains of n (from word positions pos_a, pos_b) walked together by
+ * the interleaved two-chain walker the shuffle_windows engine uses, over words handed
+ * over in pieces ending at multiples of `piece` words; *end_a / *end_b = the positions
+ * after each shuffle (must equal bppo_debug_shuffle_chain's) */
+bppo_status bppo_debug_chain_walk2(uint64_t seed, uint64_t stream, uint64_t pos_a, uint64_t pos_b, uint32_t n,
+                                   uint32_t piece, uint64_t *end_a, uint64_t *end_b);
 /* the whole shuffle engine (GPU-made ChaCha words, speculative walks, J rebuilt on
  * the GPU) for `jobs` updates of `epochs` shuffles of n: the first from word
  * position start, each next update `gap` words after the previous one's last

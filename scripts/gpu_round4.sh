@@ -18,7 +18,7 @@ fi
 if [ "$PART" = win ]; then
   # shuffle_windows parity + the 2-CPU bench (an 8-rank node's per-rank share) with and
   # without the windows, then the default bench and one PMC pass (LDS bank conflicts)
-  timeout -k 10 600 python -u -m pytest tests/test_shuffle.py tests/test_gpu_multirank.py -m gpu -q -k "windows" --timeout 300 --timeout-method thread -rf > gpurun_out/${TAG}_pytest_win.log 2>&1
+  timeout -k 10 900 python -u -m pytest ${WIN_TESTS:-tests/test_shuffle.py tests/test_gpu_multirank.py} -m gpu -q -k "${WIN_K:-windows}" --timeout 300 --timeout-method thread -rf > gpurun_out/${TAG}_pytest_win.log 2>&1
   rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|FAILED" gpurun_out/${TAG}_pytest_win.log | tail -12; [ $rc -eq 0 ] || exit $rc
   for v in "2 on" "2 off" "0 auto"; do
     set -- $v

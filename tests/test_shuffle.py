@@ -183,3 +183,19 @@ def test_shuffle_engine_windows_equal_sequential(monkeypatch, threads, seed, sta
             assert end.value - (S + e * _window(n)) < _window(n)      # the walk stays inside its window
             assert np.array_equal(J[k * n:(k + 1) * n], Je), (j, e)
         S = S + epochs * _window(n) + gap
+
+
+@pytest.mark.parametrize("seed,pa,pb,n,piece", [
+    (1, 0, 5, 1000, 1024), (7, 123, 99_999, 100_003, 1024), (42, 16_777_216, 1 << 30, 1 << 20, 1024),
+    (3, 1, 2, 70_000, 37), (9, 0, 0, 5000, 1), (11, 1 << 33, 77, 3, 1024)])
+def test_two_chain_walker_equals_sequential(seed, pa, pb, n, piece):
+    """the interleaved two-chain walker (shuffle_windows pairs, shuffle_host.cpp
+    chain_walk2_nj) over words handed over in pieces, incl. 1-word and odd-length pieces
+    and band edges: both chains end exactly where the sequential walks end (host only)"""
+    ea, eb = C.c_uint64(), C.c_uint64()
+    assert L.lib().bppo_debug_chain_walk2(seed, 0, pa, pb, n, piece, C.byref(ea), C.byref(eb)) == 0
+    for p, got in ((pa, ea.value), (pb, eb.value)):
+        J = np.zeros(n, np.uint32)
+        end = C.c_uint64()
+        assert L.lib().bppo_debug_shuffle_chain(seed, 0, p, n, J.ctypes.data, C.byref(end)) == 0
+        assert got == end.value
