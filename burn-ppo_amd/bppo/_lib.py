@@ -80,7 +80,7 @@ EXPORTS = (
     "bppo_obs_norm_get", "bppo_obs_norm_set", "bppo_ret_norm_get", "bppo_ret_norm_set",
     "bppo_collect_rollouts", "bppo_rollout_episodes", "bppo_compute_gae", "bppo_ppo_update", "bppo_train_step", "bppo_train_steps",
     "bppo_set_allreduce", "bppo_set_allreduce_async", "bppo_get_stream", "bppo_opponents_set", "bppo_opponents_get_envs", "bppo_buffer_get", "bppo_buffer_set", "bppo_gae_device", "bppo_gae_rows_device",
-    "bppo_gae_mp_device", "bppo_last_kernel_ms", "bppo_debug_libm", "bppo_debug_shuffle_chain", "bppo_debug_chain_walk2",
+    "bppo_gae_mp_device", "bppo_last_kernel_ms", "bppo_debug_libm", "bppo_debug_shuffle_chain", "bppo_debug_chain_walk2", "bppo_minibatch_rows",
     "bppo_debug_fisher_yates", "bppo_debug_gemm", "bppo_debug_shuffle_engine", "bppo_debug_sample",
     "bppo_rng_fill_bytes", "bppo_rng_from_seed", "bppo_rng_key_get", "bppo_num_param_tensors",
     "bppo_optimizer_get", "bppo_optimizer_set", "bppo_popart_get", "bppo_popart_set",
@@ -154,6 +154,7 @@ def lib():
         "bppo_last_kernel_ms": (i32, [vp, C.c_char_p, fp]),
         "bppo_debug_libm": (i32, [i32, i32, vp, vp, sz]),
         "bppo_debug_shuffle_chain": (i32, [u64, u64, u64, C.c_uint32, vp, C.POINTER(u64)]),
+        "bppo_minibatch_rows": (i32, [vp, vp, i32, C.POINTER(i32)]),
         "bppo_debug_chain_walk2": (i32, [u64, u64, u64, u64, C.c_uint32, C.c_uint32, C.POINTER(u64), C.POINTER(u64)]),
         "bppo_debug_fisher_yates": (i32, [i32, vp, C.c_uint32, vp]),
         "bppo_debug_gemm": (i32, [i32, i32, i32, i32, vp, vp, vp, i32, vp, vp]),

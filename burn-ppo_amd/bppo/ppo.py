@@ -78,6 +78,17 @@ class Context:
         self._chk(L.lib().bppo_buffer_get(self.h, name.encode(), out.ctypes.data, out.nbytes))
         return out.reshape(shape) if shape else out
 
+    def minibatch_rows(self):
+        """the last update's per-minibatch metric rows [runs, width] (bppo_minibatch_rows):
+        columns 0-4 = sums of policy loss, 2 x value loss, entropy, approx KL, clip
+        fraction; column 10 = the minibatch's row count"""
+        w = C.c_int32()
+        n = L.lib().bppo_minibatch_rows(self.h, None, 0, C.byref(w))
+        out = np.zeros((max(n, 0), w.value), np.float32)
+        if n > 0:
+            L.lib().bppo_minibatch_rows(self.h, out.ctypes.data, n, C.byref(w))
+        return out
+
     def set_buffer(self, name, arr):
         arr = np.ascontiguousarray(arr)
         self._chk(L.lib().bppo_buffer_set(self.h, name.encode(), arr.ctypes.data, arr.nbytes))

@@ -1165,6 +1165,7 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
     }
     c->last_ms[TM_FWDBWD] = fw_ms;
     c->last_ms[TM_SHUFFLE] = sh_ms;
+    c->last_rows = rows;
     if (m) {
         std::memset(m, 0, sizeof *m);
         const int nup = (int)(rows.size() / (NM + 4));
@@ -1347,6 +1348,16 @@ extern "C" bppo_status bppo_buffer_get(bppo_ctx *c, const char *name, void *host
     BPPO_HIP(c, hipMemcpyAsync(host, b.ptr, b.bytes, hipMemcpyDeviceToHost, c->stream));
     BPPO_HIP(c, sync_stream(c));
     return BPPO_OK;
+}
+
+extern "C" int32_t bppo_minibatch_rows(bppo_ctx *c, float *out, int32_t max_rows, int32_t *row_width) {
+    if (!c) return -1;
+    const int32_t w = WM_COUNT + 4;
+    const int32_t n = (int32_t)(c->last_rows.size() / (size_t)w);
+    if (row_width) *row_width = w;
+    if (out && max_rows > 0)
+        std::memcpy(out, c->last_rows.data(), sizeof(float) * (size_t)std::min(n, max_rows) * (size_t)w);
+    return n;
 }
 
 extern "C" bppo_status bppo_buffer_set(bppo_ctx *c, const char *name, const void *host, size_t bytes) {

@@ -302,6 +302,7 @@ struct bppo_ctx {
     float *d_mb_stats = nullptr;      // advantage [mean, std, min, max] of each minibatch of the epoch [M][4]
     float *d_mb_cur = nullptr;        // the current minibatch's row of d_mb_stats
     float *d_rows = nullptr;          // per-minibatch metric rows of one update [E*M][WM_COUNT + 4]
+    std::vector<float> last_rows;     // the last update's rows, host copy (bppo_buffer_get "minibatch_rows")
     // CfgB net: the update's minibatch rows packed in two arrays, so every store of the
     // rollout and of GAE covers whole 32-byte sectors of consecutive rows: d_rowA [B][2]
     // float4 = [obs 0..3][obs 4, action, log-prob, value] (32 B, the rollout writes it),

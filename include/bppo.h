@@ -267,6 +267,12 @@ bppo_status bppo_opponents_get_envs(bppo_ctx *ctx, int32_t *learner_pos, int32_t
  * "actions" (i32), "rewards", "dones", "values", "log_probs", "advantages",
  * "returns", "players" (i32), "all_rewards", "masks", "last_v_pp", "perm" (u32,
  * last epoch's shuffled indices) */
+/* the last update's per-minibatch metric rows in run order (parity diagnosis: which
+ * minibatch's statistics first leave the bar): row k = the minibatch's sums
+ * [policy_loss, 2*value_loss, entropy, approx_kl, clip_fraction, value, return, |v-R|,
+ * (v-R)^2, max |v-R|, rows, ...] then 4 advantage statistics; returns the row count,
+ * copies up to max_rows rows of *row_width floats into out (may be NULL) */
+int32_t bppo_minibatch_rows(bppo_ctx *ctx, float *out, int32_t max_rows, int32_t *row_width);
 bppo_status bppo_buffer_get(bppo_ctx *ctx, const char *name, void *host, size_t bytes);
 bppo_status bppo_buffer_set(bppo_ctx *ctx, const char *name, const void *host, size_t bytes);
 

@@ -316,6 +316,10 @@ void or_adam_step(const or_net_desc *d, or_adam *a, float *params, float *grads,
 
 /* ---------------------------------------------------------- trainer ------ */
 typedef struct or_trainer or_trainer;
+#define OR_MB_LOG_MAX 256
+/* the last update's per-minibatch statistics in run order (the metrics of all ranks'
+ * rows at W > 1); returns how many minibatches ran, copies up to max */
+int or_trainer_mb_log(const or_trainer *t, or_mb_stats *out, int max);
 typedef struct {
     int env_kind;
     int num_envs, num_steps;

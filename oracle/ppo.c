@@ -111,6 +111,9 @@ struct or_trainer {
     int32_t *lpos, *p2o, *curopp;
     int Pa;                  /* seated players: EnvState's num_players (main.rs:552, 649) */
     float *valid;
+    /* the last update's per-minibatch statistics, in run order (parity diagnosis) */
+    or_mb_stats mblog[OR_MB_LOG_MAX];
+    int n_mblog;
 };
 
 static double now_s(void) {
@@ -590,6 +593,7 @@ void or_trainers_update(or_trainer **ts, int W, or_update_metrics *ms) {
     float tp = 0, tv = 0, th = 0, tk = 0, tc = 0, tl = 0, tvm = 0, trm = 0;
     float tvem = 0, tves = 0, tav = 0, tevp = 0;
     int nup = 0, epochs_run = 0, stop = 0;
+    for (int r = 0; r < W; r++) ts[r]->n_mblog = 0;
     uint64_t S[64];                      /* each rank's first shuffle word (shuffle_windows) */
     for (int r = 0; r < W && r < 64; r++) S[r] = ts[r]->rng.word_pos;
     const int windows = t0r->c.shuffle_windows;
@@ -666,6 +670,8 @@ void or_trainers_update(or_trainer **ts, int W, or_update_metrics *ms) {
                 w->tvemax = fmaxf(w->tvemax, w->st.value_error_max);
                 w->start += sz;
             }
+            for (int r = 0; r < W; r++)
+                if (ts[r]->n_mblog < OR_MB_LOG_MAX) ts[r]->mblog[ts[r]->n_mblog++] = stg;
             tp += stg.policy_loss; tv += stg.value_loss; th += stg.entropy; tk += stg.approx_kl;
             tc += stg.clip_fraction; tl += stg.loss; tvm += stg.value_mean; trm += stg.returns_mean;
             tvem += stg.value_error_mean; tves += stg.value_error_std;
@@ -774,4 +780,10 @@ int or_trainer_episodes(const or_trainer *t, or_episode *out, int cap) {
     int n = t->n_eps < cap ? t->n_eps : cap;
     if (out) memcpy(out, t->eps, sizeof(or_episode) * n);
     return t->n_eps;
+}
+
+int or_trainer_mb_log(const or_trainer *t, or_mb_stats *out, int max) {
+    const int n = t->n_mblog < max ? t->n_mblog : max;
+    if (out) memcpy(out, t->mblog, sizeof(or_mb_stats) * (size_t)n);
+    return t->n_mblog;
 }

@@ -225,6 +225,7 @@ def lib():
             "or_trainer_update": (None, [C.c_void_p, C.POINTER(UpdateMetrics)]),
             "or_trainers_update": (None, [C.c_void_p, C.c_int, C.c_void_p]),
             "or_trainer_set_buffer": (C.c_int, [C.c_void_p, C.c_char_p, C.c_void_p, C.c_size_t]),
+            "or_trainer_mb_log": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
             "or_trainer_buffer": (C.c_size_t, [C.c_void_p, C.c_char_p, C.c_void_p, C.c_size_t]),
             "or_trainer_obs_norm_state": (None, [C.c_void_p, f64, f64, C.POINTER(C.c_double)]),
             "or_trainer_ret_norm_state": (None, [C.c_void_p, f64, C.c_void_p]),
@@ -453,6 +454,13 @@ class Trainer:
         out = np.zeros(n // 4, dtype)
         lib().or_trainer_buffer(self.h, name.encode(), out.ctypes.data, n)
         return out
+
+    def minibatch_log(self):
+        """the last update's per-minibatch statistics in run order: list of dicts"""
+        n = lib().or_trainer_mb_log(self.h, None, 0)
+        arr = (MbStats * max(n, 1))()
+        lib().or_trainer_mb_log(self.h, arr, n)
+        return [{f: getattr(arr[i], f) for f, _ in MbStats._fields_} for i in range(n)]
 
     def set_buffer(self, name, arr):
         a = np.ascontiguousarray(arr)
