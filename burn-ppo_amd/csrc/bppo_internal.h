@@ -103,6 +103,8 @@ struct WordBuf {                                  // ChaCha12 words made on the 
     int nreg = 0;
     std::vector<hipEvent_t> ev;                   // per SHUF_CHUNK chunk of h
     std::unique_ptr<std::atomic<int>[]> ok;
+    uint32_t *hd = nullptr;                       // windowed: h registered with the GPU, its device address
+    bool gpu = false;                             // windowed: chunks of h are written by the GPU (ev[c] completes)
 };
 
 // target-range table of the ranged Fisher-Yates bucketing (k_shuffle.hip)
@@ -131,6 +133,8 @@ struct ShuffleEngine {
     uint64_t gap = 0;                             // words between an update's last shuffle and the next update's first
     uint64_t win = 0;                             // shuffle_windows: epoch e starts at job start + e * win (0: chained)
     bool pair = false;                            // windowed: worker 2m walks epochs 2m and 2m+1 interleaved
+    bool win_producers = false;                   // windowed: host word producers (default: the walks make their words)
+    bool win_gpu_words = false;                   // windowed: the GPU writes the job's words into host memory too
     double Ew = 0.0, sigma = 0.0;                 // expected words per shuffle, its std dev
     int K = 0;                                    // speculative walks per epoch boundary
     int host_cpus = 16;                           // CPU budget of this rank (BPPO_HOST_THREADS)

@@ -57,6 +57,24 @@ static bool shuf_debug() {
     } while (0)
 
 // ChaCha12 words [base, base + len) (base a multiple of 16): one block per thread
+// the same words into device memory and, over PCIe, into the registered host buffer the
+// walks read (shuffle_windows: the host then makes no words itself)
+__global__ void k_chacha_words2(Key8 key, uint64_t stream, uint64_t base, uint64_t len, uint32_t *out,
+                                uint32_t *host) {
+    const uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (b * 16 >= len) return;
+    uint32_t blk[16];
+    chacha12_block(key, (base >> 4) + b, stream, blk);
+    uint4 *o = reinterpret_cast<uint4 *>(out + b * 16);
+    uint4 *hh = reinterpret_cast<uint4 *>(host + b * 16);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint4 v = make_uint4(blk[4 * i], blk[4 * i + 1], blk[4 * i + 2], blk[4 * i + 3]);
+        o[i] = v;
+        hh[i] = v;
+    }
+}
+
 __global__ void k_chacha_words(Key8 key, uint64_t stream, uint64_t base, uint64_t len, uint32_t *out) {
     const uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (b * 16 >= len) return;
@@ -254,6 +272,9 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
     // and the epochs' walks go in pairs, two chains interleaved per thread (half the
     // walking CPU of one chain per thread: the walker is latency-bound)
     pair = win && !(getenv("BPPO_SHUFFLE_PAIR") && atoi(getenv("BPPO_SHUFFLE_PAIR")) == 0);
+    win_producers = win && getenv("BPPO_SHUFFLE_WIN_PRODUCERS") && atoi(getenv("BPPO_SHUFFLE_WIN_PRODUCERS")) == 1;
+    win_gpu_words = win && !win_producers &&
+                    !(getenv("BPPO_SHUFFLE_GPU_WORDS") && atoi(getenv("BPPO_SHUFFLE_GPU_WORDS")) == 0);
     // exact continuations need the last epoch in the in-job groups
     const bool cont_on = !win && epochs - 1 >= C;
     K = std::min(K, SHUF_MAX_SPEC / (std::max(epochs - C, 0) + 2 * C + (cont_on ? 2 : 0)));
@@ -305,12 +326,24 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
             err = "shuffle word buffers: allocation failed";
             return BPPO_ERR_HIP;
         }
+        if (win_gpu_words) {
+            // the walks' word buffer, registered so the GPU can write it (the words are
+            // made on the GPU anyway for the J expansion); only queried, never waited on
+            const size_t huge = (size_t)2 << 20, sz = ((size_t)w.cap * 4 + huge - 1) / huge * huge;
+            if (hipHostRegister(w.h, sz, hipHostRegisterMapped) != hipSuccess ||
+                hipHostGetDevicePointer((void **)&w.hd, w.h, 0) != hipSuccess) {
+                (void)hipGetLastError();
+                w.hd = nullptr;          // the walks make their own words
+            }
+            w.gpu = w.hd != nullptr;
+        }
         const size_t nch = w.cap / SHUF_CHUNK;
         w.ev.assign(nch, nullptr);
         w.ok.reset(new std::atomic<int>[nch]);
         for (size_t c = 0; c < nch; c++) {
             w.ok[c] = 0;
-            if (hipEventCreateWithFlags(&w.ev[c], hipEventDisableTiming | hipEventBlockingSync) != hipSuccess) {
+            if (hipEventCreateWithFlags(&w.ev[c], w.gpu ? hipEventDisableTiming
+                                                         : hipEventDisableTiming | hipEventBlockingSync) != hipSuccess) {
                 err = "shuffle chunk events: creation failed";
                 return BPPO_ERR_HIP;
             }
@@ -319,7 +352,7 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
     const uint64_t nck = (uint64_t)((Ew + 24.0 * sigma) / SHUF_CK) + 4;
     for (int i = 0; i < nspec; i++) spec[i].ck.assign(nck, 0xFFFFFFFFu);
     for (int i = 0; i < nspec; i++) workers.emplace_back([this, i]() { worker(i); });
-    const int ngen = std::max(1, std::min(4, host_cpus / 4));
+    const int ngen = win && !win_producers ? 0 : std::max(1, std::min(4, host_cpus / 4));
     for (int i = 0; i < ngen; i++) gens.emplace_back([this]() { generator(); });
     th = std::thread([this]() { run(); });
     return BPPO_OK;
@@ -385,6 +418,10 @@ const uint32_t *ShuffleEngine::words(int b, uint64_t pos, uint64_t len, std::vec
             // a chunk the producers have not reached yet: the walk makes this piece
             // itself (ChaCha12, ~0.3 ns/word) rather than waiting for them
             if (w.ok[c].load(std::memory_order_acquire)) return w.h + o;
+            if (w.gpu && hipEventQuery(w.ev[c]) == hipSuccess) {   // written by the GPU
+                w.ok[c].store(1, std::memory_order_release);
+                return w.h + o;
+            }
             break;
         }
     }
@@ -1010,8 +1047,9 @@ bool ShuffleEngine::run_windowed(int slot, uint64_t start) {
         R.base = (start + (uint64_t)e * win) / SHUF_CK * SHUF_CK;
         R.off = (uint64_t)e * rlen;
         R.len = rlen;
-        hipLaunchKernelGGL(k_chacha_words, dim3((unsigned)((R.len / 16 + 255) / 256)), dim3(256), 0, copy, key,
-                           stream, R.base, R.len, W.d + R.off);
+        if (!W.gpu)
+            hipLaunchKernelGGL(k_chacha_words, dim3((unsigned)((R.len / 16 + 255) / 256)), dim3(256), 0, copy, key,
+                               stream, R.base, R.len, W.d + R.off);
         for (uint64_t o = 0; o < R.len; o += SHUF_CHUNK) {
             const size_t c = (size_t)((R.off + o) / SHUF_CHUNK);
             W.ok[c] = 0;
@@ -1019,14 +1057,31 @@ bool ShuffleEngine::run_windowed(int slot, uint64_t start) {
         }
     }
     std::sort(order.begin(), order.end());
+    if (W.gpu) {
+        // chunk by chunk in the order the walks reach them, each into HBM (J expansion)
+        // and into the walks' host buffer; a walk reads a chunk once its event completes
+        // and makes the piece itself before that
+        for (auto &oc : order) {
+            const size_t c = oc.second;
+            const WordBuf::Region &R = W.reg[c * SHUF_CHUNK / rlen];
+            const uint64_t o = c * SHUF_CHUNK, len = std::min<uint64_t>(SHUF_CHUNK, R.off + R.len - o);
+            hipLaunchKernelGGL(k_chacha_words2, dim3((unsigned)((len / 16 + 255) / 256)), dim3(256), 0, copy, key,
+                               stream, R.base + (o - R.off), len, W.d + o, W.hd + o);
+            (void)hipEventRecord(W.ev[c], copy);
+        }
+    }
     {
         std::unique_lock<std::mutex> lk(mu);
         cv.wait(lk, [&] { return gen_active == 0 || quit; });
         gen_order.clear();
-        for (auto &oc : order) {
-            const WordBuf::Region &R = W.reg[oc.second * SHUF_CHUNK / rlen];
-            gen_order.push_back({R.base + (oc.second * SHUF_CHUNK - R.off), oc.second});
-        }
+        // every word of a windowed job is on a true chain and read by exactly one walk:
+        // the walks make their own pieces (no producer threads making the same words
+        // twice when the walks outrun them; BPPO_SHUFFLE_WIN_PRODUCERS=1 restores them)
+        if (win_producers)
+            for (auto &oc : order) {
+                const WordBuf::Region &R = W.reg[oc.second * SHUF_CHUNK / rlen];
+                gen_order.push_back({R.base + (oc.second * SHUF_CHUNK - R.off), oc.second});
+            }
         gen_buf = &W;
         gen_next.store(0, std::memory_order_relaxed);
         gen_job++;
@@ -1114,6 +1169,8 @@ void ShuffleEngine::shutdown() {
         for (auto &e : wb[b].ev) if (e) (void)hipEventDestroy(e);
         wb[b].ev.clear();
         if (wb[b].d) { (void)hipFree(wb[b].d); wb[b].d = nullptr; }
+        if (wb[b].h && wb[b].hd) (void)hipHostUnregister(wb[b].h);
+        wb[b].hd = nullptr;
         if (wb[b].h) { host_words_free(wb[b].h, wb[b].cap); wb[b].h = nullptr; }
     }
 }

@@ -229,7 +229,7 @@ def test_cnn_64ch_per_minibatch_drift():
             n = r[10]
             dev = {"policy_loss": r[0] / n, "value_loss": 0.5 * r[1] / n, "entropy": r[2] / n,
                    "approx_kl": r[3] / n, "clip_fraction": r[4] / n}
-            rel = {f: abs(dev[f] - o[f]) / max(abs(o[f]), floors[f], 1e-30) for f in dev}
+            rel = {f: float(abs(dev[f] - o[f]) / max(abs(o[f]), floors[f], 1e-30)) for f in dev}
             per.append({"minibatch": k, "max_rel": max(rel.values()), "worst": max(rel, key=rel.get), **rel})
         first = next((p["minibatch"] for p in per if p["max_rel"] > 1e-5), None)
         out = {"net": "2x64-channel conv, FC 128x2", "N": N, "T": T, "minibatches": len(per),
