@@ -271,10 +271,17 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
     if (win) { K = 1; C = 0; fr_depth = 0; }
     // and the epochs' walks go in pairs, two chains interleaved per thread (half the
     // walking CPU of one chain per thread: the walker is latency-bound)
-    pair = win && !(getenv("BPPO_SHUFFLE_PAIR") && atoi(getenv("BPPO_SHUFFLE_PAIR")) == 0);
+    // (only when the rank has fewer CPUs than epochs: with one CPU per epoch each walk
+    // runs alone, 0.45 instead of 0.54 ns per word of wall time; BPPO_SHUFFLE_PAIR=0/1 forces)
+    pair = win && host_cpus < epochs;
+    if (const char *e = getenv("BPPO_SHUFFLE_PAIR")) pair = win && atoi(e) != 0;
     win_producers = win && getenv("BPPO_SHUFFLE_WIN_PRODUCERS") && atoi(getenv("BPPO_SHUFFLE_WIN_PRODUCERS")) == 1;
-    win_gpu_words = win && !win_producers &&
-                    !(getenv("BPPO_SHUFFLE_GPU_WORDS") && atoi(getenv("BPPO_SHUFFLE_GPU_WORDS")) == 0);
+    // opt-in (BPPO_SHUFFLE_GPU_WORDS=1): the GPU also writes the job's words into the walks'
+    // host buffer.  Measured slower (r04k, profiles/r04/windows_ab.txt): the low-priority
+    // chunk kernels land behind the update's kernels, so the walks make most pieces anyway,
+    // and they stretch the rollout (1.2 -> 4.0 ms), which leaves no room for side kernels
+    win_gpu_words = win && !win_producers && getenv("BPPO_SHUFFLE_GPU_WORDS") &&
+                    atoi(getenv("BPPO_SHUFFLE_GPU_WORDS")) == 1;
     // exact continuations need the last epoch in the in-job groups
     const bool cont_on = !win && epochs - 1 >= C;
     K = std::min(K, SHUF_MAX_SPEC / (std::max(epochs - C, 0) + 2 * C + (cont_on ? 2 : 0)));
