@@ -277,7 +277,7 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
     if (const char *e = getenv("BPPO_SHUFFLE_PAIR")) pair = win && atoi(e) != 0;
     win_producers = win && getenv("BPPO_SHUFFLE_WIN_PRODUCERS") && atoi(getenv("BPPO_SHUFFLE_WIN_PRODUCERS")) == 1;
     // opt-in (BPPO_SHUFFLE_GPU_WORDS=1): the GPU also writes the job's words into the walks'
-    // host buffer.  Measured slower (r04k, profiles/r04/windows_ab.txt): the low-priority
+    // host buffer.  Measured slower (r04k, profiles/r04_windows/windows_ab.txt): the low-priority
     // chunk kernels land behind the update's kernels, so the walks make most pieces anyway,
     // and they stretch the rollout (1.2 -> 4.0 ms), which leaves no room for side kernels
     win_gpu_words = win && !win_producers && getenv("BPPO_SHUFFLE_GPU_WORDS") &&
