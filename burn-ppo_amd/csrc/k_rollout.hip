@@ -872,8 +872,13 @@ bppo_status launch_cartpole_rollout(bppo_ctx *c, uint64_t base_pos, const double
         const uint64_t blocks = ((base_pos + count + 15) >> 4) - (base_pos >> 4);
         hipLaunchKernelGGL(k_gumbel_words, dim3((unsigned)((blocks + 255) / 256)), dim3(256), 0, c->stream, c->rng_key,
                            (uint64_t)c->cfg.rng_stream, base_pos, count, c->d_gumbel);
-        static const bool tiles32 = getenv("BPPO_ROLLOUT_TILES32") != nullptr;   // A/B: r03's half-wave kernel
-        if (tiles32) {
+        // default: r03's half-wave kernel (2 waves/SIMD, ~180 VGPRs: the side-stream
+        // Fisher-Yates passes share its CUs).  BPPO_ROLLOUT_LANES64=1: the 64-lane kernel,
+        // faster alone (1.05 vs 1.32 ms) but one 475-register wave per SIMD leaves no room
+        // beside it, and device-bound A/B runs end 0.1-0.15 ms/update slower with it
+        // (profiles/r04_rollout/rollout_ab.txt)
+        const bool lanes64 = getenv("BPPO_ROLLOUT_LANES64") && atoi(getenv("BPPO_ROLLOUT_LANES64")) == 1;
+        if (!lanes64) {
             const int waves = (c->N + mmb::TR - 1) / mmb::TR;
             hipLaunchKernelGGL(k_cartpole_rollout_mfma, dim3((waves + mmb::WAVES - 1) / mmb::WAVES), dim3(64 * mmb::WAVES),
                                mmb::LDS, c->stream, a, (const float *)c->d_gumbel);

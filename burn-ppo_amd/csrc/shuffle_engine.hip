@@ -51,9 +51,13 @@ static bool shuf_debug() {
     if (v < 0) v = getenv("BPPO_SHUFFLE_DEBUG") ? 1 : 0;
     return v == 1;
 }
+static double shuf_t_ms() {   // debug timestamps: ms since the first call
+    static const auto t0 = std::chrono::steady_clock::now();
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
 #define SHUF_LOG(...)                                        \
     do {                                                     \
-        if (shuf_debug()) { fprintf(stderr, __VA_ARGS__); fflush(stderr); } \
+        if (shuf_debug()) { fprintf(stderr, "%9.3f ", shuf_t_ms()); fprintf(stderr, __VA_ARGS__); fflush(stderr); } \
     } while (0)
 
 // ChaCha12 words [base, base + len) (base a multiple of 16): one block per thread
@@ -398,7 +402,9 @@ int ShuffleEngine::ensure(uint64_t start) {
 
 void ShuffleEngine::wait_epoch(int slot, int e) {
     std::unique_lock<std::mutex> lk(mu);
+    const bool had = ready[slot] > e;
     cv.wait(lk, [&] { return ready[slot] > e || !slot_valid[slot]; });
+    SHUF_LOG("[shuf] consumer epoch %d %s\n", e, had ? "ready" : "waited");
 }
 
 bool ShuffleEngine::epoch_ready(int slot, int e) {

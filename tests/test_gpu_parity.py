@@ -324,3 +324,32 @@ def test_tanh_second_rollout_and_forward_rows_bit_exact():
     lg, vals = tr.model.forward(obs)
     assert np.array_equal(vals.reshape(-1).view(np.uint32), ot.buffer("values").view(np.uint32))
     tr.close(); ot.close()
+
+
+@pytest.mark.parametrize("N", [1000, 2048])
+def test_rollout_lanes64_bit_exact(monkeypatch, N):
+    """the 64-lane CfgB rollout kernel (BPPO_ROLLOUT_LANES64=1, k_cartpole_rollout_mfma64:
+    transposed layers, permlane32 swaps, W1 in registers) bit-exact against the oracle
+    over two consecutive rollouts (env state, episode and RNG carry), a partial last wave
+    at N = 1000, with obs + return normalizers"""
+    import oracle_ffi as O
+    from parity_util import cmp_cartpole_rollout, oracle_train_cfg
+    monkeypatch.setenv("BPPO_ROLLOUT_LANES64", "1")
+    cfg = bppo.make_config("cartpole", num_envs=N, num_steps=32)
+    params = bppo.orthogonal_init(cfg, seed=11)
+    tr = bppo.Trainer(cfg, params=params)
+    ot = O.Trainer(oracle_train_cfg(cfg), params)
+    try:
+        for _ in range(2):
+            bppo.collect_rollouts(tr.ctx); ot.collect()
+            cmp_cartpole_rollout(tr, ot)
+            tr.ctx.set_buffer("rewards", ot.buffer("rewards"))
+            bppo.compute_gae(tr.ctx); ot.gae()
+            bppo.ppo_update(tr.ctx, bppo.schedule_get(cfg["learning_rate"], 0), bppo.schedule_get(cfg["entropy_coef"], 0))
+            ot.update()
+            tr.model.set_params(ot.params())
+            mvc, rets = ot.ret_norm_state(returns=True)
+            tr.ctx.set_ret_norm(mvc, rets)
+            tr.ctx.set_obs_norm(*ot.obs_norm_state(5))
+    finally:
+        tr.close(); ot.close()
