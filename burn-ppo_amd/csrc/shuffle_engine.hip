@@ -259,14 +259,19 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
     // (the job-start policy ran every boundary's group at once, sqrt(e) wide, and
     // oversubscribed a 16-CPU share).  Needs the next job's first D + 1 epochs as
     // carry groups.  BPPO_SHUFFLE_FRONTIER=0: the job-start policy.
-    fr_depth = getenv("BPPO_SHUFFLE_FRONTIER") ? atoi(getenv("BPPO_SHUFFLE_FRONTIER")) : 1;
+    // Default depth 2 with >= 8 CPUs (r04: the walk binds at depth 1 — epoch e+2's walks
+    // start when e resolves, so two resolved epochs take at least one epoch's walk, ~5.2 ms;
+    // depth 2 gives the walks of e+3 that head start.  A/B on two boxes, 3 + 2 runs each:
+    // 12.41-12.57 vs 12.42-13.75 ms/update, shuffle_wait ~0 vs 0.7-5 ms,
+    // profiles/r04_windows/frontier_ab.txt); depth 1 below 8 CPUs (more CPU per update)
+    fr_depth = getenv("BPPO_SHUFFLE_FRONTIER") ? atoi(getenv("BPPO_SHUFFLE_FRONTIER")) : (host_cpus >= 8 ? 2 : 1);
     if (fr_depth > 0 && epochs >= 3 && K > 0) {
         C = std::min(fr_depth + 1, epochs - 1);
         fr_depth = C - 1;
         // one-sigma anchors: K = 5 over +-2 sigma misses ~1 in 40 boundaries and
         // meets after ~2 M words (scripts/microbench/comb_sim.cpp); fewer walks
         // leave the true walk and the met chains their CPUs
-        if (!getenv("BPPO_SHUFFLE_SPEC")) K = std::max(1, std::min(5, (5 * host_cpus + 8) / 16));
+        if (!getenv("BPPO_SHUFFLE_SPEC")) K = std::max(1, std::min(fr_depth >= 2 ? 4 : 5, (5 * host_cpus + 8) / 16));
     } else {
         fr_depth = 0;
     }
