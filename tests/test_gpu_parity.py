@@ -353,3 +353,40 @@ def test_rollout_lanes64_bit_exact(monkeypatch, N):
             tr.ctx.set_obs_norm(*ot.obs_norm_state(5))
     finally:
         tr.close(); ot.close()
+
+
+@pytest.mark.parametrize("threads", ["16", "2"])
+def test_shuffle_windows_single_rank_matches_oracle(monkeypatch, threads):
+    """shuffle_windows at W = 1 through the pipelined bppo_train_steps (the engine walks the
+    epochs at once: alone with 16 CPUs, in interleaved pairs with 2): permutations, RNG
+    positions, metrics and parameters against the oracle's windowed update, two updates"""
+    import oracle_ffi as O
+    from parity_util import oracle_train_cfg
+    monkeypatch.setenv("BPPO_HOST_THREADS", threads)
+    cfg = bppo.make_config("cartpole", num_envs=2048, num_steps=32, shuffle_windows=True)
+    params = bppo.orthogonal_init(cfg, seed=12)
+    tr = bppo.Trainer(cfg, params=params)
+    ot = O.Trainer(oracle_train_cfg(cfg), params)
+    try:
+        bppo.collect_rollouts(tr.ctx); ot.collect()
+        tr.ctx.set_buffer("rewards", ot.buffer("rewards"))
+        bppo.compute_gae(tr.ctx); ot.gae()
+        m = bppo.ppo_update(tr.ctx, bppo.schedule_get(cfg["learning_rate"], 0), bppo.schedule_get(cfg["entropy_coef"], 0))
+        om = ot.update()
+        assert tr.ctx.rng_pos() == ot.rng_pos()
+        assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"), advantages=ot.buffer("advantages"))
+        assert_params_close(tr.model.get_params(), ot.params())
+        # second update through the pipelined path, from the oracle's state
+        tr.model.set_params(ot.params())
+        mvc, rets = ot.ret_norm_state(returns=True)
+        tr.ctx.set_ret_norm(mvc, rets)
+        tr.ctx.set_obs_norm(*ot.obs_norm_state(5))
+        ms2, _ = tr.train_updates(1)
+        ot.collect(); ot.gae()
+        assert np.array_equal(tr.buffer.actions.reshape(-1), ot.buffer("actions", np.int32))
+        om2 = ot.update()
+        assert tr.ctx.rng_pos() == ot.rng_pos()
+        assert_metrics_close(ms2[0], om2, values=ot.buffer("values"), returns=ot.buffer("returns"), advantages=ot.buffer("advantages"))
+        assert_params_close(tr.model.get_params(), ot.params())
+    finally:
+        tr.close(); ot.close()
