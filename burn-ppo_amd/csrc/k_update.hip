@@ -888,6 +888,10 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
         for (int ct = 0; ct < 2; ct++)
 #pragma unroll
             for (int q = 0; q < 16; q++) h2[ct][q] = 0.0f;
+        // matrix segments at wave priority 3 (the other wave's VALU segments take the
+        // leftover issue slots): launch mean 0.487 -> 0.466-0.476 ms, update -0.17 ms
+        // (A/B, profiles/r04_windows/split_prio_ab.txt)
+        __builtin_amdgcn_s_setprio(3);
 #pragma unroll
         for (int it = 0; it < 2; it++) {
             f32x16_t a1;
@@ -908,6 +912,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
                 __builtin_amdgcn_sched_barrier(0);   // bound the piece-load hoisting (registers)
             }
         }
+        __builtin_amdgcn_s_setprio(0);
         // H2 = relu(. + b1) -> the row-major tile for the heads
 #pragma unroll
         for (int ct = 0; ct < 2; ct++)
@@ -1034,6 +1039,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
             }
             if ((q & 3) == 3) __builtin_amdgcn_sched_barrier(0);
         }
+        __builtin_amdgcn_s_setprio(3);
         // ---- layer 1 again, C/D orientation: H1[row][j1] (rows in registers)
         f32x16_t h1[2];
 #pragma unroll
@@ -1096,6 +1102,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
                 mfma6(dz1[ct], Az, load_pieces(S.W1n, (c + 32 * ct) * WPS + 16 * ks + 8 * h));
             __builtin_amdgcn_sched_barrier(0);
         }
+        __builtin_amdgcn_s_setprio(0);
         // dZ1 masked by relu'(H1); dW0 and db0 on the VALU (lane = hidden unit)
 #pragma unroll
         for (int q = 0; q < 16; q++) {
