@@ -132,6 +132,7 @@ struct ShuffleEngine {
     uint64_t stream = 0;
     uint64_t gap = 0;                             // words between an update's last shuffle and the next update's first
     uint64_t win = 0;                             // shuffle_windows: epoch e starts at job start + e * win (0: chained)
+    bool keep_guess = true;                       // keep the nearest guessed walks beside an exact continuation
     bool pair = false;                            // windowed: worker 2m walks epochs 2m and 2m+1 interleaved
     bool win_producers = false;                   // windowed: host word producers (default: the walks make their words)
     bool win_gpu_words = false;                   // windowed: the GPU writes the job's words into host memory too

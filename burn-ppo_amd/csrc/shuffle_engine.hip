@@ -282,6 +282,7 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
     // walking CPU of one chain per thread: the walker is latency-bound)
     // (only when the rank has fewer CPUs than epochs: with one CPU per epoch each walk
     // runs alone, 0.45 instead of 0.54 ns per word of wall time; BPPO_SHUFFLE_PAIR=0/1 forces)
+    keep_guess = !(getenv("BPPO_SHUFFLE_KEEP_GUESS") && atoi(getenv("BPPO_SHUFFLE_KEEP_GUESS")) == 0);
     pair = win && host_cpus < epochs;
     if (const char *e = getenv("BPPO_SHUFFLE_PAIR")) pair = win && atoi(e) != 0;
     win_producers = win && getenv("BPPO_SHUFFLE_WIN_PRODUCERS") && atoi(getenv("BPPO_SHUFFLE_WIN_PRODUCERS")) == 1;
@@ -859,6 +860,43 @@ void ShuffleEngine::run() {
             // closes at the earlier of its own walk and the chain's end.
             int fin = -1;                              // chain walk whose end closes the epoch
             uint64_t endp = 0, chain_front = 0;
+            // candidates on our chain at checkpoint q (range rq); keep (or switch to) the
+            // one furthest ahead — an exact continuation meets at once but started late,
+            // a guessed walk of the same chain may have a long head start
+            auto frontier = [&](int i) -> uint64_t {
+                for (int mt; (mt = spec[i].merged_to.load(std::memory_order_acquire)) >= 0;) i = mt;
+                const int64_t pr = spec[i].progress.load(std::memory_order_acquire);
+                return pr < 0 ? 0 : spec[i].ck_base + (uint64_t)pr * SHUF_CK;
+            };
+            auto try_switch = [&](uint64_t q, uint32_t rq) -> bool {
+                int best = met;
+                uint64_t bf = met >= 0 ? frontier(met) : 0;
+                for (int g = 0; g < 2; g++)
+                    for (int i = g ? s0 : c0; i < (g ? s1 : c1); i++) {
+                        uint32_t rs = 0;
+                        if (i == met || peek(i, q, &rs) != 1 || rs != rq) continue;
+                        const uint64_t f = frontier(i);
+                        if (best < 0 || f > bf) { best = i; bf = f; }
+                    }
+                if (best == met) return false;
+                met = best;
+                // from here on the epoch's chain lives only in the met walk and the walks
+                // it has merged into (merges go leftwards): every other walk of this
+                // boundary is stopped and frees its CPU — except, while the met walk is an
+                // exact continuation, the guessed walks (g = 1): one of them may carry the
+                // same chain further once they coalesce, and the leapfrog below keeps
+                // checking them.  (Should the chain's head later merge into a neighbour
+                // stopped here, that neighbour's recorded states stay valid and the true
+                // walk walks on from its end -- slower, never wrong.)
+                const bool on_cont = met >= c0 && met < c1;
+                bool keep[SHUF_MAX_SPEC] = {};
+                for (int i = met; i >= 0; i = spec[i].merged_to.load(std::memory_order_acquire)) keep[i] = true;
+                for (int g = 0; g < 2; g++)
+                    for (int i = g ? s0 : c0; i < (g ? s1 : c1); i++)
+                        if (!keep[i] && !(on_cont && g == 1 && keep_guess))
+                            spec[i].stop.store(true, std::memory_order_relaxed);
+                return true;
+            };
             while (r >= 2) {
                 if (met >= 0) {
                     if (cancel.load(std::memory_order_relaxed) || quit) { cancelled = true; break; }
@@ -867,10 +905,14 @@ void ShuffleEngine::run() {
                     const bool chain_done = spec[f].done.load(std::memory_order_acquire) != 0 &&
                                             spec[f].merged_to.load(std::memory_order_acquire) < 0;
                     uint32_t rr = 0;
+                    const bool recheck = keep_guess && s1 > s0 && met >= c0 && met < c1;
                     for (uint64_t q = (pos / SHUF_CK + 1) * SHUF_CK; r >= 2 && peek(met, q, &rr) == 1; q += SHUF_CK) {
                         tck.push_back({q, rr});
                         pos = q;
                         r = rr;
+                        // following an exact continuation: a guessed walk of this boundary
+                        // that has coalesced with the chain is further ahead -- jump to it
+                        if (recheck && try_switch(q, rr)) break;
                     }
                     if (r < 2) break;
                     if (chain_done && spec[f].end > pos && spec[f].end - pos <= SHUF_CK) {
@@ -894,37 +936,7 @@ void ShuffleEngine::run() {
                 tck.push_back({q, r});
                 if (s0 == s1 && c0 == c1) continue;
                 if (met < 0) walked++;
-                // candidates on our chain at q; keep (or switch to) the one furthest
-                // ahead — an exact continuation meets at once but started late, a
-                // guessed walk of the same chain may have a long head start
-                auto frontier = [&](int i) -> uint64_t {
-                    for (int mt; (mt = spec[i].merged_to.load(std::memory_order_acquire)) >= 0;) i = mt;
-                    const int64_t pr = spec[i].progress.load(std::memory_order_acquire);
-                    return pr < 0 ? 0 : spec[i].ck_base + (uint64_t)pr * SHUF_CK;
-                };
-                int best = met;
-                uint64_t bf = met >= 0 ? frontier(met) : 0;
-                for (int g = 0; g < 2; g++)
-                    for (int i = g ? s0 : c0; i < (g ? s1 : c1); i++) {
-                        uint32_t rs = 0;
-                        if (i == met || peek(i, q, &rs) != 1 || rs != r) continue;
-                        const uint64_t f = frontier(i);
-                        if (best < 0 || f > bf) { best = i; bf = f; }
-                    }
-                if (best != met) {
-                    met = best;
-                    // from here on the epoch's chain lives only in the met walk and the
-                    // walks it has merged into (merges go leftwards): every other walk of
-                    // this boundary, in both candidate groups, is stopped and frees its
-                    // CPU.  (Should the chain's head later merge into a neighbour stopped
-                    // here, that neighbour's recorded states stay valid and the true walk
-                    // walks on from its end -- slower, never wrong.)
-                    bool keep[SHUF_MAX_SPEC] = {};
-                    for (int i = met; i >= 0; i = spec[i].merged_to.load(std::memory_order_acquire)) keep[i] = true;
-                    for (int g = 0; g < 2; g++)
-                        for (int i = g ? s0 : c0; i < (g ? s1 : c1); i++)
-                            if (!keep[i]) spec[i].stop.store(true, std::memory_order_relaxed);
-                }
+                try_switch(q, r);
             }
             flush(tst, true_words);
             if (cancelled) break;
@@ -967,11 +979,16 @@ void ShuffleEngine::run() {
                     if (e + 1 < C) { if (carry_valid[cs]) prune(cp0 + (e + 1) * K, cp0 + (e + 2) * K, pos); }
                     else prune(cur0 + (e + 1 - C) * K, cur0 + (e + 2 - C) * K, pos);
                 } else {
-                    // the next job's first epoch: an exact continuation makes the
-                    // guessed walks redundant
+                    // the next job's first epoch.  An exact continuation is the true
+                    // chain, but it started only when a walk of this epoch finished; the
+                    // guessed walks started when the boundary fr_depth epochs earlier
+                    // resolved, so the two nearest x may be far ahead on the same chain
+                    // once they coalesce with it: keep them beside the continuation (the
+                    // true walk follows whichever is ahead).  keep_guess = 0: r02's rule
+                    // (an exact continuation stops every guessed walk).
                     const uint64_t x = pos + gap;
                     const int ex = cont0 ? prune(ccn0, ccn0 + K, x) : -1;
-                    if (ex >= 0) for (int i = cn0; i < cn0 + K; i++) spec[i].stop.store(true, std::memory_order_relaxed);
+                    if (ex >= 0 && !keep_guess) for (int i = cn0; i < cn0 + K; i++) spec[i].stop.store(true, std::memory_order_relaxed);
                     else prune(cn0, cn0 + K, x);
                 }
             }
