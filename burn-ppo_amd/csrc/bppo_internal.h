@@ -103,8 +103,9 @@ struct WordBuf {                                  // ChaCha12 words made on the 
     int nreg = 0;
     std::vector<hipEvent_t> ev;                   // per SHUF_CHUNK chunk of h
     std::unique_ptr<std::atomic<int>[]> ok;
-    uint32_t *hd = nullptr;                       // windowed: h registered with the GPU, its device address
-    bool gpu = false;                             // windowed: chunks of h are written by the GPU (ev[c] completes)
+    uint32_t *hd = nullptr;                       // windowed GPU words: h is registered (pinned)
+    bool gpu = false;                             // windowed: chunks of h are copied from d (ev[c] completes)
+    uint64_t made_for = ~0ull;                    // job start whose words d (and h's copies) hold
 };
 
 // target-range table of the ranged Fisher-Yates bucketing (k_shuffle.hip)
@@ -135,7 +136,9 @@ struct ShuffleEngine {
     bool keep_guess = true;                       // keep the nearest guessed walks beside an exact continuation
     bool pair = false;                            // windowed: worker 2m walks epochs 2m and 2m+1 interleaved
     bool win_producers = false;                   // windowed: host word producers (default: the walks make their words)
-    bool win_gpu_words = false;                   // windowed: the GPU writes the job's words into host memory too
+    bool win_gpu_words = false;                   // windowed: the job's GPU words are copied to the host (SDMA)
+    hipStream_t d2h = nullptr;                    // those copies
+    hipEvent_t words_made = nullptr;
     double Ew = 0.0, sigma = 0.0;                 // expected words per shuffle, its std dev
     int K = 0;                                    // speculative walks per epoch boundary
     int host_cpus = 16;                           // CPU budget of this rank (BPPO_HOST_THREADS)

@@ -61,24 +61,6 @@ static double shuf_t_ms() {   // debug timestamps: ms since the first call
     } while (0)
 
 // ChaCha12 words [base, base + len) (base a multiple of 16): one block per thread
-// the same words into device memory and, over PCIe, into the registered host buffer the
-// walks read (shuffle_windows: the host then makes no words itself)
-__global__ void k_chacha_words2(Key8 key, uint64_t stream, uint64_t base, uint64_t len, uint32_t *out,
-                                uint32_t *host) {
-    const uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (b * 16 >= len) return;
-    uint32_t blk[16];
-    chacha12_block(key, (base >> 4) + b, stream, blk);
-    uint4 *o = reinterpret_cast<uint4 *>(out + b * 16);
-    uint4 *hh = reinterpret_cast<uint4 *>(host + b * 16);
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const uint4 v = make_uint4(blk[4 * i], blk[4 * i + 1], blk[4 * i + 2], blk[4 * i + 3]);
-        o[i] = v;
-        hh[i] = v;
-    }
-}
-
 __global__ void k_chacha_words(Key8 key, uint64_t stream, uint64_t base, uint64_t len, uint32_t *out) {
     const uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (b * 16 >= len) return;
@@ -286,10 +268,15 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
     pair = win && host_cpus < epochs;
     if (const char *e = getenv("BPPO_SHUFFLE_PAIR")) pair = win && atoi(e) != 0;
     win_producers = win && getenv("BPPO_SHUFFLE_WIN_PRODUCERS") && atoi(getenv("BPPO_SHUFFLE_WIN_PRODUCERS")) == 1;
-    // opt-in (BPPO_SHUFFLE_GPU_WORDS=1): the GPU also writes the job's words into the walks'
-    // host buffer.  Measured slower (r04k, profiles/r04_windows/windows_ab.txt): the low-priority
-    // chunk kernels land behind the update's kernels, so the walks make most pieces anyway,
-    // and they stretch the rollout (1.2 -> 4.0 ms), which leaves no room for side kernels
+    // opt-in (BPPO_SHUFFLE_GPU_WORDS=1): the job's words, made on the GPU for the J
+    // expansion a whole job ahead, are copied (hipMemcpyAsync D2H) to the walks' pinned
+    // host buffer, so the walks make no words themselves: 2-CPU walk 14.0 -> 8.3 ms and
+    // 40.8 -> 35.6 ms of CPU per update, but on this image HIP runs those copies as blit
+    // kernels (__amd_rocclr_copyBuffer, 462 launches in the r04ai trace) that take CUs
+    // from the update: 13.8 -> 16.1 ms/update (profiles/r04_windows/windows_ab.txt).  An
+    // SDMA path (hsa_amd_memory_async_copy, r03n: 10-50 GB/s by box) is the way to keep
+    // the CPU saving without the CU cost.  (r04k's first form, kernels writing host memory
+    // over PCIe, stretched the rollout 1.2 -> 4.0 ms.)
     win_gpu_words = win && !win_producers && getenv("BPPO_SHUFFLE_GPU_WORDS") &&
                     atoi(getenv("BPPO_SHUFFLE_GPU_WORDS")) == 1;
     // exact continuations need the last epoch in the in-job groups
@@ -322,6 +309,12 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
             err = "shuffle events: creation failed";
             return BPPO_ERR_HIP;
         }
+    if (win && getenv("BPPO_SHUFFLE_GPU_WORDS") && atoi(getenv("BPPO_SHUFFLE_GPU_WORDS")) == 1 &&
+        (hipStreamCreateWithFlags(&d2h, hipStreamNonBlocking) != hipSuccess ||
+         hipEventCreateWithFlags(&words_made, hipEventDisableTiming) != hipSuccess)) {
+        err = "shuffle word copies: stream creation failed";
+        return BPPO_ERR_HIP;
+    }
     if (make_side_stream(dev, &copy) != hipSuccess) {   // lowest priority
         err = "shuffle copy stream: creation failed";
         return BPPO_ERR_HIP;
@@ -344,15 +337,16 @@ bppo_status ShuffleEngine::init(int device, const Key8 &k, uint64_t strm, uint32
             return BPPO_ERR_HIP;
         }
         if (win_gpu_words) {
-            // the walks' word buffer, registered so the GPU can write it (the words are
-            // made on the GPU anyway for the J expansion); only queried, never waited on
+            // the walks' word buffer, pinned so the SDMA engines can copy the GPU's words
+            // into it (made on the GPU anyway for the J expansion); only queried
             const size_t huge = (size_t)2 << 20, sz = ((size_t)w.cap * 4 + huge - 1) / huge * huge;
-            if (hipHostRegister(w.h, sz, hipHostRegisterMapped) != hipSuccess ||
-                hipHostGetDevicePointer((void **)&w.hd, w.h, 0) != hipSuccess) {
+            if (hipHostRegister(w.h, sz, hipHostRegisterDefault) != hipSuccess) {
                 (void)hipGetLastError();
-                w.hd = nullptr;          // the walks make their own words
+                w.gpu = false;           // the walks make their own words
+            } else {
+                w.hd = w.h;              // registered (unregister at shutdown)
+                w.gpu = true;
             }
-            w.gpu = w.hd != nullptr;
         }
         const size_t nch = w.cap / SHUF_CHUNK;
         w.ev.assign(nch, nullptr);
@@ -1075,36 +1069,50 @@ bool ShuffleEngine::run_windowed(int slot, uint64_t start) {
     WordBuf &W = wb[b];
     auto chunks = [](double w) { return ((uint64_t)std::max(w, 1.0) + SHUF_CHUNK - 1) / SHUF_CHUNK * SHUF_CHUNK; };
     const uint64_t rlen = std::min(W.cap / (uint64_t)epochs, chunks(Ew + 10.0 * sigma + 4.0 * SHUF_CK));
-    W.nreg = epochs;
-    std::vector<std::pair<double, size_t>> order;
-    for (int e = 0; e < epochs; e++) {
-        WordBuf::Region &R = W.reg[e];
-        R.base = (start + (uint64_t)e * win) / SHUF_CK * SHUF_CK;
-        R.off = (uint64_t)e * rlen;
-        R.len = rlen;
-        if (!W.gpu)
-            hipLaunchKernelGGL(k_chacha_words, dim3((unsigned)((R.len / 16 + 255) / 256)), dim3(256), 0, copy, key,
-                               stream, R.base, R.len, W.d + R.off);
-        for (uint64_t o = 0; o < R.len; o += SHUF_CHUNK) {
-            const size_t c = (size_t)((R.off + o) / SHUF_CHUNK);
-            W.ok[c] = 0;
-            order.push_back({(double)o + 0.25 * e, c});     // every epoch's words in walk order, interleaved
+    // one job's regions (epoch e at s0 + e * win) and its chunks in the order the walks
+    // reach them (every epoch's words interleaved)
+    auto regions = [&](WordBuf &B, uint64_t s0, std::vector<size_t> &order) {
+        std::vector<std::pair<double, size_t>> ord;
+        B.nreg = epochs;
+        for (int e = 0; e < epochs; e++) {
+            WordBuf::Region &R = B.reg[e];
+            R.base = (s0 + (uint64_t)e * win) / SHUF_CK * SHUF_CK;
+            R.off = (uint64_t)e * rlen;
+            R.len = rlen;
+            for (uint64_t o = 0; o < R.len; o += SHUF_CHUNK) {
+                const size_t c = (size_t)((R.off + o) / SHUF_CHUNK);
+                B.ok[c] = 0;
+                ord.push_back({(double)o + 0.25 * e, c});
+            }
         }
-    }
-    std::sort(order.begin(), order.end());
-    if (W.gpu) {
-        // chunk by chunk in the order the walks reach them, each into HBM (J expansion)
-        // and into the walks' host buffer; a walk reads a chunk once its event completes
-        // and makes the piece itself before that
-        for (auto &oc : order) {
-            const size_t c = oc.second;
-            const WordBuf::Region &R = W.reg[c * SHUF_CHUNK / rlen];
-            const uint64_t o = c * SHUF_CHUNK, len = std::min<uint64_t>(SHUF_CHUNK, R.off + R.len - o);
-            hipLaunchKernelGGL(k_chacha_words2, dim3((unsigned)((len / 16 + 255) / 256)), dim3(256), 0, copy, key,
-                               stream, R.base + (o - R.off), len, W.d + o, W.hd + o);
-            (void)hipEventRecord(W.ev[c], copy);
+        std::sort(ord.begin(), ord.end());
+        order.clear();
+        for (auto &oc : ord) order.push_back(oc.second);
+    };
+    // the job's words on the GPU (the J expansion reads them) and, with GPU-made host
+    // words, copied to the walks' pinned host buffer chunk by chunk on the SDMA engines
+    auto make_words = [&](WordBuf &B, uint64_t s0, std::vector<size_t> &order) {
+        regions(B, s0, order);
+        for (int e = 0; e < epochs; e++)
+            hipLaunchKernelGGL(k_chacha_words, dim3((unsigned)((B.reg[e].len / 16 + 255) / 256)), dim3(256), 0, copy,
+                               key, stream, B.reg[e].base, B.reg[e].len, B.d + B.reg[e].off);
+        if (B.gpu) {
+            (void)hipEventRecord(words_made, copy);
+            (void)hipStreamWaitEvent(d2h, words_made, 0);
+            for (size_t c : order) {
+                const uint64_t o = c * SHUF_CHUNK;
+                (void)hipMemcpyAsync(B.h + o, B.d + o, SHUF_CHUNK * 4, hipMemcpyDeviceToHost, d2h);
+                (void)hipEventRecord(B.ev[c], d2h);
+            }
         }
-    }
+        B.made_for = s0;
+    };
+    std::vector<size_t> order, next_order;
+    if (!(W.gpu && W.made_for == start)) make_words(W, start, order);   // not made a job ahead (first job, moved start)
+    else regions(W, start, order);                                      // (made a job ago: same regions)
+    // the next job's words now, a whole job ahead of its walks (its start is known:
+    // this job's fixed span plus the next rollout's words)
+    if (W.gpu) make_words(wb[b ^ 1], start + (uint64_t)epochs * win + gap, next_order);
     {
         std::unique_lock<std::mutex> lk(mu);
         cv.wait(lk, [&] { return gen_active == 0 || quit; });
@@ -1113,9 +1121,9 @@ bool ShuffleEngine::run_windowed(int slot, uint64_t start) {
         // the walks make their own pieces (no producer threads making the same words
         // twice when the walks outrun them; BPPO_SHUFFLE_WIN_PRODUCERS=1 restores them)
         if (win_producers)
-            for (auto &oc : order) {
-                const WordBuf::Region &R = W.reg[oc.second * SHUF_CHUNK / rlen];
-                gen_order.push_back({R.base + (oc.second * SHUF_CHUNK - R.off), oc.second});
+            for (size_t c : order) {
+                const WordBuf::Region &R = W.reg[c * SHUF_CHUNK / rlen];
+                gen_order.push_back({R.base + (c * SHUF_CHUNK - R.off), c});
             }
         gen_buf = &W;
         gen_next.store(0, std::memory_order_relaxed);
@@ -1193,6 +1201,8 @@ void ShuffleEngine::shutdown() {
         gens.clear();
     }
     if (copy) { (void)hipStreamSynchronize(copy); (void)hipStreamDestroy(copy); copy = nullptr; }
+    if (d2h) { (void)hipStreamSynchronize(d2h); (void)hipStreamDestroy(d2h); d2h = nullptr; }
+    if (words_made) { (void)hipEventDestroy(words_made); words_made = nullptr; }
     for (int s = 0; s < 2; s++) {
         if (consumed[s]) { (void)hipEventDestroy(consumed[s]); consumed[s] = nullptr; }
         for (int e = 0; e < epochs; e++) if (ev[s][e]) { (void)hipEventDestroy(ev[s][e]); ev[s][e] = nullptr; }

@@ -157,17 +157,19 @@ def _window(n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("gpu_words", ["0", "1"])
 @pytest.mark.parametrize("threads", ["16", "2"])
 @pytest.mark.parametrize("seed,start,n,epochs,gap,jobs", [
     (5, 77, 1 << 23, 4, 16_777_216, 3),
     (9, 3, 100_003, 6, 700_000, 3),
 ])
-def test_shuffle_engine_windows_equal_sequential(monkeypatch, threads, seed, start, n, epochs, gap, jobs):
+def test_shuffle_engine_windows_equal_sequential(monkeypatch, gpu_words, threads, seed, start, n, epochs, gap, jobs):
     """shuffle_windows: epoch e of an update starts at S + e * (2 n + 2^20), the next
     update gap words after S + epochs * (2 n + 2^20).  The engine walks the epochs at
     once, exactly (no speculation), with 16 or 2 host CPUs; J and the end positions must
     equal the single-thread walks from those starts."""
     monkeypatch.setenv("BPPO_HOST_THREADS", threads)
+    monkeypatch.setenv("BPPO_SHUFFLE_GPU_WORDS", gpu_words)     # 1: the walks read the GPU's words (SDMA copies)
     J = np.zeros(n * epochs * jobs, np.uint32)
     ends = np.zeros(epochs * jobs, np.uint64)
     assert L.lib().bppo_debug_shuffle_engine(seed, 0, start, n, epochs, gap, jobs, 1, J.ctypes.data,
