@@ -475,8 +475,10 @@ def main():
                       "parallelism": f"dp{world}",
                       "collective": ("RCCL all-reduce (torch.distributed nccl) of the gradient, 1 per minibatch, "
                                      "stream-ordered" if world > 1 else None),
-                      "w_gt_1_semantics": ("per-rank obs/return normalizers and per-rank minibatch advantage "
-                                           "stats (SURVEY 8e); parity is defined at N=1" if world > 1 else None),
+                      "w_gt_1_semantics": ("rank r: envs seed+r*N+i, ChaCha stream r, per-rank obs/return "
+                                           "normalizers and minibatch advantage stats, gradients summed then /W "
+                                           "(oracle-pinned: tests/test_gpu_multirank.py); shuffle_windows "
+                                           "epoch placement (config.shuffle)" if world > 1 else None),
                       "shuffle": ("shuffle_windows: epoch e shuffles from S + e*(2B + 2^20), all epochs "
                                   "walked at once" if windows else "sequential (the reference's word positions)"),
                       "host_cpus_per_rank": int(os.environ["BPPO_HOST_THREADS"]),
