@@ -408,7 +408,7 @@ __global__ void __launch_bounds__(512, 2) k_cartpole_rollout_mfma(RolloutArgs a,
 // holds 64 envs as two 32-env MFMA tiles (lane l = env l; tile A = lanes 0-31,
 // tile B = lanes 32-63 of the wave's 64 envs) and runs both layers TRANSPOSED
 // (H^T = W^T X^T on v_mfma_f32_32x32x2_f32, units on the MFMA rows, envs on
-// its columns), with no LDS round trip:
+// its columns), with no LDS round trip for H1:
 //  * layer 1's K pairs (x0,x1) (x2,x3) (x4,1) come from the env lanes through one
 //    v_permlane32_swap per pair; b0 rides in the K pad (fma(1, b0, acc) is the
 //    reference's separate + b0, rounded once);
@@ -416,13 +416,17 @@ __global__ void __launch_bounds__(512, 2) k_cartpole_rollout_mfma(RolloutArgs a,
 //    register m of lane half h holds unit 2m + h: register m is then directly the
 //    B operand of layer 2's K step m (k = 2m on half 0, 2m + 1 on half 1), in
 //    natural k order (same fma chain as the reference's matmul);
-//  * layer 2's output rows are permuted so register m holds unit 32h + m; one
-//    v_permlane32_swap per register pair (tile A, tile B) leaves lane l with all
-//    64 units of env l (register m: unit m, its partner: unit 32 + m) for the
-//    heads' k-ordered chains (+ b1, relu, three fma chains per lane);
-//  * W0 (+b0) and W1 live in VGPRs for the whole rollout (70 per lane), the
-//    heads' {wp0, wp1, wv, b1} rows are LDS broadcasts, expf/logf tables in LDS.
-// One wave per SIMD (CfgB: 65,536 envs = 1,024 waves): ~300 VGPRs incl. AGPRs.
+//  * layer 2's output rows are permuted so register m holds unit 32h + m; the
+//    registers go to the wave's [env][unit] tile and lane l reads env l's row for the
+//    heads' k-ordered chains (+ b1, relu, three fma chains per lane).  (Swapping them
+//    with v_permlane32_swap instead kept 64 more registers live: 475 per wave, no room
+//    for other kernels' waves; r04 first form, profiles/r04_rollout/rollout_ab.txt);
+//  * W0 (+b0) lives in VGPRs for the whole rollout, W1's operands in LDS (one
+//    conflict-free ds_read_b64 per K step for both tiles); H2 goes through a per-wave
+//    [env][unit] LDS tile (stride 65) to the heads, whose {wp0, wp1, wv, b1} rows are LDS
+//    broadcasts; expf/logf tables in LDS.
+// One wave per SIMD (CfgB: 65,536 envs = 1,024 waves) in 269 registers and 84 KB of LDS
+// per block, which leaves room on every CU for the side-stream shuffle kernels' waves.
 namespace mmr {
 constexpr int H = 64, WAVES = 4;
 struct Params {
@@ -458,10 +462,12 @@ __device__ __forceinline__ float log_prob2(const Params &S, const float (&x)[2],
 }
 }  // namespace mmr
 
-__global__ void __launch_bounds__(256, 1) k_cartpole_rollout_mfma64(RolloutArgs a, const float *__restrict__ gum) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) k_cartpole_rollout_mfma64(RolloutArgs a, const float *__restrict__ gum) {
     using namespace mmr;
     constexpr CpOffsets O = cp_offsets<64, 2>();
     __shared__ Params S;
+    __shared__ float2 w1r[32][64];                // layer 2's A operands [K step][lane] = {ct 0, ct 1}
+    __shared__ float T2[WAVES][64 * 65];          // H2 [env][unit], row stride 65 (conflict-free both ways)
     const float *__restrict__ P = a.params;
     for (int i = threadIdx.x; i < H; i += blockDim.x)
         S.hw[i] = make_float4(P[O.wp + 2 * i], P[O.wp + 2 * i + 1], P[O.wv + i], P[O.b1 + i]);
@@ -478,8 +484,14 @@ __global__ void __launch_bounds__(256, 1) k_cartpole_rollout_mfma64(RolloutArgs 
     const int N = a.N;
     const int e = (blockIdx.x * WAVES + (threadIdx.x >> 6)) * 64 + lane;
     const bool mine = e < N;
-    // the weights this lane feeds the MFMAs for the whole rollout
-    float w0r[3][2], w1r[32][2];
+    for (int i = threadIdx.x; i < 32 * 64; i += blockDim.x) {
+        const int st = i >> 6, l = i & 63, lc = l & 31, lh = l >> 5;
+        w1r[st][l] = make_float2(P[O.w1 + (2 * st + lh) * H + unit2(lc)], P[O.w1 + (2 * st + lh) * H + unit2(lc + 32)]);
+    }
+    __syncthreads();
+    float *Tw = T2[threadIdx.x >> 6];
+    // layer 1's A operands stay in registers for the whole rollout
+    float w0r[3][2];
 #pragma unroll
     for (int st = 0; st < 3; st++)
 #pragma unroll
@@ -487,10 +499,6 @@ __global__ void __launch_bounds__(256, 1) k_cartpole_rollout_mfma64(RolloutArgs 
             const int d = 2 * st + h, u = unit1(c + 32 * ct);
             w0r[st][ct] = d < 5 ? P[O.w0 + d * H + u] : P[O.b0 + u];
         }
-#pragma unroll
-    for (int st = 0; st < 32; st++)
-#pragma unroll
-        for (int ct = 0; ct < 2; ct++) w1r[st][ct] = P[O.w1 + (2 * st + h) * H + unit2(c + 32 * ct)];
 
     CartPoleState s{};
     uint64_t env_pos = 0;
@@ -563,32 +571,36 @@ __global__ void __launch_bounds__(256, 1) k_cartpole_rollout_mfma64(RolloutArgs 
             for (int ct = 0; ct < 2; ct++)
 #pragma unroll
                 for (int q = 0; q < 16; q++) h2[tl][ct][q] = 0.0f;
+        int zero1 = 0;
+        asm volatile("" : "+v"(zero1));   // the operand reads stay in the step loop
+        const float2 *w1p = &w1r[0][lane] + zero1;
 #pragma unroll
-        for (int st = 0; st < 32; st++)
+        for (int st = 0; st < 32; st++) {
+            const float2 w = w1p[st * 64];
 #pragma unroll
-            for (int ct = 0; ct < 2; ct++)
-#pragma unroll
-                for (int tl = 0; tl < 2; tl++)
-                    h2[tl][ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(w1r[st][ct], h1[tl][st >> 4][st & 15],
-                                                                      h2[tl][ct], 0, 0, 0);
-        // lane l <- all 64 units of env l: hA[m] = unit m, hB[m] = unit 32 + m
-        float hA[32], hB[32];
-#pragma unroll
-        for (int m = 0; m < 32; m++) {
-            hA[m] = h2[0][m >> 4][m & 15];
-            hB[m] = h2[1][m >> 4][m & 15];
-            swap_halves(hA[m], hB[m]);
+            for (int tl = 0; tl < 2; tl++) {
+                h2[tl][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.x, h1[tl][st >> 4][st & 15], h2[tl][0], 0, 0, 0);
+                h2[tl][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.y, h1[tl][st >> 4][st & 15], h2[tl][1], 0, 0, 0);
+            }
         }
+        // H2 -> the wave's [env][unit] tile (register m of lane (c, h) holds unit 32h + m of
+        // env c of tile tl), then lane l reads env l's row
+#pragma unroll
+        for (int tl = 0; tl < 2; tl++)
+#pragma unroll
+            for (int m = 0; m < 32; m++) Tw[(32 * tl + c) * 65 + 32 * h + m] = h2[tl][m >> 4][m & 15];
+        wave_sync();
         // ---- heads: + b1, relu, the k-ordered chains of logit 0, logit 1, value
         // (the row reads stay in the step loop: hoisted, they would pin 256 VGPRs)
         int zero = 0;
         asm volatile("" : "+v"(zero));
         const float4 *hw = S.hw + zero;
+        const float *hrow = Tw + lane * 65 + zero;
         float l0 = 0.0f, l1 = 0.0f, vv = 0.0f;
-#pragma unroll
+#pragma unroll 16
         for (int k = 0; k < H; k++) {
             const float4 w = hw[k];
-            float z = __fadd_rn(k < 32 ? hA[k] : hB[k - 32], w.w);
+            float z = __fadd_rn(hrow[k], w.w);
             z = z > 0.0f ? z : 0.0f;
             l0 = __builtin_fmaf(z, w.x, l0);
             l1 = __builtin_fmaf(z, w.y, l1);
@@ -640,6 +652,7 @@ __global__ void __launch_bounds__(256, 1) k_cartpole_rollout_mfma64(RolloutArgs 
             }
         }
         gz = gz_next;
+        wave_sync();                      // this step's tile reads done before the next step's writes
     }
     if (mine) {
         store_state(a.cp, a.steps, N, e, s);
@@ -872,12 +885,11 @@ bppo_status launch_cartpole_rollout(bppo_ctx *c, uint64_t base_pos, const double
         const uint64_t blocks = ((base_pos + count + 15) >> 4) - (base_pos >> 4);
         hipLaunchKernelGGL(k_gumbel_words, dim3((unsigned)((blocks + 255) / 256)), dim3(256), 0, c->stream, c->rng_key,
                            (uint64_t)c->cfg.rng_stream, base_pos, count, c->d_gumbel);
-        // default: r03's half-wave kernel (2 waves/SIMD, ~180 VGPRs: the side-stream
-        // Fisher-Yates passes share its CUs).  BPPO_ROLLOUT_LANES64=1: the 64-lane kernel,
-        // faster alone (1.05 vs 1.32 ms) but one 475-register wave per SIMD leaves no room
-        // beside it, and device-bound A/B runs end 0.1-0.15 ms/update slower with it
-        // (profiles/r04_rollout/rollout_ab.txt)
-        const bool lanes64 = getenv("BPPO_ROLLOUT_LANES64") && atoi(getenv("BPPO_ROLLOUT_LANES64")) == 1;
+        // default: the 64-lane kernel (269 registers and 84 KB of LDS per 4-wave block, so
+        // the side-stream Fisher-Yates passes still share its CUs): device-bound A/B
+        // 0.1-0.28 ms/update faster than r03's half-wave kernel (profiles/r04_rollout/
+        // rollout_ab.txt).  BPPO_ROLLOUT_LANES64=0: the half-wave kernel.
+        const bool lanes64 = !(getenv("BPPO_ROLLOUT_LANES64") && atoi(getenv("BPPO_ROLLOUT_LANES64")) == 0);
         if (!lanes64) {
             const int waves = (c->N + mmb::TR - 1) / mmb::TR;
             hipLaunchKernelGGL(k_cartpole_rollout_mfma, dim3((waves + mmb::WAVES - 1) / mmb::WAVES), dim3(64 * mmb::WAVES),

@@ -326,15 +326,17 @@ def test_tanh_second_rollout_and_forward_rows_bit_exact():
     tr.close(); ot.close()
 
 
+@pytest.mark.parametrize("lanes64", ["1", "0"])
 @pytest.mark.parametrize("N", [1000, 2048])
-def test_rollout_lanes64_bit_exact(monkeypatch, N):
-    """the 64-lane CfgB rollout kernel (BPPO_ROLLOUT_LANES64=1, k_cartpole_rollout_mfma64:
-    transposed layers, permlane32 swaps, W1 in registers) bit-exact against the oracle
-    over two consecutive rollouts (env state, episode and RNG carry), a partial last wave
-    at N = 1000, with obs + return normalizers"""
+def test_rollout_lanes64_bit_exact(monkeypatch, N, lanes64):
+    """both CfgB rollout kernels — the 64-lane k_cartpole_rollout_mfma64 (default:
+    transposed layers, permlane32 input swaps, W1 and H2 through LDS) and r03's half-wave
+    k_cartpole_rollout_mfma (BPPO_ROLLOUT_LANES64=0) — bit-exact against the oracle over
+    two consecutive rollouts (env state, episode and RNG carry), a partial last wave at
+    N = 1000, with obs + return normalizers"""
     import oracle_ffi as O
     from parity_util import cmp_cartpole_rollout, oracle_train_cfg
-    monkeypatch.setenv("BPPO_ROLLOUT_LANES64", "1")
+    monkeypatch.setenv("BPPO_ROLLOUT_LANES64", lanes64)
     cfg = bppo.make_config("cartpole", num_envs=N, num_steps=32)
     params = bppo.orthogonal_init(cfg, seed=11)
     tr = bppo.Trainer(cfg, params=params)
