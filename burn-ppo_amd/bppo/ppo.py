@@ -174,6 +174,11 @@ class Context:
         bit for bit (ppo.rs:1268-1294), on a host thread beside the update"""
         self._chk(L.lib().bppo_set_explained_variance_mode(self.h, int(mode)))
 
+    def set_minibatch_kernel(self, mode):
+        """0: exact f32 kernel for the update's first minibatch, split-bf16 for the rest
+        (default); 1: exact for every minibatch; 2: split for every minibatch (parity hook)"""
+        self._chk(L.lib().bppo_set_minibatch_kernel(self.h, int(mode)))
+
     def set_allreduce(self, fn, world, stream_ordered=False):
         """fn(device_ptr:int, n:int) -> None must leave the SUM over ranks in place.
         stream_ordered: fn only enqueues the reduction on `self.stream` (no host

@@ -147,12 +147,6 @@ static bppo_status dalloc(bppo_ctx *c, T **p, size_t n) {
     return BPPO_OK;
 }
 
-#define TRY(x)                                 \
-    do {                                       \
-        bppo_status _s = (x);                  \
-        if (_s != BPPO_OK) return _s;          \
-    } while (0)
-
 extern "C" size_t bppo_config_size(void) { return sizeof(bppo_config); }
 extern "C" size_t bppo_update_metrics_size(void) { return sizeof(bppo_update_metrics); }
 extern "C" size_t bppo_episode_size(void) { return sizeof(bppo_episode); }
@@ -173,11 +167,11 @@ extern "C" const char *bppo_last_error(const bppo_ctx *c) { return c ? c->err.c_
 // in r03h), CPU the shuffle walkers of an 8-rank node need.
 static hipError_t wait_event(bppo_ctx *c, hipEvent_t ev) {   // sleeping poll (see sync_stream)
     const auto t0 = std::chrono::steady_clock::now();
-    hipError_t e = hipEventQuery(ev);
+    hipError_t e = event_query(ev);
     if (e == hipErrorNotReady) {
         if (c->wait_est_us > 200.0)
             std::this_thread::sleep_for(std::chrono::microseconds((long)(0.7 * c->wait_est_us)));
-        while ((e = hipEventQuery(ev)) == hipErrorNotReady) std::this_thread::sleep_for(std::chrono::microseconds(20));
+        while ((e = event_query(ev)) == hipErrorNotReady) std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     c->wait_est_us = c->wait_est_us > 0.0 ? 0.5 * c->wait_est_us + 500.0 * ms : 1000.0 * ms;
@@ -193,7 +187,7 @@ static hipError_t sync_stream(bppo_ctx *c) {
         static thread_local bool slack = false;
         if (!slack) { (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0); slack = true; }
         e = hipEventRecord(c->ev_block, c->stream);
-        while (e == hipSuccess && (e = hipEventQuery(c->ev_block)) == hipErrorNotReady) {
+        while (e == hipSuccess && (e = event_query(c->ev_block)) == hipErrorNotReady) {
             std::this_thread::sleep_for(std::chrono::microseconds(20));
             e = hipSuccess;
         }
@@ -554,8 +548,8 @@ extern "C" bppo_status bppo_optimizer_get(bppo_ctx *c, float *m1, float *m2, int
 
 extern "C" bppo_status bppo_optimizer_set(bppo_ctx *c, const float *m1, const float *m2, const int32_t *steps,
                                           size_t n) {
+    // (a rollout enqueued ahead does not read the Adam moments: it stays valid)
     if (!c || !m1 || !m2 || !steps || n != c->net.n_params) {
-    drop_prefetch(c);
         if (c) c->err = "optimizer_set: size mismatch";
         return BPPO_ERR_ARG;
     }
@@ -714,11 +708,17 @@ extern "C" bppo_status bppo_popart_set(bppo_ctx *c, const double *st) {
     return BPPO_OK;
 }
 
-static void tm_begin(bppo_ctx *c, int slot) { (void)hipEventRecord(c->ev[slot][0], c->stream); }
-static void tm_end(bppo_ctx *c, int slot) { (void)hipEventRecord(c->ev[slot][1], c->stream); }
+static bppo_status tm_begin(bppo_ctx *c, int slot) {
+    BPPO_HIP(c, hipEventRecord(c->ev[slot][0], c->stream));
+    return BPPO_OK;
+}
+static bppo_status tm_end(bppo_ctx *c, int slot) {
+    BPPO_HIP(c, hipEventRecord(c->ev[slot][1], c->stream));
+    return BPPO_OK;
+}
 static void tm_read(bppo_ctx *c, int slot) {
     float ms = 0;
-    if (hipEventElapsedTime(&ms, c->ev[slot][0], c->ev[slot][1]) == hipSuccess) c->last_ms[slot] = ms;
+    if (event_ms(c->ev[slot][0], c->ev[slot][1], &ms)) c->last_ms[slot] = ms;
 }
 
 // Fisher-Yates of every epoch of the engine's job in `slot` whose J is already on
@@ -734,15 +734,16 @@ static bppo_status fy_enqueue_ready(bppo_ctx *c, int slot) {
         c->fy_slot = slot; c->fy_done = 0;
         BPPO_HIP(c, hipStreamWaitEvent(c->fy_stream, c->ev_upd, 0));
     }
+    if (c->shuf.failed(c->err)) return BPPO_ERR_HIP;
     while (c->fy_done < c->cfg.num_epochs && c->shuf.epoch_ready(slot, c->fy_done)) {
         const int e = c->fy_done;
         BPPO_HIP(c, hipStreamWaitEvent(c->fy_stream, c->shuf.ev[slot][e], 0));
         if (e > 0) BPPO_HIP(c, hipStreamWaitEvent(c->fy_stream, c->fy_ev[e - 1], 0));   // shared scratch
-        (void)hipEventRecord(c->ev[TM_SHUFFLE][0], c->fy_stream);
+        BPPO_HIP(c, hipEventRecord(c->ev[TM_SHUFFLE][0], c->fy_stream));
         BPPO_HIP(c, fisher_yates_device(c->shuf.d_J[slot] + (size_t)e * B, (uint32_t)B, c->d_fy, c->d_scan,
                                         c->d_perm_ep + (size_t)e * B, c->fy_stream, &c->fyr,
                                         c->d_inv_ep + (size_t)e * B));
-        (void)hipEventRecord(c->ev[TM_SHUFFLE][1], c->fy_stream);
+        BPPO_HIP(c, hipEventRecord(c->ev[TM_SHUFFLE][1], c->fy_stream));
         BPPO_HIP(c, hipEventRecord(c->fy_ev[e], c->fy_stream));
         c->fy_done++;
     }
@@ -763,13 +764,13 @@ static bppo_status collect_enqueue(bppo_ctx *c, bool summary) {
     BPPO_HIP(c, hipMemsetAsync(c->d_ep_count, 0, 4, c->stream));
     BPPO_HIP(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
     const uint64_t base = c->rng_pos;
-    tm_begin(c, tro);
+    TRY(tm_begin(c, tro));
     if (c->wide) TRY(wide_collect(c, base));
     else {
         TRY(launch_cartpole_rollout(c, base, nullptr, nullptr, c->cfg.normalize_obs));
         TRY(popart_denorm(c, c->d_val, TN));            // ppo.rs:355-359 (multi-player: in the sampler)
     }
-    tm_end(c, tro);
+    TRY(tm_end(c, tro));
     // self-play: the update's shuffles start right after this rollout's Gumbel words,
     // so the epochs the engine has resolved are permuted now, beside the rollout
     // (beside the rollout is where they cost least: it leaves VGPRs and LDS free on every
@@ -787,10 +788,10 @@ static bppo_status collect_enqueue(bppo_ctx *c, bool summary) {
         c->shuf_slot = c->shuf.ensure(c->rng_pos);
     }
     if (c->cfg.normalize_obs) TRY(launch_obs_norm_merge(c));       // ppo.rs:495-497
-    tm_begin(c, trn);
+    TRY(tm_begin(c, trn));
     if (c->cfg.normalize_returns) TRY(launch_return_norm(c));      // ppo.rs:390-408
     else if (!c->wide) BPPO_HIP(c, hipMemcpyAsync(c->d_rew, c->d_rew_raw, TN * 4, hipMemcpyDeviceToDevice, c->stream));
-    tm_end(c, trn);
+    TRY(tm_end(c, trn));
     if (summary) TRY(launch_episode_summary(c));
     int32_t *hv = reinterpret_cast<int32_t *>(roll_host(c, c->coll_slot));     // pinned: truly async copies
     double *part = roll_host(c, c->coll_slot) + 2;
@@ -808,8 +809,8 @@ static bppo_status collect_enqueue(bppo_ctx *c, bool summary) {
 static bppo_status collect_finish(bppo_ctx *c, bppo_rollout_info *info, int slot) {
     float ms = 0;
     const int tro = slot ? TM_ROLLOUT_B : TM_ROLLOUT, trn = slot ? TM_RETNORM_B : TM_RETNORM;
-    if (hipEventElapsedTime(&ms, c->ev[tro][0], c->ev[tro][1]) == hipSuccess) c->last_ms[TM_ROLLOUT] = ms;
-    if (hipEventElapsedTime(&ms, c->ev[trn][0], c->ev[trn][1]) == hipSuccess) c->last_ms[TM_RETNORM] = ms;
+    if (event_ms(c->ev[tro][0], c->ev[tro][1], &ms)) c->last_ms[TM_ROLLOUT] = ms;
+    if (event_ms(c->ev[trn][0], c->ev[trn][1], &ms)) c->last_ms[TM_RETNORM] = ms;
     const int32_t *hv = reinterpret_cast<const int32_t *>(roll_host(c, slot));
     const double *part = roll_host(c, slot) + 2;
     // device error bits: 1 non-finite log-prob, 2 empty action mask, 4 opponent seat
@@ -871,24 +872,25 @@ extern "C" bppo_status bppo_rollout_episodes(bppo_ctx *c, bppo_episode *eps, int
 static bppo_status gae_enqueue(bppo_ctx *c) {
     c->prefetched = false;        // a pending rollout is consumed here (e.g. after a bppo_train_steps error)
     if (c->wide) {
-        tm_begin(c, TM_GAE);
+        TRY(tm_begin(c, TM_GAE));
         TRY(wide_bootstrap_gae(c));
-        tm_end(c, TM_GAE);
+        TRY(tm_end(c, TM_GAE));
         c->gae_done = 1;
         return BPPO_OK;
     }
-    tm_begin(c, TM_BOOT);
+    TRY(tm_begin(c, TM_BOOT));
     TRY(launch_bootstrap(c, nullptr, nullptr, c->cfg.normalize_obs));
     TRY(popart_denorm(c, c->d_last_v, (size_t)c->N));   // main.rs:898-907
-    tm_end(c, TM_BOOT);
-    tm_begin(c, TM_GAE);
+    TRY(tm_end(c, TM_BOOT));
+    TRY(tm_begin(c, TM_GAE));
     bool packed = false;
+    hipError_t he = hipSuccess;
     bppo_status s = launch_gae_1p(c->d_rew, c->d_done, c->d_val, c->d_last_v, c->T, c->N,
                                   (float)c->cfg.gamma, (float)c->cfg.gae_lambda, c->d_adv, c->d_ret,
-                                  c->stream, c->rows_from_rollout ? c->d_rowB : nullptr, &packed);
+                                  c->stream, c->rows_from_rollout ? c->d_rowB : nullptr, &packed, &he);
     c->rows_packed = packed;
-    tm_end(c, TM_GAE);
-    if (s != BPPO_OK) { c->err = "gae launch failed"; return s; }
+    if (s != BPPO_OK) return he != hipSuccess ? hip_fail(c, he, "k_gae_1p launch") : s;
+    TRY(tm_end(c, TM_GAE));
     c->gae_done = 1;
     return BPPO_OK;
 }
@@ -935,15 +937,35 @@ static float ev_reference_f32(const float *v, const float *r, const float *valid
 extern "C" bppo_status bppo_set_explained_variance_mode(bppo_ctx *c, int32_t mode) {
     if (!c || mode < 0 || mode > 1) return BPPO_ERR_ARG;
     if (mode == 1 && !c->h_ev_v) {
+        // every resource into a local first: committed together, or all released
         const size_t TN = (size_t)c->T * c->N;
-        BPPO_HIP(c, hipStreamCreateWithFlags(&c->ev_stream, hipStreamNonBlocking));
-        BPPO_HIP(c, hipEventCreateWithFlags(&c->ev_gae, hipEventDisableTiming));
-        BPPO_HIP(c, hipEventCreateWithFlags(&c->ev_copied, hipEventDisableTiming | hipEventBlockingSync));
-        BPPO_HIP(c, hipHostMalloc((void **)&c->h_ev_v, TN * 4, hipHostMallocDefault));
-        BPPO_HIP(c, hipHostMalloc((void **)&c->h_ev_r, TN * 4, hipHostMallocDefault));
-        BPPO_HIP(c, hipHostMalloc((void **)&c->h_ev_valid, TN * 4, hipHostMallocDefault));
+        hipStream_t st = nullptr;
+        hipEvent_t e_gae = nullptr, e_cp = nullptr;
+        float *hv = nullptr, *hr = nullptr, *hm = nullptr;
+        hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&e_gae, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&e_cp, hipEventDisableTiming | hipEventBlockingSync);
+        if (e == hipSuccess) e = hipHostMalloc((void **)&hv, TN * 4, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipHostMalloc((void **)&hr, TN * 4, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipHostMalloc((void **)&hm, TN * 4, hipHostMallocDefault);
+        if (e != hipSuccess) {
+            for (float *h : {hv, hr, hm}) if (h) (void)hipHostFree(h);
+            if (e_cp) (void)hipEventDestroy(e_cp);
+            if (e_gae) (void)hipEventDestroy(e_gae);
+            if (st) (void)hipStreamDestroy(st);
+            return hip_fail(c, e, "explained-variance reference mode: allocation");
+        }
+        c->ev_stream = st; c->ev_gae = e_gae; c->ev_copied = e_cp;
+        c->h_ev_r = hr; c->h_ev_valid = hm;
+        c->h_ev_v = hv;                    // last: marks the set complete
     }
     c->ev_mode = mode;
+    return BPPO_OK;
+}
+
+extern "C" bppo_status bppo_set_minibatch_kernel(bppo_ctx *c, int32_t mode) {
+    if (!c || mode < 0 || mode > 2) return BPPO_ERR_ARG;
+    c->mb_kernel = mode;
     return BPPO_OK;
 }
 
@@ -951,6 +973,9 @@ extern "C" bppo_status bppo_set_explained_variance_mode(bppo_ctx *c, int32_t mod
 // later rewrites them) and sum them on a host thread while the update runs
 static bppo_status ev_reference_begin(bppo_ctx *c, const float *d_valid) {
     const size_t TN = (size_t)c->T * c->N;
+    // a thread left by an update that returned early still reads the pinned buffers
+    // (or waits on ev_copied): it ends before they are refilled or the event re-recorded
+    if (c->ev_thread.joinable()) c->ev_thread.join();
     BPPO_HIP(c, hipEventRecord(c->ev_gae, c->stream));
     BPPO_HIP(c, hipStreamWaitEvent(c->ev_stream, c->ev_gae, 0));
     BPPO_HIP(c, hipMemcpyAsync(c->h_ev_v, c->d_val, TN * 4, hipMemcpyDeviceToHost, c->ev_stream));
@@ -958,7 +983,6 @@ static bppo_status ev_reference_begin(bppo_ctx *c, const float *d_valid) {
     if (d_valid) BPPO_HIP(c, hipMemcpyAsync(c->h_ev_valid, d_valid, TN * 4, hipMemcpyDeviceToHost, c->ev_stream));
     BPPO_HIP(c, hipEventRecord(c->ev_copied, c->ev_stream));
     const bool vf = d_valid != nullptr;
-    if (c->ev_thread.joinable()) c->ev_thread.join();      // an update that returned early
     c->ev_thread = std::thread([c, TN, vf]() {
         (void)pthread_setname_np(pthread_self(), "bppo-ev");
         (void)hipEventSynchronize(c->ev_copied);
@@ -995,8 +1019,15 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
     int epochs_run = 0;
     bool stop = false;
     double wait_ms = 0.0;
-    tm_begin(c, TM_UPDATE);
-    if (c->ev_mode == 1) TRY(ev_reference_begin(c, opp ? c->d_valid : nullptr));
+    TRY(tm_begin(c, TM_UPDATE));
+    // mode 1 copies d_val / d_ret on ev_stream beside the update: on every return from here
+    // the context stream waits for those copies, so the next rollout cannot overwrite the
+    // buffers under them (the normal path enqueues the wait itself below)
+    struct EvCopyGuard {
+        bppo_ctx *c; bool armed = false;
+        ~EvCopyGuard() { if (armed) (void)hipStreamWaitEvent(c->stream, c->ev_copied, 0); }
+    } ev_guard{c};
+    if (c->ev_mode == 1) { TRY(ev_reference_begin(c, opp ? c->d_valid : nullptr)); ev_guard.armed = true; }
     TRY(popart_update_begin(c, opp ? c->d_valid : nullptr));   // ppo.rs:1787-1808
     if (c->d_rowA && !c->rows_packed) TRY(launch_pack_rows(c));
     c->rows_packed = false;
@@ -1017,10 +1048,10 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
             opp_pos = shuffle_walk_host(c->rng_key, c->cfg.rng_stream, opp_pos, (uint32_t)B, J);   // ppo.rs:1816
             wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
             BPPO_HIP(c, hipMemcpyAsync(c->d_Jopp, J, sizeof(uint32_t) * B, hipMemcpyHostToDevice, c->stream));
-            (void)hipEventRecord(s0, c->stream);
+            BPPO_HIP(c, hipEventRecord(s0, c->stream));
             if (B) TRY(launch_fisher_yates(c, c->d_Jopp, (uint32_t)B));
             if (B) TRY(opp_map_perm(c, (uint32_t)B));
-            (void)hipEventRecord(s1, c->stream);
+            BPPO_HIP(c, hipEventRecord(s1, c->stream));
         } else {
             if (slot != c->fy_slot || ep >= c->fy_done) {
                 auto w0 = std::chrono::steady_clock::now();
@@ -1039,14 +1070,14 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
         for (int mb = 0; mb < M; mb++) {
             const size_t sz = base_mb + ((size_t)mb < rem ? 1 : 0);
             if (sz == 0) continue;
-            (void)hipEventRecord(c->ev[TM_FWDBWD][0], c->stream);
+            BPPO_HIP(c, hipEventRecord(c->ev[TM_FWDBWD][0], c->stream));
             c->d_mb_cur = c->d_mb_stats + 4 * mb;
             if (c->wide) {
                 TRY(wide_minibatch(c, (uint32_t)start, (uint32_t)sz, (float)ent_coef));
             } else {
                 TRY(launch_minibatch(c, (uint32_t)start, (uint32_t)sz, (float)ent_coef, first_mb));
             }
-            (void)hipEventRecord(c->ev[TM_FWDBWD][1], c->stream);
+            BPPO_HIP(c, hipEventRecord(c->ev[TM_FWDBWD][1], c->stream));
             first_mb = false;
             if (c->allreduce && c->world > 1) {
                 if (!c->allreduce_async) BPPO_HIP(c, sync_stream(c));
@@ -1072,8 +1103,8 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
                                            hipMemcpyDeviceToHost, c->stream));
                 BPPO_HIP(c, sync_stream(c));
                 float ms = 0;
-                if (hipEventElapsedTime(&ms, c->ev[TM_FWDBWD][0], c->ev[TM_FWDBWD][1]) == hipSuccess) fw_ms = ms;
-                if (mb == 0 && hipEventElapsedTime(&ms, s0, s1) == hipSuccess) sh_ms = ms;
+                if (event_ms(c->ev[TM_FWDBWD][0], c->ev[TM_FWDBWD][1], &ms)) fw_ms = ms;
+                if (mb == 0 && event_ms(s0, s1, &ms)) sh_ms = ms;
                 rows.insert(rows.end(), row.begin(), row.end());
             }
             if (!deferred && c->cfg.target_kl >= 0) {
@@ -1091,7 +1122,7 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
         // read after the one stream wait below, behind the explained-variance pass
         BPPO_HIP(c, hipMemcpyAsync(c->h_rows, c->d_rows, sizeof(float) * rows.size(), hipMemcpyDeviceToHost, c->stream));
     }
-    tm_end(c, TM_UPDATE);
+    TRY(tm_end(c, TM_UPDATE));
     c->last_wait_ms = wait_ms;
     c->last_walk_ms = 0.0;
     c->last_met = 0;
@@ -1118,13 +1149,13 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
             BPPO_HIP(c, hipStreamWaitEvent(c->stream, c->fy_ev[c->fy_done - 1], 0));
         c->fy_slot = -1;
         c->fy_done = 0;
-        c->shuf.release(slot, c->stream);
+        BPPO_HIP(c, c->shuf.release(slot, c->stream));
         c->shuf.ensure(c->rng_pos + (uint64_t)c->T * c->N * (uint64_t)c->A);
     }
     TRY(popart_target_stats(c, stop ? epochs_run - 1 : epochs_run, rows_done, opp ? c->d_valid : nullptr));
     TRY(launch_explained_variance(c, opp ? c->d_valid : nullptr));
     // mode 1: nothing after this update (the next rollout) overwrites the copied buffers early
-    if (c->ev_mode == 1) BPPO_HIP(c, hipStreamWaitEvent(c->stream, c->ev_copied, 0));
+    if (ev_guard.armed) { ev_guard.armed = false; BPPO_HIP(c, hipStreamWaitEvent(c->stream, c->ev_copied, 0)); }
     BPPO_HIP(c, hipEventRecord(c->ev_upd, c->stream));      // end of this update's work
     if (c->prefetch_next) {
         // bppo_train_steps: the next rollout goes in behind this update (it needs only the
@@ -1141,8 +1172,8 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
     if (deferred && nrow > 0) {
         std::memcpy(rows.data(), c->h_rows, sizeof(float) * rows.size());
         float ms = 0;
-        if (hipEventElapsedTime(&ms, c->ev[TM_FWDBWD][0], c->ev[TM_FWDBWD][1]) == hipSuccess) fw_ms = ms;
-        if (hipEventElapsedTime(&ms, c->ev[TM_SHUFFLE][0], c->ev[TM_SHUFFLE][1]) == hipSuccess) sh_ms = ms;
+        if (event_ms(c->ev[TM_FWDBWD][0], c->ev[TM_FWDBWD][1], &ms)) fw_ms = ms;
+        if (event_ms(c->ev[TM_SHUFFLE][0], c->ev[TM_SHUFFLE][1], &ms)) sh_ms = ms;
     }
     double ev4[4];
     explained_variance_sums(c, ev4);
@@ -1154,7 +1185,7 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
         int n = 0, kn[2] = {0, 0};
         for (int i = 0; i < c->mb_ev_n; i++) {
             float ms = 0.0f;
-            if (hipEventElapsedTime(&ms, c->mb_ev[i][0], c->mb_ev[i][1]) != hipSuccess) continue;
+            if (!event_ms(c->mb_ev[i][0], c->mb_ev[i][1], &ms)) continue;
             sum += ms; lo = std::min(lo, ms); hi = std::max(hi, ms); n++;
             ks[c->mb_ev_split[i]] += ms; kn[c->mb_ev_split[i]]++;
         }

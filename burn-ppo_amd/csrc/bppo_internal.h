@@ -207,8 +207,15 @@ struct ShuffleEngine {
                      std::string &err, bool windows = false);
     bool run_windowed(int slot, uint64_t start);   // one job of independent epoch walks (false: cancelled)
     uint64_t job_end(int slot) const { return win ? slot_start[slot] + (uint64_t)epochs * win : end_pos[slot][epochs - 1]; }
+    // a HIP call of the engine's own thread that failed (its uploads, J expansions, events):
+    // the first one is kept and the caller's next wait on the engine reports it
+    std::atomic<bool> hip_bad{false};
+    std::mutex hip_mu;
+    std::string hip_msg;                          // (hip_mu) written once, before hip_bad is set
+    void hip_note(hipError_t e, const char *what);
+    bool failed(std::string &msg) const;          // -> true and the message after a failure
     int ensure(uint64_t start);               // job for this start (reused if already running/done) -> slot
-    void release(int slot, hipStream_t st);   // the caller is done enqueuing reads of d_J[slot] on st
+    hipError_t release(int slot, hipStream_t st);   // the caller is done enqueuing reads of d_J[slot] on st
     void wait_epoch(int slot, int e);
     bool epoch_ready(int slot, int e);        // non-blocking wait_epoch
     void shutdown();
@@ -251,6 +258,7 @@ struct bppo_ctx {
     size_t slab_rows = 0;
     int slab_used = 0;                // waves that wrote a row in the last minibatch launch
     int relu_mfma = 1;                // CfgB net (64x2 relu): the MFMA minibatch kernel
+    int mb_kernel = 0;                // bppo_set_minibatch_kernel: 0 exact first / split rest, 1 exact, 2 split
     // env state (CartPole SoA)
     float *d_cp = nullptr;            // x, x_dot, theta, theta_dot  [4][N]
     int32_t *d_steps = nullptr;
@@ -444,12 +452,13 @@ bppo_status launch_bootstrap(bppo_ctx *c, const double *mean, const double *sd, 
 bppo_status launch_forward_rows(bppo_ctx *c, const float *d_obs, int B, float *d_logits,
                                 float *d_values);
 // (k_gae.hip)
+// (no context: the launch's HIP status goes to *herr when given)
 bppo_status launch_gae_1p(const float *r, const float *d, const float *v, const float *lv, int T,
                           int N, float gamma, float lambda, float *adv, float *ret, hipStream_t s,
-                          float2 *pairs = nullptr, bool *pairs_done = nullptr);
+                          float2 *pairs = nullptr, bool *pairs_done = nullptr, hipError_t *herr = nullptr);
 bppo_status launch_gae_mp(const float *ar, const int32_t *pl, const float *d, const float *v,
                           const float *lvpp, int T, int N, int P, float gamma, float lambda,
-                          float *adv, float *ret, hipStream_t s);
+                          float *adv, float *ret, hipStream_t s, hipError_t *herr = nullptr);
 bppo_status launch_return_norm(bppo_ctx *c);
 // (k_update.hip)
 bppo_status launch_fisher_yates(bppo_ctx *c, const uint32_t *d_J, uint32_t n);
@@ -529,7 +538,34 @@ inline bppo_status hip_fail(bppo_ctx *c, hipError_t e, const char *what) {
     if (c) c->err = std::string(what) + ": " + hipGetErrorString(e);
     return BPPO_ERR_HIP;
 }
+// A kernel launch's status is read with hipGetLastError, which returns the last error
+// of ANY earlier HIP call on this thread that nobody cleared.  So every call whose
+// status is handled where it is made clears the slot there (event_query / event_ms
+// below: "not ready" is an answer, not a failure), every other call on the enqueue
+// path is checked, and each launch helper names its kernel in the message.
+// (r04: a pipelined run reported "gae launch failed" for an earlier call's status;
+// DESIGN.md section 5b names it.)
+inline bppo_status launch_check(bppo_ctx *c, const char *kernel) {
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? BPPO_OK : hip_fail(c, e, kernel);
+}
+inline hipError_t event_query(hipEvent_t ev) {
+    const hipError_t e = hipEventQuery(ev);
+    if (e != hipSuccess) (void)hipGetLastError();
+    return e;
+}
+inline bool event_ms(hipEvent_t a, hipEvent_t b, float *ms) {
+    const hipError_t e = hipEventElapsedTime(ms, a, b);
+    if (e != hipSuccess) (void)hipGetLastError();
+    return e == hipSuccess;
+}
 }  // namespace bppo
+
+#define TRY(x)                                 \
+    do {                                       \
+        bppo_status _s = (x);                  \
+        if (_s != BPPO_OK) return _s;          \
+    } while (0)
 
 #define BPPO_HIP(c, expr)                                                   \
     do {                                                                    \

@@ -282,7 +282,7 @@ __global__ void __launch_bounds__(GSEG_WAVES * 64) k_gae_mp_seg(const float *__r
 
 bppo_status launch_gae_1p(const float *r, const float *d, const float *v, const float *lv, int T,
                           int N, float gamma, float lambda, float *adv, float *ret, hipStream_t s,
-                          float2 *pairs, bool *pairs_done) {
+                          float2 *pairs, bool *pairs_done, hipError_t *herr) {
     if (pairs_done) *pairs_done = false;
     if (T <= 0 || N <= 0) return BPPO_OK;
     const bool al = ((uintptr_t)r | (uintptr_t)d | (uintptr_t)v | (uintptr_t)lv | (uintptr_t)adv | (uintptr_t)ret |
@@ -297,12 +297,14 @@ bppo_status launch_gae_1p(const float *r, const float *d, const float *v, const 
         hipLaunchKernelGGL(k_gae_1p, dim3((N + 255) / 256), dim3(256), 0, s, r, d, v, lv, T, N, gamma,
                            lambda, adv, ret);
     }
-    return hipGetLastError() == hipSuccess ? BPPO_OK : BPPO_ERR_HIP;
+    const hipError_t e = hipGetLastError();
+    if (herr) *herr = e;
+    return e == hipSuccess ? BPPO_OK : BPPO_ERR_HIP;
 }
 
 bppo_status launch_gae_mp(const float *ar, const int32_t *pl, const float *d, const float *v,
                           const float *lvpp, int T, int N, int P, float gamma, float lambda,
-                          float *adv, float *ret, hipStream_t s) {
+                          float *adv, float *ret, hipStream_t s, hipError_t *herr) {
     if (T <= 0 || N <= 0) return BPPO_OK;
     if (T <= GSEG_WAVES * GSEG_L && P >= 1 && P <= 6) {
         const int L = (T + GSEG_WAVES - 1) / GSEG_WAVES;
@@ -317,7 +319,9 @@ bppo_status launch_gae_mp(const float *ar, const int32_t *pl, const float *d, co
         default: MPSEG(6); break;
         }
 #undef MPSEG
-        return hipGetLastError() == hipSuccess ? BPPO_OK : BPPO_ERR_HIP;
+        const hipError_t e = hipGetLastError();
+        if (herr) *herr = e;
+        return e == hipSuccess ? BPPO_OK : BPPO_ERR_HIP;
     }
     dim3 g((N + 255) / 256), b(256);
     switch (P) {
@@ -329,7 +333,9 @@ bppo_status launch_gae_mp(const float *ar, const int32_t *pl, const float *d, co
     case 6: hipLaunchKernelGGL(k_gae_mp<6>, g, b, 0, s, ar, pl, d, v, lvpp, T, N, gamma, lambda, adv, ret); break;
     default: return BPPO_ERR_ARG;
     }
-    return hipGetLastError() == hipSuccess ? BPPO_OK : BPPO_ERR_HIP;
+    const hipError_t e = hipGetLastError();
+    if (herr) *herr = e;
+    return e == hipSuccess ? BPPO_OK : BPPO_ERR_HIP;
 }
 
 // --------------------------------------------------------- ReturnNormalizer --
@@ -533,7 +539,7 @@ bppo_status launch_return_norm(bppo_ctx *c) {
     if (c->wide)
         hipLaunchKernelGGL(k_rn_scatter_acting, dim3((unsigned)std::min<size_t>((n + 255) / 256, 4096)), dim3(256), 0,
                            c->stream, n, c->P, c->d_players, c->d_rew, c->d_allr);
-    BPPO_HIP(c, hipGetLastError());
+    TRY(launch_check(c, __func__));
     return BPPO_OK;
 }
 

@@ -839,7 +839,7 @@ __global__ void k_obs_norm_final(int D, int nblk, const double *bp, double *on) 
 #define CP_DISPATCH(H_, NL_, CALL)                                                 \
     if (h == H_ && nl == NL_) {                                                    \
         if (c->cfg.relu) CALL(H_, NL_, ACT_RELU); else CALL(H_, NL_, ACT_TANH);   \
-        return BPPO_OK;                                                            \
+        return launch_check(c, __func__);                                          \
     }
 
 static bool cp_supported(int h, int nl) {
@@ -851,7 +851,7 @@ bppo_status launch_cartpole_reset(bppo_ctx *c) {
     hipLaunchKernelGGL(k_cartpole_reset, dim3((N + 255) / 256), dim3(256), 0, c->stream, N,
                        c->cfg.env_seed_base, c->d_cp, c->d_steps, c->d_env_pos, c->d_ep_ret,
                        c->d_ep_len, nullptr);
-    BPPO_HIP(c, hipGetLastError());
+    TRY(launch_check(c, __func__));
     return BPPO_OK;
 }
 
@@ -899,7 +899,7 @@ bppo_status launch_cartpole_rollout(bppo_ctx *c, uint64_t base_pos, const double
             hipLaunchKernelGGL(k_cartpole_rollout_mfma64, dim3((waves + mmr::WAVES - 1) / mmr::WAVES),
                                dim3(64 * mmr::WAVES), 0, c->stream, a, (const float *)c->d_gumbel);
         }
-        BPPO_HIP(c, hipGetLastError());
+        TRY(launch_check(c, __func__));
         return BPPO_OK;
     }
     dim3 grid((c->N + 255) / 256), blk(256);
@@ -942,7 +942,7 @@ bppo_status launch_cartpole_vecenv_step(bppo_ctx *c, const int32_t *d_actions, f
                        c->cfg.env_seed_base, c->d_cp, c->d_steps, c->d_env_pos, c->d_ep_ret,
                        c->d_ep_len, d_actions, d_rew, d_done, d_obs_out, c->d_eps, c->d_ep_count,
                        c->eps_cap);
-    BPPO_HIP(c, hipGetLastError());
+    TRY(launch_check(c, __func__));
     return BPPO_OK;
 }
 
@@ -950,7 +950,7 @@ bppo_status launch_cartpole_observe(bppo_ctx *c, float *d_obs_out) {
     int N = c->N;
     hipLaunchKernelGGL(k_cartpole_observe, dim3((N + 255) / 256), dim3(256), 0, c->stream, N,
                        c->d_cp, c->d_steps, d_obs_out);
-    BPPO_HIP(c, hipGetLastError());
+    TRY(launch_check(c, __func__));
     return BPPO_OK;
 }
 
@@ -984,7 +984,7 @@ bppo_status launch_obs_norm_rows_on(bppo_ctx *c, int rows, float *x, int ld, flo
     const size_t n = (size_t)rows * c->D;
     hipLaunchKernelGGL(k_obs_norm_rows, dim3((unsigned)std::min<size_t>((n + 255) / 256, 8192)), dim3(256), 0,
                        c->stream, rows, c->D, ld, x, raw, on, 10.0f);
-    BPPO_HIP(c, hipGetLastError());
+    TRY(launch_check(c, __func__));
     return BPPO_OK;
 }
 
@@ -1039,7 +1039,7 @@ bppo_status launch_obs_norm_merge(bppo_ctx *c) {
         hipLaunchKernelGGL(k_obsw_final, dim3((c->D + 255) / 256), dim3(256), 0, c->stream, c->D, OBSW_CHUNKS,
                            c->d_obsw_part, c->d_on);
         hipLaunchKernelGGL(k_obsw_count, dim3(1), dim3(1), 0, c->stream, c->D, (double)rows, c->d_on);
-        BPPO_HIP(c, hipGetLastError());
+        TRY(launch_check(c, __func__));
         return BPPO_OK;
     }
     if (c->D > OBS_MAX_D) { c->err = "observation normalizer: obs dim > 8"; return BPPO_ERR_UNSUPPORTED; }
@@ -1047,7 +1047,7 @@ bppo_status launch_obs_norm_merge(bppo_ctx *c) {
     hipLaunchKernelGGL(k_obs_norm_part, dim3(nblk), dim3(256), 0, c->stream, c->N, c->D, (double)c->T,
                        c->d_obs_part, c->d_red);
     hipLaunchKernelGGL(k_obs_norm_final, dim3(1), dim3(64), 0, c->stream, c->D, nblk, c->d_red, c->d_on);
-    BPPO_HIP(c, hipGetLastError());
+    TRY(launch_check(c, __func__));
     return BPPO_OK;
 }
 
@@ -1076,7 +1076,7 @@ __global__ void __launch_bounds__(256) k_ep_summary(const EpisodeRec *eps, const
 bppo_status launch_episode_summary(bppo_ctx *c) {
     hipLaunchKernelGGL(k_ep_summary, dim3(EP_SUMMARY_BLOCKS), dim3(256), 0, c->stream, c->d_eps, c->d_ep_count,
                        c->eps_cap, c->d_ep_sum);
-    BPPO_HIP(c, hipGetLastError());
+    TRY(launch_check(c, __func__));
     return BPPO_OK;
 }
 

@@ -348,7 +348,7 @@ bppo_status launch_pack_rows(bppo_ctx *c) {
     const size_t B = (size_t)c->T * c->N;
     hipLaunchKernelGGL(k_pack_rows, dim3(2048), dim3(256), 0, c->stream, B, c->d_obs, c->d_act, c->d_logp, c->d_adv,
                        c->u_ret, c->u_val, c->d_rowA, c->d_rowB);
-    BPPO_HIP(c, hipGetLastError());
+    TRY(launch_check(c, __func__));
     return BPPO_OK;
 }
 
@@ -725,8 +725,12 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
 // v_mfma_f32_32x32x16_bf16 (1/16 the cycles of the f32 MFMA per FLOP) with every f32
 // operand split exactly into three bf16 pieces x = x0 + x1 + x2 (8 significand bits each)
 // and the six products of order <= 2 accumulated in f32 (x0y0, x0y1, x1y0, x0y2, x1y1,
-// x2y0; the dropped terms are < 2^-26 relative): 48 bf16 MFMAs of 32 cycles per
-// contraction per 32-row tile instead of 64 f32 MFMAs of 64 cycles.
+// x2y0).  |x1| <= 2^-8 |x| and |x2| <= 2^-16 |x|, so each dropped product (x1y2, x2y1,
+// x2y2) is at most 2^-24 |xy|, together <= (2^-23 + 2^-32) |xy|; with the f32 additions a
+// product is within 2^-22 of xy (tests/test_split_bf16.py), and the kernel's gradient is
+// checked against the oracle from identical parameters (tests/test_gpu_split_kernel.py):
+// 48 bf16 MFMAs of 32 cycles per contraction per 32-row tile instead of 64 f32 MFMAs of
+// 64 cycles.
 //   layer 1 twice on the f32 MFMA (K = 6, b0 folded into the pad row): transposed
 //     (H1^T: units in registers, rows on lanes = layer 2's A fragments, no LDS) and in
 //     the C/D orientation (rows in registers = dW1's A fragments and the relu mask);
@@ -1539,7 +1543,7 @@ bppo_status launch_epoch_adv_stats(bppo_ctx *c, uint32_t B, int M, const uint32_
         else if (MB == 8) hipLaunchKernelGGL(k_adv_stream<8>, dim3(nblk), dim3(256), 0, c->stream, c->d_adv, inv, sp, C, c->d_advpart);
         else hipLaunchKernelGGL(k_adv_stream<16>, dim3(nblk), dim3(256), 0, c->stream, c->d_adv, inv, sp, C, c->d_advpart);
         hipLaunchKernelGGL(k_adv_stream_final, dim3(M), dim3(256), 0, c->stream, c->d_advpart, nblk, MB, sp, c->d_mb_stats);
-        BPPO_HIP(c, hipGetLastError());
+        TRY(launch_check(c, __func__));
         return BPPO_OK;
     }
     uint32_t C = (B + 511) / 512;
@@ -1549,7 +1553,7 @@ bppo_status launch_epoch_adv_stats(bppo_ctx *c, uint32_t B, int M, const uint32_
     if ((size_t)nblk * 8 > 4 * 1024 + 64) { c->err = "epoch advantage stats: too many minibatches"; return BPPO_ERR_UNSUPPORTED; }
     hipLaunchKernelGGL(k_adv_epoch, dim3(nblk), dim3(ADV_THREADS), 0, c->stream, c->d_adv, c->d_perm, sp, C, c->d_red);
     hipLaunchKernelGGL(k_adv_epoch_final, dim3(M), dim3(256), 0, c->stream, c->d_red, (int)nblk, C, sp, c->d_mb_stats);
-    BPPO_HIP(c, hipGetLastError());
+    TRY(launch_check(c, __func__));
     return BPPO_OK;
 }
 
@@ -1582,16 +1586,17 @@ bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_
         // the update's first minibatch runs with the rollout's parameters: the exact
         // f32 kernel, so the ratio is exactly 1; the others on the split-bf16 kernel
         // (BPPO_MB_EXACT_ALL=1: the exact kernel for every minibatch, for A/B runs)
+        // (bppo_set_minibatch_kernel: 1 = exact for every minibatch, 2 = split for every one)
         static const bool exact_all = getenv("BPPO_MB_EXACT_ALL") != nullptr;
-        const bool use_exact = exact || exact_all;
+        const bool use_exact = c->mb_kernel == 1 || (c->mb_kernel == 0 && (exact || exact_all));
         const size_t lds_split = std::max(mmf::LDS_TILES, (size_t)mmf::WAVES * (c->net.n_params + NUM_M) * sizeof(float));
         const int ei = c->mb_ev_n < bppo_ctx::MB_EV ? c->mb_ev_n++ : -1;
-        if (ei >= 0) { c->mb_ev_split[ei] = !use_exact; (void)hipEventRecord(c->mb_ev[ei][0], c->stream); }
+        if (ei >= 0) { c->mb_ev_split[ei] = !use_exact; BPPO_HIP(c, hipEventRecord(c->mb_ev[ei][0], c->stream)); }
         if (use_exact)
             hipLaunchKernelGGL(k_minibatch_mfma, dim3(blocks), dim3(64 * mmb::WAVES), mmb::LDSB, c->stream, g);
         else
             hipLaunchKernelGGL(k_minibatch_split, dim3(blocks), dim3(64 * mmf::WAVES), lds_split, c->stream, g);
-        if (ei >= 0) (void)hipEventRecord(c->mb_ev[ei][1], c->stream);
+        if (ei >= 0) BPPO_HIP(c, hipEventRecord(c->mb_ev[ei][1], c->stream));
 #ifdef BPPO_MB_STAMPS
         {   // mean per-wave cycles per segment, accumulated over launches; printed every 16
             static double acc_s[MB_NSEG] = {};
@@ -1625,12 +1630,12 @@ bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_
         return BPPO_ERR_UNSUPPORTED;
     }
 #undef L
-    BPPO_HIP(c, hipGetLastError());
+    TRY(launch_check(c, __func__));
     const int width = (int)c->net.n_params + NUM_M;
     static_assert(M_VEMAX == GRAD_VEMAX && NUM_M <= GRAD_METRIC_SLOTS, "metric slot layout");
     hipLaunchKernelGGL(k_slab_reduce1, dim3((width + 63) / 64), dim3(64 * SLAB1_WAVES), 0, c->stream, c->d_slab,
                        c->slab_used, width, c->d_grad, c->d_grad + c->net.n_params + GRAD_VEMAX_LOCAL);
-    BPPO_HIP(c, hipGetLastError());
+    TRY(launch_check(c, __func__));
     return BPPO_OK;
 }
 
@@ -1643,7 +1648,7 @@ __global__ void k_metric_row(const float *gtail, const float *mb_stats, int nm, 
 bppo_status launch_metric_row(bppo_ctx *c, float *dst, int nm) {
     hipLaunchKernelGGL(k_metric_row, dim3(1), dim3(64), 0, c->stream, c->d_grad + c->net.n_params, c->d_mb_cur, nm,
                        dst);
-    BPPO_HIP(c, hipGetLastError());
+    TRY(launch_check(c, __func__));
     return BPPO_OK;
 }
 
@@ -1664,12 +1669,12 @@ bppo_status launch_adam(bppo_ctx *c, float lr, const float *c1, const float *c2,
     if (nb == a.nt && metric_dst) {       // one chunk per tensor: fused
         hipLaunchKernelGGL(k_adam1, dim3(nb), dim3(ADAM1_THREADS), 0, c->stream, a, c->d_grad + c->net.n_params,
                            c->d_mb_cur, nm, metric_dst);
-        BPPO_HIP(c, hipGetLastError());
+        TRY(launch_check(c, __func__));
         return BPPO_OK;
     }
     hipLaunchKernelGGL(k_adam_norm, dim3(nb), dim3(256), 0, c->stream, a);
     hipLaunchKernelGGL(k_adam, dim3(nb), dim3(256), 0, c->stream, a);
-    BPPO_HIP(c, hipGetLastError());
+    TRY(launch_check(c, __func__));
     if (metric_dst) return launch_metric_row(c, metric_dst, nm);
     return BPPO_OK;
 }
@@ -1679,6 +1684,7 @@ bppo_status launch_adam(bppo_ctx *c, float lr, const float *c1, const float *c2,
 bppo_status launch_explained_variance(bppo_ctx *c, const float *valid) {
     const size_t n = (size_t)c->T * c->N;
     hipLaunchKernelGGL(k_ev, dim3(STAT_BLOCKS), dim3(256), 0, c->stream, n, c->d_val, c->d_ret, valid, c->d_red);
+    TRY(launch_check(c, __func__));
     BPPO_HIP(c, hipMemcpyAsync(c->h_red, c->d_red, sizeof(double) * 4 * STAT_BLOCKS,
                                hipMemcpyDeviceToHost, c->stream));
     return BPPO_OK;

@@ -24,12 +24,6 @@
 #include <cstring>
 #include <vector>
 
-#define TRY(x)                                 \
-    do {                                       \
-        bppo_status _s = (x);                  \
-        if (_s != BPPO_OK) return _s;          \
-    } while (0)
-
 namespace bppo {
 
 constexpr int OPP_MAX_MODELS = 15;
@@ -283,7 +277,7 @@ bppo_status opp_alloc(bppo_ctx *c) {
 
 bppo_status opp_rollout_begin(bppo_ctx *c, uint64_t base) {
     hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(1), 0, c->stream, c->d_rngpos, base);
-    BPPO_HIP(c, hipGetLastError());
+    TRY(launch_check(c, __func__));
     return BPPO_OK;
 }
 
@@ -294,7 +288,7 @@ bppo_status opp_step_group(bppo_ctx *c, int t) {
                                hipMemcpyDeviceToDevice, c->stream));
     hipLaunchKernelGGL(k_opp_group, dim3(1), dim3(OG_THREADS), 0, c->stream, c->N, c->n_opp, c->Pa, c->opp_K + 1,
                        c->d_players + r0, c->d_lpos, c->d_p2o, c->d_group, c->d_gpos, c->d_gbase, c->d_err);
-    BPPO_HIP(c, hipGetLastError());
+    TRY(launch_check(c, __func__));
     // the per-model row counts size the opponents' GEMMs: one small read per step
     BPPO_HIP(c, hipMemcpyAsync(c->h_gbase, c->d_gbase, sizeof(int32_t) * (c->opp_K + 2), hipMemcpyDeviceToHost,
                                c->stream));
@@ -312,7 +306,7 @@ bppo_status opp_step_forwards(bppo_ctx *c) {
         const size_t n = (size_t)c->N * c->L;
         hipLaunchKernelGGL(k_opp_sort_rows, dim3((unsigned)std::min<size_t>((n + 255) / 256, 8192)), dim3(256), 0,
                            c->stream, c->N, c->L, c->d_group, c->d_gpos, c->d_oraw, c->d_oxc);
-        BPPO_HIP(c, hipGetLastError());
+        TRY(launch_check(c, __func__));
     }
     for (int k = 0; k < c->opp_K; k++) {
         const int r0 = gb[k + 1], rows = gb[k + 2] - gb[k + 1];
@@ -325,7 +319,7 @@ bppo_status opp_step_forwards(bppo_ctx *c) {
     const int n = c->N * c->A;
     hipLaunchKernelGGL(k_opp_select, dim3((n + 255) / 256), dim3(256), 0, c->stream, c->N, c->A, c->d_group,
                        c->d_gpos, c->d_ologits, c->d_logits);
-    BPPO_HIP(c, hipGetLastError());
+    TRY(launch_check(c, __func__));
     return BPPO_OK;
 }
 
@@ -334,7 +328,7 @@ bppo_status opp_step_seats(bppo_ctx *c, int t) {
     hipLaunchKernelGGL(k_opp_seats, dim3(1), dim3(SEAT_THREADS), 0, c->stream, c->N, c->n_opp, c->Pa, c->A, c->d_done + r0,
                        c->d_players + r0, c->rng_key, (uint64_t)c->cfg.rng_stream, c->d_curopp, c->d_rngpos,
                        c->d_lpos, c->d_p2o, c->d_valid + r0);
-    BPPO_HIP(c, hipGetLastError());
+    TRY(launch_check(c, __func__));
     return BPPO_OK;
 }
 
@@ -359,7 +353,7 @@ bppo_status opp_compact_valid(bppo_ctx *c) {
 
 bppo_status opp_map_perm(bppo_ctx *c, uint32_t n) {
     hipLaunchKernelGGL(k_map_perm, dim3((n + 255) / 256), dim3(256), 0, c->stream, n, c->d_vidx, c->d_perm);
-    BPPO_HIP(c, hipGetLastError());
+    TRY(launch_check(c, __func__));
     return BPPO_OK;
 }
 

@@ -412,10 +412,27 @@ bool ShuffleEngine::epoch_ready(int slot, int e) {
     return slot_valid[slot] && ready[slot] > e;
 }
 
-void ShuffleEngine::release(int slot, hipStream_t st) {
-    (void)hipEventRecord(consumed[slot], st);
+hipError_t ShuffleEngine::release(int slot, hipStream_t st) {
+    const hipError_t e = hipEventRecord(consumed[slot], st);
+    if (e != hipSuccess) return e;
     std::lock_guard<std::mutex> lk(mu);
     consumed_used[slot] = true;
+    return hipSuccess;
+}
+
+void ShuffleEngine::hip_note(hipError_t e, const char *what) {
+    if (e == hipSuccess) return;
+    (void)hipGetLastError();                         // this thread's slot: reported here
+    std::lock_guard<std::mutex> lk(hip_mu);
+    if (hip_bad.load(std::memory_order_relaxed)) return;
+    hip_msg = std::string("shuffle engine: ") + what + ": " + hipGetErrorString(e);
+    hip_bad.store(true, std::memory_order_release);
+}
+
+bool ShuffleEngine::failed(std::string &msg) const {
+    if (!hip_bad.load(std::memory_order_acquire)) return false;
+    msg = hip_msg;
+    return true;
 }
 
 // words [pos, pos + len) of word buffer b (one checkpoint piece: never crosses a
@@ -431,7 +448,7 @@ const uint32_t *ShuffleEngine::words(int b, uint64_t pos, uint64_t len, std::vec
             // a chunk the producers have not reached yet: the walk makes this piece
             // itself (ChaCha12, ~0.3 ns/word) rather than waiting for them
             if (w.ok[c].load(std::memory_order_acquire)) return w.h + o;
-            if (w.gpu && hipEventQuery(w.ev[c]) == hipSuccess) {   // written by the GPU
+            if (w.gpu && event_query(w.ev[c]) == hipSuccess) {   // written by the GPU
                 w.ok[c].store(1, std::memory_order_release);
                 return w.h + o;
             }
@@ -518,9 +535,12 @@ void ShuffleEngine::worker(int i) {
     // 2's, ..., the next job's carry set last (16 CPUs run ~K (E + 1) walks; the
     // scheduler otherwise shares them evenly and delays the walk needed first)
     {
-        // frontier scheduling keeps few walks alive at once: one niceness (1) for all
+        // frontier scheduling keeps few walks alive at once: one niceness (1) for all;
+        // so do windowed jobs, whose epochs are all needed within the same update (a
+        // graded niceness, up to 19, starved the later epochs' walks on a node where
+        // other ranks' threads run at normal priority)
         const int g = i < ncur ? i / std::max(K, 1) : std::max(epochs - C, 0);
-        const int nv = fr_depth > 0 ? 1 : 3 * g;
+        const int nv = (fr_depth > 0 || win) ? 1 : 3 * g;
         if (nv > 0) (void)setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), std::min(19, nv));
     }
     std::vector<uint32_t> scratch;
@@ -710,7 +730,7 @@ void ShuffleEngine::run() {
             start = slot_start[slot];
             wait_consumed = consumed_used[slot];
         }
-        if (wait_consumed) (void)hipStreamWaitEvent(copy, consumed[slot], 0);
+        if (wait_consumed) hip_note(hipStreamWaitEvent(copy, consumed[slot], 0), "hipStreamWaitEvent");
         seq++;
         if (win) {
             const bool ok = run_windowed(slot, start);
@@ -777,6 +797,7 @@ void ShuffleEngine::run() {
             const WordBuf::Region &R = W.reg[g];
             hipLaunchKernelGGL(k_chacha_words, dim3((unsigned)((R.len / 16 + 255) / 256)), dim3(256), 0, copy, key,
                                stream, R.base, R.len, W.d + R.off);
+            hip_note(hipGetLastError(), "k_chacha_words launch");
             for (uint64_t o = 0; o < R.len; o += SHUF_CHUNK) {
                 const size_t c = (size_t)((R.off + o) / SHUF_CHUNK);
                 W.ok[c] = 0;
@@ -837,7 +858,7 @@ void ShuffleEngine::run() {
         std::vector<std::pair<uint64_t, uint32_t>> tck;
         for (int e = 0; e < epochs && !cancelled; e++) {
             auto t0 = std::chrono::steady_clock::now();
-            if (ev_used[slot][e]) (void)hipEventSynchronize(ev[slot][e]);   // previous upload of this buffer
+            if (ev_used[slot][e]) hip_note(hipEventSynchronize(ev[slot][e]), "hipEventSynchronize");   // previous upload of this buffer
             uint32_t r = n;
             int met = -1, walked = 0;
             int s0 = 0, s1 = 0;                        // candidate speculative walks for this epoch
@@ -1004,8 +1025,8 @@ void ShuffleEngine::run() {
             if (overflow) {   // never at sane sizes: fall back to the sequential walk of the epoch
                 std::vector<uint32_t> Jh(n);
                 const uint64_t e0 = shuffle_walk_host(key, stream, tck.front().first, n, Jh.data());
-                (void)hipMemcpyAsync(d_J[slot] + (size_t)e * n, Jh.data(), 4ull * n, hipMemcpyHostToDevice, copy);
-                (void)hipStreamSynchronize(copy);
+                hip_note(hipMemcpyAsync(d_J[slot] + (size_t)e * n, Jh.data(), 4ull * n, hipMemcpyHostToDevice, copy), "hipMemcpyAsync");
+                hip_note(hipStreamSynchronize(copy), "hipStreamSynchronize");
                 pos = e0;
             } else {
                 WordRegions wr{};
@@ -1017,13 +1038,14 @@ void ShuffleEngine::run() {
                         wr.n++;
                     }
                 Seg *dS = d_seg[slot] + (size_t)e * maxseg;
-                (void)hipMemcpyAsync(dS, S, sizeof(Seg) * (size_t)std::max(ns, 1), hipMemcpyHostToDevice, copy);
+                hip_note(hipMemcpyAsync(dS, S, sizeof(Seg) * (size_t)std::max(ns, 1), hipMemcpyHostToDevice, copy), "hipMemcpyAsync");
                 hipLaunchKernelGGL(k_expand_J, dim3((unsigned)((std::max(ns, 1) + XJ_WAVES - 1) / XJ_WAVES)),
                                    dim3(64 * XJ_WAVES), 0, copy, key, stream, (const Seg *)dS, ns, wr,
                                    d_J[slot] + (size_t)e * n);
+                hip_note(hipGetLastError(), "k_expand_J launch");
             }
             end_pos[slot][e] = pos;
-            (void)hipEventRecord(ev[slot][e], copy);
+            hip_note(hipEventRecord(ev[slot][e], copy), "hipEventRecord");
             ev_used[slot][e] = true;
             walk_ms[slot][e] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
             SHUF_LOG("[shuf] epoch %d end=%llu met=%d segs=%d (%.2f ms)\n", e, (unsigned long long)pos,
@@ -1096,13 +1118,14 @@ bool ShuffleEngine::run_windowed(int slot, uint64_t start) {
         for (int e = 0; e < epochs; e++)
             hipLaunchKernelGGL(k_chacha_words, dim3((unsigned)((B.reg[e].len / 16 + 255) / 256)), dim3(256), 0, copy,
                                key, stream, B.reg[e].base, B.reg[e].len, B.d + B.reg[e].off);
+        hip_note(hipGetLastError(), "k_chacha_words launch");
         if (B.gpu) {
-            (void)hipEventRecord(words_made, copy);
-            (void)hipStreamWaitEvent(d2h, words_made, 0);
+            hip_note(hipEventRecord(words_made, copy), "hipEventRecord");
+            hip_note(hipStreamWaitEvent(d2h, words_made, 0), "hipStreamWaitEvent");
             for (size_t c : order) {
                 const uint64_t o = c * SHUF_CHUNK;
-                (void)hipMemcpyAsync(B.h + o, B.d + o, SHUF_CHUNK * 4, hipMemcpyDeviceToHost, d2h);
-                (void)hipEventRecord(B.ev[c], d2h);
+                hip_note(hipMemcpyAsync(B.h + o, B.d + o, SHUF_CHUNK * 4, hipMemcpyDeviceToHost, d2h), "hipMemcpyAsync");
+                hip_note(hipEventRecord(B.ev[c], d2h), "hipEventRecord");
             }
         }
         B.made_for = s0;
@@ -1133,7 +1156,7 @@ bool ShuffleEngine::run_windowed(int slot, uint64_t start) {
     cv.notify_all();
     for (int e = 0; e < epochs; e++) {
         const auto t0 = std::chrono::steady_clock::now();
-        if (ev_used[slot][e]) (void)hipEventSynchronize(ev[slot][e]);   // previous upload of this buffer
+        if (ev_used[slot][e]) hip_note(hipEventSynchronize(ev[slot][e]), "hipEventSynchronize");   // previous upload of this buffer
         SpecWalk &w = spec[e];
         {
             std::unique_lock<std::mutex> lk(mu);
@@ -1160,20 +1183,21 @@ bool ShuffleEngine::run_windowed(int slot, uint64_t start) {
         if (overflow) {   // never at sane sizes: the sequential walk of the epoch
             std::vector<uint32_t> Jh(n);
             (void)shuffle_walk_host(key, stream, p0, n, Jh.data());
-            (void)hipMemcpyAsync(d_J[slot] + (size_t)e * n, Jh.data(), 4ull * n, hipMemcpyHostToDevice, copy);
-            (void)hipStreamSynchronize(copy);
+            hip_note(hipMemcpyAsync(d_J[slot] + (size_t)e * n, Jh.data(), 4ull * n, hipMemcpyHostToDevice, copy), "hipMemcpyAsync");
+            hip_note(hipStreamSynchronize(copy), "hipStreamSynchronize");
         } else {
             WordRegions wr{};
             wr.ptr[0] = W.d + W.reg[e].off; wr.base[0] = W.reg[e].base; wr.len[0] = W.reg[e].len; wr.n = 1;
             Seg *dS = d_seg[slot] + (size_t)e * maxseg;
-            (void)hipMemcpyAsync(dS, S, sizeof(Seg) * (size_t)std::max(ns, 1), hipMemcpyHostToDevice, copy);
+            hip_note(hipMemcpyAsync(dS, S, sizeof(Seg) * (size_t)std::max(ns, 1), hipMemcpyHostToDevice, copy), "hipMemcpyAsync");
             hipLaunchKernelGGL(k_expand_J, dim3((unsigned)((std::max(ns, 1) + XJ_WAVES - 1) / XJ_WAVES)),
                                dim3(64 * XJ_WAVES), 0, copy, key, stream, (const Seg *)dS, ns, wr,
                                d_J[slot] + (size_t)e * n);
+            hip_note(hipGetLastError(), "k_expand_J launch");
         }
         end_pos[slot][e] = pend;
         coalesced[slot][e] = -1;
-        (void)hipEventRecord(ev[slot][e], copy);
+        hip_note(hipEventRecord(ev[slot][e], copy), "hipEventRecord");
         ev_used[slot][e] = true;
         walk_ms[slot][e] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         {

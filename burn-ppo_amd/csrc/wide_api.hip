@@ -247,15 +247,19 @@ bppo_status wide_bootstrap_gae(bppo_ctx *c) {
     WTRY(popart_denorm(c, c->d_values, (size_t)N));    // main.rs:898-907
     WHIP(c, wide_boot_lvpp(c->stream, N, c->P, c->d_values, c->d_bplayers, c->d_lvpp));
     WHIP(c, hipMemcpyAsync(c->d_last_v, c->d_values, sizeof(float) * N, hipMemcpyDeviceToDevice, c->stream));
+    hipError_t he = hipSuccess;
     if (c->P == 1) {   // CartPole on this path: main.rs:928-946 dispatches single-player to compute_gae
         bppo_status s1 = launch_gae_1p(c->d_rew, c->d_done, c->d_val, c->d_last_v, c->T, N, (float)c->cfg.gamma,
-                                       (float)c->cfg.gae_lambda, c->d_adv, c->d_ret, c->stream);
-        if (s1 != BPPO_OK) c->err = "GAE launch failed";
+                                       (float)c->cfg.gae_lambda, c->d_adv, c->d_ret, c->stream, nullptr, nullptr, &he);
+        if (s1 != BPPO_OK) return he != hipSuccess ? hip_fail(c, he, "k_gae_1p launch") : s1;
         return s1;
     }
     bppo_status s = launch_gae_mp(c->d_allr, c->d_players, c->d_done, c->d_val, c->d_lvpp, c->T, N, c->P,
-                                  (float)c->cfg.gamma, (float)c->cfg.gae_lambda, c->d_adv, c->d_ret, c->stream);
-    if (s != BPPO_OK) c->err = "multiplayer GAE launch failed";
+                                  (float)c->cfg.gamma, (float)c->cfg.gae_lambda, c->d_adv, c->d_ret, c->stream, &he);
+    if (s != BPPO_OK) {
+        if (he != hipSuccess) return hip_fail(c, he, "k_gae_mp launch");
+        c->err = "multiplayer GAE: unsupported player count";
+    }
     return s;
 }
 

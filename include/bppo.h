@@ -208,8 +208,9 @@ bppo_status bppo_train_step(bppo_ctx *ctx, double lr, double ent_coef, bppo_roll
  * the envs are past it): it stays the context's next rollout, which bppo_collect_rollouts,
  * bppo_train_step and bppo_train_steps use instead of drawing another one (bppo_compute_gae
  * consumes it too).  A setter of the state it was drawn with (bppo_params_set,
- * bppo_optimizer_set, bppo_rng_set / _from_seed, bppo_obs_norm_set, bppo_ret_norm_set,
- * bppo_popart_set, bppo_vecenv_reset) discards it; the next rollout is then drawn anew.
+ * bppo_rng_set / _from_seed, bppo_obs_norm_set, bppo_ret_norm_set, bppo_popart_set,
+ * bppo_vecenv_reset) discards it; the next rollout is then drawn anew (bppo_optimizer_set
+ * keeps it: a rollout does not read the Adam moments).
  * infos / ms: n entries each (may be NULL); phase_keys (bppo_last_kernel_ms names, nkeys of
  * them): per-key sums over the n iterations into phase_sums */
 bppo_status bppo_train_steps(bppo_ctx *ctx, int32_t n, const double *lr, const double *ent_coef,
@@ -301,6 +302,15 @@ bppo_status bppo_gae_mp_device(const float *all_rewards, const int32_t *players,
  * over the buffer, on a host thread from device->host copies made beside the update
  * (it waits for them at the update's end: ~10 ms of one CPU per 8.4 M rows) */
 bppo_status bppo_set_explained_variance_mode(bppo_ctx *ctx, int32_t mode);
+
+/* which minibatch kernel runs (a parity / A-B hook; it has an effect only where a
+ * split-bf16 kernel exists: the 2x64 relu MLP of CfgB).  mode 0 (default): the update's
+ * first minibatch on the exact f32 kernel (it runs with the rollout's parameters, so the
+ * ratio is exactly 1 and the forward equals the rollout's bit for bit), every later one on
+ * the f32-accurate split-bf16 kernel; 1: the exact kernel for every minibatch; 2: the split
+ * kernel for every minibatch, the first included (its gradient from the rollout's parameters
+ * can then be compared with the oracle's, tests/test_gpu_split_kernel.py) */
+bppo_status bppo_set_minibatch_kernel(bppo_ctx *ctx, int32_t mode);
 
 /* device timing of the last call of each phase kernel (ms), for bench.py's roofline */
 bppo_status bppo_last_kernel_ms(bppo_ctx *ctx, const char *kernel, float *ms);

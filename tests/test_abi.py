@@ -143,3 +143,18 @@ def test_create_rejects_nets_over_16_layers_before_any_hip_call(so, preset, over
         assert b"16 layers" in L.lib().bppo_last_error(h)
     finally:
         L.lib().bppo_destroy(h)
+
+
+def test_null_context_is_an_argument_error(so):
+    """every setter checks its context before touching it (bppo_optimizer_set
+    dereferenced a NULL ctx); no HIP call is made, so this runs without a GPU."""
+    import bppo._lib as L
+    lib = L.lib()
+    buf = (C.c_float * 4)()
+    steps = (C.c_int32 * 4)()
+    assert lib.bppo_optimizer_set(None, buf, buf, steps, 4) == L.ERR_ARG
+    assert lib.bppo_optimizer_get(None, buf, buf, steps, 4) == L.ERR_ARG
+    assert lib.bppo_params_set(None, buf, 4) == L.ERR_ARG
+    assert lib.bppo_rng_set(None, 0) == L.ERR_ARG
+    assert lib.bppo_set_explained_variance_mode(None, 1) == L.ERR_ARG
+    assert lib.bppo_set_minibatch_kernel(None, 2) == L.ERR_ARG

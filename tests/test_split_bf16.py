@@ -3,8 +3,10 @@ every f32 operand x is split exactly into three bf16 pieces x = x0 + x1 + x2 (ea
 rounded to nearest even, as v_cvt_pk_bf16_f32 does), and a product x*y is taken as the
 six piece products of order <= 2 (x0y0, x0y1, x1y0, x0y2, x1y1, x2y0), each exact in
 f32, accumulated in f32.  Host emulation (numpy, no GPU): the split is exact for normal
-f32 values, and the six-product sum is within ~2^-24 of the true product, i.e. as
-accurate as an f32 multiply."""
+f32 values; |x1| <= 2^-8 |x| and |x2| <= 2^-16 |x|, so each dropped product (x1y2, x2y1,
+x2y2) is at most 2^-24 |xy| and the three together at most (2^-23 + 2^-32) |xy|; with the
+f32 additions the six-product sum is within 2^-22 of the true product.  The hardware's
+own accumulation is checked on the GPU against the oracle (tests/test_gpu_split_kernel.py)."""
 import numpy as np
 
 
@@ -43,6 +45,13 @@ def test_six_products_match_f32_multiply():
     ya, yb, yc = split3(y)
     # the piece products are exact in f32 (8 x 8 significant bits); the kernel adds them in f32
     terms = [xc * ya, xb * yb, xa * yc, xb * ya, xa * yb, xa * ya]
+    # the dropped products, in f64 (exact): the stated bound
+    ax, ay = np.abs(x.astype(np.float64)), np.abs(y.astype(np.float64))
+    assert np.all(np.abs(xb.astype(np.float64)) <= 2.0 ** -8 * ax)
+    assert np.all(np.abs(xc.astype(np.float64)) <= 2.0 ** -16 * ax)
+    dropped = (np.abs(xb.astype(np.float64) * yc) + np.abs(xc.astype(np.float64) * yb)
+               + np.abs(xc.astype(np.float64) * yc))
+    assert np.all(dropped <= (2.0 ** -23 + 2.0 ** -32) * ax * ay)
     s = np.zeros(n, np.float32)
     for t in terms:
         s = (s + t.astype(np.float32)).astype(np.float32)
