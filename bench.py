@@ -431,7 +431,8 @@ def main():
     mb_ex = phase["minibatch_kernel_exact"] / args.steps
     mb_min, mb_max = phase["minibatch_kernel_min"] / args.steps, phase["minibatch_kernel_max"] / args.steps
     flop = mb_rows * FLOP_PER_ROW_FWD_BWD
-    achieved = flop / (mb_ms * 1e-3) / 1e12
+    # (no timed launches, BPPO_MB_EVENTS=0 diagnostic runs: no roofline figure)
+    achieved = flop / (mb_ms * 1e-3) / 1e12 if mb_ms > 0 else 0.0
     cfgB = (N == 65536 and T == 128)
     kname = "k_minibatch_split" if phase["minibatch_kernel_split"] > 0 else "k_minibatch_mfma"
     mb_tr, mb_src = traffic_for(kname, "k_update.hip") if cfgB else (None, "not the profiled shape")
@@ -492,6 +493,11 @@ def main():
            "host_cpu_ms_per_step_by_thread": host_cpu_threads,
            "roofline": roof, "gae_roofline": gae_roof,
            "phase_ms_per_update": {k: round(v / args.steps, 3) for k, v in phase.items()},
+           # the reference's perf/* scalars (main.rs:1092-1132) over the timed interval: the
+           # job's env steps per second and the phases' summed device seconds (rollout = the
+           # rollout kernels + return normalizer; gae = GAE; update = the PPO update)
+           "perf": {k: round(v, 6) for k, v in bppo.perf_scalars(
+               env_steps, dt, phase["rollout"] + phase["return_norm"], phase["gae"], phase["update"]).items()},
            "last_update": {k: (round(v, 5) if isinstance(v, float) else v) for k, v in last.items()
                            if k in ("policy_loss", "value_loss", "entropy", "approx_kl", "mean_return",
                                     "episodes", "explained_variance")},

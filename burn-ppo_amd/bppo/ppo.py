@@ -373,6 +373,23 @@ def train_step(ctx, learning_rate, entropy_coef):
     return info, _metrics_dict(m)
 
 
+def perf_scalars(env_steps, seconds, rollout_ms, gae_ms, update_ms):
+    """The reference's perf/* scalars (main.rs:1092-1132) over one logging interval:
+    perf/sps = env steps / wall seconds, perf/{rollout,gae,update}_time = the phases' summed
+    seconds, perf/{rollout,update}_pct of their sum.  The phase times here are the device
+    times of the phases (HIP events on the context's stream; the reference times its host
+    calls, which on the device path only enqueue), so the reference's dashboards read the
+    same names with the same meaning."""
+    r, g, u = rollout_ms * 1e-3, gae_ms * 1e-3, update_ms * 1e-3
+    tot = r + g + u
+    out = {"perf/sps": env_steps / seconds if seconds > 0 else 0.0, "perf/rollout_time": r, "perf/gae_time": g,
+           "perf/update_time": u}
+    if tot > 0:
+        out["perf/rollout_pct"] = r / tot * 100.0
+        out["perf/update_pct"] = u / tot * 100.0
+    return out
+
+
 class Trainer:
     """run_training's per-update loop body (main.rs:684-988) on one GPU (or one
     rank of a data-parallel job)."""

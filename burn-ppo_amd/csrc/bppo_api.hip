@@ -1070,31 +1070,35 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
         for (int mb = 0; mb < M; mb++) {
             const size_t sz = base_mb + ((size_t)mb < rem ? 1 : 0);
             if (sz == 0) continue;
-            BPPO_HIP(c, hipEventRecord(c->ev[TM_FWDBWD][0], c->stream));
+            // the "minibatch" phase time is the last minibatch's (read after the update in the
+            // deferred path): only that one is bracketed there -- each timestamp marker on the
+            // stream costs a few us of idle compute stream
+            const bool fw_timed = !deferred || (ep == c->cfg.num_epochs - 1 && mb == M - 1);
+            if (fw_timed) BPPO_HIP(c, hipEventRecord(c->ev[TM_FWDBWD][0], c->stream));
             c->d_mb_cur = c->d_mb_stats + 4 * mb;
-            if (c->wide) {
-                TRY(wide_minibatch(c, (uint32_t)start, (uint32_t)sz, (float)ent_coef));
-            } else {
-                TRY(launch_minibatch(c, (uint32_t)start, (uint32_t)sz, (float)ent_coef, first_mb));
-            }
-            BPPO_HIP(c, hipEventRecord(c->ev[TM_FWDBWD][1], c->stream));
-            first_mb = false;
-            if (c->allreduce && c->world > 1) {
-                if (!c->allreduce_async) BPPO_HIP(c, sync_stream(c));
-                if (c->allreduce(c->d_grad, (size_t)np + NM, c->allreduce_user) != 0) {
-                    c->err = "all-reduce callback failed";
-                    return BPPO_ERR_COMM;
-                }
-            }
+            // Adam's bias corrections for this step (burn-optim: per tensor, f32 powers)
             float c1[64], c2[64];
             for (int t = 0; t < 2 * c->net.n_layers; t++) {
                 int ti = ++c->adam_t[t];
                 c1[t] = 1.0f - powi_f32(0.9f, ti);
                 c2[t] = 1.0f - powi_f32(0.999f, ti);
             }
+            float *metric_dst = c->d_rows + (size_t)nrow * (NM + 4);
+            const bool multi = c->allreduce && c->world > 1;
+            if (c->wide) TRY(wide_minibatch(c, (uint32_t)start, (uint32_t)sz, ent_coef));
+            else TRY(launch_minibatch(c, (uint32_t)start, (uint32_t)sz, (float)ent_coef, first_mb));
+            if (fw_timed) BPPO_HIP(c, hipEventRecord(c->ev[TM_FWDBWD][1], c->stream));
+            first_mb = false;
+            if (multi) {
+                if (!c->allreduce_async) BPPO_HIP(c, sync_stream(c));
+                if (c->allreduce(c->d_grad, (size_t)np + NM, c->allreduce_user) != 0) {
+                    c->err = "all-reduce callback failed";
+                    return BPPO_ERR_COMM;
+                }
+            }
             // clip + Adam; the metric row (grad[np .. np+NM) and adv stats) into the
             // update's device rows
-            TRY(launch_adam(c, (float)lr, c1, c2, c->d_rows + (size_t)nrow * (NM + 4), NM));
+            TRY(launch_adam(c, (float)lr, c1, c2, metric_dst, NM));
             if (c->wide) TRY(wide_pack(c));
             nrow++;
             if (!deferred) {
@@ -1194,6 +1198,7 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
         c->mb_k_split = kn[1] ? (float)(ks[1] / kn[1]) : 0.0f;
         c->mb_ev_n = 0;
     }
+    c->mb_launch = 0;
     c->last_ms[TM_FWDBWD] = fw_ms;
     c->last_ms[TM_SHUFFLE] = sh_ms;
     c->last_rows = rows;

@@ -375,6 +375,7 @@ struct bppo_ctx {
     float *d_cnn_dy[2] = {nullptr, nullptr};
     float *d_cnn_wt = nullptr, *d_cnn_wd = nullptr, *d_cnn_owt = nullptr, *d_cnn_dwt = nullptr;
     size_t cnn_wt_off[2][4] = {};
+    size_t cnn_wd_off[2][4] = {};     // the input-gradient operands (taps padded, gemm_conv_tap_pad)
     int cnn_stacks = 1;
     // PopArt value normalization (popart.hip, normalization.rs:262-366): running
     // statistics on the host, normalized update buffers, the update's views
@@ -402,6 +403,7 @@ struct bppo_ctx {
     static constexpr int MB_EV = 64;
     hipEvent_t mb_ev[MB_EV][2] = {};
     int mb_ev_n = 0;
+    int mb_launch = 0;                // minibatch kernel launches of this update (mb_ev sampling)
     float mb_k_mean = 0.0f, mb_k_min = 0.0f, mb_k_max = 0.0f;
     bool mb_ev_split[MB_EV] = {};     // launch i ran k_minibatch_split (else the exact k_minibatch_mfma)
     float mb_k_split = 0.0f, mb_k_exact = 0.0f;   // mean of each kind's launches (0: none)
@@ -487,7 +489,16 @@ bppo_status cnn_alloc(bppo_ctx *c);
 void cnn_free(bppo_ctx *c);
 bppo_status cnn_pack(bppo_ctx *c, const float *params, float *wt, float *wd);
 bppo_status cnn_features(bppo_ctx *c, int s, int rows, const float *x, int ldx, const float *params, const float *wt);
-bppo_status cnn_backward(bppo_ctx *c, int s, int rows, const float *x, int ldx, float *dF, float *grad);
+bppo_status cnn_backward(bppo_ctx *c, int s, int rows, const float *x, int ldx, float *dF, float *grad, int exact);
+// how the wide path sums its weight gradients (gemm_wgrad's `exact`): 0 f32 split-K MFMA
+// chains; 1 f64 products and sums on the f64 MFMA (k_gemm_wg64), the CNN default: an f32 chain
+// over a conv layer's B*42 positions leaves the parameters ~1 ulp off the oracle's after each
+// Adam step, which the PPO loss amplifies; 2 the oracle's row-ordered f64 sums (k_wg_seq,
+// bppo_set_minibatch_kernel 1: the reference-exact parity mode)
+inline int wide_exact_grad(const bppo_ctx *c) {
+    if (c->mb_kernel == 1) return 2;
+    return c->mb_kernel == 0 && c->net.n_conv > 0 ? 1 : 0;
+}
 // opponent pool (opponents.hip)
 bool opp_active(const bppo_ctx *c);
 bppo_status opp_alloc(bppo_ctx *c);
@@ -501,7 +512,7 @@ bppo_status opp_compact_valid(bppo_ctx *c);
 bppo_status opp_map_perm(bppo_ctx *c, uint32_t n);
 bppo_status wide_collect(bppo_ctx *c, uint64_t base);
 bppo_status wide_bootstrap_gae(bppo_ctx *c);
-bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_coef);
+bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, double ent_coef);
 bppo_status wide_observe_host(bppo_ctx *c, float *obs, int32_t *players, uint8_t *masks, float *priv);
 bppo_status wide_step_host(bppo_ctx *c, const int32_t *actions, float *obs, float *rewards, uint8_t *dones,
                            int32_t *n_eps);

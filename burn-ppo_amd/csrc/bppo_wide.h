@@ -63,6 +63,9 @@ struct LossArgs {
     float *dout;                    // [n][A+1]
     double *part;                   // [blocks][WM_COUNT]
     float lo, hi, ceps, inv_mb, ent_coef, value_coef;
+    // the gradient of the loss in f64, rounded once (the oracle's hand-written autodiff:
+    // inv = 1 / mb, entropy / value coefficients as the config's f64 values)
+    double inv_mb_d, ent_coef_d, value_coef_d;
     int clip_value;
 };
 

@@ -62,12 +62,13 @@ __global__ void k_cnn_transpose(int R, int Cc, const float *__restrict__ src, fl
     dst[(size_t)cc * R + r] = src[i];
 }
 
-// Burn conv weight [Co][Cin][kk] -> the transposed-conv operand Wd[ci][t*Co + co]
-__global__ void k_cnn_pack_dx(int Co, int Cin, int kk, const float *__restrict__ w, float *__restrict__ wd) {
+// Burn conv weight [Co][Cin][kk] -> the transposed-conv operand Wd[ci][t*cpad + co], the
+// padding channels co in [Co, cpad) zero
+__global__ void k_cnn_pack_dx(int Co, int Cin, int kk, int cpad, const float *__restrict__ w, float *__restrict__ wd) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= Co * Cin * kk) return;
+    if (i >= cpad * Cin * kk) return;
     const int co = i / (Cin * kk), r = i % (Cin * kk), ci = r / kk, t = r % kk;
-    wd[(size_t)ci * kk * Co + t * Co + co] = w[i];
+    wd[(size_t)ci * kk * cpad + t * cpad + co] = co < Co ? w[i] : 0.0f;
 }
 
 static dim3 grid_for(size_t n) { return dim3((unsigned)std::min<size_t>((n + 255) / 256, 65536)); }
@@ -75,7 +76,7 @@ static dim3 grid_for(size_t n) { return dim3((unsigned)std::min<size_t>((n + 255
 bppo_status cnn_alloc(bppo_ctx *c) {
     const NetLayout &n = c->net;
     const size_t HW = (size_t)n.H * n.W, R = (size_t)c->rows_max * HW;
-    size_t kmax = 0, cmax = 0, wt = 0;
+    size_t kmax = 0, cmax = 0, wt = 0, wd = 0;
     c->cnn_stacks = n.critic_fc0 > n.critic_first ? 2 : 1;
     for (int s = 0; s < c->cnn_stacks; s++) {
         for (int l = 0; l < n.n_conv; l++) {
@@ -83,6 +84,8 @@ bppo_status cnn_alloc(bppo_ctx *c) {
             cmax = std::max(cmax, (size_t)std::max(n.out[l], n.conv_cin[l]));
             c->cnn_wt_off[s][l] = wt;
             wt += (size_t)n.in[l] * n.out[l];
+            c->cnn_wd_off[s][l] = wd;
+            wd += (size_t)n.in[l] * gemm_conv_tap_pad(n.out[l]);   // Cin*kk*cpad
             CHIP(c, hipMalloc((void **)&c->d_cnn_y[s][l], R * n.out[l] * 4));
         }
         CHIP(c, hipMalloc((void **)&c->d_cnn_f[s], (size_t)c->rows_max * n.fdim * 4));
@@ -91,7 +94,7 @@ bppo_status cnn_alloc(bppo_ctx *c) {
     CHIP(c, hipMalloc((void **)&c->d_cnn_dy[0], dy * 4));
     CHIP(c, hipMalloc((void **)&c->d_cnn_dy[1], dy * 4));
     CHIP(c, hipMalloc((void **)&c->d_cnn_wt, wt * 4));
-    CHIP(c, hipMalloc((void **)&c->d_cnn_wd, wt * 4));
+    CHIP(c, hipMalloc((void **)&c->d_cnn_wd, wd * 4));
     CHIP(c, hipMalloc((void **)&c->d_cnn_owt, wt * 4));
     CHIP(c, hipMalloc((void **)&c->d_cnn_dwt, kmax * cmax * 4));
     return BPPO_OK;
@@ -117,9 +120,11 @@ bppo_status cnn_pack(bppo_ctx *c, const float *params, float *wt, float *wd) {
             const int R = n.out[l], Cc = n.in[l], lg = n.conv_base(s) + l;   // [Cout][K] -> [K][Cout]
             hipLaunchKernelGGL(k_cnn_transpose, dim3((R * Cc + 255) / 256), dim3(256), 0, c->stream, R, Cc,
                                params + n.w[lg], wt + c->cnn_wt_off[s][l]);
-            if (wd && l > 0)
-                hipLaunchKernelGGL(k_cnn_pack_dx, dim3((R * Cc + 255) / 256), dim3(256), 0, c->stream, R,
-                                   n.conv_cin[l], kk, params + n.w[lg], wd + c->cnn_wt_off[s][l]);
+            if (wd && l > 0) {
+                const int cpad = gemm_conv_tap_pad(R);
+                hipLaunchKernelGGL(k_cnn_pack_dx, dim3((cpad * Cc + 255) / 256), dim3(256), 0, c->stream, R,
+                                   n.conv_cin[l], kk, cpad, params + n.w[lg], wd + c->cnn_wd_off[s][l]);
+            }
         }
     CHIP(c, hipGetLastError());
     return BPPO_OK;
@@ -142,7 +147,7 @@ bppo_status cnn_features(bppo_ctx *c, int s, int rows, const float *x, int ldx, 
 // dF = dL/dF [rows][fdim] (relu' of the last conv already applied) -> conv weight
 // and bias gradients of stack s into grad (Burn layout); the activations of the last
 // cnn_features call of that stack on the same rows are reused
-bppo_status cnn_backward(bppo_ctx *c, int s, int rows, const float *x, int ldx, float *dF, float *grad) {
+bppo_status cnn_backward(bppo_ctx *c, int s, int rows, const float *x, int ldx, float *dF, float *grad, int exact) {
     const NetLayout &n = c->net;
     const int HW = n.H * n.W, M = rows * HW, last = n.n_conv - 1, l0 = n.conv_base(s);
     float *dy = c->d_cnn_dy[0], *dy2 = c->d_cnn_dy[1];
@@ -155,13 +160,13 @@ bppo_status cnn_backward(bppo_ctx *c, int s, int rows, const float *x, int ldx, 
         const float *src = l ? c->d_cnn_y[s][l - 1] : x;
         const int sp = gemm_wg_splits(K, Co, M);
         CHIP(c, gemm_conv_wgrad(c->stream, rows, Co, n.conv_cin[l], n.ksize, src, l ? 0 : ldx, dy, c->d_part,
-                                c->d_colsum, c->d_cnn_dwt, grad + n.b[l0 + l], sp));
+                                c->d_colsum, c->d_cnn_dwt, grad + n.b[l0 + l], sp, exact));
         hipLaunchKernelGGL(k_cnn_transpose, dim3((K * Co + 255) / 256), dim3(256), 0, c->stream, K, Co,
                            (const float *)c->d_cnn_dwt, grad + n.w[l0 + l]);
         CHIP(c, hipGetLastError());
         if (l == 0) break;
         // the input gradient straight into the previous layer's NHWC rows, relu' applied
-        CHIP(c, gemm_conv_dx(c->stream, rows, n.conv_cin[l], Co, n.ksize, dy, c->d_cnn_wd + c->cnn_wt_off[s][l],
+        CHIP(c, gemm_conv_dx(c->stream, rows, n.conv_cin[l], Co, n.ksize, dy, c->d_cnn_wd + c->cnn_wd_off[s][l],
                              c->d_cnn_y[s][l - 1], dy2));
         std::swap(dy, dy2);
     }

@@ -85,6 +85,7 @@ struct TileLoader {
 struct ConvA {
     int kind = 0;
     int cin = 0, ks = 1, pad = 0;   // channels of the gathered planes; kernel size; same padding
+    int cpad = 0;                   // kind 2: k's per tap (cin rounded up to GBK; the rest read 0)
     int obs = 0, ld = 0;            // kind 1 layer 0: src = observation rows, row stride ld
 };
 constexpr int CV_H = 6, CV_W = 7, CV_HW = CV_H * CV_W;
@@ -108,16 +109,17 @@ struct ConvLoader {
             const int t = fixed - ci * kk2, kh = t / cv.ks;
             dh = kh - cv.pad; dw = t - kh * cv.ks - cv.pad;
         } else {
-            const int tap = fixed / cv.cin, kh = tap / cv.ks;
-            ci = fixed - tap * cv.cin;
+            const int tap = fixed / cv.cpad, kh = tap / cv.ks;
+            ci = fixed - tap * cv.cpad;
             dh = cv.pad - kh; dw = cv.pad - (tap - kh * cv.ks);
         }
+        const bool cok = ci < cv.cin;   // kind 2: a tap's padding channels read 0
         int b = row / CV_HW, hw = row - b * CV_HW;
 #pragma unroll
         for (int e = 0; e < E; e++) {
             const int h = hw / CV_W + dh, w = hw % CV_W + dw;
             float x = 0.0f;
-            if (fok && row < rowmax && h >= 0 && h < CV_H && w >= 0 && w < CV_W) {
+            if (fok && cok && row < rowmax && h >= 0 && h < CV_H && w >= 0 && w < CV_W) {
                 const int hw2 = h * CV_W + w;
                 x = cv.obs ? src[(size_t)b * cv.ld + hw2 * cv.cin + ci] : src[((size_t)b * CV_HW + hw2) * cv.cin + ci];
             }
@@ -149,12 +151,33 @@ struct GemmArgs {
     // DX epilogue: activation derivative from the layer output H [M][ldh]
     // (nullptr: none): dact 1 relu mask [H > 0], 2 tanh (1 - H^2)
     const float *H; int ldh; int dact;
+    // DX, exact shared heads: + round(xa[row * ldxa] * xw[col]) after the chain (the value
+    // head's contribution added as the oracle / autodiff does: a separate rounded product)
+    const float *xa; int ldxa; const float *xw;
+    // DX of a convolution (AK = 2): the chain restarts every kblk k's (one tap's Co channels)
+    // and the finished taps are summed in tap order (the col2im gather's f32 adds); 0: off
+    int kblk;
     // WG: partial slab [split][M][N] and column sums [split][N]; rows of the
-    // reduction per split
+    // reduction per split (float, or double for k_gemm_wg64)
     float *part; float *colsum; int k_per_split;
+    int xcd;                     // XCD-aware tile order (tile_of)
 };
 
 enum { GEMM_FWD = 0, GEMM_DX = 1, GEMM_WG = 2 };
+
+// XCD-aware tile order.  The hardware deals blocks round-robin over the 8 XCDs (block b on
+// XCD b % 8), each with its own L2.  Dealt in grid order, the N-tiles of one row tile (which
+// read the same A rows) land on different XCDs and every XCD fetches those rows from HBM.
+// Remapped, XCD j runs the logical tiles [j T/8, (j+1) T/8): consecutive tiles -- the N-tiles
+// of a row tile, the tiles of one split -- share an L2.  g.xcd = 0: grid order.
+struct Tile { int x, y, z; };
+__device__ __forceinline__ Tile tile_of(int xcd) {
+    const unsigned gx = gridDim.x, gy = gridDim.y;
+    const unsigned total = gx * gy * gridDim.z;
+    unsigned b = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    if (xcd && total % 8 == 0) b = (b % 8) * (total / 8) + b / 8;
+    return Tile{(int)(b % gx), (int)((b / gx) % gy), (int)(b / (gx * gy))};
+}
 
 template <int MODE, int BM, int BN, int WM, int WN, int AK>
 __global__ void __launch_bounds__(256, 2) k_gemm(GemmArgs g) {
@@ -165,10 +188,11 @@ __global__ void __launch_bounds__(256, 2) k_gemm(GemmArgs g) {
     __shared__ float sB[2][GBK * S::BPAD];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WN, wn = wave % WN;
-    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+    const Tile tl = tile_of(g.xcd);
+    const int m0 = tl.y * BM, n0 = tl.x * BN;
     int kbeg = 0, kend = g.K;
     if constexpr (MODE == GEMM_WG) {
-        kbeg = blockIdx.z * g.k_per_split;
+        kbeg = tl.z * g.k_per_split;
         kend = min(g.K, kbeg + g.k_per_split);
     }
     // A: a plain operand, or (AK) the implicit convolution form g.cv
@@ -187,7 +211,7 @@ __global__ void __launch_bounds__(256, 2) k_gemm(GemmArgs g) {
             for (int r = 0; r < 16; r++) { acc[i][j][r] = 0.0f; tot[i][j][r] = 0.0f; }
     // bias-gradient column sums (WG, first row tile only): 256/BN threads per column
     float csum = 0.0f;
-    const bool do_colsum = MODE == GEMM_WG && g.colsum != nullptr && blockIdx.y == 0;
+    const bool do_colsum = MODE == GEMM_WG && g.colsum != nullptr && tl.y == 0;
 
     load_a(kbeg);
     lb.load(g.B, g.ldb, n0, g.N, kbeg, kend, tid);
@@ -220,6 +244,21 @@ __global__ void __launch_bounds__(256, 2) k_gemm(GemmArgs g) {
 #pragma unroll
                 for (int j = 0; j < S::TN; j++)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+        }
+        if constexpr (MODE == GEMM_DX && AK == 2) {
+            // conv input gradient: taps are padded to kblk (a multiple of GBK) k's, so a tap
+            // ends at a stage boundary: its chain is complete, add it to the tap sum
+            if (g.kblk > 0 && ((k0 + GBK) % g.kblk) == 0) {
+#pragma unroll
+                for (int i = 0; i < S::TM; i++)
+#pragma unroll
+                    for (int j = 0; j < S::TN; j++)
+#pragma unroll
+                        for (int q = 0; q < 16; q++) {
+                            tot[i][j][q] = __fadd_rn(tot[i][j][q], acc[i][j][q]);
+                            acc[i][j][q] = 0.0f;
+                        }
+            }
         }
         if constexpr (MODE == GEMM_FWD) {
             // matrixmultiply KC block boundary: the chain restarts from 0 and the
@@ -254,6 +293,16 @@ __global__ void __launch_bounds__(256, 2) k_gemm(GemmArgs g) {
                     for (int q = 0; q < 16; q++) acc[i][j][q] = __fadd_rn(tot[i][j][q], acc[i][j][q]);
         }
     }
+    if constexpr (MODE == GEMM_DX && AK == 2) {
+        if (g.kblk > 0) {        // every tap flushed (K is a multiple of kblk): the tap sum
+#pragma unroll
+            for (int i = 0; i < S::TM; i++)
+#pragma unroll
+                for (int j = 0; j < S::TN; j++)
+#pragma unroll
+                    for (int q = 0; q < 16; q++) acc[i][j][q] = __fadd_rn(tot[i][j][q], acc[i][j][q]);
+        }
+    }
     // ---- epilogue: C/D map col = lane&31, row = (q&3) + 8*(q>>2) + 4*(lane>>5)
     const int col_l = lane & 31, rq = 4 * (lane >> 5);
 #pragma unroll
@@ -272,6 +321,7 @@ __global__ void __launch_bounds__(256, 2) k_gemm(GemmArgs g) {
                     if (col < g.n0) g.out0[(size_t)row * g.ld0 + col] = v;
                     else g.out1[(size_t)row * g.ld1 + (col - g.n0)] = v;
                 } else if constexpr (MODE == GEMM_DX) {
+                    if (g.xa) v = __fadd_rn(v, __fmul_rn(g.xa[(size_t)row * g.ldxa], g.xw[col]));
                     if (g.H) {
                         const float hv = g.H[(size_t)row * g.ldh + col];
                         if (g.dact == 2) v = __fmul_rn(v, __fsub_rn(1.0f, __fmul_rn(hv, hv)));
@@ -279,7 +329,7 @@ __global__ void __launch_bounds__(256, 2) k_gemm(GemmArgs g) {
                     }
                     g.out0[(size_t)row * g.ld0 + col] = v;
                 } else {
-                    g.part[((size_t)blockIdx.z * g.M + row) * g.N + col] = v;
+                    g.part[((size_t)tl.z * g.M + row) * g.N + col] = v;
                 }
             }
         }
@@ -291,9 +341,170 @@ __global__ void __launch_bounds__(256, 2) k_gemm(GemmArgs g) {
             float s = 0.0f;
             for (int p = 0; p < 256 / BN; p++) s += red[tid + p * BN];
             const int col = n0 + tid;
-            if (col < g.N) g.colsum[(size_t)blockIdx.z * g.N + col] = s;
+            if (col < g.N) g.colsum[(size_t)tl.z * g.N + col] = s;
         }
     }
+}
+
+// ---- exact weight gradients: dW = X^T dZ on v_mfma_f64_16x16x4_f64 --------------
+// The oracle (and autodiff in f64) sums x * dz over the rows in f64: every product of
+// two f32 values is exact in f64, so the only rounding left is the f64 additions, and
+// the f32 result equals the oracle's except in the ~2^-29-rare case of an f64 sum within
+// its ordering error of an f32 rounding boundary.  The f32 MFMA accumulates in f32 over
+// each split's rows (tens of thousands for a conv layer): its last-bit differences, fed
+// through Adam, move the parameters off the oracle's by ~1 ulp, which the PPO loss then
+// amplifies (tests/test_gpu_cnn.py).  Same LDS staging and loaders as k_gemm (WG form:
+// A = X^T k-major, B = dZ k-major), f64 operands converted from the staged f32 values,
+// 16x16 f64 tiles (f64 C/D map: col = lane & 15, row = (lane >> 4) + 4 reg), f64
+// partial slabs [split][M][N] and f64 column sums, reduced in f64 and rounded once.
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+template <int BM, int BN, int AK>
+__global__ void __launch_bounds__(256, 2) k_gemm_wg64(GemmArgs g) {
+    constexpr int WM = 2, WN = 2, TM = BM / WM / 16, TN = BN / WN / 16;
+    constexpr int APAD = BM + 1, BPAD = BN + 1;
+    static_assert(TM >= 1 && TN >= 1, "wave tile >= 16x16");
+    __shared__ float sA[2][GBK * APAD];
+    __shared__ float sB[2][GBK * BPAD];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const Tile tl = tile_of(g.xcd);
+    const int m0 = tl.y * BM, n0 = tl.x * BN;
+    const int kbeg = tl.z * g.k_per_split, kend = min(g.K, kbeg + g.k_per_split);
+    typename std::conditional<AK != 0, ConvLoader<BM, false>, TileLoader<BM, false>>::type la;
+    TileLoader<BN, false> lb;
+    auto load_a = [&](int k) {
+        if constexpr (AK != 0) la.load(g.A, g.cv, m0, g.M, k, kend, tid);
+        else la.load(g.A, g.lda, m0, g.M, k, kend, tid);
+    };
+    f64x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) acc[i][j][r] = 0.0;
+    double csum = 0.0;
+    const bool do_colsum = g.colsum != nullptr && tl.y == 0;
+    load_a(kbeg);
+    lb.load(g.B, g.ldb, n0, g.N, kbeg, kend, tid);
+    la.store(sA[0], tid);
+    lb.store(sB[0], tid);
+    __syncthreads();
+    int buf = 0;
+    const int li = lane & 15, lk = lane >> 4;
+    for (int k0 = kbeg; k0 < kend; k0 += GBK) {
+        const bool more = k0 + GBK < kend;
+        if (more) {
+            load_a(k0 + GBK);
+            lb.load(g.B, g.ldb, n0, g.N, k0 + GBK, kend, tid);
+        }
+        if (do_colsum) {
+            const int c = tid % BN, part = tid / BN, np = 256 / BN;
+#pragma unroll 4
+            for (int k = part; k < GBK; k += np) csum += (double)sB[buf][k * BPAD + c];
+        }
+        const float *a = sA[buf], *b = sB[buf];
+#pragma unroll
+        for (int kk = 0; kk < GBK; kk += 4) {
+            double af[TM], bf[TN];
+#pragma unroll
+            for (int i = 0; i < TM; i++) af[i] = (double)a[(kk + lk) * APAD + (wm * TM + i) * 16 + li];
+#pragma unroll
+            for (int j = 0; j < TN; j++) bf[j] = (double)b[(kk + lk) * BPAD + (wn * TN + j) * 16 + li];
+#pragma unroll
+            for (int i = 0; i < TM; i++)
+#pragma unroll
+                for (int j = 0; j < TN; j++)
+                    acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
+        }
+        if (more) {
+            __syncthreads();
+            la.store(sA[buf ^ 1], tid);
+            lb.store(sB[buf ^ 1], tid);
+            __syncthreads();
+            buf ^= 1;
+        }
+    }
+    double *part = reinterpret_cast<double *>(g.part);
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++) {
+            const int col = n0 + (wn * TN + j) * 16 + li;
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int row = m0 + (wm * TM + i) * 16 + lk + 4 * r;
+                if (row < g.M && col < g.N) part[((size_t)tl.z * g.M + row) * g.N + col] = acc[i][j][r];
+            }
+        }
+    if (do_colsum) {
+        __shared__ double red[256];
+        red[tid] = csum;
+        __syncthreads();
+        if (tid < BN) {
+            double s = 0.0;
+            for (int p = 0; p < 256 / BN; p++) s += red[tid + p * BN];
+            const int col = n0 + tid;
+            if (col < g.N) reinterpret_cast<double *>(g.colsum)[(size_t)tl.z * g.N + col] = s;
+        }
+    }
+}
+
+// ---- reference-exact weight gradients (bppo_set_minibatch_kernel 1) --------------------
+// dW[k][o] = sum over the rows r IN ORDER of (double)X[r][k] * (double)dZ[r][o], one thread
+// per (k, o), rounded to f32 once: the oracle's linear_bwd loop (oracle/net.c) bit for bit
+// (each product of two f32 values is exact in f64, so the sequence of f64 additions is the
+// whole arithmetic).  Latency-bound (one dependent f64 add per row per thread): a parity
+// mode, for the sizes the tests run.  Threads of a wave take consecutive o (coalesced dZ
+// reads, the X element shared); column sums (bias gradients) the same way.
+struct SeqWg {
+    ConvA cv;
+    const float *X; int ldx;       // X [rows][Kin] (or the implicit im2col form cv)
+    const float *dZ; int ldz;      // dZ [rows][N]
+    int Kin, N, rows;
+    float *dW0; int ldw0; int n0;  // cols [0, n0) -> dW0 [Kin][ldw0], [n0, N) -> dW1 [Kin][ldw1]
+    float *dW1; int ldw1;
+    float *db0, *db1;              // column sums likewise (may be null)
+};
+__device__ __forceinline__ float conv_x(const ConvA &cv, const float *src, int row, int k) {
+    const int kk2 = cv.ks * cv.ks, ci = k / kk2, t = k - ci * kk2, kh = t / cv.ks;
+    const int b = row / CV_HW, hw = row - b * CV_HW;
+    const int h = hw / CV_W + kh - cv.pad, w = hw % CV_W + (t - kh * cv.ks) - cv.pad;
+    if (h < 0 || h >= CV_H || w < 0 || w >= CV_W) return 0.0f;
+    const int hw2 = h * CV_W + w;
+    return cv.obs ? src[(size_t)b * cv.ld + hw2 * cv.cin + ci] : src[((size_t)b * CV_HW + hw2) * cv.cin + ci];
+}
+__global__ void __launch_bounds__(256) k_wg_seq(SeqWg a) {
+    const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const size_t nw = (size_t)a.Kin * a.N;
+    if (t >= nw + (size_t)((a.db0 || a.db1) ? a.N : 0)) return;
+    const bool bias = t >= nw;
+    const int k = bias ? 0 : (int)(t / a.N), o = (int)(bias ? t - nw : t % a.N);
+    double s = 0.0;
+    if (bias) {
+        for (int r = 0; r < a.rows; r++) s += (double)a.dZ[(size_t)r * a.ldz + o];
+    } else if (a.cv.kind) {
+        for (int r = 0; r < a.rows; r++) s += (double)conv_x(a.cv, a.X, r, k) * (double)a.dZ[(size_t)r * a.ldz + o];
+    } else {
+        for (int r = 0; r < a.rows; r++) s += (double)a.X[(size_t)r * a.ldx + k] * (double)a.dZ[(size_t)r * a.ldz + o];
+    }
+    if (bias) {
+        float *d = o < a.n0 ? a.db0 : a.db1;
+        if (d) d[o < a.n0 ? o : o - a.n0] = (float)s;
+    } else if (o < a.n0) a.dW0[(size_t)k * a.ldw0 + o] = (float)s;
+    else a.dW1[(size_t)k * a.ldw1 + (o - a.n0)] = (float)s;
+}
+
+// the f64 partials in split order, rounded to f32 once
+__global__ void k_split_reduce64(const double *__restrict__ part, int splits, int M, int N, int n0,
+                                 float *out0, int ld0, float *out1, int ld1) {
+    const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= (size_t)M * N) return;
+    double s = 0.0;
+    for (int k = 0; k < splits; k++) s += part[(size_t)k * M * N + i];
+    const int r = (int)(i / N), c = (int)(i % N);
+    if (c < n0) out0[(size_t)r * ld0 + c] = (float)s;
+    else out1[(size_t)r * ld1 + (c - n0)] = (float)s;
 }
 
 // fixed-order sum of the split partials: dst[r][c] = sum_s part[s][r][c] (f64),
@@ -329,11 +540,32 @@ static hipError_t tanh_inplace(hipStream_t st, float *y, int M, int cols, int ld
 }
 
 // -------------------------------------------------------------- launchers --
+// BPPO_GEMM_XCD=0: grid-order tiles (A/B of the XCD-aware order)
+static int gemm_xcd() {
+    static const int v = getenv("BPPO_GEMM_XCD") ? atoi(getenv("BPPO_GEMM_XCD")) : 1;
+    return v;
+}
 template <int MODE, int BM, int BN, int WM, int WN, int AK>
-static hipError_t launch(const GemmArgs &g, int splits, hipStream_t st) {
+static hipError_t launch(GemmArgs g, int splits, hipStream_t st) {
     dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, splits);
+    g.xcd = gemm_xcd();
     hipLaunchKernelGGL((k_gemm<MODE, BM, BN, WM, WN, AK>), grid, dim3(256), 0, st, g);
     return hipGetLastError();
+}
+
+template <int BM, int BN, int AK>
+static hipError_t launch64(GemmArgs g, int splits, hipStream_t st) {
+    dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, splits);
+    g.xcd = gemm_xcd();
+    hipLaunchKernelGGL((k_gemm_wg64<BM, BN, AK>), grid, dim3(256), 0, st, g);
+    return hipGetLastError();
+}
+// the same output tiling as launch_by_width, so gemm_wg_splits holds for both
+template <int AK = 0>
+static hipError_t launch64_by_width(const GemmArgs &g, int splits, hipStream_t st) {
+    if (g.N <= 32) return launch64<128, 32, AK>(g, splits, st);
+    if (g.N <= 64) return launch64<128, 64, AK>(g, splits, st);
+    return launch64<128, 128, AK>(g, splits, st);
 }
 
 template <int MODE, int AK = 0>
@@ -370,23 +602,31 @@ hipError_t gemm_conv_fwd(hipStream_t st, int rows, int Co, int Cin, int ks, cons
 }
 
 // conv input gradient (transposed taps): dX [rows*42][Cin] = (A_t(dY) Wd^T) * [H > 0],
-// Wd [Cin][ks*ks*Co] with Wd[ci][(kh*ks + kw)*Co + co] = weight[co][ci][kh][kw]
+// Wd [Cin][ks*ks*cpad] with Wd[ci][(kh*ks + kw)*cpad + co] = weight[co][ci][kh][kw] (zero for
+// co >= Co), cpad = gemm_conv_tap_pad(Co).  Each tap's chain over its channels is finished
+// and added to the tap sum in (kh, kw) order -- the oracle's per-tap dA chains and col2im
+// adds, bit for bit (the zero padding leaves a chain unchanged: fma(0, w, a) = a).
+int gemm_conv_tap_pad(int Co) { return (Co + GBK - 1) / GBK * GBK; }
 hipError_t gemm_conv_dx(hipStream_t st, int rows, int Cin, int Co, int ks, const float *dY, const float *Wd,
                         const float *H, float *out) {
     if (rows <= 0 || Cin <= 0) return hipSuccess;
+    const int cpad = gemm_conv_tap_pad(Co);
     GemmArgs g{};
-    g.cv.kind = 2; g.cv.cin = Co; g.cv.ks = ks; g.cv.pad = ks / 2;
-    g.A = dY; g.B = Wd; g.ldb = ks * ks * Co; g.M = rows * CV_HW; g.N = Cin; g.K = ks * ks * Co;
+    g.cv.kind = 2; g.cv.cin = Co; g.cv.ks = ks; g.cv.pad = ks / 2; g.cv.cpad = cpad;
+    g.A = dY; g.B = Wd; g.ldb = ks * ks * cpad; g.M = rows * CV_HW; g.N = Cin; g.K = ks * ks * cpad;
     g.H = H; g.ldh = Cin; g.dact = 1; g.out0 = out; g.ld0 = Cin; g.n0 = Cin;
+    g.kblk = cpad;
     return launch_by_width<GEMM_DX, 2>(g, 1, st);
 }
 
 hipError_t gemm_dx(hipStream_t st, int M, int N, int K, const float *dZ, int ldz, const float *W,
-                   int ldw, const float *H, int ldh, int act, float *out, int ldo) {
+                   int ldw, const float *H, int ldh, int act, float *out, int ldo, const float *xa, int ldxa,
+                   const float *xw) {
     if (M <= 0 || N <= 0) return hipSuccess;
     GemmArgs g{};
     g.A = dZ; g.lda = ldz; g.B = W; g.ldb = ldw; g.M = M; g.N = N; g.K = K;
     g.H = H; g.ldh = ldh; g.dact = act == 2 ? 2 : 1; g.out0 = out; g.ld0 = ldo; g.n0 = N;
+    g.xa = xa; g.ldxa = ldxa; g.xw = xw;
     return launch_by_width<GEMM_DX>(g, 1, st);
 }
 
@@ -402,44 +642,63 @@ int gemm_wg_splits(int Kin, int N, int rows) {
 
 static hipError_t wgrad(hipStream_t st, const ConvA &cv, int Kin, int N, int rows, const float *X, int ldx,
                         const float *dZ, int ldz, float *part, float *colsum, float *dW0, int ldw0, int n0,
-                        float *dW1, int ldw1, float *db0, float *db1, int splits);
+                        float *dW1, int ldw1, float *db0, float *db1, int splits, int exact);
 
 hipError_t gemm_wgrad(hipStream_t st, int Kin, int N, int rows, const float *X, int ldx, const float *dZ,
                       int ldz, float *part, float *colsum, float *dW0, int ldw0, int n0, float *dW1, int ldw1,
-                      float *db0, float *db1, int splits) {
-    return wgrad(st, ConvA{}, Kin, N, rows, X, ldx, dZ, ldz, part, colsum, dW0, ldw0, n0, dW1, ldw1, db0, db1, splits);
+                      float *db0, float *db1, int splits, int exact) {
+    return wgrad(st, ConvA{}, Kin, N, rows, X, ldx, dZ, ldz, part, colsum, dW0, ldw0, n0, dW1, ldw1, db0, db1, splits,
+                 exact);
 }
 
 // conv weight gradient (implicit im2col X): dWt [Cin*ks*ks][Co] = X(src)^T dY over rows*42 positions
 hipError_t gemm_conv_wgrad(hipStream_t st, int rows, int Co, int Cin, int ks, const float *src, int obs_ld,
-                           const float *dY, float *part, float *colsum, float *dWt, float *db, int splits) {
+                           const float *dY, float *part, float *colsum, float *dWt, float *db, int splits, int exact) {
     ConvA cv;
     cv.kind = 1; cv.cin = Cin; cv.ks = ks; cv.pad = ks / 2; cv.obs = obs_ld > 0; cv.ld = obs_ld;
     return wgrad(st, cv, Cin * ks * ks, Co, rows * CV_HW, src, 0, dY, Co, part, colsum, dWt, Co, Co, nullptr, 0, db,
-                 nullptr, splits);
+                 nullptr, splits, exact);
 }
 
 static hipError_t wgrad(hipStream_t st, const ConvA &cv, int Kin, int N, int rows, const float *X, int ldx,
                         const float *dZ, int ldz, float *part, float *colsum, float *dW0, int ldw0, int n0,
-                        float *dW1, int ldw1, float *db0, float *db1, int splits) {
+                        float *dW1, int ldw1, float *db0, float *db1, int splits, int exact) {
     if (Kin <= 0 || N <= 0) return hipSuccess;
+    if (exact == 2) {        // reference-exact: row-ordered f64 sums, one thread per entry
+        SeqWg a{};
+        a.cv = cv; a.X = X; a.ldx = ldx; a.dZ = dZ; a.ldz = ldz; a.Kin = Kin; a.N = N; a.rows = rows;
+        a.dW0 = dW0; a.ldw0 = ldw0; a.n0 = dW1 ? n0 : N; a.dW1 = dW1; a.ldw1 = ldw1; a.db0 = db0; a.db1 = db1;
+        const size_t nt = (size_t)Kin * N + ((db0 || db1) ? N : 0);
+        hipLaunchKernelGGL(k_wg_seq, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st, a);
+        return hipGetLastError();
+    }
     GemmArgs g{};
     g.cv = cv;
     g.A = X; g.lda = ldx; g.B = dZ; g.ldb = ldz; g.M = Kin; g.N = N; g.K = rows;
     g.part = part; g.colsum = (db0 || db1) ? colsum : nullptr;
     g.k_per_split = ((rows + splits - 1) / splits + GBK - 1) / GBK * GBK;
     const int sp = (rows + g.k_per_split - 1) / g.k_per_split;
-    hipError_t e = cv.kind ? launch_by_width<GEMM_WG, 1>(g, sp, st) : launch_by_width<GEMM_WG>(g, sp, st);
+    hipError_t e;
+    if (exact) e = cv.kind ? launch64_by_width<1>(g, sp, st) : launch64_by_width<0>(g, sp, st);
+    else e = cv.kind ? launch_by_width<GEMM_WG, 1>(g, sp, st) : launch_by_width<GEMM_WG>(g, sp, st);
     if (e != hipSuccess) return e;
     const size_t MN = (size_t)Kin * N;
     const int nn0 = dW1 ? n0 : N;
-    hipLaunchKernelGGL(k_split_reduce, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, st, part, sp, Kin, N,
-                       nn0, dW0, ldw0, dW1, ldw1);
+    if (exact)
+        hipLaunchKernelGGL(k_split_reduce64, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, st,
+                           (const double *)part, sp, Kin, N, nn0, dW0, ldw0, dW1, ldw1);
+    else
+        hipLaunchKernelGGL(k_split_reduce, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, st, part, sp, Kin, N,
+                           nn0, dW0, ldw0, dW1, ldw1);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (db0 || db1) {
         // bias gradient: colsum [sp][N] -> db0 (cols < n0) / db1
-        hipLaunchKernelGGL(k_split_reduce, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, colsum, sp, 1, N,
-                           db1 ? n0 : N, db0, 0, db1, 0);
+        if (exact)
+            hipLaunchKernelGGL(k_split_reduce64, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st,
+                               (const double *)colsum, sp, 1, N, db1 ? n0 : N, db0, 0, db1, 0);
+        else
+            hipLaunchKernelGGL(k_split_reduce, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, colsum, sp, 1, N,
+                               db1 ? n0 : N, db0, 0, db1, 0);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     return hipSuccess;
@@ -450,12 +709,15 @@ static hipError_t wgrad(hipStream_t st, const ConvA &cv, int Kin, int N, int row
 // ------------------------------------------------------------ parity hook ---
 // bppo_debug_gemm: host buffers in/out; mode 0 FWD (bias, act 0 none / 1 relu /
 // 2 tanh), 1 DX (H optional: act 2 tanh derivative, else relu mask), 2 WG
-// (out = [Kin][N] weight grad, out2 = [N] bias grad).
+// (out = [Kin][N] weight grad, out2 = [N] bias grad), 3 WG with f64 sums (k_gemm_wg64),
+// 4 WG with row-ordered f64 sums (k_wg_seq).
 extern "C" bppo_status bppo_debug_gemm(int32_t mode, int32_t M, int32_t N, int32_t K, const float *A,
                                        const float *B, const float *bias_or_H, int32_t act, float *out,
                                        float *out2) {
     using namespace bppo;
-    if (!A || !B || !out || M <= 0 || N <= 0 || K <= 0 || mode < 0 || mode > 2) return BPPO_ERR_ARG;
+    if (!A || !B || !out || M <= 0 || N <= 0 || K <= 0 || mode < 0 || mode > 4) return BPPO_ERR_ARG;
+    const int exact = mode >= 3 ? mode - 2 : 0;   // 3: f64 MFMA sums, 4: row-ordered f64 sums
+    if (exact) mode = 2;
     float *dA = nullptr, *dB = nullptr, *dX = nullptr, *dO = nullptr, *dO2 = nullptr, *dP = nullptr, *dC = nullptr;
     size_t nA = mode == 2 ? (size_t)K * M : (size_t)M * K;   // WG: X [rows=K][Kin=M]
     size_t nB = mode == 1 ? (size_t)N * K : (size_t)K * N;
@@ -476,12 +738,12 @@ extern "C" bppo_status bppo_debug_gemm(int32_t mode, int32_t M, int32_t N, int32
             if (!dX) break;
             e = gemm_fwd(nullptr, M, N, K, dA, K, dB, N, dX, act, dO, N, N, nullptr, 0);
         } else if (mode == 1) {
-            e = gemm_dx(nullptr, M, N, K, dA, K, dB, K, dX, N, act, dO, N);
+            e = gemm_dx(nullptr, M, N, K, dA, K, dB, K, dX, N, act, dO, N, nullptr, 0, nullptr);
         } else {
             if (hipMalloc((void **)&dO2, (size_t)N * 4) != hipSuccess) break;
-            if (hipMalloc((void **)&dP, (size_t)splits * M * N * 4) != hipSuccess) break;
-            if (hipMalloc((void **)&dC, (size_t)splits * N * 4) != hipSuccess) break;
-            e = gemm_wgrad(nullptr, M, N, K, dA, M, dB, N, dP, dC, dO, N, N, nullptr, 0, dO2, nullptr, splits);
+            if (hipMalloc((void **)&dP, (size_t)splits * M * N * 8) != hipSuccess) break;
+            if (hipMalloc((void **)&dC, (size_t)splits * N * 8) != hipSuccess) break;
+            e = gemm_wgrad(nullptr, M, N, K, dA, M, dB, N, dP, dC, dO, N, N, nullptr, 0, dO2, nullptr, splits, exact);
         }
         if (e != hipSuccess || hipDeviceSynchronize() != hipSuccess) break;
         if (hipMemcpy(out, dO, (size_t)M * N * 4, hipMemcpyDeviceToHost) != hipSuccess) break;

@@ -20,6 +20,19 @@ constexpr int STAT_BLOCKS = 1024;   // partial blocks of the explained-variance 
 // metric slots appended after the parameters in the gradient slab
 enum { M_PL = 0, M_VL, M_H, M_KL, M_CF, M_V, M_R, M_VE, M_VE2, M_VEMAX, M_N, NUM_M };
 
+// per-tensor norm clip + Adam arguments (k_adam1 / k_adam, and the minibatch kernels' tail)
+constexpr int ADAM_CHUNK = 4096;
+struct AdamTensor { int off, len; float c1, c2; };
+struct AdamArgs {
+    float *params, *grad, *m1, *m2;
+    double *part;
+    AdamTensor t[32];
+    int blk0[33];          // first block of tensor i; blk0[nt] = total blocks
+    int nt;
+    float lr, max_norm, eps, inv_world;
+};
+constexpr int SLAB_GROUPS = 32;      // the slab's block rows are summed in 32 groups, then the groups in order
+
 struct MbArgs {
     const float *obs, *logp, *adv, *ret, *val;
     const int32_t *act;
@@ -1184,7 +1197,6 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
 
 // fixed-order reduction of the wave partials, grad[p] = sum_w slab[w][p]: SLAB_GROUPS
 // row groups each summed in f64 in row order, then the groups in order.
-constexpr int SLAB_GROUPS = 32;
 // both passes in one launch, same association (bit-identical grad): a block owns 64
 // columns; its 16 waves take row groups g = q, q + 16 and leave the group sums in
 // LDS, then wave 0 adds the 32 groups in order.  One dependent launch fewer per
@@ -1222,16 +1234,6 @@ __global__ void __launch_bounds__(64 * SLAB1_WAVES) k_slab_reduce1(const float *
 // per-tensor norm clip + Adam (burn-optim 0.20 restated).  Each tensor is cut
 // into ADAM_CHUNK-element blocks: pass 1 writes every block's sum of squares,
 // pass 2 sums its tensor's partials in block order (deterministic) and updates.
-constexpr int ADAM_CHUNK = 4096;
-struct AdamTensor { int off, len; float c1, c2; };
-struct AdamArgs {
-    float *params, *grad, *m1, *m2;
-    double *part;
-    AdamTensor t[32];
-    int blk0[33];          // first block of tensor i; blk0[nt] = total blocks
-    int nt;
-    float lr, max_norm, eps, inv_world;
-};
 __device__ __forceinline__ int adam_tensor_of(const AdamArgs &a, int b) {
     int t = 0;
     while (t + 1 < a.nt && a.blk0[t + 1] <= b) t++;
@@ -1557,6 +1559,23 @@ bppo_status launch_epoch_adv_stats(bppo_ctx *c, uint32_t B, int M, const uint32_
     return BPPO_OK;
 }
 
+static AdamArgs adam_args(bppo_ctx *c, float lr, const float *c1, const float *c2) {
+    AdamArgs a;
+    a.params = c->d_params; a.grad = c->d_grad; a.m1 = c->d_m1; a.m2 = c->d_m2;
+    a.nt = 2 * c->net.n_layers;
+    for (int l = 0; l < c->net.n_layers; l++) {
+        a.t[2 * l] = AdamTensor{(int)c->net.w[l], c->net.in[l] * c->net.out[l], c1[2 * l], c2[2 * l]};
+        a.t[2 * l + 1] = AdamTensor{(int)c->net.b[l], c->net.out[l], c1[2 * l + 1], c2[2 * l + 1]};
+    }
+    a.lr = lr; a.max_norm = (float)c->cfg.max_grad_norm; a.eps = (float)c->cfg.adam_epsilon;
+    a.inv_world = 1.0f / (float)c->world;
+    a.part = c->d_red;
+    int nb = 0;
+    for (int t = 0; t < a.nt; t++) { a.blk0[t] = nb; nb += (a.t[t].len + ADAM_CHUNK - 1) / ADAM_CHUNK; }
+    a.blk0[a.nt] = nb;
+    return a;
+}
+
 bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_coef, bool exact) {
     const int h = c->cfg.hidden_size, nl = c->cfg.num_hidden;
     MbArgs g;
@@ -1590,7 +1609,12 @@ bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_
         static const bool exact_all = getenv("BPPO_MB_EXACT_ALL") != nullptr;
         const bool use_exact = c->mb_kernel == 1 || (c->mb_kernel == 0 && (exact || exact_all));
         const size_t lds_split = std::max(mmf::LDS_TILES, (size_t)mmf::WAVES * (c->net.n_params + NUM_M) * sizeof(float));
-        const int ei = c->mb_ev_n < bppo_ctx::MB_EV ? c->mb_ev_n++ : -1;
+        // HIP timer events around the launch (bench.py's roofline): every launch by default;
+        // BPPO_MB_EVENTS=k times every k-th launch of an update (0: none), for A/B runs of the
+        // timestamp markers' cost on the stream
+        static const int ev_every = getenv("BPPO_MB_EVENTS") ? atoi(getenv("BPPO_MB_EVENTS")) : 1;
+        const bool timed = ev_every > 0 && c->mb_launch++ % ev_every == 0;
+        const int ei = timed && c->mb_ev_n < bppo_ctx::MB_EV ? c->mb_ev_n++ : -1;
         if (ei >= 0) { c->mb_ev_split[ei] = !use_exact; BPPO_HIP(c, hipEventRecord(c->mb_ev[ei][0], c->stream)); }
         if (use_exact)
             hipLaunchKernelGGL(k_minibatch_mfma, dim3(blocks), dim3(64 * mmb::WAVES), mmb::LDSB, c->stream, g);
@@ -1653,19 +1677,8 @@ bppo_status launch_metric_row(bppo_ctx *c, float *dst, int nm) {
 }
 
 bppo_status launch_adam(bppo_ctx *c, float lr, const float *c1, const float *c2, float *metric_dst, int nm) {
-    AdamArgs a;
-    a.params = c->d_params; a.grad = c->d_grad; a.m1 = c->d_m1; a.m2 = c->d_m2;
-    a.nt = 2 * c->net.n_layers;
-    for (int l = 0; l < c->net.n_layers; l++) {
-        a.t[2 * l] = AdamTensor{(int)c->net.w[l], c->net.in[l] * c->net.out[l], c1[2 * l], c2[2 * l]};
-        a.t[2 * l + 1] = AdamTensor{(int)c->net.b[l], c->net.out[l], c1[2 * l + 1], c2[2 * l + 1]};
-    }
-    a.lr = lr; a.max_norm = (float)c->cfg.max_grad_norm; a.eps = (float)c->cfg.adam_epsilon;
-    a.inv_world = 1.0f / (float)c->world;
-    a.part = c->d_red;
-    int nb = 0;
-    for (int t = 0; t < a.nt; t++) { a.blk0[t] = nb; nb += (a.t[t].len + ADAM_CHUNK - 1) / ADAM_CHUNK; }
-    a.blk0[a.nt] = nb;
+    const AdamArgs a = adam_args(c, lr, c1, c2);
+    const int nb = a.blk0[a.nt];
     if (nb == a.nt && metric_dst) {       // one chunk per tensor: fused
         hipLaunchKernelGGL(k_adam1, dim3(nb), dim3(ADAM1_THREADS), 0, c->stream, a, c->d_grad + c->net.n_params,
                            c->d_mb_cur, nm, metric_dst);

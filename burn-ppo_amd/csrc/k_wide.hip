@@ -279,7 +279,6 @@ __global__ void __launch_bounds__(256) k_wide_loss(LossArgs g) {
     for (int k = 0; k < WM_COUNT; k++) m[k] = 0.0;
     m[WM_VEMAX] = -INFINITY;
     const float mean = g.mb_stats[0], denom = __fadd_rn(g.mb_stats[1], 1e-8f);
-    const float ec = g.ent_coef * g.inv_mb;
     for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < g.n; r += gridDim.x * blockDim.x) {
         const uint32_t idx = g.perm[g.start + r];
         const int act = g.act[idx];
@@ -331,15 +330,20 @@ __global__ void __launch_bounds__(256) k_wide_loss(LossArgs g) {
             vl = __fmul_rn(__fsub_rn(v, R), __fsub_rn(v, R));
             dvl = 2.0f * __fsub_rn(v, R);
         }
-        const float g_ratio = (!rhs || (ratio >= g.lo && ratio <= g.hi)) ? -An * g.inv_mb : 0.0f;
-        const float g_lr = g_ratio * ratio;
+        // dL/dlogits and dL/dvalue in f64, each rounded once to f32 (ppo.rs:1923-1959 through
+        // the oracle's restatement of the autodiff, oracle/net.c or_minibatch_loss_grad)
+        const double g_ratio = (!rhs || (ratio >= g.lo && ratio <= g.hi)) ? -(double)An * g.inv_mb_d : 0.0;
+        const double g_lr = g_ratio * (double)ratio;
+        const double ecd = g.ent_coef_d * g.inv_mb_d;
         float *d = g.dout + (size_t)r * (A + 1);
 #pragma unroll
         for (int a = 0; a < A; a++) {
-            const float pr = bppo_math::expf_glibc(x[a]);
-            d[a] = g_lr * ((a == act ? 1.0f : 0.0f) - pr) + ec * pr * (x[a] + H);
+            const double pr = (double)bppo_math::expf_glibc(x[a]);
+            double gd = g_lr * ((a == act ? 1.0 : 0.0) - pr);
+            gd += ecd * pr * ((double)x[a] + (double)H);
+            d[a] = (float)gd;
         }
-        d[A] = g.value_coef * 0.5f * g.inv_mb * dvl;
+        d[A] = (float)(g.value_coef_d * 0.5 * g.inv_mb_d * (double)dvl);
         const float ve = fabsf(__fsub_rn(v, R));
         m[WM_PL] += pl; m[WM_VL] += vl; m[WM_H] += H;
         m[WM_KL] += (double)__fsub_rn(__fsub_rn(ratio, 1.0f), log_ratio);

@@ -90,8 +90,9 @@ bppo_status wide_init(bppo_ctx *c) {
         part = std::max(part, (size_t)s * Kin * N);
         cs = std::max(cs, (size_t)s * N);
     }
-    WTRY(walloc(c, &c->d_part, part));
-    WTRY(walloc(c, &c->d_colsum, cs));
+    // sized for the f64 partials of the exact weight gradients (k_gemm_wg64)
+    WTRY(walloc(c, &c->d_part, 2 * part));
+    WTRY(walloc(c, &c->d_colsum, 2 * cs));
     WTRY(walloc(c, &c->d_mpart, (size_t)1024 * WM_COUNT));
     WTRY(walloc(c, &c->d_bxc, (size_t)c->N * c->L));
     WTRY(walloc(c, &c->d_bmask, (size_t)c->N * c->A));
@@ -265,12 +266,13 @@ bppo_status wide_bootstrap_gae(bppo_ctx *c) {
 
 // one minibatch of ppo_update: gather, forward, loss, backward -> d_grad[0, np),
 // metrics -> d_grad[np, np + WM_COUNT)
-bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, float ent_coef) {
+bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, double ent_coef) {
     const NetLayout &n = c->net;
     const int hact = c->cfg.relu ? 1 : 2;   // hidden activation derivative in the DX epilogues
     const int A = c->A, L = c->L, rows = (int)mb;
     const float *P = c->d_params;
     float *G = c->d_grad;
+    const int exact = wide_exact_grad(c);
     WHIP(c, wide_gather(c->stream, c->d_perm, start, mb, c->d_xc, L, c->d_xcg));
     WTRY(wide_forward(c, rows, c->d_xcg, L, c->d_logits, c->d_values));
     LossArgs g;
@@ -278,8 +280,9 @@ bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, float ent_c
     g.ret = c->u_ret; g.val = c->u_val; g.mask = c->d_mask; g.logits = c->d_logits; g.values = c->d_values;
     g.mb_stats = c->d_mb_cur; g.dout = c->d_dout; g.part = c->d_mpart;
     g.lo = (float)(1.0 - c->cfg.clip_epsilon); g.hi = (float)(1.0 + c->cfg.clip_epsilon);
-    g.ceps = (float)c->cfg.clip_epsilon; g.inv_mb = (float)(1.0 / (double)mb); g.ent_coef = ent_coef;
+    g.ceps = (float)c->cfg.clip_epsilon; g.inv_mb = (float)(1.0 / (double)mb); g.ent_coef = (float)ent_coef;
     g.value_coef = (float)c->cfg.value_coef; g.clip_value = c->cfg.clip_value;
+    g.inv_mb_d = 1.0 / (double)mb; g.ent_coef_d = ent_coef; g.value_coef_d = c->cfg.value_coef;
     const int blocks = std::max(1, std::min(1024, (int)((mb + 255) / 256)));
     WHIP(c, wide_loss(A, c->stream, g, blocks, G + n.n_params));
     float *dz = c->d_dz[0], *dz2 = c->d_dz[1];
@@ -287,7 +290,7 @@ bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, float ent_c
                      int n0, float *dW1, int ldw1, float *db0, float *db1) -> bppo_status {
         const int sp = gemm_wg_splits(Kin, N, rows);
         WHIP(c, gemm_wgrad(c->stream, Kin, N, rows, X, ldx, dZ, ldz, c->d_part, c->d_colsum, dW0, ldw0, n0, dW1,
-                           ldw1, db0, db1, sp));
+                           ldw1, db0, db1, sp, exact));
         return BPPO_OK;
     };
     // walk hidden layers [first, last] down, dz holds dL/dz of layer `last`
@@ -313,7 +316,7 @@ bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, float ent_c
         float *dF = c->d_cnn_dy[0];
         WHIP(c, gemm_dx(c->stream, rows, n.fdim, n.out[f0], dz, n.out[f0], P + n.w[f0], n.out[f0], c->d_cnn_f[s],
                         n.fdim, 1, dF, n.fdim));
-        return cnn_backward(c, s, rows, c->d_xcg + c->G, L, dF, G);
+        return cnn_backward(c, s, rows, c->d_xcg + c->G, L, dF, G, exact);
     };
     const int la = n.n_actor_hidden - 1;
     const float *Ha = c->d_hbuf + c->hoff[la];
@@ -322,7 +325,10 @@ bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, float ent_c
         // heads: dW = H^T [dlogits | dv] split into policy / value tensors
         WTRY(wgrad(Wa, A + 1, Ha, Wa, c->d_dout, A + 1, G + n.w[n.policy], A, A, G + n.w[n.value], 1,
                    G + n.b[n.policy], G + n.b[n.value]));
-        WHIP(c, gemm_dx(c->stream, rows, Wa, A + 1, c->d_dout, A + 1, c->d_heads, A + 1, Ha, Wa, hact, dz, Wa));
+        // the trunk's input gradient: the policy head's chain over its A outputs, then the value
+        // head's product added as its own rounded term (the two heads are two Linear modules)
+        WHIP(c, gemm_dx(c->stream, rows, Wa, A, c->d_dout, A + 1, c->d_heads, A + 1, Ha, Wa, hact, dz, Wa,
+                        c->d_dout + A, A + 1, P + n.w[n.value]));
         if (!n.n_conv) {
             WTRY(hidden_chain(0, la, c->d_xcg + c->G, L));
             return BPPO_OK;

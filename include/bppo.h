@@ -303,13 +303,16 @@ bppo_status bppo_gae_mp_device(const float *all_rewards, const int32_t *players,
  * (it waits for them at the update's end: ~10 ms of one CPU per 8.4 M rows) */
 bppo_status bppo_set_explained_variance_mode(bppo_ctx *ctx, int32_t mode);
 
-/* which minibatch kernel runs (a parity / A-B hook; it has an effect only where a
- * split-bf16 kernel exists: the 2x64 relu MLP of CfgB).  mode 0 (default): the update's
- * first minibatch on the exact f32 kernel (it runs with the rollout's parameters, so the
- * ratio is exactly 1 and the forward equals the rollout's bit for bit), every later one on
- * the f32-accurate split-bf16 kernel; 1: the exact kernel for every minibatch; 2: the split
- * kernel for every minibatch, the first included (its gradient from the rollout's parameters
- * can then be compared with the oracle's, tests/test_gpu_split_kernel.py) */
+/* which minibatch kernels run (a parity / A-B hook).  CartPole's 2x64 relu MLP (CfgB):
+ * mode 0 (default) runs the update's first minibatch on the exact f32 kernel (it runs with
+ * the rollout's parameters, so the ratio is exactly 1 and the forward equals the rollout's
+ * bit for bit) and every later one on the f32-accurate split-bf16 kernel; 1 the exact kernel
+ * for every minibatch; 2 the split kernel for every minibatch, the first included (its
+ * gradient from the rollout's parameters can then be compared with the oracle's,
+ * tests/test_gpu_split_kernel.py).  The GEMM path (Connect Four, Liar's Dice, Skull, other
+ * nets): mode 0 sums the weight gradients in f64 on the f64 MFMA for CNN nets and in f32
+ * split-K chains otherwise; 1 in f64 row by row in order, the oracle's arithmetic exactly (a
+ * latency-bound parity mode); 2 in f32 split-K chains for every net. */
 bppo_status bppo_set_minibatch_kernel(bppo_ctx *ctx, int32_t mode);
 
 /* device timing of the last call of each phase kernel (ms), for bench.py's roofline */

@@ -254,6 +254,35 @@ void or_net_forward(const or_net_desc *d, const float *params, const float *obs,
     free_acts(&A);
 }
 
+/* dx = dz W^T as linear_bwd computes it: per row, each input k an f32 fma chain over the
+ * outputs o in order from 0 (W [in][out]) */
+static void dx_chain(const float *dz, const float *W, size_t B, int in, int out, float *dx, int big) {
+    float *WT = malloc(sizeof(float) * (size_t)in * out);
+    for (int k = 0; k < in; k++)
+        for (int o = 0; o < out; o++) WT[(size_t)o * in + k] = W[(size_t)k * out + o];
+#pragma omp parallel if (big)
+    {
+        float *acc = malloc(sizeof(float) * (size_t)in);
+#pragma omp for schedule(static)
+        for (size_t r = 0; r < B; r++) {
+            for (int k = 0; k < in; k++) acc[k] = 0.0f;
+            for (int o = 0; o < out; o++) {
+                const float g = dz[r * out + o];
+                const float *wo = WT + (size_t)o * in;
+                for (int k = 0; k < in; k++) acc[k] = fmaf(g, wo[k], acc[k]);
+            }
+            for (int k = 0; k < in; k++) dx[r * in + k] = acc[k];
+        }
+        free(acc);
+    }
+    free(WT);
+}
+
+/* test hook: the input gradient of one Linear (dz [B][out], W [in][out] -> dx [B][in]) */
+void or_linear_dx(const float *dz, const float *W, size_t B, int in, int out, float *dx) {
+    dx_chain(dz, W, B, in, out, dx, B * (size_t)in * (size_t)out > (1u << 18));
+}
+
 /* backward of one Linear + activation given the post-activation output y:
  * dW += x^T dz (f64, each element summed over rows in row order), db += sum dz,
  * dx = dz W^T (f32 fma chain over o).  Parallel over k (dW) and rows (dx):
@@ -281,27 +310,7 @@ static void linear_bwd(const float *x, const float *y, const float *dy, const fl
             for (int o = 0; o < out; o++) gk[o] += xk * (double)dzr[o];
         }
     }
-    if (dx) {
-        float *WT = malloc(sizeof(float) * (size_t)in * out);
-        for (int k = 0; k < in; k++)
-            for (int o = 0; o < out; o++) WT[(size_t)o * in + k] = W[(size_t)k * out + o];
-#pragma omp parallel if (big)
-        {
-            float *acc = malloc(sizeof(float) * (size_t)in);
-#pragma omp for schedule(static)
-            for (size_t r = 0; r < B; r++) {
-                for (int k = 0; k < in; k++) acc[k] = 0.0f;
-                for (int o = 0; o < out; o++) {
-                    const float g = dz[r * out + o];
-                    const float *wo = WT + (size_t)o * in;
-                    for (int k = 0; k < in; k++) acc[k] = fmaf(g, wo[k], acc[k]);
-                }
-                for (int k = 0; k < in; k++) dx[r * in + k] = acc[k];
-            }
-            free(acc);
-        }
-        free(WT);
-    }
+    if (dx) dx_chain(dz, W, B, in, out, dx, big);
     free(dz);
 }
 

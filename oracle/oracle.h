@@ -242,6 +242,8 @@ void or_set_mlp_parallel(int on);
 /* one linear layer y = x W + b with the matrixmultiply summation order */
 void or_linear(const float *x, const float *W, const float *b, size_t B, int in, int out,
                int relu, float *y);
+/* the input gradient of one Linear as the backward computes it (test hook) */
+void or_linear_dx(const float *dz, const float *W, size_t B, int in, int out, float *dx);
 
 /* ------------------------------------------------------------- policy ---- */
 void or_sample_categorical(or_rng *rng, const float *logits, size_t B, int A, int32_t *actions);

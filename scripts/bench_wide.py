@@ -39,6 +39,8 @@ def main():
     p.add_argument("--no-kl-stop", action="store_true", help="run every epoch (target_kl off)")
     p.add_argument("--opponents", type=int, default=0,
                    help="opponent-pool rollouts (ppo.rs:537-1063) against K loaded models")
+    p.add_argument("--minibatch-kernel", type=int, default=None,
+                   help="bppo_set_minibatch_kernel mode (0 default, 1 exact f64 weight gradients, 2 f32)")
     p.add_argument("--opponent-frac", type=float, default=0.25,
                    help="opponent_pool_fraction (configs/liars_dice*.toml: 0.25)")
     a = p.parse_args()
@@ -53,6 +55,8 @@ def main():
     cfg = bppo.make_config(w["preset"], num_envs=w["num_envs"], num_steps=w["num_steps"], **over)
     torch.cuda.set_device(0)
     tr = bppo.Trainer(cfg, init_seed=0)
+    if a.minibatch_kernel is not None:
+        tr.ctx.set_minibatch_kernel(a.minibatch_kernel)
     if a.opponents:
         import numpy as np
         P = tr.ctx.num_players
@@ -82,6 +86,9 @@ def main():
            "ms_per_update": round(dt / a.steps * 1000, 2), "num_envs": w["num_envs"],
            "num_steps": w["num_steps"], "minibatches_per_update": ups / a.steps,
            "phase_ms_per_update": {k: round(v / a.steps, 2) for k, v in ph.items()},
+           # the reference's own names (main.rs:1092-1132) over the timed interval
+           "perf": {k: round(v, 6) for k, v in bppo.perf_scalars(B * a.steps, dt, ph["rollout"], ph["gae"],
+                                                                 ph["update"]).items()},
            "last": {k: round(v, 5) for k, v in m.items() if isinstance(v, float)}}
     print(json.dumps(out), flush=True)
     tr.close()

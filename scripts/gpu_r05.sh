@@ -41,4 +41,42 @@ if [ "$PART" = t2 ]; then
   done
   exit 0
 fi
+if [ "$PART" = wide ]; then
+  # multi-player workloads on the current tree (name|bench_wide args)
+  for v in ${WIDE_VARIANTS:-"cfgC|--workload cfgC" "cfgD|--workload cfgD" "cnn64|--workload cfgC_cnn64" "cnn64f32|--workload cfgC_cnn64 --minibatch-kernel 2"}; do
+    IFS='|' read -r name args <<< "$v"
+    timeout -k 10 400 python scripts/bench_wide.py $args > gpurun_out/${TAG}_wide_${name}.log 2>&1
+    rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || { tail -3 gpurun_out/${TAG}_wide_${name}.log; exit $rc; }
+    tail -1 gpurun_out/${TAG}_wide_${name}.log | cut -c1-400
+  done
+  exit 0
+fi
+if [ "$PART" = cnnprobe ]; then
+  timeout -k 10 600 python -u scripts/probes/${CNN_PROBE:-cnn_exact_probe}.py > gpurun_out/${TAG}_cnn_exact_probe.log 2>&1
+  rc=$?; echo "cnn probe rc=$rc"; cat gpurun_out/${TAG}_cnn_exact_probe.log | grep -v amdgpu.ids | cut -c1-600
+  exit $rc
+fi
+if [ "$PART" = ab ]; then
+  # interleaved A/B of env variants on the default bench line: AB_VARIANTS="name|VAR=x ..." (repeated AB_REPS times)
+  for rep in $(seq 1 ${AB_REPS:-2}); do
+    for v in ${AB_VARIANTS:-"def|BPPO_MB_EVENTS=1" "ev0|BPPO_MB_EVENTS=0"}; do
+      IFS='|' read -r name envs <<< "$v"
+      timeout -k 10 300 env $envs python bench.py --no-learning --no-cpu-baseline ${AB_FLAGS:-} > gpurun_out/${TAG}_ab_${name}_${rep}.log 2>&1
+      rc=$?; echo "$name/$rep rc=$rc"; [ $rc -eq 0 ] || { tail -3 gpurun_out/${TAG}_ab_${name}_${rep}.log; exit $rc; }
+      summ gpurun_out/${TAG}_ab_${name}_${rep}.log
+    done
+  done
+  exit 0
+fi
+if [ "$PART" = widekt ]; then
+  # kernel trace of the multi-player workloads (rocprofv3 --kernel-trace --stats)
+  for w in ${WIDE_KT:-cfgC cfgD}; do
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/kt_${TAG}_$w -o kt -- python3 scripts/bench_wide.py --workload $w --steps 2 --warmup 1 > gpurun_out/kt_${TAG}_$w.log 2>&1
+    rc=$?; echo "kt $w rc=$rc"; [ $rc -eq 0 ] || exit $rc
+    DB=$(find gpurun_out/kt_${TAG}_$w -name "*.db" | head -1)
+    python3 scripts/rocpd_summary.py $DB > gpurun_out/${TAG}_${w}_kernels.txt
+    head -22 gpurun_out/${TAG}_${w}_kernels.txt | cut -c1-140
+  done
+  exit 0
+fi
 echo "unknown part $PART"; exit 2

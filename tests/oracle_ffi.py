@@ -199,6 +199,7 @@ def lib():
             "or_vecenv_env_ptr": (C.c_void_p, [C.c_void_p, C.c_int]),
             "or_net_num_params": (C.c_size_t, [C.POINTER(NetDesc)]),
             "or_linear": (None, [f32, f32, f32, C.c_size_t, C.c_int, C.c_int, C.c_int, f32]),
+            "or_linear_dx": (None, [f32, f32, C.c_size_t, C.c_int, C.c_int, f32]),
             "or_net_forward": (None, [C.POINTER(NetDesc), f32, f32, C.c_void_p, C.c_size_t, f32, f32]),
             "or_sample_categorical": (None, [C.POINTER(Rng), f32, C.c_size_t, C.c_int, i32]),
             "or_log_prob": (C.c_float, [f32, C.c_int, C.c_int32]),
@@ -350,6 +351,15 @@ def linear(x, W, b, relu):
     lib().or_linear(np.ascontiguousarray(x, np.float32), np.ascontiguousarray(W, np.float32),
                     np.ascontiguousarray(b, np.float32), B, K, N, relu, y)
     return y
+
+
+def linear_dx(dz, W):
+    """or_linear_dx: dx [B][in] = dz [B][out] W^T, W [in][out], an f32 fma chain over out from 0"""
+    B, out = dz.shape
+    dx = np.zeros((B, W.shape[0]), np.float32)
+    lib().or_linear_dx(np.ascontiguousarray(dz, np.float32), np.ascontiguousarray(W, np.float32), B, W.shape[0],
+                       out, dx)
+    return dx
 
 
 def compute_gae(rewards, dones, values, last_values, gamma, lam):

@@ -97,3 +97,55 @@ def test_gemm_weight_grad(Kin, N, rows):
     assert np.all(np.abs(out - ref) <= 1e-5 * mag + 1e-30)
     dbr = dZ.astype(np.float64).sum(0)
     assert np.all(np.abs(db - dbr) <= 1e-5 * np.abs(dZ).astype(np.float64).sum(0) + 1e-30)
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 512, 512), (257, 86, 512), (100, 256, 49), (70, 512, 1),
+                                   (129, 512, 7), (64, 576, 64)])
+def test_gemm_dx_bit_exact(M, N, K):
+    """dX = dZ W^T is the oracle's linear_bwd chain bit for bit: per element an fmaf chain over
+    the K outputs in order from 0 (v_mfma_f32_32x32x2_f32 is a k-ordered fmaf chain), then the
+    relu' mask of the layer below"""
+    rng = np.random.default_rng(M * 3 + N + K)
+    dZ = rng.standard_normal((M, K)).astype(np.float32)
+    W = rng.standard_normal((N, K)).astype(np.float32)           # W [in = N][out = K]
+    H = rng.standard_normal((M, N)).astype(np.float32)
+    ref = O.linear_dx(dZ, W)
+    out, _ = _gemm(1, M, N, K, dZ, W, None)
+    assert np.array_equal(out.view(np.uint32), ref.view(np.uint32))
+    out, _ = _gemm(1, M, N, K, dZ, W, H)
+    assert np.array_equal(out, np.where(H > 0, ref, np.float32(0)))
+
+
+@pytest.mark.parametrize("Kin,N,rows", [(512, 512, 5000), (86, 512, 4099), (256, 8, 3000), (576, 64, 70000),
+                                        (64, 8, 31)])
+def test_gemm_weight_grad_f64(Kin, N, rows):
+    """mode 3 (k_gemm_wg64): every product exact in f64, f64 sums, one rounding to f32 -- the
+    f32 rounding of the exact dot product except where the f64 sum's ordering error straddles
+    an f32 rounding boundary (~2^-19 of the entries at 10^5 rows): at most one ulp there"""
+    rng = np.random.default_rng(Kin * 5 + N + rows)
+    X = rng.standard_normal((rows, Kin)).astype(np.float32)
+    dZ = rng.standard_normal((rows, N)).astype(np.float32)
+    out, db = _gemm(3, Kin, N, rows, X, dZ, None)
+    ref = (X.astype(np.float64).T @ dZ.astype(np.float64)).astype(np.float32)
+    dbr = dZ.astype(np.float64).sum(0).astype(np.float32)
+    for got, want in ((out, ref), (db, dbr)):
+        ulps = np.abs(got.view(np.int32).astype(np.int64) - want.view(np.int32).astype(np.int64))
+        assert ulps.max() <= 1 and np.count_nonzero(ulps) <= max(2, got.size // 10000), (ulps.max(), np.count_nonzero(ulps))
+
+
+@pytest.mark.parametrize("Kin,N,rows", [(86, 512, 4099), (256, 8, 3000), (64, 8, 31)])
+def test_gemm_weight_grad_row_ordered(Kin, N, rows):
+    """mode 4 (k_wg_seq): each entry the f64 sum of the exact products in row order, rounded
+    once -- the oracle's linear_bwd loop, so equal to a sequential f64 restatement bit for bit"""
+    rng = np.random.default_rng(Kin * 7 + N + rows)
+    X = rng.standard_normal((rows, Kin)).astype(np.float32)
+    dZ = rng.standard_normal((rows, N)).astype(np.float32)
+    out, db = _gemm(4, Kin, N, rows, X, dZ, None)
+    acc = np.zeros((Kin, N), np.float64)
+    bacc = np.zeros(N, np.float64)
+    X64, dZ64 = X.astype(np.float64), dZ.astype(np.float64)
+    for r in range(rows):                    # row order, one f64 rounding per addition
+        acc += X64[r][:, None] * dZ64[r][None, :]
+        bacc += dZ64[r]
+    assert np.array_equal(out.view(np.uint32), acc.astype(np.float32).view(np.uint32))
+    assert np.array_equal(db.view(np.uint32), bacc.astype(np.float32).view(np.uint32))

@@ -128,3 +128,4 @@ def test_split_kernel_minibatch_by_minibatch(mode):
         assert not bad, (mode, bad)
     finally:
         tr.close(); ot.close()
+
