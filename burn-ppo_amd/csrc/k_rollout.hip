@@ -116,7 +116,27 @@ struct RolloutArgs {
     EpisodeRec *eps; int32_t *ep_count; int eps_cap;
     int32_t *err;
     float4 *rows;        // MFMA rollout: also the update's rows A [B][2] float4 (k_update.hip load_row), or null
+    unsigned long long *stamps;   // diagnostic build only (BPPO_RO_STAMPS): per-wave segment cycles
 };
+
+// diagnostic build (-DBPPO_RO_STAMPS): s_memtime segment sums per wave of the 64-lane CfgB
+// rollout (cdna_hip_programming.md section 7 in-kernel stamps); read the shares, not the time
+#ifdef BPPO_RO_STAMPS
+constexpr int RO_NSEG = 8;
+#define RO_STAMP(k)                                                                              \
+    do {                                                                                         \
+        __builtin_amdgcn_sched_barrier(0);                                                       \
+        unsigned long long t_;                                                                   \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");               \
+        __builtin_amdgcn_sched_barrier(0);                                                       \
+        ro_acc[k] += t_ - ro_prev;                                                               \
+        ro_prev = t_;                                                                            \
+    } while (0)
+#else
+#define RO_STAMP(k) \
+    do {            \
+    } while (0)
+#endif
 
 template <int H, int NL, int ACT>
 __global__ void __launch_bounds__(256) k_cartpole_rollout(RolloutArgs a) {
@@ -521,6 +541,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
     int32_t bad = 0;
     float2 gz = make_float2(0.0f, 0.0f);
     if (mine && a.T > 0) gz = *reinterpret_cast<const float2 *>(gum + (size_t)e * 2);
+#ifdef BPPO_RO_STAMPS
+    unsigned long long ro_acc[RO_NSEG] = {}, ro_prev;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ro_prev)::"memory");
+#endif
 #pragma unroll 1
     for (int t = 0; t < a.T; t++) {
         const size_t row = (size_t)t * N + e;
@@ -536,6 +560,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
 #pragma unroll
             for (int d = 0; d < 5; d++) x[d] = z[d];
         }
+        RO_STAMP(0);
         // ---- layer 1 (transposed): H1^T = [W0; b0]^T [x, 1]^T, two env tiles
         f32x16_t h1[2][2];
 #pragma unroll
@@ -563,6 +588,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
                     const float v = h1[tl][ct][q];
                     h1[tl][ct][q] = v > 0.0f ? v : 0.0f;
                 }
+        RO_STAMP(1);
         // ---- layer 2 (transposed): register m of h1 is K step m
         f32x16_t h2[2][2];
 #pragma unroll
@@ -583,6 +609,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
                 h2[tl][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.y, h1[tl][st >> 4][st & 15], h2[tl][1], 0, 0, 0);
             }
         }
+        RO_STAMP(2);
         // H2 -> the wave's [env][unit] tile (register m of lane (c, h) holds unit 32h + m of
         // env c of tile tl), then lane l reads env l's row
 #pragma unroll
@@ -590,6 +617,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
 #pragma unroll
             for (int m = 0; m < 32; m++) Tw[(32 * tl + c) * 65 + 32 * h + m] = h2[tl][m >> 4][m & 15];
         wave_sync();
+        RO_STAMP(3);
         // ---- heads: + b1, relu, the k-ordered chains of logit 0, logit 1, value
         // (the row reads stay in the step loop: hoisted, they would pin 256 VGPRs)
         int zero = 0;
@@ -613,31 +641,43 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
         const float n0 = __fadd_rn(lg[0], gz.x);
         const float n1 = __fadd_rn(lg[1], gz.y);
         const int act = n1 > n0 ? 1 : 0;               // argmax, first maximum
+        RO_STAMP(4);
         const float lp = log_prob2(S, lg, act);
         bool done = false;
         float r = 0.0f;
+        RO_STAMP(5);
         if (mine) {
             bad |= !isfinite(lp);
             done = cartpole_step(s, act, r);
             ep_ret = __fadd_rn(ep_ret, r);
             ep_len += 1;
         }
+#if defined(BPPO_RO_DIAG) && (BPPO_RO_DIAG & 1)
+        const int32_t k = -1;   // diagnostic: no episode records
+#else
         const int32_t k = wave_episode_slot(done, a.ep_count);
+#endif
         if (done) {
-            if (k < a.eps_cap) {
+            if (k >= 0 && k < a.eps_cap) {
                 EpisodeRec rec;
                 rec.total_reward[0] = ep_ret;
                 for (int p = 1; p < BPPO_MAX_PLAYERS; p++) rec.total_reward[p] = 0.0f;
                 rec.length = ep_len; rec.env_index = e; rec.step = t; rec.pad = 0;
                 a.eps[k] = rec;
             }
+#if defined(BPPO_RO_DIAG) && (BPPO_RO_DIAG & 2)
+            s.x = 0.01f; s.x_dot = -0.01f; s.theta = 0.02f; s.theta_dot = -0.02f; s.steps = 0;   // diagnostic
+            env_pos += 4;
+#else
             WordCursor ec;
             ec.init(seed_key(a.seed_base + (uint64_t)e), 0, env_pos);
             cartpole_reset(s, ec);
             env_pos = ec.pos;
+#endif
             ep_ret = 0.0f;
             ep_len = 0;
         }
+        RO_STAMP(6);
         if (mine) {
 #pragma unroll
             for (int d = 0; d < 5; d++) a.obs[row * 5 + d] = x[d];
@@ -653,7 +693,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
         }
         gz = gz_next;
         wave_sync();                      // this step's tile reads done before the next step's writes
+        RO_STAMP(7);
     }
+#ifdef BPPO_RO_STAMPS
+    if (lane == 0 && a.stamps)
+        for (int k = 0; k < RO_NSEG; k++) a.stamps[(size_t)(e >> 6) * RO_NSEG + k] = ro_acc[k];
+#endif
     if (mine) {
         store_state(a.cp, a.steps, N, e, s);
         a.env_pos[e] = env_pos;
@@ -871,6 +916,7 @@ bppo_status launch_cartpole_rollout(bppo_ctx *c, uint64_t base_pos, const double
     a.logp = c->d_logp; a.act = c->d_act; a.obs_part = c->d_obs_part; a.eps = c->d_eps;
     a.ep_count = c->d_ep_count; a.eps_cap = c->eps_cap; a.err = c->d_err;
     a.rows = nullptr;
+    a.stamps = nullptr;
     c->rows_from_rollout = false;
     if (h == 64 && nl == 2 && c->cfg.relu && c->d_gumbel) {
         // the update's packed rows (obs, action, log-prob, value) written by the rollout
@@ -896,8 +942,31 @@ bppo_status launch_cartpole_rollout(bppo_ctx *c, uint64_t base_pos, const double
                                mmb::LDS, c->stream, a, (const float *)c->d_gumbel);
         } else {
             const int waves = (c->N + 63) / 64;
+#ifdef BPPO_RO_STAMPS
+            static unsigned long long *d_st = nullptr;
+            if (!d_st) BPPO_HIP(c, hipMalloc((void **)&d_st, sizeof(unsigned long long) * (size_t)waves * RO_NSEG));
+            a.stamps = d_st;
+#endif
             hipLaunchKernelGGL(k_cartpole_rollout_mfma64, dim3((waves + mmr::WAVES - 1) / mmr::WAVES),
                                dim3(64 * mmr::WAVES), 0, c->stream, a, (const float *)c->d_gumbel);
+#ifdef BPPO_RO_STAMPS
+            {   // mean per-wave cycles per segment over every launch; printed every 4 launches
+                static double acc_s[RO_NSEG] = {};
+                static int nl = 0;
+                std::vector<unsigned long long> hs((size_t)waves * RO_NSEG);
+                BPPO_HIP(c, hipMemcpyAsync(hs.data(), d_st, hs.size() * 8, hipMemcpyDeviceToHost, c->stream));
+                BPPO_HIP(c, hipStreamSynchronize(c->stream));
+                for (int w = 0; w < waves; w++)
+                    for (int k = 0; k < RO_NSEG; k++) acc_s[k] += (double)hs[(size_t)w * RO_NSEG + k] / waves;
+                if (++nl % 4 == 0) {
+                    double tot = 0;
+                    for (int k = 0; k < RO_NSEG; k++) tot += acc_s[k];
+                    fprintf(stderr, "[rostamp] launches=%d cycles/wave/step=%.0f shares:", nl, tot / nl / c->T);
+                    for (int k = 0; k < RO_NSEG; k++) fprintf(stderr, " s%d=%.3f", k, acc_s[k] / tot);
+                    fprintf(stderr, "\n");
+                }
+            }
+#endif
         }
         TRY(launch_check(c, __func__));
         return BPPO_OK;

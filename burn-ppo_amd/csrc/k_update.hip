@@ -1257,6 +1257,11 @@ __global__ void __launch_bounds__(256) k_adam_norm(AdamArgs a) {
     }
     if (threadIdx.x == 0) a.part[blockIdx.x] = red[0];
 }
+// adam_sqrt_note: the square root is sqrtf (correctly rounded under -fno-fast-math), not
+// __fsqrt_rn: on this toolchain __fsqrt_rn lowers to the 1-ulp hardware approximation
+// and differs from the host's sqrtf in ~15% of operands (scripts/probes/
+// fp_rounding_probe.hip, profiles/r05b/fp_rounding_probe.txt) — one ulp in an update
+// that the chaotic CNN trajectory then amplifies past 1e-5 within a few minibatches
 __global__ void __launch_bounds__(256) k_adam(AdamArgs a) {
     __shared__ double tot;
     const int ti = adam_tensor_of(a, blockIdx.x);
@@ -1280,7 +1285,7 @@ __global__ void __launch_bounds__(256) k_adam(AdamArgs a) {
         a.m1[T.off + i] = m1;
         a.m2[T.off + i] = m2;
         const float m1c = __fdiv_rn(m1, T.c1), m2c = __fdiv_rn(m2, T.c2);
-        const float upd = __fdiv_rn(m1c, __fadd_rn(__fsqrt_rn(m2c), a.eps));
+        const float upd = __fdiv_rn(m1c, __fadd_rn(sqrtf(m2c), a.eps));   // sqrtf: see adam_sqrt_note
         a.params[T.off + i] = __fsub_rn(a.params[T.off + i], __fmul_rn(upd, a.lr));
     }
 }
@@ -1324,7 +1329,7 @@ __global__ void __launch_bounds__(ADAM1_THREADS) k_adam1(AdamArgs a, const float
         a.m1[T.off + i] = m1;
         a.m2[T.off + i] = m2;
         const float m1c = __fdiv_rn(m1, T.c1), m2c = __fdiv_rn(m2, T.c2);
-        const float upd = __fdiv_rn(m1c, __fadd_rn(__fsqrt_rn(m2c), a.eps));
+        const float upd = __fdiv_rn(m1c, __fadd_rn(sqrtf(m2c), a.eps));   // sqrtf: see adam_sqrt_note
         a.params[T.off + i] = __fsub_rn(a.params[T.off + i], __fmul_rn(upd, a.lr));
     }
     if (blockIdx.x == 0 && metric_dst) {

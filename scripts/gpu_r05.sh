@@ -33,7 +33,9 @@ if [ "$PART" = tests ]; then
 fi
 if [ "$PART" = t2 ]; then
   # name|env|flags
-  for v in ${T2_VARIANTS:-"t2|BPPO_HOST_THREADS=2|--shuffle-windows on" "t2gw|BPPO_HOST_THREADS=2 BPPO_SHUFFLE_GPU_WORDS=1|--shuffle-windows on" "t2np|BPPO_HOST_THREADS=2 BPPO_SHUFFLE_PAIR=0|--shuffle-windows on" "t2wp|BPPO_HOST_THREADS=2 BPPO_SHUFFLE_WIN_PRODUCERS=1|--shuffle-windows on"}; do
+  # variants separated by ';' (fields inside a variant by '|')
+  IFS=';' read -ra VS <<< "${T2_VARIANTS:-t2|BPPO_HOST_THREADS=2|--shuffle-windows on;t2gw|BPPO_HOST_THREADS=2 BPPO_SHUFFLE_GPU_WORDS=1|--shuffle-windows on;t2np|BPPO_HOST_THREADS=2 BPPO_SHUFFLE_PAIR=0|--shuffle-windows on;t2wp|BPPO_HOST_THREADS=2 BPPO_SHUFFLE_WIN_PRODUCERS=1|--shuffle-windows on}"
+  for v in "${VS[@]}"; do
     IFS='|' read -r name envs flags <<< "$v"
     timeout -k 10 300 env $envs python bench.py --no-learning --no-cpu-baseline $flags > gpurun_out/${TAG}_${name}.log 2>&1
     rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || { tail -3 gpurun_out/${TAG}_${name}.log; exit $rc; }
@@ -43,13 +45,19 @@ if [ "$PART" = t2 ]; then
 fi
 if [ "$PART" = wide ]; then
   # multi-player workloads on the current tree (name|bench_wide args)
-  for v in ${WIDE_VARIANTS:-"cfgC|--workload cfgC" "cfgD|--workload cfgD" "cnn64|--workload cfgC_cnn64" "cnn64f32|--workload cfgC_cnn64 --minibatch-kernel 2"}; do
-    IFS='|' read -r name args <<< "$v"
-    timeout -k 10 400 python scripts/bench_wide.py $args > gpurun_out/${TAG}_wide_${name}.log 2>&1
+  IFS=';' read -ra VS <<< "${WIDE_VARIANTS:-cfgC|--workload cfgC;cfgD|--workload cfgD;cnn64|--workload cfgC_cnn64;cnn64f32|--workload cfgC_cnn64 --minibatch-kernel 2}"
+  for v in "${VS[@]}"; do
+    IFS='|' read -r name args envs <<< "$v"
+    timeout -k 10 400 env ${envs:-BPPO_NOP=0} python scripts/bench_wide.py $args > gpurun_out/${TAG}_wide_${name}.log 2>&1
     rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || { tail -3 gpurun_out/${TAG}_wide_${name}.log; exit $rc; }
     tail -1 gpurun_out/${TAG}_wide_${name}.log | cut -c1-400
   done
   exit 0
+fi
+if [ "$PART" = cnn ]; then
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_cnn.py ${CNN_TESTS:-} -m gpu -v --timeout 300 --timeout-method thread -rf > gpurun_out/${TAG}_pytest_cnn.log 2>&1
+  rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|FAILED|Error|assert" gpurun_out/${TAG}_pytest_cnn.log | tail -20
+  exit $rc
 fi
 if [ "$PART" = cnnprobe ]; then
   timeout -k 10 600 python -u scripts/probes/${CNN_PROBE:-cnn_exact_probe}.py > gpurun_out/${TAG}_cnn_exact_probe.log 2>&1
@@ -59,7 +67,8 @@ fi
 if [ "$PART" = ab ]; then
   # interleaved A/B of env variants on the default bench line: AB_VARIANTS="name|VAR=x ..." (repeated AB_REPS times)
   for rep in $(seq 1 ${AB_REPS:-2}); do
-    for v in ${AB_VARIANTS:-"def|BPPO_MB_EVENTS=1" "ev0|BPPO_MB_EVENTS=0"}; do
+    IFS=';' read -ra VS <<< "${AB_VARIANTS:-def|BPPO_MB_EVENTS=1;ev0|BPPO_MB_EVENTS=0}"
+    for v in "${VS[@]}"; do
       IFS='|' read -r name envs <<< "$v"
       timeout -k 10 300 env $envs python bench.py --no-learning --no-cpu-baseline ${AB_FLAGS:-} > gpurun_out/${TAG}_ab_${name}_${rep}.log 2>&1
       rc=$?; echo "$name/$rep rc=$rc"; [ $rc -eq 0 ] || { tail -3 gpurun_out/${TAG}_ab_${name}_${rep}.log; exit $rc; }
@@ -76,6 +85,19 @@ if [ "$PART" = widekt ]; then
     DB=$(find gpurun_out/kt_${TAG}_$w -name "*.db" | head -1)
     python3 scripts/rocpd_summary.py $DB > gpurun_out/${TAG}_${w}_kernels.txt
     head -22 gpurun_out/${TAG}_${w}_kernels.txt | cut -c1-140
+  done
+  exit 0
+fi
+if [ "$PART" = fpprobe ]; then
+  timeout -k 10 120 ./scripts/probes/fp_rounding_probe > gpurun_out/${TAG}_fp_rounding_probe.txt 2>&1
+  rc=$?; echo "fp probe rc=$rc"; cat gpurun_out/${TAG}_fp_rounding_probe.txt
+  exit $rc
+fi
+if [ "$PART" = rostamp ]; then
+  # CfgB rollout segment stamps (diagnostic build burn-ppo_amd/bppo/libbppo_rostamps.so)
+  for L in ${RO_LIBS:-rostamps}; do
+    timeout -k 10 300 env BPPO_LIB_PATH=$GRAFT_REPO_ROOT/burn-ppo_amd/bppo/libbppo_$L.so python bench.py --steps 8 --warmup 0 --no-learning --no-cpu-baseline --no-gae-isolated > gpurun_out/${TAG}_$L.log 2>&1
+    rc=$?; echo "$L rc=$rc"; grep rostamp gpurun_out/${TAG}_$L.log | tail -1; [ $rc -eq 0 ] || exit $rc
   done
   exit 0
 fi

@@ -73,16 +73,16 @@ def test_cnn_forward_bit_exact(net):
     tr.close()
 
 
-# rtol of the update metrics: 1e-5, except the 64-channel net at N=1024 over
-# connect_four.toml's 6 epochs x 4 minibatches (24 Adam steps): 2e-4.  Its
-# single-minibatch gradient is within 1e-5 of each tensor's max
-# (test_cnn_single_minibatch_gradient); what grows over the steps is the f32
-# reduction-order difference of the conv weight gradients (sums over B*H*W
-# positions) amplified by Adam (m/sqrt(v): entries with near-zero gradient move
-# by ~lr either way) — measured 6e-5..1.1e-4 on approx_kl / value_mean, and
-# 0.18 % of the parameters beyond atol 2e-5 (max 1.7e-4 = 0.17 lr): parameter
-# atol 5e-4 for that case.
-@pytest.mark.parametrize("net,N,T,rtol", [(NETS[0], 64, 16, 1e-5), (NETS[1], 64, 12, 1e-5), (NETS[2], 1024, 8, 2e-4),
+# Every net at the north-star bar (1e-5 on the metrics, PARAM_RTOL / PARAM_ATOL on the
+# parameters), the reference-default 64-channel net at N = 1024 over connect_four.toml's
+# 6 epochs x 4 minibatches (24 Adam steps) included.  Until r04 that case needed 2e-4: its
+# conv weight gradients were f32 split-K sums over B*H*W positions, and a 1-ulp difference
+# in ~1 % of the parameters is enough for the PPO loss to carry the two runs apart by
+# 1e-5..1.5e-4 after a dozen steps (the oracle against itself with such a perturbation
+# does the same).  CNN nets now take their weight gradients in f64 (k_gemm_wg64), their
+# loss gradient in f64 and their input gradients in the oracle's chain order, so the
+# update follows the oracle's step for step.
+@pytest.mark.parametrize("net,N,T,rtol", [(NETS[0], 64, 16, 1e-5), (NETS[1], 64, 12, 1e-5), (NETS[2], 1024, 8, 1e-5),
                                           (NETS[3], 48, 10, 1e-5)])
 def test_cnn_rollout_update_second_rollout(net, N, T, rtol):
     from parity_util import PARAM_ATOL, PARAM_RTOL
@@ -95,8 +95,7 @@ def test_cnn_rollout_update_second_rollout(net, N, T, rtol):
     om = ot.update()
     assert tr.ctx.rng_pos() == ot.rng_pos()
     assert_metrics_close(m, om, values=ot.buffer("values"), returns=ot.buffer("returns"), rtol=rtol, advantages=ot.buffer("advantages"))
-    np.testing.assert_allclose(tr.model.get_params(), ot.params(), rtol=PARAM_RTOL,
-                               atol=PARAM_ATOL if rtol == 1e-5 else 5e-4)
+    np.testing.assert_allclose(tr.model.get_params(), ot.params(), rtol=PARAM_RTOL, atol=PARAM_ATOL)
     tr.model.set_params(ot.params())
     bppo.collect_rollouts(tr.ctx); ot.collect()
     _cmp(tr, ot)
@@ -159,9 +158,10 @@ def test_cnn_requires_observation_shape():
 
 def test_cnn_single_minibatch_gradient():
     """one minibatch over the whole buffer (1 epoch x 1 minibatch) from identical
-    parameters: losses within 1e-5 and every gradient entry within 1e-5 of its
-    tensor's largest entry (the device reduces the conv weight gradients over
-    B*H*W positions in f32 split-K partials summed in f64; the oracle in f64)."""
+    parameters: losses within 1e-5, and the gradient equal to the oracle's to the last bit
+    but in the rare entries whose f64 sum (device: v_mfma_f64 in its own order; oracle: row
+    order) lies within its ordering error of an f32 rounding boundary: at most one ulp
+    there, in at most 1e-4 of the entries."""
     import ctypes as C
     net = NETS[2]
     N, T = 1024, 8
@@ -188,25 +188,18 @@ def test_cnn_single_minibatch_gradient():
                                    C.byref(ms))
     for k in ("policy_loss", "value_loss", "entropy"):
         assert abs(m[k] - getattr(ms, k)) <= 1e-5 * max(abs(getattr(ms, k)), 1.0 if k == "policy_loss" else 0.0), k
-    shapes, _ = bppo.host.layer_shapes(cfg)
-    off = 0
-    for i, o in shapes:
-        for n in (i * o, o):
-            a, b = g[off:off + n], grads[off:off + n]
-            np.testing.assert_allclose(a, b, rtol=0, atol=1e-5 * max(np.abs(b).max(), 1e-30))
-            off += n
+    ulps = np.abs(g.view(np.int32).astype(np.int64) - grads.view(np.int32).astype(np.int64))
+    assert ulps.max() <= 1 and np.count_nonzero(ulps) <= max(2, g.size // 10000), (ulps.max(), np.count_nonzero(ulps))
     tr.close(); ot.close()
 
 
 def test_cnn_64ch_per_minibatch_drift():
-    """Where the 64-channel CNN update leaves the 1e-5 bar: the
+    """The 64-channel CNN update minibatch by minibatch: the
     per-minibatch statistics of the device (bppo_minibatch_rows) against the oracle's
-    (or_trainer_mb_log), minibatch by minibatch through connect_four.toml's 6 epochs x
-    4 minibatches.  Minibatch 0 runs from identical parameters: its statistics must be
-    within 1e-5; after it, each Adam step carries the previous steps' last-bit
-    gradient differences (f32 split-K partials vs the oracle's f64 conv-weight sums)
-    into the parameters, and the test records at which minibatch the first statistic
-    passes 1e-5 (gpurun_out/cnn64_minibatch_drift.json when run on the box)."""
+    (or_trainer_mb_log) through connect_four.toml's 6 epochs x 4 minibatches, every one
+    within 1e-5 (r04, with f32 split-K conv weight gradients: minibatch 12 was the first past
+    it, 1.4e-4 by minibatch 20).  The record goes to gpurun_out/cnn64_minibatch_drift.json
+    when run on the box."""
     import json
     import os
     net = NETS[2]
@@ -241,5 +234,6 @@ def test_cnn_64ch_per_minibatch_drift():
         print(json.dumps({k: out[k] for k in ("first_minibatch_over_1e-5", "minibatches")}),
               [round(p["max_rel"], 8) for p in per])
         assert per[0]["max_rel"] <= 1e-5, per[0]       # identical parameters: within the bar
+        assert first is None, per[first]                # and every later minibatch (r04: #12 was the first out)
     finally:
         tr.close(); ot.close()
