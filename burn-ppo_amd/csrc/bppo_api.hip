@@ -295,7 +295,11 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     TRY(dalloc(c, &c->d_act, TN));
     if (!c->wide || cfg->normalize_returns) TRY(dalloc(c, &c->d_X, TN));
     if (!c->wide && cfg->hidden_size == 64 && cfg->num_hidden == 2 && cfg->relu)
+    {
         TRY(dalloc(c, &c->d_gumbel, TN * 2));
+        TRY(dalloc(c, &c->d_rpool, (size_t)RPOOL_K * c->N));
+        TRY(dalloc(c, &c->d_rpos, (size_t)RPOOL_K * c->N));
+    }
     TRY(dalloc(c, &c->d_on, (size_t)2 * c->D + 1));
     if (!c->wide) TRY(dalloc(c, &c->d_obs_part, (size_t)c->N * 2 * c->D));
     if (!c->wide) {   // VecEnv::step / get_observations scratch (freed by wide_free with the rest)
@@ -400,7 +404,7 @@ extern "C" void bppo_destroy(bppo_ctx *c) {
                     c->d_done, c->d_val, c->d_logp, c->d_adv, c->d_ret, c->d_act, c->d_X, c->d_on,
                     c->d_obs_part, c->d_rn_returns, c->d_rn_stats, c->d_scan_agg, c->d_last_v,
                     c->d_eps, c->d_ep_count, c->d_ep_sum, c->d_err, c->d_perm_base, c->d_perm_ep, c->d_inv_ep, c->d_advpart, c->d_fy, c->d_scan,
-                    c->d_red, c->d_mb_stats, c->d_gumbel, c->d_rows, c->d_rowA, c->d_rowB};
+                    c->d_red, c->d_mb_stats, c->d_gumbel, c->d_rpool, c->d_rpos, c->d_rows, c->d_rowA, c->d_rowB};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     fy_ranges_free(c->fyr);
     if (c->h_red) (void)hipHostFree(c->h_red);
@@ -1085,7 +1089,7 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
             }
             float *metric_dst = c->d_rows + (size_t)nrow * (NM + 4);
             const bool multi = c->allreduce && c->world > 1;
-            if (c->wide) TRY(wide_minibatch(c, (uint32_t)start, (uint32_t)sz, ent_coef));
+            if (c->wide) TRY(wide_minibatch(c, (uint32_t)start, (uint32_t)sz, ent_coef, first_mb));
             else TRY(launch_minibatch(c, (uint32_t)start, (uint32_t)sz, (float)ent_coef, first_mb));
             if (fw_timed) BPPO_HIP(c, hipEventRecord(c->ev[TM_FWDBWD][1], c->stream));
             first_mb = false;

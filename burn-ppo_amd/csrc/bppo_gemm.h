@@ -10,9 +10,10 @@ constexpr int GEMM_MAX_SPLITS = 1024;   // narrow conv weight gradients (Kin x C
 // go to out0 (ld0), [n0, N) to out1 (ld1) when out1 != nullptr.  Bit-exact
 // with matrixmultiply's KC=256 k-ordered fma chains (see k_gemm.hip).
 // act: 0 none, 1 relu, 2 tanh (glibc tanhf, bit-exact).
+// split != 0: the split-bf16 contraction (k_gemm_split: f32 accuracy, not the chains)
 hipError_t gemm_fwd(hipStream_t st, int M, int N, int K, const float *X, int ldx, const float *W,
                     int ldw, const float *bias, int act, float *out0, int ld0, int n0, float *out1,
-                    int ld1);
+                    int ld1, int split = 0);
 // out = (dZ W^T) * act'(H) given the layer OUTPUT H (may be null: no factor):
 // act 2 tanh -> (1 - H^2), otherwise relu -> [H > 0].  dZ [M][K] (ldz), W [N][K] (ldw).
 // Each element is the k-ordered fmaf chain from 0 (the oracle's linear_bwd dx).  xa / xw
@@ -21,14 +22,15 @@ hipError_t gemm_fwd(hipStream_t st, int M, int N, int K, const float *X, int ldx
 // value head beside the policy head's chain)
 hipError_t gemm_dx(hipStream_t st, int M, int N, int K, const float *dZ, int ldz, const float *W,
                    int ldw, const float *H, int ldh, int act, float *out, int ldo, const float *xa = nullptr,
-                   int ldxa = 0, const float *xw = nullptr);
+                   int ldxa = 0, const float *xw = nullptr, int split = 0);
 // dW = X^T dZ over `rows` rows: X [rows][Kin] (ldx), dZ [rows][N] (ldz).
 // Columns [0, n0) -> dW0 [Kin][ldw0], [n0, N) -> dW1 [Kin][ldw1] (when dW1);
 // bias gradient (column sums of dZ) -> db0 / db1 likewise (either may be null).
 // part: [splits][Kin][N] scratch, colsum: [splits][N] scratch (sized for doubles when exact).
 // exact 0: f32 MFMA chains per split, f64 reduce; 1: f64 products and sums (k_gemm_wg64),
 // the f32 result equal to the oracle's f64 sum's rounding but for rare ordering ties;
-// 2: row-ordered f64 sums (k_wg_seq), the oracle's arithmetic exactly (latency-bound).
+// 2: row-ordered f64 sums (k_wg_seq), the oracle's arithmetic exactly (latency-bound);
+// -1: the split-bf16 contraction (k_gemm_split) per split, f64 reduce.
 hipError_t gemm_wgrad(hipStream_t st, int Kin, int N, int rows, const float *X, int ldx, const float *dZ,
                       int ldz, float *part, float *colsum, float *dW0, int ldw0, int n0, float *dW1, int ldw1,
                       float *db0, float *db1, int splits, int exact = 0);

@@ -45,6 +45,7 @@ NetLayout make_layout(const bppo_config &c, int obs_dim, int priv_dim, int act_d
 
 // episode record written by the rollout kernel
 constexpr int EP_SUMMARY_BLOCKS = 128;   // k_ep_summary grid (partial sums per block)
+constexpr int RPOOL_K = 16;              // CfgB rollout: reset states drawn ahead per env (k_reset_pool)
 constexpr int TM_SLOTS = 10;             // phase timer event pairs (enum TM_* below)
 constexpr int ROLL_HOST_WORDS = 2 + 2 * EP_SUMMARY_BLOCKS;     // pinned doubles per rollout slot
 constexpr int ADV_STREAM_BLOCKS = 512, ADV_STREAM_MAXM = 16;   // k_adv_stream grid, most minibatches
@@ -275,6 +276,8 @@ struct bppo_ctx {
     int32_t *d_act = nullptr;
     double *d_X = nullptr;            // rolling returns per (t,e) for the return-normalizer scan
     float *d_gumbel = nullptr;        // CfgB MFMA rollout: Gumbel noise [T][N][2], made ahead of it
+    float4 *d_rpool = nullptr;        // CfgB MFMA rollout: each env's next RPOOL_K reset states [K][N], made ahead of it
+    uint64_t *d_rpos = nullptr;       //   and the stream position after each [K][N]
     // normalizers
     double *d_on = nullptr;           // [3][D]: mean, M2, (count in slot) ; host mirror below
     std::vector<double> on_mean, on_m2;
@@ -481,7 +484,8 @@ bppo_status wide_init(bppo_ctx *c);
 void wide_free(bppo_ctx *c);
 bppo_status wide_reset(bppo_ctx *c);
 bppo_status wide_pack(bppo_ctx *c);
-bppo_status wide_forward(bppo_ctx *c, int rows, const float *xc, int ldxc, float *logits, float *values);
+bppo_status wide_forward(bppo_ctx *c, int rows, const float *xc, int ldxc, float *logits, float *values,
+                         int split = 0);   // split: the update GEMMs on k_gemm_split (wide_minibatch)
 bppo_status wide_forward_actor(bppo_ctx *c, int rows, const float *xc, int ldxc, const float *params, float *logits);
 // CNN trunk (cnn.hip): conv stack + flatten of `rows` obs rows -> d_cnn_f; backward
 // of the conv stack from dF (dL/d features, [rows][fdim]) into the gradient
@@ -512,7 +516,7 @@ bppo_status opp_compact_valid(bppo_ctx *c);
 bppo_status opp_map_perm(bppo_ctx *c, uint32_t n);
 bppo_status wide_collect(bppo_ctx *c, uint64_t base);
 bppo_status wide_bootstrap_gae(bppo_ctx *c);
-bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, double ent_coef);
+bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, double ent_coef, bool first);
 bppo_status wide_observe_host(bppo_ctx *c, float *obs, int32_t *players, uint8_t *masks, float *priv);
 bppo_status wide_step_host(bppo_ctx *c, const int32_t *actions, float *obs, float *rewards, uint8_t *dones,
                            int32_t *n_eps);

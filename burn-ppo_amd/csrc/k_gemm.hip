@@ -161,6 +161,7 @@ struct GemmArgs {
     // reduction per split (float, or double for k_gemm_wg64)
     float *part; float *colsum; int k_per_split;
     int xcd;                     // XCD-aware tile order (tile_of)
+    int avec, bvec;              // k_gemm_split: operand 16-B aligned with ld % 4 == 0 (float4 loads)
 };
 
 enum { GEMM_FWD = 0, GEMM_DX = 1, GEMM_WG = 2 };
@@ -179,9 +180,46 @@ __device__ __forceinline__ Tile tile_of(int xcd) {
     return Tile{(int)(b % gx), (int)((b / gx) % gy), (int)(b / (gx * gy))};
 }
 
+// ---- epilogue of a wave's TM x TN 32x32 accumulator tiles at (mw, nw): C/D map
+// col = lane & 31, row = (q & 3) + 8 (q >> 2) + 4 (lane >> 5)
+template <int MODE, int TM, int TN>
+__device__ __forceinline__ void gemm_epilogue(const GemmArgs &g, const f32x16 (&acc)[TM][TN], const Tile &tl, int mw,
+                                              int nw, int lane) {
+    const int col_l = lane & 31, rq = 4 * (lane >> 5);
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++) {
+            const int col = nw + j * 32 + col_l;
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const int row = mw + i * 32 + (q & 3) + 8 * (q >> 2) + rq;
+                if (row >= g.M || col >= g.N) continue;
+                float v = acc[i][j][q];
+                if constexpr (MODE == GEMM_FWD) {
+                    v = __fadd_rn(v, g.bias[col]);
+                    if (g.act == 1) v = v > 0.0f ? v : 0.0f;
+                    if (col < g.n0) g.out0[(size_t)row * g.ld0 + col] = v;
+                    else g.out1[(size_t)row * g.ld1 + (col - g.n0)] = v;
+                } else if constexpr (MODE == GEMM_DX) {
+                    if (g.xa) v = __fadd_rn(v, __fmul_rn(g.xa[(size_t)row * g.ldxa], g.xw[col]));
+                    if (g.H) {
+                        const float hv = g.H[(size_t)row * g.ldh + col];
+                        if (g.dact == 2) v = __fmul_rn(v, __fsub_rn(1.0f, __fmul_rn(hv, hv)));
+                        else if (!(hv > 0.0f)) v = 0.0f;
+                    }
+                    g.out0[(size_t)row * g.ld0 + col] = v;
+                } else {
+                    g.part[((size_t)tl.z * g.M + row) * g.N + col] = v;
+                }
+            }
+        }
+}
+
 template <int MODE, int BM, int BN, int WM, int WN, int AK>
 __global__ void __launch_bounds__(256, 2) k_gemm(GemmArgs g) {
     using S = GemmShape<BM, BN, WM, WN>;
+    constexpr int TM_ = S::TM, TN_ = S::TN;
     constexpr bool A_KC = MODE != GEMM_WG;        // FWD/DX: A row-major [M][K]; WG: A = X^T, X [K][M]
     constexpr bool B_KC = MODE == GEMM_DX;        // FWD: W [K][N]; DX: W [N][K]; WG: dZ [K][N]
     __shared__ float sA[2][GBK * S::APAD];
@@ -303,36 +341,7 @@ __global__ void __launch_bounds__(256, 2) k_gemm(GemmArgs g) {
                     for (int q = 0; q < 16; q++) acc[i][j][q] = __fadd_rn(tot[i][j][q], acc[i][j][q]);
         }
     }
-    // ---- epilogue: C/D map col = lane&31, row = (q&3) + 8*(q>>2) + 4*(lane>>5)
-    const int col_l = lane & 31, rq = 4 * (lane >> 5);
-#pragma unroll
-    for (int i = 0; i < S::TM; i++)
-#pragma unroll
-        for (int j = 0; j < S::TN; j++) {
-            const int col = n0 + (wn * S::TN + j) * 32 + col_l;
-#pragma unroll
-            for (int q = 0; q < 16; q++) {
-                const int row = m0 + (wm * S::TM + i) * 32 + (q & 3) + 8 * (q >> 2) + rq;
-                if (row >= g.M || col >= g.N) continue;
-                float v = acc[i][j][q];
-                if constexpr (MODE == GEMM_FWD) {
-                    v = __fadd_rn(v, g.bias[col]);
-                    if (g.act == 1) v = v > 0.0f ? v : 0.0f;
-                    if (col < g.n0) g.out0[(size_t)row * g.ld0 + col] = v;
-                    else g.out1[(size_t)row * g.ld1 + (col - g.n0)] = v;
-                } else if constexpr (MODE == GEMM_DX) {
-                    if (g.xa) v = __fadd_rn(v, __fmul_rn(g.xa[(size_t)row * g.ldxa], g.xw[col]));
-                    if (g.H) {
-                        const float hv = g.H[(size_t)row * g.ldh + col];
-                        if (g.dact == 2) v = __fmul_rn(v, __fsub_rn(1.0f, __fmul_rn(hv, hv)));
-                        else if (!(hv > 0.0f)) v = 0.0f;
-                    }
-                    g.out0[(size_t)row * g.ld0 + col] = v;
-                } else {
-                    g.part[((size_t)tl.z * g.M + row) * g.N + col] = v;
-                }
-            }
-        }
+    gemm_epilogue<MODE, TM_, TN_>(g, acc, tl, m0 + wm * S::TM * 32, n0 + wn * S::TN * 32, lane);
     if (do_colsum) {
         __shared__ float red[256];
         red[tid] = csum;
@@ -342,6 +351,213 @@ __global__ void __launch_bounds__(256, 2) k_gemm(GemmArgs g) {
             for (int p = 0; p < 256 / BN; p++) s += red[tid + p * BN];
             const int col = n0 + tid;
             if (col < g.N) g.colsum[(size_t)tl.z * g.N + col] = s;
+        }
+    }
+}
+
+// ---- split-bf16 contraction (every update minibatch after the first) -----------------
+// The forward, input-gradient and weight-gradient GEMMs of the update's later minibatches
+// need f32 ACCURACY, not the reference's rounding: their parameters already differ from
+// the reference's in the last bits after the first Adam step (the first minibatch keeps
+// the exact k_gemm chains: ratio exactly 1).  Each f32 operand is split exactly into three
+// bf16 pieces x = x0 + x1 + x2 (8 significand bits each, round-to-nearest) when its LDS
+// stage is filled -- once per block, not per wave -- and the six products of order <= 2
+// (x2y0, x1y1, x0y2, x1y0, x0y1, x0y0, smallest first) accumulate in f32 on
+// v_mfma_f32_32x32x16_bf16: |x1| <= 2^-8 |x|, |x2| <= 2^-16 |x|, so the dropped products
+// are within (2^-23 + 2^-32) |xy| (tests/test_split_bf16.py), and 6 MFMAs of 32 cycles do
+// the work of 8 f32 MFMAs of 64 cycles (2.7x the f32 MFMA rate; MI355X guide: 32x32x16
+// bf16 = 16x the f32 rate per FLOP).
+// LDS: the three piece images of A [BM][KP] and B [BN][KP] for one GBK = 32 stage, k
+// contiguous (one ds_read_b128 per 8-k fragment), row stride KP = 40 bf16 (80 B: the 32
+// rows of a fragment read hit distinct bank groups); one stage (60 KB at 128 x 128, two
+// blocks per CU), the next stage's f32 values prefetched into registers under the MFMAs.
+typedef __bf16 sbf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 sbf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 sbf16x2 __attribute__((ext_vector_type(2)));
+constexpr int SKP = GBK + 8;
+
+// three pieces of Q consecutive-k values -> LDS rows at s[p * plane + off]
+template <int Q>
+__device__ __forceinline__ void split_store(const float *x, __bf16 *s, int plane, int off) {
+    __bf16 p0[Q], p1[Q], p2[Q];
+#pragma unroll
+    for (int j = 0; j < Q; j++) {
+        const __bf16 a = (__bf16)x[j];
+        const float r = x[j] - (float)a;
+        const __bf16 b = (__bf16)r;
+        p0[j] = a; p1[j] = b; p2[j] = (__bf16)(r - (float)b);
+    }
+    if constexpr (Q == 4) {
+        *reinterpret_cast<sbf16x4 *>(s + off) = sbf16x4{p0[0], p0[1], p0[2], p0[3]};
+        *reinterpret_cast<sbf16x4 *>(s + plane + off) = sbf16x4{p1[0], p1[1], p1[2], p1[3]};
+        *reinterpret_cast<sbf16x4 *>(s + 2 * plane + off) = sbf16x4{p2[0], p2[1], p2[2], p2[3]};
+    } else if constexpr (Q == 2) {
+        *reinterpret_cast<sbf16x2 *>(s + off) = sbf16x2{p0[0], p0[1]};
+        *reinterpret_cast<sbf16x2 *>(s + plane + off) = sbf16x2{p1[0], p1[1]};
+        *reinterpret_cast<sbf16x2 *>(s + 2 * plane + off) = sbf16x2{p2[0], p2[1]};
+    } else {
+        s[off] = p0[0]; s[plane + off] = p1[0]; s[2 * plane + off] = p2[0];
+    }
+}
+
+// four consecutive elements of a row of `base` from `idx` (bounded by `lim`): one float4
+// when the operand is aligned (vec) and the quad is whole, else guarded scalars
+__device__ __forceinline__ void load4(const float *__restrict__ base, size_t row_off, int idx, int lim, bool vec,
+                                      bool row_ok, float (&v)[4]) {
+    if (row_ok && vec && idx + 3 < lim) {
+        const float4 q = *reinterpret_cast<const float4 *>(base + row_off + idx);
+        v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+    } else {
+#pragma unroll
+        for (int u = 0; u < 4; u++) v[u] = (row_ok && idx + u < lim) ? base[row_off + idx + u] : 0.0f;
+    }
+}
+
+// one operand's GBK x R stage.  KCONTIG (element (r, k) at base[r ld + k]): thread -> rows
+// (tid >> 3) + 32 e, k quad (tid & 7) * 4.  k-major (element at base[k ld + r]): thread ->
+// KQ consecutive k (KQ = 4, 2, 1 for R = 128, 64, 32) times an r quad, so each piece row
+// segment it writes is KQ contiguous k's.
+template <int R, bool KCONTIG>
+struct SplitLoader {
+    static constexpr int E = GBK * R / 256;            // elements per thread
+    static constexpr int KQ = KCONTIG ? 4 : E / 4;     // consecutive k per piece write
+    static constexpr int NKB = GBK / KQ;               // k-major: k blocks per r quad
+    float v[E];
+    __device__ __forceinline__ void load(const float *__restrict__ base, int ld, int r0, int rmax, int k0, int kmax,
+                                         int tid, bool vec) {
+        if constexpr (KCONTIG) {
+#pragma unroll
+            for (int e = 0; e < E / 4; e++) {
+                const int r = r0 + (tid >> 3) + 32 * e, k = k0 + (tid & 7) * 4;
+                float q[4];
+                load4(base, (size_t)r * ld, k, kmax, vec, r < rmax, q);
+#pragma unroll
+                for (int u = 0; u < 4; u++) v[4 * e + u] = q[u];
+            }
+        } else {
+            const int kb = (tid % NKB) * KQ, r4 = (tid / NKB) * 4;
+#pragma unroll
+            for (int j = 0; j < KQ; j++) {
+                const int k = k0 + kb + j;
+                float q[4];
+                load4(base, (size_t)k * ld, r0 + r4, rmax, vec, k < kmax, q);
+#pragma unroll
+                for (int u = 0; u < 4; u++) v[4 * j + u] = q[u];
+            }
+        }
+    }
+    // pieces into s (three planes of R * SKP)
+    __device__ __forceinline__ void store(__bf16 *s, int tid) const {
+        constexpr int plane = R * SKP;
+        if constexpr (KCONTIG) {
+#pragma unroll
+            for (int e = 0; e < E / 4; e++)
+                split_store<4>(v + 4 * e, s, plane, ((tid >> 3) + 32 * e) * SKP + (tid & 7) * 4);
+        } else {
+            const int kb = (tid % NKB) * KQ, r4 = (tid / NKB) * 4;
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                float x[KQ];
+#pragma unroll
+                for (int j = 0; j < KQ; j++) x[j] = v[4 * j + u];
+                split_store<KQ>(x, s, plane, (r4 + u) * SKP + kb);
+            }
+        }
+    }
+    // k-major: column sums of this thread's KQ k's per r (the bias gradient of WG's B)
+    __device__ __forceinline__ void colsum(float (&cs)[4]) const {
+        if constexpr (!KCONTIG) {
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+#pragma unroll
+                for (int j = 0; j < KQ; j++) cs[u] += v[4 * j + u];
+        }
+    }
+};
+
+__device__ __forceinline__ void mfma6_split(f32x16 &acc, const sbf16x8 (&a)[3], const sbf16x8 (&b)[3]) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
+}
+
+template <int MODE, int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(256, 2) k_gemm_split(GemmArgs g) {
+    using S = GemmShape<BM, BN, WM, WN>;
+    constexpr bool A_KC = MODE != GEMM_WG;
+    constexpr bool B_KC = MODE == GEMM_DX;
+    __shared__ __attribute__((aligned(16))) __bf16 sA[3 * BM * SKP];
+    __shared__ __attribute__((aligned(16))) __bf16 sB[3 * BN * SKP];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const Tile tl = tile_of(g.xcd);
+    const int m0 = tl.y * BM, n0 = tl.x * BN;
+    int kbeg = 0, kend = g.K;
+    if constexpr (MODE == GEMM_WG) {
+        kbeg = tl.z * g.k_per_split;
+        kend = min(g.K, kbeg + g.k_per_split);
+    }
+    SplitLoader<BM, A_KC> la;
+    SplitLoader<BN, B_KC> lb;
+    f32x16 acc[S::TM][S::TN];
+#pragma unroll
+    for (int i = 0; i < S::TM; i++)
+#pragma unroll
+        for (int j = 0; j < S::TN; j++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[i][j][r] = 0.0f;
+    float cs[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    const bool do_colsum = MODE == GEMM_WG && g.colsum != nullptr && tl.y == 0;
+    const int r = lane & 31, h = lane >> 5;
+
+    la.load(g.A, g.lda, m0, g.M, kbeg, kend, tid, g.avec);
+    lb.load(g.B, g.ldb, n0, g.N, kbeg, kend, tid, g.bvec);
+    for (int k0 = kbeg; k0 < kend; k0 += GBK) {
+        if (k0 != kbeg) __syncthreads();          // every wave done reading the previous stage
+        la.store(sA, tid);
+        lb.store(sB, tid);
+        if (do_colsum) lb.colsum(cs);
+        __syncthreads();
+        if (k0 + GBK < kend) {                    // the next stage's values, in flight under the MFMAs
+            la.load(g.A, g.lda, m0, g.M, k0 + GBK, kend, tid, g.avec);
+            lb.load(g.B, g.ldb, n0, g.N, k0 + GBK, kend, tid, g.bvec);
+        }
+#pragma unroll
+        for (int kk = 0; kk < GBK; kk += 16) {
+            sbf16x8 af[S::TM][3], bf[S::TN][3];
+#pragma unroll
+            for (int i = 0; i < S::TM; i++)
+#pragma unroll
+                for (int p = 0; p < 3; p++)
+                    af[i][p] = *reinterpret_cast<const sbf16x8 *>(sA + p * BM * SKP + ((wm * S::TM + i) * 32 + r) * SKP + kk + 8 * h);
+#pragma unroll
+            for (int j = 0; j < S::TN; j++)
+#pragma unroll
+                for (int p = 0; p < 3; p++)
+                    bf[j][p] = *reinterpret_cast<const sbf16x8 *>(sB + p * BN * SKP + ((wn * S::TN + j) * 32 + r) * SKP + kk + 8 * h);
+#pragma unroll
+            for (int i = 0; i < S::TM; i++)
+#pragma unroll
+                for (int j = 0; j < S::TN; j++) mfma6_split(acc[i][j], af[i], bf[j]);
+        }
+    }
+    gemm_epilogue<MODE, S::TM, S::TN>(g, acc, tl, m0 + wm * S::TM * 32, n0 + wn * S::TN * 32, lane);
+    if (do_colsum) {
+        // the NKB threads of an r quad are consecutive lanes of one wave
+        constexpr int NKB = SplitLoader<BN, false>::NKB;
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+#pragma unroll
+            for (int o = 1; o < NKB; o <<= 1) cs[u] += __shfl_xor(cs[u], o, 64);
+        if (tid % NKB == 0) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int col = n0 + (tid / NKB) * 4 + u;
+                if (col < g.N) g.colsum[(size_t)tl.z * g.N + col] = cs[u];
+            }
         }
     }
 }
@@ -553,6 +769,22 @@ static hipError_t launch(GemmArgs g, int splits, hipStream_t st) {
     return hipGetLastError();
 }
 
+static bool vec_ok(const float *p, int ld) { return ((uintptr_t)p & 15) == 0 && (ld & 3) == 0; }
+template <int MODE, int BM, int BN, int WM, int WN>
+static hipError_t launch_split(GemmArgs g, int splits, hipStream_t st) {
+    dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, splits);
+    g.xcd = gemm_xcd();
+    g.avec = vec_ok(g.A, g.lda); g.bvec = vec_ok(g.B, g.ldb);
+    hipLaunchKernelGGL((k_gemm_split<MODE, BM, BN, WM, WN>), grid, dim3(256), 0, st, g);
+    return hipGetLastError();
+}
+template <int MODE>
+static hipError_t launch_split_by_width(const GemmArgs &g, int splits, hipStream_t st) {
+    if (g.N <= 32) return launch_split<MODE, 128, 32, 4, 1>(g, splits, st);
+    if (g.N <= 64) return launch_split<MODE, 128, 64, 4, 1>(g, splits, st);
+    return launch_split<MODE, 128, 128, 2, 2>(g, splits, st);
+}
+
 template <int BM, int BN, int AK>
 static hipError_t launch64(GemmArgs g, int splits, hipStream_t st) {
     dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, splits);
@@ -577,13 +809,13 @@ static hipError_t launch_by_width(const GemmArgs &g, int splits, hipStream_t st)
 
 hipError_t gemm_fwd(hipStream_t st, int M, int N, int K, const float *X, int ldx, const float *W,
                     int ldw, const float *bias, int act, float *out0, int ld0, int n0, float *out1,
-                    int ld1) {
+                    int ld1, int split) {
     if (M <= 0 || N <= 0) return hipSuccess;
     GemmArgs g{};
     g.A = X; g.lda = ldx; g.B = W; g.ldb = ldw; g.M = M; g.N = N; g.K = K;
     g.bias = bias; g.act = act == 1 ? 1 : 0;
     g.out0 = out0; g.ld0 = ld0; g.n0 = out1 ? n0 : N; g.out1 = out1; g.ld1 = ld1;
-    hipError_t e = launch_by_width<GEMM_FWD>(g, 1, st);
+    hipError_t e = split ? launch_split_by_width<GEMM_FWD>(g, 1, st) : launch_by_width<GEMM_FWD>(g, 1, st);
     if (e != hipSuccess || act != 2) return e;
     if ((e = tanh_inplace(st, out0, M, g.n0, ld0)) != hipSuccess) return e;
     return out1 ? tanh_inplace(st, out1, M, N - g.n0, ld1) : hipSuccess;
@@ -621,13 +853,13 @@ hipError_t gemm_conv_dx(hipStream_t st, int rows, int Cin, int Co, int ks, const
 
 hipError_t gemm_dx(hipStream_t st, int M, int N, int K, const float *dZ, int ldz, const float *W,
                    int ldw, const float *H, int ldh, int act, float *out, int ldo, const float *xa, int ldxa,
-                   const float *xw) {
+                   const float *xw, int split) {
     if (M <= 0 || N <= 0) return hipSuccess;
     GemmArgs g{};
     g.A = dZ; g.lda = ldz; g.B = W; g.ldb = ldw; g.M = M; g.N = N; g.K = K;
     g.H = H; g.ldh = ldh; g.dact = act == 2 ? 2 : 1; g.out0 = out; g.ld0 = ldo; g.n0 = N;
     g.xa = xa; g.ldxa = ldxa; g.xw = xw;
-    return launch_by_width<GEMM_DX>(g, 1, st);
+    return split ? launch_split_by_width<GEMM_DX>(g, 1, st) : launch_by_width<GEMM_DX>(g, 1, st);
 }
 
 int gemm_wg_splits(int Kin, int N, int rows) {
@@ -679,9 +911,11 @@ static hipError_t wgrad(hipStream_t st, const ConvA &cv, int Kin, int N, int row
     g.k_per_split = ((rows + splits - 1) / splits + GBK - 1) / GBK * GBK;
     const int sp = (rows + g.k_per_split - 1) / g.k_per_split;
     hipError_t e;
-    if (exact) e = cv.kind ? launch64_by_width<1>(g, sp, st) : launch64_by_width<0>(g, sp, st);
+    if (exact < 0 && cv.kind == 0) e = launch_split_by_width<GEMM_WG>(g, sp, st);
+    else if (exact > 0) e = cv.kind ? launch64_by_width<1>(g, sp, st) : launch64_by_width<0>(g, sp, st);
     else e = cv.kind ? launch_by_width<GEMM_WG, 1>(g, sp, st) : launch_by_width<GEMM_WG>(g, sp, st);
     if (e != hipSuccess) return e;
+    if (exact < 0) exact = 0;                 // f32 partials either way
     const size_t MN = (size_t)Kin * N;
     const int nn0 = dW1 ? n0 : N;
     if (exact)
@@ -710,14 +944,22 @@ static hipError_t wgrad(hipStream_t st, const ConvA &cv, int Kin, int N, int row
 // bppo_debug_gemm: host buffers in/out; mode 0 FWD (bias, act 0 none / 1 relu /
 // 2 tanh), 1 DX (H optional: act 2 tanh derivative, else relu mask), 2 WG
 // (out = [Kin][N] weight grad, out2 = [N] bias grad), 3 WG with f64 sums (k_gemm_wg64),
-// 4 WG with row-ordered f64 sums (k_wg_seq).
+// 4 WG with row-ordered f64 sums (k_wg_seq), 5 / 6 / 7: FWD / DX / WG on the split-bf16
+// contraction (k_gemm_split).
 extern "C" bppo_status bppo_debug_gemm(int32_t mode, int32_t M, int32_t N, int32_t K, const float *A,
                                        const float *B, const float *bias_or_H, int32_t act, float *out,
                                        float *out2) {
     using namespace bppo;
-    if (!A || !B || !out || M <= 0 || N <= 0 || K <= 0 || mode < 0 || mode > 4) return BPPO_ERR_ARG;
-    const int exact = mode >= 3 ? mode - 2 : 0;   // 3: f64 MFMA sums, 4: row-ordered f64 sums
-    if (exact) mode = 2;
+    if (!A || !B || !out || M <= 0 || N <= 0 || K <= 0 || mode < 0 || mode > 7) return BPPO_ERR_ARG;
+    int exact = 0, split = 0;
+    if (mode >= 5) {                   // split-bf16
+        split = 1;
+        mode -= 5;
+        if (mode == 2) exact = -1;
+    } else if (mode >= 3) {            // 3: f64 MFMA sums, 4: row-ordered f64 sums
+        exact = mode - 2;
+        mode = 2;
+    }
     float *dA = nullptr, *dB = nullptr, *dX = nullptr, *dO = nullptr, *dO2 = nullptr, *dP = nullptr, *dC = nullptr;
     size_t nA = mode == 2 ? (size_t)K * M : (size_t)M * K;   // WG: X [rows=K][Kin=M]
     size_t nB = mode == 1 ? (size_t)N * K : (size_t)K * N;
@@ -736,9 +978,9 @@ extern "C" bppo_status bppo_debug_gemm(int32_t mode, int32_t M, int32_t N, int32
         hipError_t e;
         if (mode == 0) {
             if (!dX) break;
-            e = gemm_fwd(nullptr, M, N, K, dA, K, dB, N, dX, act, dO, N, N, nullptr, 0);
+            e = gemm_fwd(nullptr, M, N, K, dA, K, dB, N, dX, act, dO, N, N, nullptr, 0, split);
         } else if (mode == 1) {
-            e = gemm_dx(nullptr, M, N, K, dA, K, dB, K, dX, N, act, dO, N, nullptr, 0, nullptr);
+            e = gemm_dx(nullptr, M, N, K, dA, K, dB, K, dX, N, act, dO, N, nullptr, 0, nullptr, split);
         } else {
             if (hipMalloc((void **)&dO2, (size_t)N * 4) != hipSuccess) break;
             if (hipMalloc((void **)&dP, (size_t)splits * M * N * 8) != hipSuccess) break;

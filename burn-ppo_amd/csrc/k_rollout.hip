@@ -117,6 +117,7 @@ struct RolloutArgs {
     int32_t *err;
     float4 *rows;        // MFMA rollout: also the update's rows A [B][2] float4 (k_update.hip load_row), or null
     unsigned long long *stamps;   // diagnostic build only (BPPO_RO_STAMPS): per-wave segment cycles
+    const float4 *rpool; const uint64_t *rpos; int rpool_k;   // 64-lane MFMA rollout: k_reset_pool's states
 };
 
 // diagnostic build (-DBPPO_RO_STAMPS): s_memtime segment sums per wave of the 64-lane CfgB
@@ -253,6 +254,29 @@ __global__ void __launch_bounds__(GUM_THREADS) k_gumbel_words(Key8 key, uint64_t
         const int k = j * GUM_THREADS + threadIdx.x;
         const uint64_t w = wb + k;
         if (w >= base && w < base + count) g[w - base] = tile[k + (k >> 5)];
+    }
+}
+
+// The next K reset states of every env, drawn ahead of the 64-lane rollout from the env's
+// own stream (cartpole.rs:275-278: four gen_range draws with rejection, from env_pos on),
+// with the stream position after each.  In the rollout a reset is then a register copy of
+// a prefetched entry instead of a ChaCha block evaluated under divergence: any of a wave's
+// 64 lanes finishing an episode made the whole wave wait on one (segment stamps: 1.7k of
+// 23.7k cycles per step, profiles/r05b/rollout_stamps.txt).  Entries [j][e]: the threads
+// of a wave write consecutive envs.  An env that resets more than K times in one rollout
+// falls back to drawing in the kernel (bit-identical: the same cursor, from the position
+// after entry K - 1).
+__global__ void __launch_bounds__(256) k_reset_pool(int N, int K, uint64_t seed_base, const uint64_t *__restrict__ env_pos,
+                                                    float4 *__restrict__ pool, uint64_t *__restrict__ ppos) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= N) return;
+    WordCursor c;
+    c.init(seed_key(seed_base + (uint64_t)e), 0, env_pos[e]);
+    for (int j = 0; j < K; j++) {
+        CartPoleState s;
+        cartpole_reset(s, c);
+        pool[(size_t)j * N + e] = make_float4(s.x, s.x_dot, s.theta, s.theta_dot);
+        ppos[(size_t)j * N + e] = c.pos;
     }
 }
 
@@ -539,18 +563,50 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
         oa.init(raw0);
     }
     int32_t bad = 0;
-    float2 gz = make_float2(0.0f, 0.0f);
-    if (mine && a.T > 0) gz = *reinterpret_cast<const float2 *>(gum + (size_t)e * 2);
+    // the next reset state: k_reset_pool entry rj, read at every step's start (an L2 hit
+    // until the entry is used) so that no load is waited on in the step's reset branch
+    int rj = 0;
+    // the previous step's finished episodes: the slot counter's atomic return is read one
+    // step later (under this step's MFMAs) instead of stalling the wave where it is issued
+    uint64_t pm = 0;          // ballot of the previous step's done lanes
+    int32_t pbase = 0;        // its leader lane's atomicAdd return
+    float pret = 0.0f;
+    int32_t plen = 0;
+    auto flush_eps = [&](int step) {
+        if (pm == 0) return;
+        const int leader = __ffsll((unsigned long long)pm) - 1;
+        const int32_t base = __builtin_amdgcn_readlane(pbase, leader);
+        if ((pm >> lane) & 1ull) {
+            const int32_t k = base + (int32_t)__popcll(pm & ((1ull << lane) - 1ull));
+            if (k < a.eps_cap) {
+                EpisodeRec rec;
+                rec.total_reward[0] = pret;
+                for (int p = 1; p < BPPO_MAX_PLAYERS; p++) rec.total_reward[p] = 0.0f;
+                rec.length = plen; rec.env_index = e; rec.step = step; rec.pad = 0;
+                a.eps[k] = rec;
+            }
+        }
+    };
 #ifdef BPPO_RO_STAMPS
     unsigned long long ro_acc[RO_NSEG] = {}, ro_prev;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ro_prev)::"memory");
 #endif
+    // the prologue's loads (W0 fragments, state) complete before the step loop: left pending
+    // at the loop header, the wait-count pass waited on every step's fresh loads (the Gumbel
+    // pair, the reset entry) at layer 1's first use of the W0 registers
+    __builtin_amdgcn_s_waitcnt(0);
 #pragma unroll 1
     for (int t = 0; t < a.T; t++) {
         const size_t row = (size_t)t * N + e;
         // the next step's Gumbel pair, in flight under this step's MFMAs
-        float2 gz_next = make_float2(0.0f, 0.0f);
-        if (mine && t + 1 < a.T) gz_next = *reinterpret_cast<const float2 *>(gum + (row + N) * 2);
+        // this step's Gumbel pair: in flight under the layer MFMAs, first used by the argmax (a
+        // pair prefetched a step ahead needs a register copy at the loop latch, where the
+        // wait-count pass then waited for the whole step's stores)
+        float2 gz = make_float2(0.0f, 0.0f);
+        if (mine) gz = *reinterpret_cast<const float2 *>(gum + row * 2);
+        float4 rnx = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        uint64_t rnpos = 0;
+        if (mine && rj < a.rpool_k) { rnx = a.rpool[(size_t)rj * N + e]; rnpos = a.rpos[(size_t)rj * N + e]; }
         float x[6] = {0, 0, 0, 0, 0, 1.0f};
         if (mine) {
             float raw[5], z[5];
@@ -624,15 +680,24 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
         asm volatile("" : "+v"(zero));
         const float4 *hw = S.hw + zero;
         const float *hrow = Tw + lane * 65 + zero;
+        // batches of 8 units: the batch's 8 weight rows and 8 activations are all read before
+        // its chains consume them, one LDS round trip per batch (the per-unit form waited on
+        // every read: 24% of the step under the segment stamps)
         float l0 = 0.0f, l1 = 0.0f, vv = 0.0f;
-#pragma unroll 16
-        for (int k = 0; k < H; k++) {
-            const float4 w = hw[k];
-            float z = __fadd_rn(hrow[k], w.w);
-            z = z > 0.0f ? z : 0.0f;
-            l0 = __builtin_fmaf(z, w.x, l0);
-            l1 = __builtin_fmaf(z, w.y, l1);
-            vv = __builtin_fmaf(z, w.z, vv);
+#pragma unroll 1
+        for (int k0 = 0; k0 < H; k0 += 8) {
+            float4 w[8];
+            float hz[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) { w[j] = hw[k0 + j]; hz[j] = hrow[k0 + j]; }
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                float z = __fadd_rn(hz[j], w[j].w);
+                z = z > 0.0f ? z : 0.0f;
+                l0 = __builtin_fmaf(z, w[j].x, l0);
+                l1 = __builtin_fmaf(z, w[j].y, l1);
+                vv = __builtin_fmaf(z, w[j].z, vv);
+            }
         }
         float lg[2];
         lg[0] = __fadd_rn(l0, S.bp[0]);
@@ -652,28 +717,27 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
             ep_ret = __fadd_rn(ep_ret, r);
             ep_len += 1;
         }
-#if defined(BPPO_RO_DIAG) && (BPPO_RO_DIAG & 1)
-        const int32_t k = -1;   // diagnostic: no episode records
-#else
-        const int32_t k = wave_episode_slot(done, a.ep_count);
-#endif
+        // episode records: the previous step's slots, then this step's counter reservation
+        flush_eps(t - 1);
+        const uint64_t m = (uint64_t)__ballot(done ? 1 : 0);
+        if (m) {
+            const int leader = __ffsll((unsigned long long)m) - 1;
+            if (lane == leader) pbase = atomicAdd(a.ep_count, (int32_t)__popcll(m));
+        }
+        pm = m;
         if (done) {
-            if (k >= 0 && k < a.eps_cap) {
-                EpisodeRec rec;
-                rec.total_reward[0] = ep_ret;
-                for (int p = 1; p < BPPO_MAX_PLAYERS; p++) rec.total_reward[p] = 0.0f;
-                rec.length = ep_len; rec.env_index = e; rec.step = t; rec.pad = 0;
-                a.eps[k] = rec;
+            pret = ep_ret;
+            plen = ep_len;
+            if (rj < a.rpool_k) {
+                s.x = rnx.x; s.x_dot = rnx.y; s.theta = rnx.z; s.theta_dot = rnx.w; s.steps = 0;
+                env_pos = rnpos;
+                rj++;
+            } else {
+                WordCursor ec;
+                ec.init(seed_key(a.seed_base + (uint64_t)e), 0, env_pos);
+                cartpole_reset(s, ec);
+                env_pos = ec.pos;
             }
-#if defined(BPPO_RO_DIAG) && (BPPO_RO_DIAG & 2)
-            s.x = 0.01f; s.x_dot = -0.01f; s.theta = 0.02f; s.theta_dot = -0.02f; s.steps = 0;   // diagnostic
-            env_pos += 4;
-#else
-            WordCursor ec;
-            ec.init(seed_key(a.seed_base + (uint64_t)e), 0, env_pos);
-            cartpole_reset(s, ec);
-            env_pos = ec.pos;
-#endif
             ep_ret = 0.0f;
             ep_len = 0;
         }
@@ -691,10 +755,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
                 a.rows[row * 2 + 1] = make_float4(x[4], __int_as_float(act), lp, v);
             }
         }
-        gz = gz_next;
         wave_sync();                      // this step's tile reads done before the next step's writes
         RO_STAMP(7);
     }
+    flush_eps(a.T - 1);
 #ifdef BPPO_RO_STAMPS
     if (lane == 0 && a.stamps)
         for (int k = 0; k < RO_NSEG; k++) a.stamps[(size_t)(e >> 6) * RO_NSEG + k] = ro_acc[k];
@@ -917,6 +981,7 @@ bppo_status launch_cartpole_rollout(bppo_ctx *c, uint64_t base_pos, const double
     a.ep_count = c->d_ep_count; a.eps_cap = c->eps_cap; a.err = c->d_err;
     a.rows = nullptr;
     a.stamps = nullptr;
+    a.rpool = nullptr; a.rpos = nullptr; a.rpool_k = 0;
     c->rows_from_rollout = false;
     if (h == 64 && nl == 2 && c->cfg.relu && c->d_gumbel) {
         // the update's packed rows (obs, action, log-prob, value) written by the rollout
@@ -942,6 +1007,15 @@ bppo_status launch_cartpole_rollout(bppo_ctx *c, uint64_t base_pos, const double
                                mmb::LDS, c->stream, a, (const float *)c->d_gumbel);
         } else {
             const int waves = (c->N + 63) / 64;
+            // BPPO_RESET_POOL_K (tests): a shorter pool (exercises the in-kernel fallback), 0: none
+            int pk = RPOOL_K;
+            if (const char *v = getenv("BPPO_RESET_POOL_K")) pk = std::max(0, std::min(RPOOL_K, atoi(v)));
+            if (c->d_rpool && pk > 0) {
+                hipLaunchKernelGGL(k_reset_pool, dim3((c->N + 255) / 256), dim3(256), 0, c->stream, c->N, pk,
+                                   c->cfg.env_seed_base, (const uint64_t *)c->d_env_pos, c->d_rpool, c->d_rpos);
+                TRY(launch_check(c, "k_reset_pool"));
+                a.rpool = c->d_rpool; a.rpos = c->d_rpos; a.rpool_k = pk;
+            }
 #ifdef BPPO_RO_STAMPS
             static unsigned long long *d_st = nullptr;
             if (!d_st) BPPO_HIP(c, hipMalloc((void **)&d_st, sizeof(unsigned long long) * (size_t)waves * RO_NSEG));

@@ -137,7 +137,7 @@ bppo_status wide_pack(bppo_ctx *c) {
 
 // forward (mlp.rs:140-206 / ctde.rs:132-183) of `rows` rows [priv | obs] (ld ldxc);
 // hidden activations stay in d_hbuf for the backward
-bppo_status wide_forward(bppo_ctx *c, int rows, const float *xc, int ldxc, float *logits, float *values) {
+bppo_status wide_forward(bppo_ctx *c, int rows, const float *xc, int ldxc, float *logits, float *values, int split) {
     const NetLayout &n = c->net;
     const float *P = c->d_params;
     const float *x = xc + c->G;
@@ -149,17 +149,17 @@ bppo_status wide_forward(bppo_ctx *c, int rows, const float *xc, int ldxc, float
     for (int l = n.n_conv; l < n.n_actor_hidden; l++) {
         float *h = c->d_hbuf + c->hoff[l];
         WHIP(c, gemm_fwd(c->stream, rows, n.out[l], n.in[l], x, ldx, P + n.w[l], n.out[l], P + n.b[l], c->cfg.relu ? 1 : 2, h,
-                         n.out[l], n.out[l], nullptr, 0));
+                         n.out[l], n.out[l], nullptr, 0, split));
         x = h; ldx = n.out[l];
     }
     const int K = n.in[n.policy];
     if (!n.ctde) {
         WHIP(c, gemm_fwd(c->stream, rows, c->A + 1, K, x, ldx, c->d_heads, c->A + 1, c->d_heads_b, 0, logits, c->A,
-                         c->A, values, 1));
+                         c->A, values, 1, split));
         return BPPO_OK;
     }
     WHIP(c, gemm_fwd(c->stream, rows, c->A, K, x, ldx, P + n.w[n.policy], c->A, P + n.b[n.policy], 0, logits,
-                     c->A, c->A, nullptr, 0));
+                     c->A, c->A, nullptr, 0, split));
     const float *xq = xc;
     int ldq = ldxc;
     if (n.n_conv) {                                  // split CNN critic: its own conv stack (cnn.rs:284-296)
@@ -169,11 +169,11 @@ bppo_status wide_forward(bppo_ctx *c, int rows, const float *xc, int ldxc, float
     for (int l = n.critic_fc0; l < n.value; l++) {
         float *h = c->d_hbuf + c->hoff[l];
         WHIP(c, gemm_fwd(c->stream, rows, n.out[l], n.in[l], xq, ldq, P + n.w[l], n.out[l], P + n.b[l], c->cfg.relu ? 1 : 2, h,
-                         n.out[l], n.out[l], nullptr, 0));
+                         n.out[l], n.out[l], nullptr, 0, split));
         xq = h; ldq = n.out[l];
     }
     WHIP(c, gemm_fwd(c->stream, rows, 1, n.in[n.value], xq, ldq, P + n.w[n.value], 1, P + n.b[n.value], 0, values,
-                     1, 1, nullptr, 0));
+                     1, 1, nullptr, 0, split));
     return BPPO_OK;
 }
 
@@ -266,15 +266,20 @@ bppo_status wide_bootstrap_gae(bppo_ctx *c) {
 
 // one minibatch of ppo_update: gather, forward, loss, backward -> d_grad[0, np),
 // metrics -> d_grad[np, np + WM_COUNT)
-bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, double ent_coef) {
+bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, double ent_coef, bool first) {
     const NetLayout &n = c->net;
     const int hact = c->cfg.relu ? 1 : 2;   // hidden activation derivative in the DX epilogues
     const int A = c->A, L = c->L, rows = (int)mb;
     const float *P = c->d_params;
     float *G = c->d_grad;
-    const int exact = wide_exact_grad(c);
+    // the split-bf16 contraction (k_gemm_split) for the MLP GEMMs of every minibatch after the
+    // update's first (mode 0) or of all of them (bppo_set_minibatch_kernel 2); the first keeps
+    // the exact chains (ratio exactly 1) -- as the CfgB update's k_minibatch_split
+    static const bool exact_all = getenv("BPPO_MB_EXACT_ALL") != nullptr;
+    const int split = n.n_conv == 0 && (c->mb_kernel == 2 || (c->mb_kernel == 0 && !first && !exact_all)) ? 1 : 0;
+    const int exact = split ? -1 : wide_exact_grad(c);
     WHIP(c, wide_gather(c->stream, c->d_perm, start, mb, c->d_xc, L, c->d_xcg));
-    WTRY(wide_forward(c, rows, c->d_xcg, L, c->d_logits, c->d_values));
+    WTRY(wide_forward(c, rows, c->d_xcg, L, c->d_logits, c->d_values, split));
     LossArgs g;
     g.perm = c->d_perm; g.start = start; g.n = mb; g.act = c->d_act; g.logp = c->d_logp; g.adv = c->d_adv;
     g.ret = c->u_ret; g.val = c->u_val; g.mask = c->d_mask; g.logits = c->d_logits; g.values = c->d_values;
@@ -303,7 +308,8 @@ bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, double ent_
                        G + n.b[l], nullptr));
             if (l > first) {
                 WHIP(c, gemm_dx(c->stream, rows, n.in[l], n.out[l], dz, n.out[l], P + n.w[l], n.out[l],
-                                c->d_hbuf + c->hoff[l - 1], n.out[l - 1], hact, dz2, n.in[l]));
+                                c->d_hbuf + c->hoff[l - 1], n.out[l - 1], hact, dz2, n.in[l], nullptr, 0, nullptr,
+                                split));
                 std::swap(dz, dz2);
             }
         }
@@ -328,7 +334,7 @@ bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, double ent_
         // the trunk's input gradient: the policy head's chain over its A outputs, then the value
         // head's product added as its own rounded term (the two heads are two Linear modules)
         WHIP(c, gemm_dx(c->stream, rows, Wa, A, c->d_dout, A + 1, c->d_heads, A + 1, Ha, Wa, hact, dz, Wa,
-                        c->d_dout + A, A + 1, P + n.w[n.value]));
+                        c->d_dout + A, A + 1, P + n.w[n.value], split));
         if (!n.n_conv) {
             WTRY(hidden_chain(0, la, c->d_xcg + c->G, L));
             return BPPO_OK;
@@ -340,7 +346,8 @@ bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, double ent_
     }
     // CTDE actor
     WTRY(wgrad(Wa, A, Ha, Wa, c->d_dout, A + 1, G + n.w[n.policy], A, A, nullptr, 0, G + n.b[n.policy], nullptr));
-    WHIP(c, gemm_dx(c->stream, rows, Wa, A, c->d_dout, A + 1, P + n.w[n.policy], A, Ha, Wa, hact, dz, Wa));
+    WHIP(c, gemm_dx(c->stream, rows, Wa, A, c->d_dout, A + 1, P + n.w[n.policy], A, Ha, Wa, hact, dz, Wa, nullptr, 0,
+                    nullptr, split));
     if (n.n_conv) WTRY(cnn_trunk_backward(0, n.n_conv, la));   // split CNN actor
     else WTRY(hidden_chain(0, la, c->d_xcg + c->G, L));
     // CTDE critic
@@ -349,7 +356,8 @@ bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, double ent_
     const int Wc = n.out[lc];
     dz = c->d_dz[0]; dz2 = c->d_dz[1];
     WTRY(wgrad(Wc, 1, Hc, Wc, c->d_dout + A, A + 1, G + n.w[n.value], 1, 1, nullptr, 0, G + n.b[n.value], nullptr));
-    WHIP(c, gemm_dx(c->stream, rows, Wc, 1, c->d_dout + A, A + 1, P + n.w[n.value], 1, Hc, Wc, hact, dz, Wc));
+    WHIP(c, gemm_dx(c->stream, rows, Wc, 1, c->d_dout + A, A + 1, P + n.w[n.value], 1, Hc, Wc, hact, dz, Wc, nullptr,
+                    0, nullptr, split));
     if (n.n_conv) return cnn_trunk_backward(1, n.critic_fc0, lc);   // split CNN critic
     WTRY(hidden_chain(n.critic_first, lc, c->d_xcg, L));
     return BPPO_OK;

@@ -88,6 +88,11 @@ if [ "$PART" = widekt ]; then
   done
   exit 0
 fi
+if [ "$PART" = mfmaprobe ]; then
+  timeout -k 10 60 ./scripts/probes/mfma_round_probe > gpurun_out/${TAG}_mfma_round_probe.txt 2>&1
+  rc=$?; echo "mfma probe rc=$rc"; cat gpurun_out/${TAG}_mfma_round_probe.txt
+  exit $rc
+fi
 if [ "$PART" = fpprobe ]; then
   timeout -k 10 120 ./scripts/probes/fp_rounding_probe > gpurun_out/${TAG}_fp_rounding_probe.txt 2>&1
   rc=$?; echo "fp probe rc=$rc"; cat gpurun_out/${TAG}_fp_rounding_probe.txt

@@ -456,6 +456,15 @@ class Trainer:
         lib().or_trainer_get_params(self.h, out)
         return out
 
+    def episodes(self):
+        """the last collect's EpisodeStats in the reference's order (step, then env index):
+        (total_rewards[0] bits, length, env_index)"""
+        n = lib().or_trainer_episodes(self.h, None, 0)
+        eps = (Episode * max(n, 1))()
+        lib().or_trainer_episodes(self.h, eps, n)
+        return [(np.float32(eps[i].total_rewards[0]).view(np.uint32).item(), eps[i].length, eps[i].env_index)
+                for i in range(n)]
+
     def rng_pos(self):
         return lib().or_trainer_rng_pos(self.h)
 

@@ -357,6 +357,43 @@ def test_rollout_lanes64_bit_exact(monkeypatch, N, lanes64):
         tr.close(); ot.close()
 
 
+@pytest.mark.parametrize("pool_k", ["16", "2", "0"])
+def test_rollout_lanes64_episodes_and_reset_pool(monkeypatch, pool_k):
+    """the 64-lane rollout's episode records (deferred slot reservation) and resets from
+    k_reset_pool's states drawn ahead (16: the default pool; 2: most envs run past the pool
+    and fall back to drawing in the kernel; 0: no pool) -- records, env state and RNG
+    positions bit-exact against the oracle over two rollouts of T = 128"""
+    import oracle_ffi as O
+    from parity_util import cmp_cartpole_rollout, oracle_train_cfg
+    monkeypatch.setenv("BPPO_RESET_POOL_K", pool_k)
+    N, T = 2048, 128
+    cfg = bppo.make_config("cartpole", num_envs=N, num_steps=T)
+    params = bppo.orthogonal_init(cfg, seed=5)
+    tr = bppo.Trainer(cfg, params=params)
+    ot = O.Trainer(oracle_train_cfg(cfg), params)
+    try:
+        for _ in range(2):
+            info = bppo.collect_rollouts(tr.ctx)
+            n_eps = ot.collect()
+            cmp_cartpole_rollout(tr, ot)
+            assert info.episodes == n_eps > N
+            dev = [(np.float32(e["total_rewards"][0]).view(np.uint32).item(), e["length"], e["env_index"])
+                   for e in bppo.rollout_episodes(tr.ctx)]
+            oe = ot.episodes()            # the oracle stores the first 4 N + 1024 (oracle/ppo.c eps_cap)
+            assert len(dev) == n_eps and len(oe) >= min(n_eps, 4 * N)
+            assert dev[:len(oe)] == oe
+            tr.ctx.set_buffer("rewards", ot.buffer("rewards"))
+            bppo.compute_gae(tr.ctx); ot.gae()
+            bppo.ppo_update(tr.ctx, bppo.schedule_get(cfg["learning_rate"], 0), bppo.schedule_get(cfg["entropy_coef"], 0))
+            ot.update()
+            tr.model.set_params(ot.params())
+            mvc, rets = ot.ret_norm_state(returns=True)
+            tr.ctx.set_ret_norm(mvc, rets)
+            tr.ctx.set_obs_norm(*ot.obs_norm_state(5))
+    finally:
+        tr.close(); ot.close()
+
+
 @pytest.mark.parametrize("threads", ["16", "2"])
 def test_shuffle_windows_single_rank_matches_oracle(monkeypatch, threads):
     """shuffle_windows at W = 1 through the pipelined bppo_train_steps (the engine walks the
