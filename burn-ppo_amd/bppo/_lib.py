@@ -85,7 +85,7 @@ EXPORTS = (
     "bppo_rng_fill_bytes", "bppo_rng_from_seed", "bppo_rng_key_get", "bppo_num_param_tensors",
     "bppo_optimizer_get", "bppo_optimizer_set", "bppo_popart_get", "bppo_popart_set",
     "bppo_config_size", "bppo_update_metrics_size", "bppo_episode_size", "bppo_rollout_info_size",
-    "bppo_set_explained_variance_mode", "bppo_set_minibatch_kernel",
+    "bppo_set_explained_variance_mode", "bppo_set_minibatch_kernel", "bppo_set_rank",
 )
 
 # ABI struct -> the library's sizeof export (checked when the library loads)
@@ -142,6 +142,7 @@ def lib():
         "bppo_train_steps": (i32, [vp, i32, vp, vp, C.c_uint64, vp, vp, vp, i32, vp]),
         "bppo_set_allreduce": (i32, [vp, ALLREDUCE_FN, vp, i32]),
         "bppo_set_allreduce_async": (i32, [vp, ALLREDUCE_FN, vp, i32]),
+        "bppo_set_rank": (i32, [vp, i32]),
         "bppo_get_stream": (i32, [vp, C.POINTER(vp)]),
         "bppo_opponents_set": (i32, [vp, i32, vp, vp, vp, vp, i32, vp, vp, vp]),
         "bppo_opponents_get_envs": (i32, [vp, vp, vp]),

@@ -191,6 +191,7 @@ class Context:
                 return 1
         self._ar_keep = L.ALLREDUCE_FN(_cb)
         setter = L.lib().bppo_set_allreduce_async if stream_ordered else L.lib().bppo_set_allreduce
+        self._chk(L.lib().bppo_set_rank(self.h, self.rank))     # PopArt's W > 1 all-gather slot
         self._chk(setter(self.h, self._ar_keep, None, world))
 
     @property

@@ -1327,12 +1327,21 @@ extern "C" bppo_status bppo_train_steps(bppo_ctx *c, int32_t n, const double *lr
     return BPPO_OK;
 }
 
-// W > 1: PopArt's running return statistics and value-head rescale
-// are per rank, so the ranks' parameters would drift apart; an opponent pool trains a
-// per-rank number of learner rows, so the ranks' minibatches would not line up
+// W > 1: an opponent pool trains a per-rank number of learner rows,
+// so the ranks' minibatches would not line up.  PopArt's statistics are all-gathered
+// (popart.hip): its scratch is sized for the world here
 static bppo_status check_world(bppo_ctx *c, int32_t world) {
-    if (world > 1 && c->cfg.normalize_values) { c->err = "normalize_values (PopArt): single-rank only"; return BPPO_ERR_UNSUPPORTED; }
     if (world > 1 && opp_active(c)) { c->err = "opponent pool: single-rank only"; return BPPO_ERR_UNSUPPORTED; }
+    if (world > 1 && c->cfg.normalize_values) {
+        if (c->d_pa_gather) { BPPO_HIP(c, hipFree(c->d_pa_gather)); c->d_pa_gather = nullptr; }
+        BPPO_HIP(c, hipMalloc((void **)&c->d_pa_gather, sizeof(float) * 9 * (size_t)world));
+    }
+    return BPPO_OK;
+}
+
+extern "C" bppo_status bppo_set_rank(bppo_ctx *c, int32_t rank) {
+    if (!c || rank < 0) return BPPO_ERR_ARG;
+    c->rank = rank;
     return BPPO_OK;
 }
 

@@ -45,6 +45,7 @@ NetLayout make_layout(const bppo_config &c, int obs_dim, int priv_dim, int act_d
 
 // episode record written by the rollout kernel
 constexpr int EP_SUMMARY_BLOCKS = 128;   // k_ep_summary grid (partial sums per block)
+constexpr int WIDE_SPLIT_MIN_ROWS = 32768;   // wide_minibatch: the split-bf16 GEMMs from this minibatch size on
 constexpr int RPOOL_K = 16;              // CfgB rollout: reset states drawn ahead per env (k_reset_pool)
 constexpr int TM_SLOTS = 10;             // phase timer event pairs (enum TM_* below)
 constexpr int ROLL_HOST_WORDS = 2 + 2 * EP_SUMMARY_BLOCKS;     // pinned doubles per rollout slot
@@ -332,6 +333,8 @@ struct bppo_ctx {
     bppo_allreduce_fn allreduce = nullptr;
     void *allreduce_user = nullptr;
     int world = 1;
+    int rank = 0;                     // bppo_set_rank: this context's slot in W > 1 all-gathers
+    float *d_pa_gather = nullptr;     // PopArt at W > 1: [world][9] floats (3 doubles, 3 floats each)
     int allreduce_async = 0;          // callback enqueues on the stream (no host sync per minibatch)
     // ---- multi-player ("wide") path: Connect Four / Liar's Dice (wide_api.hip)
     int wide = 0;                     // env_kind != CartPole

@@ -372,31 +372,44 @@ __global__ void __launch_bounds__(256, 2) k_gemm(GemmArgs g) {
 // rows of a fragment read hit distinct bank groups); one stage (60 KB at 128 x 128, two
 // blocks per CU), the next stage's f32 values prefetched into registers under the MFMAs.
 typedef __bf16 sbf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 sbf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 sbf16x2 __attribute__((ext_vector_type(2)));
 constexpr int SKP = GBK + 8;
 
-// three pieces of Q consecutive-k values -> LDS rows at s[p * plane + off]
+// three pieces of Q consecutive-k values -> LDS rows at s[p * plane + off].  Pairs: one
+// v_cvt_pk_bf16_f32 per piece pair, the pieces' f32 values read back from that word (the
+// asm makes it opaque: otherwise each half is converted again on its own)
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+    uint32_t u = __builtin_bit_cast(uint32_t, sbf16x2{(__bf16)a, (__bf16)b});
+    asm("" : "+v"(u));
+    return u;
+}
 template <int Q>
 __device__ __forceinline__ void split_store(const float *x, __bf16 *s, int plane, int off) {
-    __bf16 p0[Q], p1[Q], p2[Q];
+    if constexpr (Q >= 2) {
+        uint32_t p0[Q / 2], p1[Q / 2], p2[Q / 2];
 #pragma unroll
-    for (int j = 0; j < Q; j++) {
-        const __bf16 a = (__bf16)x[j];
-        const float r = x[j] - (float)a;
-        const __bf16 b = (__bf16)r;
-        p0[j] = a; p1[j] = b; p2[j] = (__bf16)(r - (float)b);
-    }
-    if constexpr (Q == 4) {
-        *reinterpret_cast<sbf16x4 *>(s + off) = sbf16x4{p0[0], p0[1], p0[2], p0[3]};
-        *reinterpret_cast<sbf16x4 *>(s + plane + off) = sbf16x4{p1[0], p1[1], p1[2], p1[3]};
-        *reinterpret_cast<sbf16x4 *>(s + 2 * plane + off) = sbf16x4{p2[0], p2[1], p2[2], p2[3]};
-    } else if constexpr (Q == 2) {
-        *reinterpret_cast<sbf16x2 *>(s + off) = sbf16x2{p0[0], p0[1]};
-        *reinterpret_cast<sbf16x2 *>(s + plane + off) = sbf16x2{p1[0], p1[1]};
-        *reinterpret_cast<sbf16x2 *>(s + 2 * plane + off) = sbf16x2{p2[0], p2[1]};
+        for (int j = 0; j < Q / 2; j++) {
+            const float xa = x[2 * j], xb = x[2 * j + 1];
+            const uint32_t A = pk_bf16(xa, xb);
+            const float ra = xa - __uint_as_float(A << 16), rb = xb - __uint_as_float(A & 0xffff0000u);
+            const uint32_t B = pk_bf16(ra, rb);
+            const float sa = ra - __uint_as_float(B << 16), sb = rb - __uint_as_float(B & 0xffff0000u);
+            p0[j] = A; p1[j] = B; p2[j] = pk_bf16(sa, sb);
+        }
+        if constexpr (Q == 4) {
+            *reinterpret_cast<uint2 *>(s + off) = make_uint2(p0[0], p0[1]);
+            *reinterpret_cast<uint2 *>(s + plane + off) = make_uint2(p1[0], p1[1]);
+            *reinterpret_cast<uint2 *>(s + 2 * plane + off) = make_uint2(p2[0], p2[1]);
+        } else {
+            *reinterpret_cast<uint32_t *>(s + off) = p0[0];
+            *reinterpret_cast<uint32_t *>(s + plane + off) = p1[0];
+            *reinterpret_cast<uint32_t *>(s + 2 * plane + off) = p2[0];
+        }
     } else {
-        s[off] = p0[0]; s[plane + off] = p1[0]; s[2 * plane + off] = p2[0];
+        const __bf16 a = (__bf16)x[0];
+        const float r = x[0] - (float)a;
+        const __bf16 b = (__bf16)r;
+        s[off] = a; s[plane + off] = b; s[2 * plane + off] = (__bf16)(r - (float)b);
     }
 }
 
@@ -538,10 +551,19 @@ __global__ void __launch_bounds__(256, 2) k_gemm_split(GemmArgs g) {
 #pragma unroll
                 for (int p = 0; p < 3; p++)
                     bf[j][p] = *reinterpret_cast<const sbf16x8 *>(sB + p * BN * SKP + ((wn * S::TN + j) * 32 + r) * SKP + kk + 8 * h);
+            // each 16-deep step's six products into a fresh partial, added to the running sum
+            // with a round-to-nearest f32 add (the MFMA's own accumulation then spans 16 k's)
 #pragma unroll
             for (int i = 0; i < S::TM; i++)
 #pragma unroll
-                for (int j = 0; j < S::TN; j++) mfma6_split(acc[i][j], af[i], bf[j]);
+                for (int j = 0; j < S::TN; j++) {
+                    f32x16 part;
+#pragma unroll
+                    for (int q = 0; q < 16; q++) part[q] = 0.0f;
+                    mfma6_split(part, af[i], bf[j]);
+#pragma unroll
+                    for (int q = 0; q < 16; q++) acc[i][j][q] = __fadd_rn(acc[i][j][q], part[q]);
+                }
         }
     }
     gemm_epilogue<MODE, S::TM, S::TN>(g, acc, tl, m0 + wm * S::TM * 32, n0 + wn * S::TN * 32, lane);
@@ -864,7 +886,9 @@ hipError_t gemm_dx(hipStream_t st, int M, int N, int K, const float *dZ, int ldz
 
 int gemm_wg_splits(int Kin, int N, int rows) {
     const int tiles = ((Kin + 127) / 128) * ((N + (N <= 32 ? 31 : N <= 64 ? 63 : 127)) / (N <= 32 ? 32 : N <= 64 ? 64 : 128));
-    int s = (2048 + tiles - 1) / tiles;                  // ~2048 blocks
+    // ~2048 blocks (BPPO_WG_BLOCKS: another target, for A/B runs of the slab traffic)
+    static const int target = getenv("BPPO_WG_BLOCKS") ? std::max(1, atoi(getenv("BPPO_WG_BLOCKS"))) : 2048;
+    int s = (target + tiles - 1) / tiles;
     const int max_by_rows = (rows + 1023) / 1024;        // >= 1024 rows per split
     if (s > max_by_rows) s = max_by_rows;
     if (s > GEMM_MAX_SPLITS) s = GEMM_MAX_SPLITS;

@@ -782,17 +782,30 @@ constexpr size_t LDS_TILES = sizeof(Params) + WAVES * sizeof(Wave);
 static_assert(LDS_TILES <= 160 * 1024, "split minibatch kernel LDS over the gfx950 limit");
 __device__ __forceinline__ int perm_j1(int j) { return (j & ~12) | ((j & 4) << 1) | ((j & 8) >> 1); }
 struct Split8 { bf16x8_t p[3]; };
-// exact three-piece split of 8 f32 values
+// exact three-piece split of 8 f32 values, a pair at a time: one v_cvt_pk_bf16_f32 per
+// piece pair, the pieces' f32 values taken back from the packed word (<< 16, & 0xffff0000)
+// and the residuals as one packed subtract -- the per-element form converted every value
+// twice (once alone for its residual, once paired for the operand) plus moves
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+    uint32_t u = __builtin_bit_cast(uint32_t, bf16x2_t{(__bf16)a, (__bf16)b});
+    asm("" : "+v"(u));      // opaque: the halves are read back from THIS word (no re-conversion)
+    return u;
+}
+union Pieces8 { bf16x8_t v; uint32_t u[4]; };
 __device__ __forceinline__ Split8 split8(const float (&x)[8]) {
-    Split8 s;
+    Pieces8 p0, p1, p2;
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
-        const __bf16 a = (__bf16)x[j];
-        const float r = x[j] - (float)a;
-        const __bf16 b = (__bf16)r;
-        const __bf16 c = (__bf16)(r - (float)b);
-        s.p[0][j] = a; s.p[1][j] = b; s.p[2][j] = c;
+    for (int j = 0; j < 4; j++) {
+        const float xa = x[2 * j], xb = x[2 * j + 1];
+        const uint32_t A = pk_bf16(xa, xb);
+        const float ra = xa - __uint_as_float(A << 16), rb = xb - __uint_as_float(A & 0xffff0000u);
+        const uint32_t B = pk_bf16(ra, rb);
+        const float sa = ra - __uint_as_float(B << 16), sb = rb - __uint_as_float(B & 0xffff0000u);
+        p0.u[j] = A; p1.u[j] = B; p2.u[j] = pk_bf16(sa, sb);
     }
+    Split8 s;
+    s.p[0] = p0.v; s.p[1] = p1.v; s.p[2] = p2.v;
     return s;
 }
 __device__ __forceinline__ void mfma6(f32x16_t &acc, const Split8 &a, const Split8 &b) {
@@ -1197,35 +1210,34 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
 
 // fixed-order reduction of the wave partials, grad[p] = sum_w slab[w][p]: SLAB_GROUPS
 // row groups each summed in f64 in row order, then the groups in order.
-// both passes in one launch, same association (bit-identical grad): a block owns 64
-// columns; its 16 waves take row groups g = q, q + 16 and leave the group sums in
-// LDS, then wave 0 adds the 32 groups in order.  One dependent launch fewer per
-// minibatch; 16 waves per block keep loads in flight while the side-stream
-// Fisher-Yates passes load HBM
-constexpr int SLAB1_WAVES = 16;
-__global__ void __launch_bounds__(64 * SLAB1_WAVES) k_slab_reduce1(const float *__restrict__ slab, int rows, int width,
-                                                      float *__restrict__ grad, float *__restrict__ vemax_local) {
-    __shared__ double part[SLAB_GROUPS][64];
-    const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
-    const int p = blockIdx.x * 64 + lane;
+// both passes in one launch, same association (bit-identical grad): a block owns 16
+// columns and all 32 row groups, thread (column tid % 16, group tid / 16), the group sums
+// through LDS, then 16 threads add the groups in order.  ~300 blocks for the CfgB width
+// (r02-r04: 64 columns per block, 75 blocks of 16 waves each looping over two groups --
+// 35 us mean per minibatch in the loop)
+constexpr int SLAB1_COLS = 16;
+__global__ void __launch_bounds__(SLAB1_COLS * SLAB_GROUPS) k_slab_reduce1(const float *__restrict__ slab, int rows,
+                                                                           int width, float *__restrict__ grad,
+                                                                           float *__restrict__ vemax_local) {
+    __shared__ double part[SLAB_GROUPS][SLAB1_COLS];
+    const int c = threadIdx.x % SLAB1_COLS, g = threadIdx.x / SLAB1_COLS;
+    const int p = blockIdx.x * SLAB1_COLS + c;
     const bool live = p < width, is_max = p == width - NUM_M + M_VEMAX;
     const int per = (rows + SLAB_GROUPS - 1) / SLAB_GROUPS;
     if (live) {
-        for (int g = q; g < SLAB_GROUPS; g += SLAB1_WAVES) {
-            const int w0 = g * per, w1 = min(rows, w0 + per);
-            double s = is_max ? -INFINITY : 0.0;
+        const int w0 = g * per, w1 = min(rows, w0 + per);
+        double s = is_max ? -INFINITY : 0.0;
 #pragma unroll 8
-            for (int w = w0; w < w1; w++) {
-                const double v = slab[(size_t)w * width + p];
-                s = is_max ? fmax(s, v) : s + v;
-            }
-            part[g][lane] = s;
+        for (int w = w0; w < w1; w++) {
+            const double v = slab[(size_t)w * width + p];
+            s = is_max ? fmax(s, v) : s + v;
         }
+        part[g][c] = s;
     }
     __syncthreads();
-    if (q == 0 && live) {
+    if (g == 0 && live) {
         double s = is_max ? -INFINITY : 0.0;
-        for (int g = 0; g < SLAB_GROUPS; g++) s = is_max ? fmax(s, part[g][lane]) : s + part[g][lane];
+        for (int q = 0; q < SLAB_GROUPS; q++) s = is_max ? fmax(s, part[q][c]) : s + part[q][c];
         grad[p] = (float)s;
         if (is_max) *vemax_local = (float)s;     // kept out of the W > 1 SUM all-reduce
     }
@@ -1662,7 +1674,8 @@ bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_
     TRY(launch_check(c, __func__));
     const int width = (int)c->net.n_params + NUM_M;
     static_assert(M_VEMAX == GRAD_VEMAX && NUM_M <= GRAD_METRIC_SLOTS, "metric slot layout");
-    hipLaunchKernelGGL(k_slab_reduce1, dim3((width + 63) / 64), dim3(64 * SLAB1_WAVES), 0, c->stream, c->d_slab,
+    hipLaunchKernelGGL(k_slab_reduce1, dim3((width + SLAB1_COLS - 1) / SLAB1_COLS), dim3(SLAB1_COLS * SLAB_GROUPS), 0,
+                       c->stream, c->d_slab,
                        c->slab_used, width, c->d_grad, c->d_grad + c->net.n_params + GRAD_VEMAX_LOCAL);
     TRY(launch_check(c, __func__));
     return BPPO_OK;

@@ -137,6 +137,49 @@ void popart_free(bppo_ctx *c) {
     if (c->d_ret_n) (void)hipFree(c->d_ret_n);
     if (c->d_val_n) (void)hipFree(c->d_val_n);
     if (c->d_pa_part) (void)hipFree(c->d_pa_part);
+    if (c->d_pa_gather) (void)hipFree(c->d_pa_gather);
+}
+
+static void chan_merge(Welford &a, const Welford &b) {
+    if (b.n <= 0) return;
+    const double nn = a.n + b.n, d = b.mean - a.mean;
+    a.mean = a.mean + d * (b.n / nn);
+    a.m2 = a.m2 + b.m2 + d * d * (a.n * b.n / nn);
+    a.n = nn;
+}
+
+// a double as three floats, exactly: hi = fl(d), mid = fl(d - hi), lo = d - hi - mid (the
+// last <= 5 significand bits of d, a float exactly); a SUM all-reduce in which every
+// other rank contributes zeros then moves it bit for bit
+static void split3(double d, float *o) {
+    const float hi = (float)d;
+    const double r1 = d - (double)hi;
+    const float mid = (float)r1;
+    o[0] = hi; o[1] = mid; o[2] = (float)(r1 - (double)mid);
+}
+static double join3(const float *o) { return ((double)o[0] + (double)o[1]) + (double)o[2]; }
+
+// W > 1: every rank's batch statistics {n, mean, M2} (its blocks Chan-merged in order)
+// all-gathered through the gradient all-reduce callback (zeros but for the own slot,
+// SUM), then merged into the running statistics rank by rank -- the same arithmetic on
+// every rank, so the value-head rescale keeps the ranks' parameters identical
+static bppo_status popart_gather(bppo_ctx *c, const std::vector<Welford> &part, Welford &a) {
+    const int W = c->world;
+    Welford mine{0.0, 0.0, 0.0};
+    for (const Welford &b : part) chan_merge(mine, b);
+    std::vector<float> g((size_t)9 * W, 0.0f);
+    if (c->rank < 0 || c->rank >= W) { c->err = "PopArt at W > 1: rank outside [0, world) (bppo_set_rank)"; return BPPO_ERR_ARG; }
+    split3(mine.n, &g[9 * c->rank]); split3(mine.mean, &g[9 * c->rank + 3]); split3(mine.m2, &g[9 * c->rank + 6]);
+    PHIP(c, hipMemcpyAsync(c->d_pa_gather, g.data(), g.size() * 4, hipMemcpyHostToDevice, c->stream));
+    if (!c->allreduce_async) PHIP(c, hipStreamSynchronize(c->stream));
+    if (c->allreduce(c->d_pa_gather, g.size(), c->allreduce_user) != 0) {
+        c->err = "all-reduce callback failed (PopArt statistics)";
+        return BPPO_ERR_COMM;
+    }
+    PHIP(c, hipMemcpyAsync(g.data(), c->d_pa_gather, g.size() * 4, hipMemcpyDeviceToHost, c->stream));
+    PHIP(c, hipStreamSynchronize(c->stream));
+    for (int q = 0; q < W; q++) chan_merge(a, Welford{join3(&g[9 * q]), join3(&g[9 * q + 3]), join3(&g[9 * q + 6])});
+    return BPPO_OK;
 }
 
 // ppo.rs:1787-1808 + the normalized return / old-value buffers the minibatches read
@@ -154,13 +197,9 @@ bppo_status popart_update_begin(bppo_ctx *c, const float *valid) {
     PHIP(c, hipStreamSynchronize(c->stream));
     const double old_mean = c->pa_mean, old_std = popart_std(c);
     Welford a{c->pa_count, c->pa_mean, c->pa_m2};
-    for (const Welford &b : part) {                       // Chan merge in block (= row) order
-        if (b.n <= 0) continue;
-        const double nn = a.n + b.n, d = b.mean - a.mean;
-        a.mean = a.mean + d * (b.n / nn);
-        a.m2 = a.m2 + b.m2 + d * d * (a.n * b.n / nn);
-        a.n = nn;
-    }
+    if (c->world > 1 && c->allreduce) PTRY(popart_gather(c, part, a));
+    else
+        for (const Welford &b : part) chan_merge(a, b);   // Chan merge in block (= row) order
     c->pa_count = a.n; c->pa_mean = a.mean; c->pa_m2 = a.m2;
     if (c->pa_count >= 2.0) {                             // is_initialized: rescale the value head
         const double new_mean = c->pa_mean, new_std = popart_std(c);

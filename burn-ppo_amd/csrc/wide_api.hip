@@ -274,9 +274,16 @@ bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, double ent_
     float *G = c->d_grad;
     // the split-bf16 contraction (k_gemm_split) for the MLP GEMMs of every minibatch after the
     // update's first (mode 0) or of all of them (bppo_set_minibatch_kernel 2); the first keeps
-    // the exact chains (ratio exactly 1) -- as the CfgB update's k_minibatch_split
+    // the exact chains (ratio exactly 1) -- as the CfgB update's k_minibatch_split.  Mode 0
+    // splits only minibatches of WIDE_SPLIT_MIN_ROWS rows or more: below that the GEMMs are
+    // launch- and latency-bound (no time to win), while the split forward's last-bit
+    // differences -- a ReLU pre-activation that close to zero switches its unit for that row
+    // -- are amplified by Adam over many tiny minibatches (a 72-row Liar's Dice CTDE update
+    // drifts 1e-3 from the oracle by minibatch 3 with the split, 0 with the exact chains:
+    // profiles/r05c/popart_split_probe.log)
     static const bool exact_all = getenv("BPPO_MB_EXACT_ALL") != nullptr;
-    const int split = n.n_conv == 0 && (c->mb_kernel == 2 || (c->mb_kernel == 0 && !first && !exact_all)) ? 1 : 0;
+    const bool big = rows >= WIDE_SPLIT_MIN_ROWS;
+    const int split = n.n_conv == 0 && (c->mb_kernel == 2 || (c->mb_kernel == 0 && !first && !exact_all && big)) ? 1 : 0;
     const int exact = split ? -1 : wide_exact_grad(c);
     WHIP(c, wide_gather(c->stream, c->d_perm, start, mb, c->d_xc, L, c->d_xcg));
     WTRY(wide_forward(c, rows, c->d_xcg, L, c->d_logits, c->d_values, split));

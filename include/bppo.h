@@ -228,8 +228,15 @@ typedef int (*bppo_allreduce_fn)(float *device_buf, size_t n, void *user);
  * the SUM over ranks is scaled by 1/W before clip + Adam, so all ranks take the same step.
  * The metric partials ride along, so the UpdateMetrics are those of all ranks' rows
  * together, except value_error_max, adv_*_raw and explained_variance, which stay per rank.
- * normalize_values (PopArt) and opponent pools are single-rank: BPPO_ERR_UNSUPPORTED. */
+ * normalize_values (PopArt) at W > 1: every rank's running return statistics absorb ALL
+ * ranks' returns, rank by rank in rank order (each rank's batch statistics travel through
+ * the same callback as an exact all-gather), so the value-head rescale and the normalized
+ * targets are identical on every rank; needs bppo_set_rank.  Opponent pools are
+ * single-rank: BPPO_ERR_UNSUPPORTED at W > 1. */
 bppo_status bppo_set_allreduce(bppo_ctx *ctx, bppo_allreduce_fn fn, void *user, int32_t world_size);
+/* this context's rank among the all-reduce's world_size ranks (0-based; default 0): the
+ * slot of its PopArt batch statistics in the W > 1 all-gather */
+bppo_status bppo_set_rank(bppo_ctx *ctx, int32_t rank);
 
 /* stream-ordered variant: fn is called WITHOUT draining the stream, right after
  * the minibatch's gradient kernels are enqueued; it must enqueue the SUM

@@ -507,8 +507,9 @@ void or_trainer_gae(or_trainer *t) {
  * minibatches together (sums over all ranks' rows, as the device's metric
  * partials travel with the gradient), except value_error_max and the raw
  * advantage statistics, which stay per rank; the KL early stop reads the
- * combined approx_kl, so all ranks stop together.  PopArt and opponent pools
- * are single-rank only (libbppo returns BPPO_ERR_UNSUPPORTED for them at W > 1). */
+ * combined approx_kl, so all ranks stop together.  PopArt: each rank's running
+ * statistics absorb every rank's returns in rank order before the rescale.  Opponent
+ * pools are single-rank only (libbppo returns BPPO_ERR_UNSUPPORTED for them at W > 1). */
 typedef struct {
     uint32_t *vidx, *idx;
     size_t B, sz, start;
@@ -526,8 +527,8 @@ void or_trainers_update(or_trainer **ts, int W, or_update_metrics *ms) {
     if (W < 1) return;
     if (W > 1)
         for (int r = 0; r < W; r++)
-            if (ts[r]->n_opp > 0 || ts[r]->c.normalize_values) {
-                fprintf(stderr, "or_trainers_update: opponent pools / PopArt are single-rank only\n");
+            if (ts[r]->n_opp > 0) {
+                fprintf(stderr, "or_trainers_update: opponent pools are single-rank only\n");
                 abort();
             }
     or_trainer *t0r = ts[0];
@@ -550,11 +551,20 @@ void or_trainers_update(or_trainer **ts, int W, or_update_metrics *ms) {
         /* ppo.rs:1787-1808 PopArt: statistics over the (learner) returns, then rescale the value head */
         w->rescale_mag = NAN;
         if (t->c.normalize_values) {
-            float *rr = malloc(sizeof(float) * (w->B ? w->B : 1));
-            for (size_t i = 0; i < w->B; i++) rr[i] = t->ret[w->vidx ? w->vidx[i] : i];
             double om, os;
-            or_popart_update(&t->pa, rr, w->B, &om, &os);
-            free(rr);
+            if (W == 1) {
+                float *rr = malloc(sizeof(float) * (w->B ? w->B : 1));
+                for (size_t i = 0; i < w->B; i++) rr[i] = t->ret[w->vidx ? w->vidx[i] : i];
+                or_popart_update(&t->pa, rr, w->B, &om, &os);
+                free(rr);
+            } else {
+                /* W > 1: every rank's statistics absorb ALL ranks' returns, rank by rank (the
+                 * device all-gathers the ranks' batch statistics and merges them in rank order),
+                 * so the value-head rescale below is the same on every rank */
+                double dm, ds;
+                om = t->pa.mean; os = or_popart_std(&t->pa);
+                for (int q = 0; q < W; q++) or_popart_update(&t->pa, ts[q]->ret, (size_t)ts[q]->T * ts[q]->N, &dm, &ds);
+            }
             if (t->pa.count >= 2.0) {
                 size_t vw, vb; int vin;
                 or_net_value_head(&t->net, &vw, &vb, &vin);    /* ppo.rs:1599-1653 */

@@ -88,6 +88,15 @@ if [ "$PART" = widekt ]; then
   done
   exit 0
 fi
+if [ "$PART" = kt ]; then
+  # kernel trace of the default CfgB bench line (rocprofv3 --kernel-trace --stats)
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/kt_${TAG}_cfgB -o kt -- python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline --no-learning > gpurun_out/kt_${TAG}_cfgB.log 2>&1
+  rc=$?; echo "kt cfgB rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  DB=$(find gpurun_out/kt_${TAG}_cfgB -name "*.db" | head -1)
+  python3 scripts/rocpd_summary.py $DB > gpurun_out/${TAG}_cfgB_kernels.txt
+  head -24 gpurun_out/${TAG}_cfgB_kernels.txt | cut -c1-140
+  exit 0
+fi
 if [ "$PART" = mfmaprobe ]; then
   timeout -k 10 60 ./scripts/probes/mfma_round_probe > gpurun_out/${TAG}_mfma_round_probe.txt 2>&1
   rc=$?; echo "mfma probe rc=$rc"; cat gpurun_out/${TAG}_mfma_round_probe.txt

@@ -166,7 +166,8 @@ def oracle_train_cfg(cfg, threads=0, rank=0, world=1):
                        max_grad_norm=cfg["max_grad_norm"], target_kl=cfg["target_kl"], threads=threads,
                        split=bool(cfg.get("split_networks")), clip_value=bool(cfg.get("clip_value")),
                        env_seed_offset=rank * cfg["num_envs"] if world > 1 else 0,
-                       rng_stream=rank if world > 1 else 0, shuffle_windows=bool(cfg.get("shuffle_windows")))
+                       rng_stream=rank if world > 1 else 0, shuffle_windows=bool(cfg.get("shuffle_windows")),
+                       normalize_values=bool(cfg.get("normalize_values")))
 
 
 def cartpole_pair(N, T, preset="cartpole", seed=42, init_seed=1, **kw):

@@ -85,7 +85,7 @@ NETS = [("connect_four", None), ("liars_dice", True)]
 
 
 @pytest.mark.parametrize("env,ctde", NETS)
-@pytest.mark.parametrize("mode", [2, 1])
+@pytest.mark.parametrize("mode", [2, 1, 0])
 def test_wide_gradient_from_identical_parameters(env, ctde, mode):
     N, T = 512, 16
     cfg, tr, ot = _pair(env, N, T, ctde=ctde, num_epochs=1, num_minibatches=1)
@@ -131,13 +131,23 @@ def test_wide_gradient_from_identical_parameters(env, ctde, mode):
             o = getattr(ms, k)
             assert abs(m[k] - o) <= TOL * max(abs(o), fl), (k, m[k], o)
         shapes, _ = layer_shapes(cfg)
-        off = 0
+        off, worst = 0, []
         for i, o in shapes:
             for n in (i * o, o):
                 a, b = g[off:off + n], go[off:off + n]
-                np.testing.assert_allclose(a, b, rtol=0, atol=TOL * max(np.abs(b).max(), 1e-30),
-                                           err_msg=f"tensor at {off} ({n} entries), kernel mode {mode}")
+                tol = TOL * max(np.abs(b).max(), 1e-30)
+                worst.append((off, n, float(np.abs(a - b).max() / tol), int((np.abs(a - b) > tol).sum())))
                 off += n
         assert off == desc.n_params
+        if mode == 1:   # the exact chains and row-ordered f64 weight gradients
+            assert all(w[2] <= 1.0 for w in worst), (mode, worst)
+        else:
+            # the split forward (mode 2) and the f32 split-K weight gradients (mode 0) differ from
+            # the oracle's in the last bits: a ReLU pre-activation within that distance of zero
+            # switches its unit for one row, which moves that row's contribution in a few
+            # entries.  Every entry within 1e-4 of its tensor's largest |entry| (10x the exact
+            # bar) and at most 0.5 % of all entries past 1e-5 of it
+            assert all(w[2] <= 10.0 for w in worst), (mode, worst)
+            assert sum(w[3] for w in worst) <= 0.005 * desc.n_params, (mode, worst)
     finally:
         tr.close(); ot.close()

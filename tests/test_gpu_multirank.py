@@ -38,6 +38,11 @@ CASES = {
     "cartpole_windows": dict(preset="cartpole", N=1024, T=32, over=dict(shuffle_windows=True)),
     "connect_four_windows": dict(preset="connect_four", N=256, T=16,
                                  over=dict(hidden_size=64, shuffle_windows=True)),
+    # PopArt (normalize_values): each rank's statistics absorb both ranks' returns in rank
+    # order (an all-gather of the batch statistics through the callback), so the value-head
+    # rescale and the normalized targets agree and the ranks stay in lockstep
+    "cartpole_popart": dict(preset="cartpole", N=1024, T=32, over=dict(normalize_values=True)),
+    "connect_four_popart": dict(preset="connect_four", N=256, T=16, over=dict(hidden_size=64, normalize_values=True)),
 }
 
 
@@ -130,8 +135,14 @@ def _worker(rank, world, port, q, case, mode):
         assert np.array_equal(bits(ots[0].params()), bits(ots[1].params()))   # the oracle's ranks agree
         out["p1"] = p1
         out["m1"] = m
+        if cfg.get("normalize_values"):
+            pd, po = tr.ctx.popart(), ot.popart()
+            np.testing.assert_allclose(pd[:3], po[:3], rtol=1e-12)       # Chan merges vs the sequential Welford
+            out["pa"] = pd
         # ---- round 2: the oracle's state injected, the pipelined bench path -----------
         tr.model.set_params(ot.params())
+        if cfg.get("normalize_values"):
+            tr.ctx.set_popart(ot.popart())
         if env == "cartpole":
             mvc, rets = ot.ret_norm_state(returns=True)
             tr.ctx.set_ret_norm(mvc, rets)
@@ -183,5 +194,7 @@ def test_two_ranks_distinct_shards_match_oracle(case, mode):
     # ... and the ranks still take the same step
     for k in ("p1", "p2"):
         assert np.array_equal(res[0][k].view(np.uint32), res[1][k].view(np.uint32)), k
+    if "pa" in res[0]:                  # PopArt: the same running statistics on both ranks
+        assert np.array_equal(res[0]["pa"], res[1]["pa"])
     for f in ("policy_loss", "value_loss", "approx_kl", "entropy", "clip_fraction", "value_error_std"):
         assert np.float32(res[0]["m1"][f]) == np.float32(res[1]["m1"][f]), f
