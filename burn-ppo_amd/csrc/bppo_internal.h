@@ -497,14 +497,17 @@ void cnn_free(bppo_ctx *c);
 bppo_status cnn_pack(bppo_ctx *c, const float *params, float *wt, float *wd);
 bppo_status cnn_features(bppo_ctx *c, int s, int rows, const float *x, int ldx, const float *params, const float *wt);
 bppo_status cnn_backward(bppo_ctx *c, int s, int rows, const float *x, int ldx, float *dF, float *grad, int exact);
-// how the wide path sums its weight gradients (gemm_wgrad's `exact`): 0 f32 split-K MFMA
-// chains; 1 f64 products and sums on the f64 MFMA (k_gemm_wg64), the CNN default: an f32 chain
-// over a conv layer's B*42 positions leaves the parameters ~1 ulp off the oracle's after each
-// Adam step, which the PPO loss amplifies; 2 the oracle's row-ordered f64 sums (k_wg_seq,
+// how the wide path sums its weight gradients (gemm_wgrad's `exact`) where it does not run the
+// split-bf16 contraction: 0 f32 split-K MFMA chains (mode 2); 1 f64 products and sums on the
+// f64 MFMA (k_gemm_wg64), the default (mode 0): f32 chains over a minibatch's rows leave the
+// parameters ~1 ulp off the oracle's after each Adam step, which the PPO loss amplifies (a
+// 64-channel conv layer's B*42 positions from minibatch 12 on, r04; the Liar's Dice MLP's
+// 1024-row minibatches at minibatch 26 of 32, profiles/r05c/wide_scale_probe.json), f64 sums
+// round to the oracle's f32 but for rare ties; 2 the oracle's row-ordered f64 sums (k_wg_seq,
 // bppo_set_minibatch_kernel 1: the reference-exact parity mode)
 inline int wide_exact_grad(const bppo_ctx *c) {
     if (c->mb_kernel == 1) return 2;
-    return c->mb_kernel == 0 && c->net.n_conv > 0 ? 1 : 0;
+    return c->mb_kernel == 0 ? 1 : 0;
 }
 // opponent pool (opponents.hip)
 bool opp_active(const bppo_ctx *c);

@@ -375,41 +375,31 @@ typedef __bf16 sbf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 sbf16x2 __attribute__((ext_vector_type(2)));
 constexpr int SKP = GBK + 8;
 
-// three pieces of Q consecutive-k values -> LDS rows at s[p * plane + off].  Pairs: one
-// v_cvt_pk_bf16_f32 per piece pair, the pieces' f32 values read back from that word (the
-// asm makes it opaque: otherwise each half is converted again on its own)
-__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
-    uint32_t u = __builtin_bit_cast(uint32_t, sbf16x2{(__bf16)a, (__bf16)b});
-    asm("" : "+v"(u));
-    return u;
-}
+// three pieces of Q consecutive-k values -> LDS rows at s[p * plane + off].  (A pair-wise
+// form -- one v_cvt_pk_bf16_f32 per piece pair, the halves read back from the packed word
+// through an opaque asm -- ran the CfgC update 151-166 ms against 143 ms for this one:
+// profiles/r05c/split_store_ab.txt)
+typedef __bf16 sbf16x4 __attribute__((ext_vector_type(4)));
 template <int Q>
 __device__ __forceinline__ void split_store(const float *x, __bf16 *s, int plane, int off) {
-    if constexpr (Q >= 2) {
-        uint32_t p0[Q / 2], p1[Q / 2], p2[Q / 2];
+    __bf16 p0[Q], p1[Q], p2[Q];
 #pragma unroll
-        for (int j = 0; j < Q / 2; j++) {
-            const float xa = x[2 * j], xb = x[2 * j + 1];
-            const uint32_t A = pk_bf16(xa, xb);
-            const float ra = xa - __uint_as_float(A << 16), rb = xb - __uint_as_float(A & 0xffff0000u);
-            const uint32_t B = pk_bf16(ra, rb);
-            const float sa = ra - __uint_as_float(B << 16), sb = rb - __uint_as_float(B & 0xffff0000u);
-            p0[j] = A; p1[j] = B; p2[j] = pk_bf16(sa, sb);
-        }
-        if constexpr (Q == 4) {
-            *reinterpret_cast<uint2 *>(s + off) = make_uint2(p0[0], p0[1]);
-            *reinterpret_cast<uint2 *>(s + plane + off) = make_uint2(p1[0], p1[1]);
-            *reinterpret_cast<uint2 *>(s + 2 * plane + off) = make_uint2(p2[0], p2[1]);
-        } else {
-            *reinterpret_cast<uint32_t *>(s + off) = p0[0];
-            *reinterpret_cast<uint32_t *>(s + plane + off) = p1[0];
-            *reinterpret_cast<uint32_t *>(s + 2 * plane + off) = p2[0];
-        }
-    } else {
-        const __bf16 a = (__bf16)x[0];
-        const float r = x[0] - (float)a;
+    for (int j = 0; j < Q; j++) {
+        const __bf16 a = (__bf16)x[j];
+        const float r = x[j] - (float)a;
         const __bf16 b = (__bf16)r;
-        s[off] = a; s[plane + off] = b; s[2 * plane + off] = (__bf16)(r - (float)b);
+        p0[j] = a; p1[j] = b; p2[j] = (__bf16)(r - (float)b);
+    }
+    if constexpr (Q == 4) {
+        *reinterpret_cast<sbf16x4 *>(s + off) = sbf16x4{p0[0], p0[1], p0[2], p0[3]};
+        *reinterpret_cast<sbf16x4 *>(s + plane + off) = sbf16x4{p1[0], p1[1], p1[2], p1[3]};
+        *reinterpret_cast<sbf16x4 *>(s + 2 * plane + off) = sbf16x4{p2[0], p2[1], p2[2], p2[3]};
+    } else if constexpr (Q == 2) {
+        *reinterpret_cast<sbf16x2 *>(s + off) = sbf16x2{p0[0], p0[1]};
+        *reinterpret_cast<sbf16x2 *>(s + plane + off) = sbf16x2{p1[0], p1[1]};
+        *reinterpret_cast<sbf16x2 *>(s + 2 * plane + off) = sbf16x2{p2[0], p2[1]};
+    } else {
+        s[off] = p0[0]; s[plane + off] = p1[0]; s[2 * plane + off] = p2[0];
     }
 }
 

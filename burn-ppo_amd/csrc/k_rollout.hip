@@ -682,7 +682,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
         const float *hrow = Tw + lane * 65 + zero;
         // batches of 8 units: the batch's 8 weight rows and 8 activations are all read before
         // its chains consume them, one LDS round trip per batch (the per-unit form waited on
-        // every read: 24% of the step under the segment stamps)
+        // every read: 24% of the step under the segment stamps; a double-buffered 4-unit form
+        // measured no better, profiles/r05c/rollout_stamps.txt)
         float l0 = 0.0f, l1 = 0.0f, vv = 0.0f;
 #pragma unroll 1
         for (int k0 = 0; k0 < H; k0 += 8) {

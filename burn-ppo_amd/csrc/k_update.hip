@@ -794,6 +794,17 @@ __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
 }
 union Pieces8 { bf16x8_t v; uint32_t u[4]; };
 __device__ __forceinline__ Split8 split8(const float (&x)[8]) {
+#ifdef BPPO_SPLIT8_SCALAR       // A/B build: each element converted on its own (r04 form)
+    Split8 t;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const __bf16 a = (__bf16)x[j];
+        const float r = x[j] - (float)a;
+        const __bf16 b = (__bf16)r;
+        t.p[0][j] = a; t.p[1][j] = b; t.p[2][j] = (__bf16)(r - (float)b);
+    }
+    return t;
+#endif
     Pieces8 p0, p1, p2;
 #pragma unroll
     for (int j = 0; j < 4; j++) {

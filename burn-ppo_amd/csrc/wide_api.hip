@@ -284,7 +284,12 @@ bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, double ent_
     static const bool exact_all = getenv("BPPO_MB_EXACT_ALL") != nullptr;
     const bool big = rows >= WIDE_SPLIT_MIN_ROWS;
     const int split = n.n_conv == 0 && (c->mb_kernel == 2 || (c->mb_kernel == 0 && !first && !exact_all && big)) ? 1 : 0;
-    const int exact = split ? -1 : wide_exact_grad(c);
+    // weight-gradient sums: f64 (or row-ordered, mode 1) for the small minibatches; from
+    // WIDE_SPLIT_MIN_ROWS rows the f32 split-K chains (the update's first minibatch, and the
+    // CNN's) -- the f64 MFMA runs them ~4x slower (CfgC 142 -> 151 ms per update, CfgD 482 ->
+    // 517 ms, profiles/r05c/r05t_wide_*.log) and the minibatches after the first run the
+    // split-bf16 contraction anyway
+    const int exact = split ? -1 : (big && c->mb_kernel == 0 ? 0 : wide_exact_grad(c));
     WHIP(c, wide_gather(c->stream, c->d_perm, start, mb, c->d_xc, L, c->d_xcg));
     WTRY(wide_forward(c, rows, c->d_xcg, L, c->d_logits, c->d_values, split));
     LossArgs g;
