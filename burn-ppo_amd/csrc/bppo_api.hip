@@ -1067,13 +1067,17 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
             c->d_perm = c->d_perm_ep + (size_t)ep * B;
         }
         // no learner rows (opponent pool): the reference shuffles an empty index
-        // list (no RNG words) and skips every minibatch (ppo.rs:1815-1831)
-        if (B == 0) continue;
-        TRY(launch_epoch_adv_stats(c, (uint32_t)B, M, opp ? nullptr : c->d_inv_ep + (size_t)ep * B));
+        // list (no RNG words) and skips every minibatch (ppo.rs:1815-1831).  W > 1: the
+        // ranks' learner-row counts differ, so every rank runs all M minibatch slots of
+        // every epoch in lockstep (one all-reduce each); a rank whose slot is empty adds a
+        // zero gradient and zero metric partials (oracle/ppo.c or_trainers_update)
+        const bool lockstep = c->allreduce && c->world > 1;
+        if (B == 0 && !lockstep) continue;
+        if (B) TRY(launch_epoch_adv_stats(c, (uint32_t)B, M, opp ? nullptr : c->d_inv_ep + (size_t)ep * B));
         size_t start = 0;
         for (int mb = 0; mb < M; mb++) {
             const size_t sz = base_mb + ((size_t)mb < rem ? 1 : 0);
-            if (sz == 0) continue;
+            if (sz == 0 && !lockstep) continue;
             // the "minibatch" phase time is the last minibatch's (read after the update in the
             // deferred path): only that one is bracketed there -- each timestamp marker on the
             // stream costs a few us of idle compute stream
@@ -1089,8 +1093,14 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
             }
             float *metric_dst = c->d_rows + (size_t)nrow * (NM + 4);
             const bool multi = c->allreduce && c->world > 1;
-            if (c->wide) TRY(wide_minibatch(c, (uint32_t)start, (uint32_t)sz, ent_coef, first_mb));
-            else TRY(launch_minibatch(c, (uint32_t)start, (uint32_t)sz, (float)ent_coef, first_mb));
+            if (sz == 0) {                 // lockstep slot without rows on this rank
+                BPPO_HIP(c, hipMemsetAsync(c->d_grad, 0, sizeof(float) * ((size_t)np + 64), c->stream));   // + tail
+                BPPO_HIP(c, hipMemsetAsync(c->d_mb_cur, 0, sizeof(float) * 4, c->stream));
+            } else if (c->wide) {
+                TRY(wide_minibatch(c, (uint32_t)start, (uint32_t)sz, ent_coef, first_mb));
+            } else {
+                TRY(launch_minibatch(c, (uint32_t)start, (uint32_t)sz, (float)ent_coef, first_mb));
+            }
             if (fw_timed) BPPO_HIP(c, hipEventRecord(c->ev[TM_FWDBWD][1], c->stream));
             first_mb = false;
             if (multi) {
@@ -1327,11 +1337,9 @@ extern "C" bppo_status bppo_train_steps(bppo_ctx *c, int32_t n, const double *lr
     return BPPO_OK;
 }
 
-// W > 1: an opponent pool trains a per-rank number of learner rows,
-// so the ranks' minibatches would not line up.  PopArt's statistics are all-gathered
-// (popart.hip): its scratch is sized for the world here
+// W > 1.  PopArt's statistics are all-gathered (popart.hip): its
+// scratch is sized for the world here
 static bppo_status check_world(bppo_ctx *c, int32_t world) {
-    if (world > 1 && opp_active(c)) { c->err = "opponent pool: single-rank only"; return BPPO_ERR_UNSUPPORTED; }
     if (world > 1 && c->cfg.normalize_values) {
         if (c->d_pa_gather) { BPPO_HIP(c, hipFree(c->d_pa_gather)); c->d_pa_gather = nullptr; }
         BPPO_HIP(c, hipMalloc((void **)&c->d_pa_gather, sizeof(float) * 9 * (size_t)world));

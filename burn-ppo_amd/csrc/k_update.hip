@@ -1231,6 +1231,9 @@ __global__ void __launch_bounds__(SLAB1_COLS * SLAB_GROUPS) k_slab_reduce1(const
                                                                            int width, float *__restrict__ grad,
                                                                            float *__restrict__ vemax_local) {
     __shared__ double part[SLAB_GROUPS][SLAB1_COLS];
+#ifndef BPPO_NO_PRIO
+    __builtin_amdgcn_s_setprio(3);      // ahead of the side-stream Fisher-Yates waves beside it
+#endif
     const int c = threadIdx.x % SLAB1_COLS, g = threadIdx.x / SLAB1_COLS;
     const int p = blockIdx.x * SLAB1_COLS + c;
     const bool live = p < width, is_max = p == width - NUM_M + M_VEMAX;

@@ -370,9 +370,6 @@ extern "C" bppo_status bppo_opponents_set(bppo_ctx *c, int32_t n_models, const f
     if (!c->wide) { c->err = "opponent pool: multi-player envs only"; return BPPO_ERR_UNSUPPORTED; }
     if (n_models < 0 || n_models > OPP_MAX_MODELS) { c->err = "opponent pool: 0..15 models"; return BPPO_ERR_ARG; }
     if (num_opponent_envs < 0 || num_opponent_envs > c->N) { c->err = "opponent pool: num_opponent_envs > num_envs"; return BPPO_ERR_ARG; }
-    // the learner-row count differs per rank, so the ranks' minibatches (and their
-    // all-reduce calls) would not line up: single-rank only
-    if (num_opponent_envs > 0 && c->world > 1) { c->err = "opponent pool: single-rank only (world_size > 1)"; return BPPO_ERR_UNSUPPORTED; }
     if (num_opponent_envs > 0 && c->cfg.shuffle_windows) { c->err = "opponent pool: not with shuffle_windows"; return BPPO_ERR_UNSUPPORTED; }
     if (num_opponent_envs > 0 && (!params || !learner_pos || !pos_to_opp || !current_opp || n_models == 0)) {
         c->err = "opponent pool: models and seat state required";

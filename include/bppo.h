@@ -231,8 +231,10 @@ typedef int (*bppo_allreduce_fn)(float *device_buf, size_t n, void *user);
  * normalize_values (PopArt) at W > 1: every rank's running return statistics absorb ALL
  * ranks' returns, rank by rank in rank order (each rank's batch statistics travel through
  * the same callback as an exact all-gather), so the value-head rescale and the normalized
- * targets are identical on every rank; needs bppo_set_rank.  Opponent pools are
- * single-rank: BPPO_ERR_UNSUPPORTED at W > 1. */
+ * targets are identical on every rank; needs bppo_set_rank.  Opponent pools at W > 1: each
+ * rank trains on its own learner rows, cut into num_minibatches of its own sizes; the
+ * minibatch slots run in lockstep (one callback each), a rank without rows in a slot
+ * contributing a zero gradient and zero metric partials. */
 bppo_status bppo_set_allreduce(bppo_ctx *ctx, bppo_allreduce_fn fn, void *user, int32_t world_size);
 /* this context's rank among the all-reduce's world_size ranks (0-based; default 0): the
  * slot of its PopArt batch statistics in the W > 1 all-gather */

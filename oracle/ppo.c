@@ -509,7 +509,8 @@ void or_trainer_gae(or_trainer *t) {
  * advantage statistics, which stay per rank; the KL early stop reads the
  * combined approx_kl, so all ranks stop together.  PopArt: each rank's running
  * statistics absorb every rank's returns in rank order before the rescale.  Opponent
- * pools are single-rank only (libbppo returns BPPO_ERR_UNSUPPORTED for them at W > 1). */
+ * pools: each rank trains on its own learner rows, cut into num_minibatches of its own
+ * sizes; the slots run in lockstep, a rank without rows in one adding a zero gradient. */
 typedef struct {
     uint32_t *vidx, *idx;
     size_t B, sz, start;
@@ -525,12 +526,6 @@ typedef struct {
 void or_trainers_update(or_trainer **ts, int W, or_update_metrics *ms) {
     double t0 = now_s();
     if (W < 1) return;
-    if (W > 1)
-        for (int r = 0; r < W; r++)
-            if (ts[r]->n_opp > 0) {
-                fprintf(stderr, "or_trainers_update: opponent pools are single-rank only\n");
-                abort();
-            }
     or_trainer *t0r = ts[0];
     const int D = t0r->D, A = t0r->A, G = t0r->G;
     const or_ppo_cfg *c = &t0r->c.ppo;
@@ -548,6 +543,10 @@ void or_trainers_update(or_trainer **ts, int W, or_update_metrics *ms) {
             for (size_t i = 0; i < w->B; i++) if (t->valid[i] > 0.5f) w->vidx[nv++] = (uint32_t)i;
             w->B = nv;
         }
+    }
+    for (int r = 0; r < W; r++) {
+        or_trainer *t = ts[r];
+        rank_ws *w = &ws[r];
         /* ppo.rs:1787-1808 PopArt: statistics over the (learner) returns, then rescale the value head */
         w->rescale_mag = NAN;
         if (t->c.normalize_values) {
@@ -563,7 +562,13 @@ void or_trainers_update(or_trainer **ts, int W, or_update_metrics *ms) {
                  * so the value-head rescale below is the same on every rank */
                 double dm, ds;
                 om = t->pa.mean; os = or_popart_std(&t->pa);
-                for (int q = 0; q < W; q++) or_popart_update(&t->pa, ts[q]->ret, (size_t)ts[q]->T * ts[q]->N, &dm, &ds);
+                for (int q = 0; q < W; q++) {
+                    const rank_ws *wq = &ws[q];
+                    float *rr = malloc(sizeof(float) * (wq->B ? wq->B : 1));
+                    for (size_t i = 0; i < wq->B; i++) rr[i] = ts[q]->ret[wq->vidx ? wq->vidx[i] : i];
+                    or_popart_update(&t->pa, rr, wq->B, &dm, &ds);
+                    free(rr);
+                }
             }
             if (t->pa.count >= 2.0) {
                 size_t vw, vb; int vin;
@@ -574,7 +579,6 @@ void or_trainers_update(or_trainer **ts, int W, or_update_metrics *ms) {
                 w->rescale_mag = (float)fabs(sc);
             }
         }
-        if (W > 1 && w->B != ws[0].B) { fprintf(stderr, "or_trainers_update: ranks differ in rows\n"); abort(); }
         size_t mbm = w->B / c->num_minibatches + 1;
         if (mbm > mbmax) mbmax = mbm;
     }
@@ -617,15 +621,28 @@ void or_trainers_update(or_trainer **ts, int W, or_update_metrics *ms) {
             or_shuffle_u32(&ts[r]->rng, w->idx, w->B);                    /* :1816 */
             w->start = 0;
         }
-        const size_t B = ws[0].B;
-        size_t base = B / c->num_minibatches, rem = B % c->num_minibatches;
+        /* each rank cuts its own rows into num_minibatches (its learner-row count under an
+         * opponent pool); W > 1 runs every slot on every rank in lockstep, a rank without
+         * rows in a slot adding a zero gradient (the device's all-reduce count must match) */
         for (int mbi = 0; mbi < c->num_minibatches; mbi++) {
-            size_t sz = base + ((size_t)mbi < rem ? 1 : 0);
-            if (sz == 0) continue;
+            size_t sz_any = 0;
+            for (int r = 0; r < W; r++) {
+                const size_t Br = ws[r].B;
+                ws[r].sz = Br / c->num_minibatches + ((size_t)mbi < Br % c->num_minibatches ? 1 : 0);
+                sz_any += ws[r].sz;
+            }
+            if (W == 1 && sz_any == 0) continue;
             for (int r = 0; r < W; r++) {
                 or_trainer *t = ts[r];
                 rank_ws *w = &ws[r];
-                w->sz = sz;
+                const size_t sz = w->sz;
+                if (sz == 0) {
+                    memset(w->grads, 0, sizeof(float) * np);
+                    memset(&w->st, 0, sizeof w->st);
+                    w->am = w->as = 0.0f; w->amn = INFINITY; w->amx = -INFINITY;
+                    w->st.value_error_max = -INFINITY;
+                    continue;
+                }
                 for (size_t q = 0; q < sz; q++) {                    /* :1833-1857 gather */
                     size_t i = w->vidx ? w->vidx[w->idx[w->start + q]] : w->idx[w->start + q];
                     memcpy(w->mo + q * D, t->obs + i * D, sizeof(float) * D);
@@ -657,14 +674,16 @@ void or_trainers_update(or_trainer **ts, int W, or_update_metrics *ms) {
                 for (size_t k = 0; k < np; k++) gstep[k] = gsum[k] * inv_world;
                 /* the metrics of all ranks' rows together */
                 size_t o = 0;
-                for (int r = 0; r < W; r++, o += sz) {
+                for (int r = 0; r < W; r++) {
                     rank_ws *w = &ws[r];
+                    const size_t sz = w->sz;
                     memcpy(co + o * D, w->mo, sizeof(float) * sz * D);
                     if (G) memcpy(cp + o * G, w->mp, sizeof(float) * sz * G);
                     if (cm) memcpy(cm + o * A, w->mm, sizeof(float) * sz * A);
                     memcpy(ca + o, w->ma, sizeof(int32_t) * sz); memcpy(clp + o, w->mlp, sizeof(float) * sz);
                     memcpy(cadv + o, w->madvn, sizeof(float) * sz); memcpy(cret + o, w->mret, sizeof(float) * sz);
                     memcpy(cov + o, w->mov, sizeof(float) * sz);
+                    o += sz;
                 }
                 or_minibatch_loss_grad(&t0r->net, t0r->params, o, co, cp, ca, clp, cadv, cret, cov, cm, c,
                                        t0r->c.ent_coef, NULL, &stg);
@@ -678,7 +697,7 @@ void or_trainers_update(or_trainer **ts, int W, or_update_metrics *ms) {
                 w->tam += w->am; w->tas += w->as;
                 w->tamin = fminf(w->tamin, w->amn); w->tamax = fmaxf(w->tamax, w->amx);
                 w->tvemax = fmaxf(w->tvemax, w->st.value_error_max);
-                w->start += sz;
+                w->start += w->sz;
             }
             for (int r = 0; r < W; r++)
                 if (ts[r]->n_mblog < OR_MB_LOG_MAX) ts[r]->mblog[ts[r]->n_mblog++] = stg;

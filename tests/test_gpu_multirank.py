@@ -43,7 +43,32 @@ CASES = {
     # rescale and the normalized targets agree and the ranks stay in lockstep
     "cartpole_popart": dict(preset="cartpole", N=1024, T=32, over=dict(normalize_values=True)),
     "connect_four_popart": dict(preset="connect_four", N=256, T=16, over=dict(hidden_size=64, normalize_values=True)),
+    # opponent pools: each rank plays its own seat assignment against the same pool, so its
+    # learner-row count differs from the other rank's; the minibatch slots run in lockstep
+    # (per-rank sizes, one all-reduce each).  Three-call path only (round 1)
+    "connect_four_opp": dict(preset="connect_four", N=128, T=16, over=dict(hidden_size=64), opp=(96, 2)),
+    "liars_dice_opp": dict(preset="liars_dice_ctde", N=96, T=12,
+                           over=dict(hidden_size=64, critic_hidden_size=64, critic_num_hidden=2), opp=(64, 3)),
 }
+
+
+def _opp_arrays(cfg, D, P, n_opp, K, rank):
+    """the pool (the same models on every rank, one with its own obs normalizer) and this
+    rank's seats (learner position, the model on every other seat, current opponents)"""
+    import bppo
+    rng = np.random.default_rng(100 + rank)
+    params = np.stack([bppo.orthogonal_init(cfg, seed=300 + k) for k in range(K)])
+    nrng = np.random.default_rng(7)
+    norms = [None] * K
+    norms[K - 1] = (nrng.normal(size=D) * 0.1, (nrng.random(D) + 0.5) * 500.0, 500.0)
+    lp = rng.integers(0, P, n_opp).astype(np.int32)
+    po = np.full((n_opp, P), -1, np.int32)
+    for e in range(n_opp):
+        for p in range(P):
+            if p != lp[e]:
+                po[e, p] = rng.integers(0, K)
+    co = rng.integers(0, K, P - 1).astype(np.int32)
+    return params, norms, lp, po, co
 
 
 def _port():
@@ -100,6 +125,16 @@ def _worker(rank, world, port, q, case, mode):
         ots = _oracle_ranks(cfg, params, world)      # both ranks' oracle (deterministic in every process)
         ot = ots[rank]
         env = cfg["env"]
+        opp = c.get("opp")
+        if opp:
+            n_opp, K = opp
+            D, P = {"connect_four": (86, 2), "liars_dice": (270, 4)}[env]
+            for r, o in enumerate(ots):        # rank r: its own seats on n_opp - 16 r envs
+                n_r = n_opp - 16 * r
+                pr, nr, lp, po, co = _opp_arrays(cfg, D, P, n_r, K, r)
+                o.set_opponents(pr, nr, n_r, lp, po.reshape(-1), co)
+                if r == rank:
+                    tr.ctx.set_opponents(pr, nr, n_r, lp, po, co)
         lr, ent = bppo.schedule_get(cfg["learning_rate"], 0), bppo.schedule_get(cfg["entropy_coef"], 0)
         # ---- round 1: the three calls, every stage compared --------------------------
         bppo.collect_rollouts(tr.ctx)
@@ -125,11 +160,19 @@ def _worker(rank, world, port, q, case, mode):
         oms = O.Trainer.update_ranks(ots)
         assert tr.ctx.rng_pos() == ot.rng_pos()
         B = c["N"] * c["T"]
-        perm, end = _last_perm(cfg["seed"], rank, start, B, m["epochs_run"],
-                               bool(cfg.get("shuffle_windows")), cfg["num_epochs"])
-        assert end == tr.ctx.rng_pos()
-        assert np.array_equal(tr.ctx.buffer("perm", np.uint32)[:B], perm)
-        assert_metrics_close(m, oms[rank], values=ot.buffer("values"), returns=ot.buffer("returns"), advantages=ot.buffer("advantages"))
+        if not opp:     # (opponent pools shuffle the learner rows: the RNG position covers it)
+            perm, end = _last_perm(cfg["seed"], rank, start, B, m["epochs_run"],
+                                   bool(cfg.get("shuffle_windows")), cfg["num_epochs"])
+            assert end == tr.ctx.rng_pos()
+            assert np.array_equal(tr.ctx.buffer("perm", np.uint32)[:B], perm)
+        if opp:
+            vm = ot.buffer("valid") > 0.5
+            assert np.array_equal(tr.ctx.buffer("valid"), ot.buffer("valid"))
+            out["rows"] = int(vm.sum())
+            assert_metrics_close(m, oms[rank], values=ot.buffer("values")[vm], returns=ot.buffer("returns")[vm],
+                                 advantages=ot.buffer("advantages")[vm])
+        else:
+            assert_metrics_close(m, oms[rank], values=ot.buffer("values"), returns=ot.buffer("returns"), advantages=ot.buffer("advantages"))
         p1 = tr.model.get_params()
         assert_params_close(p1, ot.params())
         assert np.array_equal(bits(ots[0].params()), bits(ots[1].params()))   # the oracle's ranks agree
@@ -139,6 +182,13 @@ def _worker(rank, world, port, q, case, mode):
             pd, po = tr.ctx.popart(), ot.popart()
             np.testing.assert_allclose(pd[:3], po[:3], rtol=1e-12)       # Chan merges vs the sequential Welford
             out["pa"] = pd
+        if opp:                         # three-call path only
+            out["p2"] = p1
+            tr.close()
+            for o in ots:
+                o.close()
+            out["ok"] = True
+            return
         # ---- round 2: the oracle's state injected, the pipelined bench path -----------
         tr.model.set_params(ot.params())
         if cfg.get("normalize_values"):
@@ -196,5 +246,7 @@ def test_two_ranks_distinct_shards_match_oracle(case, mode):
         assert np.array_equal(res[0][k].view(np.uint32), res[1][k].view(np.uint32)), k
     if "pa" in res[0]:                  # PopArt: the same running statistics on both ranks
         assert np.array_equal(res[0]["pa"], res[1]["pa"])
+    if "rows" in res[0]:                # opponent pools: the ranks trained on different row counts
+        assert res[0]["rows"] != res[1]["rows"]
     for f in ("policy_loss", "value_loss", "approx_kl", "entropy", "clip_fraction", "value_error_std"):
         assert np.float32(res[0]["m1"][f]) == np.float32(res[1]["m1"][f]), f

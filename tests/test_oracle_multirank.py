@@ -99,3 +99,69 @@ def test_shuffle_windows_positions():
     assert not np.array_equal(a.params().view(np.uint32), b.params().view(np.uint32))
     for t in (seq, win, a, b):
         t.close()
+
+
+def test_popart_two_ranks_absorb_both_ranks_returns():
+    """PopArt at W = 2 (normalize_values): each rank's running statistics absorb rank 0's
+    returns, then rank 1's (a sequential Welford over both), so both ranks rescale the
+    value head the same way and keep identical parameters"""
+    cfg = _cfg(num_epochs=1, num_minibatches=2, normalize_values=True)
+    params = bppo.orthogonal_init(cfg, seed=6)
+    ranks = [O.Trainer(oracle_train_cfg(cfg, rank=r, world=2), params) for r in range(2)]
+    for t in ranks:
+        t.collect(); t.gae()
+    rets = [t.buffer("returns").astype(np.float64) for t in ranks]
+    O.Trainer.update_ranks(ranks)
+    st = [t.popart() for t in ranks]
+    assert np.array_equal(st[0], st[1])
+    n, mean, m2 = 0.0, 0.0, 0.0
+    for x in np.concatenate(rets):               # the sequential Welford, rank 0's rows first
+        n += 1.0
+        d = x - mean
+        mean += d / n
+        m2 += d * (x - mean)
+    assert st[0][2] == n and st[0][0] == mean and st[0][1] == m2
+    assert np.array_equal(ranks[0].params().view(np.uint32), ranks[1].params().view(np.uint32))
+    for t in ranks:
+        t.close()
+
+
+def test_opponent_pool_two_ranks_lockstep():
+    """opponent pools at W = 2: the ranks' learner-row counts differ (their own seats), each
+    cuts its rows into num_minibatches of its own sizes and the slots run in lockstep; both
+    ranks end with identical parameters, and W = 2 ranks with IDENTICAL shards and seats
+    equal the single-rank opponent-pool update bit for bit"""
+    cfg = bppo.make_config("connect_four", num_envs=24, num_steps=8, hidden_size=32, num_epochs=2,
+                           num_minibatches=3)
+    params = bppo.orthogonal_init(cfg, seed=8)
+    K, n_opp, P = 2, 20, 2
+    pool = np.stack([bppo.orthogonal_init(cfg, seed=40 + k) for k in range(K)])
+
+    def seats(seed, n):
+        rng = np.random.default_rng(seed)
+        lp = rng.integers(0, P, n).astype(np.int32)
+        po = np.full((n, P), -1, np.int32)
+        for e in range(n):
+            po[e, 1 - lp[e]] = rng.integers(0, K)
+        return n, lp, po.reshape(-1), rng.integers(0, K, P - 1).astype(np.int32)
+
+    ranks = [O.Trainer(oracle_train_cfg(cfg, rank=r, world=2), params) for r in range(2)]
+    for r, t in enumerate(ranks):
+        t.set_opponents(pool, [None] * K, *seats(r, n_opp - 8 * r))
+        t.collect(); t.gae()
+    rows = [int((t.buffer("valid") > 0.5).sum()) for t in ranks]
+    assert rows[0] != rows[1]
+    O.Trainer.update_ranks(ranks)
+    assert np.array_equal(ranks[0].params().view(np.uint32), ranks[1].params().view(np.uint32))
+    # identical shards and seats at W = 2 = the single-rank update
+    solo = O.Trainer(oracle_train_cfg(cfg), params)
+    pair = [O.Trainer(oracle_train_cfg(cfg), params) for _ in range(2)]
+    for t in [solo] + pair:
+        t.set_opponents(pool, [None] * K, *seats(5, n_opp))
+        t.collect(); t.gae()
+    solo.update()
+    O.Trainer.update_ranks(pair)
+    for t in pair:
+        assert np.array_equal(t.params().view(np.uint32), solo.params().view(np.uint32))
+    for t in ranks + pair + [solo]:
+        t.close()
