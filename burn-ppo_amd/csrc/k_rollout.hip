@@ -595,11 +595,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
     // at the loop header, the wait-count pass waited on every step's fresh loads (the Gumbel
     // pair, the reset entry) at layer 1's first use of the W0 registers
     __builtin_amdgcn_s_waitcnt(0);
-#ifndef BPPO_NO_PRIO
-    // wave priority 3 for the step loop: the side-stream Fisher-Yates waves that share these
-    // SIMDs (the rollout keeps one wave per SIMD) take the leftover issue slots
-    __builtin_amdgcn_s_setprio(3);
-#endif
 #pragma unroll 1
     for (int t = 0; t < a.T; t++) {
         const size_t row = (size_t)t * N + e;

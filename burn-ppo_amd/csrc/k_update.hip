@@ -871,6 +871,10 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
     Wave &B = reinterpret_cast<Wave *>(smem + sizeof(Params) / 4)[wv];
     load_params_split(S, g.params);
     __syncthreads();
+#ifdef BPPO_MB_STAMPS
+    unsigned long long st_acc[MB_NSEG] = {}, st_prev;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_prev)::"memory");
+#endif
 
     const int c = lane & 31, h = lane >> 5;
     const int gwave = blockIdx.x * WAVES + wv, nwaves = gridDim.x * WAVES;
@@ -918,6 +922,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
             for (int d = 0; d < 5; d++) B.X[c * 5 + d] = cur.x(d);
         }
         wave_sync();
+        MB_STAMP(0);   // gather: row loads issued, this tile's X staged
         // ---- layer 1, transposed: H1^T[j1][row c] (j1 = cd_row(q, h) + 32 it)
         float xs[3];
 #pragma unroll
@@ -954,6 +959,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
             }
         }
         __builtin_amdgcn_s_setprio(0);
+        MB_STAMP(1);   // layers 1 and 2
         // H2 = relu(. + b1) -> the row-major tile for the heads
 #pragma unroll
         for (int ct = 0; ct < 2; ct++)
@@ -963,6 +969,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
                 B.T[cd_row(q, h) * WS + c + 32 * ct] = v > 0.0f ? v : 0.0f;
             }
         wave_sync();
+        MB_STAMP(2);   // H2 epilogue
         // ---- heads: lane = row c, lane half h over units [32 h, 32 h + 32), 2 chains each
         float l0, l1, vv;
         {
@@ -982,6 +989,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
             t0 += __shfl_xor(t0, 32, 64); t1 += __shfl_xor(t1, 32, 64); t2 += __shfl_xor(t2, 32, 64);
             l0 = t0; l1 = t1; vv = t2;
         }
+        MB_STAMP(3);   // heads
         // ---- loss (as k_minibatch_mfma), dl per row
         {
             const float lg0 = __fadd_rn(l0, S.bp[0]), lg1 = __fadd_rn(l1, S.bp[1]), v = __fadd_rn(vv, S.bv[0]);
@@ -1041,6 +1049,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
           }
         }
         wave_sync();
+        MB_STAMP(4);   // loss
         // ---- head weight gradients (lane = hidden unit), dZ2 before the mask on the f32 MFMA
 #pragma unroll 4
         for (int q = 0; q < 16; q++) {
@@ -1080,6 +1089,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
             }
             if ((q & 3) == 3) __builtin_amdgcn_sched_barrier(0);
         }
+        MB_STAMP(5);   // head gradients, dZ2
         __builtin_amdgcn_s_setprio(3);
         // ---- layer 1 again, C/D orientation: H1[row][j1] (rows in registers)
         f32x16_t h1[2];
@@ -1103,6 +1113,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
                 m1 |= on ? (1u << (q + 16 * jt)) : 0u;
                 h1[jt][q] = on ? h1[jt][q] : 0.0f;
             }
+        MB_STAMP(6);   // layer 1 again, relu mask
         // ---- dW1 += H1^T dZ2: both operands straight from the C/D registers (k = rows)
 #pragma unroll
         for (int s2 = 0; s2 < 2; s2++) {
@@ -1126,6 +1137,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
             }
         }
         wave_sync();
+        MB_STAMP(7);   // dW1
         // ---- dZ1 = dZ2 W1^T: A = dZ2 rows (natural k = j2) from the tile, B = W1 pieces
         f32x16_t dz1[2];
 #pragma unroll
@@ -1144,6 +1156,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
             __builtin_amdgcn_sched_barrier(0);
         }
         __builtin_amdgcn_s_setprio(0);
+        MB_STAMP(8);   // dZ1
         // dZ1 masked by relu'(H1); dW0 and db0 on the VALU (lane = hidden unit)
 #pragma unroll
         for (int q = 0; q < 16; q++) {
@@ -1161,6 +1174,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
             if ((q & 3) == 3) __builtin_amdgcn_sched_barrier(0);
         }
         wave_sync();
+        MB_STAMP(9);   // dW0
     }
     // ---- this wave's partial gradient row (as k_minibatch_mfma)
 #pragma unroll
@@ -1217,6 +1231,11 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
         }
         g.slab[(size_t)blockIdx.x * W_ + p] = a2;
     }
+#ifdef BPPO_MB_STAMPS
+    MB_STAMP(10);  // the block's gradient row
+    if (lane == 0)
+        for (int k = 0; k < MB_NSEG; k++) g.stamps[(size_t)gwave * MB_NSEG + k] = st_acc[k];
+#endif
 }
 
 // fixed-order reduction of the wave partials, grad[p] = sum_w slab[w][p]: SLAB_GROUPS
@@ -1231,9 +1250,6 @@ __global__ void __launch_bounds__(SLAB1_COLS * SLAB_GROUPS) k_slab_reduce1(const
                                                                            int width, float *__restrict__ grad,
                                                                            float *__restrict__ vemax_local) {
     __shared__ double part[SLAB_GROUPS][SLAB1_COLS];
-#ifndef BPPO_NO_PRIO
-    __builtin_amdgcn_s_setprio(3);      // ahead of the side-stream Fisher-Yates waves beside it
-#endif
     const int c = threadIdx.x % SLAB1_COLS, g = threadIdx.x / SLAB1_COLS;
     const int p = blockIdx.x * SLAB1_COLS + c;
     const bool live = p < width, is_max = p == width - NUM_M + M_VEMAX;
@@ -1653,7 +1669,9 @@ bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_
             hipLaunchKernelGGL(k_minibatch_split, dim3(blocks), dim3(64 * mmf::WAVES), lds_split, c->stream, g);
         if (ei >= 0) BPPO_HIP(c, hipEventRecord(c->mb_ev[ei][1], c->stream));
 #ifdef BPPO_MB_STAMPS
-        {   // mean per-wave cycles per segment, accumulated over launches; printed every 16
+        if (!use_exact || getenv("BPPO_MB_STAMPS_EXACT")) {
+            // mean per-wave cycles per segment of the split launches (the exact kernel's with
+            // BPPO_MB_STAMPS_EXACT), accumulated over launches; printed every 16
             static double acc_s[MB_NSEG] = {};
             static int nl = 0;
             std::vector<unsigned long long> h((size_t)blocks * mmb::WAVES * MB_NSEG);
