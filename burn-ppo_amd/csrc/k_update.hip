@@ -314,32 +314,45 @@ __global__ void __launch_bounds__(256, 1) k_minibatch(MbArgs g) {
 // one minibatch row (ppo.rs:1833-1857 gather), loaded branch-free: an absent
 // row (idx = ~0) reads row 0 and is zeroed by selects, so the record stays in
 // registers (a branchy per-member fill lands it in scratch)
+// a row as loaded one tile ahead: the raw values and whether the row exists.  The loads
+// are unconditional (a missing row reads row 0) and the zeroing of a missing row waits
+// for the consumer (row_used): selects right after the loads made the wave wait for the
+// gather at once (s_waitcnt vmcnt(0) behind the prefetch), exposing its latency every tile
 struct RowData {
     float x0, x1, x2, x3, x4;
     int a;
     float olp, A, R, ov;
+    bool ok;
     __device__ __forceinline__ float x(int d) const { return d == 0 ? x0 : d == 1 ? x1 : d == 2 ? x2 : d == 3 ? x3 : x4; }
 };
 __device__ __forceinline__ RowData load_row(const MbArgs &g, uint32_t idx) {
     const bool ok = idx != 0xFFFFFFFFu;
     const size_t i = ok ? idx : 0;
     RowData d;
+    d.ok = ok;
     if (g.rowA) {                     // one 32-byte sector [obs 0..3][obs 4, action, log-prob, value] + [adv, ret]
         const float4 a = g.rowA[i * 2], b = g.rowA[i * 2 + 1];
         const float2 c = g.rowB[i];
-        d.x0 = ok ? a.x : 0.0f; d.x1 = ok ? a.y : 0.0f; d.x2 = ok ? a.z : 0.0f; d.x3 = ok ? a.w : 0.0f;
-        d.x4 = ok ? b.x : 0.0f;
-        d.a = ok ? __float_as_int(b.y) : 0;
-        d.olp = ok ? b.z : 0.0f; d.A = ok ? c.x : 0.0f; d.R = ok ? c.y : 0.0f;
-        d.ov = (ok && g.clip_value) ? b.w : 0.0f;
+        d.x0 = a.x; d.x1 = a.y; d.x2 = a.z; d.x3 = a.w;
+        d.x4 = b.x; d.a = __float_as_int(b.y); d.olp = b.z; d.ov = b.w;
+        d.A = c.x; d.R = c.y;
         return d;
     }
     const float *o = g.obs + i * 5;
-    d.x0 = ok ? o[0] : 0.0f; d.x1 = ok ? o[1] : 0.0f; d.x2 = ok ? o[2] : 0.0f;
-    d.x3 = ok ? o[3] : 0.0f; d.x4 = ok ? o[4] : 0.0f;
-    d.a = ok ? g.act[i] : 0;
-    d.olp = ok ? g.logp[i] : 0.0f; d.A = ok ? g.adv[i] : 0.0f; d.R = ok ? g.ret[i] : 0.0f;
-    d.ov = (ok && g.clip_value) ? g.val[i] : 0.0f;
+    d.x0 = o[0]; d.x1 = o[1]; d.x2 = o[2]; d.x3 = o[3]; d.x4 = o[4];
+    d.a = g.act[i]; d.olp = g.logp[i]; d.A = g.adv[i]; d.R = g.ret[i];
+    d.ov = g.clip_value ? g.val[i] : 0.0f;
+    return d;
+}
+// the row as the kernel uses it: a missing row all zeros, the old value only with clip_value
+__device__ __forceinline__ RowData row_used(const RowData &r, int clip_value) {
+    RowData d;
+    d.ok = r.ok;
+    d.x0 = r.ok ? r.x0 : 0.0f; d.x1 = r.ok ? r.x1 : 0.0f; d.x2 = r.ok ? r.x2 : 0.0f;
+    d.x3 = r.ok ? r.x3 : 0.0f; d.x4 = r.ok ? r.x4 : 0.0f;
+    d.a = r.ok ? r.a : 0;
+    d.olp = r.ok ? r.olp : 0.0f; d.A = r.ok ? r.A : 0.0f; d.R = r.ok ? r.R : 0.0f;
+    d.ov = (r.ok && clip_value) ? r.ov : 0.0f;
     return d;
 }
 
@@ -429,7 +442,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
     for (uint32_t base = (uint32_t)gwave * TR; base < g.n; base += stride) {
         const uint32_t r = base + c;
         const bool valid = h == 0 && r < g.n;
-        const RowData cur = nxt;
+        const RowData cur = row_used(nxt, g.clip_value);
         // re-derive the lane coordinates from an opaque copy each iteration: every
         // LDS address below is then one base VGPR + an immediate offset, instead
         // of ~100 loop-invariant addresses hoisted out of the loop (and spilled)
@@ -819,6 +832,14 @@ __device__ __forceinline__ Split8 split8(const float (&x)[8]) {
     s.p[0] = p0.v; s.p[1] = p1.v; s.p[2] = p2.v;
     return s;
 }
+// relu as a signed-integer max of the bits (a negative float is a negative int; -0 -> +0):
+// one v_max_i32, where `v > 0 ? v : 0` is a v_max_f32 behind a canonicalising v_max_f32
+// (IEEE mode).  Differs only for a NaN with a clear sign bit, which it passes on
+// (split launches 0.481 -> 0.462 ms mean in the bench, profiles/r05d/r05z_ab_*.log)
+__device__ __forceinline__ float relu_bits(float v) {
+    const int b = __float_as_int(v);
+    return __int_as_float(b > 0 ? b : 0);
+}
 __device__ __forceinline__ void mfma6(f32x16_t &acc, const Split8 &a, const Split8 &b) {
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[2], b.p[0], acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[1], b.p[1], acc, 0, 0, 0);
@@ -908,7 +929,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
     for (uint32_t base = (uint32_t)gwave * TR; base < g.n; base += stride) {
         const uint32_t r = base + c;
         const bool valid = h == 0 && r < g.n;
-        const RowData cur = nxt;
+        const RowData cur = row_used(nxt, g.clip_value);
         int ln_ = lane;
         asm volatile("" : "+v"(ln_));
         const int c = ln_ & 31, h = ln_ >> 5;
@@ -950,7 +971,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
             for (int s2 = 0; s2 < 2; s2++) {
                 float v8[8];
 #pragma unroll
-                for (int j = 0; j < 8; j++) { const float v = a1[8 * s2 + j]; v8[j] = v > 0.0f ? v : 0.0f; }
+                for (int j = 0; j < 8; j++) v8[j] = relu_bits(a1[8 * s2 + j]);
                 const Split8 Af = split8(v8);
 #pragma unroll
                 for (int ct = 0; ct < 2; ct++)
@@ -966,7 +987,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
 #pragma unroll
             for (int q = 0; q < 16; q++) {
                 const float v = h2[ct][q] + S.b1[c + 32 * ct];
-                B.T[cd_row(q, h) * WS + c + 32 * ct] = v > 0.0f ? v : 0.0f;
+                B.T[cd_row(q, h) * WS + c + 32 * ct] = relu_bits(v);
             }
         wave_sync();
         MB_STAMP(2);   // H2 epilogue
@@ -1109,9 +1130,9 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
         for (int jt = 0; jt < 2; jt++)
 #pragma unroll
             for (int q = 0; q < 16; q++) {
-                const bool on = h1[jt][q] > 0.0f;
-                m1 |= on ? (1u << (q + 16 * jt)) : 0u;
-                h1[jt][q] = on ? h1[jt][q] : 0.0f;
+                h1[jt][q] = relu_bits(h1[jt][q]);
+                const uint32_t hb = __float_as_uint(h1[jt][q]);
+                m1 |= (hb < 1u ? hb : 1u) << (q + 16 * jt);
             }
         MB_STAMP(6);   // layer 1 again, relu mask
         // ---- dW1 += H1^T dZ2: both operands straight from the C/D registers (k = rows)
@@ -1166,7 +1187,9 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
             for (int d = 0; d < 5; d++) xr[d] = B.X[row * 5 + d];
 #pragma unroll
             for (int jt = 0; jt < 2; jt++) {
-                const float dzv = (m1 >> (q + 16 * jt)) & 1u ? dz1[jt][q] : 0.0f;
+                // bit q + 16 jt of m1 sign-extended to a 0 / all-ones mask
+                const int mk = (int)(m1 << (31 - (q + 16 * jt))) >> 31;
+                const float dzv = __int_as_float(__float_as_int(dz1[jt][q]) & mk);
                 gb0[jt] += dzv;
 #pragma unroll
                 for (int d = 0; d < 5; d++) gW0[d][jt] = __builtin_fmaf(xr[d], dzv, gW0[d][jt]);

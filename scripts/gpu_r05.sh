@@ -115,4 +115,9 @@ if [ "$PART" = rostamp ]; then
   done
   exit 0
 fi
+if [ "$PART" = mbstamp ]; then
+  # split minibatch kernel segment stamps (diagnostic build burn-ppo_amd/bppo/libbppo_stamps.so)
+  timeout -k 10 300 env BPPO_LIB_PATH=$GRAFT_REPO_ROOT/burn-ppo_amd/bppo/libbppo_stamps.so python bench.py --steps 6 --warmup 1 --no-learning --no-cpu-baseline --no-gae-isolated > gpurun_out/${TAG}_mbstamps.log 2>&1
+  rc=$?; echo "mbstamp rc=$rc"; grep mbstamp gpurun_out/${TAG}_mbstamps.log | tail -2; exit $rc
+fi
 echo "unknown part $PART"; exit 2
