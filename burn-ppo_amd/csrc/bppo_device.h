@@ -132,6 +132,26 @@ __device__ __forceinline__ float gumbel_from_word(uint32_t w) {
     return -bppo_math::logf_glibc(-bppo_math::logf_glibc(u));
 }
 
+// the glibc expf / logf tables staged in LDS by a kernel whose lanes each evaluate many of
+// them (the masked sampler's 2 A logf, the wide loss's 3 A expf per row): a lane-varying
+// index into the __constant__ copies is a vector global load per evaluation, each waited
+// on in turn (k_wide_loss<49>: 152 table loads per row)
+struct MathLds {
+    uint64_t exp2tab[32];
+    double linvc[16], llogc[16];
+    __device__ __forceinline__ void load() {     // every thread of the block; then a barrier
+        if (threadIdx.x < 32) exp2tab[threadIdx.x] = bppo_math::kExp2fTab[threadIdx.x];
+        if (threadIdx.x < 16) { linvc[threadIdx.x] = bppo_math::kLogfInvc[threadIdx.x]; llogc[threadIdx.x] = bppo_math::kLogfLogc[threadIdx.x]; }
+        __syncthreads();
+    }
+    __device__ __forceinline__ float expf(float x) const { return bppo_math::expf_glibc_tab(x, exp2tab); }
+    __device__ __forceinline__ float logf(float x) const { return bppo_math::logf_glibc_tab(x, linvc, llogc); }
+    __device__ __forceinline__ float gumbel(uint32_t w) const {
+        float u = __fadd_rn(__fmul_rn(unit_from_word(w), 1.0f), 1e-10f);
+        return -logf(-logf(u));
+    }
+};
+
 // ---------------------------------------------------------------- CartPole --
 struct CartPoleState {
     float x, x_dot, theta, theta_dot;
@@ -182,15 +202,19 @@ __device__ __forceinline__ bool cartpole_step(CartPoleState &s, int action, floa
 // ------------------------------------------------------------------ policy --
 // log_softmax (Burn activation::log_softmax: (x - max) - ln(sum(exp(x - max))))
 // with glibc expf/logf; returns log-prob of `a`, entropy optionally.
-template <int A>
-__device__ __forceinline__ float log_prob_row(const float x[A], int a) {
+struct MathConst {               // the __constant__ tables (kernels without an LDS copy)
+    __device__ __forceinline__ float expf(float x) const { return bppo_math::expf_glibc(x); }
+    __device__ __forceinline__ float logf(float x) const { return bppo_math::logf_glibc(x); }
+};
+template <int A, typename M = MathConst>
+__device__ __forceinline__ float log_prob_row(const float x[A], int a, const M &T = M{}) {
     float m = x[0];
 #pragma unroll
     for (int i = 1; i < A; i++) m = x[i] > m ? x[i] : m;
     float s = 0.0f;
 #pragma unroll
-    for (int i = 0; i < A; i++) s = __fadd_rn(s, bppo_math::expf_glibc(__fsub_rn(x[i], m)));
-    const float lse = bppo_math::logf_glibc(s);
+    for (int i = 0; i < A; i++) s = __fadd_rn(s, T.expf(__fsub_rn(x[i], m)));
+    const float lse = T.logf(s);
     float xa = x[0];
 #pragma unroll
     for (int i = 1; i < A; i++) xa = a == i ? x[i] : xa;

@@ -371,21 +371,29 @@ __global__ void k_rn_returns(int T, int N, double gamma, const float *__restrict
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= N) return;
     double x = returns_state[e];
-    for (int t0 = 0; t0 < T; t0 += RN_TU) {
+    // whole RN_TU blocks without a break inside (a conditional exit let the compiler sink
+    // every load next to its use: one round trip per step), then the tail
+    int t0 = 0;
+    for (; t0 + RN_TU <= T; t0 += RN_TU) {
         float r[RN_TU], d[RN_TU];
 #pragma unroll
         for (int k = 0; k < RN_TU; k++) {
-            const size_t i = (size_t)min(t0 + k, T - 1) * N + e;
+            const size_t i = (size_t)(t0 + k) * N + e;
             r[k] = rew_raw[i];
             d[k] = done[i];
         }
 #pragma unroll
         for (int k = 0; k < RN_TU; k++) {
-            if (t0 + k >= T) break;
             x = x * gamma + (double)r[k];
             X[(size_t)(t0 + k) * N + e] = x;
             if (d[k] != 0.0f) x = 0.0;
         }
+    }
+    for (; t0 < T; t0++) {
+        const size_t i = (size_t)t0 * N + e;
+        x = x * gamma + (double)rew_raw[i];
+        X[i] = x;
+        if (done[i] != 0.0f) x = 0.0;
     }
     returns_state[e] = x;
 }
@@ -401,14 +409,30 @@ __global__ void k_rn_returns_mp(int T, int N, int P, double gamma, const float *
     if (e >= N) return;
     double R0 = returns_state[(size_t)e * P], R1 = P > 1 ? returns_state[(size_t)e * P + 1] : 0.0;
     double R2 = P > 2 ? returns_state[(size_t)e * P + 2] : 0.0, R3 = P > 3 ? returns_state[(size_t)e * P + 3] : 0.0;
-    for (int t = 0; t < T; t++) {
-        const size_t i = (size_t)t * N + e;
-        const int p = players[i];
+    auto step = [&](size_t i, int p, float r, float d, bool ok) {
         double x = p == 0 ? R0 : p == 1 ? R1 : p == 2 ? R2 : R3;
-        x = x * gamma + (double)rew_raw[i];
-        X[i] = (valid && !(valid[i] > 0.5f)) ? __longlong_as_double(0x7ff8000000000000ll) : x;
-        if (done[i] != 0.0f) x = 0.0;
+        x = x * gamma + (double)r;
+        X[i] = ok ? x : __longlong_as_double(0x7ff8000000000000ll);
+        if (d != 0.0f) x = 0.0;
         R0 = p == 0 ? x : R0; R1 = p == 1 ? x : R1; R2 = p == 2 ? x : R2; R3 = p == 3 ? x : R3;
+    };
+    int t0 = 0;
+    for (; t0 + RN_TU <= T; t0 += RN_TU) {       // the loads of RN_TU steps ahead of their chain
+        int pl[RN_TU];
+        float r[RN_TU], d[RN_TU];
+        bool ok[RN_TU];
+#pragma unroll
+        for (int k = 0; k < RN_TU; k++) {
+            const size_t i = (size_t)(t0 + k) * N + e;
+            pl[k] = players[i]; r[k] = rew_raw[i]; d[k] = done[i];
+            ok[k] = !valid || valid[i] > 0.5f;
+        }
+#pragma unroll
+        for (int k = 0; k < RN_TU; k++) step((size_t)(t0 + k) * N + e, pl[k], r[k], d[k], ok[k]);
+    }
+    for (; t0 < T; t0++) {
+        const size_t i = (size_t)t0 * N + e;
+        step(i, players[i], rew_raw[i], done[i], !valid || valid[i] > 0.5f);
     }
     returns_state[(size_t)e * P] = R0;
     if (P > 1) returns_state[(size_t)e * P + 1] = R1;
@@ -444,12 +468,22 @@ __device__ Welford block_exclusive_scan(Welford mine, Welford *sh) {
 // the block's RN_SEG returns staged through LDS with coalesced loads; thread t
 // then walks its RN_IPT consecutive values (one pad double per RN_IPT keeps the
 // per-thread rows on distinct banks)
+// (all RN_IPT loads of a thread issued before the LDS stores: the plain loop waited on
+// each load in turn; the raw rewards of k_rn_apply are staged the same way)
 constexpr int RN_PAD = RN_IPT + 1;
-__device__ __forceinline__ void rn_stage(size_t n, const double *X, double *xs) {
+template <typename V>
+__device__ __forceinline__ void rn_stage(size_t n, const V *X, V *xs) {
     const size_t base = (size_t)blockIdx.x * RN_SEG;
-    for (int k = threadIdx.x; k < RN_SEG; k += RN_BLOCK) {
-        const size_t i = base + k;
-        xs[(k / RN_IPT) * RN_PAD + (k % RN_IPT)] = i < n ? X[i] : 0.0;
+    V v[RN_IPT];
+#pragma unroll
+    for (int j = 0; j < RN_IPT; j++) {
+        const size_t i = base + threadIdx.x + (size_t)j * RN_BLOCK;
+        v[j] = i < n ? X[i] : (V)0;
+    }
+#pragma unroll
+    for (int j = 0; j < RN_IPT; j++) {
+        const int k = threadIdx.x + j * RN_BLOCK;
+        xs[(k / RN_IPT) * RN_PAD + (k % RN_IPT)] = v[j];
     }
     __syncthreads();
 }
@@ -493,6 +527,7 @@ __global__ void __launch_bounds__(RN_BLOCK) k_rn_apply(size_t n, const double *X
     __shared__ Welford sh[RN_BLOCK];
     __shared__ double xs[RN_BLOCK * RN_PAD];
     __shared__ float rs[RN_BLOCK * RN_PAD];
+    rn_stage(n, rew_raw, rs);                     // the raw rewards, replaced in place below
     rn_stage(n, X, xs);
     const size_t base = (size_t)blockIdx.x * RN_SEG + (size_t)threadIdx.x * RN_IPT;
     Welford s{0, 0, 0};
@@ -504,7 +539,7 @@ __global__ void __launch_bounds__(RN_BLOCK) k_rn_apply(size_t n, const double *X
         const size_t i = base + k;
         if (i >= n) break;
         if (!isnan(xs[threadIdx.x * RN_PAD + k])) wpush(run, xs[threadIdx.x * RN_PAD + k]);
-        float r = rew_raw[i];
+        float r = rs[threadIdx.x * RN_PAD + k];
         if (run.n >= 2.0) {                                  // normalization.rs:187-197
             const double sd = sqrt(run.m2 / run.n + 1e-8);
             float z = (float)((double)r / sd);

@@ -134,9 +134,10 @@ __global__ void __launch_bounds__(64) k_wide_observe(int N, const void *state, f
     using E = EnvT<ENV>;
     constexpr int G = PRIV ? E::G : 0;
     constexpr int L = G + E::D;
-    __shared__ float rows[64 * L];
+    __shared__ __attribute__((aligned(16))) float rows[64 * L];
     const int e0 = blockIdx.x * 64, e = e0 + threadIdx.x;
-    for (int i = threadIdx.x; i < 64 * L; i += 64) rows[i] = 0.0f;
+    static_assert((64 * L) % 4 == 0, "observation tile in float4s");
+    for (int i = threadIdx.x; i < 64 * L / 4; i += 64) reinterpret_cast<float4 *>(rows)[i] = make_float4(0, 0, 0, 0);
     __syncthreads();
     if (e < N) {
         const typename E::S s = env_state<ENV>(const_cast<void *>(state))[e];
@@ -149,7 +150,14 @@ __global__ void __launch_bounds__(64) k_wide_observe(int N, const void *state, f
     __syncthreads();
     const int nrows = min(64, N - e0);
     float *dst = xc + (size_t)e0 * L;
-    for (int i = threadIdx.x; i < nrows * L; i += 64) dst[i] = rows[i];
+    // float4 stores when the tile's start is 16-B aligned (e0 L a multiple of 4), then the tail
+    int i0 = 0;
+    if (((size_t)e0 * L) % 4 == 0) {
+        const int n4 = nrows * L / 4;
+        for (int i = threadIdx.x; i < n4; i += 64) reinterpret_cast<float4 *>(dst)[i] = reinterpret_cast<const float4 *>(rows)[i];
+        i0 = 4 * n4;
+    }
+    for (int i = i0 + threadIdx.x; i < nrows * L; i += 64) dst[i] = rows[i];
 }
 
 // VecEnv::step (env.rs:400-487) + the reward bookkeeping of collect_rollouts
@@ -200,8 +208,19 @@ __global__ void k_wide_step(WideStepArgs a) {
 // apply_action_mask + sample_categorical + log_prob_categorical (ppo.rs:337-366):
 // masked logits get -inf; Gumbel u from the main stream at word
 // base + e*A + a (row-major [env][action], one word per draw); first argmax.
+// The A words of a row span at most NB ChaCha blocks; every lane makes exactly NB blocks
+// (the same instructions in every lane) into its own LDS row and reads word a at its row
+// offset.  A WordCursor walk here made a block whenever ANY lane of the wave crossed a
+// block boundary -- with A = 49 every draw index is some lane's boundary, so each wave ran
+// up to 49 divergent blocks per step instead of 4 (110 us per CfgD step)
+constexpr int SAMPLE_THREADS = 64;
 template <int A>
-__global__ void k_sample_masked(SampleArgs g) {
+__global__ void __launch_bounds__(SAMPLE_THREADS) k_sample_masked(SampleArgs g) {
+    constexpr int NB = (15 + A - 1) / 16 + 1;
+    constexpr int WS = 16 * NB + 1;               // odd row stride: the lanes' rows on distinct banks
+    __shared__ uint32_t wbuf[SAMPLE_THREADS * WS];
+    __shared__ MathLds T;
+    T.load();
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= g.N) return;
     float x[A];
@@ -213,14 +232,22 @@ __global__ void k_sample_masked(SampleArgs g) {
         x[a] = ok ? __fadd_rn(g.logits[(size_t)e * A + a], 0.0f) : -INFINITY;
     }
     if (!any) { atomicOr(g.err, 2); return; }   // utils.rs:115-123 "Empty action mask"
-    WordCursor c;
     const uint64_t row = g.gpos ? (uint64_t)g.gpos[e] : (uint64_t)e;   // ppo.rs:737 / :850 batch order
-    c.init(g.key, g.stream, (g.dbase ? *g.dbase : g.base) + row * A);
+    const uint64_t w0 = (g.dbase ? *g.dbase : g.base) + row * A;
+    uint32_t *words = wbuf + threadIdx.x * WS;
+#pragma unroll 1
+    for (int j = 0; j < NB; j++) {
+        uint32_t blk[16];
+        chacha12_block(g.key, (w0 >> 4) + j, g.stream, blk);
+#pragma unroll
+        for (int w = 0; w < 16; w++) words[16 * j + w] = blk[w];
+    }
+    const int off = (int)(w0 & 15);
     int best = 0;
     float bv = 0.0f;
 #pragma unroll
     for (int a = 0; a < A; a++) {
-        const float v = __fadd_rn(x[a], gumbel_from_word(c.next()));
+        const float v = __fadd_rn(x[a], T.gumbel(words[off + a]));
         if (a == 0 || v > bv) { bv = v; best = a; }
     }
     g.act[e] = best;
@@ -229,7 +256,7 @@ __global__ void k_sample_masked(SampleArgs g) {
         g.val[e] = 0.0f;
         return;
     }
-    const float lp = log_prob_row<A>(x, best);
+    const float lp = log_prob_row<A>(x, best, T);
     if (!isfinite(lp)) atomicOr(g.err, 1);       // ppo.rs:363-366
     float v = g.values[e];
     if (g.pa_on) v = (float)((double)v * g.pa_std + g.pa_mean);
@@ -246,13 +273,27 @@ __global__ void k_boot_lvpp(int N, int P, const float *values, const int32_t *pl
     lvpp[(size_t)e * P + players[e]] = values[e];
 }
 
-// minibatch gather (ppo.rs:1833-1857): dst[r][:] = src[perm[start + r]][:]
-__global__ void k_gather_rows(const uint32_t *perm, uint32_t start, uint32_t n, const float *src, int L,
-                              float *dst) {
-    const size_t total = (size_t)n * L;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-        const size_t r = i / L, c = i % L;
-        dst[i] = src[(size_t)perm[start + r] * L + c];
+// minibatch gather (ppo.rs:1833-1857): dst[r][:] = src[perm[start + r]][:].  One wave per
+// row: the row index loaded once, the row's loads (64 consecutive floats per instruction,
+// clamped so none is conditional) all issued before its stores.  The element-per-thread
+// form (a 64-bit division and a dependent perm -> src load pair per element) moved
+// ~2 TB/s: 575 us per CfgD observation gather
+constexpr int GATHER_U = 8;
+__global__ void __launch_bounds__(256) k_gather_rows(const uint32_t *perm, uint32_t start, uint32_t n,
+                                                     const float *src, int L, float *dst) {
+    const int lane = threadIdx.x & 63;
+    const size_t nw = ((size_t)gridDim.x * blockDim.x) >> 6;
+    for (size_t r = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < n; r += nw) {
+        const float *s = src + (size_t)perm[start + r] * L;
+        float *d = dst + r * L;
+        for (int c0 = 0; c0 < L; c0 += 64 * GATHER_U) {
+            float v[GATHER_U];
+#pragma unroll
+            for (int u = 0; u < GATHER_U; u++) v[u] = s[min(c0 + 64 * u + lane, L - 1)];
+#pragma unroll
+            for (int u = 0; u < GATHER_U; u++)
+                if (c0 + 64 * u + lane < L) d[c0 + 64 * u + lane] = v[u];
+        }
     }
 }
 
@@ -274,6 +315,8 @@ __global__ void k_pack_heads(const float *params, int K, int A, size_t wp, size_
 template <int A>
 __global__ void __launch_bounds__(256) k_wide_loss(LossArgs g) {
     __shared__ double red[WM_COUNT][256 / 64];
+    __shared__ MathLds T;
+    T.load();
     double m[WM_COUNT];
 #pragma unroll
     for (int k = 0; k < WM_COUNT; k++) m[k] = 0.0;
@@ -296,19 +339,20 @@ __global__ void __launch_bounds__(256) k_wide_loss(LossArgs g) {
         }
         float s = 0.0f;
 #pragma unroll
-        for (int a = 0; a < A; a++) s = __fadd_rn(s, bppo_math::expf_glibc(__fsub_rn(x[a], mx)));
-        const float lse = bppo_math::logf_glibc(s);
+        for (int a = 0; a < A; a++) s = __fadd_rn(s, T.expf(__fsub_rn(x[a], mx)));
+        const float lse = T.logf(s);
         float H = 0.0f, newlp = 0.0f;
+        float pr[A];                                          // exp(log_softmax), reused below
 #pragma unroll
         for (int a = 0; a < A; a++) {
             x[a] = __fsub_rn(__fsub_rn(x[a], mx), lse);      // log_softmax
-            const float pr = bppo_math::expf_glibc(x[a]);
-            H = __fadd_rn(H, __fmul_rn(pr, x[a]));
+            pr[a] = T.expf(x[a]);
+            H = __fadd_rn(H, __fmul_rn(pr[a], x[a]));
             newlp = a == act ? x[a] : newlp;
         }
         H = -H;
         const float log_ratio = __fsub_rn(newlp, olp);
-        const float ratio = bppo_math::expf_glibc(log_ratio);
+        const float ratio = T.expf(log_ratio);
         const float na = -An;
         const float pl1 = __fmul_rn(na, ratio);
         const float rc = ratio < g.lo ? g.lo : (ratio > g.hi ? g.hi : ratio);
@@ -338,9 +382,9 @@ __global__ void __launch_bounds__(256) k_wide_loss(LossArgs g) {
         float *d = g.dout + (size_t)r * (A + 1);
 #pragma unroll
         for (int a = 0; a < A; a++) {
-            const double pr = (double)bppo_math::expf_glibc(x[a]);
-            double gd = g_lr * ((a == act ? 1.0 : 0.0) - pr);
-            gd += ecd * pr * ((double)x[a] + (double)H);
+            const double p = (double)pr[a];
+            double gd = g_lr * ((a == act ? 1.0 : 0.0) - p);
+            gd += ecd * p * ((double)x[a] + (double)H);
             d[a] = (float)gd;
         }
         d[A] = (float)(g.value_coef_d * 0.5 * g.inv_mb_d * (double)dvl);
@@ -354,7 +398,7 @@ __global__ void __launch_bounds__(256) k_wide_loss(LossArgs g) {
         m[WM_VALID] += nvalid;
         if (nvalid > 1) {
             m[WM_NCHOICE] += 1.0;
-            m[WM_HV] += (double)__fdiv_rn(H, bppo_math::logf_glibc((float)nvalid));
+            m[WM_HV] += (double)__fdiv_rn(H, T.logf((float)nvalid));
         }
     }
     // block reduction: wave shuffles, then waves through LDS, fixed order
@@ -443,7 +487,7 @@ hipError_t wide_env_step(int kind, hipStream_t st, const WideStepArgs &a) {
 }
 
 hipError_t wide_sample(int A, hipStream_t st, const SampleArgs &g) {
-    const dim3 grid((g.N + 127) / 128), block(128);
+    const dim3 grid((g.N + SAMPLE_THREADS - 1) / SAMPLE_THREADS), block(SAMPLE_THREADS);
     if (A == 2) hipLaunchKernelGGL(k_sample_masked<2>, grid, block, 0, st, g);   // CartPole (GEMM path, bppo_debug_sample)
     else if (A == C4_ACT) hipLaunchKernelGGL(k_sample_masked<C4_ACT>, grid, block, 0, st, g);
     else if (A == LD_ACT) hipLaunchKernelGGL(k_sample_masked<LD_ACT>, grid, block, 0, st, g);
@@ -459,8 +503,8 @@ hipError_t wide_boot_lvpp(hipStream_t st, int N, int P, const float *values, con
 
 hipError_t wide_gather(hipStream_t st, const uint32_t *perm, uint32_t start, uint32_t n, const float *src, int L,
                        float *dst) {
-    const size_t total = (size_t)n * L;
-    const unsigned blocks = (unsigned)std::min<size_t>((total + 255) / 256, 8192);
+    if (n == 0 || L <= 0) return hipSuccess;
+    const unsigned blocks = (unsigned)std::min<size_t>(((size_t)n + 3) / 4, 8192);   // 4 rows (waves) per block
     hipLaunchKernelGGL(k_gather_rows, dim3(blocks), dim3(256), 0, st, perm, start, n, src, L, dst);
     return hipGetLastError();
 }
