@@ -45,19 +45,27 @@ struct GemmShape {
 //   KCONTIG: element at base[r * ld + k]  (row-major, k contiguous)
 //   else:    element at base[k * ld + r]  (k-major, r contiguous)
 template <int R, bool KCONTIG>
+// A stage's loads are unconditional (clamped addresses) and an element outside the operand
+// is zeroed when the stage is stored, after the MFMAs that hide the loads: a guarded load
+// (`ok ? base[i] : 0`) was turned into a branch around the load with a wait at its end --
+// every element of the next stage fetched one round trip after the other
 struct TileLoader {
     static constexpr int E = GBK * R / 256;
+    static_assert(E <= 32, "one mask bit per element");
     float v[E];
-    // ones_row >= 0: tile row index r == ones_row (global) reads 1.0 (bias-gradient row)
+    uint32_t ok = 0;
     __device__ __forceinline__ void load(const float *__restrict__ base, int ld, int r0, int rmax, int k0,
                                          int kmax, int tid) {
+        ok = 0;
 #pragma unroll
         for (int e = 0; e < E; e++) {
             int r, k;
             if constexpr (KCONTIG) { k = tid & 31; r = (tid >> 5) + e * 8; }
             else { r = tid % R; k = tid / R + e * (256 / R); }
             const int gr = r0 + r, gk = k0 + k;
-            v[e] = (gr < rmax && gk < kmax) ? base[(size_t)(KCONTIG ? gr : gk) * ld + (KCONTIG ? gk : gr)] : 0.0f;
+            const int cr = min(gr, rmax - 1), ck = min(gk, kmax - 1);
+            v[e] = base[(size_t)(KCONTIG ? cr : ck) * ld + (KCONTIG ? ck : cr)];
+            ok |= (gr < rmax && gk < kmax) ? (1u << e) : 0u;
         }
     }
     __device__ __forceinline__ void store(float *__restrict__ s, int tid) const {
@@ -66,7 +74,8 @@ struct TileLoader {
             int r, k;
             if constexpr (KCONTIG) { k = tid & 31; r = (tid >> 5) + e * 8; }
             else { r = tid % R; k = tid / R + e * (256 / R); }
-            s[k * (R + 1) + r] = v[e];
+            const int m = (int)(ok << (31 - e)) >> 31;                    // bit e -> 0 / all ones
+            s[k * (R + 1) + r] = __int_as_float(__float_as_int(v[e]) & m);
         }
     }
 };
@@ -191,6 +200,31 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs &g, const f32x16 (&
 #pragma unroll
         for (int j = 0; j < TN; j++) {
             const int col = nw + j * 32 + col_l;
+            // DX: the tile's H (and xa) values loaded first from clamped addresses, used
+            // below -- loaded behind the per-element guard they compiled to a branch and a
+            // wait per element (64 round trips per wave for a 64 x 64 wave tile)
+            // (the empty asm statements keep the loads here: without them the compiler sinks
+            // each one into its element's guarded store again)
+            float hvs[16], xas[16], xwc = 0.0f;
+            if constexpr (MODE == GEMM_DX) {
+                const int cc = min(col, g.N - 1);
+                if (g.H) {
+#pragma unroll
+                    for (int q = 0; q < 16; q++)
+                        hvs[q] = g.H[(size_t)min(mw + i * 32 + (q & 3) + 8 * (q >> 2) + rq, g.M - 1) * g.ldh + cc];
+#pragma unroll
+                    for (int q = 0; q < 16; q++) asm volatile("" : "+v"(hvs[q]));
+                }
+                if (g.xa) {
+#pragma unroll
+                    for (int q = 0; q < 16; q++)
+                        xas[q] = g.xa[(size_t)min(mw + i * 32 + (q & 3) + 8 * (q >> 2) + rq, g.M - 1) * g.ldxa];
+                    xwc = g.xw[cc];
+#pragma unroll
+                    for (int q = 0; q < 16; q++) asm volatile("" : "+v"(xas[q]));
+                    asm volatile("" : "+v"(xwc));
+                }
+            }
 #pragma unroll
             for (int q = 0; q < 16; q++) {
                 const int row = mw + i * 32 + (q & 3) + 8 * (q >> 2) + rq;
@@ -202,9 +236,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs &g, const f32x16 (&
                     if (col < g.n0) g.out0[(size_t)row * g.ld0 + col] = v;
                     else g.out1[(size_t)row * g.ld1 + (col - g.n0)] = v;
                 } else if constexpr (MODE == GEMM_DX) {
-                    if (g.xa) v = __fadd_rn(v, __fmul_rn(g.xa[(size_t)row * g.ldxa], g.xw[col]));
+                    if (g.xa) v = __fadd_rn(v, __fmul_rn(xas[q], xwc));
                     if (g.H) {
-                        const float hv = g.H[(size_t)row * g.ldh + col];
+                        const float hv = hvs[q];
                         if (g.dact == 2) v = __fmul_rn(v, __fsub_rn(1.0f, __fmul_rn(hv, hv)));
                         else if (!(hv > 0.0f)) v = 0.0f;
                     }
@@ -415,6 +449,7 @@ __device__ __forceinline__ void load4(const float *__restrict__ base, size_t row
         for (int u = 0; u < 4; u++) v[u] = (row_ok && idx + u < lim) ? base[row_off + idx + u] : 0.0f;
     }
 }
+
 
 // one operand's GBK x R stage.  KCONTIG (element (r, k) at base[r ld + k]): thread -> rows
 // (tid >> 3) + 32 e, k quad (tid & 7) * 4.  k-major (element at base[k ld + r]): thread ->

@@ -439,6 +439,10 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
     RowData nxt;
     uint32_t idx_next = idx_of((uint32_t)gwave * TR + stride);
     nxt = load_row(g, idx_of((uint32_t)gwave * TR));
+    // the first tile's loads drained before the loop: loads still pending at the loop
+    // header made the wait-count pass wait on EVERY tile's prefetch right after issuing it
+    // (its counts for the prologue's registers applied to the loop's in-order counter)
+    __builtin_amdgcn_s_waitcnt(0);
     for (uint32_t base = (uint32_t)gwave * TR; base < g.n; base += stride) {
         const uint32_t r = base + c;
         const bool valid = h == 0 && r < g.n;
@@ -926,6 +930,10 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
     RowData nxt;
     uint32_t idx_next = idx_of((uint32_t)gwave * TR + stride);
     nxt = load_row(g, idx_of((uint32_t)gwave * TR));
+    // the first tile's loads drained before the loop: loads still pending at the loop
+    // header made the wait-count pass wait on EVERY tile's prefetch right after issuing it
+    // (its counts for the prologue's registers applied to the loop's in-order counter)
+    __builtin_amdgcn_s_waitcnt(0);
     for (uint32_t base = (uint32_t)gwave * TR; base < g.n; base += stride) {
         const uint32_t r = base + c;
         const bool valid = h == 0 && r < g.n;

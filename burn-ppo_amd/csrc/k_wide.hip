@@ -224,12 +224,17 @@ __global__ void __launch_bounds__(SAMPLE_THREADS) k_sample_masked(SampleArgs g) 
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= g.N) return;
     float x[A];
+    uint8_t mk[A];
     bool any = false;
 #pragma unroll
+    for (int a = 0; a < A; a++) { mk[a] = g.mask[(size_t)e * A + a]; x[a] = g.logits[(size_t)e * A + a]; }
+    // (all loads above, the masking after: `ok ? logits[i] : -inf` became a branch around
+    // each load with a wait at its end -- 2 A round trips per row)
+#pragma unroll
     for (int a = 0; a < A; a++) {
-        const bool ok = g.mask[(size_t)e * A + a] != 0;
+        const bool ok = mk[a] != 0;
         any |= ok;
-        x[a] = ok ? __fadd_rn(g.logits[(size_t)e * A + a], 0.0f) : -INFINITY;
+        x[a] = ok ? __fadd_rn(x[a], 0.0f) : -INFINITY;
     }
     if (!any) { atomicOr(g.err, 2); return; }   // utils.rs:115-123 "Empty action mask"
     const uint64_t row = g.gpos ? (uint64_t)g.gpos[e] : (uint64_t)e;   // ppo.rs:737 / :850 batch order
