@@ -416,17 +416,20 @@ __global__ void k_rn_returns_mp(int T, int N, int P, double gamma, const float *
         if (d != 0.0f) x = 0.0;
         R0 = p == 0 ? x : R0; R1 = p == 1 ? x : R1; R2 = p == 2 ? x : R2; R3 = p == 3 ? x : R3;
     };
+    const bool has_valid = valid != nullptr;
+    const float *vsrc = has_valid ? valid : done;  // read unconditionally (a guarded load was a branch + wait)
     int t0 = 0;
     for (; t0 + RN_TU <= T; t0 += RN_TU) {       // the loads of RN_TU steps ahead of their chain
         int pl[RN_TU];
-        float r[RN_TU], d[RN_TU];
-        bool ok[RN_TU];
+        float r[RN_TU], d[RN_TU], vv[RN_TU];
 #pragma unroll
         for (int k = 0; k < RN_TU; k++) {
             const size_t i = (size_t)(t0 + k) * N + e;
-            pl[k] = players[i]; r[k] = rew_raw[i]; d[k] = done[i];
-            ok[k] = !valid || valid[i] > 0.5f;
+            pl[k] = players[i]; r[k] = rew_raw[i]; d[k] = done[i]; vv[k] = vsrc[i];
         }
+        bool ok[RN_TU];
+#pragma unroll
+        for (int k = 0; k < RN_TU; k++) ok[k] = !has_valid || vv[k] > 0.5f;
 #pragma unroll
         for (int k = 0; k < RN_TU; k++) step((size_t)(t0 + k) * N + e, pl[k], r[k], d[k], ok[k]);
     }

@@ -209,6 +209,7 @@ __device__ __forceinline__ void fyb_load_tab(const FyTab &t, uint32_t *sx, uint3
 
 // pass 1: per-block range histogram of a contiguous chunk of steps, range-major
 // H[b][blk] so that one exclusive scan gives every (range, block) write offset
+constexpr int FYB_U = 8;
 __global__ void __launch_bounds__(FYB_THREADS) k_fyb_hist(const uint32_t *J, uint32_t n, uint32_t chunk, FyTab t,
                                                           uint32_t *H, uint32_t *flag) {
     extern __shared__ uint32_t fsm[];
@@ -218,7 +219,17 @@ __global__ void __launch_bounds__(FYB_THREADS) k_fyb_hist(const uint32_t *J, uin
     if (blockIdx.x == 0 && threadIdx.x == 0) *flag = 0u;
     __syncthreads();
     const uint32_t i0 = blockIdx.x * chunk, i1 = min(n, i0 + chunk);
-    for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) atomicAdd(&hist[fyb_range(J[i], sx, scb)], 1u);
+    // FYB_U targets loaded before their counts (the plain loop waited on each load in turn;
+    // the counts do not depend on the order)
+    uint32_t i = i0 + threadIdx.x;
+    for (; i + (FYB_U - 1) * blockDim.x < i1; i += FYB_U * blockDim.x) {
+        uint32_t jv[FYB_U];
+#pragma unroll
+        for (int u = 0; u < FYB_U; u++) jv[u] = J[i + u * blockDim.x];
+#pragma unroll
+        for (int u = 0; u < FYB_U; u++) atomicAdd(&hist[fyb_range(jv[u], sx, scb)], 1u);
+    }
+    for (; i < i1; i += blockDim.x) atomicAdd(&hist[fyb_range(J[i], sx, scb)], 1u);
     __syncthreads();
     for (int k = threadIdx.x; k < t.nb; k += blockDim.x) H[(size_t)k * gridDim.x + blockIdx.x] = hist[k];
 }
@@ -233,7 +244,16 @@ __global__ void __launch_bounds__(FYB_THREADS) k_fyb_scatter(const uint32_t *J, 
     for (int k = threadIdx.x; k < t.nb; k += blockDim.x) pos[k] = H[(size_t)k * gridDim.x + blockIdx.x];
     __syncthreads();
     const uint32_t i0 = blockIdx.x * chunk, i1 = min(n, i0 + chunk);
-    for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    uint32_t i = i0 + threadIdx.x;                // (the slot order inside a range is free: see above)
+    for (; i + (FYB_U - 1) * blockDim.x < i1; i += FYB_U * blockDim.x) {
+        uint32_t jv[FYB_U];
+#pragma unroll
+        for (int u = 0; u < FYB_U; u++) jv[u] = J[i + u * blockDim.x];
+#pragma unroll
+        for (int u = 0; u < FYB_U; u++)
+            P[atomicAdd(&pos[fyb_range(jv[u], sx, scb)], 1u)] = make_uint2(i + u * blockDim.x, jv[u]);
+    }
+    for (; i < i1; i += blockDim.x) {
         const uint32_t j = J[i];
         P[atomicAdd(&pos[fyb_range(j, sx, scb)], 1u)] = make_uint2(i, j);
     }
