@@ -274,7 +274,8 @@ bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, double ent_
     float *G = c->d_grad;
     // the split-bf16 contraction (k_gemm_split) for the MLP GEMMs of every minibatch after the
     // update's first (mode 0) or of all of them (bppo_set_minibatch_kernel 2); the first keeps
-    // the exact chains (ratio exactly 1) -- as the CfgB update's k_minibatch_split.  Mode 0
+    // the exact forward chains (ratio exactly 1) -- as the CfgB update's k_minibatch_split --
+    // and runs its backward split like the others (`bsplit` below).  Mode 0
     // splits only minibatches of WIDE_SPLIT_MIN_ROWS rows or more: below that the GEMMs are
     // launch- and latency-bound (no time to win), while the split forward's last-bit
     // differences -- a ReLU pre-activation that close to zero switches its unit for that row
@@ -284,12 +285,15 @@ bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, double ent_
     static const bool exact_all = getenv("BPPO_MB_EXACT_ALL") != nullptr;
     const bool big = rows >= WIDE_SPLIT_MIN_ROWS;
     const int split = n.n_conv == 0 && (c->mb_kernel == 2 || (c->mb_kernel == 0 && !first && !exact_all && big)) ? 1 : 0;
+    // the backward (input and weight gradients) needs f32 accuracy only -- the ratio is
+    // the forward's -- so the update's first minibatch runs its backward split too
+    const int bsplit = n.n_conv == 0 && (c->mb_kernel == 2 || (c->mb_kernel == 0 && !exact_all && big)) ? 1 : 0;
     // weight-gradient sums: f64 (or row-ordered, mode 1) for the small minibatches; from
     // WIDE_SPLIT_MIN_ROWS rows the f32 split-K chains (the update's first minibatch, and the
     // CNN's) -- the f64 MFMA runs them ~4x slower (CfgC 142 -> 151 ms per update, CfgD 482 ->
     // 517 ms, profiles/r05c/r05t_wide_*.log) and the minibatches after the first run the
     // split-bf16 contraction anyway
-    const int exact = split ? -1 : (big && c->mb_kernel == 0 ? 0 : wide_exact_grad(c));
+    const int exact = bsplit ? -1 : (big && c->mb_kernel == 0 ? 0 : wide_exact_grad(c));
     WHIP(c, wide_gather(c->stream, c->d_perm, start, mb, c->d_xc, L, c->d_xcg));
     WTRY(wide_forward(c, rows, c->d_xcg, L, c->d_logits, c->d_values, split));
     LossArgs g;
@@ -321,7 +325,7 @@ bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, double ent_
             if (l > first) {
                 WHIP(c, gemm_dx(c->stream, rows, n.in[l], n.out[l], dz, n.out[l], P + n.w[l], n.out[l],
                                 c->d_hbuf + c->hoff[l - 1], n.out[l - 1], hact, dz2, n.in[l], nullptr, 0, nullptr,
-                                split));
+                                bsplit));
                 std::swap(dz, dz2);
             }
         }
@@ -346,7 +350,7 @@ bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, double ent_
         // the trunk's input gradient: the policy head's chain over its A outputs, then the value
         // head's product added as its own rounded term (the two heads are two Linear modules)
         WHIP(c, gemm_dx(c->stream, rows, Wa, A, c->d_dout, A + 1, c->d_heads, A + 1, Ha, Wa, hact, dz, Wa,
-                        c->d_dout + A, A + 1, P + n.w[n.value], split));
+                        c->d_dout + A, A + 1, P + n.w[n.value], bsplit));
         if (!n.n_conv) {
             WTRY(hidden_chain(0, la, c->d_xcg + c->G, L));
             return BPPO_OK;
@@ -359,7 +363,7 @@ bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, double ent_
     // CTDE actor
     WTRY(wgrad(Wa, A, Ha, Wa, c->d_dout, A + 1, G + n.w[n.policy], A, A, nullptr, 0, G + n.b[n.policy], nullptr));
     WHIP(c, gemm_dx(c->stream, rows, Wa, A, c->d_dout, A + 1, P + n.w[n.policy], A, Ha, Wa, hact, dz, Wa, nullptr, 0,
-                    nullptr, split));
+                    nullptr, bsplit));
     if (n.n_conv) WTRY(cnn_trunk_backward(0, n.n_conv, la));   // split CNN actor
     else WTRY(hidden_chain(0, la, c->d_xcg + c->G, L));
     // CTDE critic
@@ -369,7 +373,7 @@ bppo_status wide_minibatch(bppo_ctx *c, uint32_t start, uint32_t mb, double ent_
     dz = c->d_dz[0]; dz2 = c->d_dz[1];
     WTRY(wgrad(Wc, 1, Hc, Wc, c->d_dout + A, A + 1, G + n.w[n.value], 1, 1, nullptr, 0, G + n.b[n.value], nullptr));
     WHIP(c, gemm_dx(c->stream, rows, Wc, 1, c->d_dout + A, A + 1, P + n.w[n.value], 1, Hc, Wc, hact, dz, Wc, nullptr,
-                    0, nullptr, split));
+                    0, nullptr, bsplit));
     if (n.n_conv) return cnn_trunk_backward(1, n.critic_fc0, lc);   // split CNN critic
     WTRY(hidden_chain(n.critic_first, lc, c->d_xcg, L));
     return BPPO_OK;
