@@ -2,6 +2,12 @@
 #   bash scripts/gpu_r05.sh probe TAG   HIP last-error probe + the split-kernel parity tests
 #   bash scripts/gpu_r05.sh tests TAG   smoke + the whole GPU suite
 #   bash scripts/gpu_r05.sh t2 TAG      2-CPU shuffle_windows bench variants (the r04u failure)
+#   bash scripts/gpu_r05.sh wide TAG    CfgC / CfgD (and CNN) bench_wide lines (WIDE_VARIANTS="name|args|envs;...")
+#   bash scripts/gpu_r05.sh ab TAG      interleaved CfgB bench A/B (AB_VARIANTS="name|envs;...", AB_REPS)
+#   bash scripts/gpu_r05.sh kt TAG      rocprofv3 kernel trace of the CfgB bench line; widekt: of CfgC / CfgD
+#   bash scripts/gpu_r05.sh mbstamp TAG split minibatch kernel segment stamps (libbppo_stamps.so);
+#                                       rostamp: the 64-lane rollout's (RO_LIBS); cnn, cnnprobe: CNN parity;
+#                                       mfmaprobe, fpprobe: the MFMA / f32 rounding probes
 set -u
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
