@@ -132,25 +132,6 @@ __device__ __forceinline__ float gumbel_from_word(uint32_t w) {
     return -bppo_math::logf_glibc(-bppo_math::logf_glibc(u));
 }
 
-// block-wide copy of n floats into LDS (the parameter prologues), BLOCK_COPY_U loads of a
-// thread in flight before their stores: the plain strided loop waited on every load in
-// turn (19 round trips for the CartPole bootstrap's 4,739 parameters)
-constexpr int BLOCK_COPY_U = 8;
-__device__ __forceinline__ void block_copy(float *__restrict__ dst, const float *__restrict__ src, int n) {
-    const int bd = blockDim.x;
-    int i = threadIdx.x;
-    for (; i + (BLOCK_COPY_U - 1) * bd < n; i += BLOCK_COPY_U * bd) {
-        float v[BLOCK_COPY_U];
-#pragma unroll
-        for (int u = 0; u < BLOCK_COPY_U; u++) v[u] = src[i + u * bd];
-#pragma unroll
-        for (int u = 0; u < BLOCK_COPY_U; u++) asm volatile("" : "+v"(v[u]));
-#pragma unroll
-        for (int u = 0; u < BLOCK_COPY_U; u++) dst[i + u * bd] = v[u];
-    }
-    for (; i < n; i += bd) dst[i] = src[i];
-}
-
 // the glibc expf / logf tables staged in LDS by a kernel whose lanes each evaluate many of
 // them (the masked sampler's 2 A logf, the wide loss's 3 A expf per row): a lane-varying
 // index into the __constant__ copies is a vector global load per evaluation, each waited

@@ -50,23 +50,7 @@ static_assert(LDSB <= 160 * 1024, "minibatch kernel LDS over the gfx950 limit");
 __device__ __forceinline__ void load_params(Params &S, const float *__restrict__ P) {
     constexpr CpOffsets O = cp_offsets<64, 2>();
     for (int i = threadIdx.x; i < 6 * H; i += blockDim.x) S.W0[i] = i < 5 * H ? P[O.w0 + i] : 0.0f;
-    {   // W1: the thread's 8 loads ahead of its stores (4096 / 512 threads)
-        constexpr int U = 8;
-        int i = threadIdx.x;
-        for (; i + (U - 1) * (int)blockDim.x < H * H; i += U * blockDim.x) {
-            float w[U];
-#pragma unroll
-            for (int u = 0; u < U; u++) w[u] = P[O.w1 + i + u * blockDim.x];
-#pragma unroll
-            for (int u = 0; u < U; u++) asm volatile("" : "+v"(w[u]));
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                const int k = i + u * blockDim.x;
-                S.W1[(k / H) * RS + (k % H)] = w[u];
-            }
-        }
-        for (; i < H * H; i += blockDim.x) S.W1[(i / H) * RS + (i % H)] = P[O.w1 + i];
-    }
+    for (int i = threadIdx.x; i < H * H; i += blockDim.x) S.W1[(i / H) * RS + (i % H)] = P[O.w1 + i];
     for (int i = threadIdx.x; i < H; i += blockDim.x) {
         S.b0[i] = P[O.b0 + i]; S.b1[i] = P[O.b1 + i]; S.Wv[i] = P[O.wv + i];
         S.Wp[2 * i] = P[O.wp + 2 * i]; S.Wp[2 * i + 1] = P[O.wp + 2 * i + 1];

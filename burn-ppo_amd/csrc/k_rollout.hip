@@ -143,7 +143,7 @@ template <int H, int NL, int ACT>
 __global__ void __launch_bounds__(256) k_cartpole_rollout(RolloutArgs a) {
     extern __shared__ __attribute__((aligned(16))) float sP[];
     constexpr CpOffsets O = cp_offsets<H, NL>();
-    block_copy(sP, a.params, O.n);
+    for (int i = threadIdx.x; i < O.n; i += blockDim.x) sP[i] = a.params[i];
     __syncthreads();
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= a.N) return;
@@ -831,7 +831,7 @@ __global__ void __launch_bounds__(256) k_cartpole_bootstrap(int N, const float *
                                                             int norm_on, float *last_v) {
     extern __shared__ __attribute__((aligned(16))) float sP[];
     constexpr CpOffsets O = cp_offsets<H, NL>();
-    block_copy(sP, params, O.n);
+    for (int i = threadIdx.x; i < O.n; i += blockDim.x) sP[i] = params[i];
     __syncthreads();
     int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= N) return;
@@ -852,7 +852,7 @@ __global__ void __launch_bounds__(256) k_cartpole_forward_rows(int B, const floa
                                                                float *values) {
     extern __shared__ __attribute__((aligned(16))) float sP[];
     constexpr CpOffsets O = cp_offsets<H, NL>();
-    block_copy(sP, params, O.n);
+    for (int i = threadIdx.x; i < O.n; i += blockDim.x) sP[i] = params[i];
     __syncthreads();
     int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= B) return;

@@ -97,7 +97,7 @@ __global__ void __launch_bounds__(256, 1) k_minibatch(MbArgs g) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float *sPbase = smem;
     WaveStage<H> *stages = reinterpret_cast<WaveStage<H> *>(smem + ((O.n + 3) & ~3));
-    block_copy(sPbase, g.params, O.n);
+    for (int i = threadIdx.x; i < O.n; i += blockDim.x) sPbase[i] = g.params[i];
     __syncthreads();
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     WaveStage<H> &S = stages[wv];
@@ -861,18 +861,9 @@ __device__ __forceinline__ Split8 load_pieces(const __bf16 (*img)[H * WPS], int 
 __device__ __forceinline__ void load_params_split(Params &S, const float *__restrict__ P) {
     constexpr CpOffsets O = cp_offsets<64, 2>();
     for (int i = threadIdx.x; i < 6 * H; i += blockDim.x) S.W0[i] = i < 5 * H ? P[O.w0 + i] : P[O.b0 + i - 5 * H];
-    for (int i0 = 0; i0 < H * H; i0 += 8 * (int)blockDim.x) {
-      float wq[8];                                   // the thread's next 8 W1 values, loaded ahead
-#pragma unroll
-      for (int u = 0; u < 8; u++) wq[u] = P[O.w1 + min(i0 + (int)threadIdx.x + u * (int)blockDim.x, H * H - 1)];
-#pragma unroll
-      for (int u = 0; u < 8; u++) asm volatile("" : "+v"(wq[u]));   // (kept ahead of the guarded uses)
-#pragma unroll
-      for (int u = 0; u < 8; u++) {
-        const int i = i0 + threadIdx.x + u * blockDim.x;
-        if (i >= H * H) continue;
+    for (int i = threadIdx.x; i < H * H; i += blockDim.x) {
         const int j1 = i / H, j2 = i % H;
-        const float w = wq[u];                       // W1 [in = j1][out = j2]
+        const float w = P[O.w1 + i];                 // W1 [in = j1][out = j2]
         const __bf16 a = (__bf16)w;
         const float r = w - (float)a;
         const __bf16 b = (__bf16)r;
@@ -880,7 +871,6 @@ __device__ __forceinline__ void load_params_split(Params &S, const float *__rest
         S.W1n[0][j1 * WPS + j2] = a; S.W1n[1][j1 * WPS + j2] = b; S.W1n[2][j1 * WPS + j2] = c;
         const int t = j2 * WPS + perm_j1(j1);
         S.W1t[0][t] = a; S.W1t[1][t] = b; S.W1t[2][t] = c;
-      }
     }
     for (int i = threadIdx.x; i < H; i += blockDim.x) {
         S.b1[i] = P[O.b1 + i];
