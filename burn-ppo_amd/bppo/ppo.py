@@ -74,6 +74,8 @@ class Context:
         n = {"obs": TN * self.obs_dim, "last_values": self.N, "grad": self.n_params,
              "priv": TN * self.priv_dim, "masks": TN * self.num_actions,
              "all_rewards": TN * self.num_players, "last_v_pp": self.N * self.num_players}.get(name, TN)
+        if shape is not None:
+            n = int(np.prod(shape))
         out = np.zeros(n, dtype)
         self._chk(L.lib().bppo_buffer_get(self.h, name.encode(), out.ctypes.data, out.nbytes))
         return out.reshape(shape) if shape else out

@@ -741,6 +741,9 @@ static bppo_status fy_enqueue_ready(bppo_ctx *c, int slot) {
     if (c->shuf.failed(c->err)) return BPPO_ERR_HIP;
     while (c->fy_done < c->cfg.num_epochs && c->shuf.epoch_ready(slot, c->fy_done)) {
         const int e = c->fy_done;
+        // the engine thread may have recorded a HIP failure (J upload, expansion, event) and
+        // then marked this epoch ready: its J is not to be permuted
+        if (c->shuf.failed(c->err)) return BPPO_ERR_HIP;
         BPPO_HIP(c, hipStreamWaitEvent(c->fy_stream, c->shuf.ev[slot][e], 0));
         if (e > 0) BPPO_HIP(c, hipStreamWaitEvent(c->fy_stream, c->fy_ev[e - 1], 0));   // shared scratch
         BPPO_HIP(c, hipEventRecord(c->ev[TM_SHUFFLE][0], c->fy_stream));
@@ -1041,6 +1044,11 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
     // are read once after the last one (no per-minibatch stream drain)
     const bool deferred = c->cfg.target_kl < 0 && !(c->allreduce && c->world > 1 && !c->allreduce_async);
     int nrow = 0;
+    // the deferred path times the update's last minibatch that runs: sizes do not grow with
+    // the slot index, so it is slot M-1 unless B < M (then rem-1; none when B == 0); lockstep
+    // slots (W > 1) all run
+    const int last_run_mb = (base_mb > 0 || (c->allreduce && c->world > 1)) ? M - 1 : (int)rem - 1;
+    bool fw_recorded = false;
     bool first_mb = true;                 // the update's first minibatch: the rollout's parameters
     size_t rows_done = 0;                 // rows of the KL-stopped epoch's minibatches that ran
     for (int ep = 0; ep < c->cfg.num_epochs && !stop; ep++) {
@@ -1081,7 +1089,7 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
             // the "minibatch" phase time is the last minibatch's (read after the update in the
             // deferred path): only that one is bracketed there -- each timestamp marker on the
             // stream costs a few us of idle compute stream
-            const bool fw_timed = !deferred || (ep == c->cfg.num_epochs - 1 && mb == M - 1);
+            const bool fw_timed = !deferred || (ep == c->cfg.num_epochs - 1 && mb == last_run_mb);
             if (fw_timed) BPPO_HIP(c, hipEventRecord(c->ev[TM_FWDBWD][0], c->stream));
             c->d_mb_cur = c->d_mb_stats + 4 * mb;
             // Adam's bias corrections for this step (burn-optim: per tensor, f32 powers)
@@ -1096,12 +1104,17 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
             if (sz == 0) {                 // lockstep slot without rows on this rank
                 BPPO_HIP(c, hipMemsetAsync(c->d_grad, 0, sizeof(float) * ((size_t)np + 64), c->stream));   // + tail
                 BPPO_HIP(c, hipMemsetAsync(c->d_mb_cur, 0, sizeof(float) * 4, c->stream));
+                // value_error_max of no rows: -inf, as the oracle's (the metric row reads the
+                // rank-local copy; the summed slot GRAD_VEMAX is not read)
+                static const float ninf = -INFINITY;
+                BPPO_HIP(c, hipMemcpyAsync(c->d_grad + np + GRAD_VEMAX_LOCAL, &ninf, sizeof(float),
+                                           hipMemcpyHostToDevice, c->stream));
             } else if (c->wide) {
                 TRY(wide_minibatch(c, (uint32_t)start, (uint32_t)sz, ent_coef, first_mb));
             } else {
                 TRY(launch_minibatch(c, (uint32_t)start, (uint32_t)sz, (float)ent_coef, first_mb));
             }
-            if (fw_timed) BPPO_HIP(c, hipEventRecord(c->ev[TM_FWDBWD][1], c->stream));
+            if (fw_timed) { BPPO_HIP(c, hipEventRecord(c->ev[TM_FWDBWD][1], c->stream)); fw_recorded = true; }
             first_mb = false;
             if (multi) {
                 if (!c->allreduce_async) BPPO_HIP(c, sync_stream(c));
@@ -1190,7 +1203,7 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
     if (deferred && nrow > 0) {
         std::memcpy(rows.data(), c->h_rows, sizeof(float) * rows.size());
         float ms = 0;
-        if (event_ms(c->ev[TM_FWDBWD][0], c->ev[TM_FWDBWD][1], &ms)) fw_ms = ms;
+        if (fw_recorded && event_ms(c->ev[TM_FWDBWD][0], c->ev[TM_FWDBWD][1], &ms)) fw_ms = ms;   // else 0
         if (event_ms(c->ev[TM_SHUFFLE][0], c->ev[TM_SHUFFLE][1], &ms)) sh_ms = ms;
     }
     double ev4[4];

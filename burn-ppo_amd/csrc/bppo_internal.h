@@ -333,7 +333,7 @@ struct bppo_ctx {
     bppo_allreduce_fn allreduce = nullptr;
     void *allreduce_user = nullptr;
     int world = 1;
-    int rank = 0;                     // bppo_set_rank: this context's slot in W > 1 all-gathers
+    int rank = -1;                    // bppo_set_rank: this context's slot in W > 1 all-gathers (unset: -1)
     float *d_pa_gather = nullptr;     // PopArt at W > 1: [world][9] floats (3 doubles, 3 floats each)
     int allreduce_async = 0;          // callback enqueues on the stream (no host sync per minibatch)
     // ---- multi-player ("wide") path: Connect Four / Liar's Dice (wide_api.hip)

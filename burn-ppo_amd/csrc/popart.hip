@@ -21,6 +21,7 @@
 //                        returns of every minibatch run (f64 sums), rescale_mag.
 #include "bppo_internal.h"
 #include <cmath>
+#include <cstring>
 #include <vector>
 
 namespace bppo {
@@ -163,13 +164,19 @@ static double join3(const float *o) { return ((double)o[0] + (double)o[1]) + (do
 // all-gathered through the gradient all-reduce callback (zeros but for the own slot,
 // SUM), then merged into the running statistics rank by rank -- the same arithmetic on
 // every rank, so the value-head rescale keeps the ranks' parameters identical
-static bppo_status popart_gather(bppo_ctx *c, const std::vector<Welford> &part, Welford &a) {
+// (every_rank_has_rows: the self-play path, where each rank's batch holds T x N > 0 returns)
+static bppo_status popart_gather(bppo_ctx *c, const std::vector<Welford> &part, Welford &a, bool every_rank_has_rows) {
     const int W = c->world;
     Welford mine{0.0, 0.0, 0.0};
     for (const Welford &b : part) chan_merge(mine, b);
     std::vector<float> g((size_t)9 * W, 0.0f);
-    if (c->rank < 0 || c->rank >= W) { c->err = "PopArt at W > 1: rank outside [0, world) (bppo_set_rank)"; return BPPO_ERR_ARG; }
+    // the slot must come from bppo_set_rank: a default would put every rank into one slot,
+    // and the SUM would then scale that slot's statistics by W on every rank alike
+    if (c->rank < 0) { c->err = "PopArt at W > 1 needs this context's rank (bppo_set_rank)"; return BPPO_ERR_ARG; }
+    if (c->rank >= W) { c->err = "PopArt at W > 1: rank outside [0, world) (bppo_set_rank)"; return BPPO_ERR_ARG; }
     split3(mine.n, &g[9 * c->rank]); split3(mine.mean, &g[9 * c->rank + 3]); split3(mine.m2, &g[9 * c->rank + 6]);
+    float own[9];
+    std::memcpy(own, &g[9 * c->rank], sizeof own);
     PHIP(c, hipMemcpyAsync(c->d_pa_gather, g.data(), g.size() * 4, hipMemcpyHostToDevice, c->stream));
     if (!c->allreduce_async) PHIP(c, hipStreamSynchronize(c->stream));
     if (c->allreduce(c->d_pa_gather, g.size(), c->allreduce_user) != 0) {
@@ -178,6 +185,17 @@ static bppo_status popart_gather(bppo_ctx *c, const std::vector<Welford> &part, 
     }
     PHIP(c, hipMemcpyAsync(g.data(), c->d_pa_gather, g.size() * 4, hipMemcpyDeviceToHost, c->stream));
     PHIP(c, hipStreamSynchronize(c->stream));
+    // two contexts given one rank: the slot they share holds a sum (checked by each of them),
+    // and on the self-play path some other slot stays empty (seen by every rank alike)
+    if (std::memcmp(own, &g[9 * c->rank], sizeof own) != 0) {
+        c->err = "PopArt at W > 1: another rank wrote this context's slot (duplicated bppo_set_rank)";
+        return BPPO_ERR_ARG;
+    }
+    for (int q = 0; q < W && every_rank_has_rows; q++)
+        if (!(join3(&g[9 * q]) > 0.0)) {
+            c->err = "PopArt at W > 1: a rank's slot is empty (duplicated or missing bppo_set_rank)";
+            return BPPO_ERR_ARG;
+        }
     for (int q = 0; q < W; q++) chan_merge(a, Welford{join3(&g[9 * q]), join3(&g[9 * q + 3]), join3(&g[9 * q + 6])});
     return BPPO_OK;
 }
@@ -197,7 +215,7 @@ bppo_status popart_update_begin(bppo_ctx *c, const float *valid) {
     PHIP(c, hipStreamSynchronize(c->stream));
     const double old_mean = c->pa_mean, old_std = popart_std(c);
     Welford a{c->pa_count, c->pa_mean, c->pa_m2};
-    if (c->world > 1 && c->allreduce) PTRY(popart_gather(c, part, a));
+    if (c->world > 1 && c->allreduce) PTRY(popart_gather(c, part, a, valid == nullptr));
     else
         for (const Welford &b : part) chan_merge(a, b);   // Chan merge in block (= row) order
     c->pa_count = a.n; c->pa_mean = a.mean; c->pa_m2 = a.m2;

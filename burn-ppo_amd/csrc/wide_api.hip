@@ -11,6 +11,7 @@
 // input cat[priv, obs] (ctde.rs:160-183) and the actor input obs are two views
 // of one buffer with row stride L = G + D.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 #include "bppo_internal.h"
@@ -479,6 +480,18 @@ bppo_status wide_buffer_get(bppo_ctx *c, const char *name, void *host, size_t by
         WHIP(c, hipStreamSynchronize(c->stream));
         float *o = (float *)host;
         for (size_t i = 0; i < m.size(); i++) o[i] = m[i] ? 1.0f : 0.0f;
+        return BPPO_OK;
+    }
+    if (!strncmp(name, "hidden:", 7)) {
+        // test hook: hidden layer l's activations of the last forward -- the last minibatch's
+        // rows in gather (perm) order, [rows_max][out[l]] (tests/test_gpu_gemm_split.py reads
+        // the device's ReLU decisions from them)
+        const int l = atoi(name + 7);
+        if (l < 0 || l >= c->net.n_layers || !is_hidden(c->net, l)) { c->err = "buffer_get: not a hidden layer"; return BPPO_ERR_ARG; }
+        const size_t b = (size_t)c->rows_max * c->net.out[l] * 4;
+        if (!need(b)) return BPPO_ERR_ARG;
+        WHIP(c, hipMemcpyAsync(host, c->d_hbuf + c->hoff[l], b, hipMemcpyDeviceToHost, c->stream));
+        WHIP(c, hipStreamSynchronize(c->stream));
         return BPPO_OK;
     }
     struct { const char *n; const void *p; size_t b; } tab[] = {

@@ -234,10 +234,15 @@ typedef int (*bppo_allreduce_fn)(float *device_buf, size_t n, void *user);
  * targets are identical on every rank; needs bppo_set_rank.  Opponent pools at W > 1: each
  * rank trains on its own learner rows, cut into num_minibatches of its own sizes; the
  * minibatch slots run in lockstep (one callback each), a rank without rows in a slot
- * contributing a zero gradient and zero metric partials. */
+ * contributing a zero gradient and zero metric partials (its value_error_max for the slot is
+ * -inf).  The SUM is scaled by 1/W in every slot, empty contributions included, so a slot
+ * that some ranks have no rows for takes a proportionally smaller step (the oracle's
+ * or_trainers_update does the same). */
 bppo_status bppo_set_allreduce(bppo_ctx *ctx, bppo_allreduce_fn fn, void *user, int32_t world_size);
-/* this context's rank among the all-reduce's world_size ranks (0-based; default 0): the
- * slot of its PopArt batch statistics in the W > 1 all-gather */
+/* this context's rank among the all-reduce's world_size ranks (0-based; unset by default):
+ * the slot of its PopArt batch statistics in the W > 1 all-gather.  Required for
+ * normalize_values at W > 1: an update without it returns BPPO_ERR_ARG, and so does one whose
+ * gathered statistics show two contexts in one slot (a duplicated rank) */
 bppo_status bppo_set_rank(bppo_ctx *ctx, int32_t rank);
 
 /* stream-ordered variant: fn is called WITHOUT draining the stream, right after
@@ -319,9 +324,18 @@ bppo_status bppo_set_explained_variance_mode(bppo_ctx *ctx, int32_t mode);
  * for every minibatch; 2 the split kernel for every minibatch, the first included (its
  * gradient from the rollout's parameters can then be compared with the oracle's,
  * tests/test_gpu_split_kernel.py).  The GEMM path (Connect Four, Liar's Dice, Skull, other
- * nets): mode 0 sums the weight gradients in f64 on the f64 MFMA for CNN nets and in f32
- * split-K chains otherwise; 1 in f64 row by row in order, the oracle's arithmetic exactly (a
- * latency-bound parity mode); 2 in f32 split-K chains for every net. */
+ * nets; wide_api.hip wide_minibatch):
+ *   mode 0 (default), minibatches below 32,768 rows (WIDE_SPLIT_MIN_ROWS): the exact forward
+ *     and input-gradient f32 chains, weight gradients summed in f64 on the f64 MFMA;
+ *     from 32,768 rows, MLP / CTDE nets: the update's first minibatch keeps the exact forward
+ *     (ratio exactly 1) and runs its backward (input and weight gradients) on the split-bf16
+ *     contraction, every later minibatch runs all its GEMMs split; CNN nets: the exact
+ *     chains with f32 split-K weight gradients;
+ *   mode 1: the exact chains, weight gradients in f64 row by row in order (the oracle's
+ *     arithmetic exactly; a latency-bound parity mode);
+ *   mode 2: MLP / CTDE nets run every minibatch's forward and backward on the split-bf16
+ *     contraction (the first included); CNN nets the exact chains with f32 split-K weight
+ *     gradients. */
 bppo_status bppo_set_minibatch_kernel(bppo_ctx *ctx, int32_t mode);
 
 /* device timing of the last call of each phase kernel (ms), for bench.py's roofline */

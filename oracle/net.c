@@ -25,6 +25,23 @@
 static int g_mlp_parallel = 1;
 void or_set_mlp_parallel(int on) { g_mlp_parallel = on; }
 
+/* test hook (tests/test_gpu_gemm_split.py): per FC layer index l, an optional u8 [mb][out]
+ * mask that replaces the ReLU decision y > 0 in or_minibatch_loss_grad's backward, so the
+ * gradient can be recomputed with another forward's ReLU decisions (the device's split
+ * forward, whose pre-activations within rounding of 0 may fall on the other side) */
+static const uint8_t *g_relu_masks[32];
+void or_set_relu_masks(const uint8_t *const *masks, int n) {
+    for (int l = 0; l < 32; l++) g_relu_masks[l] = masks && l < n ? masks[l] : NULL;
+}
+/* the post-activation argument of linear_bwd for layer l: y, or the override as 0/1 */
+static const float *relu_y(int l, const float *y, size_t n, float **tmp) {
+    *tmp = NULL;
+    if (l < 0 || l >= 32 || !g_relu_masks[l]) return y;
+    *tmp = malloc(sizeof(float) * n);
+    for (size_t i = 0; i < n; i++) (*tmp)[i] = g_relu_masks[l][i] ? 1.0f : 0.0f;
+    return *tmp;
+}
+
 typedef struct { int in, out; size_t w, b; } layer_t;
 
 /* two trunks: CTDE, or split_networks (the critic on obs alone) */
@@ -571,8 +588,11 @@ void or_minibatch_loss_grad(const or_net_desc *d, const float *p, size_t mb, con
             for (int l = li - 1; l >= l0; l--) {
                 const float *xl = l > l0 ? acts.buf[l - 1] : (d->cnn ? acts.buf[ACT_F] : obs);
                 float *dxl = (l > l0 || d->cnn) ? malloc(sizeof(float) * mb * L[l].in) : NULL;
-                linear_bwd(xl, acts.buf[l], dh, p + L[l].w, mb, L[l].in, L[l].out, d->relu,
+                float *ym = NULL;
+                const float *yl = d->relu ? relu_y(l, acts.buf[l], mb * (size_t)L[l].out, &ym) : acts.buf[l];
+                linear_bwd(xl, yl, dh, p + L[l].w, mb, L[l].in, L[l].out, d->relu,
                            g + L[l].w, g + L[l].b, dxl);
+                free(ym);
                 free(dh);
                 dh = dxl;
             }
@@ -591,8 +611,11 @@ void or_minibatch_loss_grad(const or_net_desc *d, const float *p, size_t mb, con
             for (int l = vi - 1; l >= c0; l--) {
                 const float *xl = l > c0 ? acts.buf[l - 1] : x0;
                 float *dxl = (l > c0 || d->cnn) ? malloc(sizeof(float) * mb * L[l].in) : NULL;
-                linear_bwd(xl, acts.buf[l], dh, p + L[l].w, mb, L[l].in, L[l].out, d->relu,
+                float *ym = NULL;
+                const float *yl = d->relu ? relu_y(l, acts.buf[l], mb * (size_t)L[l].out, &ym) : acts.buf[l];
+                linear_bwd(xl, yl, dh, p + L[l].w, mb, L[l].in, L[l].out, d->relu,
                            g + L[l].w, g + L[l].b, dxl);
+                free(ym);
                 free(dh);
                 dh = dxl;
             }

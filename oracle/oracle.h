@@ -242,6 +242,9 @@ void or_set_mlp_parallel(int on);
 /* one linear layer y = x W + b with the matrixmultiply summation order */
 void or_linear(const float *x, const float *W, const float *b, size_t B, int in, int out,
                int relu, float *y);
+/* test hook: ReLU decisions of FC layer l's backward taken from masks[l] (u8 [mb][out]),
+ * NULL entries / NULL masks = the forward's own (y > 0) */
+void or_set_relu_masks(const uint8_t *const *masks, int n);
 /* the input gradient of one Linear as the backward computes it (test hook) */
 void or_linear_dx(const float *dz, const float *W, size_t B, int in, int out, float *dx);
 

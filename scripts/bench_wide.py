@@ -40,7 +40,10 @@ def main():
     p.add_argument("--opponents", type=int, default=0,
                    help="opponent-pool rollouts (ppo.rs:537-1063) against K loaded models")
     p.add_argument("--minibatch-kernel", type=int, default=None,
-                   help="bppo_set_minibatch_kernel mode (0 default, 1 exact f64 weight gradients, 2 f32)")
+                   help="bppo_set_minibatch_kernel mode: 0 default (below 32768-row minibatches exact chains + "
+                        "f64 weight gradients; from 32768 rows MLP nets split-bf16 GEMMs after the first "
+                        "minibatch's exact forward, CNN nets f32 split-K weight gradients), 1 exact chains + "
+                        "row-ordered f64 weight gradients, 2 split-bf16 for every MLP minibatch (CNN: f32 split-K)")
     p.add_argument("--opponent-frac", type=float, default=0.25,
                    help="opponent_pool_fraction (configs/liars_dice*.toml: 0.25)")
     a = p.parse_args()

@@ -23,6 +23,9 @@ What a fixture holds (data only, no reference source):
     strided sample and the f64 sum of every step row;
   * the 19 UpdateMetrics, num_updates / epochs_run, the exact f64 explained
     variance of the buffers, the sha256 of the last epoch's permutation;
+  * every minibatch's statistics in run order (or_trainer_mb_log, ppo.rs:1923-1988:
+    `mb_log`, columns `mb_fields`), so the device's per-minibatch rows can be held to
+    1e-5 at the benched minibatch sizes (VERDICT r5, next-round item 1);
   * the parameters after the update (all of them for CfgB; a fixed random sample
     plus per-tensor f64 sums of |p - p0| for the larger nets);
   * the sha256 of the initial parameters (bppo.orthogonal_init(cfg, init_seed)), so
@@ -149,6 +152,9 @@ def make(name):
     out["metrics"] = np.array([om[k] for k in METRICS], np.float32)
     out["num_updates"], out["epochs_run"] = om["num_updates"], om["epochs_run"]
     out["rng_update"] = ot.rng_pos()
+    log = ot.minibatch_log()
+    out["mb_fields"] = np.array([f for f, _ in O.MbStats._fields_])
+    out["mb_log"] = np.array([[r[f] for f, _ in O.MbStats._fields_] for r in log], np.float32)
     out["sha_perm"] = sha(last_perm(cfg["seed"], start, N * T, om["epochs_run"]))
     p = ot.params()
     idx = param_sample_idx(p.size)

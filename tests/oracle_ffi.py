@@ -200,6 +200,7 @@ def lib():
             "or_net_num_params": (C.c_size_t, [C.POINTER(NetDesc)]),
             "or_linear": (None, [f32, f32, f32, C.c_size_t, C.c_int, C.c_int, C.c_int, f32]),
             "or_linear_dx": (None, [f32, f32, C.c_size_t, C.c_int, C.c_int, f32]),
+            "or_set_relu_masks": (None, [C.c_void_p, C.c_int]),
             "or_net_forward": (None, [C.POINTER(NetDesc), f32, f32, C.c_void_p, C.c_size_t, f32, f32]),
             "or_sample_categorical": (None, [C.POINTER(Rng), f32, C.c_size_t, C.c_int, i32]),
             "or_log_prob": (C.c_float, [f32, C.c_int, C.c_int32]),

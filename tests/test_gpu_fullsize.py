@@ -66,6 +66,44 @@ def _layer_sizes(cfg):
     return [sz for i, n in shapes for sz in (i * n, n)]
 
 
+def _check_minibatch_rows(rows, fx, mb, pl_mag):
+    """every minibatch of the update (bppo_minibatch_rows) against the oracle's statistics of
+    the same minibatch (or_trainer_mb_log, recorded in the fixture) at 1e-5, at the benched
+    minibatch sizes and with the benched arithmetic: CfgB the exact f32 kernel on the first
+    minibatch and k_minibatch_split after; CfgC / CfgD the exact forward with f32 split-K
+    weight gradients and the split-bf16 backward on the first minibatch, the split-bf16 GEMMs
+    on the rest (>= 32,768 rows).  Each minibatch runs from the device's own parameters after
+    its earlier Adam steps (ppo.rs:1923-1988).  Floors as for the update's metrics: the
+    policy loss's summand magnitude, value/returns means their own magnitude; approx_kl an
+    absolute 2^-24/sqrt(mb) (each row's (ratio-1) - log ratio from a ratio within f32
+    resolution of 1); clip_fraction 4 rows of the minibatch (ratios within rounding of
+    1 +- eps)."""
+    fields = [str(f) for f in fx["mb_fields"]]
+    log = [dict(zip(fields, (float(v) for v in r))) for r in fx["mb_log"]]
+    assert len(rows) == len(log), (len(rows), len(log))
+    worst, bad = [], []
+    for k, (r, o) in enumerate(zip(rows, log)):
+        n = float(r[10])
+        assert n == mb, (k, n, mb)
+        dev = {"policy_loss": r[0] / n, "value_loss": 0.5 * r[1] / n, "entropy": r[2] / n,
+               "approx_kl": r[3] / n, "clip_fraction": r[4] / n, "value_mean": r[5] / n,
+               "returns_mean": r[6] / n, "value_error_mean": r[7] / n, "value_error_max": r[9]}
+        if "sha_masks" in fx.files and o["avg_valid_actions"] > 0:
+            dev["avg_valid_actions"] = r[11] / n
+            dev["entropy_valid_pct"] = r[12] / r[13] if r[13] > 0 else 0.0
+        floor = {"policy_loss": pl_mag, "value_mean": abs(o["value_error_mean"]) + abs(o["returns_mean"]),
+                 "returns_mean": abs(o["value_error_mean"]) + abs(o["returns_mean"])}
+        absf = {"approx_kl": 2.0 ** -24 / np.sqrt(mb), "clip_fraction": 4.0 / mb}
+        rel = {f: abs(float(dev[f]) - o[f]) / max(RTOL * max(abs(o[f]), floor.get(f, 0.0)), absf.get(f, 0.0), 1e-37)
+               for f in dev}
+        f = max(rel, key=rel.get)
+        worst.append((k, f, round(rel[f], 3)))
+        if rel[f] > 1.0:
+            bad.append((k, f, float(dev[f]), o[f]))
+    print(f"\nper-minibatch worst error / bar: {worst}")
+    assert not bad, bad
+
+
 @pytest.mark.parametrize("case", list(CASES))
 def test_bench_path_matches_fullsize_oracle(case):
     fx = np.load(os.path.join(GOLDEN, f"full_{case}.npz"))
@@ -122,6 +160,8 @@ def test_bench_path_matches_fullsize_oracle(case):
             if not abs(d - o) <= tol:
                 bad.append((k, d, o))
         assert not bad, bad
+        if "mb_log" in fx.files:
+            _check_minibatch_rows(ctx.minibatch_rows(), fx, N * T // cfg["num_minibatches"], pl_mag)
         p = tr.model.get_params()
         # parameters after E x M Adam steps: Adam's m/sqrt(v) turns last-bit gradient
         # differences of near-zero entries into differences of up to ~lr per step, so a

@@ -84,9 +84,104 @@ def test_split_weight_grad(Kin, N, rows):
 NETS = [("connect_four", None), ("liars_dice", True)]
 
 
+def _hidden_layers(cfg):
+    """(layer index, its input source, out) of the FC hidden layers, oracle / device layer
+    numbering: MLP hidden 0..h-1 (policy h, value h+1); CTDE actor hidden 0..h-1, policy h,
+    critic hidden h+1..h+c, value (input "obs", "cat" = [priv | obs], or "prev")"""
+    shapes, _ = layer_shapes(cfg)
+    h = cfg["num_hidden"]
+    out = [(l, "obs" if l == 0 else "prev", shapes[l][1]) for l in range(h)]
+    if cfg["network_type"] == "ctde":
+        c = cfg["critic_num_hidden"]
+        out += [(l, "cat" if l == h + 1 else "prev", shapes[l][1]) for l in range(h + 1, h + 1 + c)]
+    return out
+
+
+def _offsets(cfg):
+    shapes, _ = layer_shapes(cfg)
+    off, o = [], 0
+    for i, n in shapes:
+        off.append((o, o + i * n, i, n))
+        o += i * n + n
+    return off
+
+
+def _oracle_pre_activations(cfg, p0, ot):
+    """z = x W + b of every hidden layer as the oracle's forward computes it (or_linear's
+    matrixmultiply chain order, relu on the previous layer), with |x| |W| + |b| in f64"""
+    obs = ot.buffer("obs").reshape(-1, ENV_D[cfg["env"]][0])
+    priv = ot.buffer("priv").reshape(-1, ENV_D[cfg["env"]][1]) if cfg["network_type"] == "ctde" else None
+    offs = _offsets(cfg)
+    z, mag, prev = {}, {}, None
+    for l, src, n in _hidden_layers(cfg):
+        x = obs if src == "obs" else (np.concatenate([priv, obs], 1) if src == "cat" else prev)
+        w0, b0, i, _ = offs[l]
+        W, b = p0[w0:w0 + i * n].reshape(i, n), p0[b0:b0 + n]
+        z[l] = O.linear(x, W, b, -1)
+        mag[l] = np.abs(x.astype(np.float64)) @ np.abs(W.astype(np.float64)) + np.abs(b)
+        prev = np.maximum(z[l], 0.0)
+    return z, mag
+
+
+ENV_D = {"connect_four": (86, 0), "liars_dice": (270, 120)}
+
+
+def _oracle_grad(cfg, env, p0, B, ot, logp, advn, val, ent, relu_masks=None):
+    is_ctde = cfg["network_type"] == "ctde"
+    _, D, A, P, G = {"connect_four": (0, 86, 7, 2, 0), "liars_dice": (0, 270, 49, 4, 120)}[env]
+    if is_ctde:
+        desc = O.ctde_desc(D, G, A, cfg["hidden_size"], cfg["num_hidden"], cfg["critic_hidden_size"],
+                           cfg["critic_num_hidden"], cfg["activation"] == "relu")
+    else:
+        desc = O.mlp_desc(D, A, cfg["hidden_size"], cfg["num_hidden"], cfg["activation"] == "relu")
+    go = np.zeros(desc.n_params, np.float32)
+    ms = O.MbStats()
+    pc = O.ppo_cfg(num_epochs=1, num_minibatches=1, clip=cfg["clip_epsilon"], value_coef=cfg["value_coef"])
+    priv = ot.buffer("priv") if is_ctde else None
+    masks = ot.buffer("masks")
+    keep = None
+    if relu_masks:
+        keep = [np.ascontiguousarray(relu_masks[l], np.uint8) if l in relu_masks else None for l in range(32)]
+        ptrs = (C.c_void_p * 32)(*[None if k is None else k.ctypes.data for k in keep])
+        O.lib().or_set_relu_masks(ptrs, 32)
+    try:
+        O.lib().or_minibatch_loss_grad(C.byref(desc), p0, B, ot.buffer("obs"), None if priv is None else priv.ctypes.data,
+                                       ot.buffer("actions", np.int32), logp, advn, ot.buffer("returns"), val,
+                                       masks.ctypes.data, C.byref(pc), ent, go, C.byref(ms))
+    finally:
+        O.lib().or_set_relu_masks(None, 0)
+    return desc, go, ms
+
+
+def _worst(cfg, g, go):
+    """per Burn record tensor: (offset, size, max |error| / (1e-5 x the tensor's max |entry|),
+    entries past that bar)"""
+    shapes, _ = layer_shapes(cfg)
+    off, worst = 0, []
+    for i, o in shapes:
+        for n in (i * o, o):
+            a, b = g[off:off + n], go[off:off + n]
+            tol = TOL * max(np.abs(b).max(), 1e-30)
+            worst.append((off, n, float(np.abs(a - b).max() / tol), int((np.abs(a - b) > tol).sum())))
+            off += n
+    return worst
+
+
 @pytest.mark.parametrize("env,ctde", NETS)
 @pytest.mark.parametrize("mode", [2, 1, 0])
 def test_wide_gradient_from_identical_parameters(env, ctde, mode):
+    """Mode 1 (exact chains, row-ordered f64 weight gradients) and mode 0 (the default at this
+    minibatch size: exact forward, f32 input-gradient chains, f64 weight gradients) at the
+    strict bar: every gradient entry within 1e-5 of its tensor's largest |entry|.
+
+    Mode 2 runs the split-bf16 forward, whose pre-activations differ from the oracle's chain
+    in the last bits, so a ReLU unit whose pre-activation is within rounding of zero can land
+    on the other side for a row.  The test proves that this is the only difference: it reads
+    the device's ReLU decisions of every hidden layer back (bppo_buffer_get "hidden:<l>",
+    rows in permutation order), checks that each (row, unit) where they differ from the
+    oracle's has |z| within the split forward's error bound (1e-5 of sum |x| |W| + |b|), feeds
+    the device's decisions to the oracle's backward (or_set_relu_masks) and holds the
+    gradient to the same strict 1e-5 bar."""
     N, T = 512, 16
     cfg, tr, ot = _pair(env, N, T, ctde=ctde, num_epochs=1, num_minibatches=1)
     try:
@@ -105,49 +200,44 @@ def test_wide_gradient_from_identical_parameters(env, ctde, mode):
         lr, ent = bppo.schedule_get(cfg["learning_rate"], 0), bppo.schedule_get(cfg["entropy_coef"], 0)
         m = bppo.ppo_update(tr.ctx, lr, ent)
         g = tr.ctx.buffer("grad")
-        is_ctde = cfg["network_type"] == "ctde"
-        _, D, A, P, G = {"connect_four": (0, 86, 7, 2, 0), "liars_dice": (0, 270, 49, 4, 120)}[env]
-        if is_ctde:
-            desc = O.ctde_desc(D, G, A, cfg["hidden_size"], cfg["num_hidden"], cfg["critic_hidden_size"],
-                               cfg["critic_num_hidden"], cfg["activation"] == "relu")
-        else:
-            desc = O.mlp_desc(D, A, cfg["hidden_size"], cfg["num_hidden"], cfg["activation"] == "relu")
         adv = ot.buffer("advantages")
         advn = np.zeros(B, np.float32)
         st = [C.c_float() for _ in range(4)]
         O.lib().or_normalize_advantages(adv, B, advn, *[C.byref(x) for x in st])
-        go = np.zeros(desc.n_params, np.float32)
-        ms = O.MbStats()
-        pc = O.ppo_cfg(num_epochs=1, num_minibatches=1, clip=cfg["clip_epsilon"], value_coef=cfg["value_coef"])
-        priv = ot.buffer("priv") if is_ctde else None
-        masks = ot.buffer("masks")
-        O.lib().or_minibatch_loss_grad(C.byref(desc), p0, B, ot.buffer("obs"), None if priv is None else priv.ctypes.data,
-                                       ot.buffer("actions", np.int32), logp, advn, ot.buffer("returns"), val,
-                                       masks.ctypes.data, C.byref(pc), ent, go, C.byref(ms))
+        desc, go, ms = _oracle_grad(cfg, env, p0, B, ot, logp, advn, val, ent)
+        assert go.size == desc.n_params == g.size
         assert 0.05 < ms.clip_fraction < 0.95
         floors = {"policy_loss": summand_magnitude(adv), "value_loss": 0.0, "entropy": 0.0,
                   "approx_kl": 0.0, "clip_fraction": 1.0 / B}
         for k, fl in floors.items():
             o = getattr(ms, k)
             assert abs(m[k] - o) <= TOL * max(abs(o), fl), (k, m[k], o)
-        shapes, _ = layer_shapes(cfg)
-        off, worst = 0, []
-        for i, o in shapes:
-            for n in (i * o, o):
-                a, b = g[off:off + n], go[off:off + n]
-                tol = TOL * max(np.abs(b).max(), 1e-30)
-                worst.append((off, n, float(np.abs(a - b).max() / tol), int((np.abs(a - b) > tol).sum())))
-                off += n
-        assert off == desc.n_params
-        if mode == 1:   # the exact chains and row-ordered f64 weight gradients
+        worst = _worst(cfg, g, go)
+        if mode in (0, 1):
             assert all(w[2] <= 1.0 for w in worst), (mode, worst)
-        else:
-            # the split forward (mode 2) and the f32 split-K weight gradients (mode 0) differ from
-            # the oracle's in the last bits: a ReLU pre-activation within that distance of zero
-            # switches its unit for one row, which moves that row's contribution in a few
-            # entries.  Every entry within 1e-4 of its tensor's largest |entry| (10x the exact
-            # bar) and at most 0.5 % of all entries past 1e-5 of it
-            assert all(w[2] <= 10.0 for w in worst), (mode, worst)
-            assert sum(w[3] for w in worst) <= 0.005 * desc.n_params, (mode, worst)
+            return
+        # mode 2: the device's ReLU decisions, in buffer row order
+        perm = tr.ctx.buffer("perm", np.uint32)
+        rows_max = max(N, B)
+        z, mag = _oracle_pre_activations(cfg, p0, ot)
+        dev_masks, flips = {}, {}
+        for l, _, n in _hidden_layers(cfg):
+            h = tr.ctx.buffer(f"hidden:{l}", shape=(rows_max, n))[:B]
+            mk = np.zeros((B, n), np.uint8)
+            mk[perm] = h > 0
+            dev_masks[l] = mk
+            diff = mk.astype(bool) != (z[l] > 0)
+            flips[l] = int(diff.sum())
+            # every differing decision is a rounding-level pre-activation
+            assert np.all(np.abs(z[l][diff]) <= TOL * mag[l][diff]), (l, np.abs(z[l][diff]).max())
+        _, gm, msm = _oracle_grad(cfg, env, p0, B, ot, logp, advn, val, ent, relu_masks=dev_masks)
+        worst_m = _worst(cfg, g, gm)
+        print(f"\n{env} mode 2: ReLU decisions differing from the oracle's per hidden layer {flips}; "
+              f"worst tensor error / bar: {max(w[2] for w in worst):.2f} with the oracle's decisions, "
+              f"{max(w[2] for w in worst_m):.2f} with the device's")
+        assert all(w[2] <= 1.0 for w in worst_m), (mode, flips, worst_m)
+        # where no decision differs the two oracle gradients are the same computation
+        if sum(flips.values()) == 0:
+            assert np.array_equal(gm, go)
     finally:
         tr.close(); ot.close()

@@ -96,3 +96,54 @@ def test_popart_multiplayer(env, N, T, ctde):
     cfg, tr, ot = _wide(env, N, T, ctde=ctde)
     _rounds(cfg, tr, ot, _cmp_wide)
     tr.close(); ot.close()
+
+
+def test_popart_world2_rank_slot_checked():
+    """PopArt at W > 1 gathers every rank's batch statistics into the slot bppo_set_rank
+    names (popart.hip popart_gather).  A context that never set its rank fails
+    the update with BPPO_ERR_ARG instead of writing a default slot 0 (every rank in one slot:
+    the SUM scales that slot by W on all ranks alike and no cross-rank check sees it); two
+    contexts in one slot are caught from the gathered statistics.  One process, the
+    host-staged callback standing in for the other rank: a no-op (the other rank's slot and
+    gradient all zero), then a doubling (a second context with the same data and rank)."""
+    import ctypes as C
+    import bppo._lib as L
+    hip = C.CDLL("libamdhip64.so")
+    N, T = 256, 16
+    cfg = bppo.make_config("cartpole", num_envs=N, num_steps=T, normalize_values=True)
+    params = bppo.orthogonal_init(cfg, seed=1)
+    lr, ent = bppo.schedule_get(cfg["learning_rate"], 0), bppo.schedule_get(cfg["entropy_coef"], 0)
+
+    def run(setup):
+        tr = bppo.Trainer(cfg, params=params)
+        try:
+            keep = setup(tr)
+            bppo.collect_rollouts(tr.ctx)
+            bppo.compute_gae(tr.ctx)
+            with pytest.raises(L.BppoError) as e:
+                bppo.ppo_update(tr.ctx, lr, ent)
+            del keep
+            return e.value
+        finally:
+            tr.close()
+
+    def no_rank(tr):
+        cb = L.ALLREDUCE_FN(lambda p, n, user: 0)
+        assert L.lib().bppo_set_allreduce(tr.ctx.h, cb, None, 2) == L.OK
+        return cb
+
+    def doubled(p, n):
+        buf = np.zeros(n, np.float32)
+        assert hip.hipMemcpy(buf.ctypes.data_as(C.c_void_p), C.c_void_p(p), C.c_size_t(4 * n), 2) == 0   # D2H
+        buf *= 2.0
+        assert hip.hipMemcpy(C.c_void_p(p), buf.ctypes.data_as(C.c_void_p), C.c_size_t(4 * n), 1) == 0   # H2D
+
+    def same_rank(tr):
+        tr.ctx.rank = 0
+        tr.ctx.set_allreduce(doubled, 2)
+        return None
+
+    e = run(no_rank)
+    assert e.status == L.ERR_ARG and "bppo_set_rank" in str(e), e
+    e = run(same_rank)
+    assert e.status == L.ERR_ARG and "another rank wrote" in str(e), e
