@@ -86,6 +86,7 @@ EXPORTS = (
     "bppo_optimizer_get", "bppo_optimizer_set", "bppo_popart_get", "bppo_popart_set",
     "bppo_config_size", "bppo_update_metrics_size", "bppo_episode_size", "bppo_rollout_info_size",
     "bppo_set_explained_variance_mode", "bppo_set_minibatch_kernel", "bppo_set_rank",
+    "bppo_debug_record_params",
 )
 
 # ABI struct -> the library's sizeof export (checked when the library loads)
@@ -171,6 +172,7 @@ def lib():
         "bppo_popart_set": (i32, [vp, vp]),
         "bppo_set_explained_variance_mode": (i32, [vp, i32]),
         "bppo_set_minibatch_kernel": (i32, [vp, i32]),
+        "bppo_debug_record_params": (i32, [vp, vp, i32]),
     }
     for name in STRUCT_SIZES:
         sig[name] = (sz, [])

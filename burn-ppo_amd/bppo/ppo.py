@@ -181,6 +181,18 @@ class Context:
         (default); 1: exact for every minibatch; 2: split for every minibatch (parity hook)"""
         self._chk(L.lib().bppo_set_minibatch_kernel(self.h, int(mode)))
 
+    def record_params(self, max_minibatches):
+        """parity hook (bppo_debug_record_params): the next updates copy the parameters of
+        each minibatch they run into the returned [max_minibatches, n_params] array
+        (record_params(0) stops it)"""
+        if max_minibatches <= 0:
+            self._chk(L.lib().bppo_debug_record_params(self.h, None, 0))
+            self._rec = None
+            return None
+        self._rec = np.zeros((max_minibatches, self.n_params), np.float32)
+        self._chk(L.lib().bppo_debug_record_params(self.h, self._rec.ctypes.data, max_minibatches))
+        return self._rec
+
     def set_allreduce(self, fn, world, stream_ordered=False):
         """fn(device_ptr:int, n:int) -> None must leave the SUM over ranks in place.
         stream_ordered: fn only enqueues the reduction on `self.stream` (no host

@@ -970,6 +970,13 @@ extern "C" bppo_status bppo_set_explained_variance_mode(bppo_ctx *c, int32_t mod
     return BPPO_OK;
 }
 
+extern "C" bppo_status bppo_debug_record_params(bppo_ctx *c, float *host, int32_t max_minibatches) {
+    if (!c || max_minibatches < 0) return BPPO_ERR_ARG;
+    c->dbg_params = max_minibatches > 0 ? host : nullptr;
+    c->dbg_params_max = host ? max_minibatches : 0;
+    return BPPO_OK;
+}
+
 extern "C" bppo_status bppo_set_minibatch_kernel(bppo_ctx *c, int32_t mode) {
     if (!c || mode < 0 || mode > 2) return BPPO_ERR_ARG;
     c->mb_kernel = mode;
@@ -1110,8 +1117,14 @@ extern "C" bppo_status bppo_ppo_update(bppo_ctx *c, double lr, double ent_coef, 
                 BPPO_HIP(c, hipMemcpyAsync(c->d_grad + np + GRAD_VEMAX_LOCAL, &ninf, sizeof(float),
                                            hipMemcpyHostToDevice, c->stream));
             } else if (c->wide) {
+                if (c->dbg_params && nrow < c->dbg_params_max)   // parity hook: this minibatch's parameters
+                    BPPO_HIP(c, hipMemcpyAsync(c->dbg_params + (size_t)nrow * np, c->d_params, sizeof(float) * np,
+                                               hipMemcpyDeviceToHost, c->stream));
                 TRY(wide_minibatch(c, (uint32_t)start, (uint32_t)sz, ent_coef, first_mb));
             } else {
+                if (c->dbg_params && nrow < c->dbg_params_max)
+                    BPPO_HIP(c, hipMemcpyAsync(c->dbg_params + (size_t)nrow * np, c->d_params, sizeof(float) * np,
+                                               hipMemcpyDeviceToHost, c->stream));
                 TRY(launch_minibatch(c, (uint32_t)start, (uint32_t)sz, (float)ent_coef, first_mb));
             }
             if (fw_timed) { BPPO_HIP(c, hipEventRecord(c->ev[TM_FWDBWD][1], c->stream)); fw_recorded = true; }
@@ -1401,6 +1414,11 @@ static BufDesc find_buf(bppo_ctx *c, const char *name) {
     if (!strcmp(name, "returns")) return {c->d_ret, TN * 4};
     if (!strcmp(name, "all_rewards")) return {c->d_rew, TN * 4};
     if (!strcmp(name, "perm")) return {c->d_perm, TN * 4};
+    if (!strncmp(name, "perm_ep:", 8)) {          // epoch e's permutation of the last update
+        const int e = atoi(name + 8);
+        if (e < 0 || e >= c->cfg.num_epochs || !c->d_perm_ep) return {nullptr, 0};
+        return {c->d_perm_ep + (size_t)e * TN, TN * 4};
+    }
     if (!strcmp(name, "last_values")) return {c->d_last_v, (size_t)c->N * 4};
     if (!strcmp(name, "grad")) return {c->d_grad, c->net.n_params * 4};
     return {nullptr, 0};

@@ -114,6 +114,9 @@ struct WordBuf {                                  // ChaCha12 words made on the 
 struct FyRanges {
     uint32_t *x = nullptr;            // device [nb + 1] range boundaries
     uint32_t *cb = nullptr;           // device [ncb] first range of each 2^11-target block
+    uint32_t *cursor = nullptr;       // device [nb] steps per range (k_fyb_bucket; reset by k_fyb_link)
+    uint2 *P = nullptr;               // device [nb][FYB_CAP] (step, target) slots of each range
+    uint32_t *flag = nullptr;         // device: a range overflowed (0 between permutations)
     int nb = 0, ncb = 0;              // nb = 0: direct bucketing only
     uint32_t n = 0;
 };
@@ -225,10 +228,15 @@ struct ShuffleEngine {
     void worker(int i);
     void launch_walk(int i, uint64_t start, int wbuf);   // mu held
     void stop_walks(int lo, int hi);                     // stop and wait (mu not held)
-    const uint32_t *words(int b, uint64_t pos, uint64_t len, std::vector<uint32_t> &scratch);
+    const uint32_t *words(int b, uint64_t pos, uint64_t len, std::vector<uint32_t> &scratch, bool true_walk = false);
+    // the true walk's second word source (run thread only): the previous job's carry region,
+    // which holds this job's first epochs (made once, not again in this job's region 0)
+    int alt_b = -1;
+    WordBuf::Region alt_reg;
     struct WalkStats { uint64_t words = 0, tsc_walk = 0, tsc_words = 0; };
     void walk_pair(int i, WalkStats &st);
-    uint64_t walk_piece(int b, uint64_t pos, uint32_t *r, std::vector<uint32_t> &scratch, WalkStats &st);
+    uint64_t walk_piece(int b, uint64_t pos, uint32_t *r, std::vector<uint32_t> &scratch, WalkStats &st,
+                        bool true_walk = false);
     void flush(WalkStats &st, std::atomic<uint64_t> &words_ctr);
     int peek(int i, uint64_t q, uint32_t *r);     // walk i's range at checkpoint q: 1 known, 0 not yet, -1 never
 };
@@ -261,6 +269,8 @@ struct bppo_ctx {
     int slab_used = 0;                // waves that wrote a row in the last minibatch launch
     int relu_mfma = 1;                // CfgB net (64x2 relu): the MFMA minibatch kernel
     int mb_kernel = 0;                // bppo_set_minibatch_kernel: 0 exact first / split rest, 1 exact, 2 split
+    float *dbg_params = nullptr;      // bppo_debug_record_params: host [dbg_params_max][n_params]
+    int dbg_params_max = 0;
     // env state (CartPole SoA)
     float *d_cp = nullptr;            // x, x_dot, theta, theta_dot  [4][N]
     int32_t *d_steps = nullptr;

@@ -17,9 +17,10 @@
 // per step.  The ranged one (n >= FYB_MIN_N: the per-epoch shuffles of a
 // context) partitions the steps into target ranges of equal expected load —
 // J[i] is uniform on [0, i], so E#{i : J[i] < x} = x (1 + ln(n/x)) — with LDS
-// histograms, then sorts and links each range in LDS: no global atomics.  A
-// range over its LDS capacity (inputs far from uniform) raises a flag and the
-// direct path runs after it, gated on that flag, so any J gives the same result.
+// histograms, each block reserving its slots in a range's fixed-capacity slice with
+// one global atomic per (block, range), then sorts and links each range in LDS.  A
+// range over its capacity (inputs far from uniform) raises a flag and the direct
+// path runs after it, gated on that flag, so any J gives the same result.
 #include <algorithm>
 #include <cmath>
 #include <vector>
@@ -259,11 +260,66 @@ __global__ void __launch_bounds__(FYB_THREADS) k_fyb_scatter(const uint32_t *J, 
     }
 }
 
+// passes 1 + 2 in one launch (r06; was k_fyb_hist, a three-launch scan of the [range][block]
+// counts and k_fyb_scatter): the block's range histogram in LDS, then one global atomic per
+// (block, range) reserves the block's slots in the range's fixed-capacity slice of P
+// ([nb][FYB_CAP]; cursor[b] ends as range b's step count), then the chunk's steps are
+// scattered into them (its J re-read, an L2 hit).  The slot order inside a range is free:
+// k_fyb_link sorts it.  A range past FYB_CAP raises the flag (its excess is not written)
+__global__ void __launch_bounds__(FYB_THREADS) k_fyb_bucket(const uint32_t *J, uint32_t n, uint32_t chunk, FyTab t,
+                                                            uint32_t *cursor, uint2 *P, uint32_t *flag) {
+    extern __shared__ uint32_t fsm[];
+    uint32_t *sx = fsm, *scb = sx + t.nb + 1, *hist = scb + t.ncb;
+    fyb_load_tab(t, sx, scb);
+    for (int k = threadIdx.x; k < t.nb; k += blockDim.x) hist[k] = 0u;
+    __syncthreads();
+    const uint32_t i0 = blockIdx.x * chunk, i1 = min(n, i0 + chunk);
+    uint32_t i = i0 + threadIdx.x;
+    for (; i + (FYB_U - 1) * blockDim.x < i1; i += FYB_U * blockDim.x) {
+        uint32_t jv[FYB_U];
+#pragma unroll
+        for (int u = 0; u < FYB_U; u++) jv[u] = J[i + u * blockDim.x];
+#pragma unroll
+        for (int u = 0; u < FYB_U; u++) atomicAdd(&hist[fyb_range(jv[u], sx, scb)], 1u);
+    }
+    for (; i < i1; i += blockDim.x) atomicAdd(&hist[fyb_range(J[i], sx, scb)], 1u);
+    __syncthreads();
+    for (int k = threadIdx.x; k < t.nb; k += blockDim.x) {
+        const uint32_t c = hist[k];
+        uint32_t b0 = 0u;
+        if (c) {
+            b0 = atomicAdd(&cursor[k], c);
+            if (b0 + c > (uint32_t)FYB_CAP) atomicOr(flag, 1u);
+        }
+        hist[k] = (uint32_t)k * FYB_CAP + b0;      // this block's first slot in range k
+    }
+    __syncthreads();
+    i = i0 + threadIdx.x;
+    for (; i + (FYB_U - 1) * blockDim.x < i1; i += FYB_U * blockDim.x) {
+        uint32_t jv[FYB_U];
+#pragma unroll
+        for (int u = 0; u < FYB_U; u++) jv[u] = J[i + u * blockDim.x];
+#pragma unroll
+        for (int u = 0; u < FYB_U; u++) {
+            const uint32_t rb = fyb_range(jv[u], sx, scb);
+            const uint32_t slot = atomicAdd(&hist[rb], 1u);
+            if (slot < (rb + 1u) * (uint32_t)FYB_CAP) P[slot] = make_uint2(i + u * blockDim.x, jv[u]);
+        }
+    }
+    for (; i < i1; i += blockDim.x) {
+        const uint32_t j = J[i], rb = fyb_range(j, sx, scb);
+        const uint32_t slot = atomicAdd(&hist[rb], 1u);
+        if (slot < (rb + 1u) * (uint32_t)FYB_CAP) P[slot] = make_uint2(i, j);
+    }
+}
+
 // pass 3: one block per range — counting sort by target in LDS, each target's
-// steps ordered by index, then succ / fw exactly as k_fy_link
+// steps ordered by index, then succ / fw exactly as k_fy_link.  Ranges come as a
+// [range][block] offset table H (e0 = H[b][0]) or, cursor != nullptr, as fixed slices
+// P[b * FYB_CAP ...] of cursor[b] steps (cursor[b] reset to 0 for the next permutation)
 __global__ void __launch_bounds__(FYB_LINK_THREADS) k_fyb_link(uint32_t n, FyTab t, const uint32_t *H, int nblk,
                                                                const uint2 *P, uint32_t *succ, uint32_t *fw,
-                                                               uint32_t *flag) {
+                                                               uint32_t *flag, uint32_t *cursor) {
     __shared__ uint32_t ent_i[FYB_CAP];
     __shared__ uint16_t ent_t[FYB_CAP];
     __shared__ uint32_t tst[FYB_RMAX + 1];
@@ -271,8 +327,17 @@ __global__ void __launch_bounds__(FYB_LINK_THREADS) k_fyb_link(uint32_t n, FyTab
     __shared__ uint32_t srt[FYB_CAP];
     __shared__ uint32_t sh[FYB_LINK_THREADS / 64];
     const int b = blockIdx.x;
-    const uint32_t e0 = H[(size_t)b * nblk], e1 = b + 1 < t.nb ? H[(size_t)(b + 1) * nblk] : n;
-    const uint32_t cnt = e1 - e0, lo = t.x[b], R = t.x[b + 1] - lo;
+    uint32_t e0, cnt;
+    if (cursor) {
+        e0 = (uint32_t)b * FYB_CAP;
+        cnt = cursor[b];
+        __syncthreads();                      // every thread has read the count
+        if (threadIdx.x == 0) cursor[b] = 0u;
+    } else {
+        e0 = H[(size_t)b * nblk];
+        cnt = (b + 1 < t.nb ? H[(size_t)(b + 1) * nblk] : n) - e0;
+    }
+    const uint32_t lo = t.x[b], R = t.x[b + 1] - lo;
     if (cnt > (uint32_t)FYB_CAP) {          // far from uniform: the gated direct path takes over
         if (threadIdx.x == 0) atomicOr(flag, 1u);
         return;
@@ -321,9 +386,12 @@ __global__ void __launch_bounds__(FYB_LINK_THREADS) k_fyb_link(uint32_t n, FyTab
 // capacity: J far from uniform): the direct bucketing of k_fy_zero .. k_fy_final
 // in ONE block, phase by phase (__syncthreads orders the block's global memory).
 // Slow, exact, and launched unconditionally behind the flag, so the common case
-// costs one empty launch instead of eight.
-__global__ void __launch_bounds__(SCAN_B) k_fy_direct_block(const uint32_t *J, uint32_t n, uint32_t *scratch,
-                                                            uint32_t *perm, const uint32_t *flag, uint32_t *inv) {
+// costs one empty launch instead of eight -- a block of FY_DIRECT_THREADS (r06: was 1024
+// threads, which waited 72 us on average, up to 372, for a CU with room beside the
+// update kernels, holding back the epoch's permutation event)
+constexpr int FY_DIRECT_THREADS = 256;
+__global__ void __launch_bounds__(FY_DIRECT_THREADS) k_fy_direct_block(const uint32_t *J, uint32_t n, uint32_t *scratch,
+                                                                       uint32_t *perm, uint32_t *flag, uint32_t *inv) {
     if (*flag == 0u) return;
     __shared__ uint32_t sh[SCAN_B / 64];
     uint32_t *cnt = scratch, *bucket = scratch + (size_t)n, *succ = scratch + 2 * (size_t)n,
@@ -334,7 +402,7 @@ __global__ void __launch_bounds__(SCAN_B) k_fy_direct_block(const uint32_t *J, u
     for (uint32_t i = t; i < n; i += T) atomicAdd(&cnt[J[i]], 1u);
     __syncthreads();
     uint32_t carry = 0;
-    for (uint32_t b0 = 0; b0 < n; b0 += SCAN_TILE) {
+    for (uint32_t b0 = 0; b0 < n; b0 += T * SCAN_IPT) {
         const uint32_t base = b0 + t * SCAN_IPT;
         uint32_t v[SCAN_IPT], sum = 0;
 #pragma unroll
@@ -376,6 +444,8 @@ __global__ void __launch_bounds__(SCAN_B) k_fy_direct_block(const uint32_t *J, u
         perm[i] = v;
         if (inv) inv[v] = i;
     }
+    __syncthreads();
+    if (t == 0) *flag = 0u;            // the ranged path's flag is 0 between permutations
 }
 
 static size_t fyb_lds(int nb, int ncb) { return sizeof(uint32_t) * (size_t)(2 * nb + 1 + ncb); }
@@ -415,6 +485,13 @@ hipError_t fy_ranges_init(FyRanges &r, uint32_t n) {
     if ((size_t)nb * FYB_BLOCKS > n || fyb_lds(nb, (int)cb.size()) > FYB_LDS_MAX) return hipSuccess;
     hipError_t e = hipMalloc((void **)&r.x, sizeof(uint32_t) * x.size());
     if (e == hipSuccess) e = hipMalloc((void **)&r.cb, sizeof(uint32_t) * cb.size());
+    // k_fyb_bucket's range slices, counts and overflow flag (zero: the invariant between
+    // permutations that k_fyb_link and k_fy_direct_block restore)
+    const size_t nbs = x.size() - 1;
+    if (e == hipSuccess) e = hipMalloc((void **)&r.P, sizeof(uint2) * nbs * FYB_CAP);
+    if (e == hipSuccess) e = hipMalloc((void **)&r.cursor, sizeof(uint32_t) * (nbs + 1));
+    if (e == hipSuccess) e = hipMemset(r.cursor, 0, sizeof(uint32_t) * (nbs + 1));
+    r.flag = r.cursor ? r.cursor + nbs : nullptr;
     if (e == hipSuccess) e = hipMemcpy(r.x, x.data(), sizeof(uint32_t) * x.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(r.cb, cb.data(), sizeof(uint32_t) * cb.size(), hipMemcpyHostToDevice);
     if (e != hipSuccess) { fy_ranges_free(r); return e; }
@@ -426,7 +503,10 @@ hipError_t fy_ranges_init(FyRanges &r, uint32_t n) {
 void fy_ranges_free(FyRanges &r) {
     if (r.x) (void)hipFree(r.x);
     if (r.cb) (void)hipFree(r.cb);
-    r.x = r.cb = nullptr;
+    if (r.P) (void)hipFree(r.P);
+    if (r.cursor) (void)hipFree(r.cursor);
+    r.x = r.cb = r.cursor = r.flag = nullptr;
+    r.P = nullptr;
     r.nb = r.ncb = 0;
 }
 
@@ -440,21 +520,29 @@ hipError_t fisher_yates_device(const uint32_t *d_J, uint32_t n, uint32_t *scratc
     const int grid = 2048;
     if (rg && rg->nb > 0 && rg->n == n) {
         const FyTab t{rg->x, rg->cb, rg->nb, rg->ncb};
-        uint32_t *H = perm, *flag = scan + n / 8192 + 1;
+        uint32_t *flag = rg->flag;
         const uint32_t chunk = (n + FYB_BLOCKS - 1) / FYB_BLOCKS;
         const size_t lds = fyb_lds(t.nb, t.ncb);
-        hipLaunchKernelGGL(k_fyb_hist, dim3(FYB_BLOCKS), dim3(FYB_THREADS), lds, st, d_J, n, chunk, t, H, flag);
-        launch_scan(H, (uint32_t)t.nb * FYB_BLOCKS, scan, H, nullptr, st);
-        hipLaunchKernelGGL(k_fyb_scatter, dim3(FYB_BLOCKS), dim3(FYB_THREADS), lds, st, d_J, n, chunk, t,
-                           (const uint32_t *)H, reinterpret_cast<uint2 *>(scratch));
-        hipLaunchKernelGGL(k_fyb_link, dim3(t.nb), dim3(FYB_LINK_THREADS), 0, st, n, t, (const uint32_t *)H,
-                           FYB_BLOCKS, reinterpret_cast<const uint2 *>(scratch), succ, fw, flag);
+        static const bool fused = !(getenv("BPPO_FY_FUSED") && atoi(getenv("BPPO_FY_FUSED")) == 0);
+        if (fused) {
+            hipLaunchKernelGGL(k_fyb_bucket, dim3(FYB_BLOCKS), dim3(FYB_THREADS), lds, st, d_J, n, chunk, t,
+                               rg->cursor, rg->P, flag);
+            hipLaunchKernelGGL(k_fyb_link, dim3(t.nb), dim3(FYB_LINK_THREADS), 0, st, n, t, (const uint32_t *)nullptr,
+                               FYB_BLOCKS, (const uint2 *)rg->P, succ, fw, flag, rg->cursor);
+        } else {      // r05's passes (A/B): histogram, scan of the [range][block] counts, scatter
+            uint32_t *H = perm;
+            hipLaunchKernelGGL(k_fyb_hist, dim3(FYB_BLOCKS), dim3(FYB_THREADS), lds, st, d_J, n, chunk, t, H, flag);
+            launch_scan(H, (uint32_t)t.nb * FYB_BLOCKS, scan, H, nullptr, st);
+            hipLaunchKernelGGL(k_fyb_scatter, dim3(FYB_BLOCKS), dim3(FYB_THREADS), lds, st, d_J, n, chunk, t,
+                               (const uint32_t *)H, reinterpret_cast<uint2 *>(scratch));
+            hipLaunchKernelGGL(k_fyb_link, dim3(t.nb), dim3(FYB_LINK_THREADS), 0, st, n, t, (const uint32_t *)H,
+                               FYB_BLOCKS, reinterpret_cast<const uint2 *>(scratch), succ, fw, flag, (uint32_t *)nullptr);
+        }
         // pass 4 (k_fy_final) runs unless a range overflowed; then the one-block
         // direct pass computes the permutation instead
         hipLaunchKernelGGL(k_fy_final, dim3(grid), dim3(256), 0, st, d_J, n, (const uint32_t *)succ,
                            (const uint32_t *)fw, perm, (const uint32_t *)flag, inv);
-        hipLaunchKernelGGL(k_fy_direct_block, dim3(1), dim3(SCAN_B), 0, st, d_J, n, scratch, perm,
-                           (const uint32_t *)flag, inv);
+        hipLaunchKernelGGL(k_fy_direct_block, dim3(1), dim3(FY_DIRECT_THREADS), 0, st, d_J, n, scratch, perm, flag, inv);
         return hipGetLastError();
     }
     // direct path

@@ -438,7 +438,14 @@ bool ShuffleEngine::failed(std::string &msg) const {
 // words [pos, pos + len) of word buffer b (one checkpoint piece: never crosses a
 // chunk); outside its regions (not at the usual sizes) they are made here
 
-const uint32_t *ShuffleEngine::words(int b, uint64_t pos, uint64_t len, std::vector<uint32_t> &scratch) {
+const uint32_t *ShuffleEngine::words(int b, uint64_t pos, uint64_t len, std::vector<uint32_t> &scratch, bool true_walk) {
+    if (true_walk && alt_b >= 0 && pos >= alt_reg.base && pos + len <= alt_reg.base + alt_reg.len) {
+        // the previous job's carry region (its chunks' flags are not reset before this job
+        // ends: the buffer is re-made only by the next job, after this walk)
+        WordBuf &a = wb[alt_b];
+        const uint64_t o = alt_reg.off + (pos - alt_reg.base);
+        if (a.ok[(size_t)(o / SHUF_CHUNK)].load(std::memory_order_acquire)) return a.h + o;
+    }
     WordBuf &w = wb[b];
     for (int g = 0; g < w.nreg; g++) {
         const WordBuf::Region &R = w.reg[g];
@@ -464,10 +471,11 @@ const uint32_t *ShuffleEngine::words(int b, uint64_t pos, uint64_t len, std::vec
 // (the diagnostic counters are per walk thread and folded into the engine's
 // atomics once per walk / epoch: shared counters per piece would ping-pong one
 // cache line between every walker's core)
-uint64_t ShuffleEngine::walk_piece(int b, uint64_t pos, uint32_t *r, std::vector<uint32_t> &scratch, WalkStats &st) {
+uint64_t ShuffleEngine::walk_piece(int b, uint64_t pos, uint32_t *r, std::vector<uint32_t> &scratch, WalkStats &st,
+                                   bool true_walk) {
     const uint64_t q = (pos / SHUF_CK + 1) * SHUF_CK;
     const uint64_t t0 = __rdtsc();
-    const uint32_t *w = words(b, pos, q - pos, scratch);
+    const uint32_t *w = words(b, pos, q - pos, scratch, true_walk);
     const uint64_t t1 = __rdtsc();
     const uint64_t used = bppo_host::chain_walk_nj(w, (size_t)(q - pos), r);
     st.tsc_words += t1 - t0;
@@ -598,6 +606,10 @@ void ShuffleEngine::worker(int i) {
 // windowed jobs: walks i and i + 1 (two epochs, known starts, nothing to merge with)
 // in one thread, their 32-word blocks interleaved (chain_walk2_nj); checkpoints as
 // in worker().  A walk that ends is marked done at once, the other goes on alone.
+// (r06 tried the speculative walks of chained jobs in pairs too, with worker()'s merge
+// and continuation rules: 116-119 instead of 137-148 ms of CPU per update, but each chain
+// at ~0.54 instead of 0.45 ns per word, and the walk per update 12.1-13.2 instead of
+// 10.4-10.9 ms: profiles/r06d/.  Not kept.)
 void ShuffleEngine::walk_pair(int i, WalkStats &st) {
     struct Chain {
         SpecWalk *s;
@@ -632,13 +644,16 @@ void ShuffleEngine::walk_pair(int i, WalkStats &st) {
         c.left -= used;
         c.pos += used;
         st.words += used;
-        if (c.r < 2 || c.s->stop.load(std::memory_order_relaxed)) { finish(c); cv.notify_all(); return; }
+        if (c.r < 2) { finish(c); cv.notify_all(); return; }
+        // a stop is taken only at a checkpoint, as in worker(): a stopped walk's end is then
+        // its last recorded checkpoint, never a position inside a piece
         if (c.left == 0) {                       // at a checkpoint
             const int64_t k = (int64_t)((c.pos - c.s->ck_base) / SHUF_CK);
             if (k < (int64_t)c.s->ck.size()) {
                 c.s->ck[k] = c.r;
                 c.s->progress.store(k, std::memory_order_release);
             }
+            if (c.s->stop.load(std::memory_order_relaxed)) { finish(c); cv.notify_all(); return; }
             refill(c);
         }
     };
@@ -776,10 +791,27 @@ void ShuffleEngine::run() {
         const double sE = sigma * std::sqrt((double)std::max(epochs, 1));
         {
             auto chunks = [](double w) { return ((uint64_t)std::max(w, 1.0) + SHUF_CHUNK - 1) / SHUF_CHUNK * SHUF_CHUNK; };
+            // the previous job's carry region (buffer b ^ 1, its region 1) was made for this
+            // job's first epochs: when it holds this start, region 0 begins where it ends and
+            // the true walk reads those words from it (made once per update, not twice: r06,
+            // ~35 M producer words per CfgB update).  Any region's words are the stream's
+            // words at those positions, so a mispredicted start is only a smaller overlap.
+            const uint64_t s0 = start / SHUF_CK * SHUF_CK;
+            const uint64_t end0 = s0 + chunks((double)(start - s0) + epochs * Ew + 10.0 * sE + 4.0 * SHUF_CK);
+            const WordBuf &Pv = wb[b ^ 1];
+            alt_b = -1;
+            uint64_t base0 = s0;
+            static const bool reuse = !(getenv("BPPO_SHUFFLE_CARRY_REUSE") && atoi(getenv("BPPO_SHUFFLE_CARRY_REUSE")) == 0);
+            if (reuse && seq > 1 && Pv.nreg == 2 && Pv.reg[1].len > 0 && Pv.reg[1].base <= s0 &&
+                Pv.reg[1].base + Pv.reg[1].len > s0 && Pv.reg[1].base + Pv.reg[1].len < end0) {
+                alt_b = b ^ 1;
+                alt_reg = Pv.reg[1];
+                base0 = alt_reg.base + alt_reg.len;
+            }
             W.nreg = 1;
-            W.reg[0].base = start / SHUF_CK * SHUF_CK;
+            W.reg[0].base = base0;
             W.reg[0].off = 0;
-            W.reg[0].len = std::min(W.cap, chunks((double)(start - W.reg[0].base) + epochs * Ew + 10.0 * sE + 4.0 * SHUF_CK));
+            W.reg[0].len = std::min(W.cap, chunks((double)(end0 - base0)));   // whole chunks (their ok flags)
             if (K > 0) {
                 const double sC = sigma * std::sqrt((double)(epochs + C));
                 const double lo = (double)start + epochs * Ew + (double)gap - 4.0 * sC - 4.0 * SHUF_CK;
@@ -945,7 +977,7 @@ void ShuffleEngine::run() {
                     }
                 }
                 const uint64_t q = (pos / SHUF_CK + 1) * SHUF_CK;
-                pos = walk_piece(b, pos, &r, scratch, tst);
+                pos = walk_piece(b, pos, &r, scratch, tst, true);
                 if (cancel.load(std::memory_order_relaxed)) { cancelled = true; break; }
                 if (pos != q || r < 2) continue;
                 tck.push_back({q, r});

@@ -281,7 +281,11 @@ bppo_status bppo_opponents_get_envs(bppo_ctx *ctx, int32_t *learner_pos, int32_t
 /* parity hooks: export / import a RolloutBuffer field.  names: "obs", "priv",
  * "actions" (i32), "rewards", "dones", "values", "log_probs", "advantages",
  * "returns", "players" (i32), "all_rewards", "masks", "last_v_pp", "perm" (u32,
- * last epoch's shuffled indices) */
+ * last epoch's shuffled indices), "grad" (the last minibatch's gradient); export only,
+ * multi-player nets: "hidden:<l>" = FC hidden layer l's activations of the last forward
+ * ([rows_max][width] f32, rows_max = max(num_envs, ceil(T N / num_minibatches)); the last
+ * minibatch's rows in "perm" order -- the device's ReLU decisions for
+ * tests/test_gpu_gemm_split.py) */
 /* the last update's per-minibatch metric rows in run order (parity diagnosis: which
  * minibatch's statistics first leave the bar): row k = the minibatch's sums
  * [policy_loss, 2*value_loss, entropy, approx_kl, clip_fraction, value, return, |v-R|,
@@ -337,6 +341,12 @@ bppo_status bppo_set_explained_variance_mode(bppo_ctx *ctx, int32_t mode);
  *     contraction (the first included); CNN nets the exact chains with f32 split-K weight
  *     gradients. */
 bppo_status bppo_set_minibatch_kernel(bppo_ctx *ctx, int32_t mode);
+
+/* parity hook: while host != NULL, every bppo_ppo_update copies the parameters it runs each
+ * minibatch with (the first max_minibatches in run order) to host[k * num_params], so each
+ * minibatch's statistics can be recomputed from the device's own parameters at any size
+ * (tests/test_gpu_fullsize.py); "perm_ep:<e>" (bppo_buffer_get) is epoch e's permutation */
+bppo_status bppo_debug_record_params(bppo_ctx *ctx, float *host, int32_t max_minibatches);
 
 /* device timing of the last call of each phase kernel (ms), for bench.py's roofline */
 bppo_status bppo_last_kernel_ms(bppo_ctx *ctx, const char *kernel, float *ms);

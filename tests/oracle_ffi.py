@@ -344,6 +344,30 @@ def net_forward(desc, params, obs, priv=None):
     return logits, values
 
 
+_mb_stats_fn = None
+
+
+def minibatch_stats(desc, params, obs, priv, actions, old_logp, adv_norm, returns, old_values, masks, pc, ent):
+    """or_minibatch_loss_grad's statistics alone (grads = NULL: forward and loss, no backward)"""
+    global _mb_stats_fn
+    if _mb_stats_fn is None:
+        f = lib()["or_minibatch_loss_grad"]          # a second function object: its own argtypes
+        vp = C.c_void_p
+        f.restype = None
+        f.argtypes = [C.POINTER(NetDesc), vp, C.c_size_t, vp, vp, vp, vp, vp, vp, vp, vp, C.POINTER(PpoCfg),
+                      C.c_double, vp, C.POINTER(MbStats)]
+        _mb_stats_fn = f
+    arrs = [np.ascontiguousarray(a, t) if a is not None else None
+            for a, t in ((params, np.float32), (obs, np.float32), (priv, np.float32), (actions, np.int32),
+                         (old_logp, np.float32), (adv_norm, np.float32), (returns, np.float32),
+                         (old_values, np.float32), (masks, np.float32))]
+    ptr = [None if a is None else a.ctypes.data for a in arrs]
+    ms = MbStats()
+    _mb_stats_fn(C.byref(desc), ptr[0], len(arrs[1]) if arrs[1].ndim == 1 else arrs[1].shape[0], ptr[1], ptr[2],
+                 ptr[3], ptr[4], ptr[5], ptr[6], ptr[7], ptr[8], C.byref(pc), ent, None, C.byref(ms))
+    return {f: getattr(ms, f) for f, _ in MbStats._fields_}
+
+
 def linear(x, W, b, relu):
     """or_linear: y = act(x W + b) in matrixmultiply's KC=256 fma-chain order (relu: 1, 0 tanh, -1 none)"""
     B, K = x.shape

@@ -124,16 +124,19 @@ def test_shuffle_engine_equals_sequential_walks(seed, start, n, epochs, gap, job
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("policy", ["0", "2"])
+@pytest.mark.parametrize("policy", ["0", "2", "k6"])
 @pytest.mark.parametrize("seed,start,n,epochs,gap,jobs", [
     (5, 77, 1 << 23, 4, 16_777_216, 3),
     (9, 3, 100_003, 6, 700_000, 3),
 ])
 def test_shuffle_engine_policies_equal_sequential(monkeypatch, policy, seed, start, n, epochs, gap, jobs):
-    """The job-start speculation policy (BPPO_SHUFFLE_FRONTIER=0) and frontier depth 2
-    give the same J and word positions as the sequential walk (the default, depth 1,
-    is covered above)."""
-    monkeypatch.setenv("BPPO_SHUFFLE_FRONTIER", policy)
+    """The job-start speculation policy (BPPO_SHUFFLE_FRONTIER=0), frontier depth 2 and six
+    guessed walks per boundary (BPPO_SHUFFLE_SPEC=6) give the same J and word positions as
+    the sequential walk (the default is covered above)."""
+    if policy == "k6":
+        monkeypatch.setenv("BPPO_SHUFFLE_SPEC", "6")
+    else:
+        monkeypatch.setenv("BPPO_SHUFFLE_FRONTIER", policy)
     J = np.zeros(n * epochs * jobs, np.uint32)
     ends = np.zeros(epochs * jobs, np.uint64)
     met = np.zeros(epochs * jobs, np.int32)
