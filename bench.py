@@ -421,7 +421,8 @@ def main():
     value = env_steps / dt
     ms_step = dt / args.steps * 1000.0
     # dominant kernel: the fused minibatch forward/loss/backward (16 launches per update):
-    # k_minibatch_split for 15 of them, the exact k_minibatch_mfma for the update's first
+    # k_minibatch_split for 15 of them; the update's first (ratio exactly 1) runs its exact-forward
+    # variant k_minibatch_split<true> (r06; k_minibatch_mfma with BPPO_MB_FIRST_MFMA=1)
     mb_rows = N * T // cfg["num_minibatches"]
     # the kernel alone (HIP events around EVERY launch, on its stream): the mean of the
     # split kernel's launches; the side-stream shuffle passes share the GPU with some of
@@ -447,7 +448,9 @@ def main():
             # matrix-pipe ceiling is 16/6 of the f32 one; layer 1 and the dZ2 step stay on the f32 MFMA
             "split_note": "f32-accurate: layer 2, dZ1 and dW1 on v_mfma_f32_32x32x16_bf16 with operands split "
                           "exactly into 3 bf16 pieces (6 products); peak quoted is the FP32 MFMA peak",
-            "exact_first_minibatch": {"kernel": "k_minibatch_mfma", "launch_ms": round(mb_ex, 4),
+            "exact_first_minibatch": {"kernel": "k_minibatch_mfma" if os.environ.get("BPPO_MB_FIRST_MFMA") == "1"
+                                      else "k_minibatch_split<true> (exact f32 forward, split-bf16 backward)",
+                                      "launch_ms": round(mb_ex, 4),
                                       "frac": round(flop / (mb_ex * 1e-3) / 1e12 / FP32_PEAK_TFLOPS, 4)
                                       if mb_ex > 0 else None},
             "mean_all_launches_ms": round(mb_all, 4)}

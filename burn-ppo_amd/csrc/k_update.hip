@@ -778,8 +778,12 @@ struct Params {
     float b1[H];
     float4 Wh[H];                 // {wp0, wp1, wv, 0} per hidden unit
     float bp[2], bv[2];
+    float2 PV[2][H];              // exact heads: {Wp[2k + h], Wv[k]} per lane half h (k_minibatch_mfma's pairs)
     __bf16 W1n[3][H * WPS];       // W1 pieces [j1][j2]
-    __bf16 W1t[3][H * WPS];       // W1 pieces [j2][perm(j1)]
+    union {
+        __bf16 W1t[3][H * WPS];   // W1 pieces [j2][perm(j1)] (the split forward)
+        float W1f[H * H];         // W1 [j1][j2] in f32 (the exact forward of the update's first minibatch)
+    };
     __device__ __forceinline__ float expf(float x) const { return bppo_math::expf_glibc_tab(x, exp2tab); }
     __device__ __forceinline__ float logf(float x) const { return bppo_math::logf_glibc_tab(x, linvc, llogc); }
 };
@@ -858,6 +862,7 @@ __device__ __forceinline__ Split8 load_pieces(const __bf16 (*img)[H * WPS], int 
     for (int p = 0; p < 3; p++) s.p[p] = *reinterpret_cast<const bf16x8_t *>(img[p] + off);
     return s;
 }
+template <bool EXACT_FWD>
 __device__ __forceinline__ void load_params_split(Params &S, const float *__restrict__ P) {
     constexpr CpOffsets O = cp_offsets<64, 2>();
     for (int i = threadIdx.x; i < 6 * H; i += blockDim.x) S.W0[i] = i < 5 * H ? P[O.w0 + i] : P[O.b0 + i - 5 * H];
@@ -869,12 +874,20 @@ __device__ __forceinline__ void load_params_split(Params &S, const float *__rest
         const __bf16 b = (__bf16)r;
         const __bf16 c = (__bf16)(r - (float)b);
         S.W1n[0][j1 * WPS + j2] = a; S.W1n[1][j1 * WPS + j2] = b; S.W1n[2][j1 * WPS + j2] = c;
-        const int t = j2 * WPS + perm_j1(j1);
-        S.W1t[0][t] = a; S.W1t[1][t] = b; S.W1t[2][t] = c;
+        if (EXACT_FWD) {
+            S.W1f[i] = w;
+        } else {
+            const int t = j2 * WPS + perm_j1(j1);
+            S.W1t[0][t] = a; S.W1t[1][t] = b; S.W1t[2][t] = c;
+        }
     }
     for (int i = threadIdx.x; i < H; i += blockDim.x) {
         S.b1[i] = P[O.b1 + i];
         S.Wh[i] = make_float4(P[O.wp + 2 * i], P[O.wp + 2 * i + 1], P[O.wv + i], 0.0f);
+        if (EXACT_FWD) {
+            S.PV[0][i] = make_float2(P[O.wp + 2 * i], P[O.wv + i]);
+            S.PV[1][i] = make_float2(P[O.wp + 2 * i + 1], P[O.wv + i]);
+        }
     }
     if (threadIdx.x < 32) S.exp2tab[threadIdx.x] = bppo_math::kExp2fTab[threadIdx.x];
     if (threadIdx.x < 16) {
@@ -886,6 +899,13 @@ __device__ __forceinline__ void load_params_split(Params &S, const float *__rest
 }
 }  // namespace mmf
 
+// EXACT_FWD (r06): the update's first minibatch, which runs with the rollout's parameters, so
+// the ratio must be exactly 1: the forward of k_minibatch_mfma -- layer 1 as below (the same
+// k-ordered MFMA chain, b0 added as the K pad's 1 * b0, i.e. after the five products), layer 2
+// as the f32 MFMA chain in natural k order from an [j1][row] LDS image of H1, both heads as
+// k-ordered fma chains over all 64 units (lane half h: logit h, both: the value) -- and the
+// backward of the split kernel (dW1 and dZ1 on the split-bf16 contraction): VERDICT r5 item 6
+template <bool EXACT_FWD>
 __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
     using namespace mmf;
     using mmb::cd_row;
@@ -894,7 +914,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
     Params &S = *reinterpret_cast<Params *>(smem);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     Wave &B = reinterpret_cast<Wave *>(smem + sizeof(Params) / 4)[wv];
-    load_params_split(S, g.params);
+    load_params_split<EXACT_FWD>(S, g.params);
     __syncthreads();
 #ifdef BPPO_MB_STAMPS
     unsigned long long st_acc[MB_NSEG] = {}, st_prev;
@@ -975,6 +995,13 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
 #pragma unroll
             for (int s = 0; s < 3; s++)
                 a1 = __builtin_amdgcn_mfma_f32_32x32x2f32(S.W0[(2 * s + h) * H + c + 32 * it], xs[s], a1, 0, 0, 0);
+            if (EXACT_FWD) {
+                // H1 as an [j1][row] image in the H2 tile: the C/D layout itself (row j1 =
+                // cd_row(q, h) + 32 it, column = row c), consecutive lanes, consecutive banks
+#pragma unroll
+                for (int q = 0; q < 16; q++) B.T[(cd_row(q, h) + 32 * it) * TR + c] = relu_bits(a1[q]);
+                continue;
+            }
 #pragma unroll
             for (int s2 = 0; s2 < 2; s2++) {
                 float v8[8];
@@ -987,9 +1014,21 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
                 __builtin_amdgcn_sched_barrier(0);   // bound the piece-load hoisting (registers)
             }
         }
+        if (EXACT_FWD) {
+            // layer 2 as k_minibatch_mfma: k = 2s + h per 32x32x2 step, natural order
+            wave_sync();
+#pragma unroll 4
+            for (int s = 0; s < 32; s++) {
+                const float av = B.T[(2 * s + h) * TR + c];
+                const float bv0 = S.W1f[(2 * s + h) * H + c], bv1 = S.W1f[(2 * s + h) * H + c + 32];
+                h2[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv0, h2[0], 0, 0, 0);
+                h2[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv1, h2[1], 0, 0, 0);
+            }
+        }
         __builtin_amdgcn_s_setprio(0);
         MB_STAMP(1);   // layers 1 and 2
         // H2 = relu(. + b1) -> the row-major tile for the heads
+        if (EXACT_FWD) wave_sync();          // every lane's last H1 read precedes the H2 stores
 #pragma unroll
         for (int ct = 0; ct < 2; ct++)
 #pragma unroll
@@ -1000,8 +1039,26 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
         wave_sync();
         MB_STAMP(2);   // H2 epilogue
         // ---- heads: lane = row c, lane half h over units [32 h, 32 h + 32), 2 chains each
+        // (EXACT_FWD: k_minibatch_mfma's k-ordered chains over all 64 units)
         float l0, l1, vv;
-        {
+        if (EXACT_FWD) {
+            float lh = 0.0f, vc = 0.0f;
+            const float *hr = B.T + c * WS;
+            const float2 *pv = S.PV[h];
+#pragma unroll 2
+            for (int k = 0; k < H; k += 4) {
+                const float4 x = *reinterpret_cast<const float4 *>(hr + k);
+                const float xs4[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const float2 w = pv[k + u];
+                    lh = __builtin_fmaf(xs4[u], w.x, lh);
+                    vc = __builtin_fmaf(xs4[u], w.y, vc);
+                }
+            }
+            const float lx = __shfl_xor(lh, 32, 64);
+            l0 = h ? lx : lh; l1 = h ? lh : lx; vv = vc;
+        } else {
             float pa[3] = {0, 0, 0}, pb[3] = {0, 0, 0};
             const float *hr = B.T + c * WS + 32 * h;
 #pragma unroll
@@ -1680,12 +1737,17 @@ bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_
             return BPPO_ERR_UNSUPPORTED;
         }
         c->slab_used = blocks;
-        // the update's first minibatch runs with the rollout's parameters: the exact
-        // f32 kernel, so the ratio is exactly 1; the others on the split-bf16 kernel
-        // (BPPO_MB_EXACT_ALL=1: the exact kernel for every minibatch, for A/B runs)
+        // the update's first minibatch runs with the rollout's parameters: its forward is the
+        // exact f32 one, so the ratio is exactly 1 -- since r06 the split kernel's exact-forward
+        // variant (k_minibatch_split<true>: the backward on the split-bf16 contraction; was
+        // k_minibatch_mfma, exact throughout); the others on the split-bf16 kernel
+        // (BPPO_MB_EXACT_ALL=1: the exact kernel for every minibatch; BPPO_MB_FIRST_MFMA=1:
+        // k_minibatch_mfma for the first, as r05 -- A/B runs)
         // (bppo_set_minibatch_kernel: 1 = exact for every minibatch, 2 = split for every one)
         static const bool exact_all = getenv("BPPO_MB_EXACT_ALL") != nullptr;
-        const bool use_exact = c->mb_kernel == 1 || (c->mb_kernel == 0 && (exact || exact_all));
+        static const bool first_mfma = getenv("BPPO_MB_FIRST_MFMA") && atoi(getenv("BPPO_MB_FIRST_MFMA")) == 1;
+        const bool use_exact = c->mb_kernel == 1 || (c->mb_kernel == 0 && (exact_all || (exact && first_mfma)));
+        const bool exact_fwd = !use_exact && c->mb_kernel == 0 && exact;
         const size_t lds_split = std::max(mmf::LDS_TILES, (size_t)mmf::WAVES * (c->net.n_params + NUM_M) * sizeof(float));
         // HIP timer events around the launch (bench.py's roofline): every launch by default;
         // BPPO_MB_EVENTS=k times every k-th launch of an update (0: none), for A/B runs of the
@@ -1693,14 +1755,17 @@ bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_
         static const int ev_every = getenv("BPPO_MB_EVENTS") ? atoi(getenv("BPPO_MB_EVENTS")) : 1;
         const bool timed = ev_every > 0 && c->mb_launch++ % ev_every == 0;
         const int ei = timed && c->mb_ev_n < bppo_ctx::MB_EV ? c->mb_ev_n++ : -1;
-        if (ei >= 0) { c->mb_ev_split[ei] = !use_exact; BPPO_HIP(c, hipEventRecord(c->mb_ev[ei][0], c->stream)); }
+        // (the roofline's "exact" share: the update's first minibatch, whichever kernel runs it)
+        if (ei >= 0) { c->mb_ev_split[ei] = !use_exact && !exact_fwd; BPPO_HIP(c, hipEventRecord(c->mb_ev[ei][0], c->stream)); }
         if (use_exact)
             hipLaunchKernelGGL(k_minibatch_mfma, dim3(blocks), dim3(64 * mmb::WAVES), mmb::LDSB, c->stream, g);
+        else if (exact_fwd)
+            hipLaunchKernelGGL(k_minibatch_split<true>, dim3(blocks), dim3(64 * mmf::WAVES), lds_split, c->stream, g);
         else
-            hipLaunchKernelGGL(k_minibatch_split, dim3(blocks), dim3(64 * mmf::WAVES), lds_split, c->stream, g);
+            hipLaunchKernelGGL(k_minibatch_split<false>, dim3(blocks), dim3(64 * mmf::WAVES), lds_split, c->stream, g);
         if (ei >= 0) BPPO_HIP(c, hipEventRecord(c->mb_ev[ei][1], c->stream));
 #ifdef BPPO_MB_STAMPS
-        if (!use_exact || getenv("BPPO_MB_STAMPS_EXACT")) {
+        if ((!use_exact && !exact_fwd) || getenv("BPPO_MB_STAMPS_EXACT")) {
             // mean per-wave cycles per segment of the split launches (the exact kernel's with
             // BPPO_MB_STAMPS_EXACT), accumulated over launches; printed every 16
             static double acc_s[MB_NSEG] = {};

@@ -129,3 +129,23 @@ def test_split_kernel_minibatch_by_minibatch(mode):
     finally:
         tr.close(); ot.close()
 
+
+
+def test_first_minibatch_forward_is_exact():
+    """The update's first minibatch runs with the rollout's parameters, so the reference's
+    ratio is exactly 1 there.  Since r06 it runs k_minibatch_split<true> (the exact f32 forward
+    of k_minibatch_mfma, the split-bf16 backward): every row's new log-prob must equal the
+    stored one bit for bit, i.e. the minibatch's approx_kl sum and clip count are exactly 0
+    (one differing row adds (ratio - 1) - log ratio != 0); the second minibatch, after an Adam
+    step, is not at ratio 1.  CfgB's 4 x 4 schedule at N = 8,192, T = 32."""
+    cfg, tr, ot = cartpole_pair(N, T, init_seed=5)
+    try:
+        _rollout_gae(tr, ot)
+        lr, ent = bppo.schedule_get(cfg["learning_rate"], 0), bppo.schedule_get(cfg["entropy_coef"], 0)
+        bppo.ppo_update(tr.ctx, lr, ent)
+        rows = tr.ctx.minibatch_rows()
+        assert rows[0][10] == N * T // 4
+        assert rows[0][3] == 0.0 and rows[0][4] == 0.0, (rows[0][3], rows[0][4])
+        assert rows[1][3] != 0.0
+    finally:
+        tr.close(); ot.close()
