@@ -52,6 +52,17 @@ bench)
     rc=$?; echo "bench/$rep rc=$rc"; [ $rc -eq 0 ] || { tail -3 gpurun_out/${TAG}_bench_$rep.log; exit $rc; }
     summ gpurun_out/${TAG}_bench_$rep.log
   done ;;
+ab)
+  # interleaved A/B of bench lines: AB_VARIANTS="name|ENV=1 ENV2=x;name2|...", AB_REPS rounds
+  IFS=';' read -ra VS <<< "${AB_VARIANTS:-base|BPPO_NOP=0}"
+  for rep in $(seq 1 ${AB_REPS:-2}); do
+    for v in "${VS[@]}"; do
+      IFS='|' read -r name envs <<< "$v"
+      timeout -k 10 300 env ${envs:-BPPO_NOP=0} python bench.py ${BENCH_FLAGS:---no-cpu-baseline --no-learning} > gpurun_out/${TAG}_ab_${name}_$rep.log 2>&1
+      rc=$?; echo "$name/$rep rc=$rc"; [ $rc -eq 0 ] || { tail -3 gpurun_out/${TAG}_ab_${name}_$rep.log; exit $rc; }
+      summ gpurun_out/${TAG}_ab_${name}_$rep.log
+    done
+  done ;;
 kt)
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/kt_${TAG}_cfgB -o kt -- python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline --no-learning > gpurun_out/kt_${TAG}_cfgB.log 2>&1
   rc=$?; echo "kt cfgB rc=$rc"; [ $rc -eq 0 ] || exit $rc

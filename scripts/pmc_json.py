@@ -37,6 +37,7 @@ KERNELS = {
     "k_gae_1p": ("k_gae.hip", 1.0),
     "k_minibatch_mfma": ("k_update.hip", 1.0),
     "k_minibatch_split": ("k_update.hip", 1.0),
+    "k_minibatch_split_exactfwd": ("k_update.hip", 1.0),   # k_minibatch_split<true> (first minibatch)
     "k_cartpole_rollout_mfma": ("k_rollout.hip", 1.0),
     "k_pack_rows": ("k_update.hip", 1.0),
 }
@@ -50,6 +51,8 @@ def src_sha(fname):
 def short_name(full):
     n = full.split("(")[0]
     n = n.split("::")[-1]
+    if n.startswith("k_minibatch_split<true>"):      # the update's first minibatch (exact forward)
+        return "k_minibatch_split_exactfwd"
     return n.split("<")[0]
 
 
