@@ -332,7 +332,11 @@ __device__ __forceinline__ RowData load_row(const MbArgs &g, uint32_t idx) {
     d.ok = ok;
     if (g.rowA) {                     // one 32-byte sector [obs 0..3][obs 4, action, log-prob, value] + [adv, ret]
         const float4 a = g.rowA[i * 2], b = g.rowA[i * 2 + 1];
+#ifdef BPPO_DIAG_NO_ROWB   // diagnostic build (wrong results): the gather without the second line
+        const float2 c = make_float2(a.x * 0.5f, b.x * 0.25f);
+#else
         const float2 c = g.rowB[i];
+#endif
         d.x0 = a.x; d.x1 = a.y; d.x2 = a.z; d.x3 = a.w;
         d.x4 = b.x; d.a = __float_as_int(b.y); d.olp = b.z; d.ov = b.w;
         d.A = c.x; d.R = c.y;
@@ -765,12 +769,19 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_mfma(MbArgs g) {
 //     (H1^T: units in registers, rows on lanes = layer 2's A fragments, no LDS) and in
 //     the C/D orientation (rows in registers = dW1's A fragments and the relu mask);
 //   heads on the VALU with ILP (lane = row, each lane half over 32 units);
-//   W1 split once per block into two bf16 images: [j1][j2] (dZ1's B fragments) and
-//   [j2][j1] with j1 bits 2 and 3 swapped (layer 2's B fragments, whose k order is the
-//   accumulator's permuted row order), row stride 72 (conflict-free ds_read_b128).
+//   W1 split once per block into ONE bf16 image [j1][j2] (r06; r05 kept a second,
+//   transposed copy): dZ1's B fragments read its rows (ds_read_b128), layer 2's B fragments
+//   -- k = j1 in the accumulator's permuted row order -- its columns through the
+//   transposing ds_read_b64_tr_b16; 128-B rows with the 16-B chunks XOR-swizzled so both
+//   reads are conflict-free (w1_at);
+//   dZ2 split once (r06): its pieces go to a [j2][row] image (Z, over the H2 tile) that
+//   dW1 reads back per lane (B fragments, k = rows) and dZ1 reads transposed (A fragments,
+//   k = j2) -- r05 split the same values twice, once per layout.
 namespace mmf {
-constexpr int H = 64, TR = 32, WS = 68, WPS = 72;
+constexpr int H = 64, TR = 32, WS = 68;
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef short s16x8_t __attribute__((ext_vector_type(8)));
 struct Params {
     uint64_t exp2tab[32];
     double linvc[16], llogc[16];
@@ -779,18 +790,20 @@ struct Params {
     float4 Wh[H];                 // {wp0, wp1, wv, 0} per hidden unit
     float bp[2], bv[2];
     float2 PV[2][H];              // exact heads: {Wp[2k + h], Wv[k]} per lane half h (k_minibatch_mfma's pairs)
-    __bf16 W1n[3][H * WPS];       // W1 pieces [j1][j2]
-    union {
-        __bf16 W1t[3][H * WPS];   // W1 pieces [j2][perm(j1)] (the split forward)
-        float W1f[H * H];         // W1 [j1][j2] in f32 (the exact forward of the update's first minibatch)
-    };
+    __bf16 W1[3][H * H];          // W1 pieces [j1][j2], chunks swizzled (w1_at)
     __device__ __forceinline__ float expf(float x) const { return bppo_math::expf_glibc_tab(x, exp2tab); }
     __device__ __forceinline__ float logf(float x) const { return bppo_math::logf_glibc_tab(x, linvc, llogc); }
 };
 constexpr int MET_STRIDE = 20;
+// EXACT_FWD (the update's first minibatch) keeps dZ2 in f32 in the tile and splits it per
+// use (its f32 W1 copy for the exact layer 2 leaves no LDS for the piece image)
+template <bool EXACT_FWD>
 struct Wave {
     float X[TR * 5];
-    float T[TR * WS];             // H2, then dZ2 [row][j2]
+    union {
+        float T[TR * WS];             // H2, then (EXACT_FWD) dZ2 [row][j2]
+        __bf16 Z[EXACT_FWD ? 4 : 3 * H * TR];   // dZ2 pieces [j2][row], chunks swizzled (z_at)
+    };
     float dl[TR * 4];
     // per row lane: the metric sums and head-bias gradients (MT_*); row stride 20 floats,
     // not 16: lanes c and c+4 of a b128 access then fall in different bank groups
@@ -799,9 +812,33 @@ struct Wave {
 };
 enum { MT_PL = 0, MT_VL, MT_H, MT_KL, MT_CF, MT_V, MT_R, MT_VE, MT_VE2, MT_VEMAX, MT_N, MT_BP0, MT_BP1, MT_BV };
 constexpr int WAVES = 8;
-constexpr size_t LDS_TILES = sizeof(Params) + WAVES * sizeof(Wave);
-static_assert(LDS_TILES <= 160 * 1024, "split minibatch kernel LDS over the gfx950 limit");
-__device__ __forceinline__ int perm_j1(int j) { return (j & ~12) | ((j & 4) << 1) | ((j & 8) >> 1); }
+constexpr size_t W1F_BYTES = H * H * sizeof(float);   // EXACT_FWD: W1 in f32 after Params
+template <bool EXACT_FWD>
+constexpr size_t lds_tiles() { return sizeof(Params) + (EXACT_FWD ? W1F_BYTES : 0) + WAVES * sizeof(Wave<EXACT_FWD>); }
+static_assert(lds_tiles<false>() <= 160 * 1024 && lds_tiles<true>() <= 160 * 1024,
+              "split minibatch kernel LDS over the gfx950 limit");
+static_assert(sizeof(Params) % 16 == 0 && offsetof(Params, W1) % 16 == 0 && sizeof(Wave<false>) % 16 == 0 &&
+              sizeof(Wave<true>) % 16 == 0, "LDS images 16-B aligned");
+// W1 image: 16-B chunk k of row j1 stored at chunk k ^ w1_swz(j1), w1_swz a bijection of
+// bits 1-3 of j1.  Row reads (dZ1, ds_read_b128: 16 lanes j1, one chunk) then land on
+// (j1 & 1, chunk) pairs that differ within each lane group; the transposed reads (layer 2:
+// rows j1 .. j1+3, j1 = 0 mod 4, 32 columns per lane half) put rows j1 and j1+2 in
+// different 64-B halves of the bank space (bit 2 of the swizzle = bit 1 of j1)
+__device__ __forceinline__ int w1_swz(int j1) { return (((j1 >> 1) & 1) << 2) | (((j1 >> 2) & 1) << 1) | ((j1 >> 3) & 1); }
+__device__ __forceinline__ int w1_at(int j1, int j2) { return j1 * H + ((((j2 >> 3) ^ w1_swz(j1)) << 3) | (j2 & 7)); }
+// Z image: [j2][row] rows of 64 B, 8-B chunk k (rows 4k .. 4k+3) stored at k ^ z_swz(j2):
+// conflict-free for the ds_write_b64 stores (16 lanes j2, one chunk), the per-lane
+// ds_read_b64 reads (32 lanes j2) and the transposed reads (4 rows j2 x 32 columns)
+__device__ __forceinline__ int z_swz(int j2) { return ((j2 >> 2) & 7) ^ (((j2 >> 1) & 1) << 2); }
+__device__ __forceinline__ int z_at(int j2, int row) { return j2 * TR + ((((row >> 2) ^ z_swz(j2)) << 2) | (row & 3)); }
+// ds_read_b64_tr_b16: lane 4q + p of each 16-lane group addresses row q, columns 4p .. 4p+3
+// of a 4 x 16 block; lane i receives column i, row q in element q
+__device__ __forceinline__ s16x4_t lds_tr4(const __bf16 *p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t *)p);
+}
+__device__ __forceinline__ bf16x8_t cat8(s16x4_t lo, s16x4_t hi) {
+    return __builtin_bit_cast(bf16x8_t, (s16x8_t)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
 struct Split8 { bf16x8_t p[3]; };
 // exact three-piece split of 8 f32 values, a pair at a time: one v_cvt_pk_bf16_f32 per
 // piece pair, the pieces' f32 values taken back from the packed word (<< 16, & 0xffff0000)
@@ -856,29 +893,40 @@ __device__ __forceinline__ void mfma6(f32x16_t &acc, const Split8 &a, const Spli
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[1], acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[0], acc, 0, 0, 0);
 }
-__device__ __forceinline__ Split8 load_pieces(const __bf16 (*img)[H * WPS], int off) {
+// dZ1's B fragment: W1[j1][j2 .. j2+7] (j2 = 0 mod 8), one ds_read_b128 per piece
+__device__ __forceinline__ Split8 w1_row_pieces(const __bf16 (*W1)[H * H], int j1, int j2) {
+    Split8 s;
+    const int off = w1_at(j1, j2);
+#pragma unroll
+    for (int p = 0; p < 3; p++) s.p[p] = *reinterpret_cast<const bf16x8_t *>(W1[p] + off);
+    return s;
+}
+// layer 2's B fragment: W1[j1 + 8e + q][j2] for e = 0, 1 and q = 0..3 (elements 4e + q),
+// two transposed reads per piece; off[e] = the lane's offset of its block row (tr_off)
+__device__ __forceinline__ Split8 w1_tr_pieces(const __bf16 (*W1)[H * H], int base, const int (&off)[2]) {
     Split8 s;
 #pragma unroll
-    for (int p = 0; p < 3; p++) s.p[p] = *reinterpret_cast<const bf16x8_t *>(img[p] + off);
+    for (int p = 0; p < 3; p++) s.p[p] = cat8(lds_tr4(W1[p] + base + off[0]), lds_tr4(W1[p] + base + off[1]));
     return s;
 }
 template <bool EXACT_FWD>
-__device__ __forceinline__ void load_params_split(Params &S, const float *__restrict__ P) {
+__device__ __forceinline__ void load_params_split(Params &S, float *W1f, const float *__restrict__ P) {
     constexpr CpOffsets O = cp_offsets<64, 2>();
     for (int i = threadIdx.x; i < 6 * H; i += blockDim.x) S.W0[i] = i < 5 * H ? P[O.w0 + i] : P[O.b0 + i - 5 * H];
-    for (int i = threadIdx.x; i < H * H; i += blockDim.x) {
-        const int j1 = i / H, j2 = i % H;
-        const float w = P[O.w1 + i];                 // W1 [in = j1][out = j2]
-        const __bf16 a = (__bf16)w;
-        const float r = w - (float)a;
-        const __bf16 b = (__bf16)r;
-        const __bf16 c = (__bf16)(r - (float)b);
-        S.W1n[0][j1 * WPS + j2] = a; S.W1n[1][j1 * WPS + j2] = b; S.W1n[2][j1 * WPS + j2] = c;
+    // W1 [in = j1][out = j2]: one 8-value chunk per thread, split and stored as three 16-B
+    // pieces (r05: 2-B stores into two images, 1.37 M bank-conflict cycles per launch)
+    for (int t = threadIdx.x; t < H * H / 8; t += blockDim.x) {
+        const int j1 = t >> 3, j2 = (t & 7) * 8;
+        float w[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) w[j] = P[O.w1 + 8 * t + j];
+        const Split8 sp = split8(w);
+        const int off = w1_at(j1, j2);
+#pragma unroll
+        for (int p = 0; p < 3; p++) *reinterpret_cast<bf16x8_t *>(S.W1[p] + off) = sp.p[p];
         if (EXACT_FWD) {
-            S.W1f[i] = w;
-        } else {
-            const int t = j2 * WPS + perm_j1(j1);
-            S.W1t[0][t] = a; S.W1t[1][t] = b; S.W1t[2][t] = c;
+#pragma unroll
+            for (int j = 0; j < 8; j++) W1f[8 * t + j] = w[j];
         }
     }
     for (int i = threadIdx.x; i < H; i += blockDim.x) {
@@ -912,9 +960,10 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
     constexpr CpOffsets O = cp_offsets<64, 2>();
     extern __shared__ __attribute__((aligned(16))) float smem[];
     Params &S = *reinterpret_cast<Params *>(smem);
+    float *W1f = smem + sizeof(Params) / 4;          // EXACT_FWD only
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    Wave &B = reinterpret_cast<Wave *>(smem + sizeof(Params) / 4)[wv];
-    load_params_split<EXACT_FWD>(S, g.params);
+    Wave<EXACT_FWD> &B = reinterpret_cast<Wave<EXACT_FWD> *>(smem + (sizeof(Params) + (EXACT_FWD ? W1F_BYTES : 0)) / 4)[wv];
+    load_params_split<EXACT_FWD>(S, W1f, g.params);
     __syncthreads();
 #ifdef BPPO_MB_STAMPS
     unsigned long long st_acc[MB_NSEG] = {}, st_prev;
@@ -924,6 +973,16 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
     const int c = lane & 31, h = lane >> 5;
     const int gwave = blockIdx.x * WAVES + wv, nwaves = gridDim.x * WAVES;
     const float mean = g.mb_stats[0], denom = g.mb_stats[1] + 1e-8f;
+    // transposed reads: lane 4q + p of its 16-lane group (column block gq = bit 4 of the lane)
+    // layer 2: W1 rows 4h + 8e + q (+ 32 it + 16 s2), columns 32 ct + 16 gq + 4p
+    int w1tr[2][2];
+    {
+        const int q = (lane >> 2) & 3, p = lane & 3, gq = (lane >> 4) & 1;
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++)
+#pragma unroll
+            for (int e = 0; e < 2; e++) w1tr[ct][e] = w1_at(4 * h + 8 * e + q, 32 * ct + 16 * gq + 4 * p);
+    }
     f32x16_t dW1[2][2];
 #pragma unroll
     for (int i = 0; i < 2; i++)
@@ -1010,7 +1069,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
                 const Split8 Af = split8(v8);
 #pragma unroll
                 for (int ct = 0; ct < 2; ct++)
-                    mfma6(h2[ct], Af, load_pieces(S.W1t, (c + 32 * ct) * WPS + 32 * it + 16 * s2 + 8 * h));
+                    mfma6(h2[ct], Af, w1_tr_pieces(S.W1, (32 * it + 16 * s2) * H, w1tr[ct]));
                 __builtin_amdgcn_sched_barrier(0);   // bound the piece-load hoisting (registers)
             }
         }
@@ -1020,7 +1079,7 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
 #pragma unroll 4
             for (int s = 0; s < 32; s++) {
                 const float av = B.T[(2 * s + h) * TR + c];
-                const float bv0 = S.W1f[(2 * s + h) * H + c], bv1 = S.W1f[(2 * s + h) * H + c + 32];
+                const float bv0 = W1f[(2 * s + h) * H + c], bv1 = W1f[(2 * s + h) * H + c + 32];
                 h2[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv0, h2[0], 0, 0, 0);
                 h2[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv1, h2[1], 0, 0, 0);
             }
@@ -1163,17 +1222,47 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
                 acc[ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, h ? 0.0f : w.z, acc[ct], 0, 0, 0);
             }
         }
-        // dZ2 = that * [H2 > 0]: kept in registers (dW1's B fragments) and written over H2
+        // dZ2 = that * [H2 > 0]
+        if (EXACT_FWD) {
+            // written over H2 in f32, split per use below
 #pragma unroll
-        for (int q = 0; q < 16; q++) {
+            for (int q = 0; q < 16; q++) {
 #pragma unroll
-            for (int ct = 0; ct < 2; ct++) {
-                const int ad = cd_row(q, h) * WS + c + 32 * ct;
-                const float dz = B.T[ad] > 0.0f ? acc[ct][q] : 0.0f;
-                gb1[ct] += dz;
-                B.T[ad] = dz;
+                for (int ct = 0; ct < 2; ct++) {
+                    const int ad = cd_row(q, h) * WS + c + 32 * ct;
+                    const float dz = B.T[ad] > 0.0f ? acc[ct][q] : 0.0f;
+                    gb1[ct] += dz;
+                    B.T[ad] = dz;
+                }
+                if ((q & 3) == 3) __builtin_amdgcn_sched_barrier(0);
             }
-            if ((q & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 16; q++)
+#pragma unroll
+                for (int ct = 0; ct < 2; ct++) {
+                    acc[ct][q] = B.T[cd_row(q, h) * WS + c + 32 * ct] > 0.0f ? acc[ct][q] : 0.0f;
+                    gb1[ct] += acc[ct][q];
+                }
+            wave_sync();    // every lane's H2 reads before the piece image overwrites the tile
+            // split once: this lane's column j2 = c + 32 t, rows cd_row(8 s2 + j, h) -> the
+            // [j2][row] image, 8 B (rows 16 s2 + 8e + 4h .. +3) per piece and half e
+#pragma unroll
+            for (int s2 = 0; s2 < 2; s2++)
+#pragma unroll
+                for (int t = 0; t < 2; t++) {
+                    float z[8];
+#pragma unroll
+                    for (int j = 0; j < 8; j++) z[j] = acc[t][8 * s2 + j];
+                    const Split8 P = split8(z);
+#pragma unroll
+                    for (int p = 0; p < 3; p++) {
+                        const uint4 u = __builtin_bit_cast(uint4, P.p[p]);
+                        *reinterpret_cast<uint2 *>(B.Z + p * H * TR + z_at(c + 32 * t, 16 * s2 + 4 * h)) = make_uint2(u.x, u.y);
+                        *reinterpret_cast<uint2 *>(B.Z + p * H * TR + z_at(c + 32 * t, 16 * s2 + 8 + 4 * h)) = make_uint2(u.z, u.w);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
         }
         MB_STAMP(5);   // head gradients, dZ2
         __builtin_amdgcn_s_setprio(3);
@@ -1206,10 +1295,20 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
             Split8 Bz[2];
 #pragma unroll
             for (int t = 0; t < 2; t++) {
-                float z[8];      // this lane's own dZ2 elements, back from the tile
+                if (EXACT_FWD) {
+                    float z[8];      // this lane's own dZ2 elements, back from the tile
 #pragma unroll
-                for (int j = 0; j < 8; j++) z[j] = B.T[cd_row(8 * s2 + j, h) * WS + c + 32 * t];
-                Bz[t] = split8(z);
+                    for (int j = 0; j < 8; j++) z[j] = B.T[cd_row(8 * s2 + j, h) * WS + c + 32 * t];
+                    Bz[t] = split8(z);
+                } else {
+                    // this lane's own pieces, back from the image
+#pragma unroll
+                    for (int p = 0; p < 3; p++) {
+                        const uint2 lo = *reinterpret_cast<const uint2 *>(B.Z + p * H * TR + z_at(c + 32 * t, 16 * s2 + 4 * h));
+                        const uint2 hi = *reinterpret_cast<const uint2 *>(B.Z + p * H * TR + z_at(c + 32 * t, 16 * s2 + 8 + 4 * h));
+                        Bz[t].p[p] = __builtin_bit_cast(bf16x8_t, make_uint4(lo.x, lo.y, hi.x, hi.y));
+                    }
+                }
             }
 #pragma unroll
             for (int it = 0; it < 2; it++) {
@@ -1232,13 +1331,24 @@ __global__ void __launch_bounds__(512, 2) k_minibatch_split(MbArgs g) {
             for (int q = 0; q < 16; q++) dz1[ct][q] = 0.0f;
 #pragma unroll
         for (int ks = 0; ks < 4; ks++) {
-            const float *zr = B.T + c * WS + 16 * ks + 8 * h;
-            const float4 z0 = *reinterpret_cast<const float4 *>(zr), z1 = *reinterpret_cast<const float4 *>(zr + 4);
-            const float zz[8] = {z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w};
-            const Split8 Az = split8(zz);
+            Split8 Az;
+            if (EXACT_FWD) {
+                const float *zr = B.T + c * WS + 16 * ks + 8 * h;
+                const float4 z0 = *reinterpret_cast<const float4 *>(zr), z1 = *reinterpret_cast<const float4 *>(zr + 4);
+                const float zz[8] = {z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w};
+                Az = split8(zz);
+            } else {
+                // transposed: lane 4q + p of its group reads j2 = 16 ks + 8h + 4e + q, rows
+                // 16 gq + 4p .. +3; lane c receives row c, element 4e + q
+                const int q = (lane >> 2) & 3, pp = lane & 3, gq = (lane >> 4) & 1;
+#pragma unroll
+                for (int p = 0; p < 3; p++)
+                    Az.p[p] = cat8(lds_tr4(B.Z + p * H * TR + z_at(16 * ks + 8 * h + q, 16 * gq + 4 * pp)),
+                                   lds_tr4(B.Z + p * H * TR + z_at(16 * ks + 8 * h + 4 + q, 16 * gq + 4 * pp)));
+            }
 #pragma unroll
             for (int ct = 0; ct < 2; ct++)
-                mfma6(dz1[ct], Az, load_pieces(S.W1n, (c + 32 * ct) * WPS + 16 * ks + 8 * h));
+                mfma6(dz1[ct], Az, w1_row_pieces(S.W1, c + 32 * ct, 16 * ks + 8 * h));
             __builtin_amdgcn_sched_barrier(0);
         }
         __builtin_amdgcn_s_setprio(0);
@@ -1748,7 +1858,9 @@ bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_
         static const bool first_mfma = getenv("BPPO_MB_FIRST_MFMA") && atoi(getenv("BPPO_MB_FIRST_MFMA")) == 1;
         const bool use_exact = c->mb_kernel == 1 || (c->mb_kernel == 0 && (exact_all || (exact && first_mfma)));
         const bool exact_fwd = !use_exact && c->mb_kernel == 0 && exact;
-        const size_t lds_split = std::max(mmf::LDS_TILES, (size_t)mmf::WAVES * (c->net.n_params + NUM_M) * sizeof(float));
+        const size_t lds_rows = (size_t)mmf::WAVES * (c->net.n_params + NUM_M) * sizeof(float);
+        const size_t lds_split = std::max(mmf::lds_tiles<false>(), lds_rows);
+        const size_t lds_split_x = std::max(mmf::lds_tiles<true>(), lds_rows);
         // HIP timer events around the launch (bench.py's roofline): every launch by default;
         // BPPO_MB_EVENTS=k times every k-th launch of an update (0: none), for A/B runs of the
         // timestamp markers' cost on the stream
@@ -1760,7 +1872,7 @@ bppo_status launch_minibatch(bppo_ctx *c, uint32_t start, uint32_t n, float ent_
         if (use_exact)
             hipLaunchKernelGGL(k_minibatch_mfma, dim3(blocks), dim3(64 * mmb::WAVES), mmb::LDSB, c->stream, g);
         else if (exact_fwd)
-            hipLaunchKernelGGL(k_minibatch_split<true>, dim3(blocks), dim3(64 * mmf::WAVES), lds_split, c->stream, g);
+            hipLaunchKernelGGL(k_minibatch_split<true>, dim3(blocks), dim3(64 * mmf::WAVES), lds_split_x, c->stream, g);
         else
             hipLaunchKernelGGL(k_minibatch_split<false>, dim3(blocks), dim3(64 * mmf::WAVES), lds_split, c->stream, g);
         if (ei >= 0) BPPO_HIP(c, hipEventRecord(c->mb_ev[ei][1], c->stream));

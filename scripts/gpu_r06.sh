@@ -5,6 +5,8 @@
 #   bash scripts/gpu_r06.sh bench TAG     default CfgB bench line(s) (BENCH_REPS, BENCH_FLAGS, BENCH_ENV)
 #   bash scripts/gpu_r06.sh kt TAG        rocprofv3 kernel trace of the CfgB bench line
 #   bash scripts/gpu_r06.sh pmc TAG       PMC passes on the CfgB bench (scripts/pmc_traffic.sh)
+#   bash scripts/gpu_r06.sh ab TAG        interleaved bench lines under env variants (AB_VARIANTS, AB_REPS)
+#   bash scripts/gpu_r06.sh mbstamp TAG   split minibatch kernel segment stamps (libbppo_stamps.so)
 set -u
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
@@ -71,5 +73,9 @@ kt)
   head -24 gpurun_out/${TAG}_cfgB_kernels.txt | cut -c1-140 ;;
 pmc)
   bash scripts/pmc_traffic.sh $TAG ;;
+mbstamp)
+  # split minibatch kernel segment stamps (diagnostic build burn-ppo_amd/bppo/libbppo_stamps.so)
+  timeout -k 10 300 env BPPO_LIB_PATH=$GRAFT_REPO_ROOT/burn-ppo_amd/bppo/libbppo_stamps.so python bench.py --steps 6 --warmup 1 --no-learning --no-cpu-baseline --no-gae-isolated > gpurun_out/${TAG}_mbstamps.log 2>&1
+  rc=$?; echo "mbstamp rc=$rc"; grep mbstamp gpurun_out/${TAG}_mbstamps.log | tail -2; exit $rc ;;
 *) echo "unknown part $PART"; exit 2 ;;
 esac
