@@ -330,6 +330,9 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
         BPPO_HIP(c, make_side_stream(dev, &c->fy_stream));
         for (int e = 0; e < cfg->num_epochs && e < SHUF_MAX_EPOCHS; e++)
             BPPO_HIP(c, hipEventCreateWithFlags(&c->fy_ev[e], hipEventDisableTiming));
+        BPPO_HIP(c, make_side_stream(dev, &c->prep_stream));
+        BPPO_HIP(c, hipEventCreateWithFlags(&c->ev_env, hipEventDisableTiming));
+        BPPO_HIP(c, hipEventCreateWithFlags(&c->ev_prep, hipEventDisableTiming));
     }
     TRY(dalloc(c, &c->d_fy, 4 * TN));
     TRY(dalloc(c, &c->d_scan, TN / 8192 + 2));
@@ -395,6 +398,7 @@ extern "C" void bppo_destroy(bppo_ctx *c) {
     if (c->ev_copied) (void)hipEventDestroy(c->ev_copied);
     for (float *h : {c->h_ev_v, c->h_ev_r, c->h_ev_valid}) if (h) (void)hipHostFree(h);
     if (c->fy_stream) (void)hipStreamSynchronize(c->fy_stream);   // reads the engine's J buffers
+    if (c->prep_stream) (void)hipStreamSynchronize(c->prep_stream);
     c->shuf.shutdown();
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     wide_free(c);
@@ -419,6 +423,8 @@ extern "C" void bppo_destroy(bppo_ctx *c) {
         for (hipEvent_t e : pr) if (e) (void)hipEventDestroy(e);
     if (c->fy_stream) { (void)hipStreamSynchronize(c->fy_stream); (void)hipStreamDestroy(c->fy_stream); }
     for (hipEvent_t e : c->fy_ev) if (e) (void)hipEventDestroy(e);
+    if (c->prep_stream) (void)hipStreamDestroy(c->prep_stream);
+    for (hipEvent_t e : {c->ev_env, c->ev_prep}) if (e) (void)hipEventDestroy(e);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }

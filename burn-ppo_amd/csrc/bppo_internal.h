@@ -320,6 +320,11 @@ struct bppo_ctx {
     double *d_advpart = nullptr;      // k_adv_stream block partials
     hipStream_t fy_stream = nullptr;
     hipEvent_t fy_ev[bppo::SHUF_MAX_EPOCHS] = {};
+    // CfgB 64-lane rollout: its Gumbel words and reset pool made on prep_stream as soon as the
+    // previous env-state writer (ev_env: the last rollout / reset / vecenv step) finished, i.e.
+    // beside the previous update's minibatches, not between them and the rollout (r06)
+    hipStream_t prep_stream = nullptr;
+    hipEvent_t ev_env = nullptr, ev_prep = nullptr;
     int fy_slot = -1, fy_done = 0;    // engine slot whose epochs [0, fy_done) are enqueued on fy_stream
     uint32_t *d_fy = nullptr;         // Fisher-Yates scratch [4][TN]: count/offset, bucket, succ, fw
     uint32_t *d_scan = nullptr;       // scan block sums

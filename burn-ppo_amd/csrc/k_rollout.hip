@@ -962,11 +962,21 @@ bppo_status launch_cartpole_reset(bppo_ctx *c) {
                        c->cfg.env_seed_base, c->d_cp, c->d_steps, c->d_env_pos, c->d_ep_ret,
                        c->d_ep_len, nullptr);
     TRY(launch_check(c, __func__));
+    if (c->ev_env) BPPO_HIP(c, hipEventRecord(c->ev_env, c->stream));   // env state written
     return BPPO_OK;
 }
 
+static bppo_status launch_cartpole_rollout_kernels(bppo_ctx *c, uint64_t base_pos, int norm_on);
+// every CartPole rollout variant, then ev_env: the env state it wrote (and the 64-lane
+// kernel's Gumbel words / reset pool it read) -- what the next rollout's prep_stream waits for
 bppo_status launch_cartpole_rollout(bppo_ctx *c, uint64_t base_pos, const double *, const double *,
                                     int norm_on) {
+    const bppo_status s = launch_cartpole_rollout_kernels(c, base_pos, norm_on);
+    if (s == BPPO_OK && c->ev_env) BPPO_HIP(c, hipEventRecord(c->ev_env, c->stream));
+    return s;
+}
+
+static bppo_status launch_cartpole_rollout_kernels(bppo_ctx *c, uint64_t base_pos, int norm_on) {
     const int h = c->cfg.hidden_size, nl = c->cfg.num_hidden;
     if (!cp_supported(h, nl)) {
         c->err = "CartPole rollout kernel supports MLPs with hidden in {16,32,64} x {1,2} layers";
@@ -995,13 +1005,22 @@ bppo_status launch_cartpole_rollout(bppo_ctx *c, uint64_t base_pos, const double
         // Gumbel noise for every (t, env, action) first, then the MFMA rollout
         const uint64_t count = (uint64_t)c->T * c->N * 2;
         const uint64_t blocks = ((base_pos + count + 15) >> 4) - (base_pos >> 4);
-        hipLaunchKernelGGL(k_gumbel_words, dim3((unsigned)((blocks + 255) / 256)), dim3(256), 0, c->stream, c->rng_key,
+        const bool lanes64 = !(getenv("BPPO_ROLLOUT_LANES64") && atoi(getenv("BPPO_ROLLOUT_LANES64")) == 0);
+        // r06: the 64-lane rollout's inputs (Gumbel words, reset pool) on prep_stream, which
+        // waits only for the last env-state writer (the previous rollout): they run beside the
+        // previous update instead of between its last minibatch and this rollout
+        // (BPPO_PREP_SIDE=0: on the update stream, as r05)
+        static const bool prep_side = !(getenv("BPPO_PREP_SIDE") && atoi(getenv("BPPO_PREP_SIDE")) == 0);
+        const bool side = lanes64 && prep_side && c->prep_stream && c->ev_env && c->ev_prep;
+        hipStream_t ps = side ? c->prep_stream : c->stream;
+        if (side) BPPO_HIP(c, hipStreamWaitEvent(ps, c->ev_env, 0));
+        hipLaunchKernelGGL(k_gumbel_words, dim3((unsigned)((blocks + 255) / 256)), dim3(256), 0, ps, c->rng_key,
                            (uint64_t)c->cfg.rng_stream, base_pos, count, c->d_gumbel);
+        TRY(launch_check(c, "k_gumbel_words"));
         // default: the 64-lane kernel (269 registers and 84 KB of LDS per 4-wave block, so
         // the side-stream Fisher-Yates passes still share its CUs): device-bound A/B
         // 0.1-0.28 ms/update faster than r03's half-wave kernel (profiles/r04_rollout/
         // rollout_ab.txt).  BPPO_ROLLOUT_LANES64=0: the half-wave kernel.
-        const bool lanes64 = !(getenv("BPPO_ROLLOUT_LANES64") && atoi(getenv("BPPO_ROLLOUT_LANES64")) == 0);
         if (!lanes64) {
             const int waves = (c->N + mmb::TR - 1) / mmb::TR;
             hipLaunchKernelGGL(k_cartpole_rollout_mfma, dim3((waves + mmb::WAVES - 1) / mmb::WAVES), dim3(64 * mmb::WAVES),
@@ -1012,7 +1031,7 @@ bppo_status launch_cartpole_rollout(bppo_ctx *c, uint64_t base_pos, const double
             int pk = RPOOL_K;
             if (const char *v = getenv("BPPO_RESET_POOL_K")) pk = std::max(0, std::min(RPOOL_K, atoi(v)));
             if (c->d_rpool && pk > 0) {
-                hipLaunchKernelGGL(k_reset_pool, dim3((c->N + 255) / 256), dim3(256), 0, c->stream, c->N, pk,
+                hipLaunchKernelGGL(k_reset_pool, dim3((c->N + 255) / 256), dim3(256), 0, ps, c->N, pk,
                                    c->cfg.env_seed_base, (const uint64_t *)c->d_env_pos, c->d_rpool, c->d_rpos);
                 TRY(launch_check(c, "k_reset_pool"));
                 a.rpool = c->d_rpool; a.rpos = c->d_rpos; a.rpool_k = pk;
@@ -1022,6 +1041,10 @@ bppo_status launch_cartpole_rollout(bppo_ctx *c, uint64_t base_pos, const double
             if (!d_st) BPPO_HIP(c, hipMalloc((void **)&d_st, sizeof(unsigned long long) * (size_t)waves * RO_NSEG));
             a.stamps = d_st;
 #endif
+            if (side) {
+                BPPO_HIP(c, hipEventRecord(c->ev_prep, ps));
+                BPPO_HIP(c, hipStreamWaitEvent(c->stream, c->ev_prep, 0));
+            }
             hipLaunchKernelGGL(k_cartpole_rollout_mfma64, dim3((waves + mmr::WAVES - 1) / mmr::WAVES),
                                dim3(64 * mmr::WAVES), 0, c->stream, a, (const float *)c->d_gumbel);
 #ifdef BPPO_RO_STAMPS
@@ -1087,6 +1110,7 @@ bppo_status launch_cartpole_vecenv_step(bppo_ctx *c, const int32_t *d_actions, f
                        c->d_ep_len, d_actions, d_rew, d_done, d_obs_out, c->d_eps, c->d_ep_count,
                        c->eps_cap);
     TRY(launch_check(c, __func__));
+    if (c->ev_env) BPPO_HIP(c, hipEventRecord(c->ev_env, c->stream));   // env state written
     return BPPO_OK;
 }
 
