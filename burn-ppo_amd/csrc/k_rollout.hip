@@ -1006,11 +1006,13 @@ static bppo_status launch_cartpole_rollout_kernels(bppo_ctx *c, uint64_t base_po
         const uint64_t count = (uint64_t)c->T * c->N * 2;
         const uint64_t blocks = ((base_pos + count + 15) >> 4) - (base_pos >> 4);
         const bool lanes64 = !(getenv("BPPO_ROLLOUT_LANES64") && atoi(getenv("BPPO_ROLLOUT_LANES64")) == 0);
-        // r06: the 64-lane rollout's inputs (Gumbel words, reset pool) on prep_stream, which
-        // waits only for the last env-state writer (the previous rollout): they run beside the
-        // previous update instead of between its last minibatch and this rollout
-        // (BPPO_PREP_SIDE=0: on the update stream, as r05)
-        static const bool prep_side = !(getenv("BPPO_PREP_SIDE") && atoi(getenv("BPPO_PREP_SIDE")) == 0);
+        // BPPO_PREP_SIDE=1 (r06, A/B): the 64-lane rollout's inputs (Gumbel words, reset pool)
+        // on prep_stream, which waits only for the last env-state writer (the previous
+        // rollout), so they run beside the previous update instead of between its last
+        // minibatch and this rollout.  Kernel traces: the gap before the rollout 285-607 ->
+        // 121-295 us, but the update's minibatches 0.2-0.45 ms longer beside them (update span
+        // 11.04 / 12.39 vs 11.36 / 12.24 ms, profiles/r06p/): off by default
+        static const bool prep_side = getenv("BPPO_PREP_SIDE") && atoi(getenv("BPPO_PREP_SIDE")) == 1;
         const bool side = lanes64 && prep_side && c->prep_stream && c->ev_env && c->ev_prep;
         hipStream_t ps = side ? c->prep_stream : c->stream;
         if (side) BPPO_HIP(c, hipStreamWaitEvent(ps, c->ev_env, 0));
