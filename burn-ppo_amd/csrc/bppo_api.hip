@@ -319,7 +319,7 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     c->eps_cap = (int)std::min<size_t>((size_t)c->T * c->N + 4096, (size_t)INT32_MAX / 2);
     TRY(dalloc(c, &c->d_eps, (size_t)c->eps_cap));
     TRY(dalloc(c, &c->d_ep_count, 1));
-    TRY(dalloc(c, &c->d_ep_sum, 2 * EP_SUMMARY_BLOCKS));
+    TRY(dalloc(c, &c->d_ep_sum, ROLL_HOST_WORDS));   // [count, err] + the partial sums: one host slot's layout
     TRY(dalloc(c, &c->d_err, 1));
     TRY(dalloc(c, &c->d_perm_base, TN));
     c->d_perm = c->d_perm_base;
@@ -351,6 +351,7 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     }
     BPPO_HIP(c, hipHostMalloc((void **)&c->h_red, sizeof(double) * (4 * 1024 + 64 + 2 * ROLL_HOST_WORDS),
                               hipHostMallocDefault));   // + two slots of the rollout's flags and episode partials
+    BPPO_HIP(c, hipHostGetDevicePointer((void **)&c->hd_red, c->h_red, 0));
     BPPO_HIP(c, hipEventCreateWithFlags(&c->ev_upd, hipEventDisableTiming));
     BPPO_HIP(c, hipEventRecord(c->ev_upd, c->stream));      // recorded once, so every wait on it is defined
     BPPO_HIP(c, hipEventCreateWithFlags(&c->ev_block, hipEventDisableTiming | hipEventBlockingSync));
@@ -774,8 +775,12 @@ static bppo_status collect_enqueue(bppo_ctx *c, bool summary) {
     const size_t TN = (size_t)c->T * c->N;
     c->coll_slot ^= 1;
     const int tro = c->coll_slot ? TM_ROLLOUT_B : TM_ROLLOUT, trn = c->coll_slot ? TM_RETNORM_B : TM_RETNORM;
-    BPPO_HIP(c, hipMemsetAsync(c->d_ep_count, 0, 4, c->stream));
-    BPPO_HIP(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
+    // the episode counter and error flags start at 0: zeroed here for the wide envs, by the
+    // CartPole launcher (in its Gumbel kernel where that runs on the update stream)
+    if (c->wide) {
+        BPPO_HIP(c, hipMemsetAsync(c->d_ep_count, 0, 4, c->stream));
+        BPPO_HIP(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
+    }
     const uint64_t base = c->rng_pos;
     TRY(tm_begin(c, tro));
     if (c->wide) TRY(wide_collect(c, base));
@@ -805,13 +810,22 @@ static bppo_status collect_enqueue(bppo_ctx *c, bool summary) {
     if (c->cfg.normalize_returns) TRY(launch_return_norm(c));      // ppo.rs:390-408
     else if (!c->wide) BPPO_HIP(c, hipMemcpyAsync(c->d_rew, c->d_rew_raw, TN * 4, hipMemcpyDeviceToDevice, c->stream));
     TRY(tm_end(c, trn));
-    if (summary) TRY(launch_episode_summary(c));
-    int32_t *hv = reinterpret_cast<int32_t *>(roll_host(c, c->coll_slot));     // pinned: truly async copies
-    double *part = roll_host(c, c->coll_slot) + 2;
-    BPPO_HIP(c, hipMemcpyAsync(&hv[0], c->d_ep_count, 4, hipMemcpyDeviceToHost, c->stream));
-    BPPO_HIP(c, hipMemcpyAsync(&hv[1], c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
-    if (summary) BPPO_HIP(c, hipMemcpyAsync(part, c->d_ep_sum, sizeof(double) * 2 * EP_SUMMARY_BLOCKS,
-                                            hipMemcpyDeviceToHost, c->stream));
+    int32_t *hv = reinterpret_cast<int32_t *>(roll_host(c, c->coll_slot));     // pinned
+    if (summary) {
+        // the summary kernel writes the episode count, the error flags and its partial sums in
+        // the host slot's layout: into d_ep_sum and ONE copy (r05: three), or with
+        // BPPO_ZERO_COPY=1 straight into the pinned slot (A/B: slower, gaps after the kernels
+        // that write host memory -- profiles/r06t/)
+        if (zero_copy()) {
+            TRY(launch_episode_summary(c, c->hd_red + (roll_host(c, c->coll_slot) - c->h_red)));
+        } else {
+            TRY(launch_episode_summary(c, c->d_ep_sum));
+            BPPO_HIP(c, hipMemcpyAsync(hv, c->d_ep_sum, sizeof(double) * ROLL_HOST_WORDS, hipMemcpyDeviceToHost, c->stream));
+        }
+    } else {
+        BPPO_HIP(c, hipMemcpyAsync(&hv[0], c->d_ep_count, 4, hipMemcpyDeviceToHost, c->stream));
+        BPPO_HIP(c, hipMemcpyAsync(&hv[1], c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
+    }
     c->collected = 1; c->gae_done = 0;
     c->rollout_rng_pos[c->coll_slot] = c->rng_pos;   // RNG position after the rollout (info; the update moves it on)
     return BPPO_OK;

@@ -333,6 +333,8 @@ struct bppo_ctx {
     // scratch
     double *d_red = nullptr;          // reduction scratch
     double *h_red = nullptr;          // pinned mirror
+    double *hd_red = nullptr;         // h_red's device address (BPPO_ZERO_COPY=1: kernels write their
+                                      // few host-bound results there instead of a D2H copy)
     float *h_rows = nullptr;          // pinned: the update's metric rows
     float *d_mb_stats = nullptr;      // advantage [mean, std, min, max] of each minibatch of the epoch [M][4]
     float *d_mb_cur = nullptr;        // the current minibatch's row of d_mb_stats
@@ -468,7 +470,13 @@ bppo_status launch_cartpole_vecenv_step(bppo_ctx *c, const int32_t *d_actions, f
                                         uint8_t *d_done, float *d_obs_out);
 bppo_status launch_cartpole_observe(bppo_ctx *c, float *d_obs_out);
 bppo_status launch_obs_norm_merge(bppo_ctx *c);
-bppo_status launch_episode_summary(bppo_ctx *c);
+bppo_status launch_episode_summary(bppo_ctx *c, double *host_slot);
+// BPPO_ZERO_COPY=1 (A/B): the episode summary and the explained-variance sums written into
+// pinned host memory by their kernels instead of copied after them
+inline bool zero_copy() {
+    static const bool z = getenv("BPPO_ZERO_COPY") && atoi(getenv("BPPO_ZERO_COPY")) == 1;
+    return z;
+}
 bppo_status launch_obs_norm_rows(bppo_ctx *c, int rows, float *x, int ld, float *raw);
 bppo_status launch_obs_norm_rows_on(bppo_ctx *c, int rows, float *x, int ld, float *raw, const double *on);
 bppo_status launch_bootstrap(bppo_ctx *c, const double *mean, const double *sd, int norm_on);

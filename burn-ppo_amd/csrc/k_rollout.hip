@@ -234,9 +234,13 @@ __global__ void __launch_bounds__(256) k_cartpole_rollout(RolloutArgs a) {
 // instruction writes 256 consecutive floats (a thread's own 16 words would be
 // a 64-B-strided store per word)
 constexpr int GUM_THREADS = 256;
+// zero0 / zero1 (optional): the rollout's episode counter and error flags, set to 0 here
+// (one store each) instead of by two fill launches ahead of it
 __global__ void __launch_bounds__(GUM_THREADS) k_gumbel_words(Key8 key, uint64_t stream, uint64_t base,
-                                                              uint64_t count, float *__restrict__ g) {
+                                                              uint64_t count, float *__restrict__ g,
+                                                              int32_t *zero0, int32_t *zero1) {
     __shared__ float tile[16 * GUM_THREADS + GUM_THREADS / 2];
+    if (zero0 && blockIdx.x == 0 && threadIdx.x == 0) { *zero0 = 0; *zero1 = 0; }
     const uint64_t blk0 = (base >> 4) + blockIdx.x * (uint64_t)GUM_THREADS;
     const uint64_t b = blk0 + threadIdx.x, wb = blk0 * 16;
     if (b * 16 < base + count) {
@@ -978,6 +982,16 @@ bppo_status launch_cartpole_rollout(bppo_ctx *c, uint64_t base_pos, const double
 
 static bppo_status launch_cartpole_rollout_kernels(bppo_ctx *c, uint64_t base_pos, int norm_on) {
     const int h = c->cfg.hidden_size, nl = c->cfg.num_hidden;
+    // the episode counter and error flags at 0 before the rollout: in the Gumbel kernel when it
+    // runs on the update stream (below), else two fills here
+    static const bool prep_side = getenv("BPPO_PREP_SIDE") && atoi(getenv("BPPO_PREP_SIDE")) == 1;
+    const bool lanes64 = !(getenv("BPPO_ROLLOUT_LANES64") && atoi(getenv("BPPO_ROLLOUT_LANES64")) == 0);
+    const bool gum_path = h == 64 && nl == 2 && c->cfg.relu && c->d_gumbel;
+    const bool side = gum_path && lanes64 && prep_side && c->prep_stream && c->ev_env && c->ev_prep;
+    if (!gum_path || side) {
+        BPPO_HIP(c, hipMemsetAsync(c->d_ep_count, 0, 4, c->stream));
+        BPPO_HIP(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
+    }
     if (!cp_supported(h, nl)) {
         c->err = "CartPole rollout kernel supports MLPs with hidden in {16,32,64} x {1,2} layers";
         return BPPO_ERR_UNSUPPORTED;
@@ -994,7 +1008,7 @@ static bppo_status launch_cartpole_rollout_kernels(bppo_ctx *c, uint64_t base_po
     a.stamps = nullptr;
     a.rpool = nullptr; a.rpos = nullptr; a.rpool_k = 0;
     c->rows_from_rollout = false;
-    if (h == 64 && nl == 2 && c->cfg.relu && c->d_gumbel) {
+    if (gum_path) {
         // the update's packed rows (obs, action, log-prob, value) written by the rollout
         // itself; GAE adds advantage and return, so k_pack_rows is not needed (PopArt
         // trains on normalized values computed at update start: packed there instead)
@@ -1005,19 +1019,17 @@ static bppo_status launch_cartpole_rollout_kernels(bppo_ctx *c, uint64_t base_po
         // Gumbel noise for every (t, env, action) first, then the MFMA rollout
         const uint64_t count = (uint64_t)c->T * c->N * 2;
         const uint64_t blocks = ((base_pos + count + 15) >> 4) - (base_pos >> 4);
-        const bool lanes64 = !(getenv("BPPO_ROLLOUT_LANES64") && atoi(getenv("BPPO_ROLLOUT_LANES64")) == 0);
         // BPPO_PREP_SIDE=1 (r06, A/B): the 64-lane rollout's inputs (Gumbel words, reset pool)
         // on prep_stream, which waits only for the last env-state writer (the previous
         // rollout), so they run beside the previous update instead of between its last
         // minibatch and this rollout.  Kernel traces: the gap before the rollout 285-607 ->
         // 121-295 us, but the update's minibatches 0.2-0.45 ms longer beside them (update span
         // 11.04 / 12.39 vs 11.36 / 12.24 ms, profiles/r06p/): off by default
-        static const bool prep_side = getenv("BPPO_PREP_SIDE") && atoi(getenv("BPPO_PREP_SIDE")) == 1;
-        const bool side = lanes64 && prep_side && c->prep_stream && c->ev_env && c->ev_prep;
         hipStream_t ps = side ? c->prep_stream : c->stream;
         if (side) BPPO_HIP(c, hipStreamWaitEvent(ps, c->ev_env, 0));
         hipLaunchKernelGGL(k_gumbel_words, dim3((unsigned)((blocks + 255) / 256)), dim3(256), 0, ps, c->rng_key,
-                           (uint64_t)c->cfg.rng_stream, base_pos, count, c->d_gumbel);
+                           (uint64_t)c->cfg.rng_stream, base_pos, count, c->d_gumbel,
+                           side ? nullptr : c->d_ep_count, side ? nullptr : (int32_t *)c->d_err);
         TRY(launch_check(c, "k_gumbel_words"));
         // default: the 64-lane kernel (269 registers and 84 KB of LDS per 4-wave block, so
         // the side-stream Fisher-Yates passes still share its CUs): device-bound A/B
@@ -1224,9 +1236,18 @@ bppo_status launch_obs_norm_merge(bppo_ctx *c) {
 // the rollout's completed-episode summary (mean return of player 0, mean length)
 // for bppo_rollout_info: per-block f64 partial sums in a fixed order, combined on
 // the host — no episode records cross PCIe (there are ~N * T / 20 of them)
-__global__ void __launch_bounds__(256) k_ep_summary(const EpisodeRec *eps, const int32_t *count, int cap,
-                                                    double *part) {
-    const int n = min(*count, cap);
+// host_slot: the rollout's slot of the pinned host buffer (its device address): [count, err]
+// as two int32 in double 0, then the partials -- written here instead of copied after
+__global__ void __launch_bounds__(256) k_ep_summary(const EpisodeRec *eps, const int32_t *count, const int32_t *err,
+                                                    int cap, double *host_slot) {
+    const int cnt = *count;
+    const int n = min(cnt, cap);
+    double *part = host_slot + 2;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        int32_t *hv = reinterpret_cast<int32_t *>(host_slot);
+        hv[0] = cnt;
+        hv[1] = *err;
+    }
     double sr = 0.0, sl = 0.0;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         sr += (double)eps[i].total_reward[0];
@@ -1243,9 +1264,9 @@ __global__ void __launch_bounds__(256) k_ep_summary(const EpisodeRec *eps, const
     }
 }
 
-bppo_status launch_episode_summary(bppo_ctx *c) {
+bppo_status launch_episode_summary(bppo_ctx *c, double *host_slot) {
     hipLaunchKernelGGL(k_ep_summary, dim3(EP_SUMMARY_BLOCKS), dim3(256), 0, c->stream, c->d_eps, c->d_ep_count,
-                       c->eps_cap, c->d_ep_sum);
+                       (const int32_t *)c->d_err, c->eps_cap, host_slot);
     TRY(launch_check(c, __func__));
     return BPPO_OK;
 }

@@ -1954,10 +1954,14 @@ bppo_status launch_adam(bppo_ctx *c, float lr, const float *c1, const float *c2,
 // caller has waited for the stream
 bppo_status launch_explained_variance(bppo_ctx *c, const float *valid) {
     const size_t n = (size_t)c->T * c->N;
-    hipLaunchKernelGGL(k_ev, dim3(STAT_BLOCKS), dim3(256), 0, c->stream, n, c->d_val, c->d_ret, valid, c->d_red);
+    // BPPO_ZERO_COPY=1: the block sums straight into the pinned buffer (its device address)
+    const bool zc = zero_copy();
+    hipLaunchKernelGGL(k_ev, dim3(STAT_BLOCKS), dim3(256), 0, c->stream, n, c->d_val, c->d_ret, valid,
+                       zc ? c->hd_red : c->d_red);
     TRY(launch_check(c, __func__));
-    BPPO_HIP(c, hipMemcpyAsync(c->h_red, c->d_red, sizeof(double) * 4 * STAT_BLOCKS,
-                               hipMemcpyDeviceToHost, c->stream));
+    if (!zc)
+        BPPO_HIP(c, hipMemcpyAsync(c->h_red, c->d_red, sizeof(double) * 4 * STAT_BLOCKS,
+                                   hipMemcpyDeviceToHost, c->stream));
     return BPPO_OK;
 }
 void explained_variance_sums(bppo_ctx *c, double *out4) {
