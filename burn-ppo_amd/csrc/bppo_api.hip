@@ -365,6 +365,7 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     }
     c->rng_key = seed_key(cfg->seed);
     c->rng_pos = 0;
+    c->shuf.gate = c->ev_upd;     // before init: the engine thread starts in it
     TRY(c->shuf.init(dev, c->rng_key, cfg->rng_stream, (uint32_t)TN, cfg->num_epochs, TN * (uint64_t)c->A, c->err,
                      cfg->shuffle_windows != 0));
     c->on_mean.assign(c->D, 0.0); c->on_m2.assign(c->D, 0.0); c->on_count = 0;
@@ -532,6 +533,7 @@ extern "C" bppo_status bppo_rng_from_seed(bppo_ctx *c, const uint8_t *seed) {
     c->rng_pos = 0;
     c->shuf_slot = -1;
     const size_t TN = (size_t)c->T * c->N;
+    c->shuf.gate = c->ev_upd;
     TRY(c->shuf.init(c->dev, c->rng_key, c->cfg.rng_stream, (uint32_t)TN, c->cfg.num_epochs, TN * (uint64_t)c->A, c->err,
                      c->cfg.shuffle_windows != 0));
     return BPPO_OK;

@@ -204,6 +204,10 @@ struct ShuffleEngine {
     hipEvent_t ev[2][SHUF_MAX_EPOCHS] = {};
     bool ev_used[2][SHUF_MAX_EPOCHS] = {};
     hipStream_t copy = nullptr;
+    // the caller's end-of-update event (bppo_ctx::ev_upd): with BPPO_XJ_GATE the J expansions
+    // wait for the update enqueued last, so a job the walks finished early is not expanded
+    // beside that update's minibatches (1: every epoch, 2: epochs after the first)
+    hipEvent_t gate = nullptr;
     double walk_ms[2][SHUF_MAX_EPOCHS] = {};
     int coalesced[2][SHUF_MAX_EPOCHS] = {};       // checkpoints walked before meeting a speculative walk (-1: none)
     std::atomic<uint64_t> spec_words{0}, true_words{0};   // words walked since the caller last read them
@@ -211,6 +215,7 @@ struct ShuffleEngine {
     bppo_status init(int device, const Key8 &key, uint64_t stream, uint32_t n_, int epochs_, uint64_t gap_,
                      std::string &err, bool windows = false);
     bool run_windowed(int slot, uint64_t start);   // one job of independent epoch walks (false: cancelled)
+    void xj_gate_wait(int e);                      // BPPO_XJ_GATE: copy waits on `gate` before epoch e's expansion
     uint64_t job_end(int slot) const { return win ? slot_start[slot] + (uint64_t)epochs * win : end_pos[slot][epochs - 1]; }
     // a HIP call of the engine's own thread that failed (its uploads, J expansions, events):
     // the first one is kept and the caller's next wait on the engine reports it

@@ -182,6 +182,15 @@ __global__ void __launch_bounds__(64 * XJ_WAVES) k_expand_J(Key8 key, uint64_t s
     }
 }
 
+// A job's J expansions on the copy stream wait for the end of the update the caller enqueued
+// last (its ev_upd) when BPPO_XJ_GATE is set: 1 every epoch, 2 epochs after the first.  No
+// deadlock: an update waits only for its own job's epochs, and the caller records its ev_upd
+// after enqueuing every epoch it runs, i.e. after those expansions were launched
+void ShuffleEngine::xj_gate_wait(int e) {
+    static const int mode = getenv("BPPO_XJ_GATE") ? atoi(getenv("BPPO_XJ_GATE")) : 0;
+    if (gate && (mode == 1 || (mode == 2 && e > 0))) hip_note(hipStreamWaitEvent(copy, gate, 0), "hipStreamWaitEvent");
+}
+
 // expected words per shuffle of n and its std dev: draw with range R accepts with
 // probability a = (R << lz(R)) / 2^32 (uniform.rs zone), geometric word count
 static void shuffle_word_stats(uint32_t n, double &mean, double &sd) {
@@ -1071,6 +1080,7 @@ void ShuffleEngine::run() {
                     }
                 Seg *dS = d_seg[slot] + (size_t)e * maxseg;
                 hip_note(hipMemcpyAsync(dS, S, sizeof(Seg) * (size_t)std::max(ns, 1), hipMemcpyHostToDevice, copy), "hipMemcpyAsync");
+                xj_gate_wait(e);
                 hipLaunchKernelGGL(k_expand_J, dim3((unsigned)((std::max(ns, 1) + XJ_WAVES - 1) / XJ_WAVES)),
                                    dim3(64 * XJ_WAVES), 0, copy, key, stream, (const Seg *)dS, ns, wr,
                                    d_J[slot] + (size_t)e * n);
@@ -1222,6 +1232,7 @@ bool ShuffleEngine::run_windowed(int slot, uint64_t start) {
             wr.ptr[0] = W.d + W.reg[e].off; wr.base[0] = W.reg[e].base; wr.len[0] = W.reg[e].len; wr.n = 1;
             Seg *dS = d_seg[slot] + (size_t)e * maxseg;
             hip_note(hipMemcpyAsync(dS, S, sizeof(Seg) * (size_t)std::max(ns, 1), hipMemcpyHostToDevice, copy), "hipMemcpyAsync");
+            xj_gate_wait(e);
             hipLaunchKernelGGL(k_expand_J, dim3((unsigned)((std::max(ns, 1) + XJ_WAVES - 1) / XJ_WAVES)),
                                dim3(64 * XJ_WAVES), 0, copy, key, stream, (const Seg *)dS, ns, wr,
                                d_J[slot] + (size_t)e * n);
