@@ -330,11 +330,10 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
         BPPO_HIP(c, make_side_stream(dev, &c->fy_stream));
         for (int e = 0; e < cfg->num_epochs && e < SHUF_MAX_EPOCHS; e++)
             BPPO_HIP(c, hipEventCreateWithFlags(&c->fy_ev[e], hipEventDisableTiming));
-        // the prep stream only when it is used (BPPO_PREP_SIDE=1): HIP maps streams onto the
-        // process's GPU_MAX_HW_QUEUES (4) hardware queues, and with one more stream the update
-        // stream shared a queue with a side stream -- every run whose host walk finished early
-        // then ran the device phases 15-25 % slower (13.1-13.6 vs 11.1-12.1 ms per update,
-        // profiles/r06x/)
+        // the prep stream only when it is used (BPPO_PREP_SIDE=1): with this third low-priority
+        // stream created (even idle) every device-bound run took 13.1-13.6 instead of
+        // 10.9-11.2 ms per update, the phases outside the minibatch kernels 15-25 % slower;
+        // GPU_MAX_HW_QUEUES=8 did not remove it (profiles/r06y/, r06z/)
         if (getenv("BPPO_PREP_SIDE") && atoi(getenv("BPPO_PREP_SIDE")) == 1) {
             BPPO_HIP(c, make_side_stream(dev, &c->prep_stream));
             BPPO_HIP(c, hipEventCreateWithFlags(&c->ev_prep, hipEventDisableTiming));
