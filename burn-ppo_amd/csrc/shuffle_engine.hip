@@ -1287,10 +1287,14 @@ void ShuffleEngine::shutdown() {
     }
 }
 
+// side streams (J expansion, Fisher-Yates): lowest priority; BPPO_SIDE_PRIO=normal (A/B)
+// creates them at the default priority
 hipError_t make_side_stream(int device, hipStream_t *st) {
     (void)device;
     int lo = 0, hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+    static const bool normal = getenv("BPPO_SIDE_PRIO") && std::string(getenv("BPPO_SIDE_PRIO")) == "normal";
+    if (normal) return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
     return hipStreamCreateWithPriority(st, hipStreamNonBlocking, lo);
 }
 
