@@ -327,7 +327,10 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     TRY(dalloc(c, &c->d_inv_ep, TN * (size_t)cfg->num_epochs));
     TRY(dalloc(c, &c->d_advpart, (size_t)ADV_STREAM_BLOCKS * ADV_STREAM_MAXM * 4));
     {
-        BPPO_HIP(c, make_side_stream(dev, &c->fy_stream));
+        // BPPO_FY_ON_COPY=1 (A/B): the permutations on the shuffle engine's copy stream (one
+        // side stream instead of two; set after the engine's init below)
+        c->fy_shared = getenv("BPPO_FY_ON_COPY") && atoi(getenv("BPPO_FY_ON_COPY")) == 1;
+        if (!c->fy_shared) BPPO_HIP(c, make_side_stream(dev, &c->fy_stream));
         for (int e = 0; e < cfg->num_epochs && e < SHUF_MAX_EPOCHS; e++)
             BPPO_HIP(c, hipEventCreateWithFlags(&c->fy_ev[e], hipEventDisableTiming));
         // the prep stream only when it is used (BPPO_PREP_SIDE=1): with this third low-priority
@@ -374,6 +377,7 @@ static bppo_status ctx_init(bppo_ctx *c, const bppo_config *cfg, int dev, void *
     c->shuf.gate = c->ev_upd;     // before init: the engine thread starts in it
     TRY(c->shuf.init(dev, c->rng_key, cfg->rng_stream, (uint32_t)TN, cfg->num_epochs, TN * (uint64_t)c->A, c->err,
                      cfg->shuffle_windows != 0));
+    if (c->fy_shared) c->fy_stream = c->shuf.copy;
     c->on_mean.assign(c->D, 0.0); c->on_m2.assign(c->D, 0.0); c->on_count = 0;
     c->u_ret = c->d_ret; c->u_val = c->d_val;
     c->shaping_v.assign(1, cfg->reward_shaping_coef); c->shaping_s.assign(1, 0);   // Schedule::constant
@@ -429,7 +433,7 @@ extern "C" void bppo_destroy(bppo_ctx *c) {
     }
     for (auto &pr : c->mb_ev)
         for (hipEvent_t e : pr) if (e) (void)hipEventDestroy(e);
-    if (c->fy_stream) { (void)hipStreamSynchronize(c->fy_stream); (void)hipStreamDestroy(c->fy_stream); }
+    if (c->fy_stream && !c->fy_shared) { (void)hipStreamSynchronize(c->fy_stream); (void)hipStreamDestroy(c->fy_stream); }
     for (hipEvent_t e : c->fy_ev) if (e) (void)hipEventDestroy(e);
     if (c->prep_stream) (void)hipStreamDestroy(c->prep_stream);
     for (hipEvent_t e : {c->ev_env, c->ev_prep}) if (e) (void)hipEventDestroy(e);
@@ -542,6 +546,7 @@ extern "C" bppo_status bppo_rng_from_seed(bppo_ctx *c, const uint8_t *seed) {
     c->shuf.gate = c->ev_upd;
     TRY(c->shuf.init(c->dev, c->rng_key, c->cfg.rng_stream, (uint32_t)TN, c->cfg.num_epochs, TN * (uint64_t)c->A, c->err,
                      c->cfg.shuffle_windows != 0));
+    if (c->fy_shared) c->fy_stream = c->shuf.copy;
     return BPPO_OK;
 }
 

@@ -324,6 +324,7 @@ struct bppo_ctx {
     uint32_t *d_inv_ep = nullptr;     // [epochs][TN] their inverses (row -> shuffled position)
     double *d_advpart = nullptr;      // k_adv_stream block partials
     hipStream_t fy_stream = nullptr;
+    bool fy_shared = false;           // BPPO_FY_ON_COPY=1 (A/B): fy_stream IS the engine's copy stream
     hipEvent_t fy_ev[bppo::SHUF_MAX_EPOCHS] = {};
     // CfgB 64-lane rollout: its Gumbel words and reset pool made on prep_stream as soon as the
     // previous env-state writer (ev_env: the last rollout / reset / vecenv step) finished, i.e.
