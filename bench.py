@@ -362,6 +362,13 @@ def main():
         ctypes.CDLL(None).prctl(15, b"bench-main", 0, 0, 0)       # PR_SET_NAME
     except (OSError, AttributeError):
         pass
+    # BPPO_BENCH_EXTRA_STREAMS=k (diagnostic): k more torch streams with one small kernel each
+    # before the timed region, as a multi-rank run's collective streams would add (an idle extra
+    # low-priority stream of the library cost ~2.5 ms per update)
+    extra = [torch.cuda.Stream() for _ in range(int(os.environ.get("BPPO_BENCH_EXTRA_STREAMS", "0")))]
+    for st_x in extra:
+        with torch.cuda.stream(st_x):
+            torch.zeros(1024, device="cuda").add_(1.0)
     tr.train_updates(args.warmup)
     torch.cuda.synchronize()
     if dist:
