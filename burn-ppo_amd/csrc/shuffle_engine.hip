@@ -118,9 +118,14 @@ __global__ void __launch_bounds__(64 * XJ_WAVES) k_expand_J(Key8 key, uint64_t s
     const ShuffleEngine::Seg g = segs[si];
     uint32_t r = g.r0;
     uint64_t q = g.pos0;
+    uint32_t avail = q < g.pos1 ? (uint32_t)min((uint64_t)64, g.pos1 - q) : 0u;
+    uint32_t w = lane < (int)avail ? xj_word(key, stream, wr, q + lane) : 0u;
     while (q < g.pos1 && r >= 2) {
-        const uint32_t avail = (uint32_t)min((uint64_t)64, g.pos1 - q);
-        const uint32_t w = lane < (int)avail ? xj_word(key, stream, wr, q + lane) : 0u;
+        // the next step's words in flight under this one (r06), assuming it consumes all 64
+        // (it does unless XJ_H rejections end it early or the segment ends)
+        const uint64_t qn = q + 64;
+        const uint32_t availn = qn < g.pos1 ? (uint32_t)min((uint64_t)64, g.pos1 - qn) : 0u;
+        const uint32_t wn = lane < (int)availn ? xj_word(key, stream, wr, qn + lane) : 0u;
         const int lz = __clz(r);
         const uint32_t lowr = 1u << (31 - lz);
         if (r >= lowr + 64 && r >= 66) {
@@ -178,6 +183,13 @@ __global__ void __launch_bounds__(64 * XJ_WAVES) k_expand_J(Key8 key, uint64_t s
             }
             r = __shfl(rr, 0, 64);
             q += __shfl(used, 0, 64);
+        }
+        if (q == qn) {
+            w = wn;
+            avail = availn;
+        } else if (q < g.pos1) {
+            avail = (uint32_t)min((uint64_t)64, g.pos1 - q);
+            w = lane < (int)avail ? xj_word(key, stream, wr, q + lane) : 0u;
         }
     }
 }
